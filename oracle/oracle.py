@@ -1,0 +1,345 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+CPU restatement of the reference's hot path, used by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py as the CHECKER (never as the thing measured on the GPU, never
+imported by the product package `pingpong-selfplay-ai_amd/`).
+
+  env / physics / CPython `random`  -> C (oracle/pong_oracle.c, built into oracle/_build/liborcpong.so)
+  QNet forward                      -> numpy, float64        models/qnet.py:43-50,71-75
+  NoisyLinear.reset_noise transform -> numpy                 models/qnet.py:33-41
+  PrioritizedReplay                 -> numpy                 scripts/train_iterative.py:49-76
+  double-DQN train_step + Adam      -> numpy, float64        scripts/train_iterative.py:132-168,
+                                                             torch.optim.Adam (torch 2.x single-tensor)
+
+Pinned against tests/golden/*.npz produced from the reference by tests/golden/make_golden.py.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(HERE, "_build", "liborcpong.so")
+_lib = None
+
+ENV_PARAM_NAMES = ["paddle_width", "paddle_speed", "magnus_factor", "restitution", "friction", "ball_mass",
+                   "world_ball_radius", "speed_lo", "speed_hi", "spin_lo", "spin_hi", "ang0_lo", "ang0_hi",
+                   "ang1_lo", "ang1_hi", "speed_increment", "max_score", "speed_scale_every", "enable_spin"]
+
+
+class OrParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in ENV_PARAM_NAMES[:16]] + \
+               [("max_score", ctypes.c_int32), ("speed_scale_every", ctypes.c_int32),
+                ("enable_spin", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+
+
+class OrArena(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in ("x", "y", "vx", "vy", "spin", "top", "bot")] + \
+               [("scoreA", ctypes.c_int32), ("scoreB", ctypes.c_int32), ("bounces", ctypes.c_int32),
+                ("_pad", ctypes.c_int32)]
+
+
+class OrMT(ctypes.Structure):
+    _fields_ = [("mt", ctypes.c_uint32 * 624), ("mti", ctypes.c_int)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(HERE, "pong_oracle.c")
+        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        L = ctypes.CDLL(_LIB_PATH)
+        P, D, I32, U64 = ctypes.c_void_p, ctypes.c_double, ctypes.c_int32, ctypes.c_uint64
+        L.or_collide.argtypes = [D] * 8 + [P]
+        L.or_mt_seed.argtypes = [P, U64]
+        L.or_mt_random.argtypes = [P]
+        L.or_mt_random.restype = D
+        L.or_mt_u32.argtypes = [P]
+        L.or_mt_u32.restype = ctypes.c_uint32
+        L.or_mt_randbelow.argtypes = [P, I32]
+        L.or_mt_randbelow.restype = I32
+        L.or_reset_draws.argtypes = [P, P, P]
+        L.or_reset_apply.argtypes = [P, D, D, D]
+        L.or_obs.argtypes = [P, P, P]
+        L.or_step.argtypes = [P, P, I32, I32, P]
+        L.or_step.restype = I32
+        L.or_step_batch.argtypes = [P, P, P, P, P, P, P, P, I32]
+        L.or_rollout_random.argtypes = [P, U64, ctypes.c_int64, P]
+        L.or_rollout_random.restype = ctypes.c_int64
+        for f in ("or_mt_sizeof", "or_params_sizeof", "or_arena_sizeof"):
+            getattr(L, f).restype = I32
+        assert L.or_mt_sizeof() == ctypes.sizeof(OrMT)
+        assert L.or_params_sizeof() == ctypes.sizeof(OrParams)
+        assert L.or_arena_sizeof() == ctypes.sizeof(OrArena)
+        _lib = L
+    return _lib
+
+
+# ----------------------------------------------------------------------------- env params
+def env_params_from_kwargs(**kw):
+    """Same defaults as PongEnv2P.__init__ (envs/my_pong_env_2p.py:19-37)."""
+    d = dict(paddle_width=0.2, paddle_speed=0.02, max_score=3, enable_spin=True, magnus_factor=0.01,
+             restitution=0.9, friction=0.2, ball_mass=1.0, world_ball_radius=0.03, ball_speed_range=(0.01, 0.05),
+             spin_range=(-10, 10), ball_angle_intervals=None, speed_scale_every=3, speed_increment=0.2)
+    d.update({k: v for k, v in kw.items() if k in d})
+    ai = d["ball_angle_intervals"] or [[-60, -30], [30, 60]]
+    return dict(paddle_width=d["paddle_width"], paddle_speed=d["paddle_speed"], magnus_factor=d["magnus_factor"],
+                restitution=float(d["restitution"]), friction=d["friction"], ball_mass=d["ball_mass"],
+                world_ball_radius=d["world_ball_radius"], speed_lo=d["ball_speed_range"][0],
+                speed_hi=d["ball_speed_range"][1], spin_lo=d["spin_range"][0], spin_hi=d["spin_range"][1],
+                ang0_lo=ai[0][0], ang0_hi=ai[0][1], ang1_lo=ai[1][0], ang1_hi=ai[1][1],
+                speed_increment=d["speed_increment"], max_score=int(d["max_score"]),
+                speed_scale_every=int(d["speed_scale_every"]), enable_spin=int(bool(d["enable_spin"])))
+
+
+def make_params(p):
+    s = OrParams()
+    for n in ENV_PARAM_NAMES:
+        setattr(s, n, int(p[n]) if n in ("max_score", "speed_scale_every", "enable_spin") else float(p[n]))
+    return s
+
+
+# ----------------------------------------------------------------------------- physics / env
+def collide(vn, vt, u, omega, e, mu, m, R):
+    out = (ctypes.c_double * 3)()
+    lib().or_collide(vn, vt, u, omega, e, mu, m, R, out)
+    return out[0], out[1], out[2]
+
+
+class MT:
+    """CPython-compatible `random` stream (random.seed(n) / random() / uniform / randint)."""
+
+    def __init__(self, seed):
+        self.s = OrMT()
+        lib().or_mt_seed(ctypes.byref(self.s), seed)
+
+    def random(self):
+        return lib().or_mt_random(ctypes.byref(self.s))
+
+    def randbelow(self, n):
+        return lib().or_mt_randbelow(ctypes.byref(self.s), n)
+
+    def reset_draws(self, params):
+        out = (ctypes.c_double * 3)()
+        lib().or_reset_draws(ctypes.byref(self.s), ctypes.byref(params), out)
+        return out[0], out[1], out[2]
+
+
+def new_arena(vx, vy, spin):
+    a = OrArena()
+    lib().or_reset_apply(ctypes.byref(a), vx, vy, spin)
+    return a
+
+
+def arena_state(a):
+    return np.array([a.x, a.y, a.vx, a.vy, a.spin, a.top, a.bot, a.scoreA, a.scoreB, a.bounces], np.float64)
+
+
+def arena_from_state(st):
+    a = OrArena()
+    a.x, a.y, a.vx, a.vy, a.spin, a.top, a.bot = [float(v) for v in st[:7]]
+    a.scoreA, a.scoreB, a.bounces = [int(v) for v in st[7:10]]
+    return a
+
+
+def arena_obs(a):
+    oa = np.zeros(7, np.float32)
+    ob = np.zeros(7, np.float32)
+    lib().or_obs(ctypes.byref(a), oa.ctypes.data, ob.ctypes.data)
+    return oa, ob
+
+
+def step(params, a, aA, aB):
+    r = np.zeros(2, np.float32)
+    d = lib().or_step(ctypes.byref(params), ctypes.byref(a), int(aA), int(aB), r.ctypes.data)
+    oa, ob = arena_obs(a)
+    return oa, ob, r, bool(d)
+
+
+def step_batch_soa(params, st, aA, aB):
+    """Advance SoA state dict (x,y,vx,vy,spin,top,bot float64 [n]; scoreA,scoreB,bounces int32 [n])
+    one tick without reset. Returns obsA, obsB [n,7] f32, rew [n,2] f32, done [n] u8; updates st."""
+    n = st["x"].shape[0]
+    arr = (OrArena * n)()
+    for i in range(n):
+        a = arr[i]
+        a.x, a.y, a.vx, a.vy = st["x"][i], st["y"][i], st["vx"][i], st["vy"][i]
+        a.spin, a.top, a.bot = st["spin"][i], st["top"][i], st["bot"][i]
+        a.scoreA, a.scoreB, a.bounces = int(st["scoreA"][i]), int(st["scoreB"][i]), int(st["bounces"][i])
+    aA = np.ascontiguousarray(aA, np.int8)
+    aB = np.ascontiguousarray(aB, np.int8)
+    obsA = np.zeros((n, 7), np.float32)
+    obsB = np.zeros((n, 7), np.float32)
+    rew = np.zeros((n, 2), np.float32)
+    done = np.zeros(n, np.uint8)
+    lib().or_step_batch(ctypes.byref(params), arr, aA.ctypes.data, aB.ctypes.data, obsA.ctypes.data,
+                        obsB.ctypes.data, rew.ctypes.data, done.ctypes.data, n)
+    for i in range(n):
+        a = arr[i]
+        st["x"][i], st["y"][i], st["vx"][i], st["vy"][i] = a.x, a.y, a.vx, a.vy
+        st["spin"][i], st["top"][i], st["bot"][i] = a.spin, a.top, a.bot
+        st["scoreA"][i], st["scoreB"][i], st["bounces"][i] = a.scoreA, a.scoreB, a.bounces
+    return obsA, obsB, rew, done
+
+
+def rollout_random(params, seed, steps):
+    ssum = ctypes.c_int64(0)
+    ep = lib().or_rollout_random(ctypes.byref(params), seed, steps, ctypes.byref(ssum))
+    return ep, ssum.value
+
+
+# ----------------------------------------------------------------------------- QNet (numpy)
+def scale_noise(raw):
+    """models/qnet.py:35-36: x.sign() * sqrt(|x|)."""
+    raw = np.asarray(raw, np.float32)
+    return (np.sign(raw) * np.sqrt(np.abs(raw))).astype(np.float32)
+
+
+def noise_from_raw(raw_in, raw_out):
+    """models/qnet.py:37-41 -> (weight_epsilon = outer(f(out), f(in)), bias_epsilon = f(out))."""
+    ei, eo = scale_noise(raw_in), scale_noise(raw_out)
+    return np.outer(eo, ei).astype(np.float32), eo
+
+
+def qnet_effective(sd, noisy, eps=None):
+    """Fold a QNet state_dict into the effective weights the forward uses (models/qnet.py:43-50).
+    noisy=True is train mode: W = mu + sigma*eps (eps from `eps` dict or the state_dict buffers)."""
+    g = lambda k: np.asarray(sd[k], np.float64)  # noqa: E731
+    out = {"W1": g("features.0.weight"), "b1": g("features.0.bias"),
+           "W2": g("features.2.weight"), "b2": g("features.2.bias")}
+    for h in ("fc_V", "fc_A"):
+        W, b = g(f"{h}.weight_mu"), g(f"{h}.bias_mu")
+        if noisy:
+            we = np.asarray((eps or sd)[f"{h}.weight_epsilon"], np.float64)
+            be = np.asarray((eps or sd)[f"{h}.bias_epsilon"], np.float64)
+            # torch evaluates mu + sigma*eps in float32
+            W = (np.float32(1) * (np.asarray(sd[f"{h}.weight_mu"], np.float32) +
+                                  np.asarray(sd[f"{h}.weight_sigma"], np.float32) * we.astype(np.float32))).astype(np.float64)
+            b = (np.asarray(sd[f"{h}.bias_mu"], np.float32) +
+                 np.asarray(sd[f"{h}.bias_sigma"], np.float32) * be.astype(np.float32)).astype(np.float64)
+        out[h + ".W"], out[h + ".b"] = W, b
+    return out
+
+
+def qnet_features(eff, x):
+    x = np.asarray(x, np.float64)
+    h1 = np.maximum(x @ eff["W1"].T + eff["b1"], 0.0)
+    return np.maximum(h1 @ eff["W2"].T + eff["b2"], 0.0)
+
+
+def qnet_heads(eff, h):
+    V = h @ eff["fc_V.W"].T + eff["fc_V.b"]
+    A = h @ eff["fc_A.W"].T + eff["fc_A.b"]
+    return V + (A - A.mean(axis=1, keepdims=True))
+
+
+def qnet_forward(eff, x):
+    """QNet.forward (models/qnet.py:71-75), float64."""
+    return qnet_heads(eff, qnet_features(eff, x))
+
+
+def argmax_first(q):
+    """torch argmax: first index of the maximum."""
+    return np.argmax(q, axis=1)
+
+
+# ----------------------------------------------------------------------------- PER (numpy)
+def per_sample(prios, size, bs, beta, uniforms, alpha=0.6):
+    """PrioritizedReplay.sample (scripts/train_iterative.py:64-73) with np.random.choice's own
+    algorithm (cdf = cumsum(p) in float64, cdf /= cdf[-1], searchsorted(u, 'right')) on given uniforms."""
+    pr = np.asarray(prios[:size], np.float32)
+    probs = pr ** np.float32(alpha)
+    probs /= probs.sum()
+    cdf = probs.astype(np.float64).cumsum()
+    cdf /= cdf[-1]
+    idxs = cdf.searchsorted(np.asarray(uniforms, np.float64), side="right")
+    w = (np.float32(size) * probs[idxs]) ** np.float32(-beta)
+    w = w / w.max()
+    return idxs.astype(np.int64), w.astype(np.float32)
+
+
+def per_update(prios, idxs, errors):
+    """update_priorities (:74-76): sequential, so the last duplicate wins."""
+    for i, e in zip(idxs, errors):
+        prios[i] = np.float32(abs(e)) + np.float32(1e-6)
+
+
+# ----------------------------------------------------------------------------- DQN (numpy)
+HEAD_LAYOUT = [("fc_V.weight_mu", (1, 64)), ("fc_V.bias_mu", (1,)), ("fc_V.weight_sigma", (1, 64)),
+               ("fc_V.bias_sigma", (1,)), ("fc_A.weight_mu", (3, 64)), ("fc_A.bias_mu", (3,)),
+               ("fc_A.weight_sigma", (3, 64)), ("fc_A.bias_sigma", (3,))]
+N_HEAD = sum(int(np.prod(s)) for _, s in HEAD_LAYOUT)  # 520
+
+
+def pack_heads(sd):
+    return np.concatenate([np.asarray(sd[k], np.float64).ravel() for k, _ in HEAD_LAYOUT])
+
+
+def unpack_heads(vec):
+    out, o = {}, 0
+    for k, s in HEAD_LAYOUT:
+        n = int(np.prod(s))
+        out[k] = np.asarray(vec[o:o + n]).reshape(s)
+        o += n
+    return out
+
+
+def dqn_loss_grads(sdB, heads, target_heads, epsB, s, a, r, ns, d, iw, gamma):
+    """Double-DQN loss and head gradients (scripts/train_iterative.py:152-163), float64.
+    heads/target_heads: packed 520-vectors (HEAD_LAYOUT). epsB: noise buffers for modelB.
+    targetB is in eval mode (train_iterative.py:100) so it uses mu only."""
+    hd = unpack_heads(heads)
+    th = unpack_heads(target_heads)
+    W1 = np.asarray(sdB["features.0.weight"], np.float64)
+    feat = {"W1": W1, "b1": np.asarray(sdB["features.0.bias"], np.float64),
+            "W2": np.asarray(sdB["features.2.weight"], np.float64), "b2": np.asarray(sdB["features.2.bias"], np.float64)}
+    wV_eps = np.asarray(epsB["fc_V.weight_epsilon"], np.float64)
+    bV_eps = np.asarray(epsB["fc_V.bias_epsilon"], np.float64)
+    wA_eps = np.asarray(epsB["fc_A.weight_epsilon"], np.float64)
+    bA_eps = np.asarray(epsB["fc_A.bias_epsilon"], np.float64)
+    eff = dict(feat)
+    eff["fc_V.W"] = hd["fc_V.weight_mu"] + hd["fc_V.weight_sigma"] * wV_eps
+    eff["fc_V.b"] = hd["fc_V.bias_mu"] + hd["fc_V.bias_sigma"] * bV_eps
+    eff["fc_A.W"] = hd["fc_A.weight_mu"] + hd["fc_A.weight_sigma"] * wA_eps
+    eff["fc_A.b"] = hd["fc_A.bias_mu"] + hd["fc_A.bias_sigma"] * bA_eps
+    teff = dict(feat)
+    teff["fc_V.W"], teff["fc_V.b"] = th["fc_V.weight_mu"], th["fc_V.bias_mu"]
+    teff["fc_A.W"], teff["fc_A.b"] = th["fc_A.weight_mu"], th["fc_A.bias_mu"]
+    hs = qnet_features(feat, s)
+    hn = qnet_features(feat, ns)
+    Qs = qnet_heads(eff, hs)
+    B = len(a)
+    q = Qs[np.arange(B), a]
+    na = argmax_first(qnet_heads(eff, hn))
+    nq = qnet_heads(teff, hn)[np.arange(B), na]
+    t = np.asarray(r, np.float64) + gamma * nq * (~np.asarray(d, bool))
+    diff = q - t
+    iw = np.asarray(iw, np.float64)
+    loss = np.mean(iw * diff ** 2)
+    g = 2.0 * iw * diff / B                       # dL/dq
+    gA = np.zeros((B, 3))
+    gA[np.arange(B), a] = 1.0
+    gA = (gA - 1.0 / 3.0) * g[:, None]            # dL/dA_k
+    gV = g[:, None]                               # dL/dV
+    dWV = gV.T @ hs                               # [1,64]
+    dbV = gV.sum(0)
+    dWA = gA.T @ hs                               # [3,64]
+    dbA = gA.sum(0)
+    grads = {"fc_V.weight_mu": dWV, "fc_V.bias_mu": dbV, "fc_V.weight_sigma": dWV * wV_eps,
+             "fc_V.bias_sigma": dbV * bV_eps, "fc_A.weight_mu": dWA, "fc_A.bias_mu": dbA,
+             "fc_A.weight_sigma": dWA * wA_eps, "fc_A.bias_sigma": dbA * bA_eps}
+    gvec = np.concatenate([grads[k].ravel() for k, _ in HEAD_LAYOUT])
+    return dict(loss=loss, q=q, targets=t, na=na, errors=np.abs(diff), grads=gvec)
+
+
+def adam_step(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
+    """torch.optim.Adam single-tensor update (no weight decay, no amsgrad), step t >= 1."""
+    m = m + (1 - beta1) * (g - m)                 # exp_avg.lerp_(grad, 1-beta1)
+    v = v * beta2 + (1 - beta2) * g * g
+    bc1 = 1 - beta1 ** t
+    bc2 = 1 - beta2 ** t
+    denom = np.sqrt(v) / np.sqrt(bc2) + eps
+    p = p - (lr / bc1) * (m / denom)
+    return p, m, v

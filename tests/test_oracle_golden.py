@@ -1,0 +1,127 @@
+"""Pin the oracle (CPU restatement) against the reference's own outputs (tests/golden/*.npz,
+generated from /root/reference by tests/golden/make_golden.py). CPU-only."""
+import numpy as np
+import pytest
+
+
+def _params(orc, g):
+    names = [str(n) for n in g["param_names"]]
+    vals = dict(zip(names, g["param_values"].tolist()))
+    return vals, orc.make_params(vals)
+
+
+def test_collide_kat_bit_exact(orc, golden):
+    g = golden("collide_kat")
+    for row, exp in zip(g["inputs"], g["outputs"]):
+        got = orc.collide(*row.tolist())
+        assert np.array_equal(np.array(got), exp), (row, got, exp)
+    # the +-0.0 vrel slide cases keep their sign through copysign
+    assert np.array_equal(np.signbit(g["outputs"]), np.signbit(np.array([orc.collide(*r.tolist()) for r in g["inputs"]])))
+
+
+@pytest.mark.parametrize("name", ["cfg", "rnn", "default"])
+def test_env_trajectories_bit_exact(orc, golden, name):
+    """Oracle replays the reference trajectory: serves from a CPython-identical MT19937 stream
+    seeded like random.seed(seed_i), steps with the recorded actions — every fp64 state word,
+    every f32 obs, reward, done and score must be identical."""
+    g = golden(f"env_{name}")
+    pv, P = _params(orc, g)
+    n, T = g["actA"].shape
+    for i in range(n):
+        mt = orc.MT(int(g["seeds"][i]))
+        a = orc.new_arena(*mt.reset_draws(P))
+        assert np.array_equal(orc.arena_state(a), g["init"][i])
+        for t in range(T):
+            oa, ob, r, d = orc.step(P, a, g["actA"][i, t], g["actB"][i, t])
+            assert np.array_equal(orc.arena_state(a), g["state"][i, t]), (name, i, t)
+            assert np.array_equal(oa, g["obsA"][i, t]) and np.array_equal(ob, g["obsB"][i, t])
+            assert np.array_equal(r, g["rew"][i, t]) and d == bool(g["done"][i, t])
+            if d:
+                a = orc.new_arena(*mt.reset_draws(P))
+                assert np.array_equal(orc.arena_state(a), g["reset_state"][i, t])
+                oa, ob = orc.arena_obs(a)
+                assert np.array_equal(oa, g["reset_obs"][i, t, 0]) and np.array_equal(ob, g["reset_obs"][i, t, 1])
+
+
+def test_env_fixture_covers_edge_events(golden):
+    """The trajectories must exercise stick and slide hits, speed-ups, misses with ghost play-on
+    (scores keep counting after the first miss) and episode ends."""
+    stick = sum(int(golden(f"env_{n}")["hits_stick"]) for n in ("cfg", "rnn", "default"))
+    slide = sum(int(golden(f"env_{n}")["hits_slide"]) for n in ("cfg", "rnn", "default"))
+    assert stick > 50 and slide > 20
+    g = golden("env_cfg")
+    assert g["done"].sum() > 20 and g["state"][..., 9].max() >= 5
+
+
+def test_rollout_random_matches_reference_loop(orc, golden):
+    """Config 1 (BASELINE.json configs[0]): random-vs-random loop on the CPython stream."""
+    g = golden("rollout_random")
+    for name in ("cfg", "rnn"):
+        from oracle.oracle import env_params_from_kwargs
+        import yaml, os
+        cfgfile = {"cfg": "config.yaml", "rnn": "config_rnn.yaml"}[name]
+        path = os.path.join(os.path.dirname(__file__), "..", "pingpong-selfplay-ai_amd", cfgfile)
+        with open(path) as f:
+            envkw = yaml.safe_load(f)["env"]
+        P = orc.make_params(env_params_from_kwargs(**envkw))
+        ep, ssum = orc.rollout_random(P, 0, int(g[f"{name}_steps"]))
+        assert ep == int(g[f"{name}_episodes"]) and ssum == int(g[f"{name}_score_sum"])
+
+
+def test_qnet_forward_matches_reference(orc, golden):
+    g = golden("qnet")
+    for who in ("modelB", "modelA"):
+        sd = {k[len(who) + 1:]: v for k, v in g.items() if k.startswith(who + ".") and "q_" not in k}
+        q_eval = orc.qnet_forward(orc.qnet_effective(sd, noisy=False), g["obs"])
+        q_train = orc.qnet_forward(orc.qnet_effective(sd, noisy=True), g["obs"])
+        np.testing.assert_allclose(q_eval, g[f"{who}.q_eval"], rtol=0, atol=2e-5)
+        np.testing.assert_allclose(q_train, g[f"{who}.q_train"], rtol=0, atol=2e-5)
+        gap = np.sort(q_eval, 1)
+        clear = (gap[:, -1] - gap[:, -2]) > 1e-4
+        assert np.array_equal(orc.argmax_first(q_eval)[clear], np.argmax(g[f"{who}.q_eval"], 1)[clear])
+
+
+def test_noise_transform_matches_reference(orc, golden):
+    g = golden("qnet")
+    we, be = orc.noise_from_raw(g["noise.raw_in"], g["noise.raw_out"])
+    assert np.array_equal(we, g["noise.weight_epsilon"]) and np.array_equal(be, g["noise.bias_epsilon"])
+
+
+def test_per_matches_reference(orc, golden):
+    g = golden("per")
+    for ph in range(int(g["n_phases"])):
+        u = 0
+        while f"p{ph}.u{u}.idxs" in g:
+            k = f"p{ph}.u{u}."
+            idxs, w = orc.per_sample(g[k + "prios_before"], int(g[k + "size"]), 64, float(g[k + "beta"]),
+                                     g[k + "uniforms"])
+            assert np.array_equal(idxs, g[k + "idxs"])
+            np.testing.assert_allclose(w, g[k + "weights"], rtol=1e-6)
+            pr = g[k + "prios_before"].copy()
+            orc.per_update(pr, g[k + "upd_idx"], g[k + "upd_err"])
+            assert np.array_equal(pr, g[k + "prios_after"])
+            u += 1
+
+
+def test_dqn_steps_match_reference(orc, golden):
+    g = golden("dqn_steps")
+    sd = {k[5:]: v for k, v in g.items() if k.startswith("init.")}
+    heads = orc.pack_heads(sd)
+    target = heads.copy()
+    m = np.zeros_like(heads)
+    v = np.zeros_like(heads)
+    for s in range(3):
+        k = f"s{s}."
+        eps = {kk[len(k) + 7:]: vv for kk, vv in g.items() if kk.startswith(k + "noiseB.")}
+        res = orc.dqn_loss_grads(sd, heads, target, eps, g[k + "s"], g[k + "a"], g[k + "r"], g[k + "ns"],
+                                 g[k + "d"], g[k + "iw"], 0.99)
+        np.testing.assert_allclose(res["loss"], g[k + "loss"], rtol=2e-5)
+        np.testing.assert_allclose(res["q"], g[k + "q"], atol=3e-5)
+        np.testing.assert_allclose(res["targets"], g[k + "targets"], atol=3e-5)
+        np.testing.assert_allclose(res["errors"], g[k + "errors"], atol=3e-5)
+        np.testing.assert_allclose(res["grads"], g[k + "grads"], rtol=1e-4, atol=1e-6)
+        heads, m, v = orc.adam_step(heads, res["grads"], m, v, s + 1, 2.5e-4)
+        np.testing.assert_allclose(heads, g[k + "params_after"], rtol=3e-7, atol=2e-6)  # fp32 storage
+        if (s + 1) % 2 == 0:
+            target = heads.copy()
+        np.testing.assert_allclose(target, g[k + "target_heads_after"], rtol=3e-7, atol=2e-6)

@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env-steps/sec of the batched self-play DQN learner (BASELINE.json configs[2]:
+65 536 arenas per GPU, the full train_iterative loop — both players acting, env tick, PER replay
+push + proportional sample, double-DQN update with target net, Adam), weak-scaled over N GPUs
+(configs[3]: one RCCL all-reduce of the 520 head gradients + counters per update).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--arenas 65536] [--pool 8]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+A step = one vector step: every arena on every rank advances one env step and every rank runs one
+PER update of batch 256. value = total env-steps (all ranks) / max-over-ranks wall time of K steps.
+Rank 0 prints one JSON line. Also reported (rank 0, N=1 only):
+  roofline      the dominant kernel (k_rollout: 2 QNet forwards + env tick per arena) timed with
+                HIP events on the stream it runs on, FP32 FLOP/s vs the 157.3 TF FP32 peak
+  env_step_roofline  K1 (pm_env_step) alone at the same n: algorithmic 203 B / env-step vs 8 TB/s
+  cpu_baseline  the oracle's CPU port of the same vector step, 1 core, bounded sample
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pingpong-selfplay-ai_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+ENV_KW = dict(paddle_width=0.2, paddle_speed=0.03, max_score=3, enable_spin=True, magnus_factor=0.025,
+              restitution=1, friction=0.6, ball_mass=1.0, world_ball_radius=0.03, ball_speed_range=[0.03, 0.05],
+              spin_range=[-5, 5], ball_angle_intervals=[[-60, -30], [30, 60]], speed_scale_every=1,
+              speed_increment=0.1)  # config.yaml env (render keys dropped)
+FLOP_PER_ARENA = 2 * 2 * (7 * 64 + 64 * 64 + 64 * 4)  # two QNet forwards (MACs x 2)
+ENV_BYTES = 203  # K1 algorithmic bytes per env-step
+PEAK_FP32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def synthetic_qnet(seed):
+    from models.qnet import QNet
+    torch.manual_seed(seed)
+    return {k: v.clone() for k, v in QNet(7, 3).state_dict().items()}
+
+
+def time_env_step(n, reps=200):
+    from pongmi.env import PongEnv2PBatch
+    env = PongEnv2PBatch(n, seed=3, autoreset=True, **ENV_KW)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    aA = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=g)
+    aB = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=g)
+    for _ in range(20):
+        env.step(aA, aB)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    total = 0.0
+    for _ in range(reps):
+        e0.record()
+        env.step(aA, aB)
+        e1.record()
+        e1.synchronize()
+        total += e0.elapsed_time(e1)
+    t = total / reps * 1e-3
+    achieved = n * ENV_BYTES / t / 1e9
+    return {"bound": "hbm", "kernel": "k_env_step", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+            "avg_us": round(t * 1e6, 2), "bytes_per_env_step": ENV_BYTES, "n": n}
+
+
+def cpu_baseline(n, seconds=12.0):
+    from threadpoolctl import threadpool_limits
+    from oracle.cpu_selfplay import CpuSelfPlay
+    sdB, sdA = synthetic_qnet(1), synthetic_qnet(2)
+    pool = [synthetic_qnet(100 + k) for k in range(4)]
+    with threadpool_limits(1):
+        cpu = CpuSelfPlay(ENV_KW, n, {k: v.numpy() for k, v in sdB.items()}, {k: v.numpy() for k, v in sdA.items()},
+                          [{k: v.numpy() for k, v in s.items()} for s in pool], batch=256, cap=1_000_000)
+        for _ in range(2):
+            cpu.step()
+        t0 = time.perf_counter()
+        steps = 0
+        while time.perf_counter() - t0 < seconds:
+            cpu.step()
+            steps += 1
+        dt = time.perf_counter() - t0
+    return {"value": round(n * steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/cpu_selfplay.py: {steps} vector steps x {n} arenas (full DQN loop, PER cap 1e6, "
+                      f"batch 256), {dt:.1f} s on 1 host core"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--arenas", type=int, default=65536, help="arenas per GPU")
+    ap.add_argument("--pool", type=int, default=8, help="opponent pool size (synthetic nets)")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--memory", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from pongmi.selfplay import SelfPlayLearner
+
+    sdB, sdA = synthetic_qnet(1), synthetic_qnet(2)
+    pool = [synthetic_qnet(100 + k) for k in range(args.pool)]
+    allreduce = (lambda t: dist.all_reduce(t)) if dist else None
+    L = SelfPlayLearner(ENV_KW, args.arenas, sdB, sdA, pool, batch=args.batch, memory_size=args.memory,
+                        epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce)
+
+    def one_step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        L.rollout()
+        if ev is not None:
+            ev[1].record()
+        L.learn()
+        if dist is not None:
+            dist.all_reduce(L.grad)
+        L.apply()
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(evs[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    rollout_s = sum(a.elapsed_time(b) for a, b in evs) * 1e-3 / args.steps
+    c = L.counters()
+
+    if rank == 0:
+        total = args.arenas * world * args.steps
+        value = total / dt
+        achieved = args.arenas * FLOP_PER_ARENA / rollout_s / 1e12
+        out = {
+            "metric": "env-steps/sec (whole node) at 65536 arenas, 1/2/4/8 GPUs; CPU-ref baseline",
+            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64 env state / f32 QNet",
+            "data": "synthetic (random-init QNet weights of the reference architecture, Philox serves)",
+            "config": {"workload": "configs[2]: 65536 arenas/GPU, full DQN train_iterative loop (act both players + "
+                                   "env tick + PER push/sample + double-DQN update + Adam + target sync)",
+                       "arenas_per_gpu": args.arenas, "global_arenas": args.arenas * world,
+                       "pool": args.pool, "batch": args.batch, "updates_per_vector_step": 1,
+                       "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)"},
+            "roofline": {"bound": "mfma", "kernel": "k_rollout", "compute": "fp32 VALU v_fmac_f32 (FP32 peak = "
+                                                                           "matrix peak = 157.3 TF)",
+                         "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "avg_us": round(rollout_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
+            "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
+                        "last_loss": c["last_loss"]},
+        }
+        if world == 1:
+            out["env_step_roofline"] = time_env_step(args.arenas)
+            if not args.no_cpu_baseline:
+                out["cpu_baseline"] = cpu_baseline(args.arenas, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,229 @@
+/*
+ * pongmi.h — C-ABI of libpongmi.so, the MI355X (gfx950) hot path of pingpong-selfplay-ai:
+ * batched PongEnv2P rollout (SoA fp64 arenas), fused two-player QNet acting, device replay +
+ * prioritized sampling, and the double-DQN head update.
+ *
+ * The reference (MaxChen228/pingpong-selfplay-ai) is pure Python and has no FFI; every entry point
+ * below replaces a Python function on its hot path, cited as reference file:line. The Python
+ * mirror of the reference API (pingpong-selfplay-ai_amd/{envs,models,scripts}) binds these with
+ * ctypes.
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer owned by the caller (e.g. a torch tensor's
+ *    data_ptr()); the library never allocates or frees caller memory. Parameter structs
+ *    (pm_env_params, pm_env_state, pm_selfplay) are HOST structs passed by pointer and copied
+ *    into the launch; the pointers inside them are device pointers.
+ *  - Every call is asynchronous on `stream` (a hipStream_t; NULL = the null stream) and never
+ *    synchronizes the host, so a caller may capture calls into a hipGraph.
+ *  - Return 0 on success, a negative PM_E* code on an argument error, or a positive hipError_t
+ *    if a launch failed. pm_last_error() returns a thread-local message for the last failure.
+ *  - Randomness is Philox4x32-10, keyed by a 64-bit seed, countered by (index, purpose, step):
+ *    results depend only on (seed, counters), never on launch geometry.
+ */
+#ifndef PONGMI_H
+#define PONGMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PM_ABI_VERSION 1
+
+#define PM_OK 0
+#define PM_E_ARG (-1)     /* null / inconsistent argument */
+#define PM_E_SIZE (-2)    /* size outside the supported range */
+#define PM_E_LAUNCH (-3)  /* launch failed (see pm_last_error) */
+
+/* ---------------------------------------------------------------- environment (K1) */
+
+/* PongEnv2P constructor parameters (envs/my_pong_env_2p.py:19-81). The last four doubles are
+ * derived constants the HOST computes with the reference's own Python expressions so the device
+ * reproduces them bit for bit:
+ *   half_width   = paddle_width/2                     (:152,190)
+ *   speed_scale  = 1.0 + speed_increment              (:230)
+ *   inertia      = (2/5) * ball_mass * radius**2      (envs/physics.py:9)
+ *   jt_coef      = 2*ball_mass/7.0                    (envs/physics.py:10)                  */
+typedef struct pm_env_params {
+    double paddle_width, paddle_speed, magnus_factor, restitution, friction, ball_mass, radius;
+    double speed_lo, speed_hi, spin_lo, spin_hi;
+    double ang0_lo, ang0_hi, ang1_lo, ang1_hi;
+    double half_width, speed_scale, inertia, jt_coef;
+    int32_t max_score, speed_scale_every, enable_spin, _pad;
+} pm_env_params;
+
+/* Struct-of-arrays arena state, [n] each (PongEnv2P attributes ball_x, ball_y, ball_vx, ball_vy,
+ * spin, top_paddle_x, bottom_paddle_x, scoreA, scoreB, bounce_count). `serves` counts the resets
+ * an arena has consumed: it indexes the injected serve table / the Philox serve stream. */
+typedef struct pm_env_state {
+    double *x, *y, *vx, *vy, *spin, *top, *bot;
+    int32_t *scoreA, *scoreB, *bounces, *serves;
+} pm_env_state;
+
+/* PongEnv2P.reset (envs/my_pong_env_2p.py:83-114) for every arena with mask[i] != 0 (mask NULL =
+ * all). Serve (vx, vy, spin) comes from `inject` when non-NULL — layout [n][inject_cap][3],
+ * entry serves[i] mod inject_cap (parity mode: the host draws it with CPython's `random` exactly
+ * as the reference does) — else from Philox(seed) with counter (i, serves[i]) (production mode:
+ * speed~U(speed_lo,speed_hi), angle~U(ang0) or U(ang1) by a fair coin, spin~U(spin_lo,spin_hi)).
+ * serves[i] is incremented. Writes obsA/obsB [n][7] (may be NULL). `status` (nullable, device
+ * int32) is reserved for error bits. */
+int pm_env_reset(const pm_env_params* p, const pm_env_state* s, const uint8_t* mask, const double* inject,
+                 int32_t inject_cap, uint64_t seed, float* obsA, float* obsB, int32_t* status, int32_t n,
+                 void* stream);
+
+/* PongEnv2P.step (envs/my_pong_env_2p.py:116-225, physics.py:3-23, _maybe_scale_speed :227-232,
+ * _get_obs :235-263) for n arenas: aA/aB [n] in {0,1,2}; writes obsA/obsB [n][7], rA/rB [n]
+ * (values -1/0/+1), done [n]. With autoreset != 0, done arenas are then reset as pm_env_reset
+ * (inject / seed as above); obsA/obsB then hold the post-reset observation, and term_obsA /
+ * term_obsB (nullable) the observation returned by the terminal step (the `nB` the reference
+ * stores in replay, scripts/train_iterative.py:242-243). */
+int pm_env_step(const pm_env_params* p, const pm_env_state* s, const int8_t* aA, const int8_t* aB, float* obsA,
+                float* obsB, float* rA, float* rB, uint8_t* done, float* term_obsA, float* term_obsB,
+                int32_t autoreset, const double* inject, int32_t inject_cap, uint64_t seed, int32_t* status,
+                int32_t n, void* stream);
+
+/* collide_sphere_with_moving_plane (envs/physics.py:3-23) over n rows: in [n][8] =
+ * (vn, vt, u, omega, e, mu, m, R) fp64, with I = (2/5)*m*R**2 supplied per row in inertia[n]
+ * (CPython's value); out [n][3] = (vn', vt', omega'). A test/diagnostic entry point. */
+int pm_collide(const double* in, const double* inertia, double* out, int32_t n, void* stream);
+
+/* ---------------------------------------------------------------- QNet (K2) */
+
+/* Packed QNet parameter block (models/qnet.py:52-69), PM_QNET_NP floats, in this order:
+ *   features.0.weight [64,7] | features.0.bias [64] | features.2.weight [64,64] | features.2.bias [64]
+ *   fc_V.{weight_mu [1,64], bias_mu [1], weight_sigma [1,64], bias_sigma [1]}
+ *   fc_A.{weight_mu [3,64], bias_mu [3], weight_sigma [3,64], bias_sigma [3]}      (the 520 "heads",
+ *        in the order train_iterative.py:101-104 hands them to Adam)
+ *   fc_V.{weight_epsilon [1,64], bias_epsilon [1]} | fc_A.{weight_epsilon [3,64], bias_epsilon [3]}
+ * Effective (folded) weights, PM_QNET_NW floats: W1 [64,7] | b1 [64] | W2 [64,64] | b2 [64] |
+ *   Wh [4,64] (row 0 = V, rows 1..3 = A) | bh [4]. */
+#define PM_QNET_NP 5452
+#define PM_QNET_NHEAD 520
+#define PM_QNET_HEAD_OFF 4672
+#define PM_QNET_EPS_OFF 5192
+#define PM_QNET_NW 4932
+
+#define PM_FOLD_EVAL 0        /* NoisyLinear eval mode: W = mu                          (qnet.py:47-49) */
+#define PM_FOLD_TRAIN 1       /* train mode with the block's epsilon buffers: mu+sigma*eps (qnet.py:44-46) */
+#define PM_FOLD_TRAIN_FRESH 2 /* reset_noise() then train mode (qnet.py:33-41): fresh factorised
+                                 Gaussian noise from Philox(seed, counter); written back into the
+                                 block's epsilon slots when params_out != NULL                   */
+
+/* Fold `count` parameter blocks [count][PM_QNET_NP] into effective weights [count][PM_QNET_NW].
+ * counter_dev (nullable, device uint64) is added to `counter` so a captured graph advances it. */
+int pm_qnet_fold(const float* params, float* params_out, int32_t mode, uint64_t seed, uint64_t counter,
+                 const uint64_t* counter_dev, float* w_eff, int32_t count, void* stream);
+
+/* QNet.forward (models/qnet.py:71-75) on effective weights: x [n][7] -> q [n][3]. */
+int pm_qnet_q(const float* w_eff, const float* x, float* q, int32_t n, void* stream);
+
+/* Both players' action selection for n arenas (fused):
+ *   A: argmax_a Q_opp(obsA) with opponent weights w_opp[opp_id[i]] (opp_id NULL = 0)
+ *      (scripts/train_iterative.py:240; tests/arena.py:294-320)
+ *   B: random.random() < epsilon ? randint(0,2) : argmax_a Q_B(obsB)          (train_iterative.py:124-130)
+ * argmax keeps the first maximal index (torch). epsilon is *eps_dev when eps_dev != NULL.
+ * qA/qB [n][3] nullable. Philox counter for the epsilon draws: (i, counter + *counter_dev). */
+int pm_qnet_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B, const float* obsA,
+                const float* obsB, float epsilon, const double* eps_dev, uint64_t seed, uint64_t counter,
+                const uint64_t* counter_dev, int8_t* aA, int8_t* aB, float* qA, float* qB, int32_t n,
+                void* stream);
+
+/* ---------------------------------------------------------------- replay + PER (K4) */
+
+/* Transition record, PM_TRANS_F floats per row (64 B): s [7] | r | s' [7] | bits(a | done << 8).
+ * (memory.push((oB, aB, rB, nB, done)), scripts/train_iterative.py:243) */
+#define PM_TRANS_F 16
+
+/* PrioritizedReplay.sample (scripts/train_iterative.py:64-73): `bs` indices drawn from
+ * prios[0:size]^alpha (proportional, with replacement) using the uniforms u[bs] (NULL -> Philox)
+ * exactly as np.random.choice does (cdf, searchsorted right); writes idx [bs] and the IS weight
+ * w [bs] = (size*P(i))^-beta / max. Scratch: `work` of pm_per_work_bytes(cap) bytes. */
+int64_t pm_per_work_bytes(int64_t cap);
+int pm_per_sample(const float* prios, int64_t size, float alpha, float beta, const double* u, uint64_t seed,
+                  uint64_t counter, int64_t* idx, float* w, int32_t bs, void* work, void* stream);
+
+/* update_priorities (train_iterative.py:74-76): prios[idx[j]] = |err[j]| + 1e-6, sequential order
+ * (the last duplicate index wins). */
+int pm_per_update(float* prios, const int64_t* idx, const float* err, int32_t bs, void* stream);
+
+/* ---------------------------------------------------------------- self-play learner (K1+K2+K3+K4) */
+
+/* Device control block (one per shard): the loop counters of scripts/train_iterative.py:106-118,
+ * kept on the device so a vector step never syncs the host. */
+typedef struct pm_ctrl {
+    uint64_t step;           /* vector steps done                                       */
+    int64_t pos, size;       /* replay ring position / fill (memory.pos, len(buffer))     */
+    int64_t train_steps;     /* train_step() calls that updated (Adam t, target sync)     */
+    int64_t frame_idx;       /* beta annealing counter (:136-137)                        */
+    int64_t episodes;        /* global_episode_count (:107,234)                          */
+    double epsilon;          /* exploration rate of B (:106,261)                         */
+    float max_prio;          /* PER max priority for the next push (:57)                 */
+    float last_loss;         /* loss of the last update                                  */
+    int64_t ep_step;         /* episodes finished during the current vector step          */
+    int64_t win_A, ep_A, win_P, ep_P; /* wins / episodes of B vs modelA and vs pool (:247-248) */
+    double reward_B;         /* sum of rB over finished episodes                          */
+    int32_t status;          /* error bits                                               */
+    int32_t _pad;
+} pm_ctrl;
+
+/* One shard of the batched self-play learner: every buffer is a device pointer, [n] = per arena. */
+typedef struct pm_selfplay {
+    pm_env_params env;
+    pm_env_state st;
+    int32_t *opp;            /* [n] opponent of the running episode: 0 = modelA, 1..n_pool = pool  */
+    float *ep_reward;        /* [n] ep_reward of B (:238,245)                                     */
+    float *w_opp;            /* [1+n_pool][PM_QNET_NW] opponent effective weights                */
+    float *paramsB;          /* [PM_QNET_NP] modelB parameter block (trained heads)              */
+    float *paramsT;          /* [PM_QNET_NP] targetB parameter block (eval mode: mu only)         */
+    float *w_B;              /* [PM_QNET_NW] modelB acting weights for the current step           */
+    float *adam_m, *adam_v;  /* [PM_QNET_NHEAD] Adam state                                        */
+    float *trans;            /* [cap][PM_TRANS_F] replay ring                                     */
+    float *prios;            /* [cap] priorities                                                  */
+    void *per_work;          /* pm_per_work_bytes(cap)                                            */
+    int64_t *idx;            /* [batch] sampled indices                                           */
+    float *isw;              /* [batch] IS weights                                                */
+    float *grad;             /* [PM_QNET_NHEAD + 8] grads + packed counters (all-reduced when sharded) */
+    int64_t *partials;       /* [ceil(n/256)][8] per-block episode counters of the rollout          */
+    float *hfeat;            /* [2*batch][64] learner scratch: features of s and s'                 */
+    pm_ctrl *ctrl;
+    int32_t n, n_pool, batch, world;
+    int64_t cap;
+    double gamma, alpha, lr, beta1, beta2, adam_eps;  /* train_iterative.py:33-37, torch.optim.Adam defaults */
+    double min_epsilon, epsilon_decay, pool_ratio, beta_start;
+    int64_t beta_frames, target_update_interval;
+    uint64_t seed_env;       /* rank-specific: serves, opponents, epsilon draws */
+    uint64_t seed_net;       /* rank-independent: NoisyNet noise, so replicas stay identical */
+} pm_selfplay;
+
+/* Limits: 1 <= batch <= PM_MAX_BATCH (one learner workgroup), batch < n <= cap (every vector step
+ * pushes n > batch transitions, which keeps the tracked max priority exact), n_pool <= 4096. */
+#define PM_MAX_BATCH 256
+
+/* One vector step of scripts/train_iterative.py:239-245 for all n arenas, as device work only:
+ *   rollout: act (both players, :240-241) + env step (:242) + replay push (:243) + episode
+ *            bookkeeping (:245-249, next opponent :235-236, env.reset :238);
+ *   learn:   once the replay holds >= batch transitions: PER sample + double-DQN loss/grads +
+ *            priority update (train_step, :132-164), leaving grads and the finished-episode count
+ *            in sp->grad;
+ *   apply:   grads /= world, Adam on the 520 head parameters (:159-161), target sync every
+ *            target_update_interval updates (:166-168), epsilon decay per finished episode
+ *            (:261), replay/step counters, next step's acting noise (:125).
+ * A sharded learner all-reduces sp->grad [PM_QNET_NHEAD + 8] (sum) between learn and apply.
+ * pm_selfplay_step = rollout + learn + apply (unsharded). pm_selfplay_init serves every arena,
+ * draws first opponents and folds the acting weights of step ctrl->step. */
+int pm_selfplay_init(const pm_selfplay* sp, void* stream);
+int pm_selfplay_rollout(const pm_selfplay* sp, void* stream);
+int pm_selfplay_learn(const pm_selfplay* sp, void* stream);
+int pm_selfplay_apply(const pm_selfplay* sp, void* stream);
+int pm_selfplay_step(const pm_selfplay* sp, void* stream);
+
+/* ---------------------------------------------------------------- misc */
+const char* pm_last_error(void);
+int pm_abi_version(void);
+int32_t pm_sizeof(int32_t which); /* 0: pm_env_params 1: pm_env_state 2: pm_ctrl 3: pm_selfplay */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PONGMI_H */

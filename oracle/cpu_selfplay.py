@@ -1,0 +1,108 @@
+"""ORACLE — TEST INFRASTRUCTURE / CPU BASELINE ONLY.
+
+A plain CPU port of the batched self-play vector step (the same workload bench.py measures on the
+GPU): both players act (numpy float32 MLPs, epsilon-greedy), every arena ticks (the C oracle of
+envs/my_pong_env_2p.py), transitions go to a numpy PER ring (scripts/train_iterative.py:49-76),
+then one double-DQN update of `batch` (train_iterative.py:132-168, numpy) with Adam. Used only
+as bench.py's `cpu_baseline` ("kind": "port"), on one core.
+"""
+import numpy as np
+
+from . import oracle as orc
+
+
+def _eff32(sd, noisy, eps=None):
+    e = orc.qnet_effective(sd, noisy, eps)
+    return {k: np.asarray(v, np.float32) for k, v in e.items()}
+
+
+def _q32(e, x):
+    h = np.maximum(x @ e["W1"].T + e["b1"], 0)
+    h = np.maximum(h @ e["W2"].T + e["b2"], 0)
+    V = h @ e["fc_V.W"].T + e["fc_V.b"]
+    A = h @ e["fc_A.W"].T + e["fc_A.b"]
+    return V + (A - A.mean(1, keepdims=True))
+
+
+class CpuSelfPlay:
+    def __init__(self, env_kw, n, sdB, sdA, pool_sds, batch=256, cap=1_000_000, epsilon=0.02, pool_ratio=0.33,
+                 seed=0, gamma=0.99, lr=2.5e-4):
+        self.rng = np.random.RandomState(seed)
+        self.pv = orc.env_params_from_kwargs(**env_kw)
+        self.P = orc.make_params(self.pv)
+        self.n, self.batch, self.cap = n, batch, cap
+        self.sdB = {k: np.asarray(v, np.float32) for k, v in sdB.items()}
+        self.effA = _eff32({k: np.asarray(v) for k, v in sdA.items()}, True)
+        self.effP = [_eff32({k: np.asarray(v) for k, v in s.items()}, False) for s in pool_sds]
+        self.heads = orc.pack_heads(self.sdB)
+        self.target = self.heads.copy()
+        self.m = np.zeros_like(self.heads)
+        self.v = np.zeros_like(self.heads)
+        self.t = 0
+        self.eps, self.pool_ratio, self.gamma, self.lr = epsilon, pool_ratio, gamma, lr
+        self.arr = np.zeros(n, orc.ARENA_DTYPE)
+        self.opp = np.zeros(n, np.int64)
+        self._serve(np.ones(n, bool))
+        self.s = np.zeros((cap, 7), np.float32)
+        self.ns = np.zeros((cap, 7), np.float32)
+        self.a = np.zeros(cap, np.int64)
+        self.r = np.zeros(cap, np.float32)
+        self.d = np.zeros(cap, bool)
+        self.prios = np.zeros(cap, np.float32)
+        self.pos = self.size = 0
+        self.frame = 0
+
+    def _serve(self, mask):
+        k = int(mask.sum())
+        if k == 0:
+            return
+        p = self.pv
+        speed = self.rng.uniform(p["speed_lo"], p["speed_hi"], k)
+        coin = self.rng.rand(k) < 0.5
+        ang = np.where(coin, self.rng.uniform(p["ang0_lo"], p["ang0_hi"], k), self.rng.uniform(p["ang1_lo"], p["ang1_hi"], k))
+        rad = np.radians(ang)
+        orc.serve_arenas(self.arr, mask, speed * np.cos(rad), speed * np.sin(rad),
+                         self.rng.uniform(p["spin_lo"], p["spin_hi"], k))
+        use = (self.rng.rand(k) < self.pool_ratio) & (len(self.effP) > 0)
+        self.opp[mask] = np.where(use, 1 + self.rng.randint(0, max(len(self.effP), 1), k), 0)
+
+    def step(self):
+        n = self.n
+        oA, oB = orc.obs_of_arenas(self.arr)
+        qa = np.empty((n, 3), np.float32)
+        for k, e in enumerate([self.effA] + self.effP):
+            sel = self.opp == k
+            if sel.any():
+                qa[sel] = _q32(e, oA[sel])
+        wn = orc.noise_from_raw(self.rng.randn(64).astype(np.float32), self.rng.randn(1).astype(np.float32))
+        an = orc.noise_from_raw(self.rng.randn(64).astype(np.float32), self.rng.randn(3).astype(np.float32))
+        eps_act = {"fc_V.weight_epsilon": wn[0], "fc_V.bias_epsilon": wn[1], "fc_A.weight_epsilon": an[0],
+                   "fc_A.bias_epsilon": an[1]}
+        qb = _q32(_eff32({**self.sdB, **orc.unpack_heads(self.heads.astype(np.float32))}, True, eps_act), oB)
+        aA = np.argmax(qa, 1).astype(np.int8)
+        aB = np.where(self.rng.rand(n) < self.eps, self.rng.randint(0, 3, n), np.argmax(qb, 1)).astype(np.int8)
+        nA, nB, rew, done = orc.step_arenas(self.P, self.arr, aA, aB)
+        slots = (self.pos + np.arange(n)) % self.cap
+        self.s[slots], self.ns[slots], self.a[slots], self.r[slots], self.d[slots] = oB, nB, aB, rew[:, 1], done > 0
+        self.prios[slots] = self.prios.max() if self.size else 1.0
+        self.pos = (self.pos + n) % self.cap
+        self.size = min(self.size + n, self.cap)
+        self._serve(done > 0)
+        D = int(done.sum())
+        self.eps = max(0.02, self.eps * 0.995 ** D)
+        if self.size >= self.batch:
+            self.frame += 1
+            beta = min(1.0, 0.4 + self.frame * 0.6 / 100000)
+            idx, w = orc.per_sample(self.prios, self.size, self.batch, beta, self.rng.random_sample(self.batch))
+            tn = orc.noise_from_raw(self.rng.randn(64).astype(np.float32), self.rng.randn(1).astype(np.float32))
+            ta = orc.noise_from_raw(self.rng.randn(64).astype(np.float32), self.rng.randn(3).astype(np.float32))
+            eps_tr = {"fc_V.weight_epsilon": tn[0], "fc_V.bias_epsilon": tn[1], "fc_A.weight_epsilon": ta[0],
+                      "fc_A.bias_epsilon": ta[1]}
+            res = orc.dqn_loss_grads(self.sdB, self.heads, self.target, eps_tr, self.s[idx], self.a[idx], self.r[idx],
+                                     self.ns[idx], self.d[idx], w, self.gamma)
+            self.t += 1
+            self.heads, self.m, self.v = orc.adam_step(self.heads, res["grads"], self.m, self.v, self.t, self.lr)
+            orc.per_update(self.prios, idx, res["errors"])
+            if self.t % 1000 == 0:
+                self.target = self.heads.copy()
+        return n

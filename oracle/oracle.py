@@ -158,30 +158,46 @@ def step(params, a, aA, aB):
     return oa, ob, r, bool(d)
 
 
-def step_batch_soa(params, st, aA, aB):
-    """Advance SoA state dict (x,y,vx,vy,spin,top,bot float64 [n]; scoreA,scoreB,bounces int32 [n])
-    one tick without reset. Returns obsA, obsB [n,7] f32, rew [n,2] f32, done [n] u8; updates st."""
-    n = st["x"].shape[0]
-    arr = (OrArena * n)()
-    for i in range(n):
-        a = arr[i]
-        a.x, a.y, a.vx, a.vy = st["x"][i], st["y"][i], st["vx"][i], st["vy"][i]
-        a.spin, a.top, a.bot = st["spin"][i], st["top"][i], st["bot"][i]
-        a.scoreA, a.scoreB, a.bounces = int(st["scoreA"][i]), int(st["scoreB"][i]), int(st["bounces"][i])
+ARENA_DTYPE = np.dtype([("x", "f8"), ("y", "f8"), ("vx", "f8"), ("vy", "f8"), ("spin", "f8"), ("top", "f8"),
+                        ("bot", "f8"), ("scoreA", "i4"), ("scoreB", "i4"), ("bounces", "i4"), ("_pad", "i4")])
+
+
+def arenas_from_soa(st):
+    n = np.asarray(st["x"]).shape[0]
+    arr = np.zeros(n, ARENA_DTYPE)
+    for k in ("x", "y", "vx", "vy", "spin", "top", "bot", "scoreA", "scoreB", "bounces"):
+        arr[k] = st[k]
+    return arr
+
+
+def step_arenas(params, arr, aA, aB):
+    """Advance a structured array of arenas (ARENA_DTYPE, C layout of or_arena) one tick, no reset.
+    Returns obsA, obsB [n,7] f32, rew [n,2] f32, done [n] u8; updates arr in place."""
+    assert arr.dtype == ARENA_DTYPE and arr.flags.c_contiguous and ARENA_DTYPE.itemsize == ctypes.sizeof(OrArena)
+    n = arr.shape[0]
     aA = np.ascontiguousarray(aA, np.int8)
     aB = np.ascontiguousarray(aB, np.int8)
     obsA = np.zeros((n, 7), np.float32)
     obsB = np.zeros((n, 7), np.float32)
     rew = np.zeros((n, 2), np.float32)
     done = np.zeros(n, np.uint8)
-    lib().or_step_batch(ctypes.byref(params), arr, aA.ctypes.data, aB.ctypes.data, obsA.ctypes.data,
+    lib().or_step_batch(ctypes.byref(params), arr.ctypes.data, aA.ctypes.data, aB.ctypes.data, obsA.ctypes.data,
                         obsB.ctypes.data, rew.ctypes.data, done.ctypes.data, n)
-    for i in range(n):
-        a = arr[i]
-        st["x"][i], st["y"][i], st["vx"][i], st["vy"][i] = a.x, a.y, a.vx, a.vy
-        st["spin"][i], st["top"][i], st["bot"][i] = a.spin, a.top, a.bot
-        st["scoreA"][i], st["scoreB"][i], st["bounces"][i] = a.scoreA, a.scoreB, a.bounces
     return obsA, obsB, rew, done
+
+
+def obs_of_arenas(arr):
+    """_get_obs_for_A/_B (envs/my_pong_env_2p.py:235-257) for a structured array."""
+    oA = np.stack([arr["x"], 1.0 - arr["y"], arr["vx"], -arr["vy"], arr["top"], arr["bot"], arr["spin"]], 1)
+    oB = np.stack([arr["x"], arr["y"], arr["vx"], arr["vy"], arr["bot"], arr["top"], arr["spin"]], 1)
+    return oA.astype(np.float32), oB.astype(np.float32)
+
+
+def serve_arenas(arr, mask, vx, vy, spin):
+    """reset() (:83-114) applied to arr[mask] with serves (vx, vy, spin)."""
+    for k, v in (("scoreA", 0), ("scoreB", 0), ("bounces", 0), ("top", 0.5), ("bot", 0.5), ("x", 0.5), ("y", 0.5)):
+        arr[k][mask] = v
+    arr["vx"][mask], arr["vy"][mask], arr["spin"][mask] = vx, vy, spin
 
 
 def rollout_random(params, seed, steps):
@@ -343,3 +359,74 @@ def adam_step(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
     denom = np.sqrt(v) / np.sqrt(bc2) + eps
     p = p - (lr / bc1) * (m / denom)
     return p, m, v
+
+
+# ----------------------------------------------------------------------------- Philox (numpy)
+# Restatement of the counter-based generator libpongmi draws from (Philox4x32-10, Salmon et al.
+# SC'11), so tests can replay the device's serves / epsilon draws / PER uniforms / noise.
+TAG_SERVE, TAG_ACT, TAG_OPP, TAG_NOISE_ACT, TAG_PER, TAG_NOISE_TRAIN = 1, 2, 3, 4, 5, 6
+_M0, _M1, _W0, _W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+
+
+def philox(c0, c1, c2, c3, key):
+    """Vectorised Philox4x32-10 over uint32 arrays; key is a 64-bit int."""
+    m32 = np.uint64(0xFFFFFFFF)
+    c = [np.asarray(v, np.uint64) & m32 for v in (c0, c1, c2, c3)]
+    k0, k1 = np.uint64(key & 0xFFFFFFFF), np.uint64((key >> 32) & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = c[0] * np.uint64(_M0)
+        p1 = c[2] * np.uint64(_M1)
+        hi0, lo0 = p0 >> np.uint64(32), p0 & m32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & m32
+        c = [(hi1 ^ c[1] ^ k0) & m32, lo1, (hi0 ^ c[3] ^ k1) & m32, lo0]
+        k0 = (k0 + np.uint64(_W0)) & m32
+        k1 = (k1 + np.uint64(_W1)) & m32
+    return [v.astype(np.uint32) for v in c]
+
+
+def philox64(index, tag, ctr, key):
+    ctr = np.asarray(ctr, np.uint64)
+    return philox(index, tag, ctr & np.uint64(0xFFFFFFFF), ctr >> np.uint64(32), key)
+
+
+def u53(hi, lo):
+    v = ((np.asarray(hi, np.uint64) << np.uint64(32)) | np.asarray(lo, np.uint64)) >> np.uint64(11)
+    return v.astype(np.float64) * 2.0 ** -53
+
+
+def below(r, n):
+    return ((np.asarray(r, np.uint64) * np.uint64(n)) >> np.uint64(32)).astype(np.int64)
+
+
+def normal_f32(a, b):
+    """Box-Muller cos branch in float32, as the device's normal()."""
+    u1 = ((np.asarray(a, np.uint32) >> 8).astype(np.float32) + np.float32(1.0)) * np.float32(2.0 ** -24)
+    u2 = (np.asarray(b, np.uint32) >> 8).astype(np.float32) * np.float32(2.0 ** -24)
+    r = np.sqrt(np.float32(-2.0) * np.log(u1))
+    return (r * np.cos(np.float32(6.28318530717958647692) * u2)).astype(np.float32)
+
+
+def philox_serve(params_dict, i, nserve, seed):
+    """The device's production serve (pm_dev.h philox_serve) restated: arrays i, nserve."""
+    p = params_dict
+    r0 = philox(i, TAG_SERVE, nserve, 0, seed)
+    r1 = philox(i, TAG_SERVE | 0x100, nserve, 0, seed)
+    speed = p["speed_lo"] + (p["speed_hi"] - p["speed_lo"]) * u53(r0[0], r0[1])
+    coin = u53(r0[2], r0[3]) < 0.5
+    u = u53(r1[0], r1[1])
+    ang = np.where(coin, p["ang0_lo"] + (p["ang0_hi"] - p["ang0_lo"]) * u, p["ang1_lo"] + (p["ang1_hi"] - p["ang1_lo"]) * u)
+    rad = ang * (3.141592653589793 / 180.0)
+    spin = p["spin_lo"] + (p["spin_hi"] - p["spin_lo"]) * u53(r1[2], r1[3])
+    return speed * np.cos(rad), speed * np.sin(rad), spin
+
+
+def philox_noise(seed, tag, ctr):
+    """Factorised noise of one QNet head pair as the device draws it (pm_dev.h fold_heads):
+    returns (fV_in[64], fV_out[1], fA_in[64], fA_out[3]) after scale_noise."""
+    out = []
+    for layer, (n_in, n_out) in enumerate(((64, 1), (64, 3))):
+        for which, n in ((0, n_in), (1, n_out)):
+            e = np.arange(n)
+            r = philox64(e, tag | (layer << 8) | (which << 12), np.full(n, ctr, np.uint64), seed)
+            out.append(scale_noise(normal_f32(r[0], r[1])))
+    return out

@@ -1,0 +1,302 @@
+// Device-side building blocks shared by the libpongmi kernels (gfx950 / CDNA4, wave64).
+//
+//   philox()        counter-based RNG (Philox4x32-10): every draw is a pure function of
+//                   (seed, index, purpose, step) -> results never depend on launch geometry.
+//   Arena/tick()    one PongEnv2P.step on a register-resident arena (envs/my_pong_env_2p.py:116-232,
+//                   envs/physics.py:3-23), IEEE binary64 in the reference's evaluation order.
+//                   The library is compiled with -ffp-contract=off: no FMA is ever formed here.
+//   qnet_q()        QNet.forward (models/qnet.py:71-75) for one row per lane on effective weights
+//                   whose base pointer is wave-uniform, so every weight is a scalar (SMEM) load
+//                   broadcast to the 64 lanes and every MAC is one v_fmac_f32 with an SGPR operand.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pongmi.h"
+
+namespace pm {
+
+// ----------------------------------------------------------------------------- RNG
+enum : uint32_t { TAG_SERVE = 1, TAG_ACT = 2, TAG_OPP = 3, TAG_NOISE_ACT = 4, TAG_PER = 5, TAG_NOISE_TRAIN = 6 };
+
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_t key) {
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return {c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ U4 philox64(uint32_t index, uint32_t tag, uint64_t ctr, uint64_t key) {
+    return philox(index, tag, (uint32_t)ctr, (uint32_t)(ctr >> 32), key);
+}
+
+// uniform double in [0, 1) with 53 random bits (like CPython's random.random())
+__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
+    const uint64_t v = (((uint64_t)hi << 32) | lo) >> 11;
+    return (double)v * 0x1.0p-53;
+}
+// uniform integer in [0, n) (randint(0, n-1)); bias <= n / 2^32
+__device__ __forceinline__ int32_t below(uint32_t r, uint32_t n) {
+    return (int32_t)(((uint64_t)r * n) >> 32);
+}
+// one N(0,1) float by Box-Muller from two u32 (torch.randn stand-in, distribution parity)
+__device__ __forceinline__ float normal(uint32_t a, uint32_t b, bool second) {
+    const float u1 = ((float)(a >> 8) + 1.0f) * 0x1.0p-24f;  // (0, 1]
+    const float u2 = (float)(b >> 8) * 0x1.0p-24f;           // [0, 1)
+    const float r = sqrtf(-2.0f * logf(u1));
+    const float th = 6.28318530717958647692f * u2;
+    return second ? r * sinf(th) : r * cosf(th);
+}
+// NoisyLinear._scale_noise (models/qnet.py:35-36): sign(x) * sqrt(|x|)
+__device__ __forceinline__ float scale_noise(float x) {
+    const float s = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+    return s * sqrtf(fabsf(x));
+}
+
+// ----------------------------------------------------------------------------- environment
+struct Arena {
+    double x, y, vx, vy, spin, top, bot;
+    int32_t sA, sB, bounces;
+};
+
+__device__ __forceinline__ Arena load_arena(const pm_env_state& s, int i) {
+    Arena a;
+    a.x = s.x[i]; a.y = s.y[i]; a.vx = s.vx[i]; a.vy = s.vy[i];
+    a.spin = s.spin[i]; a.top = s.top[i]; a.bot = s.bot[i];
+    a.sA = s.scoreA[i]; a.sB = s.scoreB[i]; a.bounces = s.bounces[i];
+    return a;
+}
+
+__device__ __forceinline__ void store_arena(const pm_env_state& s, int i, const Arena& a) {
+    s.x[i] = a.x; s.y[i] = a.y; s.vx[i] = a.vx; s.vy[i] = a.vy;
+    s.spin[i] = a.spin; s.top[i] = a.top; s.bot[i] = a.bot;
+    s.scoreA[i] = a.sA; s.scoreB[i] = a.sB; s.bounces[i] = a.bounces;
+}
+
+// _get_obs_for_A / _get_obs_for_B (envs/my_pong_env_2p.py:235-257): fp64 -> f32 round-to-nearest
+__device__ __forceinline__ void observe(const Arena& a, float* oA, float* oB) {
+    oA[0] = (float)a.x; oA[1] = (float)(1.0 - a.y); oA[2] = (float)a.vx; oA[3] = (float)(-a.vy);
+    oA[4] = (float)a.top; oA[5] = (float)a.bot; oA[6] = (float)a.spin;
+    oB[0] = (float)a.x; oB[1] = (float)a.y; oB[2] = (float)a.vx; oB[3] = (float)a.vy;
+    oB[4] = (float)a.bot; oB[5] = (float)a.top; oB[6] = (float)a.spin;
+}
+
+// reset() (:83-114) with a given serve (vx, vy, spin)
+__device__ __forceinline__ void serve(Arena& a, double vx, double vy, double spin) {
+    a.sA = 0; a.sB = 0; a.bounces = 0;
+    a.top = 0.5; a.bot = 0.5; a.x = 0.5; a.y = 0.5;
+    a.vx = vx; a.vy = vy; a.spin = spin;
+}
+
+// Production serve draws from Philox: speed = U(lo,hi), coin < 0.5 picks the angle interval,
+// angle = U(interval) degrees -> radians (math.radians: deg * (pi/180)), spin = U(lo,hi).
+__device__ __forceinline__ void philox_serve(const pm_env_params& p, uint32_t i, uint32_t nserve, uint64_t seed,
+                                             double& vx, double& vy, double& spin) {
+    const U4 r0 = philox(i, TAG_SERVE, nserve, 0u, seed);
+    const U4 r1 = philox(i, TAG_SERVE | 0x100u, nserve, 0u, seed);
+    const double speed = p.speed_lo + (p.speed_hi - p.speed_lo) * u53(r0.x, r0.y);
+    double ang;
+    if (u53(r0.z, r0.w) < 0.5) ang = p.ang0_lo + (p.ang0_hi - p.ang0_lo) * u53(r1.x, r1.y);
+    else ang = p.ang1_lo + (p.ang1_hi - p.ang1_lo) * u53(r1.x, r1.y);
+    const double rad = ang * (3.141592653589793 / 180.0);
+    vx = speed * cos(rad);
+    vy = speed * sin(rad);
+    spin = p.spin_lo + (p.spin_hi - p.spin_lo) * u53(r1.z, r1.w);
+}
+
+__device__ __forceinline__ double clip01(double v) { return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v); }
+
+// collide_sphere_with_moving_plane (envs/physics.py:3-23)
+__device__ __forceinline__ void collide(const pm_env_params& p, double vn, double vt, double u, double om,
+                                        double& vn2, double& vt2, double& om2) {
+    const double e = p.restitution, m = p.ball_mass, R = p.radius;
+    vn2 = (-e) * vn;
+    const double Jn = (m * (1.0 + e)) * fabs(vn);
+    const double Jt_star = p.jt_coef * ((u + R * om) - vt);
+    const double mf = p.friction * Jn;
+    double Jt;
+    if (fabs(Jt_star) <= mf) {
+        Jt = Jt_star;
+    } else {
+        const double vrel = (vt - u) - R * om;
+        Jt = (-mf) * copysign(1.0, vrel);
+    }
+    vt2 = vt + (Jt / m);
+    om2 = om - (R * Jt) / p.inertia;
+}
+
+// One PongEnv2P.step. Returns done; rewards are exactly -1/0/+1.
+__device__ __forceinline__ int tick(const pm_env_params& p, Arena& a, int aA, int aB, float& rA, float& rB) {
+    if (aA == 0) a.top = a.top - p.paddle_speed;
+    else if (aA == 2) a.top = a.top + p.paddle_speed;
+    a.top = clip01(a.top);
+    if (aB == 0) a.bot = a.bot - p.paddle_speed;
+    else if (aB == 2) a.bot = a.bot + p.paddle_speed;
+    a.bot = clip01(a.bot);
+
+    int done = 0;
+    rA = 0.f; rB = 0.f;
+    if (p.enable_spin) a.vx = a.vx + (p.magnus_factor * a.spin) * a.vy;
+    a.x = a.x + a.vx;
+    a.y = a.y + a.vy;
+    if (a.x < 0.0) { a.x = -a.x; a.vx = -a.vx; }
+    else if (a.x > 1.0) { a.x = 2.0 - a.x; a.vx = -a.vx; }
+
+    if (a.y < 0.0) {
+        const double lo = a.top - p.half_width, hi = a.top + p.half_width;
+        if (lo <= a.x && a.x <= hi) {
+            const double u = aA == 0 ? -p.paddle_speed : (aA == 2 ? p.paddle_speed : 0.0);
+            double vn2, vt2, om2;
+            collide(p, a.vy, a.vx, u, a.spin, vn2, vt2, om2);
+            a.vy = vn2; a.vx = vt2; a.spin = om2;
+            a.y = 0.0;
+            a.bounces += 1;
+            if (a.bounces % p.speed_scale_every == 0) { a.vx = a.vx * p.speed_scale; a.vy = a.vy * p.speed_scale; }
+        } else {
+            rA = -1.f; rB = 1.f;
+            a.sB += 1;
+            done = a.sB >= p.max_score;
+        }
+    } else if (a.y > 1.0) {
+        const double lo = a.bot - p.half_width, hi = a.bot + p.half_width;
+        if (lo <= a.x && a.x <= hi) {
+            const double u = aB == 0 ? -p.paddle_speed : (aB == 2 ? p.paddle_speed : 0.0);
+            double vn2, vt2, om2;
+            collide(p, -a.vy, a.vx, u, a.spin, vn2, vt2, om2);
+            a.vy = -vn2; a.vx = vt2; a.spin = om2;
+            a.y = 1.0;
+            a.bounces += 1;
+            if (a.bounces % p.speed_scale_every == 0) { a.vx = a.vx * p.speed_scale; a.vy = a.vy * p.speed_scale; }
+        } else {
+            rA = 1.f; rB = -1.f;
+            a.sA += 1;
+            done = a.sA >= p.max_score;
+        }
+    }
+    return done;
+}
+
+// ----------------------------------------------------------------------------- QNet
+enum : int { W1 = 0, B1 = 448, W2 = 512, B2 = 4608, WH = 4672, BH = 4928 };  // effective-weight offsets
+static_assert(BH + 4 == PM_QNET_NW, "effective weight layout");
+
+// Parameter-block offsets (pongmi.h PM_QNET_NP layout): heads at PM_QNET_HEAD_OFF, eps at PM_QNET_EPS_OFF
+enum : int {
+    P_VWMU = PM_QNET_HEAD_OFF + 0, P_VBMU = P_VWMU + 64, P_VWSG = P_VBMU + 1, P_VBSG = P_VWSG + 64,
+    P_AWMU = P_VBSG + 1, P_ABMU = P_AWMU + 192, P_AWSG = P_ABMU + 3, P_ABSG = P_AWSG + 192,
+    P_VWEP = PM_QNET_EPS_OFF + 0, P_VBEP = P_VWEP + 64, P_AWEP = P_VBEP + 1, P_ABEP = P_AWEP + 192,
+};
+static_assert(P_ABSG + 3 == PM_QNET_EPS_OFF, "head layout");
+static_assert(P_ABEP + 3 == PM_QNET_NP, "eps layout");
+
+// QNet.forward on one row per lane. `w` MUST be wave-uniform (same pointer in every lane).
+__device__ __forceinline__ void qnet_q(const float* __restrict__ w, const float* x, float* q) {
+    float h1[64];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        float a = w[B1 + j];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) a = fmaf(w[W1 + j * 7 + k], x[k], a);
+        h1[j] = fmaxf(a, 0.f);
+    }
+    float v = w[BH + 0], a0 = w[BH + 1], a1 = w[BH + 2], a2 = w[BH + 3];
+#pragma unroll 2
+    for (int j = 0; j < 64; ++j) {
+        float a = w[B2 + j];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) a = fmaf(w[W2 + j * 64 + k], h1[k], a);
+        a = fmaxf(a, 0.f);
+        v = fmaf(w[WH + j], a, v);
+        a0 = fmaf(w[WH + 64 + j], a, a0);
+        a1 = fmaf(w[WH + 128 + j], a, a1);
+        a2 = fmaf(w[WH + 192 + j], a, a2);
+    }
+    const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
+    q[0] = v + (a0 - mean);
+    q[1] = v + (a1 - mean);
+    q[2] = v + (a2 - mean);
+}
+
+// torch argmax: first maximal index
+__device__ __forceinline__ int argmax3(const float* q) {
+    int b = 0;
+    if (q[1] > q[b]) b = 1;
+    if (q[2] > q[b]) b = 2;
+    return b;
+}
+
+// Q for a per-lane opponent index: waterfall over the distinct ids present in the wave so that
+// each pass runs qnet_q with a wave-uniform weight pointer.
+__device__ __forceinline__ void qnet_q_grouped(const float* __restrict__ wtab, int id, const float* x, float* q,
+                                               bool active = true) {
+    bool pending = active;
+    while (true) {
+        const unsigned long long m = __ballot(pending);
+        if (m == 0ull) break;
+        const int lead = __ffsll((long long)m) - 1;
+        const int cur = __builtin_amdgcn_readfirstlane(__shfl(id, lead));
+        if (pending && id == cur) {
+            qnet_q(wtab + (size_t)cur * PM_QNET_NW, x, q);
+            pending = false;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- NoisyNet fold
+// Block-cooperative fold of one parameter block's heads into effective weights (models/qnet.py:43-50):
+//   EVAL: W = mu; TRAIN: W = mu + sigma*eps (block's eps buffers); TRAIN_FRESH: reset_noise()
+//   (models/qnet.py:33-41) from Philox(seed, tag, ctr) then TRAIN, the new eps written to eps_out.
+// `noise` is LDS scratch of >= 132 floats. Writes heads[0,260) = Wh [4][64] | bh [4] (the WH..BH+4
+// slice of an effective-weight block, or any 260-float scratch). Call with all threads.
+__device__ __forceinline__ void fold_heads(const float* params, float* eps_out, int mode, uint64_t seed, uint32_t tag,
+                                           uint64_t ctr, float* heads, float* noise) {
+    // noise: [0,64) f(eps_in) of fc_V | [64] f(eps_out) of fc_V | [65,129) f(eps_in) of fc_A | [129,132) f(eps_out) of fc_A
+    const int t = threadIdx.x, nt = blockDim.x;
+    if (mode == PM_FOLD_TRAIN_FRESH) {
+        for (int k = t; k < 132; k += nt) {
+            const uint32_t layer = k < 65 ? 0u : 1u;
+            const uint32_t kk = layer ? (uint32_t)(k - 65) : (uint32_t)k;
+            const uint32_t which = layer ? (kk < 64 ? 0u : 1u) : (kk < 64 ? 0u : 1u);
+            const uint32_t e = which ? kk - 64 : kk;
+            const U4 r = philox64(e, tag | (layer << 8) | (which << 12), ctr, seed);
+            noise[k] = scale_noise(normal(r.x, r.y, false));
+        }
+        __syncthreads();
+    }
+    for (int k = t; k < 260; k += nt) {
+        // k in [0,256): weight row k/64 (0 = V, 1..3 = A), column k%64; [256,260): biases
+        const int row = k < 256 ? k >> 6 : k - 256, col = k & 63;
+        const bool w = k < 256;
+        float mu, sg, ep = 0.f;
+        if (row == 0) {
+            mu = w ? params[P_VWMU + col] : params[P_VBMU];
+            sg = w ? params[P_VWSG + col] : params[P_VBSG];
+            if (mode == PM_FOLD_TRAIN) ep = w ? params[P_VWEP + col] : params[P_VBEP];
+            else if (mode == PM_FOLD_TRAIN_FRESH) ep = w ? noise[64] * noise[col] : noise[64];
+        } else {
+            const int a = row - 1;
+            mu = w ? params[P_AWMU + a * 64 + col] : params[P_ABMU + a];
+            sg = w ? params[P_AWSG + a * 64 + col] : params[P_ABSG + a];
+            if (mode == PM_FOLD_TRAIN) ep = w ? params[P_AWEP + a * 64 + col] : params[P_ABEP + a];
+            else if (mode == PM_FOLD_TRAIN_FRESH) ep = w ? noise[129 + a] * noise[65 + col] : noise[129 + a];
+        }
+        const float v = mode == PM_FOLD_EVAL ? mu : mu + sg * ep;
+        heads[w ? k : 256 + row] = v;
+        if (mode == PM_FOLD_TRAIN_FRESH && eps_out) {
+            if (row == 0) eps_out[w ? P_VWEP + col : P_VBEP] = ep;
+            else eps_out[w ? P_AWEP + (row - 1) * 64 + col : P_ABEP + row - 1] = ep;
+        }
+    }
+}
+
+}  // namespace pm

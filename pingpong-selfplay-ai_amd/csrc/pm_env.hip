@@ -1,0 +1,165 @@
+// K1 — batched PongEnv2P reset / step over struct-of-arrays fp64 arenas, one arena per lane.
+//
+// HBM-bound: per env-step 203 algorithmic bytes (fp64 state 7x8 read + write, int32 scores /
+// bounces 12 read + write, actions 2, obs 56, rewards 8, done 1). Observations leave the kernel
+// through an LDS transpose so every store is a full 16-byte-per-lane coalesced write.
+#include "pm_dev.h"
+#include "pm_host.h"
+
+using namespace pm;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// Stage [kBlock][7] floats per block in LDS and write them back as contiguous float4s.
+__device__ __forceinline__ void store_rows7(float* __restrict__ dst, float (*lds)[7], const float* row, int i0,
+                                            int n) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) lds[t][k] = row[k];
+    __syncthreads();
+    const int rows = min(kBlock, n - i0);
+    const int nf = rows * 7;
+    float* base = dst + (size_t)i0 * 7;
+    const float* src = &lds[0][0];
+    if (rows == kBlock && (((uintptr_t)base) & 15) == 0) {
+        float4* d4 = reinterpret_cast<float4*>(base);
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        for (int f = t; f < nf / 4; f += kBlock) d4[f] = s4[f];
+    } else {
+        for (int f = t; f < nf; f += kBlock) base[f] = src[f];
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void do_serve(const pm_env_params& p, const pm_env_state& s, Arena& a, int i,
+                                         const double* __restrict__ inject, int inject_cap, uint64_t seed,
+                                         int32_t* status) {
+    const int32_t ns = s.serves[i];
+    double vx, vy, sp;
+    if (inject) {
+        const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
+        vx = r[0]; vy = r[1]; sp = r[2];
+    } else {
+        philox_serve(p, (uint32_t)i, (uint32_t)ns, seed, vx, vy, sp);
+    }
+    serve(a, vx, vy, sp);
+    s.serves[i] = ns + 1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_env_reset(pm_env_params p, pm_env_state s, const uint8_t* __restrict__ mask,
+                                                      const double* __restrict__ inject, int inject_cap, uint64_t seed,
+                                                      float* __restrict__ obsA, float* __restrict__ obsB,
+                                                      int32_t* status, int n) {
+    __shared__ float lds[kBlock][7];
+    const int i0 = blockIdx.x * kBlock;
+    const int i = i0 + threadIdx.x;
+    float oA[7] = {0}, oB[7] = {0};
+    if (i < n) {
+        Arena a = load_arena(s, i);
+        if (!mask || mask[i]) {
+            do_serve(p, s, a, i, inject, inject_cap, seed, status);
+            store_arena(s, i, a);
+        }
+        observe(a, oA, oB);
+    }
+    if (obsA) store_rows7(obsA, lds, oA, i0, n);
+    if (obsB) store_rows7(obsB, lds, oB, i0, n);
+}
+
+__global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
+                                                     const int8_t* __restrict__ aB, float* __restrict__ obsA,
+                                                     float* __restrict__ obsB, float* __restrict__ rA,
+                                                     float* __restrict__ rB, uint8_t* __restrict__ done,
+                                                     float* __restrict__ tobsA, float* __restrict__ tobsB,
+                                                     int autoreset, const double* __restrict__ inject, int inject_cap,
+                                                     uint64_t seed, int32_t* status, int n) {
+    __shared__ float lds[kBlock][7];
+    const int i0 = blockIdx.x * kBlock;
+    const int i = i0 + threadIdx.x;
+    float oA[7] = {0}, oB[7] = {0};
+    float tA[7] = {0}, tB[7] = {0};
+    if (i < n) {
+        Arena a = load_arena(s, i);
+        float ra, rb;
+        const int d = tick(p, a, aA[i], aB[i], ra, rb);
+        observe(a, oA, oB);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) { tA[k] = oA[k]; tB[k] = oB[k]; }
+        if (autoreset && d) {
+            do_serve(p, s, a, i, inject, inject_cap, seed, status);
+            observe(a, oA, oB);
+        }
+        store_arena(s, i, a);
+        rA[i] = ra;
+        rB[i] = rb;
+        done[i] = (uint8_t)d;
+    }
+    store_rows7(obsA, lds, oA, i0, n);
+    store_rows7(obsB, lds, oB, i0, n);
+    if (tobsA) store_rows7(tobsA, lds, tA, i0, n);
+    if (tobsB) store_rows7(tobsB, lds, tB, i0, n);
+}
+
+__global__ __launch_bounds__(kBlock) void k_collide(const double* __restrict__ in, const double* __restrict__ inertia,
+                                                    double* __restrict__ out, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const double* r = in + (size_t)i * 8;
+    pm_env_params p = {};
+    p.restitution = r[4]; p.friction = r[5]; p.ball_mass = r[6]; p.radius = r[7];
+    p.inertia = inertia[i];
+    p.jt_coef = (2.0 * r[6]) / 7.0;
+    double vn2, vt2, om2;
+    collide(p, r[0], r[1], r[2], r[3], vn2, vt2, om2);
+    out[(size_t)i * 3 + 0] = vn2;
+    out[(size_t)i * 3 + 1] = vt2;
+    out[(size_t)i * 3 + 2] = om2;
+}
+
+bool state_ok(const pm_env_state* s) {
+    return s && s->x && s->y && s->vx && s->vy && s->spin && s->top && s->bot && s->scoreA && s->scoreB &&
+           s->bounces && s->serves;
+}
+
+}  // namespace
+
+extern "C" int pm_env_reset(const pm_env_params* p, const pm_env_state* s, const uint8_t* mask, const double* inject,
+                            int32_t inject_cap, uint64_t seed, float* obsA, float* obsB, int32_t* status, int32_t n,
+                            void* stream) {
+    PM_REQUIRE(p && state_ok(s), PM_E_ARG, "pm_env_reset: null params/state");
+    PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_env_reset: n=%d", n);
+    PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_reset: inject without capacity");
+    PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_reset: speed_scale_every must be > 0");
+    if (n == 0) return PM_OK;
+    hipLaunchKernelGGL(k_env_reset, dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *p, *s, mask,
+                       inject, inject_cap, seed, obsA, obsB, status, n);
+    PM_LAUNCHED("k_env_reset");
+    return PM_OK;
+}
+
+extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const int8_t* aA, const int8_t* aB,
+                           float* obsA, float* obsB, float* rA, float* rB, uint8_t* done, float* term_obsA,
+                           float* term_obsB, int32_t autoreset, const double* inject, int32_t inject_cap,
+                           uint64_t seed, int32_t* status, int32_t n, void* stream) {
+    PM_REQUIRE(p && state_ok(s), PM_E_ARG, "pm_env_step: null params/state");
+    PM_REQUIRE(aA && aB && obsA && obsB && rA && rB && done, PM_E_ARG, "pm_env_step: null buffer");
+    PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_env_step: n=%d", n);
+    PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
+    PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
+    if (n == 0) return PM_OK;
+    hipLaunchKernelGGL(k_env_step, dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *p, *s, aA, aB,
+                       obsA, obsB, rA, rB, done, term_obsA, term_obsB, autoreset, inject, inject_cap, seed, status, n);
+    PM_LAUNCHED("k_env_step");
+    return PM_OK;
+}
+
+extern "C" int pm_collide(const double* in, const double* inertia, double* out, int32_t n, void* stream) {
+    PM_REQUIRE(in && inertia && out, PM_E_ARG, "pm_collide: null buffer");
+    PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_collide: n=%d", n);
+    if (n == 0) return PM_OK;
+    hipLaunchKernelGGL(k_collide, dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0, pm_stream(stream), in, inertia, out, n);
+    PM_LAUNCHED("k_collide");
+    return PM_OK;
+}

@@ -1,0 +1,420 @@
+// The batched self-play learner: one vector step of scripts/train_iterative.py:239-245 for n arenas.
+//
+//   k_rollout   (n lanes)      act both players + env tick + replay push + episode bookkeeping
+//   k_per_reduce (<=4096 WGs)  per-1024 block sums of prio^alpha              [pm_replay.hip]
+//   k_sp_sample (batch waves)  proportional sample + un-normalised IS weights
+//   k_dqn_feat  (2*batch rows) frozen features h2 = relu(W2 relu(W1 x + b1) + b2) of s and s'
+//   k_dqn       (1 WG)         double-DQN heads, IS-weighted MSE, head grads, priority update
+//   ----------------------------- (sharded: RCCL all-reduce of sp.grad here)
+//   k_adam      (1 WG)         Adam on the 520 head params, target sync, epsilon decay,
+//                              replay/step counters, next step's acting noise
+//
+// Nothing returns to the host: every loop counter lives in the device control block (pm_ctrl), so
+// a whole vector step can be replayed from a captured graph.
+#include "pm_dev.h"
+#include "pm_host.h"
+#include "pm_per.h"
+
+using namespace pm;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kGradN = PM_QNET_NHEAD;  // grad[520] = finished episodes, grad[521] = updated flag
+
+__device__ __forceinline__ bool learner_active(const pm_selfplay& sp) {
+    const int64_t s = sp.ctrl->size + sp.n;
+    return (s < sp.cap ? s : sp.cap) >= sp.batch;
+}
+
+// ------------------------------------------------------------------------------------ rollout
+__global__ __launch_bounds__(kBlock) void k_rollout(const pm_selfplay sp) {
+    __shared__ long long red[kBlock / 64][6];
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = i < sp.n;
+    const int ii = valid ? i : sp.n - 1;
+    const pm_ctrl* c = sp.ctrl;
+    const uint64_t step = c->step;
+    const int64_t pos = c->pos, size = c->size;
+    const double eps = c->epsilon;
+    const float maxp = size == 0 ? 1.0f : c->max_prio;  // max(prios) if buffer else 1.0 (:57)
+
+    Arena a = load_arena(sp.st, ii);
+    float oA[7], oB[7];
+    observe(a, oA, oB);
+    const int o = min(max(sp.opp[ii], 0), sp.n_pool);
+    float qa[3], qb[3];
+    qnet_q_grouped(sp.w_opp, o, oA, qa, valid);  // opponent: modelA or a pool net (:235-236,240)
+    qnet_q(sp.w_B, oB, qb);                      // modelB with this step's noise (:124-130)
+    const int aA = argmax3(qa);
+    const U4 r = philox64((uint32_t)ii, TAG_ACT, step, sp.seed_env);
+    const int aB = u53(r.x, r.y) < eps ? below(r.z, 3u) : argmax3(qb);
+
+    float rA, rB;
+    const int d = tick(sp.env, a, aA, aB, rA, rB);
+    float nA[7], nB[7];
+    observe(a, nA, nB);
+    const float er = sp.ep_reward[ii] + rB;  // ep_reward += rB (:245)
+    const bool fin = valid && d;
+
+    // ---- episode bookkeeping: per-block partials, no atomics (:247-249)
+    {
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const bool win = er > 0.f;
+        const unsigned long long mf = __ballot(fin), mA = __ballot(fin && o == 0), mwA = __ballot(fin && o == 0 && win);
+        const unsigned long long mP = __ballot(fin && o != 0), mwP = __ballot(fin && o != 0 && win);
+        int rs = fin ? (int)er : 0;
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) rs += __shfl_xor(rs, s);
+        if (lane == 0) {
+            red[wv][0] = __popcll(mf); red[wv][1] = __popcll(mA); red[wv][2] = __popcll(mwA);
+            red[wv][3] = __popcll(mP); red[wv][4] = __popcll(mwP); red[wv][5] = rs;
+        }
+        __syncthreads();
+        if (threadIdx.x < 6) {
+            long long t = 0;
+            for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
+            sp.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = t;
+        }
+    }
+    if (!valid) return;
+
+    // ---- memory.push((oB, aB, rB, nB, done)) (:243, :56-63)
+    const int64_t slot = (pos + i) % sp.cap;
+    float4* row = reinterpret_cast<float4*>(sp.trans + slot * PM_TRANS_F);
+    row[0] = make_float4(oB[0], oB[1], oB[2], oB[3]);
+    row[1] = make_float4(oB[4], oB[5], oB[6], rB);
+    row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
+    row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
+    sp.prios[slot] = maxp;
+
+    int onew = o;
+    float ernew = er;
+    if (d) {  // next episode: opponent draw (:235-236) then env.reset() (:238)
+        const uint32_t ns = (uint32_t)sp.st.serves[i];
+        const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
+        onew = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
+        double vx, vy, spn;
+        philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
+        serve(a, vx, vy, spn);
+        sp.st.serves[i] = (int32_t)ns + 1;
+        ernew = 0.f;
+    }
+    store_arena(sp.st, i, a);
+    sp.opp[i] = onew;
+    sp.ep_reward[i] = ernew;
+}
+
+// ------------------------------------------------------------------------------------ init
+__global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= sp.n) return;
+    const uint32_t ns = (uint32_t)sp.st.serves[i];
+    const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
+    sp.opp[i] = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
+    Arena a;
+    double vx, vy, spn;
+    philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
+    serve(a, vx, vy, spn);
+    store_arena(sp.st, i, a);
+    sp.st.serves[i] = (int32_t)ns + 1;
+    sp.ep_reward[i] = 0.f;
+}
+
+// ------------------------------------------------------------------------------------ learner
+__device__ __forceinline__ double beta_of(const pm_selfplay& sp, int64_t frame) {  // :137
+    const double b = sp.beta_start + (double)frame * (1.0 - sp.beta_start) / (double)sp.beta_frames;
+    return b < 1.0 ? b : 1.0;
+}
+
+__global__ __launch_bounds__(256) void k_sp_sample(const pm_selfplay sp, const double* __restrict__ bsum) {
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= sp.batch || !learner_active(sp)) return;  // wave-uniform
+    const int64_t s = sp.ctrl->size + sp.n;
+    const int64_t size = s < sp.cap ? s : sp.cap;
+    const int64_t frame = sp.ctrl->frame_idx + 1;  // frame_idx += 1 before sampling (:136)
+    const U4 r = philox64((uint32_t)j, TAG_PER, (uint64_t)frame, sp.seed_env);
+    int64_t idx;
+    float wr;
+    per_sample_one(sp.prios, size, bsum, (float)sp.alpha, beta_of(sp, frame), u53(r.x, r.y), idx, wr);
+    if ((threadIdx.x & 63) == 0) { sp.idx[j] = idx; sp.isw[j] = wr; }
+}
+
+// features of the 2*batch rows (s then s'): 64 rows per block, wave w owns outputs [16w, 16w+16)
+__global__ __launch_bounds__(256) void k_dqn_feat(const pm_selfplay sp) {
+    __shared__ float h1s[64][65];
+    if (!learner_active(sp)) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int row = blockIdx.x * 64 + lane;
+    const int nrows = 2 * sp.batch;
+    const int rr = row < nrows ? row : nrows - 1;
+    const int j = rr < sp.batch ? rr : rr - sp.batch;
+    const float* tr = sp.trans + sp.idx[j] * PM_TRANS_F + (rr < sp.batch ? 0 : 8);
+    float x[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) x[k] = tr[k];
+    const float* __restrict__ w = sp.paramsB;  // modelB.features (frozen, == targetB.features)
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+        const int o = wv * 16 + jj;
+        float a = w[B1 + o];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) a = fmaf(w[W1 + o * 7 + k], x[k], a);
+        h1s[lane][o] = fmaxf(a, 0.f);
+    }
+    __syncthreads();
+    float h1[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) h1[k] = h1s[lane][k];
+    float* out = sp.hfeat + (size_t)rr * 64;
+#pragma unroll 4
+    for (int jj = 0; jj < 16; ++jj) {
+        const int o = wv * 16 + jj;
+        float a = w[B2 + o];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) a = fmaf(w[W2 + o * 64 + k], h1[k], a);
+        if (row < nrows) out[o] = fmaxf(a, 0.f);
+    }
+}
+
+// heads on one feature row: V, A0..2 -> dueling Q (models/qnet.py:71-75)
+__device__ __forceinline__ void heads_q(const float* hw, const float* h, float* q) {
+    float v = hw[256], a0 = hw[257], a1 = hw[258], a2 = hw[259];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        v = fmaf(hw[k], h[k], v);
+        a0 = fmaf(hw[64 + k], h[k], a0);
+        a1 = fmaf(hw[128 + k], h[k], a1);
+        a2 = fmaf(hw[192 + k], h[k], a2);
+    }
+    const float mean = ((a0 + a1) + a2) / 3.0f;
+    q[0] = v + (a0 - mean);
+    q[1] = v + (a1 - mean);
+    q[2] = v + (a2 - mean);
+}
+
+__global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
+    __shared__ float Hs[PM_MAX_BATCH][65];
+    __shared__ float coef[PM_MAX_BATCH][4];
+    __shared__ float hwB[260], hwT[260], noise[132];
+    __shared__ int64_t sidx[PM_MAX_BATCH];
+    __shared__ float red[4][2];
+    __shared__ long long cnt[6];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    pm_ctrl* c = sp.ctrl;
+
+    // ---- rollout partials -> episode counters (fixed order)
+    if (t < 6) {
+        const int nbr = (sp.n + kBlock - 1) / kBlock;
+        long long s = 0;
+        for (int b = 0; b < nbr; ++b) s += sp.partials[(size_t)b * 8 + t];
+        cnt[t] = s;
+    }
+    __syncthreads();
+    const bool train = learner_active(sp);
+    if (t == 0) {
+        c->ep_step = cnt[0];
+        c->episodes += cnt[0];
+        c->ep_A += cnt[1]; c->win_A += cnt[2];
+        c->ep_P += cnt[3]; c->win_P += cnt[4];
+        c->reward_B += (double)cnt[5];
+        sp.grad[kGradN] = (float)cnt[0];
+        sp.grad[kGradN + 1] = train ? 1.f : 0.f;
+    }
+    if (!train) {
+        for (int k = t; k < kGradN; k += 256) sp.grad[k] = 0.f;
+        return;
+    }
+
+    // ---- fresh noise for modelB (reset_noise, :142); targetB is in eval mode -> mu (:100)
+    // (the fresh eps lands in modelB's epsilon buffers, as reset_noise leaves them in the reference)
+    fold_heads(sp.paramsB, sp.paramsB, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_TRAIN,
+               (uint64_t)(c->train_steps + 1), hwB, noise);
+    fold_heads(sp.paramsT, nullptr, PM_FOLD_EVAL, 0, 0, 0, hwT, nullptr);
+    __syncthreads();
+
+    const int B = sp.batch;
+    const bool act = t < B;
+    // ---- IS weights: w /= max(w) over the batch (:72)
+    float wraw = act ? sp.isw[t] : 0.f;
+    {
+        float m = wraw;
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
+        if (lane == 0) red[wv][0] = m;
+    }
+    __syncthreads();
+    const float wmax = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
+    float lossp = 0.f, prio = 0.f;
+    if (act) {
+        const int64_t id = sp.idx[t];
+        sidx[t] = id;
+        const float* tr = sp.trans + id * PM_TRANS_F;
+        const float rwd = tr[7];
+        const int bits = __float_as_int(tr[15]);
+        const int a = bits & 0xff, dn = (bits >> 8) & 1;
+        float h[64], qs[3], qn[3], qt[3];
+        const float* hs = sp.hfeat + (size_t)t * 64;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) { h[k] = hs[k]; Hs[t][k] = h[k]; }
+        heads_q(hwB, h, qs);                      // modelB(s)                (:152)
+        const float* hn = sp.hfeat + (size_t)(B + t) * 64;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) h[k] = hn[k];
+        heads_q(hwB, h, qn);                      // modelB(ns).argmax        (:154)
+        heads_q(hwT, h, qt);                      // targetB(ns)              (:155)
+        const float q = qs[a];
+        const float nq = qt[argmax3(qn)];
+        const float tgt = rwd + (float)sp.gamma * nq * (dn ? 0.f : 1.f);  // r + gamma*nq*(~d) (:156)
+        const float diff = q - tgt;
+        const float w = wraw / wmax;
+        lossp = w * (diff * diff);
+        const float g = 2.f * w * diff / (float)B;  // d mean(w (q-t)^2) / dq
+        coef[t][0] = g;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) coef[t][1 + k] = g * ((k == a ? 1.f : 0.f) - 1.f / 3.f);
+        prio = fabsf(diff) + 1e-6f;                 // |err| + 1e-6 (:76)
+    }
+    {
+        float s = lossp, m = prio;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o); m = fmaxf(m, __shfl_xor(m, o)); }
+        __syncthreads();
+        if (lane == 0) { red[wv][0] = s; red[wv][1] = m; }
+    }
+    __syncthreads();
+    if (act) {  // update_priorities: sequential order, the last duplicate wins (:74-76)
+        bool last = true;
+        for (int k = t + 1; k < B; ++k) last &= sidx[k] != sidx[t];
+        if (last) sp.prios[sidx[t]] = prio;
+    }
+    if (t == 0) {
+        c->last_loss = (((red[0][0] + red[1][0]) + red[2][0]) + red[3][0]) / (float)B;
+        const float mp = fmaxf(fmaxf(red[0][1], red[1][1]), fmaxf(red[2][1], red[3][1]));
+        c->max_prio = fmaxf(c->max_prio, mp);  // n > batch pushes of max_prio survive the scatter
+    }
+    // ---- head gradients: dL/dW_mu = sum_j coef_j h_j ; dL/dW_sigma = dL/dW_mu * eps
+    for (int o = t; o < 260; o += 256) {
+        const int row = o < 256 ? o >> 6 : o - 256, col = o & 63;
+        const bool wgt = o < 256;
+        float g = 0.f;
+        for (int j = 0; j < B; ++j) g = fmaf(coef[j][row], wgt ? Hs[j][col] : 1.f, g);
+        const float ein = wgt ? (row == 0 ? noise[col] : noise[65 + col]) : 1.f;
+        const float eout = row == 0 ? noise[64] : noise[129 + row - 1];
+        const float eps = ein * eout;  // weight_epsilon / bias_epsilon entry
+        if (row == 0) {
+            sp.grad[(wgt ? 0 : 64) + (wgt ? col : 0)] = g;            // fc_V.weight_mu / bias_mu
+            sp.grad[(wgt ? 65 : 129) + (wgt ? col : 0)] = g * eps;    // fc_V.weight_sigma / bias_sigma
+        } else {
+            const int a = row - 1;
+            sp.grad[wgt ? 130 + a * 64 + col : 322 + a] = g;          // fc_A.weight_mu / bias_mu
+            sp.grad[wgt ? 325 + a * 64 + col : 517 + a] = g * eps;    // fc_A.weight_sigma / bias_sigma
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------ Adam + commit
+__global__ __launch_bounds__(1024) void k_adam(const pm_selfplay sp) {
+    __shared__ float noise[132];
+    const int t = threadIdx.x;
+    pm_ctrl* c = sp.ctrl;
+    const bool train = sp.grad[kGradN + 1] > 0.5f;
+    const int64_t ts = c->train_steps + (train ? 1 : 0);
+    if (train && t < PM_QNET_NHEAD) {  // torch.optim.Adam step (:161)
+        const float g = sp.grad[t] / (float)sp.world;
+        float m = sp.adam_m[t], v = sp.adam_v[t];
+        m = m + (float)(1.0 - sp.beta1) * (g - m);  // exp_avg.lerp_(grad, 1-beta1)
+        v = v * (float)sp.beta2 + (float)(1.0 - sp.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
+        const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
+        const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
+        const float step_size = (float)(sp.lr / bc1);
+        const float denom = sqrtf(v) / (float)sqrt(bc2) + (float)sp.adam_eps;
+        float* p = sp.paramsB + PM_QNET_HEAD_OFF + t;
+        *p = *p - step_size * (m / denom);
+        sp.adam_m[t] = m;
+        sp.adam_v[t] = v;
+    }
+    __syncthreads();
+    if (train && ts % sp.target_update_interval == 0) {  // targetB.load_state_dict(modelB) (:166-168)
+        for (int k = t; k < PM_QNET_NP; k += 1024) sp.paramsT[k] = sp.paramsB[k];
+    }
+    // next vector step's acting noise for modelB (select_action_B -> reset_noise, :125)
+    fold_heads(sp.paramsB, sp.paramsB, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_ACT, c->step + 1, sp.w_B + WH,
+               noise);
+    __syncthreads();
+    if (t == 0) {
+        const double D = (double)sp.grad[kGradN];  // finished episodes (all shards)
+        const double e = c->epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
+        c->epsilon = e > sp.min_epsilon ? e : sp.min_epsilon;
+        if (train) { c->train_steps = ts; c->frame_idx += 1; }
+        c->pos = (c->pos + sp.n) % sp.cap;
+        const int64_t s = c->size + sp.n;
+        c->size = s < sp.cap ? s : sp.cap;
+        c->step += 1;
+    }
+}
+
+int check(const pm_selfplay* sp) {
+    PM_REQUIRE(sp && sp->ctrl && sp->trans && sp->prios && sp->per_work && sp->idx && sp->isw && sp->grad &&
+                   sp->partials && sp->hfeat && sp->w_opp && sp->paramsB && sp->paramsT && sp->w_B && sp->adam_m &&
+                   sp->adam_v && sp->opp && sp->ep_reward,
+               PM_E_ARG, "pm_selfplay: null buffer");
+    PM_REQUIRE(sp->n > 0 && sp->batch >= 1 && sp->batch <= PM_MAX_BATCH && sp->n > sp->batch && sp->cap >= sp->n,
+               PM_E_SIZE, "pm_selfplay: n=%d batch=%d cap=%lld", sp->n, sp->batch, (long long)sp->cap);
+    PM_REQUIRE(sp->n_pool >= 0 && sp->n_pool <= 4096 && sp->world >= 1, PM_E_SIZE, "pm_selfplay: n_pool/world");
+    PM_REQUIRE(sp->env.speed_scale_every > 0 && sp->target_update_interval > 0 && sp->beta_frames > 0, PM_E_ARG,
+               "pm_selfplay: zero interval");
+    return PM_OK;
+}
+
+}  // namespace
+
+extern "C" int pm_selfplay_init(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipStream_t st = pm_stream(stream);
+    hipLaunchKernelGGL(k_sp_init, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, st, *sp);
+    PM_LAUNCHED("k_sp_init");
+    // acting weights of step ctrl->step: features + heads folded with fresh noise, eps kept in paramsB
+    return pm_qnet_fold(sp->paramsB, sp->paramsB, PM_FOLD_TRAIN_FRESH, sp->seed_net, 0, &sp->ctrl->step, sp->w_B, 1,
+                        stream);
+}
+
+extern "C" int pm_selfplay_rollout(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_rollout, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *sp);
+    PM_LAUNCHED("k_rollout");
+    return PM_OK;
+}
+
+extern "C" int pm_selfplay_learn(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipStream_t st = pm_stream(stream);
+    double* bsum = reinterpret_cast<double*>(sp->per_work);
+    PerSize sz{0, sp->ctrl, sp->n, sp->cap};
+    rc = per_launch_reduce(sp->prios, sz, sp->cap, (float)sp->alpha, bsum, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_sp_sample, dim3(pm_blocks(sp->batch, 4)), dim3(256), 0, st, *sp, bsum);
+    PM_LAUNCHED("k_sp_sample");
+    hipLaunchKernelGGL(k_dqn_feat, dim3(pm_blocks(2 * sp->batch, 64)), dim3(256), 0, st, *sp);
+    PM_LAUNCHED("k_dqn_feat");
+    hipLaunchKernelGGL(k_dqn, dim3(1), dim3(256), 0, st, *sp);
+    PM_LAUNCHED("k_dqn");
+    return PM_OK;
+}
+
+extern "C" int pm_selfplay_apply(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_adam, dim3(1), dim3(1024), 0, pm_stream(stream), *sp);
+    PM_LAUNCHED("k_adam");
+    return PM_OK;
+}
+
+extern "C" int pm_selfplay_step(const pm_selfplay* sp, void* stream) {
+    int rc = pm_selfplay_rollout(sp, stream);
+    if (!rc) rc = pm_selfplay_learn(sp, stream);
+    return rc ? rc : pm_selfplay_apply(sp, stream);
+}

@@ -1,0 +1,190 @@
+"""The batched self-play DQN learner: scripts/train_iterative.py's hot loop (:239-245) for n arenas
+per device, as four libpongmi launches sequences per vector step (rollout / learn / [all-reduce] /
+apply) on one stream, with every loop counter in a device control block.
+
+Semantics the batching fixes (the reference steps ONE env and updates once per env step):
+  * one vector step = one env step in every arena; one PER update of `batch` per vector step
+    (`updates_per_step` repeats learn+apply);
+  * NoisyNet acting noise is fresh per vector step and shared by all arenas (reset_noise per
+    select_action_B, :125), the update draws its own fresh noise (:142);
+  * epsilon decays once per finished episode: eps <- max(min_eps, eps * decay^D) for the D
+    episodes finished in a vector step (:261);
+  * each episode independently plays modelA or (p = opponent_pool_ratio) a uniformly drawn pool
+    net (:235-236);
+  * pushes of a vector step all receive the max priority held before the step (:57).
+Sharded (world > 1): every rank owns n arenas and its own replay; `sp.grad` (520 head grads +
+counters) is summed by one all-reduce per update and every rank applies the identical Adam step.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import PM_QNET_NHEAD, PM_QNET_NP, PM_QNET_NW, PM_TRANS_F, check, ptr, stream_ptr
+from .env import env_config, env_params
+from .qnet import HEAD_KEYS, fold, pack_state_dict, unpack_state_dict
+
+
+def splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+class SelfPlayLearner:
+    def __init__(self, env_kw, n_arenas, modelB_state, modelA_state=None, pool_states=(), *, batch=256,
+                 memory_size=1_000_000, gamma=0.99, lr=2.5e-4, epsilon=0.02, min_epsilon=0.02, epsilon_decay=0.995,
+                 target_update_interval=1000, pool_ratio=0.33, alpha=0.6, beta_start=0.4, beta_frames=100000,
+                 episode=0, seed=0, rank=0, world=1, allreduce=None, device=None, modelA_noisy=True):
+        self.lib = _lib.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise _lib.PongmiError("SelfPlayLearner runs on a ROCm device only")
+        self.n, self.batch, self.cap = int(n_arenas), int(batch), int(memory_size)
+        self.world, self.rank = int(world), int(rank)
+        if self.world > 1 and allreduce is None:
+            raise ValueError("world > 1 needs an allreduce(tensor) callable (torch.distributed.all_reduce)")
+        self.allreduce = allreduce
+        self.env_cfg = env_config(**env_kw)
+        dev, n = self.device, self.n
+        f32 = dict(dtype=torch.float32, device=dev)
+
+        # ---- environment SoA + per-arena bookkeeping
+        self.f64 = torch.zeros((7, n), dtype=torch.float64, device=dev)
+        self.i32 = torch.zeros((4, n), dtype=torch.int32, device=dev)
+        self.opp = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.ep_reward = torch.zeros(n, **f32)
+        # ---- networks
+        self.paramsB = pack_state_dict(modelB_state, dev)
+        self.paramsT = self.paramsB.clone()
+        self.adam_m = torch.zeros(PM_QNET_NHEAD, **f32)
+        self.adam_v = torch.zeros(PM_QNET_NHEAD, **f32)
+        self.w_B = torch.zeros(PM_QNET_NW, **f32)
+        self.n_pool = len(pool_states)
+        self.w_opp = torch.zeros((1 + self.n_pool, PM_QNET_NW), **f32)
+        self.modelA_noisy = modelA_noisy
+        self.set_modelA(modelA_state if modelA_state is not None else modelB_state)
+        if self.n_pool:
+            pool = torch.stack([pack_state_dict(s, dev) for s in pool_states])
+            self.w_opp[1:] = fold(pool, _lib.PM_FOLD_EVAL)  # pool nets are .eval() (:205)
+        # ---- replay + learner scratch
+        self.trans = torch.zeros((self.cap, PM_TRANS_F), **f32)
+        self.prios = torch.zeros(self.cap, **f32)
+        self.per_work = torch.zeros(max(self.lib.pm_per_work_bytes(self.cap), 256), dtype=torch.uint8, device=dev)
+        self.idx = torch.zeros(self.batch, dtype=torch.int64, device=dev)
+        self.isw = torch.zeros(self.batch, **f32)
+        self.grad = torch.zeros(PM_QNET_NHEAD + 8, **f32)
+        self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
+        self.hfeat = torch.zeros((2 * self.batch, 64), **f32)
+        # ---- control block
+        c = _lib.Ctrl()
+        c.epsilon = float(epsilon)
+        c.max_prio = 1.0
+        c.episodes = int(episode)
+        self.ctrl = torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8).to(dev)
+
+        self.seed = int(seed)
+        sp = _lib.SelfPlay()
+        sp.env = env_params(**env_kw)
+        sp.st = _lib.EnvState(*[ptr(self.f64[k]) for k in range(7)], *[ptr(self.i32[k]) for k in range(4)])
+        for name in ("opp", "ep_reward", "w_opp", "paramsB", "paramsT", "w_B", "adam_m", "adam_v", "trans", "prios",
+                     "per_work", "idx", "isw", "grad", "partials", "hfeat", "ctrl"):
+            setattr(sp, name, ptr(getattr(self, name)))
+        sp.n, sp.n_pool, sp.batch, sp.world, sp.cap = n, self.n_pool, self.batch, self.world, self.cap
+        sp.gamma, sp.alpha, sp.lr = gamma, alpha, lr
+        sp.beta1, sp.beta2, sp.adam_eps = 0.9, 0.999, 1e-8
+        sp.min_epsilon, sp.epsilon_decay, sp.pool_ratio, sp.beta_start = min_epsilon, epsilon_decay, pool_ratio, beta_start
+        sp.beta_frames, sp.target_update_interval = int(beta_frames), int(target_update_interval)
+        sp.seed_env = splitmix64(self.seed * 0x100000001B3 + 1 + self.rank)
+        sp.seed_net = splitmix64(self.seed ^ 0x5EED5EED5EED)
+        self.sp = sp
+        self.hparams = dict(gamma=gamma, lr=lr, min_epsilon=min_epsilon, epsilon_decay=epsilon_decay,
+                            target_update_interval=target_update_interval, pool_ratio=pool_ratio, alpha=alpha,
+                            beta_start=beta_start, beta_frames=beta_frames)
+        check(self.lib.pm_selfplay_init(ctypes.byref(sp), stream_ptr()), "pm_selfplay_init")
+
+    # ------------------------------------------------------------------ stepping
+    def rollout(self):
+        check(self.lib.pm_selfplay_rollout(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_rollout")
+
+    def learn(self):
+        check(self.lib.pm_selfplay_learn(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_learn")
+
+    def apply(self):
+        check(self.lib.pm_selfplay_apply(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_apply")
+
+    def step(self):
+        """One vector step (n env-steps on this rank)."""
+        if self.world == 1:
+            check(self.lib.pm_selfplay_step(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step")
+            return
+        self.rollout()
+        self.learn()
+        self.allreduce(self.grad)  # one RCCL all-reduce per update: 520 grads + counters
+        self.apply()
+
+    # ------------------------------------------------------------------ state readout (syncs)
+    def counters(self):
+        c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))
+        return {k: getattr(c, k) for k, _ in _lib.Ctrl._fields_ if not k.startswith("_")}
+
+    def set_epsilon(self, eps):
+        c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))
+        c.epsilon = float(eps)
+        self.ctrl.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
+
+    def modelB_state_dict(self):
+        return unpack_state_dict(self.paramsB)
+
+    def targetB_state_dict(self):
+        return unpack_state_dict(self.paramsT)
+
+    def set_modelA(self, state):
+        """Opponent slot 0. modelA is never put in eval() by the reference (train_iterative.py:90-92),
+        so it acts with its frozen epsilon buffers: W = mu + sigma*eps."""
+        self.paramsA = pack_state_dict(state, self.device)
+        self.w_opp[0] = fold(self.paramsA, _lib.PM_FOLD_TRAIN if self.modelA_noisy else _lib.PM_FOLD_EVAL)[0]
+
+    def modelA_state_dict(self):
+        return unpack_state_dict(self.paramsA)
+
+    def optimizer_state_dict(self):
+        """torch.optim.Adam state_dict for the 8 head tensors (train_iterative.py:101-104)."""
+        c = self.counters()
+        m, v = self.adam_m.cpu(), self.adam_v.cpu()
+        state, o = {}, 0
+        shapes = [(1, 64), (1,), (1, 64), (1,), (3, 64), (3,), (3, 64), (3,)]
+        for i, s in enumerate(shapes):
+            k = int(np.prod(s))
+            if c["train_steps"] > 0:
+                state[i] = {"step": torch.tensor(float(c["train_steps"])), "exp_avg": m[o:o + k].reshape(s).clone(),
+                            "exp_avg_sq": v[o:o + k].reshape(s).clone()}
+            o += k
+        return {"state": state, "param_groups": [{
+            "lr": self.hparams["lr"], "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 0, "amsgrad": False,
+            "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+            "decoupled_weight_decay": False, "params": list(range(8))}]}
+
+    def reset_B(self, state, epsilon=1.0):
+        """reset_B (train_iterative.py:213-224): fresh modelB from `state`, new Adam, empty replay,
+        epsilon 1.0, target = modelB, train_steps = frame_idx = 0."""
+        self.paramsB.copy_(pack_state_dict(state, self.device))
+        self.paramsT.copy_(self.paramsB)
+        self.adam_m.zero_()
+        self.adam_v.zero_()
+        self.prios.zero_()
+        c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))
+        c.pos = c.size = c.train_steps = c.frame_idx = 0
+        c.max_prio = 1.0
+        c.epsilon = float(epsilon)
+        self.ctrl.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
+        # acting weights for the current step from the new parameters
+        w = fold(self.paramsB, _lib.PM_FOLD_TRAIN_FRESH, seed=self.sp.seed_net,
+                 counter_dev=self.ctrl[:8].view(torch.int64), params_out=self.paramsB)
+        self.w_B.copy_(w[0])
+
+
+HEAD_NAMES = HEAD_KEYS
+__all__ = ["SelfPlayLearner", "splitmix64", "HEAD_NAMES", "PM_QNET_NP"]

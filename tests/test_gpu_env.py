@@ -1,0 +1,140 @@
+"""K1 parity on the device: pm_env_reset / pm_env_step / pm_collide against the reference's own
+trajectories (tests/golden, bit-exact) and against the oracle at full batch sizes (bit-exact)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+STATE_ORDER = ("x", "y", "vx", "vy", "spin", "top", "bot", "scoreA", "scoreB", "bounces")
+
+
+def _kwargs_from_golden(g):
+    pv = dict(zip([str(n) for n in g["param_names"]], g["param_values"].tolist()))
+    return dict(paddle_width=pv["paddle_width"], paddle_speed=pv["paddle_speed"], max_score=int(pv["max_score"]),
+                enable_spin=bool(pv["enable_spin"]), magnus_factor=pv["magnus_factor"],
+                restitution=pv["restitution"], friction=pv["friction"], ball_mass=pv["ball_mass"],
+                world_ball_radius=pv["world_ball_radius"], ball_speed_range=(pv["speed_lo"], pv["speed_hi"]),
+                spin_range=(pv["spin_lo"], pv["spin_hi"]),
+                ball_angle_intervals=[[pv["ang0_lo"], pv["ang0_hi"]], [pv["ang1_lo"], pv["ang1_hi"]]],
+                speed_scale_every=int(pv["speed_scale_every"]), speed_increment=pv["speed_increment"]), pv
+
+
+def _state_matrix(env):
+    st = env.get_state()
+    return np.stack([np.asarray(st[k], np.float64) for k in STATE_ORDER], 1)
+
+
+@pytest.mark.parametrize("name", ["cfg", "rnn", "default"])
+def test_env_matches_reference_trajectories_bit_exact(golden, name):
+    """All golden arenas stepped in one batch with the recorded actions; serves drawn host-side
+    with CPython's random exactly as the reference (parity mode). Every fp64 state word, obs,
+    reward, done and score must be identical at every step, including autoreset serves."""
+    from pongmi.env import PongEnv2PBatch, serve_table_from_random
+
+    g = golden(f"env_{name}")
+    kw, _ = _kwargs_from_golden(g)
+    n, T = g["actA"].shape
+    table = serve_table_from_random(g["seeds"], int(g["done"].sum(1).max()) + 1, **kw)
+    env = PongEnv2PBatch(n, seed=0, serve_table=table, autoreset=True, **kw)
+    oA, oB = env.reset()
+    assert np.array_equal(_state_matrix(env), g["init"])
+    assert np.array_equal(oA.cpu().numpy(), g["init_obs"][:, 0]) and np.array_equal(oB.cpu().numpy(), g["init_obs"][:, 1])
+    for t in range(T):
+        (oA, oB), (rA, rB), done, info = env.step(torch.from_numpy(g["actA"][:, t]), torch.from_numpy(g["actB"][:, t]))
+        d = done.cpu().numpy().astype(bool)
+        assert np.array_equal(d, g["done"][:, t].astype(bool)), t
+        assert np.array_equal(rA.cpu().numpy(), g["rew"][:, t, 0]) and np.array_equal(rB.cpu().numpy(), g["rew"][:, t, 1])
+        assert np.array_equal(info["term_obsA"].cpu().numpy(), g["obsA"][:, t])
+        assert np.array_equal(info["term_obsB"].cpu().numpy(), g["obsB"][:, t])
+        exp_state = np.where(d[:, None], g["reset_state"][:, t], g["state"][:, t])
+        assert np.array_equal(_state_matrix(env), exp_state), (name, t)
+        exp_oA = np.where(d[:, None], g["reset_obs"][:, t, 0], g["obsA"][:, t])
+        exp_oB = np.where(d[:, None], g["reset_obs"][:, t, 1], g["obsB"][:, t])
+        assert np.array_equal(oA.cpu().numpy(), exp_oA) and np.array_equal(oB.cpu().numpy(), exp_oB)
+
+
+@pytest.mark.parametrize("n", [1, 255, 65536])
+def test_env_step_matches_oracle_at_scale(orc, n):
+    """n arenas from random mid-game states (including y beyond the lines, paddles at the walls),
+    random actions, 40 ticks without reset: bit-exact with the C oracle."""
+    from pongmi.env import PongEnv2PBatch
+
+    kw = dict(paddle_speed=0.03, max_score=3, magnus_factor=0.025, restitution=1, friction=0.6,
+              ball_speed_range=[0.03, 0.05], spin_range=[-5, 5], speed_scale_every=1, speed_increment=0.1)
+    P = orc.make_params(orc.env_params_from_kwargs(**kw))
+    rng = np.random.RandomState(n)
+    st = dict(x=rng.uniform(-0.02, 1.02, n), y=rng.uniform(-0.05, 1.05, n), vx=rng.uniform(-0.08, 0.08, n),
+              vy=rng.uniform(-0.08, 0.08, n), spin=rng.uniform(-6, 6, n), top=rng.choice([0.0, 0.5, 1.0, 0.31], n),
+              bot=rng.uniform(0, 1, n), scoreA=rng.randint(0, 3, n), scoreB=rng.randint(0, 3, n),
+              bounces=rng.randint(0, 9, n), serves=np.zeros(n))
+    env = PongEnv2PBatch(n, **kw)
+    env.set_state(st)
+    arr = orc.arenas_from_soa(st)
+    for t in range(40):
+        aA = rng.randint(0, 3, n).astype(np.int8)
+        aB = rng.randint(0, 3, n).astype(np.int8)
+        (oA, oB), (rA, rB), done, _ = env.step(torch.from_numpy(aA), torch.from_numpy(aB))
+        eA, eB, rew, ed = orc.step_arenas(P, arr, aA, aB)
+        assert np.array_equal(done.cpu().numpy(), ed)
+        assert np.array_equal(rA.cpu().numpy(), rew[:, 0]) and np.array_equal(rB.cpu().numpy(), rew[:, 1])
+        assert np.array_equal(oA.cpu().numpy(), eA) and np.array_equal(oB.cpu().numpy(), eB)
+    got = env.get_state()
+    for k in STATE_ORDER:
+        assert np.array_equal(got[k], arr[k]), k
+
+
+def test_env_empty_and_bad_arguments():
+    from pongmi import _lib
+    from pongmi.env import PongEnv2PBatch, env_params
+
+    env = PongEnv2PBatch(0)
+    env.reset()
+    env.step(np.zeros(0, np.int8), np.zeros(0, np.int8))
+    with pytest.raises(ZeroDivisionError):
+        env_params(speed_scale_every=0)
+    with pytest.raises(TypeError):
+        env_params(bogus=1)
+    with pytest.raises(ValueError):
+        PongEnv2PBatch(4).step(np.zeros(3), np.zeros(4))
+    with pytest.raises(_lib.PongmiError):
+        _lib.check(_lib.load().pm_env_step(None, None, None, None, None, None, None, None, None, None, None, 0, None,
+                                           0, 0, None, 4, None))
+
+
+def test_production_serves_match_philox_restatement(orc):
+    """Philox serves: distribution of speed/angle/spin as reset() draws them, and each value equal
+    to the oracle's Philox restatement (cos/sin within 1 ulp of libm)."""
+    from pongmi.env import PongEnv2PBatch
+
+    n = 200000
+    kw = dict(ball_speed_range=[0.03, 0.05], spin_range=[-5, 5])
+    env = PongEnv2PBatch(n, seed=1234, **kw)
+    env.reset()
+    st = env.get_state()
+    p = orc.env_params_from_kwargs(**kw)
+    vx, vy, sp = orc.philox_serve(p, np.arange(n), np.zeros(n, np.int64), 1234)
+    np.testing.assert_allclose(st["vx"], vx, rtol=4e-16, atol=1e-18)
+    np.testing.assert_allclose(st["vy"], vy, rtol=4e-16, atol=1e-18)
+    assert np.array_equal(st["spin"], sp)
+    speed = np.hypot(st["vx"], st["vy"])
+    ang = np.degrees(np.arctan2(st["vy"], st["vx"]))
+    assert speed.min() >= 0.03 - 1e-12 and speed.max() <= 0.05 + 1e-12
+    assert np.all(((ang >= -60 - 1e-9) & (ang <= -30 + 1e-9)) | ((ang >= 30 - 1e-9) & (ang <= 60 + 1e-9)))
+    assert abs(np.mean(ang > 0) - 0.5) < 0.01 and abs(np.mean(sp)) < 0.05
+    assert np.all(st["serves"] == 1) and np.all(st["x"] == 0.5) and np.all(st["top"] == 0.5)
+
+
+def test_collide_kat_bit_exact(golden):
+    from pongmi import _lib
+
+    g = golden("collide_kat")
+    inp = g["inputs"]
+    inertia = np.array([(2 / 5) * r[6] * r[7] ** 2 for r in inp])  # CPython's I (physics.py:9)
+    d_in = torch.from_numpy(np.ascontiguousarray(inp)).cuda()
+    d_I = torch.from_numpy(inertia).cuda()
+    out = torch.empty((len(inp), 3), dtype=torch.float64, device="cuda")
+    _lib.check(_lib.load().pm_collide(d_in.data_ptr(), d_I.data_ptr(), out.data_ptr(), len(inp), _lib.stream_ptr()))
+    got = out.cpu().numpy()
+    assert np.array_equal(got, g["outputs"])
+    assert np.array_equal(np.signbit(got), np.signbit(g["outputs"]))

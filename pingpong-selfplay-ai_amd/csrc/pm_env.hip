@@ -128,8 +128,9 @@ bool state_ok(const pm_env_state* s) {
 extern "C" int pm_env_reset(const pm_env_params* p, const pm_env_state* s, const uint8_t* mask, const double* inject,
                             int32_t inject_cap, uint64_t seed, float* obsA, float* obsB, int32_t* status, int32_t n,
                             void* stream) {
-    PM_REQUIRE(p && state_ok(s), PM_E_ARG, "pm_env_reset: null params/state");
     PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_env_reset: n=%d", n);
+    if (n == 0) return PM_OK;
+    PM_REQUIRE(p && state_ok(s), PM_E_ARG, "pm_env_reset: null params/state");
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_reset: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_reset: speed_scale_every must be > 0");
     if (n == 0) return PM_OK;
@@ -143,9 +144,10 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
                            float* obsA, float* obsB, float* rA, float* rB, uint8_t* done, float* term_obsA,
                            float* term_obsB, int32_t autoreset, const double* inject, int32_t inject_cap,
                            uint64_t seed, int32_t* status, int32_t n, void* stream) {
+    PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_env_step: n=%d", n);
+    if (n == 0) return PM_OK;
     PM_REQUIRE(p && state_ok(s), PM_E_ARG, "pm_env_step: null params/state");
     PM_REQUIRE(aA && aB && obsA && obsB && rA && rB && done, PM_E_ARG, "pm_env_step: null buffer");
-    PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_env_step: n=%d", n);
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
     if (n == 0) return PM_OK;
@@ -156,9 +158,9 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
 }
 
 extern "C" int pm_collide(const double* in, const double* inertia, double* out, int32_t n, void* stream) {
-    PM_REQUIRE(in && inertia && out, PM_E_ARG, "pm_collide: null buffer");
     PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_collide: n=%d", n);
     if (n == 0) return PM_OK;
+    PM_REQUIRE(in && inertia && out, PM_E_ARG, "pm_collide: null buffer");
     hipLaunchKernelGGL(k_collide, dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0, pm_stream(stream), in, inertia, out, n);
     PM_LAUNCHED("k_collide");
     return PM_OK;

@@ -82,9 +82,9 @@ extern "C" int pm_qnet_fold(const float* params, float* params_out, int32_t mode
 }
 
 extern "C" int pm_qnet_q(const float* w_eff, const float* x, float* q, int32_t n, void* stream) {
-    PM_REQUIRE(w_eff && x && q, PM_E_ARG, "pm_qnet_q: null buffer");
     PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_qnet_q: n=%d", n);
     if (n == 0) return PM_OK;
+    PM_REQUIRE(w_eff && x && q, PM_E_ARG, "pm_qnet_q: null buffer");
     hipLaunchKernelGGL(k_qnet_q, dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0, pm_stream(stream), w_eff, x, q, n);
     PM_LAUNCHED("k_qnet_q");
     return PM_OK;
@@ -94,9 +94,9 @@ extern "C" int pm_qnet_act(const float* w_opp, const int32_t* opp_id, int32_t n_
                            const float* obsA, const float* obsB, float epsilon, const double* eps_dev, uint64_t seed,
                            uint64_t counter, const uint64_t* counter_dev, int8_t* aA, int8_t* aB, float* qA, float* qB,
                            int32_t n, void* stream) {
-    PM_REQUIRE(w_opp && w_B && obsA && obsB && aA && aB, PM_E_ARG, "pm_qnet_act: null buffer");
     PM_REQUIRE(n >= 0 && n_opp >= 1, PM_E_SIZE, "pm_qnet_act: n=%d n_opp=%d", n, n_opp);
     if (n == 0) return PM_OK;
+    PM_REQUIRE(w_opp && w_B && obsA && obsB && aA && aB, PM_E_ARG, "pm_qnet_act: null buffer");
     hipLaunchKernelGGL(k_act, dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0, pm_stream(stream), w_opp, opp_id, w_B, obsA,
                        obsB, epsilon, eps_dev, seed, counter, counter_dev, aA, aB, qA, qB, n_opp, n);
     PM_LAUNCHED("k_act");

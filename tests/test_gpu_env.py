@@ -100,6 +100,9 @@ def test_env_empty_and_bad_arguments():
     with pytest.raises(_lib.PongmiError):
         _lib.check(_lib.load().pm_env_step(None, None, None, None, None, None, None, None, None, None, None, 0, None,
                                            0, 0, None, 4, None))
+    with pytest.raises(_lib.PongmiError):
+        _lib.check(_lib.load().pm_env_step(None, None, None, None, None, None, None, None, None, None, None, 0, None,
+                                           0, 0, None, -1, None))
 
 
 def test_production_serves_match_philox_restatement(orc):

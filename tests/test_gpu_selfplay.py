@@ -177,8 +177,8 @@ def test_learn_and_apply_match_oracle(orc, golden):
         pr = L.prios.cpu().numpy()
         exp_pr = pre["prios"].copy()
         orc.per_update(exp_pr, idx, res["errors"])
-        np.testing.assert_allclose(pr, exp_pr, rtol=2e-5, atol=1e-6)
-        assert np.isclose(L.counters()["max_prio"], max(c["max_prio"], exp_pr[idx].max()), rtol=2e-5)
+        np.testing.assert_allclose(pr, exp_pr, rtol=2e-5, atol=3e-5)  # |q-t| carries fp32 error
+        assert np.isclose(L.counters()["max_prio"], max(c["max_prio"], exp_pr[idx].max()), rtol=2e-5, atol=3e-5)
         L.apply()
         updates += 1
         p_ref, m_ref, v_ref = orc.adam_step(heads, grad[:520].astype(np.float64), m_ref, v_ref, updates, 2.5e-4)

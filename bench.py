@@ -34,6 +34,9 @@ ENV_KW = dict(paddle_width=0.2, paddle_speed=0.03, max_score=3, enable_spin=True
               speed_increment=0.1)  # config.yaml env (render keys dropped)
 FLOP_PER_ARENA = 2 * 2 * (7 * 64 + 64 * 64 + 64 * 4)  # two QNet forwards (MACs x 2)
 ENV_BYTES = 203  # K1 algorithmic bytes per env-step
+# k_env (self-play tick): state 7x8 + 3x4 read and written (136), actions 2, opp 4 + ep_reward 4 read and
+# written (16), replay row 64 + priority 4 written, next observations 2x28 written
+SP_ENV_BYTES = 136 + 2 + 16 + 68 + 56
 PEAK_FP32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
@@ -57,6 +60,7 @@ def time_env_step(n, reps=200):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     total = 0.0
     for _ in range(reps):
+        torch.cuda._sleep(200_000)  # keep the queue busy so the events bracket the kernel, not the host launch
         e0.record()
         env.step(aA, aB)
         e1.record()
@@ -123,9 +127,12 @@ def main():
     def one_step(ev=None):
         if ev is not None:
             ev[0].record()
-        L.rollout()
+        L.act()
         if ev is not None:
             ev[1].record()
+        L.env_step()
+        if ev is not None:
+            ev[2].record()
         L.learn()
         if dist is not None:
             dist.all_reduce(L.grad)
@@ -134,7 +141,7 @@ def main():
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -149,13 +156,15 @@ def main():
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    rollout_s = sum(a.elapsed_time(b) for a, b in evs) * 1e-3 / args.steps
+    act_s = sum(e[0].elapsed_time(e[1]) for e in evs) * 1e-3 / args.steps
+    env_s = sum(e[1].elapsed_time(e[2]) for e in evs) * 1e-3 / args.steps
     c = L.counters()
 
     if rank == 0:
         total = args.arenas * world * args.steps
         value = total / dt
-        achieved = args.arenas * FLOP_PER_ARENA / rollout_s / 1e12
+        achieved = args.arenas * FLOP_PER_ARENA / act_s / 1e12
+        env_gbs = args.arenas * SP_ENV_BYTES / env_s / 1e9
         out = {
             "metric": "env-steps/sec (whole node) at 65536 arenas, 1/2/4/8 GPUs; CPU-ref baseline",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -167,11 +176,14 @@ def main():
                        "arenas_per_gpu": args.arenas, "global_arenas": args.arenas * world,
                        "pool": args.pool, "batch": args.batch, "updates_per_vector_step": 1,
                        "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)"},
-            "roofline": {"bound": "mfma", "kernel": "k_rollout", "compute": "fp32 VALU v_fmac_f32 (FP32 peak = "
-                                                                           "matrix peak = 157.3 TF)",
+            "roofline": {"bound": "mfma", "kernel": "k_act_sp", "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; "
+                                                                          "dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                         "avg_us": round(rollout_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
+                         "avg_us": round(act_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
+            "env_roofline": {"bound": "hbm", "kernel": "k_env", "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS,
+                             "unit": "GB/s", "frac": round(env_gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                             "avg_us": round(env_s * 1e6, 2), "bytes_per_env_step": SP_ENV_BYTES},
             "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
                         "last_loss": c["last_loss"]},
         }

@@ -96,13 +96,15 @@ int pm_collide(const double* in, const double* inertia, double* out, int32_t n, 
  *   fc_A.{weight_mu [3,64], bias_mu [3], weight_sigma [3,64], bias_sigma [3]}      (the 520 "heads",
  *        in the order train_iterative.py:101-104 hands them to Adam)
  *   fc_V.{weight_epsilon [1,64], bias_epsilon [1]} | fc_A.{weight_epsilon [3,64], bias_epsilon [3]}
- * Effective (folded) weights, PM_QNET_NW floats: W1 [64,7] | b1 [64] | W2 [64,64] | b2 [64] |
- *   Wh [4,64] (row 0 = V, rows 1..3 = A) | bh [4]. */
+ * Effective (folded) weights, PM_QNET_NW floats: the plain part W1 [64,7] | b1 [64] | W2 [64,64] |
+ *   b2 [64] | Wh [4,64] (row 0 = V, rows 1..3 = A) | bh [4] (4932 floats, padded to 4936), then the
+ *   same weights re-ordered into MFMA operand fragments (5008 floats) for the matrix-core forward.
+ *   Produce it with pm_qnet_fold; treat the fragment part as opaque. */
 #define PM_QNET_NP 5452
 #define PM_QNET_NHEAD 520
 #define PM_QNET_HEAD_OFF 4672
 #define PM_QNET_EPS_OFF 5192
-#define PM_QNET_NW 4932
+#define PM_QNET_NW 9944
 
 #define PM_FOLD_EVAL 0        /* NoisyLinear eval mode: W = mu                          (qnet.py:47-49) */
 #define PM_FOLD_TRAIN 1       /* train mode with the block's epsilon buffers: mu+sigma*eps (qnet.py:44-46) */
@@ -118,16 +120,18 @@ int pm_qnet_fold(const float* params, float* params_out, int32_t mode, uint64_t 
 /* QNet.forward (models/qnet.py:71-75) on effective weights: x [n][7] -> q [n][3]. */
 int pm_qnet_q(const float* w_eff, const float* x, float* q, int32_t n, void* stream);
 
-/* Both players' action selection for n arenas (fused):
- *   A: argmax_a Q_opp(obsA) with opponent weights w_opp[opp_id[i]] (opp_id NULL = 0)
+/* Both players' action selection for n arenas (fused, matrix cores):
+ *   A: argmax_a Q_opp(obsA) with opponent weights w_opp[opp_id[i]] (opp_id NULL = net 0)
  *      (scripts/train_iterative.py:240; tests/arena.py:294-320)
  *   B: random.random() < epsilon ? randint(0,2) : argmax_a Q_B(obsB)          (train_iterative.py:124-130)
  * argmax keeps the first maximal index (torch). epsilon is *eps_dev when eps_dev != NULL.
- * qA/qB [n][3] nullable. Philox counter for the epsilon draws: (i, counter + *counter_dev). */
+ * qA/qB [n][3] nullable. Philox counter for the epsilon draws: (i, counter + *counter_dev).
+ * Rows are grouped by opponent net: net 0 is gathered per chunk0 arenas, nets >= 1 per chunk1
+ * arenas (0 = defaults 256 / 4096; at most 4096); choose each so a chunk holds >= ~64 of its rows. */
 int pm_qnet_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B, const float* obsA,
                 const float* obsB, float epsilon, const double* eps_dev, uint64_t seed, uint64_t counter,
                 const uint64_t* counter_dev, int8_t* aA, int8_t* aB, float* qA, float* qB, int32_t n,
-                void* stream);
+                int32_t chunk0, int32_t chunk1, void* stream);
 
 /* ---------------------------------------------------------------- replay + PER (K4) */
 
@@ -185,9 +189,12 @@ typedef struct pm_selfplay {
     float *isw;              /* [batch] IS weights                                                */
     float *grad;             /* [PM_QNET_NHEAD + 8] grads + packed counters (all-reduced when sharded) */
     int64_t *partials;       /* [ceil(n/256)][8] per-block episode counters of the rollout          */
+    float *obsA, *obsB;      /* [n][7] observations of the current step (written by the env kernel) */
+    int8_t *aA, *aB;         /* [n] actions of the current step (written by the act kernel)        */
     float *hfeat;            /* [2*batch][64] learner scratch: features of s and s'                 */
     pm_ctrl *ctrl;
     int32_t n, n_pool, batch, world;
+    int32_t chunk_A, chunk_P;  /* act grouping: arenas per compaction chunk for modelA / pool nets */
     int64_t cap;
     double gamma, alpha, lr, beta1, beta2, adam_eps;  /* train_iterative.py:33-37, torch.optim.Adam defaults */
     double min_epsilon, epsilon_decay, pool_ratio, beta_start;
@@ -201,8 +208,8 @@ typedef struct pm_selfplay {
 #define PM_MAX_BATCH 256
 
 /* One vector step of scripts/train_iterative.py:239-245 for all n arenas, as device work only:
- *   rollout: act (both players, :240-241) + env step (:242) + replay push (:243) + episode
- *            bookkeeping (:245-249, next opponent :235-236, env.reset :238);
+ *   rollout: act (both players, :240-241; matrix-core kernel) then env step (:242) + replay push
+ *            (:243) + episode bookkeeping (:245-249, next opponent :235-236, env.reset :238);
  *   learn:   once the replay holds >= batch transitions: PER sample + double-DQN loss/grads +
  *            priority update (train_step, :132-164), leaving grads and the finished-episode count
  *            in sp->grad;
@@ -213,7 +220,9 @@ typedef struct pm_selfplay {
  * pm_selfplay_step = rollout + learn + apply (unsharded). pm_selfplay_init serves every arena,
  * draws first opponents and folds the acting weights of step ctrl->step. */
 int pm_selfplay_init(const pm_selfplay* sp, void* stream);
-int pm_selfplay_rollout(const pm_selfplay* sp, void* stream);
+int pm_selfplay_rollout(const pm_selfplay* sp, void* stream); /* = pm_selfplay_act + pm_selfplay_env */
+int pm_selfplay_act(const pm_selfplay* sp, void* stream);     /* both players' actions -> sp->aA/aB   */
+int pm_selfplay_env(const pm_selfplay* sp, void* stream);     /* tick + push + bookkeeping + serves   */
 int pm_selfplay_learn(const pm_selfplay* sp, void* stream);
 int pm_selfplay_apply(const pm_selfplay* sp, void* stream);
 int pm_selfplay_step(const pm_selfplay* sp, void* stream);

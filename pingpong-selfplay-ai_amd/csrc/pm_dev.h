@@ -5,9 +5,8 @@
 //   Arena/tick()    one PongEnv2P.step on a register-resident arena (envs/my_pong_env_2p.py:116-232,
 //                   envs/physics.py:3-23), IEEE binary64 in the reference's evaluation order.
 //                   The library is compiled with -ffp-contract=off: no FMA is ever formed here.
-//   qnet_q()        QNet.forward (models/qnet.py:71-75) for one row per lane on effective weights
-//                   whose base pointer is wave-uniform, so every weight is a scalar (SMEM) load
-//                   broadcast to the 64 lanes and every MAC is one v_fmac_f32 with an SGPR operand.
+//   fold_heads()    NoisyLinear folding / reset_noise (models/qnet.py:33-50) of the two dueling heads.
+//   (the MFMA QNet forward lives in pm_mfma.h)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -89,6 +88,28 @@ __device__ __forceinline__ void observe(const Arena& a, float* oA, float* oB) {
     oA[4] = (float)a.top; oA[5] = (float)a.bot; oA[6] = (float)a.spin;
     oB[0] = (float)a.x; oB[1] = (float)a.y; oB[2] = (float)a.vx; oB[3] = (float)a.vy;
     oB[4] = (float)a.bot; oB[5] = (float)a.top; oB[6] = (float)a.spin;
+}
+
+// Stage [blockDim][7] floats per block in LDS and write them back as contiguous float4s (a row-per-lane
+// store of 28-byte rows would be seven 4-byte stores per lane). Block-wide, includes two barriers.
+__device__ __forceinline__ void store_rows7(float* __restrict__ dst, float (*lds)[7], const float* row, int i0,
+                                            int n) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) lds[t][k] = row[k];
+    __syncthreads();
+    const int rows = min((int)blockDim.x, n - i0);
+    const int nf = rows * 7;
+    float* base = dst + (size_t)i0 * 7;
+    const float* src = &lds[0][0];
+    if (rows == (int)blockDim.x && (((uintptr_t)base) & 15) == 0) {
+        float4* d4 = reinterpret_cast<float4*>(base);
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        for (int f = t; f < nf / 4; f += blockDim.x) d4[f] = s4[f];
+    } else {
+        for (int f = t; f < nf; f += blockDim.x) base[f] = src[f];
+    }
+    __syncthreads();
 }
 
 // reset() (:83-114) with a given serve (vx, vy, spin)
@@ -188,7 +209,7 @@ __device__ __forceinline__ int tick(const pm_env_params& p, Arena& a, int aA, in
 
 // ----------------------------------------------------------------------------- QNet
 enum : int { W1 = 0, B1 = 448, W2 = 512, B2 = 4608, WH = 4672, BH = 4928 };  // effective-weight offsets
-static_assert(BH + 4 == PM_QNET_NW, "effective weight layout");
+static_assert(BH + 4 == 4932, "plain effective weight layout");
 
 // Parameter-block offsets (pongmi.h PM_QNET_NP layout): heads at PM_QNET_HEAD_OFF, eps at PM_QNET_EPS_OFF
 enum : int {
@@ -199,57 +220,12 @@ enum : int {
 static_assert(P_ABSG + 3 == PM_QNET_EPS_OFF, "head layout");
 static_assert(P_ABEP + 3 == PM_QNET_NP, "eps layout");
 
-// QNet.forward on one row per lane. `w` MUST be wave-uniform (same pointer in every lane).
-__device__ __forceinline__ void qnet_q(const float* __restrict__ w, const float* x, float* q) {
-    float h1[64];
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        float a = w[B1 + j];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) a = fmaf(w[W1 + j * 7 + k], x[k], a);
-        h1[j] = fmaxf(a, 0.f);
-    }
-    float v = w[BH + 0], a0 = w[BH + 1], a1 = w[BH + 2], a2 = w[BH + 3];
-#pragma unroll 2
-    for (int j = 0; j < 64; ++j) {
-        float a = w[B2 + j];
-#pragma unroll
-        for (int k = 0; k < 64; ++k) a = fmaf(w[W2 + j * 64 + k], h1[k], a);
-        a = fmaxf(a, 0.f);
-        v = fmaf(w[WH + j], a, v);
-        a0 = fmaf(w[WH + 64 + j], a, a0);
-        a1 = fmaf(w[WH + 128 + j], a, a1);
-        a2 = fmaf(w[WH + 192 + j], a, a2);
-    }
-    const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
-    q[0] = v + (a0 - mean);
-    q[1] = v + (a1 - mean);
-    q[2] = v + (a2 - mean);
-}
-
 // torch argmax: first maximal index
 __device__ __forceinline__ int argmax3(const float* q) {
     int b = 0;
     if (q[1] > q[b]) b = 1;
     if (q[2] > q[b]) b = 2;
     return b;
-}
-
-// Q for a per-lane opponent index: waterfall over the distinct ids present in the wave so that
-// each pass runs qnet_q with a wave-uniform weight pointer.
-__device__ __forceinline__ void qnet_q_grouped(const float* __restrict__ wtab, int id, const float* x, float* q,
-                                               bool active = true) {
-    bool pending = active;
-    while (true) {
-        const unsigned long long m = __ballot(pending);
-        if (m == 0ull) break;
-        const int lead = __ffsll((long long)m) - 1;
-        const int cur = __builtin_amdgcn_readfirstlane(__shfl(id, lead));
-        if (pending && id == cur) {
-            qnet_q(wtab + (size_t)cur * PM_QNET_NW, x, q);
-            pending = false;
-        }
-    }
 }
 
 // ----------------------------------------------------------------------------- NoisyNet fold

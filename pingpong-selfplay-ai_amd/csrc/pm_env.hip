@@ -12,27 +12,6 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// Stage [kBlock][7] floats per block in LDS and write them back as contiguous float4s.
-__device__ __forceinline__ void store_rows7(float* __restrict__ dst, float (*lds)[7], const float* row, int i0,
-                                            int n) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) lds[t][k] = row[k];
-    __syncthreads();
-    const int rows = min(kBlock, n - i0);
-    const int nf = rows * 7;
-    float* base = dst + (size_t)i0 * 7;
-    const float* src = &lds[0][0];
-    if (rows == kBlock && (((uintptr_t)base) & 15) == 0) {
-        float4* d4 = reinterpret_cast<float4*>(base);
-        const float4* s4 = reinterpret_cast<const float4*>(src);
-        for (int f = t; f < nf / 4; f += kBlock) d4[f] = s4[f];
-    } else {
-        for (int f = t; f < nf; f += kBlock) base[f] = src[f];
-    }
-    __syncthreads();
-}
-
 __device__ __forceinline__ void do_serve(const pm_env_params& p, const pm_env_state& s, Arena& a, int i,
                                          const double* __restrict__ inject, int inject_cap, uint64_t seed,
                                          int32_t* status) {

@@ -1,0 +1,260 @@
+// K2 on the matrix cores: QNet.forward (models/qnet.py:71-75) for 32 rows at a time with the exact
+// f32 MFMA v_mfma_f32_32x32x2_f32 (D = A*B + C, bit-for-bit a k-ordered fmaf chain).
+//
+// Orientation: every layer computes H^T = W * X^T, weights as the A operand (rows = output units),
+// activations as the B operand (columns = the 32 arenas of the tile). The accumulator of a 32x32
+// tile holds column `lane & 31` and rows (r&3) + 8(r>>2) + 4(lane>>5) in register r, which is
+// exactly the B-operand fragment the next layer needs for a k-step covering those two rows — so
+// layer 1 -> ReLU -> layer 2 runs on registers with no LDS round trip or lane shuffle. Per tile:
+// 8 MFMAs (7->64, K padded to 8) + 64 MFMAs (64->64); the 4 head outputs (V, A0..2) are 128 VALU
+// FMAs per lane + one cross-half add, overlapped with the next tile's MFMAs.
+//
+// Weights are stored pre-arranged in "fragment order" (PM_QNET_NW block, after the plain part) so a
+// wave reads each operand with one conflict-free ds_read_b128 per 4 MFMAs after a block stages the
+// 20 KB fragment image into LDS.
+#pragma once
+#include "pm_dev.h"
+
+namespace pm {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int PLAIN = 4936;  // plain effective weights (4932) padded to 16 B
+// fragment image (floats, from w + PLAIN)
+enum : int {
+    F_W1 = 0,      // [jt 2][lane 64][s 4]            W1[32jt + (l&31)][2s + (l>>5)] (k = 7 -> 0)
+    F_W2 = 512,    // [jt 2][t 2][rq 4][lane 64][e 4] W2[32jt + (l&31)][32t + rho(4rq+e) + 4(l>>5)]
+    F_B1 = 4608,   // [jt 2][h 2][r 16]               b1[32jt + rho(r) + 4h]
+    F_B2 = 4672,   // [jt 2][h 2][r 16]               b2[32jt + rho(r) + 4h]
+    F_H = 4736,    // [h 2][t 2][r 16][c 4]           Wh[c][32t + rho(r) + 4h]
+    F_BH = 4992,   // [c 4] + 12 pad                  bh[c]
+    F_SIZE = 5008,
+};
+static_assert(PLAIN + F_SIZE == PM_QNET_NW, "effective weight block size");
+
+__device__ __forceinline__ int rho(int r) { return (r & 3) + 8 * (r >> 2); }
+
+// ----------------------------------------------------------------------------- fragment writers
+// Feature fragments (W1, W2, b1, b2) + the plain feature copy, from a parameter block. Block-wide.
+__device__ __forceinline__ void write_feature_frags(const float* __restrict__ p, float* __restrict__ w) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int k = t; k < PM_QNET_HEAD_OFF; k += nt) w[k] = p[k];
+    float* f = w + PLAIN;
+    for (int k = t; k < 512; k += nt) {  // W1
+        const int jt = k >> 8, lane = (k >> 2) & 63, s = k & 3;
+        const int row = 32 * jt + (lane & 31), kk = 2 * s + (lane >> 5);
+        f[F_W1 + k] = kk < 7 ? p[W1 + row * 7 + kk] : 0.f;
+    }
+    for (int k = t; k < 4096; k += nt) {  // W2
+        const int e = k & 3, lane = (k >> 2) & 63, rq = (k >> 8) & 3, tt = (k >> 10) & 1, jt = k >> 11;
+        const int row = 32 * jt + (lane & 31), col = 32 * tt + rho(4 * rq + e) + 4 * (lane >> 5);
+        f[F_W2 + k] = p[W2 + row * 64 + col];
+    }
+    for (int k = t; k < 64; k += nt) {  // b1, b2
+        const int r = k & 15, h = (k >> 4) & 1, jt = k >> 5;
+        f[F_B1 + k] = p[B1 + 32 * jt + rho(r) + 4 * h];
+        f[F_B2 + k] = p[B2 + 32 * jt + rho(r) + 4 * h];
+    }
+}
+
+// Head fragments + plain head slice from 260 folded head values (Wh [4][64] | bh [4]). Block-wide.
+__device__ __forceinline__ void write_head_frags(const float* heads, float* __restrict__ w) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int k = t; k < 260; k += nt) w[WH + k] = heads[k];
+    float* f = w + PLAIN;
+    for (int k = t; k < 256; k += nt) {
+        const int c = k & 3, r = (k >> 2) & 15, tt = (k >> 6) & 1, h = k >> 7;
+        f[F_H + k] = heads[c * 64 + 32 * tt + rho(r) + 4 * h];
+    }
+    if (t < 16) f[F_BH + t] = t < 4 ? heads[256 + t] : 0.f;
+}
+
+// ----------------------------------------------------------------------------- block helpers
+// Stage one net's fragment image (F_SIZE floats) into LDS. Block-wide; caller syncs.
+__device__ __forceinline__ void stage_frags(const float* __restrict__ w, float* lw) {
+    const float4* src = reinterpret_cast<const float4*>(w + PLAIN);
+    float4* dst = reinterpret_cast<float4*>(lw);
+    for (int k = threadIdx.x; k < F_SIZE / 4; k += blockDim.x) dst[k] = src[k];
+}
+
+// Append the arenas i in [lo, hi) with id[i] == net to the LDS list (order unspecified: every row
+// is computed independently, so the tile composition never changes a result). Block-wide.
+__device__ __forceinline__ void compact_rows(const int32_t* __restrict__ id, int net, int lo, int hi, int* list,
+                                             int* count) {
+    const int lane = threadIdx.x & 63;
+    for (int base = lo; base < hi; base += blockDim.x) {
+        const int i = base + (int)threadIdx.x;
+        const bool m = i < hi && id[i] == net;
+        const unsigned long long b = __ballot(m);
+        int pos = 0;
+        if (lane == 0 && b) pos = atomicAdd(count, __popcll(b));
+        pos = __shfl(pos, 0);
+        if (m) list[pos + __popcll(b & ((1ull << lane) - 1ull))] = i;
+    }
+}
+
+struct TileOut {
+    int8_t* act;     // [n] action (argmax, or eps-greedy when eps >= 0)
+    float* q;        // [n][3] Q values (nullable)
+    double eps;      // < 0: greedy
+    uint64_t seed, ctr;
+};
+
+// QNet forward + action for `count` arenas listed in LDS `list` (arena indices), weights staged in
+// LDS `lw`. Each wave takes tiles wave, wave + nwaves, ... Wave-uniform control flow throughout.
+__device__ __forceinline__ void run_tiles(const float* lw, const float* __restrict__ obs, const int* list, int count,
+                                          const TileOut& out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int ntiles = (count + 31) >> 5;
+    for (int tl = wave; tl < ntiles; tl += nw) {
+        const int row = tl * 32 + col;
+        const bool valid = row < count;
+        const int arena = list[valid ? row : tl * 32];
+        const float* o = obs + (size_t)arena * 7;
+        float xs[4];
+        xs[0] = o[h];
+        xs[1] = o[2 + h];
+        xs[2] = o[4 + h];
+        xs[3] = h ? 0.f : o[6];
+        // ---- layer 1: 7 -> 64 (bias as the initial accumulator)
+        f32x16 c1[2];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            const float4* b = reinterpret_cast<const float4*>(lw + F_B1 + (jt * 2 + h) * 16);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const float4 v = b[q4];
+                c1[jt][4 * q4 + 0] = v.x; c1[jt][4 * q4 + 1] = v.y; c1[jt][4 * q4 + 2] = v.z; c1[jt][4 * q4 + 3] = v.w;
+            }
+            const float4 w = reinterpret_cast<const float4*>(lw + F_W1)[jt * 64 + lane];
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, xs[0], c1[jt], 0, 0, 0);
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, xs[1], c1[jt], 0, 0, 0);
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, xs[2], c1[jt], 0, 0, 0);
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, xs[3], c1[jt], 0, 0, 0);
+        }
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c1[jt][r] = fmaxf(c1[jt][r], 0.f);
+        // ---- layer 2: 64 -> 64, the layer-1 accumulators are the B operands. Operand fragments are
+        // read one group (4 MFMAs = 256 cycles) ahead; sched_barrier keeps the scheduler from
+        // hoisting all 16 reads (64 registers) to the top.
+        const float4* w2 = reinterpret_cast<const float4*>(lw + F_W2) + lane;
+        f32x16 c2[2];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            const float4* b = reinterpret_cast<const float4*>(lw + F_B2 + (jt * 2 + h) * 16);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const float4 v = b[q4];
+                c2[jt][4 * q4 + 0] = v.x; c2[jt][4 * q4 + 1] = v.y; c2[jt][4 * q4 + 2] = v.z; c2[jt][4 * q4 + 3] = v.w;
+            }
+        }
+        float4 wcur = w2[0];
+#pragma unroll
+        for (int g8 = 0; g8 < 16; ++g8) {  // g8 = (jt * 2 + t) * 4 + rq
+            const int jt = g8 >> 3, t = (g8 >> 2) & 1, rq = g8 & 3;
+            const float4 wnext = w2[((g8 + 1) & 15) * 64];
+            c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.x, c1[t][4 * rq + 0], c2[jt], 0, 0, 0);
+            c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.y, c1[t][4 * rq + 1], c2[jt], 0, 0, 0);
+            c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.z, c1[t][4 * rq + 2], c2[jt], 0, 0, 0);
+            c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.w, c1[t][4 * rq + 3], c2[jt], 0, 0, 0);
+            wcur = wnext;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- heads (VALU): this lane holds 32 of the 64 hidden rows of its column
+        float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+        const float4* hw = reinterpret_cast<const float4*>(lw + F_H + h * 128);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float x = fmaxf(c2[t][r], 0.f);
+                const float4 w = hw[t * 16 + r];
+                v = fmaf(w.x, x, v);
+                a0 = fmaf(w.y, x, a0);
+                a1 = fmaf(w.z, x, a1);
+                a2 = fmaf(w.w, x, a2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        v += __shfl_xor(v, 32);
+        a0 += __shfl_xor(a0, 32);
+        a1 += __shfl_xor(a1, 32);
+        a2 += __shfl_xor(a2, 32);
+        v += lw[F_BH + 0];
+        a0 += lw[F_BH + 1];
+        a1 += lw[F_BH + 2];
+        a2 += lw[F_BH + 3];
+        const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
+        float q[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
+        int a = argmax3(q);
+        if (out.eps >= 0.0) {  // random.random() < eps ? randint(0,2) : argmax (train_iterative.py:126-130)
+            const U4 rr = philox64((uint32_t)arena, TAG_ACT, out.ctr, out.seed);
+            if (u53(rr.x, rr.y) < out.eps) a = below(rr.z, 3u);
+        }
+        if (h == 0 && valid) {
+            if (out.act) out.act[arena] = (int8_t)a;
+            if (out.q) {
+                out.q[(size_t)arena * 3 + 0] = q[0];
+                out.q[(size_t)arena * 3 + 1] = q[1];
+                out.q[(size_t)arena * 3 + 2] = q[2];
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- grouped act grid
+// Block -> work: [0, nB) chunks of 256 arenas for side B (one net: w_B); then side A: net 0 in
+// chunks of chunk0 arenas, nets 1..n_opp-1 in chunks of chunk1 arenas each, rows compacted by
+// opponent id so every tile has uniform weights.
+struct ActGrid {
+    int n, n_opp, chunk0, chunk1, side_b;
+    __host__ __device__ int nb() const { return side_b ? (n + 255) / 256 : 0; }
+    __host__ __device__ int na0() const { return (n + chunk0 - 1) / chunk0; }
+    __host__ __device__ int na1() const { return (n + chunk1 - 1) / chunk1; }
+    __host__ __device__ int blocks() const { return nb() + na0() + (n_opp - 1) * na1(); }
+};
+
+constexpr int kActBlock = 256;
+constexpr int kListMax = 4096;  // max chunk size
+
+struct ActShared {
+    float lw[F_SIZE];
+    int list[kListMax];
+    int count;
+};
+
+// Block-wide body of the grouped act kernel. side B: eps-greedy on obsB with w_B;
+// side A: greedy on obsA with w_opp[net]. opp == nullptr -> every arena plays net 0.
+__device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const float* __restrict__ w_opp,
+                                          const int32_t* __restrict__ opp, const float* __restrict__ w_B,
+                                          const float* __restrict__ obsA, const float* __restrict__ obsB,
+                                          TileOut outA, TileOut outB) {
+    int b = blockIdx.x;
+    const float* w;
+    const float* obs;
+    TileOut out;
+    int net, lo, hi;
+    bool compact;
+    if (b < g.nb()) {
+        w = w_B; obs = obsB; out = outB; net = -1; lo = b * 256; hi = min(lo + 256, g.n); compact = false;
+    } else {
+        b -= g.nb();
+        if (b < g.na0()) { net = 0; lo = b * g.chunk0; hi = min(lo + g.chunk0, g.n); }
+        else { b -= g.na0(); net = 1 + b / g.na1(); lo = (b % g.na1()) * g.chunk1; hi = min(lo + g.chunk1, g.n); }
+        w = w_opp + (size_t)net * PM_QNET_NW; obs = obsA; out = outA;
+        compact = opp != nullptr;
+        if (!compact && net != 0) return;  // block-uniform
+    }
+    stage_frags(w, sh.lw);
+    if (threadIdx.x == 0) sh.count = compact ? 0 : hi - lo;
+    __syncthreads();
+    if (compact) compact_rows(opp, net, lo, hi, sh.list, &sh.count);
+    else for (int k = threadIdx.x; k < hi - lo; k += blockDim.x) sh.list[k] = lo + k;
+    __syncthreads();
+    run_tiles(sh.lw, obs, sh.list, sh.count, out);
+}
+
+}  // namespace pm

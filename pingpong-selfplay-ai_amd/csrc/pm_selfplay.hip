@@ -1,6 +1,7 @@
 // The batched self-play learner: one vector step of scripts/train_iterative.py:239-245 for n arenas.
 //
-//   k_rollout   (n lanes)      act both players + env tick + replay push + episode bookkeeping
+//   k_act_sp    (MFMA tiles)   both players' QNet forward + eps-greedy / argmax (pm_mfma.h)
+//   k_env       (n lanes)      env tick + replay push + episode bookkeeping + serves
 //   k_per_reduce (<=4096 WGs)  per-1024 block sums of prio^alpha              [pm_replay.hip]
 //   k_sp_sample (batch waves)  proportional sample + un-normalised IS weights
 //   k_dqn_feat  (2*batch rows) frozen features h2 = relu(W2 relu(W1 x + b1) + b2) of s and s'
@@ -11,8 +12,8 @@
 //
 // Nothing returns to the host: every loop counter lives in the device control block (pm_ctrl), so
 // a whole vector step can be replayed from a captured graph.
-#include "pm_dev.h"
 #include "pm_host.h"
+#include "pm_mfma.h"
 #include "pm_per.h"
 
 using namespace pm;
@@ -28,37 +29,41 @@ __device__ __forceinline__ bool learner_active(const pm_selfplay& sp) {
 }
 
 // ------------------------------------------------------------------------------------ rollout
-__global__ __launch_bounds__(kBlock) void k_rollout(const pm_selfplay sp) {
+// Both players act (train_iterative.py:240-241) on the matrix cores: ActGrid blocks, modelB tiles
+// with epsilon-greedy, opponent tiles grouped by net (modelA / pool) so weights are tile-uniform.
+__global__ __launch_bounds__(kActBlock, 2) void k_act_sp(const pm_selfplay sp) {
+    __shared__ __attribute__((aligned(16))) ActShared sh;
+    const ActGrid g{sp.n, sp.n_pool + 1, sp.chunk_A, sp.chunk_P, 1};
+    const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
+    const TileOut outB{sp.aB, nullptr, sp.ctrl->epsilon, sp.seed_env, sp.ctrl->step};
+    act_block(sh, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, sp.w_B, sp.obsA, sp.obsB, outA, outB);
+}
+
+// env.step (:242) + memory.push (:243) + episode bookkeeping (:245-249) + next opponent (:235-236)
+// and env.reset (:238) for finished arenas; writes next step's observations. HBM-bound.
+__global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
+    __shared__ float lds[kBlock][7];
     __shared__ long long red[kBlock / 64][6];
-    const int i = blockIdx.x * kBlock + threadIdx.x;
+    const int i0 = blockIdx.x * kBlock;
+    const int i = i0 + threadIdx.x;
     const bool valid = i < sp.n;
     const int ii = valid ? i : sp.n - 1;
     const pm_ctrl* c = sp.ctrl;
-    const uint64_t step = c->step;
     const int64_t pos = c->pos, size = c->size;
-    const double eps = c->epsilon;
     const float maxp = size == 0 ? 1.0f : c->max_prio;  // max(prios) if buffer else 1.0 (:57)
 
     Arena a = load_arena(sp.st, ii);
+    const int aA = sp.aA[ii], aB = sp.aB[ii];
+    const int o = sp.opp[ii];
     float oA[7], oB[7];
-    observe(a, oA, oB);
-    const int o = min(max(sp.opp[ii], 0), sp.n_pool);
-    float qa[3], qb[3];
-    qnet_q_grouped(sp.w_opp, o, oA, qa, valid);  // opponent: modelA or a pool net (:235-236,240)
-    qnet_q(sp.w_B, oB, qb);                      // modelB with this step's noise (:124-130)
-    const int aA = argmax3(qa);
-    const U4 r = philox64((uint32_t)ii, TAG_ACT, step, sp.seed_env);
-    const int aB = u53(r.x, r.y) < eps ? below(r.z, 3u) : argmax3(qb);
-
+    observe(a, oA, oB);  // the state the actions were chosen on (= obs of the previous env kernel)
     float rA, rB;
     const int d = tick(sp.env, a, aA, aB, rA, rB);
     float nA[7], nB[7];
     observe(a, nA, nB);
     const float er = sp.ep_reward[ii] + rB;  // ep_reward += rB (:245)
     const bool fin = valid && d;
-
-    // ---- episode bookkeeping: per-block partials, no atomics (:247-249)
-    {
+    {   // per-block partials, no atomics (:247-249)
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         const bool win = er > 0.f;
         const unsigned long long mf = __ballot(fin), mA = __ballot(fin && o == 0), mwA = __ballot(fin && o == 0 && win);
@@ -70,55 +75,64 @@ __global__ __launch_bounds__(kBlock) void k_rollout(const pm_selfplay sp) {
             red[wv][0] = __popcll(mf); red[wv][1] = __popcll(mA); red[wv][2] = __popcll(mwA);
             red[wv][3] = __popcll(mP); red[wv][4] = __popcll(mwP); red[wv][5] = rs;
         }
-        __syncthreads();
-        if (threadIdx.x < 6) {
-            long long t = 0;
-            for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
-            sp.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = t;
+    }
+    if (valid) {
+        // memory.push((oB, aB, rB, nB, done)) (:243, :56-63)
+        const int64_t slot = (pos + i) % sp.cap;
+        float4* row = reinterpret_cast<float4*>(sp.trans + slot * PM_TRANS_F);
+        row[0] = make_float4(oB[0], oB[1], oB[2], oB[3]);
+        row[1] = make_float4(oB[4], oB[5], oB[6], rB);
+        row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
+        row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
+        sp.prios[slot] = maxp;
+        int onew = o;
+        float ernew = er;
+        if (d) {  // next episode: opponent draw then env.reset()
+            const uint32_t ns = (uint32_t)sp.st.serves[i];
+            const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
+            onew = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
+            double vx, vy, spn;
+            philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
+            serve(a, vx, vy, spn);
+            sp.st.serves[i] = (int32_t)ns + 1;
+            ernew = 0.f;
+            observe(a, nA, nB);
         }
+        store_arena(sp.st, i, a);
+        sp.opp[i] = onew;
+        sp.ep_reward[i] = ernew;
     }
-    if (!valid) return;
-
-    // ---- memory.push((oB, aB, rB, nB, done)) (:243, :56-63)
-    const int64_t slot = (pos + i) % sp.cap;
-    float4* row = reinterpret_cast<float4*>(sp.trans + slot * PM_TRANS_F);
-    row[0] = make_float4(oB[0], oB[1], oB[2], oB[3]);
-    row[1] = make_float4(oB[4], oB[5], oB[6], rB);
-    row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
-    row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
-    sp.prios[slot] = maxp;
-
-    int onew = o;
-    float ernew = er;
-    if (d) {  // next episode: opponent draw (:235-236) then env.reset() (:238)
-        const uint32_t ns = (uint32_t)sp.st.serves[i];
-        const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
-        onew = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
-        double vx, vy, spn;
-        philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
-        serve(a, vx, vy, spn);
-        sp.st.serves[i] = (int32_t)ns + 1;
-        ernew = 0.f;
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        long long t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
+        sp.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = t;
     }
-    store_arena(sp.st, i, a);
-    sp.opp[i] = onew;
-    sp.ep_reward[i] = ernew;
+    store_rows7(sp.obsA, lds, nA, i0, sp.n);
+    store_rows7(sp.obsB, lds, nB, i0, sp.n);
 }
 
 // ------------------------------------------------------------------------------------ init
 __global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= sp.n) return;
-    const uint32_t ns = (uint32_t)sp.st.serves[i];
-    const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
-    sp.opp[i] = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
-    Arena a;
-    double vx, vy, spn;
-    philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
-    serve(a, vx, vy, spn);
-    store_arena(sp.st, i, a);
-    sp.st.serves[i] = (int32_t)ns + 1;
-    sp.ep_reward[i] = 0.f;
+    __shared__ float lds[kBlock][7];
+    const int i0 = blockIdx.x * kBlock;
+    const int i = i0 + threadIdx.x;
+    float oA[7] = {0}, oB[7] = {0};
+    if (i < sp.n) {
+        const uint32_t ns = (uint32_t)sp.st.serves[i];
+        const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
+        sp.opp[i] = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
+        Arena a;
+        double vx, vy, spn;
+        philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
+        serve(a, vx, vy, spn);
+        store_arena(sp.st, i, a);
+        sp.st.serves[i] = (int32_t)ns + 1;
+        sp.ep_reward[i] = 0.f;
+        observe(a, oA, oB);
+    }
+    store_rows7(sp.obsA, lds, oA, i0, sp.n);
+    store_rows7(sp.obsB, lds, oB, i0, sp.n);
 }
 
 // ------------------------------------------------------------------------------------ learner
@@ -315,7 +329,7 @@ __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
 
 // ------------------------------------------------------------------------------------ Adam + commit
 __global__ __launch_bounds__(1024) void k_adam(const pm_selfplay sp) {
-    __shared__ float noise[132];
+    __shared__ float noise[132], heads[260];
     const int t = threadIdx.x;
     pm_ctrl* c = sp.ctrl;
     const bool train = sp.grad[kGradN + 1] > 0.5f;
@@ -339,9 +353,9 @@ __global__ __launch_bounds__(1024) void k_adam(const pm_selfplay sp) {
         for (int k = t; k < PM_QNET_NP; k += 1024) sp.paramsT[k] = sp.paramsB[k];
     }
     // next vector step's acting noise for modelB (select_action_B -> reset_noise, :125)
-    fold_heads(sp.paramsB, sp.paramsB, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_ACT, c->step + 1, sp.w_B + WH,
-               noise);
+    fold_heads(sp.paramsB, sp.paramsB, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_ACT, c->step + 1, heads, noise);
     __syncthreads();
+    write_head_frags(heads, sp.w_B);
     if (t == 0) {
         const double D = (double)sp.grad[kGradN];  // finished episodes (all shards)
         const double e = c->epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
@@ -362,6 +376,10 @@ int check(const pm_selfplay* sp) {
     PM_REQUIRE(sp->n > 0 && sp->batch >= 1 && sp->batch <= PM_MAX_BATCH && sp->n > sp->batch && sp->cap >= sp->n,
                PM_E_SIZE, "pm_selfplay: n=%d batch=%d cap=%lld", sp->n, sp->batch, (long long)sp->cap);
     PM_REQUIRE(sp->n_pool >= 0 && sp->n_pool <= 4096 && sp->world >= 1, PM_E_SIZE, "pm_selfplay: n_pool/world");
+    PM_REQUIRE(sp->obsA && sp->obsB && sp->aA && sp->aB, PM_E_ARG, "pm_selfplay: null obs/action buffer");
+    PM_REQUIRE(sp->chunk_A > 0 && sp->chunk_A <= kListMax && sp->chunk_P > 0 && sp->chunk_P <= kListMax, PM_E_SIZE,
+               "pm_selfplay: chunk_A/chunk_P must be in [1, %d]", kListMax);
+    PM_REQUIRE(((((uintptr_t)sp->w_opp) | ((uintptr_t)sp->w_B)) & 15) == 0, PM_E_ARG, "pm_selfplay: weights alignment");
     PM_REQUIRE(sp->env.speed_scale_every > 0 && sp->target_update_interval > 0 && sp->beta_frames > 0, PM_E_ARG,
                "pm_selfplay: zero interval");
     return PM_OK;
@@ -380,12 +398,26 @@ extern "C" int pm_selfplay_init(const pm_selfplay* sp, void* stream) {
                         stream);
 }
 
-extern "C" int pm_selfplay_rollout(const pm_selfplay* sp, void* stream) {
+extern "C" int pm_selfplay_act(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_rollout, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *sp);
-    PM_LAUNCHED("k_rollout");
+    const ActGrid g{sp->n, sp->n_pool + 1, sp->chunk_A, sp->chunk_P, 1};
+    hipLaunchKernelGGL(k_act_sp, dim3(g.blocks()), dim3(kActBlock), 0, pm_stream(stream), *sp);
+    PM_LAUNCHED("k_act_sp");
     return PM_OK;
+}
+
+extern "C" int pm_selfplay_env(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_env, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *sp);
+    PM_LAUNCHED("k_env");
+    return PM_OK;
+}
+
+extern "C" int pm_selfplay_rollout(const pm_selfplay* sp, void* stream) {
+    int rc = pm_selfplay_act(sp, stream);
+    return rc ? rc : pm_selfplay_env(sp, stream);
 }
 
 extern "C" int pm_selfplay_learn(const pm_selfplay* sp, void* stream) {

@@ -23,7 +23,8 @@ PM_QNET_NP = 5452
 PM_QNET_NHEAD = 520
 PM_QNET_HEAD_OFF = 4672
 PM_QNET_EPS_OFF = 5192
-PM_QNET_NW = 4932
+PM_QNET_NW = 9944
+PM_QNET_PLAIN = 4936
 PM_TRANS_F = 16
 PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
@@ -53,8 +54,10 @@ class Ctrl(ctypes.Structure):
 class SelfPlay(ctypes.Structure):
     _fields_ = [("env", EnvParams), ("st", EnvState)] + \
         [(n, c_void_p) for n in ("opp", "ep_reward", "w_opp", "paramsB", "paramsT", "w_B", "adam_m", "adam_v",
-                                 "trans", "prios", "per_work", "idx", "isw", "grad", "partials", "hfeat", "ctrl")] + \
-        [("n", c_i32), ("n_pool", c_i32), ("batch", c_i32), ("world", c_i32), ("cap", c_i64)] + \
+                                 "trans", "prios", "per_work", "idx", "isw", "grad", "partials", "obsA", "obsB", "aA",
+                                 "aB", "hfeat", "ctrl")] + \
+        [("n", c_i32), ("n_pool", c_i32), ("batch", c_i32), ("world", c_i32), ("chunk_A", c_i32), ("chunk_P", c_i32),
+         ("cap", c_i64)] + \
         [(n, c_double) for n in ("gamma", "alpha", "lr", "beta1", "beta2", "adam_eps", "min_epsilon", "epsilon_decay",
                                  "pool_ratio", "beta_start")] + \
         [("beta_frames", c_i64), ("target_update_interval", c_i64), ("seed_env", c_u64), ("seed_net", c_u64)]
@@ -72,13 +75,15 @@ _SIGS = {
     "pm_qnet_fold": (c_i32, [c_void_p, c_void_p, c_i32, c_u64, c_u64, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_qnet_q": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_qnet_act": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64,
-                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p]),
     "pm_per_work_bytes": (c_i64, [c_i64]),
     "pm_per_sample": (c_i32, [c_void_p, c_i64, c_float, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_i32,
                               c_void_p, c_void_p]),
     "pm_per_update": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_selfplay_init": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_rollout": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_act": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_env": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_learn": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_apply": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_step": (c_i32, [c_void_p, c_void_p]),

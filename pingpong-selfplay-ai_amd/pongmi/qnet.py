@@ -81,7 +81,7 @@ def q_values(w_eff, x, stream=None):
 
 
 def act(w_opp, opp_id, w_B, obsA, obsB, epsilon=0.0, seed=0, counter=0, eps_dev=None, counter_dev=None,
-        want_q=False, stream=None):
+        want_q=False, chunk0=0, chunk1=0, stream=None):
     """Both players' actions (fused K2): aA = argmax Q_opp(obsA), aB = eps-greedy argmax Q_B(obsB)."""
     lib = _lib.load()
     n = obsA.shape[0]
@@ -95,5 +95,6 @@ def act(w_opp, opp_id, w_B, obsA, obsB, epsilon=0.0, seed=0, counter=0, eps_dev=
         opp_id = opp_id.to(device=dev, dtype=torch.int32).contiguous()
     check(lib.pm_qnet_act(ptr(w_opp), ptr(opp_id), w_opp.shape[0], ptr(w_B.contiguous()), ptr(obsA.contiguous()),
                           ptr(obsB.contiguous()), float(epsilon), ptr(eps_dev), int(seed), int(counter),
-                          ptr(counter_dev), ptr(aA), ptr(aB), ptr(qA), ptr(qB), n, stream_ptr(stream)), "pm_qnet_act")
+                          ptr(counter_dev), ptr(aA), ptr(aB), ptr(qA), ptr(qB), n, int(chunk0), int(chunk1),
+                          stream_ptr(stream)), "pm_qnet_act")
     return (aA, aB, qA, qB) if want_q else (aA, aB)

@@ -33,6 +33,17 @@ def splitmix64(x):
     return x ^ (x >> 31)
 
 
+def act_chunk(p, rows=96, cap=4096):
+    """Arenas per compaction chunk of an opponent played with probability p: the smallest power of
+    two expected to hold >= `rows` of its arenas (so its 32-row MFMA tiles are mostly full)."""
+    if p <= 0:
+        return cap
+    c = 64
+    while c < cap and c * p < rows:
+        c *= 2
+    return c
+
+
 class SelfPlayLearner:
     def __init__(self, env_kw, n_arenas, modelB_state, modelA_state=None, pool_states=(), *, batch=256,
                  memory_size=1_000_000, gamma=0.99, lr=2.5e-4, epsilon=0.02, min_epsilon=0.02, epsilon_decay=0.995,
@@ -78,6 +89,10 @@ class SelfPlayLearner:
         self.grad = torch.zeros(PM_QNET_NHEAD + 8, **f32)
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
         self.hfeat = torch.zeros((2 * self.batch, 64), **f32)
+        self.obsA = torch.zeros((n, 7), **f32)
+        self.obsB = torch.zeros((n, 7), **f32)
+        self.aA = torch.zeros(n, dtype=torch.int8, device=dev)
+        self.aB = torch.zeros(n, dtype=torch.int8, device=dev)
         # ---- control block
         c = _lib.Ctrl()
         c.epsilon = float(epsilon)
@@ -90,9 +105,12 @@ class SelfPlayLearner:
         sp.env = env_params(**env_kw)
         sp.st = _lib.EnvState(*[ptr(self.f64[k]) for k in range(7)], *[ptr(self.i32[k]) for k in range(4)])
         for name in ("opp", "ep_reward", "w_opp", "paramsB", "paramsT", "w_B", "adam_m", "adam_v", "trans", "prios",
-                     "per_work", "idx", "isw", "grad", "partials", "hfeat", "ctrl"):
+                     "per_work", "idx", "isw", "grad", "partials", "obsA", "obsB", "aA", "aB", "hfeat", "ctrl"):
             setattr(sp, name, ptr(getattr(self, name)))
         sp.n, sp.n_pool, sp.batch, sp.world, sp.cap = n, self.n_pool, self.batch, self.world, self.cap
+        p_pool = pool_ratio if self.n_pool else 0.0
+        sp.chunk_A = act_chunk(1.0 - p_pool)
+        sp.chunk_P = act_chunk(p_pool / self.n_pool) if self.n_pool else 256
         sp.gamma, sp.alpha, sp.lr = gamma, alpha, lr
         sp.beta1, sp.beta2, sp.adam_eps = 0.9, 0.999, 1e-8
         sp.min_epsilon, sp.epsilon_decay, sp.pool_ratio, sp.beta_start = min_epsilon, epsilon_decay, pool_ratio, beta_start
@@ -108,6 +126,12 @@ class SelfPlayLearner:
     # ------------------------------------------------------------------ stepping
     def rollout(self):
         check(self.lib.pm_selfplay_rollout(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_rollout")
+
+    def act(self):
+        check(self.lib.pm_selfplay_act(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_act")
+
+    def env_step(self):
+        check(self.lib.pm_selfplay_env(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_env")
 
     def learn(self):
         check(self.lib.pm_selfplay_learn(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_learn")

@@ -100,6 +100,110 @@ struct TileOut {
     uint64_t seed, ctr;
 };
 
+// Plain folded heads (Wh [4][64] | bh [4]) -> the F_H/F_BH fragment order (260 floats). Block-wide.
+__device__ __forceinline__ void heads_to_frags(const float* heads, float* hf) {
+    for (int k = threadIdx.x; k < 260; k += blockDim.x) {
+        if (k < 256) {
+            const int c = k & 3, r = (k >> 2) & 15, tt = (k >> 6) & 1, h = k >> 7;
+            hf[k] = heads[c * 64 + 32 * tt + rho(r) + 4 * h];
+        } else {
+            hf[k] = heads[k];
+        }
+    }
+}
+
+// Layer 1 (7 -> 64) + ReLU + layer 2 (64 -> 64, pre-ReLU) for one 32-row tile on the matrix cores.
+// xs: this lane's layer-1 B operands obs[row][2s + (lane>>5)] (index 7 = 0). lw: staged fragments.
+__device__ __forceinline__ void tile_hidden(const float* lw, const float (&xs)[4], int lane, f32x16 (&c2)[2]) {
+    const int h = lane >> 5;
+    f32x16 c1[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {  // bias as the initial accumulator
+        const float4* b = reinterpret_cast<const float4*>(lw + F_B1 + (jt * 2 + h) * 16);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 v = b[q4];
+            c1[jt][4 * q4 + 0] = v.x; c1[jt][4 * q4 + 1] = v.y; c1[jt][4 * q4 + 2] = v.z; c1[jt][4 * q4 + 3] = v.w;
+        }
+        const float4 w = reinterpret_cast<const float4*>(lw + F_W1)[jt * 64 + lane];
+        c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, xs[0], c1[jt], 0, 0, 0);
+        c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, xs[1], c1[jt], 0, 0, 0);
+        c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, xs[2], c1[jt], 0, 0, 0);
+        c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, xs[3], c1[jt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) c1[jt][r] = fmaxf(c1[jt][r], 0.f);
+    // layer 2: the layer-1 accumulators are the B operands. Operand fragments are read one group
+    // (4 MFMAs = 256 cycles) ahead; sched_barrier keeps the scheduler from hoisting all 16 reads
+    // (64 registers) to the top.
+    const float4* w2 = reinterpret_cast<const float4*>(lw + F_W2) + lane;
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+        const float4* b = reinterpret_cast<const float4*>(lw + F_B2 + (jt * 2 + h) * 16);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 v = b[q4];
+            c2[jt][4 * q4 + 0] = v.x; c2[jt][4 * q4 + 1] = v.y; c2[jt][4 * q4 + 2] = v.z; c2[jt][4 * q4 + 3] = v.w;
+        }
+    }
+    float4 wcur = w2[0];
+#pragma unroll
+    for (int g8 = 0; g8 < 16; ++g8) {  // g8 = (jt * 2 + t) * 4 + rq
+        const int jt = g8 >> 3, t = (g8 >> 2) & 1, rq = g8 & 3;
+        const float4 wnext = w2[((g8 + 1) & 15) * 64];
+        c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.x, c1[t][4 * rq + 0], c2[jt], 0, 0, 0);
+        c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.y, c1[t][4 * rq + 1], c2[jt], 0, 0, 0);
+        c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.z, c1[t][4 * rq + 2], c2[jt], 0, 0, 0);
+        c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.w, c1[t][4 * rq + 3], c2[jt], 0, 0, 0);
+        wcur = wnext;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Dueling heads (VALU) on ReLU(c2): this lane holds 32 of the 64 hidden rows of its column; the two
+// lane halves are summed with one cross-half add. hf: F_H/F_BH-ordered heads (260 floats).
+// Q = V + (A - mean(A)) in every lane.
+__device__ __forceinline__ void tile_heads(const float* hf, const f32x16 (&c2)[2], int lane, float (&q)[3]) {
+    const int h = lane >> 5;
+    float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    const float4* hw = reinterpret_cast<const float4*>(hf + h * 128);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float x = fmaxf(c2[t][r], 0.f);
+            const float4 w = hw[t * 16 + r];
+            v = fmaf(w.x, x, v);
+            a0 = fmaf(w.y, x, a0);
+            a1 = fmaf(w.z, x, a1);
+            a2 = fmaf(w.w, x, a2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    v += __shfl_xor(v, 32);
+    a0 += __shfl_xor(a0, 32);
+    a1 += __shfl_xor(a1, 32);
+    a2 += __shfl_xor(a2, 32);
+    v += hf[256];
+    a0 += hf[257];
+    a1 += hf[258];
+    a2 += hf[259];
+    const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
+    q[0] = v + (a0 - mean);
+    q[1] = v + (a1 - mean);
+    q[2] = v + (a2 - mean);
+}
+
+// layer-1 B operands of this lane for observation row o (obs[2s + h], index 7 -> 0)
+__device__ __forceinline__ void tile_inputs(const float* __restrict__ o, int h, float (&xs)[4]) {
+    xs[0] = o[h];
+    xs[1] = o[2 + h];
+    xs[2] = o[4 + h];
+    xs[3] = h ? 0.f : o[6];
+}
+
 // QNet forward + action for `count` arenas listed in LDS `list` (arena indices), weights staged in
 // LDS `lw`. Each wave takes tiles wave, wave + nwaves, ... Wave-uniform control flow throughout.
 __device__ __forceinline__ void run_tiles(const float* lw, const float* __restrict__ obs, const int* list, int count,
@@ -111,84 +215,12 @@ __device__ __forceinline__ void run_tiles(const float* lw, const float* __restri
         const int row = tl * 32 + col;
         const bool valid = row < count;
         const int arena = list[valid ? row : tl * 32];
-        const float* o = obs + (size_t)arena * 7;
         float xs[4];
-        xs[0] = o[h];
-        xs[1] = o[2 + h];
-        xs[2] = o[4 + h];
-        xs[3] = h ? 0.f : o[6];
-        // ---- layer 1: 7 -> 64 (bias as the initial accumulator)
-        f32x16 c1[2];
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt) {
-            const float4* b = reinterpret_cast<const float4*>(lw + F_B1 + (jt * 2 + h) * 16);
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const float4 v = b[q4];
-                c1[jt][4 * q4 + 0] = v.x; c1[jt][4 * q4 + 1] = v.y; c1[jt][4 * q4 + 2] = v.z; c1[jt][4 * q4 + 3] = v.w;
-            }
-            const float4 w = reinterpret_cast<const float4*>(lw + F_W1)[jt * 64 + lane];
-            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, xs[0], c1[jt], 0, 0, 0);
-            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, xs[1], c1[jt], 0, 0, 0);
-            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, xs[2], c1[jt], 0, 0, 0);
-            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, xs[3], c1[jt], 0, 0, 0);
-        }
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) c1[jt][r] = fmaxf(c1[jt][r], 0.f);
-        // ---- layer 2: 64 -> 64, the layer-1 accumulators are the B operands. Operand fragments are
-        // read one group (4 MFMAs = 256 cycles) ahead; sched_barrier keeps the scheduler from
-        // hoisting all 16 reads (64 registers) to the top.
-        const float4* w2 = reinterpret_cast<const float4*>(lw + F_W2) + lane;
+        tile_inputs(obs + (size_t)arena * 7, h, xs);
         f32x16 c2[2];
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt) {
-            const float4* b = reinterpret_cast<const float4*>(lw + F_B2 + (jt * 2 + h) * 16);
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const float4 v = b[q4];
-                c2[jt][4 * q4 + 0] = v.x; c2[jt][4 * q4 + 1] = v.y; c2[jt][4 * q4 + 2] = v.z; c2[jt][4 * q4 + 3] = v.w;
-            }
-        }
-        float4 wcur = w2[0];
-#pragma unroll
-        for (int g8 = 0; g8 < 16; ++g8) {  // g8 = (jt * 2 + t) * 4 + rq
-            const int jt = g8 >> 3, t = (g8 >> 2) & 1, rq = g8 & 3;
-            const float4 wnext = w2[((g8 + 1) & 15) * 64];
-            c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.x, c1[t][4 * rq + 0], c2[jt], 0, 0, 0);
-            c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.y, c1[t][4 * rq + 1], c2[jt], 0, 0, 0);
-            c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.z, c1[t][4 * rq + 2], c2[jt], 0, 0, 0);
-            c2[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.w, c1[t][4 * rq + 3], c2[jt], 0, 0, 0);
-            wcur = wnext;
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // ---- heads (VALU): this lane holds 32 of the 64 hidden rows of its column
-        float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
-        const float4* hw = reinterpret_cast<const float4*>(lw + F_H + h * 128);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float x = fmaxf(c2[t][r], 0.f);
-                const float4 w = hw[t * 16 + r];
-                v = fmaf(w.x, x, v);
-                a0 = fmaf(w.y, x, a0);
-                a1 = fmaf(w.z, x, a1);
-                a2 = fmaf(w.w, x, a2);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        v += __shfl_xor(v, 32);
-        a0 += __shfl_xor(a0, 32);
-        a1 += __shfl_xor(a1, 32);
-        a2 += __shfl_xor(a2, 32);
-        v += lw[F_BH + 0];
-        a0 += lw[F_BH + 1];
-        a1 += lw[F_BH + 2];
-        a2 += lw[F_BH + 3];
-        const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
-        float q[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
+        tile_hidden(lw, xs, lane, c2);
+        float q[3];
+        tile_heads(lw + F_H, c2, lane, q);
         int a = argmax3(q);
         if (out.eps >= 0.0) {  // random.random() < eps ? randint(0,2) : argmax (train_iterative.py:126-130)
             const U4 rr = philox64((uint32_t)arena, TAG_ACT, out.ctr, out.seed);

@@ -60,31 +60,39 @@ struct PowPrios {
     }
 };
 
-// First k in [0, m) with (sum_{j<=k} v(j)) > t, scanning in chunks of 1024 (16 per lane).
-// Returns -1 if none; `before` gets the running sum in front of k. Wave-uniform result.
+// First k in [0, m) with (sum_{j<=k} v(j)) > t, scanning in chunks of 1024 (16 per lane). Each
+// chunk's 16 values per lane are loaded together into registers before any compare, so a search
+// costs one memory round trip per chunk. Returns -1 if none; `before` gets the running sum in
+// front of k. Wave-uniform result.
 template <class V>
 __device__ inline int64_t wave_search(const V& v, int64_t m, double t, double& before, int lane) {
     double run = 0.0;
     for (int64_t c0 = 0; c0 < m; c0 += 1024) {
-        double part = 0.0;
         const int64_t b = c0 + (int64_t)lane * 16;
+        double vals[16];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) part += v(b + e);
+        for (int e = 0; e < 16; ++e) vals[e] = v(b + e);
+        double part = 0.0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) part += vals[e];
         const double incl = wave_incl_scan(part, lane);
         const double tot = __shfl(incl, 63);
-        if (run + tot > t) {
+        if (run + tot > t) {  // wave-uniform
             const unsigned long long hit = __ballot(run + incl > t);
             const int L = __ffsll((long long)hit) - 1;
-            double base = run + __shfl(incl - part, L);
-            const int64_t bL = c0 + (int64_t)L * 16;
+            // every lane resolves its own 16 values; lane L's answer is the one broadcast
+            double base = run + (incl - part), bef = base, lastbef = base;
+            int found = -1, lastnz = -1;
+#pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const double x = v(bL + e);
-                if (base + x > t) { before = base; return bL + e; }
-                base += x;
+                if (found < 0 && base + vals[e] > t) { found = e; bef = base; }
+                if (vals[e] > 0.0) { lastnz = e; lastbef = base; }
+                base += vals[e];
             }
-            // rounding: the lane's sequential sum fell short of its scanned prefix — take its last nonzero
-            for (int e = 15; e >= 0; --e)
-                if (v(bL + e) > 0.0) { before = base - v(bL + e); return bL + e; }
+            if (found < 0) { found = lastnz; bef = lastbef; }  // rounding: lane sum fell short of its scan
+            found = __shfl(found, L);
+            before = __shfl(bef, L);
+            if (found >= 0) return c0 + (int64_t)L * 16 + found;
         }
         run += tot;
     }

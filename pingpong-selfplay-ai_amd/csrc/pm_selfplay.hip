@@ -2,10 +2,10 @@
 //
 //   k_act_sp    (MFMA tiles)   both players' QNet forward + eps-greedy / argmax (pm_mfma.h)
 //   k_env       (n lanes)      env tick + replay push + episode bookkeeping + serves
-//   k_per_reduce (<=4096 WGs)  per-1024 block sums of prio^alpha              [pm_replay.hip]
+//   k_per_refresh              per-1024 block sums of prio^alpha for the blocks that changed
 //   k_sp_sample (batch waves)  proportional sample + un-normalised IS weights
-//   k_dqn_feat  (2*batch rows) frozen features h2 = relu(W2 relu(W1 x + b1) + b2) of s and s'
-//   k_dqn       (1 WG)         double-DQN heads, IS-weighted MSE, head grads, priority update
+//   k_dqn_fwd   (MFMA tiles)   Q_B(s), Q_B(s'), Q_T(s') and features of s for the sampled batch
+//   k_dqn       (1 WG)         double-DQN targets, IS-weighted MSE, head grads, priority update
 //   ----------------------------- (sharded: RCCL all-reduce of sp.grad here)
 //   k_adam      (1 WG)         Adam on the 520 head params, target sync, epsilon decay,
 //                              replay/step counters, next step's acting noise
@@ -154,63 +154,95 @@ __global__ __launch_bounds__(256) void k_sp_sample(const pm_selfplay sp, const d
     if ((threadIdx.x & 63) == 0) { sp.idx[j] = idx; sp.isw[j] = wr; }
 }
 
-// features of the 2*batch rows (s then s'): 64 rows per block, wave w owns outputs [16w, 16w+16)
-__global__ __launch_bounds__(256) void k_dqn_feat(const pm_selfplay sp) {
-    __shared__ float h1s[64][65];
+// Priority block sums, incremental: only the 1024-entry blocks this step's push wrote ([pos, pos+n)
+// mod cap) and the blocks the previous update's priority scatter touched (sp.idx still holds its
+// indices) changed since they were last summed. Each is recomputed from scratch in the same fixed
+// order as a full pass (k_per_reduce), so the sums are identical to a full recompute.
+__global__ __launch_bounds__(256) void k_per_refresh(const pm_selfplay sp, double* __restrict__ bsum) {
+    __shared__ double part[4];
     if (!learner_active(sp)) return;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int row = blockIdx.x * 64 + lane;
-    const int nrows = 2 * sp.batch;
-    const int rr = row < nrows ? row : nrows - 1;
-    const int j = rr < sp.batch ? rr : rr - sp.batch;
-    const float* tr = sp.trans + sp.idx[j] * PM_TRANS_F + (rr < sp.batch ? 0 : 8);
-    float x[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) x[k] = tr[k];
-    const float* __restrict__ w = sp.paramsB;  // modelB.features (frozen, == targetB.features)
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {
-        const int o = wv * 16 + jj;
-        float a = w[B1 + o];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) a = fmaf(w[W1 + o * 7 + k], x[k], a);
-        h1s[lane][o] = fmaxf(a, 0.f);
+    const int64_t nbc = (sp.cap + PER_CHUNK - 1) / PER_CHUNK;
+    const int64_t npush = (int64_t)(sp.n + PER_CHUNK - 1) / PER_CHUNK + 2;
+    int64_t blk;
+    if ((int64_t)blockIdx.x < npush) {
+        const int64_t pos = sp.ctrl->pos;  // not yet committed: the push of this step started here
+        const int64_t first = pos / PER_CHUNK, last = (pos + sp.n - 1) / PER_CHUNK;
+        if (first + (int64_t)blockIdx.x > last) return;
+        blk = (first + blockIdx.x) % nbc;
+    } else {
+        blk = sp.idx[blockIdx.x - npush] / PER_CHUNK;
     }
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const float alpha = (float)sp.alpha;
+    double acc = 0.0;
+    const int64_t base = blk * PER_CHUNK;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t e = base + t + k * 256;
+        if (e < sp.cap) acc += (double)powf(sp.prios[e], alpha);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) part[wv] = acc;
     __syncthreads();
-    float h1[64];
-#pragma unroll
-    for (int k = 0; k < 64; ++k) h1[k] = h1s[lane][k];
-    float* out = sp.hfeat + (size_t)rr * 64;
-#pragma unroll 4
-    for (int jj = 0; jj < 16; ++jj) {
-        const int o = wv * 16 + jj;
-        float a = w[B2 + o];
-#pragma unroll
-        for (int k = 0; k < 64; ++k) a = fmaf(w[W2 + o * 64 + k], h1[k], a);
-        if (row < nrows) out[o] = fmaxf(a, 0.f);
-    }
+    if (t == 0) bsum[blk] = ((part[0] + part[1]) + part[2]) + part[3];
 }
 
-// heads on one feature row: V, A0..2 -> dueling Q (models/qnet.py:71-75)
-__device__ __forceinline__ void heads_q(const float* hw, const float* h, float* q) {
-    float v = hw[256], a0 = hw[257], a1 = hw[258], a2 = hw[259];
+// The three QNet evaluations of train_step (:152-155) for the sampled batch on the matrix cores:
+// rows [0, B) are s, rows [B, 2B) are s'. modelB runs with fresh noise (reset_noise, :142),
+// targetB in eval mode (mu, :100). Writes h2 = ReLU(features(s)) for the gradient and, per sample j,
+// q[j*16 + 0..2] = Q_B(s), [4..6] = Q_B(s'), [8..10] = Q_T(s').
+__global__ __launch_bounds__(64) void k_dqn_fwd(const pm_selfplay sp) {
+    __shared__ __attribute__((aligned(16))) float lw[F_SIZE];
+    __shared__ __attribute__((aligned(16))) float hfB[260];
+    __shared__ __attribute__((aligned(16))) float hfT[260];
+    __shared__ float heads[260], noise[132];
+    if (!learner_active(sp)) return;
+    const int lane = threadIdx.x, h = lane >> 5, col = lane & 31;
+    const int B = sp.batch;
+    stage_frags(sp.w_B, lw);  // modelB.features fragments (frozen; == targetB.features)
+    const uint64_t ctr = (uint64_t)(sp.ctrl->train_steps + 1);
+    fold_heads(sp.paramsB, blockIdx.x == 0 ? sp.paramsB : nullptr, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_TRAIN,
+               ctr, heads, noise);  // block 0 leaves the update's noise in modelB's epsilon buffers
+    __syncthreads();
+    heads_to_frags(heads, hfB);
+    __syncthreads();
+    fold_heads(sp.paramsT, nullptr, PM_FOLD_EVAL, 0, 0, 0, heads, nullptr);
+    __syncthreads();
+    heads_to_frags(heads, hfT);
+    __syncthreads();
+    const int g = blockIdx.x * 32 + col;
+    const bool valid = g < 2 * B;
+    const int gg = valid ? g : 2 * B - 1;
+    const bool nxt = gg >= B;
+    const int j = nxt ? gg - B : gg;
+    float xs[4];
+    tile_inputs(sp.trans + sp.idx[j] * PM_TRANS_F + (nxt ? 8 : 0), h, xs);
+    f32x16 c2[2];
+    tile_hidden(lw, xs, lane, c2);
+    float qb[3], qt[3];
+    tile_heads(hfB, c2, lane, qb);
+    tile_heads(hfT, c2, lane, qt);
+    float* hs = sp.hfeat + (size_t)j * 64;
+    float* q = sp.hfeat + (size_t)B * 64 + (size_t)j * 16;
+    if (valid && !nxt) {
 #pragma unroll
-    for (int k = 0; k < 64; ++k) {
-        v = fmaf(hw[k], h[k], v);
-        a0 = fmaf(hw[64 + k], h[k], a0);
-        a1 = fmaf(hw[128 + k], h[k], a1);
-        a2 = fmaf(hw[192 + k], h[k], a2);
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hs[32 * t + rho(r) + 4 * h] = fmaxf(c2[t][r], 0.f);
     }
-    const float mean = ((a0 + a1) + a2) / 3.0f;
-    q[0] = v + (a0 - mean);
-    q[1] = v + (a1 - mean);
-    q[2] = v + (a2 - mean);
+    if (valid && h == 0) {
+        if (!nxt) {
+            q[0] = qb[0]; q[1] = qb[1]; q[2] = qb[2];
+        } else {
+            q[4] = qb[0]; q[5] = qb[1]; q[6] = qb[2];
+            q[8] = qt[0]; q[9] = qt[1]; q[10] = qt[2];
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
     __shared__ float Hs[PM_MAX_BATCH][65];
     __shared__ float coef[PM_MAX_BATCH][4];
-    __shared__ float hwB[260], hwT[260], noise[132];
     __shared__ int64_t sidx[PM_MAX_BATCH];
     __shared__ float red[4][2];
     __shared__ long long cnt[6];
@@ -239,18 +271,19 @@ __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
         for (int k = t; k < kGradN; k += 256) sp.grad[k] = 0.f;
         return;
     }
-
-    // ---- fresh noise for modelB (reset_noise, :142); targetB is in eval mode -> mu (:100)
-    // (the fresh eps lands in modelB's epsilon buffers, as reset_noise leaves them in the reference)
-    fold_heads(sp.paramsB, sp.paramsB, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_TRAIN,
-               (uint64_t)(c->train_steps + 1), hwB, noise);
-    fold_heads(sp.paramsT, nullptr, PM_FOLD_EVAL, 0, 0, 0, hwT, nullptr);
-    __syncthreads();
-
     const int B = sp.batch;
     const bool act = t < B;
+    // ---- features of s (k_dqn_fwd) -> LDS, coalesced
+    {
+        const float4* src = reinterpret_cast<const float4*>(sp.hfeat);
+        for (int k = t; k < B * 16; k += 256) {
+            const float4 v = src[k];
+            const int row = k >> 4, c4 = (k & 15) * 4;
+            Hs[row][c4 + 0] = v.x; Hs[row][c4 + 1] = v.y; Hs[row][c4 + 2] = v.z; Hs[row][c4 + 3] = v.w;
+        }
+    }
     // ---- IS weights: w /= max(w) over the batch (:72)
-    float wraw = act ? sp.isw[t] : 0.f;
+    const float wraw = act ? sp.isw[t] : 0.f;
     {
         float m = wraw;
 #pragma unroll
@@ -267,18 +300,12 @@ __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
         const float rwd = tr[7];
         const int bits = __float_as_int(tr[15]);
         const int a = bits & 0xff, dn = (bits >> 8) & 1;
-        float h[64], qs[3], qn[3], qt[3];
-        const float* hs = sp.hfeat + (size_t)t * 64;
-#pragma unroll
-        for (int k = 0; k < 64; ++k) { h[k] = hs[k]; Hs[t][k] = h[k]; }
-        heads_q(hwB, h, qs);                      // modelB(s)                (:152)
-        const float* hn = sp.hfeat + (size_t)(B + t) * 64;
-#pragma unroll
-        for (int k = 0; k < 64; ++k) h[k] = hn[k];
-        heads_q(hwB, h, qn);                      // modelB(ns).argmax        (:154)
-        heads_q(hwT, h, qt);                      // targetB(ns)              (:155)
-        const float q = qs[a];
-        const float nq = qt[argmax3(qn)];
+        const float* qq = sp.hfeat + (size_t)B * 64 + (size_t)t * 16;
+        const float qs[3] = {qq[0], qq[1], qq[2]};
+        const float qn[3] = {qq[4], qq[5], qq[6]};
+        const float qt[3] = {qq[8], qq[9], qq[10]};
+        const float q = qs[a];                                        // modelB(s).gather(a)   (:152)
+        const float nq = qt[argmax3(qn)];                             // targetB(ns)[argmax modelB(ns)] (:154-155)
         const float tgt = rwd + (float)sp.gamma * nq * (dn ? 0.f : 1.f);  // r + gamma*nq*(~d) (:156)
         const float diff = q - tgt;
         const float w = wraw / wmax;
@@ -307,20 +334,21 @@ __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
         const float mp = fmaxf(fmaxf(red[0][1], red[1][1]), fmaxf(red[2][1], red[3][1]));
         c->max_prio = fmaxf(c->max_prio, mp);  // n > batch pushes of max_prio survive the scatter
     }
-    // ---- head gradients: dL/dW_mu = sum_j coef_j h_j ; dL/dW_sigma = dL/dW_mu * eps
+    // ---- head gradients: dL/dW_mu = sum_j coef_j h_j ; dL/dW_sigma = dL/dW_mu * eps (the update's
+    // noise, left in modelB's epsilon buffers by k_dqn_fwd)
+    const float* pB = sp.paramsB;
     for (int o = t; o < 260; o += 256) {
         const int row = o < 256 ? o >> 6 : o - 256, col = o & 63;
         const bool wgt = o < 256;
         float g = 0.f;
         for (int j = 0; j < B; ++j) g = fmaf(coef[j][row], wgt ? Hs[j][col] : 1.f, g);
-        const float ein = wgt ? (row == 0 ? noise[col] : noise[65 + col]) : 1.f;
-        const float eout = row == 0 ? noise[64] : noise[129 + row - 1];
-        const float eps = ein * eout;  // weight_epsilon / bias_epsilon entry
         if (row == 0) {
-            sp.grad[(wgt ? 0 : 64) + (wgt ? col : 0)] = g;            // fc_V.weight_mu / bias_mu
-            sp.grad[(wgt ? 65 : 129) + (wgt ? col : 0)] = g * eps;    // fc_V.weight_sigma / bias_sigma
+            const float eps = wgt ? pB[P_VWEP + col] : pB[P_VBEP];
+            sp.grad[wgt ? col : 64] = g;                                // fc_V.weight_mu / bias_mu
+            sp.grad[wgt ? 65 + col : 129] = g * eps;                    // fc_V.weight_sigma / bias_sigma
         } else {
             const int a = row - 1;
+            const float eps = wgt ? pB[P_AWEP + a * 64 + col] : pB[P_ABEP + a];
             sp.grad[wgt ? 130 + a * 64 + col : 322 + a] = g;          // fc_A.weight_mu / bias_mu
             sp.grad[wgt ? 325 + a * 64 + col : 517 + a] = g * eps;    // fc_A.weight_sigma / bias_sigma
         }
@@ -425,13 +453,13 @@ extern "C" int pm_selfplay_learn(const pm_selfplay* sp, void* stream) {
     if (rc) return rc;
     hipStream_t st = pm_stream(stream);
     double* bsum = reinterpret_cast<double*>(sp->per_work);
-    PerSize sz{0, sp->ctrl, sp->n, sp->cap};
-    rc = per_launch_reduce(sp->prios, sz, sp->cap, (float)sp->alpha, bsum, st);
-    if (rc) return rc;
+    const int npush = (sp->n + PER_CHUNK - 1) / PER_CHUNK + 2;
+    hipLaunchKernelGGL(k_per_refresh, dim3(npush + sp->batch), dim3(256), 0, st, *sp, bsum);
+    PM_LAUNCHED("k_per_refresh");
     hipLaunchKernelGGL(k_sp_sample, dim3(pm_blocks(sp->batch, 4)), dim3(256), 0, st, *sp, bsum);
     PM_LAUNCHED("k_sp_sample");
-    hipLaunchKernelGGL(k_dqn_feat, dim3(pm_blocks(2 * sp->batch, 64)), dim3(256), 0, st, *sp);
-    PM_LAUNCHED("k_dqn_feat");
+    hipLaunchKernelGGL(k_dqn_fwd, dim3(pm_blocks(2 * sp->batch, 32)), dim3(64), 0, st, *sp);
+    PM_LAUNCHED("k_dqn_fwd");
     hipLaunchKernelGGL(k_dqn, dim3(1), dim3(256), 0, st, *sp);
     PM_LAUNCHED("k_dqn");
     return PM_OK;

@@ -199,6 +199,7 @@ class SelfPlayLearner:
         self.adam_m.zero_()
         self.adam_v.zero_()
         self.prios.zero_()
+        self.per_work.zero_()  # priority block sums are maintained incrementally
         c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))
         c.pos = c.size = c.train_steps = c.frame_idx = 0
         c.max_prio = 1.0

@@ -191,10 +191,14 @@ typedef struct pm_selfplay {
     int64_t *partials;       /* [ceil(n/256)][8] per-block episode counters of the rollout          */
     float *obsA, *obsB;      /* [n][7] observations of the current step (written by the env kernel) */
     int8_t *aA, *aB;         /* [n] actions of the current step (written by the act kernel)        */
-    float *hfeat;            /* [2*batch][64] learner scratch: features of s and s'                 */
+    float *hfeat;            /* [2*batch][64] learner scratch: features of s, Q values of s and s'  */
+    float *learn_heads;      /* [3][264] next update's modelB heads (fresh noise) and targetB heads in
+                                MFMA fragment order, and that noise (epsilon-buffer layout)        */
     pm_ctrl *ctrl;
     int32_t n, n_pool, batch, world;
     int32_t chunk_A, chunk_P;  /* act grouping: arenas per compaction chunk for modelA / pool nets */
+    int32_t fuse_apply;        /* world == 1: learn also applies (pm_selfplay_apply is then a no-op) */
+    int32_t _pad0;
     int64_t cap;
     double gamma, alpha, lr, beta1, beta2, adam_eps;  /* train_iterative.py:33-37, torch.optim.Adam defaults */
     double min_epsilon, epsilon_decay, pool_ratio, beta_start;
@@ -220,6 +224,10 @@ typedef struct pm_selfplay {
  * pm_selfplay_step = rollout + learn + apply (unsharded). pm_selfplay_init serves every arena,
  * draws first opponents and folds the acting weights of step ctrl->step. */
 int pm_selfplay_init(const pm_selfplay* sp, void* stream);
+/* Re-derive the device-side weights that follow from paramsB/paramsT (acting weights of step
+ * ctrl->step, the next update's noisy / target heads) after the host replaced parameters
+ * (checkpoint load, reset_B, promotion). Called by pm_selfplay_init. */
+int pm_selfplay_prepare(const pm_selfplay* sp, void* stream);
 int pm_selfplay_rollout(const pm_selfplay* sp, void* stream); /* = pm_selfplay_act + pm_selfplay_env */
 int pm_selfplay_act(const pm_selfplay* sp, void* stream);     /* both players' actions -> sp->aA/aB   */
 int pm_selfplay_env(const pm_selfplay* sp, void* stream);     /* tick + push + bookkeeping + serves   */

@@ -231,7 +231,8 @@ __device__ __forceinline__ int argmax3(const float* q) {
 // ----------------------------------------------------------------------------- NoisyNet fold
 // Block-cooperative fold of one parameter block's heads into effective weights (models/qnet.py:43-50):
 //   EVAL: W = mu; TRAIN: W = mu + sigma*eps (block's eps buffers); TRAIN_FRESH: reset_noise()
-//   (models/qnet.py:33-41) from Philox(seed, tag, ctr) then TRAIN, the new eps written to eps_out.
+//   (models/qnet.py:33-41) from Philox(seed, tag, ctr) then TRAIN, the new eps written to eps_out
+//   (a 260-float region in the parameter block's eps layout, e.g. params + PM_QNET_EPS_OFF).
 // `noise` is LDS scratch of >= 132 floats. Writes heads[0,260) = Wh [4][64] | bh [4] (the WH..BH+4
 // slice of an effective-weight block, or any 260-float scratch). Call with all threads.
 __device__ __forceinline__ void fold_heads(const float* params, float* eps_out, int mode, uint64_t seed, uint32_t tag,
@@ -269,8 +270,9 @@ __device__ __forceinline__ void fold_heads(const float* params, float* eps_out, 
         const float v = mode == PM_FOLD_EVAL ? mu : mu + sg * ep;
         heads[w ? k : 256 + row] = v;
         if (mode == PM_FOLD_TRAIN_FRESH && eps_out) {
-            if (row == 0) eps_out[w ? P_VWEP + col : P_VBEP] = ep;
-            else eps_out[w ? P_AWEP + (row - 1) * 64 + col : P_ABEP + row - 1] = ep;
+            constexpr int E = PM_QNET_EPS_OFF;
+            if (row == 0) eps_out[(w ? P_VWEP + col : P_VBEP) - E] = ep;
+            else eps_out[(w ? P_AWEP + (row - 1) * 64 + col : P_ABEP + row - 1) - E] = ep;
         }
     }
 }

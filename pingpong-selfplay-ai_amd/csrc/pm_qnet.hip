@@ -17,7 +17,7 @@ __global__ __launch_bounds__(256) void k_fold(const float* params, float* params
                                               float* __restrict__ w_eff) {
     __shared__ float heads[260], noise[132];
     const float* pb = params + (size_t)blockIdx.x * PM_QNET_NP;
-    float* po = params_out ? params_out + (size_t)blockIdx.x * PM_QNET_NP : nullptr;
+    float* po = params_out ? params_out + (size_t)blockIdx.x * PM_QNET_NP + PM_QNET_EPS_OFF : nullptr;
     float* wb = w_eff + (size_t)blockIdx.x * PM_QNET_NW;
     write_feature_frags(pb, wb);
     const uint64_t ctr = counter + (counter_dev ? *counter_dev : 0ull);

@@ -8,7 +8,8 @@
 //   k_dqn       (1 WG)         double-DQN targets, IS-weighted MSE, head grads, priority update
 //   ----------------------------- (sharded: RCCL all-reduce of sp.grad here)
 //   k_adam      (1 WG)         Adam on the 520 head params, target sync, epsilon decay,
-//                              replay/step counters, next step's acting noise
+//                              replay/step counters, next step's acting noise and next update's
+//                              heads (fused into k_dqn when unsharded)
 //
 // Nothing returns to the host: every loop counter lives in the device control block (pm_ctrl), so
 // a whole vector step can be replayed from a captured graph.
@@ -187,30 +188,94 @@ __global__ __launch_bounds__(256) void k_per_refresh(const pm_selfplay sp, doubl
     if (t == 0) bsum[blk] = ((part[0] + part[1]) + part[2]) + part[3];
 }
 
-// The three QNet evaluations of train_step (:152-155) for the sampled batch on the matrix cores:
-// rows [0, B) are s, rows [B, 2B) are s'. modelB runs with fresh noise (reset_noise, :142),
-// targetB in eval mode (mu, :100). Writes h2 = ReLU(features(s)) for the gradient and, per sample j,
-// q[j*16 + 0..2] = Q_B(s), [4..6] = Q_B(s'), [8..10] = Q_T(s').
-__global__ __launch_bounds__(64) void k_dqn_fwd(const pm_selfplay sp) {
-    __shared__ __attribute__((aligned(16))) float lw[F_SIZE];
-    __shared__ __attribute__((aligned(16))) float hfB[260];
-    __shared__ __attribute__((aligned(16))) float hfT[260];
-    __shared__ float heads[260], noise[132];
-    if (!learner_active(sp)) return;
-    const int lane = threadIdx.x, h = lane >> 5, col = lane & 31;
-    const int B = sp.batch;
-    stage_frags(sp.w_B, lw);  // modelB.features fragments (frozen; == targetB.features)
-    const uint64_t ctr = (uint64_t)(sp.ctrl->train_steps + 1);
-    fold_heads(sp.paramsB, blockIdx.x == 0 ? sp.paramsB : nullptr, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_TRAIN,
-               ctr, heads, noise);  // block 0 leaves the update's noise in modelB's epsilon buffers
+// ------------------------------------------------------------------------------------ apply
+// The next update's heads, computed once the parameters they depend on are final: modelB with
+// fresh noise for update `ts_next` (reset_noise, :142) and targetB in eval mode (mu, :100), both in
+// MFMA fragment order, plus that noise in epsilon-buffer layout. Block-wide.
+__device__ __forceinline__ void prep_learn_heads(const pm_selfplay& sp, uint64_t ts_next, float* heads, float* noise) {
+    float* lh = sp.learn_heads;
+    fold_heads(sp.paramsB, lh + 528, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_TRAIN, ts_next, heads, noise);
     __syncthreads();
-    heads_to_frags(heads, hfB);
+    heads_to_frags(heads, lh);
     __syncthreads();
     fold_heads(sp.paramsT, nullptr, PM_FOLD_EVAL, 0, 0, 0, heads, nullptr);
     __syncthreads();
-    heads_to_frags(heads, hfT);
+    heads_to_frags(heads, lh + 264);
     __syncthreads();
-    const int g = blockIdx.x * 32 + col;
+}
+
+// Acting weights of vector step `step` (select_action_B -> reset_noise, :125): fresh noise folded
+// into w_B's heads; the noise also lands in modelB's epsilon buffers. Block-wide.
+__device__ __forceinline__ void prep_act_heads(const pm_selfplay& sp, uint64_t step, float* heads, float* noise) {
+    fold_heads(sp.paramsB, sp.paramsB + PM_QNET_EPS_OFF, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_ACT, step, heads,
+               noise);
+    __syncthreads();
+    write_head_frags(heads, sp.w_B);
+    __syncthreads();
+}
+
+// optimizer.step() (:161) on grads already divided over shards, target sync (:166-168), epsilon
+// decay (:261), replay / step counters, then the next step's acting weights and next update's
+// heads. Block-wide; `grad` = sp.grad (sums over shards).
+__device__ __forceinline__ void apply_update(const pm_selfplay& sp, float* heads, float* noise) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    pm_ctrl* c = sp.ctrl;
+    const bool train = sp.grad[kGradN + 1] > 0.5f;
+    const int64_t ts = c->train_steps + (train ? 1 : 0);
+    if (train) {
+        const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
+        const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
+        const float step_size = (float)(sp.lr / bc1);
+        const float bc2s = (float)sqrt(bc2);
+        for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
+            const float g = sp.grad[k] / (float)sp.world;
+            float m = sp.adam_m[k], v = sp.adam_v[k];
+            m = m + (float)(1.0 - sp.beta1) * (g - m);                  // exp_avg.lerp_(grad, 1-beta1)
+            v = v * (float)sp.beta2 + (float)(1.0 - sp.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
+            const float denom = sqrtf(v) / bc2s + (float)sp.adam_eps;
+            float* p = sp.paramsB + PM_QNET_HEAD_OFF + k;
+            *p = *p - step_size * (m / denom);
+            sp.adam_m[k] = m;
+            sp.adam_v[k] = v;
+        }
+    }
+    __syncthreads();
+    if (train && ts % sp.target_update_interval == 0)  // targetB.load_state_dict(modelB) (:166-168)
+        for (int k = t; k < PM_QNET_NP; k += nt) sp.paramsT[k] = sp.paramsB[k];
+    __syncthreads();
+    prep_act_heads(sp, c->step + 1, heads, noise);
+    prep_learn_heads(sp, (uint64_t)ts + 1, heads, noise);
+    if (t == 0) {
+        const double D = (double)sp.grad[kGradN];  // finished episodes (all shards)
+        const double e = c->epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
+        c->epsilon = e > sp.min_epsilon ? e : sp.min_epsilon;
+        if (train) { c->train_steps = ts; c->frame_idx += 1; }
+        c->pos = (c->pos + sp.n) % sp.cap;
+        const int64_t s = c->size + sp.n;
+        c->size = s < sp.cap ? s : sp.cap;
+        c->step += 1;
+    }
+}
+
+// ------------------------------------------------------------------------------------ learner
+// The three QNet evaluations of train_step (:152-155) for the sampled batch on the matrix cores:
+// rows [0, B) are s, rows [B, 2B) are s'. Heads come precomputed in learn_heads (modelB with the
+// update's fresh noise, targetB with mu). Writes h2 = ReLU(features(s)) for the gradient and, per
+// sample j, q[j*16 + 0..2] = Q_B(s), [4..6] = Q_B(s'), [8..10] = Q_T(s'). One tile per wave.
+__global__ __launch_bounds__(256) void k_dqn_fwd(const pm_selfplay sp) {
+    __shared__ __attribute__((aligned(16))) float lw[F_SIZE];
+    __shared__ __attribute__((aligned(16))) float hf[2][264];
+    if (!learner_active(sp)) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
+    const int B = sp.batch;
+    stage_frags(sp.w_B, lw);  // modelB.features fragments (frozen; == targetB.features)
+    for (int k = threadIdx.x; k < 2 * 264; k += blockDim.x) hf[k / 264][k % 264] = sp.learn_heads[k];
+    if (blockIdx.x == 0)  // the update's noise in modelB's epsilon buffers, as reset_noise leaves them
+        for (int k = threadIdx.x; k < 260; k += blockDim.x) sp.paramsB[PM_QNET_EPS_OFF + k] = sp.learn_heads[528 + k];
+    __syncthreads();
+    const int tile = blockIdx.x * 4 + wave;
+    if (tile * 32 >= 2 * B) return;  // wave-uniform
+    const int g = tile * 32 + col;
     const bool valid = g < 2 * B;
     const int gg = valid ? g : 2 * B - 1;
     const bool nxt = gg >= B;
@@ -220,8 +285,8 @@ __global__ __launch_bounds__(64) void k_dqn_fwd(const pm_selfplay sp) {
     f32x16 c2[2];
     tile_hidden(lw, xs, lane, c2);
     float qb[3], qt[3];
-    tile_heads(hfB, c2, lane, qb);
-    tile_heads(hfT, c2, lane, qt);
+    tile_heads(hf[0], c2, lane, qb);
+    tile_heads(hf[1], c2, lane, qt);
     float* hs = sp.hfeat + (size_t)j * 64;
     float* q = sp.hfeat + (size_t)B * 64 + (size_t)j * 16;
     if (valid && !nxt) {
@@ -245,155 +310,162 @@ __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
     __shared__ float coef[PM_MAX_BATCH][4];
     __shared__ int64_t sidx[PM_MAX_BATCH];
     __shared__ float red[4][2];
-    __shared__ long long cnt[6];
+    __shared__ float red2[4][8];
+    __shared__ long long cnt[4][6];
+    __shared__ float heads[260], noise[132];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     pm_ctrl* c = sp.ctrl;
 
-    // ---- rollout partials -> episode counters (fixed order)
-    if (t < 6) {
+    // ---- rollout partials -> episode counters: one block row per thread, then a fixed-order tree
+    {
         const int nbr = (sp.n + kBlock - 1) / kBlock;
-        long long s = 0;
-        for (int b = 0; b < nbr; ++b) s += sp.partials[(size_t)b * 8 + t];
-        cnt[t] = s;
+        long long v[6] = {0, 0, 0, 0, 0, 0};
+        for (int b = t; b < nbr; b += 256)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) v[k] += sp.partials[(size_t)b * 8 + k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+            if (lane == 0) cnt[wv][k] = v[k];
+        }
     }
     __syncthreads();
     const bool train = learner_active(sp);
     if (t == 0) {
-        c->ep_step = cnt[0];
-        c->episodes += cnt[0];
-        c->ep_A += cnt[1]; c->win_A += cnt[2];
-        c->ep_P += cnt[3]; c->win_P += cnt[4];
-        c->reward_B += (double)cnt[5];
-        sp.grad[kGradN] = (float)cnt[0];
+        long long s[6];
+        for (int k = 0; k < 6; ++k) s[k] = ((cnt[0][k] + cnt[1][k]) + cnt[2][k]) + cnt[3][k];
+        c->ep_step = s[0];
+        c->episodes += s[0];
+        c->ep_A += s[1]; c->win_A += s[2];
+        c->ep_P += s[3]; c->win_P += s[4];
+        c->reward_B += (double)s[5];
+        sp.grad[kGradN] = (float)s[0];
         sp.grad[kGradN + 1] = train ? 1.f : 0.f;
     }
-    if (!train) {
-        for (int k = t; k < kGradN; k += 256) sp.grad[k] = 0.f;
-        return;
-    }
-    const int B = sp.batch;
-    const bool act = t < B;
-    // ---- features of s (k_dqn_fwd) -> LDS, coalesced
-    {
-        const float4* src = reinterpret_cast<const float4*>(sp.hfeat);
-        for (int k = t; k < B * 16; k += 256) {
-            const float4 v = src[k];
-            const int row = k >> 4, c4 = (k & 15) * 4;
-            Hs[row][c4 + 0] = v.x; Hs[row][c4 + 1] = v.y; Hs[row][c4 + 2] = v.z; Hs[row][c4 + 3] = v.w;
+    if (train) {
+        const int B = sp.batch;
+        const bool act = t < B;
+        {   // features of s (k_dqn_fwd) -> LDS, coalesced
+            const float4* src = reinterpret_cast<const float4*>(sp.hfeat);
+            for (int k = t; k < B * 16; k += 256) {
+                const float4 v = src[k];
+                const int row = k >> 4, c4 = (k & 15) * 4;
+                Hs[row][c4 + 0] = v.x; Hs[row][c4 + 1] = v.y; Hs[row][c4 + 2] = v.z; Hs[row][c4 + 3] = v.w;
+            }
         }
-    }
-    // ---- IS weights: w /= max(w) over the batch (:72)
-    const float wraw = act ? sp.isw[t] : 0.f;
-    {
+        // ---- IS weights: w /= max(w) over the batch (:72)
+        const float wraw = act ? sp.isw[t] : 0.f;
         float m = wraw;
 #pragma unroll
         for (int s = 32; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
         if (lane == 0) red[wv][0] = m;
-    }
-    __syncthreads();
-    const float wmax = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
-    float lossp = 0.f, prio = 0.f;
-    if (act) {
-        const int64_t id = sp.idx[t];
-        sidx[t] = id;
-        const float* tr = sp.trans + id * PM_TRANS_F;
-        const float rwd = tr[7];
-        const int bits = __float_as_int(tr[15]);
-        const int a = bits & 0xff, dn = (bits >> 8) & 1;
-        const float* qq = sp.hfeat + (size_t)B * 64 + (size_t)t * 16;
-        const float qs[3] = {qq[0], qq[1], qq[2]};
-        const float qn[3] = {qq[4], qq[5], qq[6]};
-        const float qt[3] = {qq[8], qq[9], qq[10]};
-        const float q = qs[a];                                        // modelB(s).gather(a)   (:152)
-        const float nq = qt[argmax3(qn)];                             // targetB(ns)[argmax modelB(ns)] (:154-155)
-        const float tgt = rwd + (float)sp.gamma * nq * (dn ? 0.f : 1.f);  // r + gamma*nq*(~d) (:156)
-        const float diff = q - tgt;
-        const float w = wraw / wmax;
-        lossp = w * (diff * diff);
-        const float g = 2.f * w * diff / (float)B;  // d mean(w (q-t)^2) / dq
-        coef[t][0] = g;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) coef[t][1 + k] = g * ((k == a ? 1.f : 0.f) - 1.f / 3.f);
-        prio = fabsf(diff) + 1e-6f;                 // |err| + 1e-6 (:76)
-    }
-    {
-        float s = lossp, m = prio;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o); m = fmaxf(m, __shfl_xor(m, o)); }
         __syncthreads();
-        if (lane == 0) { red[wv][0] = s; red[wv][1] = m; }
-    }
-    __syncthreads();
-    if (act) {  // update_priorities: sequential order, the last duplicate wins (:74-76)
-        bool last = true;
-        for (int k = t + 1; k < B; ++k) last &= sidx[k] != sidx[t];
-        if (last) sp.prios[sidx[t]] = prio;
-    }
-    if (t == 0) {
-        c->last_loss = (((red[0][0] + red[1][0]) + red[2][0]) + red[3][0]) / (float)B;
-        const float mp = fmaxf(fmaxf(red[0][1], red[1][1]), fmaxf(red[2][1], red[3][1]));
-        c->max_prio = fmaxf(c->max_prio, mp);  // n > batch pushes of max_prio survive the scatter
-    }
-    // ---- head gradients: dL/dW_mu = sum_j coef_j h_j ; dL/dW_sigma = dL/dW_mu * eps (the update's
-    // noise, left in modelB's epsilon buffers by k_dqn_fwd)
-    const float* pB = sp.paramsB;
-    for (int o = t; o < 260; o += 256) {
-        const int row = o < 256 ? o >> 6 : o - 256, col = o & 63;
-        const bool wgt = o < 256;
-        float g = 0.f;
-        for (int j = 0; j < B; ++j) g = fmaf(coef[j][row], wgt ? Hs[j][col] : 1.f, g);
-        if (row == 0) {
-            const float eps = wgt ? pB[P_VWEP + col] : pB[P_VBEP];
-            sp.grad[wgt ? col : 64] = g;                                // fc_V.weight_mu / bias_mu
-            sp.grad[wgt ? 65 + col : 129] = g * eps;                    // fc_V.weight_sigma / bias_sigma
-        } else {
-            const int a = row - 1;
-            const float eps = wgt ? pB[P_AWEP + a * 64 + col] : pB[P_ABEP + a];
-            sp.grad[wgt ? 130 + a * 64 + col : 322 + a] = g;          // fc_A.weight_mu / bias_mu
-            sp.grad[wgt ? 325 + a * 64 + col : 517 + a] = g * eps;    // fc_A.weight_sigma / bias_sigma
+        const float wmax = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
+        float lossp = 0.f, prio = 0.f;
+        float cf[4] = {0.f, 0.f, 0.f, 0.f};
+        if (act) {
+            const int64_t id = sp.idx[t];
+            sidx[t] = id;
+            const float* tr = sp.trans + id * PM_TRANS_F;
+            const float rwd = tr[7];
+            const int bits = __float_as_int(tr[15]);
+            const int a = bits & 0xff, dn = (bits >> 8) & 1;
+            const float* qq = sp.hfeat + (size_t)B * 64 + (size_t)t * 16;
+            const float qs[3] = {qq[0], qq[1], qq[2]};
+            const float qn[3] = {qq[4], qq[5], qq[6]};
+            const float qt[3] = {qq[8], qq[9], qq[10]};
+            const float q = qs[a];                                            // modelB(s).gather(a)   (:152)
+            const float nq = qt[argmax3(qn)];                                 // targetB(ns)[argmax modelB(ns)]
+            const float tgt = rwd + (float)sp.gamma * nq * (dn ? 0.f : 1.f);  // r + gamma*nq*(~d)     (:156)
+            const float diff = q - tgt;
+            const float w = wraw / wmax;
+            lossp = w * (diff * diff);
+            const float g = 2.f * w * diff / (float)B;  // d mean(w (q-t)^2) / dq
+            cf[0] = g;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cf[1 + k] = g * ((k == a ? 1.f : 0.f) - 1.f / 3.f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) coef[t][k] = cf[k];
+            prio = fabsf(diff) + 1e-6f;  // |err| + 1e-6 (:76)
         }
+        // loss, max priority and the 4 bias gradients (sum_j coef_j) as block reductions
+        float s = lossp, mp = prio;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o);
+            mp = fmaxf(mp, __shfl_xor(mp, o));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cf[k] += __shfl_xor(cf[k], o);
+        }
+        __syncthreads();
+        if (lane == 0) {
+            red[wv][0] = s; red[wv][1] = mp;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) red2[wv][k] = cf[k];
+        }
+        __syncthreads();
+        if (act) {  // update_priorities: sequential order, the last duplicate wins (:74-76)
+            const int64_t mine = sidx[t];
+            bool last = true;
+#pragma unroll 8
+            for (int k = 0; k < B; ++k) last &= !(k > t && sidx[k] == mine);  // uniform k: broadcast reads
+            if (last) sp.prios[mine] = prio;
+        }
+        if (t == 0) {
+            c->last_loss = (((red[0][0] + red[1][0]) + red[2][0]) + red[3][0]) / (float)B;
+            const float mpx = fmaxf(fmaxf(red[0][1], red[1][1]), fmaxf(red[2][1], red[3][1]));
+            c->max_prio = fmaxf(c->max_prio, mpx);  // n > batch pushes of max_prio survive the scatter
+        }
+        // ---- head gradients: dL/dW_mu = sum_j coef_j h_j (one output per thread), dL/db_mu = sum_j
+        // coef_j; dL/dW_sigma = dL/dW_mu * eps with the update's noise (learn_heads[528..])
+        const float* ep = sp.learn_heads + 528;
+        {
+            const int row = t >> 6, col = t & 63;  // 256 weight outputs, row uniform per wave
+            float g = 0.f;
+#pragma unroll 8
+            for (int j = 0; j < B; ++j) g = fmaf(coef[j][row], Hs[j][col], g);
+            if (row == 0) {
+                sp.grad[col] = g;                                                  // fc_V.weight_mu
+                sp.grad[65 + col] = g * ep[P_VWEP - PM_QNET_EPS_OFF + col];          // fc_V.weight_sigma
+            } else {
+                const int a = row - 1;
+                sp.grad[130 + a * 64 + col] = g;                                   // fc_A.weight_mu
+                sp.grad[325 + a * 64 + col] = g * ep[P_AWEP - PM_QNET_EPS_OFF + a * 64 + col];  // fc_A.weight_sigma
+            }
+        }
+        if (t < 4) {
+            const float g = ((red2[0][t] + red2[1][t]) + red2[2][t]) + red2[3][t];
+            if (t == 0) {
+                sp.grad[64] = g;                                                   // fc_V.bias_mu
+                sp.grad[129] = g * ep[P_VBEP - PM_QNET_EPS_OFF];                     // fc_V.bias_sigma
+            } else {
+                sp.grad[322 + t - 1] = g;                                          // fc_A.bias_mu
+                sp.grad[517 + t - 1] = g * ep[P_ABEP - PM_QNET_EPS_OFF + t - 1];     // fc_A.bias_sigma
+            }
+        }
+    } else {
+        for (int k = t; k < kGradN; k += 256) sp.grad[k] = 0.f;
+    }
+    if (sp.fuse_apply) {  // unsharded: no all-reduce between the gradient and the optimizer step
+        __threadfence_block();
+        __syncthreads();
+        apply_update(sp, heads, noise);
     }
 }
 
 // ------------------------------------------------------------------------------------ Adam + commit
 __global__ __launch_bounds__(1024) void k_adam(const pm_selfplay sp) {
     __shared__ float noise[132], heads[260];
-    const int t = threadIdx.x;
-    pm_ctrl* c = sp.ctrl;
-    const bool train = sp.grad[kGradN + 1] > 0.5f;
-    const int64_t ts = c->train_steps + (train ? 1 : 0);
-    if (train && t < PM_QNET_NHEAD) {  // torch.optim.Adam step (:161)
-        const float g = sp.grad[t] / (float)sp.world;
-        float m = sp.adam_m[t], v = sp.adam_v[t];
-        m = m + (float)(1.0 - sp.beta1) * (g - m);  // exp_avg.lerp_(grad, 1-beta1)
-        v = v * (float)sp.beta2 + (float)(1.0 - sp.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
-        const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
-        const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
-        const float step_size = (float)(sp.lr / bc1);
-        const float denom = sqrtf(v) / (float)sqrt(bc2) + (float)sp.adam_eps;
-        float* p = sp.paramsB + PM_QNET_HEAD_OFF + t;
-        *p = *p - step_size * (m / denom);
-        sp.adam_m[t] = m;
-        sp.adam_v[t] = v;
-    }
-    __syncthreads();
-    if (train && ts % sp.target_update_interval == 0) {  // targetB.load_state_dict(modelB) (:166-168)
-        for (int k = t; k < PM_QNET_NP; k += 1024) sp.paramsT[k] = sp.paramsB[k];
-    }
-    // next vector step's acting noise for modelB (select_action_B -> reset_noise, :125)
-    fold_heads(sp.paramsB, sp.paramsB, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_ACT, c->step + 1, heads, noise);
-    __syncthreads();
-    write_head_frags(heads, sp.w_B);
-    if (t == 0) {
-        const double D = (double)sp.grad[kGradN];  // finished episodes (all shards)
-        const double e = c->epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
-        c->epsilon = e > sp.min_epsilon ? e : sp.min_epsilon;
-        if (train) { c->train_steps = ts; c->frame_idx += 1; }
-        c->pos = (c->pos + sp.n) % sp.cap;
-        const int64_t s = c->size + sp.n;
-        c->size = s < sp.cap ? s : sp.cap;
-        c->step += 1;
-    }
+    apply_update(sp, heads, noise);
+}
+
+// pm_selfplay_prepare: acting weights of the current step + next update's heads
+__global__ __launch_bounds__(256) void k_prepare(const pm_selfplay sp) {
+    __shared__ float noise[132], heads[260];
+    write_feature_frags(sp.paramsB, sp.w_B);
+    prep_act_heads(sp, sp.ctrl->step, heads, noise);
+    prep_learn_heads(sp, (uint64_t)sp.ctrl->train_steps + 1, heads, noise);
 }
 
 int check(const pm_selfplay* sp) {
@@ -404,7 +476,8 @@ int check(const pm_selfplay* sp) {
     PM_REQUIRE(sp->n > 0 && sp->batch >= 1 && sp->batch <= PM_MAX_BATCH && sp->n > sp->batch && sp->cap >= sp->n,
                PM_E_SIZE, "pm_selfplay: n=%d batch=%d cap=%lld", sp->n, sp->batch, (long long)sp->cap);
     PM_REQUIRE(sp->n_pool >= 0 && sp->n_pool <= 4096 && sp->world >= 1, PM_E_SIZE, "pm_selfplay: n_pool/world");
-    PM_REQUIRE(sp->obsA && sp->obsB && sp->aA && sp->aB, PM_E_ARG, "pm_selfplay: null obs/action buffer");
+    PM_REQUIRE(sp->obsA && sp->obsB && sp->aA && sp->aB && sp->learn_heads, PM_E_ARG, "pm_selfplay: null buffer");
+    PM_REQUIRE(!sp->fuse_apply || sp->world == 1, PM_E_ARG, "pm_selfplay: fuse_apply needs world == 1");
     PM_REQUIRE(sp->chunk_A > 0 && sp->chunk_A <= kListMax && sp->chunk_P > 0 && sp->chunk_P <= kListMax, PM_E_SIZE,
                "pm_selfplay: chunk_A/chunk_P must be in [1, %d]", kListMax);
     PM_REQUIRE(((((uintptr_t)sp->w_opp) | ((uintptr_t)sp->w_B)) & 15) == 0, PM_E_ARG, "pm_selfplay: weights alignment");
@@ -415,15 +488,21 @@ int check(const pm_selfplay* sp) {
 
 }  // namespace
 
+extern "C" int pm_selfplay_prepare(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_prepare, dim3(1), dim3(256), 0, pm_stream(stream), *sp);
+    PM_LAUNCHED("k_prepare");
+    return PM_OK;
+}
+
 extern "C" int pm_selfplay_init(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
     hipStream_t st = pm_stream(stream);
     hipLaunchKernelGGL(k_sp_init, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, st, *sp);
     PM_LAUNCHED("k_sp_init");
-    // acting weights of step ctrl->step: features + heads folded with fresh noise, eps kept in paramsB
-    return pm_qnet_fold(sp->paramsB, sp->paramsB, PM_FOLD_TRAIN_FRESH, sp->seed_net, 0, &sp->ctrl->step, sp->w_B, 1,
-                        stream);
+    return pm_selfplay_prepare(sp, stream);
 }
 
 extern "C" int pm_selfplay_act(const pm_selfplay* sp, void* stream) {
@@ -458,7 +537,7 @@ extern "C" int pm_selfplay_learn(const pm_selfplay* sp, void* stream) {
     PM_LAUNCHED("k_per_refresh");
     hipLaunchKernelGGL(k_sp_sample, dim3(pm_blocks(sp->batch, 4)), dim3(256), 0, st, *sp, bsum);
     PM_LAUNCHED("k_sp_sample");
-    hipLaunchKernelGGL(k_dqn_fwd, dim3(pm_blocks(2 * sp->batch, 32)), dim3(64), 0, st, *sp);
+    hipLaunchKernelGGL(k_dqn_fwd, dim3(pm_blocks(2 * sp->batch, 128)), dim3(256), 0, st, *sp);
     PM_LAUNCHED("k_dqn_fwd");
     hipLaunchKernelGGL(k_dqn, dim3(1), dim3(256), 0, st, *sp);
     PM_LAUNCHED("k_dqn");
@@ -468,6 +547,7 @@ extern "C" int pm_selfplay_learn(const pm_selfplay* sp, void* stream) {
 extern "C" int pm_selfplay_apply(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
+    if (sp->fuse_apply) return PM_OK;  // learn already applied (unsharded, fused)
     hipLaunchKernelGGL(k_adam, dim3(1), dim3(1024), 0, pm_stream(stream), *sp);
     PM_LAUNCHED("k_adam");
     return PM_OK;

@@ -55,9 +55,9 @@ class SelfPlay(ctypes.Structure):
     _fields_ = [("env", EnvParams), ("st", EnvState)] + \
         [(n, c_void_p) for n in ("opp", "ep_reward", "w_opp", "paramsB", "paramsT", "w_B", "adam_m", "adam_v",
                                  "trans", "prios", "per_work", "idx", "isw", "grad", "partials", "obsA", "obsB", "aA",
-                                 "aB", "hfeat", "ctrl")] + \
+                                 "aB", "hfeat", "learn_heads", "ctrl")] + \
         [("n", c_i32), ("n_pool", c_i32), ("batch", c_i32), ("world", c_i32), ("chunk_A", c_i32), ("chunk_P", c_i32),
-         ("cap", c_i64)] + \
+         ("fuse_apply", c_i32), ("_pad0", c_i32), ("cap", c_i64)] + \
         [(n, c_double) for n in ("gamma", "alpha", "lr", "beta1", "beta2", "adam_eps", "min_epsilon", "epsilon_decay",
                                  "pool_ratio", "beta_start")] + \
         [("beta_frames", c_i64), ("target_update_interval", c_i64), ("seed_env", c_u64), ("seed_net", c_u64)]
@@ -81,6 +81,7 @@ _SIGS = {
                               c_void_p, c_void_p]),
     "pm_per_update": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_selfplay_init": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_prepare": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_rollout": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_act": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_env": (c_i32, [c_void_p, c_void_p]),

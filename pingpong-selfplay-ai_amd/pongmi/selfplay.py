@@ -48,7 +48,8 @@ class SelfPlayLearner:
     def __init__(self, env_kw, n_arenas, modelB_state, modelA_state=None, pool_states=(), *, batch=256,
                  memory_size=1_000_000, gamma=0.99, lr=2.5e-4, epsilon=0.02, min_epsilon=0.02, epsilon_decay=0.995,
                  target_update_interval=1000, pool_ratio=0.33, alpha=0.6, beta_start=0.4, beta_frames=100000,
-                 episode=0, seed=0, rank=0, world=1, allreduce=None, device=None, modelA_noisy=True):
+                 episode=0, seed=0, rank=0, world=1, allreduce=None, device=None, modelA_noisy=True,
+                 fuse_apply=True):
         self.lib = _lib.load()
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
@@ -89,6 +90,7 @@ class SelfPlayLearner:
         self.grad = torch.zeros(PM_QNET_NHEAD + 8, **f32)
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
         self.hfeat = torch.zeros((2 * self.batch, 64), **f32)
+        self.learn_heads = torch.zeros(3 * 264, **f32)
         self.obsA = torch.zeros((n, 7), **f32)
         self.obsB = torch.zeros((n, 7), **f32)
         self.aA = torch.zeros(n, dtype=torch.int8, device=dev)
@@ -105,9 +107,11 @@ class SelfPlayLearner:
         sp.env = env_params(**env_kw)
         sp.st = _lib.EnvState(*[ptr(self.f64[k]) for k in range(7)], *[ptr(self.i32[k]) for k in range(4)])
         for name in ("opp", "ep_reward", "w_opp", "paramsB", "paramsT", "w_B", "adam_m", "adam_v", "trans", "prios",
-                     "per_work", "idx", "isw", "grad", "partials", "obsA", "obsB", "aA", "aB", "hfeat", "ctrl"):
+                     "per_work", "idx", "isw", "grad", "partials", "obsA", "obsB", "aA", "aB", "hfeat", "learn_heads",
+                     "ctrl"):
             setattr(sp, name, ptr(getattr(self, name)))
         sp.n, sp.n_pool, sp.batch, sp.world, sp.cap = n, self.n_pool, self.batch, self.world, self.cap
+        sp.fuse_apply = int(bool(fuse_apply) and self.world == 1)
         p_pool = pool_ratio if self.n_pool else 0.0
         sp.chunk_A = act_chunk(1.0 - p_pool)
         sp.chunk_P = act_chunk(p_pool / self.n_pool) if self.n_pool else 256
@@ -205,10 +209,11 @@ class SelfPlayLearner:
         c.max_prio = 1.0
         c.epsilon = float(epsilon)
         self.ctrl.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
-        # acting weights for the current step from the new parameters
-        w = fold(self.paramsB, _lib.PM_FOLD_TRAIN_FRESH, seed=self.sp.seed_net,
-                 counter_dev=self.ctrl[:8].view(torch.int64), params_out=self.paramsB)
-        self.w_B.copy_(w[0])
+        self.prepare()
+
+    def prepare(self):
+        """Re-derive acting weights / next-update heads after the host replaced parameters."""
+        check(self.lib.pm_selfplay_prepare(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_prepare")
 
 
 HEAD_NAMES = HEAD_KEYS

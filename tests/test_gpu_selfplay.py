@@ -134,7 +134,7 @@ def test_learn_and_apply_match_oracle(orc, golden):
     """Each update: PER indices from the Philox uniforms on the pre-update priorities, loss and all
     520 head gradients from the oracle's double-DQN restatement with the update's own noise, the
     priority scatter, then Adam and the target sync."""
-    L = _learner(golden, n=1024, batch=256, cap=4096, epsilon=0.5, target_update_interval=3)
+    L = _learner(golden, n=1024, batch=256, cap=4096, epsilon=0.5, target_update_interval=3, fuse_apply=False)
     sp = L.sp
     m_ref = np.zeros(520)
     v_ref = np.zeros(520)
@@ -226,3 +226,31 @@ def test_long_run_invariants(golden):
     assert np.isfinite(L.paramsB.cpu().numpy()).all() and np.isfinite(L.prios.cpu().numpy()).all()
     st = L.i32.cpu().numpy()
     assert st[0].max() < 3 and st[1].max() < 3  # finished episodes were re-served
+
+
+def test_fused_apply_is_bitwise_identical(golden):
+    """Unsharded learn+apply fused into one kernel must equal the split path bit for bit."""
+    A = _learner(golden, n=2048, batch=256, cap=8192, seed=3, fuse_apply=True)
+    B = _learner(golden, n=2048, batch=256, cap=8192, seed=3, fuse_apply=False)
+    for _ in range(15):
+        A.step()
+        B.rollout()
+        B.learn()
+        B.apply()
+    torch.cuda.synchronize()
+    for name in ("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "w_B", "learn_heads"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    ca, cb = A.counters(), B.counters()
+    assert ca == cb
+
+
+def test_deterministic_rerun(golden):
+    """Same seed, same everything: two learners stay bitwise identical (no atomics in the data path)."""
+    A = _learner(golden, n=4096, batch=256, cap=16384, seed=11)
+    B = _learner(golden, n=4096, batch=256, cap=16384, seed=11)
+    for _ in range(20):
+        A.step()
+        B.step()
+    torch.cuda.synchronize()
+    for name in ("paramsB", "prios", "trans", "f64", "opp"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name

@@ -229,52 +229,67 @@ __device__ __forceinline__ int argmax3(const float* q) {
 }
 
 // ----------------------------------------------------------------------------- NoisyNet fold
-// Block-cooperative fold of one parameter block's heads into effective weights (models/qnet.py:43-50):
-//   EVAL: W = mu; TRAIN: W = mu + sigma*eps (block's eps buffers); TRAIN_FRESH: reset_noise()
-//   (models/qnet.py:33-41) from Philox(seed, tag, ctr) then TRAIN, the new eps written to eps_out
-//   (a 260-float region in the parameter block's eps layout, e.g. params + PM_QNET_EPS_OFF).
-// `noise` is LDS scratch of >= 132 floats. Writes heads[0,260) = Wh [4][64] | bh [4] (the WH..BH+4
-// slice of an effective-weight block, or any 260-float scratch). Call with all threads.
-__device__ __forceinline__ void fold_heads(const float* params, float* eps_out, int mode, uint64_t seed, uint32_t tag,
-                                           uint64_t ctr, float* heads, float* noise) {
-    // noise: [0,64) f(eps_in) of fc_V | [64] f(eps_out) of fc_V | [65,129) f(eps_in) of fc_A | [129,132) f(eps_out) of fc_A
-    const int t = threadIdx.x, nt = blockDim.x;
-    if (mode == PM_FOLD_TRAIN_FRESH) {
-        for (int k = t; k < 132; k += nt) {
-            const uint32_t layer = k < 65 ? 0u : 1u;
-            const uint32_t kk = layer ? (uint32_t)(k - 65) : (uint32_t)k;
-            const uint32_t which = layer ? (kk < 64 ? 0u : 1u) : (kk < 64 ? 0u : 1u);
-            const uint32_t e = which ? kk - 64 : kk;
-            const U4 r = philox64(e, tag | (layer << 8) | (which << 12), ctr, seed);
-            noise[k] = scale_noise(normal(r.x, r.y, false));
-        }
-        __syncthreads();
+// Head-section offsets (relative to PM_QNET_HEAD_OFF) and eps-section offsets (relative to
+// PM_QNET_EPS_OFF) of a parameter block.
+enum : int {
+    H_VWMU = 0, H_VBMU = 64, H_VWSG = 65, H_VBSG = 129, H_AWMU = 130, H_ABMU = 322, H_AWSG = 325, H_ABSG = 517,
+    E_VWEP = 0, E_VBEP = 64, E_AWEP = 65, E_ABEP = 257,
+};
+
+// reset_noise() draws (models/qnet.py:33-41) for both heads from Philox(seed, tag, ctr), after
+// _scale_noise: noise[0,64) f(eps_in) fc_V | [64] f(eps_out) fc_V | [65,129) f(eps_in) fc_A |
+// [129,132) f(eps_out) fc_A. Threads [tid0, tid0 + nt) of the block take part.
+__device__ __forceinline__ void gen_noise(uint64_t seed, uint32_t tag, uint64_t ctr, float* noise, int tid, int nt) {
+    for (int k = tid; k < 132; k += nt) {
+        const uint32_t layer = k < 65 ? 0u : 1u;
+        const uint32_t kk = layer ? (uint32_t)(k - 65) : (uint32_t)k;
+        const uint32_t which = kk < 64 ? 0u : 1u;
+        const uint32_t e = which ? kk - 64 : kk;
+        const U4 r = philox64(e, tag | (layer << 8) | (which << 12), ctr, seed);
+        noise[k] = scale_noise(normal(r.x, r.y, false));
     }
-    for (int k = t; k < 260; k += nt) {
+}
+
+// Fold the heads (NoisyLinear.forward, models/qnet.py:43-50) into heads[0,260) = Wh [4][64] | bh [4]:
+//   EVAL: W = mu;  TRAIN: W = mu + sigma*eps with eps from `eps` (eps-section layout);
+//   FRESH: eps = f(eps_out) (x) f(eps_in) from `noise` (gen_noise), also written to eps_out (nullable).
+// hp = the 520-float head section (global or LDS). Threads [tid, tid + nt) take part.
+__device__ __forceinline__ void fold_heads_from(const float* hp, const float* eps, const float* noise, int mode,
+                                                float* heads, float* eps_out, int tid, int nt) {
+    for (int k = tid; k < 260; k += nt) {
         // k in [0,256): weight row k/64 (0 = V, 1..3 = A), column k%64; [256,260): biases
         const int row = k < 256 ? k >> 6 : k - 256, col = k & 63;
         const bool w = k < 256;
         float mu, sg, ep = 0.f;
+        int eo;
         if (row == 0) {
-            mu = w ? params[P_VWMU + col] : params[P_VBMU];
-            sg = w ? params[P_VWSG + col] : params[P_VBSG];
-            if (mode == PM_FOLD_TRAIN) ep = w ? params[P_VWEP + col] : params[P_VBEP];
-            else if (mode == PM_FOLD_TRAIN_FRESH) ep = w ? noise[64] * noise[col] : noise[64];
+            mu = w ? hp[H_VWMU + col] : hp[H_VBMU];
+            sg = w ? hp[H_VWSG + col] : hp[H_VBSG];
+            eo = w ? E_VWEP + col : E_VBEP;
+            if (mode == PM_FOLD_TRAIN_FRESH) ep = w ? noise[64] * noise[col] : noise[64];
         } else {
             const int a = row - 1;
-            mu = w ? params[P_AWMU + a * 64 + col] : params[P_ABMU + a];
-            sg = w ? params[P_AWSG + a * 64 + col] : params[P_ABSG + a];
-            if (mode == PM_FOLD_TRAIN) ep = w ? params[P_AWEP + a * 64 + col] : params[P_ABEP + a];
-            else if (mode == PM_FOLD_TRAIN_FRESH) ep = w ? noise[129 + a] * noise[65 + col] : noise[129 + a];
+            mu = w ? hp[H_AWMU + a * 64 + col] : hp[H_ABMU + a];
+            sg = w ? hp[H_AWSG + a * 64 + col] : hp[H_ABSG + a];
+            eo = w ? E_AWEP + a * 64 + col : E_ABEP + a;
+            if (mode == PM_FOLD_TRAIN_FRESH) ep = w ? noise[129 + a] * noise[65 + col] : noise[129 + a];
         }
-        const float v = mode == PM_FOLD_EVAL ? mu : mu + sg * ep;
-        heads[w ? k : 256 + row] = v;
-        if (mode == PM_FOLD_TRAIN_FRESH && eps_out) {
-            constexpr int E = PM_QNET_EPS_OFF;
-            if (row == 0) eps_out[(w ? P_VWEP + col : P_VBEP) - E] = ep;
-            else eps_out[(w ? P_AWEP + (row - 1) * 64 + col : P_ABEP + row - 1) - E] = ep;
-        }
+        if (mode == PM_FOLD_TRAIN) ep = eps[eo];
+        heads[w ? k : 256 + row] = mode == PM_FOLD_EVAL ? mu : mu + sg * ep;  // torch: mu + (sigma*eps)
+        if (mode == PM_FOLD_TRAIN_FRESH && eps_out) eps_out[eo] = ep;
     }
+}
+
+// One parameter block, block-wide (generates the noise first in FRESH mode). `noise` is LDS
+// scratch of >= 132 floats; eps_out (nullable) is the block's eps section to write.
+__device__ __forceinline__ void fold_heads(const float* params, float* eps_out, int mode, uint64_t seed, uint32_t tag,
+                                           uint64_t ctr, float* heads, float* noise) {
+    if (mode == PM_FOLD_TRAIN_FRESH) {
+        gen_noise(seed, tag, ctr, noise, threadIdx.x, blockDim.x);
+        __syncthreads();
+    }
+    fold_heads_from(params + PM_QNET_HEAD_OFF, params + PM_QNET_EPS_OFF, noise, mode, heads, eps_out, threadIdx.x,
+                    blockDim.x);
 }
 
 }  // namespace pm

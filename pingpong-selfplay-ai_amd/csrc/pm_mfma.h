@@ -78,13 +78,23 @@ __device__ __forceinline__ void stage_frags(const float* __restrict__ w, float* 
 }
 
 // Append the arenas i in [lo, hi) with id[i] == net to the LDS list (order unspecified: every row
-// is computed independently, so the tile composition never changes a result). Block-wide.
+// is computed independently, so the tile composition never changes a result). All of a thread's
+// ids are loaded before the first ballot, so a chunk costs one memory round trip. Block-wide;
+// hi - lo <= kListMax (16 ids per thread at 256 threads).
 __device__ __forceinline__ void compact_rows(const int32_t* __restrict__ id, int net, int lo, int hi, int* list,
                                              int* count) {
-    const int lane = threadIdx.x & 63;
-    for (int base = lo; base < hi; base += blockDim.x) {
-        const int i = base + (int)threadIdx.x;
-        const bool m = i < hi && id[i] == net;
+    const int lane = threadIdx.x & 63, nt = blockDim.x;
+    int ids[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int i = lo + r * nt + (int)threadIdx.x;
+        ids[r] = i < hi ? id[i] : -1;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if (lo + r * nt >= hi) break;  // block-uniform
+        const int i = lo + r * nt + (int)threadIdx.x;
+        const bool m = ids[r] == net;
         const unsigned long long b = __ballot(m);
         int pos = 0;
         if (lane == 0 && b) pos = atomicAdd(count, __popcll(b));
@@ -211,12 +221,22 @@ __device__ __forceinline__ void run_tiles(const float* lw, const float* __restri
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int h = lane >> 5, col = lane & 31;
     const int ntiles = (count + 31) >> 5;
-    for (int tl = wave; tl < ntiles; tl += nw) {
+    int tl = wave;
+    if (tl >= ntiles) return;  // wave-uniform
+    int arena = list[min(tl * 32 + col, count - 1)];
+    float xs[4];
+    tile_inputs(obs + (size_t)arena * 7, h, xs);
+    for (; tl < ntiles; tl += nw) {
         const int row = tl * 32 + col;
         const bool valid = row < count;
-        const int arena = list[valid ? row : tl * 32];
-        float xs[4];
-        tile_inputs(obs + (size_t)arena * 7, h, xs);
+        // prefetch the next tile's observations: their loads land during this tile's MFMAs
+        const int tn = tl + nw;
+        int arena_n = arena;
+        float xn[4] = {xs[0], xs[1], xs[2], xs[3]};
+        if (tn < ntiles) {
+            arena_n = list[min(tn * 32 + col, count - 1)];
+            tile_inputs(obs + (size_t)arena_n * 7, h, xn);
+        }
         f32x16 c2[2];
         tile_hidden(lw, xs, lane, c2);
         float q[3];
@@ -234,6 +254,9 @@ __device__ __forceinline__ void run_tiles(const float* lw, const float* __restri
                 out.q[(size_t)arena * 3 + 2] = q[2];
             }
         }
+        arena = arena_n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xs[k] = xn[k];
     }
 }
 

@@ -189,62 +189,82 @@ __global__ __launch_bounds__(256) void k_per_refresh(const pm_selfplay sp, doubl
 }
 
 // ------------------------------------------------------------------------------------ apply
-// The next update's heads, computed once the parameters they depend on are final: modelB with
-// fresh noise for update `ts_next` (reset_noise, :142) and targetB in eval mode (mu, :100), both in
-// MFMA fragment order, plus that noise in epsilon-buffer layout. Block-wide.
-__device__ __forceinline__ void prep_learn_heads(const pm_selfplay& sp, uint64_t ts_next, float* heads, float* noise) {
+struct ApplySmem {
+    float hp[PM_QNET_NHEAD];   // modelB head parameters (after the optimizer step)
+    float tmu[PM_QNET_NHEAD];  // targetB head parameters (mu used)
+    float nact[132], ntrain[132];
+    float heads[260];
+};
+
+// Everything that follows from the head parameters once they are final for this step, from LDS:
+// acting weights for vector step `act_ctr` (select_action_B -> reset_noise, :125; the noise lands
+// in modelB's epsilon buffers), the next update's modelB heads with fresh noise `train_ctr`
+// (reset_noise, :142) and targetB heads (eval mode: mu, :100), both in MFMA fragment order in
+// learn_heads, plus that update's noise. Block-wide; noise already in sm.nact / sm.ntrain.
+__device__ __forceinline__ void derive_weights(const pm_selfplay& sp, ApplySmem& sm) {
+    const int t = threadIdx.x, nt = blockDim.x;
     float* lh = sp.learn_heads;
-    fold_heads(sp.paramsB, lh + 528, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_TRAIN, ts_next, heads, noise);
+    fold_heads_from(sm.hp, nullptr, sm.nact, PM_FOLD_TRAIN_FRESH, sm.heads, sp.paramsB + PM_QNET_EPS_OFF, t, nt);
     __syncthreads();
-    heads_to_frags(heads, lh);
+    write_head_frags(sm.heads, sp.w_B);
     __syncthreads();
-    fold_heads(sp.paramsT, nullptr, PM_FOLD_EVAL, 0, 0, 0, heads, nullptr);
+    fold_heads_from(sm.hp, nullptr, sm.ntrain, PM_FOLD_TRAIN_FRESH, sm.heads, lh + 528, t, nt);
     __syncthreads();
-    heads_to_frags(heads, lh + 264);
+    heads_to_frags(sm.heads, lh);
     __syncthreads();
+    fold_heads_from(sm.tmu, nullptr, nullptr, PM_FOLD_EVAL, sm.heads, nullptr, t, nt);
+    __syncthreads();
+    heads_to_frags(sm.heads, lh + 264);
 }
 
-// Acting weights of vector step `step` (select_action_B -> reset_noise, :125): fresh noise folded
-// into w_B's heads; the noise also lands in modelB's epsilon buffers. Block-wide.
-__device__ __forceinline__ void prep_act_heads(const pm_selfplay& sp, uint64_t step, float* heads, float* noise) {
-    fold_heads(sp.paramsB, sp.paramsB + PM_QNET_EPS_OFF, PM_FOLD_TRAIN_FRESH, sp.seed_net, TAG_NOISE_ACT, step, heads,
-               noise);
-    __syncthreads();
-    write_head_frags(heads, sp.w_B);
-    __syncthreads();
+// Both noise draws at once, half of the block each.
+__device__ __forceinline__ void gen_both_noises(const pm_selfplay& sp, ApplySmem& sm, uint64_t act_ctr,
+                                                uint64_t train_ctr) {
+    const int t = threadIdx.x, half = blockDim.x / 2;
+    if (t < half) gen_noise(sp.seed_net, TAG_NOISE_ACT, act_ctr, sm.nact, t, half);
+    else gen_noise(sp.seed_net, TAG_NOISE_TRAIN, train_ctr, sm.ntrain, t - half, half);
 }
 
-// optimizer.step() (:161) on grads already divided over shards, target sync (:166-168), epsilon
-// decay (:261), replay / step counters, then the next step's acting weights and next update's
-// heads. Block-wide; `grad` = sp.grad (sums over shards).
-__device__ __forceinline__ void apply_update(const pm_selfplay& sp, float* heads, float* noise) {
+// optimizer.step() (:161) on the shard-summed grads, target sync (:166-168), epsilon decay (:261),
+// replay / step counters, then derive_weights for the next step. One global load round trip:
+// grads, Adam moments, modelB and targetB heads are read together; the rest runs from LDS.
+__device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& sm) {
     const int t = threadIdx.x, nt = blockDim.x;
     pm_ctrl* c = sp.ctrl;
     const bool train = sp.grad[kGradN + 1] > 0.5f;
     const int64_t ts = c->train_steps + (train ? 1 : 0);
-    if (train) {
-        const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
-        const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
-        const float step_size = (float)(sp.lr / bc1);
-        const float bc2s = (float)sqrt(bc2);
-        for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
+    const uint64_t step = c->step;
+    const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
+    const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
+    const float step_size = (float)(sp.lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
+        float p = sp.paramsB[PM_QNET_HEAD_OFF + k];
+        sm.tmu[k] = sp.paramsT[PM_QNET_HEAD_OFF + k];
+        if (train) {
             const float g = sp.grad[k] / (float)sp.world;
             float m = sp.adam_m[k], v = sp.adam_v[k];
             m = m + (float)(1.0 - sp.beta1) * (g - m);                  // exp_avg.lerp_(grad, 1-beta1)
             v = v * (float)sp.beta2 + (float)(1.0 - sp.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
             const float denom = sqrtf(v) / bc2s + (float)sp.adam_eps;
-            float* p = sp.paramsB + PM_QNET_HEAD_OFF + k;
-            *p = *p - step_size * (m / denom);
+            p = p - step_size * (m / denom);
+            sp.paramsB[PM_QNET_HEAD_OFF + k] = p;
             sp.adam_m[k] = m;
             sp.adam_v[k] = v;
         }
+        sm.hp[k] = p;
+    }
+    gen_both_noises(sp, sm, step + 1, (uint64_t)ts + 1);
+    __syncthreads();
+    if (train && ts % sp.target_update_interval == 0) {  // targetB.load_state_dict(modelB) (:166-168)
+        for (int k = t; k < PM_QNET_NHEAD; k += nt) sm.tmu[k] = sm.hp[k];
+        for (int k = t; k < PM_QNET_NP; k += nt) {
+            const int h = k - PM_QNET_HEAD_OFF;
+            sp.paramsT[k] = (h >= 0 && h < PM_QNET_NHEAD) ? sm.hp[h] : sp.paramsB[k];
+        }
     }
     __syncthreads();
-    if (train && ts % sp.target_update_interval == 0)  // targetB.load_state_dict(modelB) (:166-168)
-        for (int k = t; k < PM_QNET_NP; k += nt) sp.paramsT[k] = sp.paramsB[k];
-    __syncthreads();
-    prep_act_heads(sp, c->step + 1, heads, noise);
-    prep_learn_heads(sp, (uint64_t)ts + 1, heads, noise);
+    derive_weights(sp, sm);
     if (t == 0) {
         const double D = (double)sp.grad[kGradN];  // finished episodes (all shards)
         const double e = c->epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
@@ -253,7 +273,7 @@ __device__ __forceinline__ void apply_update(const pm_selfplay& sp, float* heads
         c->pos = (c->pos + sp.n) % sp.cap;
         const int64_t s = c->size + sp.n;
         c->size = s < sp.cap ? s : sp.cap;
-        c->step += 1;
+        c->step = step + 1;
     }
 }
 
@@ -312,7 +332,7 @@ __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
     __shared__ float red[4][2];
     __shared__ float red2[4][8];
     __shared__ long long cnt[4][6];
-    __shared__ float heads[260], noise[132];
+    __shared__ ApplySmem asm_;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     pm_ctrl* c = sp.ctrl;
 
@@ -450,22 +470,27 @@ __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
     if (sp.fuse_apply) {  // unsharded: no all-reduce between the gradient and the optimizer step
         __threadfence_block();
         __syncthreads();
-        apply_update(sp, heads, noise);
+        apply_update(sp, asm_);
     }
 }
 
 // ------------------------------------------------------------------------------------ Adam + commit
 __global__ __launch_bounds__(1024) void k_adam(const pm_selfplay sp) {
-    __shared__ float noise[132], heads[260];
-    apply_update(sp, heads, noise);
+    __shared__ ApplySmem sm;
+    apply_update(sp, sm);
 }
 
-// pm_selfplay_prepare: acting weights of the current step + next update's heads
+// pm_selfplay_prepare: features + acting weights of the current step + next update's heads
 __global__ __launch_bounds__(256) void k_prepare(const pm_selfplay sp) {
-    __shared__ float noise[132], heads[260];
+    __shared__ ApplySmem sm;
     write_feature_frags(sp.paramsB, sp.w_B);
-    prep_act_heads(sp, sp.ctrl->step, heads, noise);
-    prep_learn_heads(sp, (uint64_t)sp.ctrl->train_steps + 1, heads, noise);
+    for (int k = threadIdx.x; k < PM_QNET_NHEAD; k += blockDim.x) {
+        sm.hp[k] = sp.paramsB[PM_QNET_HEAD_OFF + k];
+        sm.tmu[k] = sp.paramsT[PM_QNET_HEAD_OFF + k];
+    }
+    gen_both_noises(sp, sm, sp.ctrl->step, (uint64_t)sp.ctrl->train_steps + 1);
+    __syncthreads();
+    derive_weights(sp, sm);
 }
 
 int check(const pm_selfplay* sp) {

@@ -22,15 +22,9 @@ import torch
 
 from . import _lib
 from ._lib import PM_QNET_NHEAD, PM_QNET_NP, PM_QNET_NW, PM_TRANS_F, check, ptr, stream_ptr
+from .dist import shard_seeds, splitmix64  # noqa: F401
 from .env import env_config, env_params
 from .qnet import HEAD_KEYS, fold, pack_state_dict, unpack_state_dict
-
-
-def splitmix64(x):
-    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
-    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
-    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
-    return x ^ (x >> 31)
 
 
 def act_chunk(p, rows=96, cap=4096):
@@ -119,8 +113,7 @@ class SelfPlayLearner:
         sp.beta1, sp.beta2, sp.adam_eps = 0.9, 0.999, 1e-8
         sp.min_epsilon, sp.epsilon_decay, sp.pool_ratio, sp.beta_start = min_epsilon, epsilon_decay, pool_ratio, beta_start
         sp.beta_frames, sp.target_update_interval = int(beta_frames), int(target_update_interval)
-        sp.seed_env = splitmix64(self.seed * 0x100000001B3 + 1 + self.rank)
-        sp.seed_net = splitmix64(self.seed ^ 0x5EED5EED5EED)
+        sp.seed_env, sp.seed_net = shard_seeds(self.seed, self.rank)
         self.sp = sp
         self.hparams = dict(gamma=gamma, lr=lr, min_epsilon=min_epsilon, epsilon_decay=epsilon_decay,
                             target_update_interval=target_update_interval, pool_ratio=pool_ratio, alpha=alpha,

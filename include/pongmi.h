@@ -184,14 +184,14 @@ typedef struct pm_selfplay {
     float *adam_m, *adam_v;  /* [PM_QNET_NHEAD] Adam state                                        */
     float *trans;            /* [cap][PM_TRANS_F] replay ring                                     */
     float *prios;            /* [cap] priorities                                                  */
-    void *per_work;          /* pm_per_work_bytes(cap)                                            */
+    void *per_work;          /* pm_per_work_bytes(cap): PER sum tree (16-byte aligned, as prios)  */
     int64_t *idx;            /* [batch] sampled indices                                           */
     float *isw;              /* [batch] IS weights                                                */
     float *grad;             /* [PM_QNET_NHEAD + 8] grads + packed counters (all-reduced when sharded) */
     int64_t *partials;       /* [ceil(n/256)][8] per-block episode counters of the rollout          */
     float *obsA, *obsB;      /* [n][7] observations of the current step (written by the env kernel) */
     int8_t *aA, *aB;         /* [n] actions of the current step (written by the act kernel)        */
-    float *hfeat;            /* [2*batch][64] learner scratch: features of s, Q values of s and s'  */
+    float *hfeat;            /* [batch][16] last update's Q_B(s) 0..2, Q_B(s') 4..6, Q_T(s') 8..10 */
     float *learn_heads;      /* [3][264] next update's modelB heads (fresh noise) and targetB heads in
                                 MFMA fragment order, and that noise (epsilon-buffer layout)        */
     pm_ctrl *ctrl;
@@ -212,11 +212,13 @@ typedef struct pm_selfplay {
 #define PM_MAX_BATCH 256
 
 /* One vector step of scripts/train_iterative.py:239-245 for all n arenas, as device work only:
- *   rollout: act (both players, :240-241; matrix-core kernel) then env step (:242) + replay push
- *            (:243) + episode bookkeeping (:245-249, next opponent :235-236, env.reset :238);
- *   learn:   once the replay holds >= batch transitions: PER sample + double-DQN loss/grads +
- *            priority update (train_step, :132-164), leaving grads and the finished-episode count
- *            in sp->grad;
+ *   rollout: act (both players, :240-241; matrix-core kernel, which also draws this step's PER
+ *            sample, :64-73, into sp->idx / sp->isw once the replay will hold >= batch) then env
+ *            step (:242) + replay push (:243) + episode bookkeeping (:245-249, next opponent
+ *            :235-236, env.reset :238);
+ *   learn:   once the replay holds >= batch transitions: double-DQN loss/grads + priority update
+ *            (train_step, :132-164) on the sampled batch, leaving grads and the finished-episode
+ *            count in sp->grad; keeps the PER sum tree in sp->per_work current (incl. the next push);
  *   apply:   grads /= world, Adam on the 520 head parameters (:159-161), target sync every
  *            target_update_interval updates (:166-168), epsilon decay per finished episode
  *            (:261), replay/step counters, next step's acting noise (:125).
@@ -224,12 +226,14 @@ typedef struct pm_selfplay {
  * pm_selfplay_step = rollout + learn + apply (unsharded). pm_selfplay_init serves every arena,
  * draws first opponents and folds the acting weights of step ctrl->step. */
 int pm_selfplay_init(const pm_selfplay* sp, void* stream);
-/* Re-derive the device-side weights that follow from paramsB/paramsT (acting weights of step
- * ctrl->step, the next update's noisy / target heads) after the host replaced parameters
- * (checkpoint load, reset_B, promotion). Called by pm_selfplay_init. */
+/* Re-derive everything the device keeps that follows from host-visible state: the weights that
+ * follow from paramsB/paramsT (acting weights of step ctrl->step, the next update's noisy / target
+ * heads) and a full rebuild of the PER sum tree from prios + ctrl. Call after the host changed
+ * parameters, priorities or replay counters (checkpoint load, reset_B, promotion). Called by
+ * pm_selfplay_init. */
 int pm_selfplay_prepare(const pm_selfplay* sp, void* stream);
 int pm_selfplay_rollout(const pm_selfplay* sp, void* stream); /* = pm_selfplay_act + pm_selfplay_env */
-int pm_selfplay_act(const pm_selfplay* sp, void* stream);     /* both players' actions -> sp->aA/aB   */
+int pm_selfplay_act(const pm_selfplay* sp, void* stream);     /* actions -> sp->aA/aB; PER sample    */
 int pm_selfplay_env(const pm_selfplay* sp, void* stream);     /* tick + push + bookkeeping + serves   */
 int pm_selfplay_learn(const pm_selfplay* sp, void* stream);
 int pm_selfplay_apply(const pm_selfplay* sp, void* stream);

@@ -29,3 +29,4 @@ extern "C" int32_t pm_sizeof(int32_t which) {
         default: return -1;
     }
 }
+

@@ -13,6 +13,33 @@
 
 #include "pongmi.h"
 
+#ifdef PM_DIAG
+// TU-local (no -fgpu-rdc): only pm_selfplay.hip stamps, and it exports the reader.
+static __device__ unsigned long long pm_diag_buf[256];
+#define PM_STAMP(slot)                                                                 \
+    do {                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x == 0) pm_diag_buf[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define PM_STAMP_ANY(slot)                                                             \
+    do {                                                                               \
+        if (threadIdx.x == 0) pm_diag_buf[(slot)] = __builtin_amdgcn_s_memrealtime();  \
+    } while (0)
+#define PM_STAMP_T(slot, tid)                                                                            \
+    do {                                                                                                 \
+        if (threadIdx.x == (tid) && blockIdx.x == 0) pm_diag_buf[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PM_STAMP_T(slot, tid) \
+    do {                      \
+    } while (0)
+#define PM_STAMP_ANY(slot) \
+    do {                   \
+    } while (0)
+#define PM_STAMP(slot) \
+    do {               \
+    } while (0)
+#endif
+
 namespace pm {
 
 // ----------------------------------------------------------------------------- RNG

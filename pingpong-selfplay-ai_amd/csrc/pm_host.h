@@ -20,3 +20,8 @@ int pm_fail(int code, const char* fmt, ...);
 
 static inline hipStream_t pm_stream(void* s) { return (hipStream_t)s; }
 static inline unsigned pm_blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+// ---------------------------------------------------------------- diagnostic stamps (PM_DIAG builds only)
+// libpongmi_diag.so is built with -DPM_DIAG: thread 0 of block 0 records s_memrealtime (100 MHz)
+// at named phase boundaries into pm_diag_buf; pm_diag_read copies them out. The product library
+// compiles every stamp to nothing.

@@ -281,13 +281,12 @@ struct ActShared {
     int count;
 };
 
-// Block-wide body of the grouped act kernel. side B: eps-greedy on obsB with w_B;
+// Block-wide body of the grouped act kernel for grid block b. side B: eps-greedy on obsB with w_B;
 // side A: greedy on obsA with w_opp[net]. opp == nullptr -> every arena plays net 0.
 __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const float* __restrict__ w_opp,
                                           const int32_t* __restrict__ opp, const float* __restrict__ w_B,
                                           const float* __restrict__ obsA, const float* __restrict__ obsB,
-                                          TileOut outA, TileOut outB) {
-    int b = blockIdx.x;
+                                          TileOut outA, TileOut outB, int b) {
     const float* w;
     const float* obs;
     TileOut out;

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(kActBlock, 2) void k_act(ActGrid g, const float* __
     __shared__ __attribute__((aligned(16))) ActShared sh;
     if (eps_dev) outB.eps = *eps_dev;
     if (counter_dev) outB.ctr += *counter_dev;
-    act_block(sh, g, w_opp, opp, w_B, obsA, obsB, outA, outB);
+    act_block(sh, g, w_opp, opp, w_B, obsA, obsB, outA, outB, blockIdx.x);
 }
 
 }  // namespace

@@ -1,10 +1,10 @@
 // K4 — prioritized replay on the device (scripts/train_iterative.py:49-76).
 //
-// Proportional sampling exactly as np.random.choice(p=...) does it (cdf = running sum of
-// p_i = prio_i^alpha, first index whose running sum exceeds u * total: searchsorted 'right'),
-// restructured for HBM: one streaming pass writes per-1024-entry block sums (fp64), then one wave
-// per sample walks block sums and its block with wave-wide inclusive scans. Every reduction has a
-// fixed order, so a sample is a pure function of (priorities, u) — no atomics anywhere.
+// Proportional sampling as np.random.choice(p=...) does it (cdf = running sum of p_i = prio_i^alpha,
+// first index whose running sum exceeds u * total: searchsorted 'right'), restructured for HBM: a
+// streaming pass builds the sum tree of pm_per.h (fp32 leaves, 64- and 1024-entry fp64 nodes), then
+// one wave per sample descends it with wave-wide inclusive scans. Every reduction has a fixed order,
+// so a sample is a pure function of (priorities, u) — no atomics anywhere.
 #include "pm_dev.h"
 #include "pm_host.h"
 #include "pm_per.h"
@@ -13,46 +13,42 @@ using namespace pm;
 
 namespace {
 
-__global__ __launch_bounds__(256) void k_per_reduce(const float* __restrict__ prios, PerSize sz, float alpha,
-                                                    double* __restrict__ bsum) {
-    __shared__ double part[4];
-    const int64_t size = sz.get();
-    const int64_t nb = (size + PER_CHUNK - 1) / PER_CHUNK;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        double s = 0.0;
-        const int64_t base = b * PER_CHUNK;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t e = base + t + k * 256;
-            if (e < size) s += (double)powf(prios[e], alpha);
-        }
-        s = wave_sum(s);
-        if (lane == 0) part[wv] = s;
-        __syncthreads();
-        if (t == 0) bsum[b] = ((part[0] + part[1]) + part[2]) + part[3];
-        __syncthreads();
-    }
+// Pending push range from the device control block (selfplay: a captured graph needs no host
+// round trip), or none.
+__device__ __forceinline__ PushRange push_range(const pm_ctrl* ctrl, int64_t n_push, int64_t cap, float alpha) {
+    if (!ctrl) return PushRange{0, 0, cap, 0.f};
+    return PushRange{ctrl->pos, n_push, cap, prio_pow(ctrl->size == 0 ? 1.0f : ctrl->max_prio, alpha)};
 }
 
-}  // namespace
+__global__ __launch_bounds__(256) void k_per_leaves(const float* __restrict__ prios, int64_t cap, float alpha,
+                                                    float* __restrict__ leaf) {
+    for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < cap; e += (int64_t)gridDim.x * 256)
+        leaf[e] = prio_pow(prios[e], alpha);
+}
 
+__global__ __launch_bounds__(256) void k_per_subs(int64_t cap, float alpha, const pm_ctrl* ctrl, int64_t n_push,
+                                                  PerTree tr) {
+    const PushRange pr = push_range(ctrl, n_push, cap, alpha);
+    for (int64_t s = blockIdx.x * 256 + threadIdx.x; s < tr.nsub; s += (int64_t)gridDim.x * 256)
+        tr.sub[s] = per_sub_sum(tr.leaf, s, pr);
+}
 
-namespace {
+__global__ __launch_bounds__(256) void k_per_chunks(PerTree tr) {
+    for (int64_t c = blockIdx.x * 256 + threadIdx.x; c < tr.nchunk; c += (int64_t)gridDim.x * 256)
+        tr.chunk[c] = per_chunk_sum(tr, c);
+}
 
-__global__ __launch_bounds__(256) void k_per_sample(const float* __restrict__ prios, PerSize sz, float alpha,
-                                                    double beta, const double* __restrict__ u, uint64_t seed,
-                                                    uint64_t counter, const double* __restrict__ bsum,
-                                                    int64_t* __restrict__ idx, float* __restrict__ w, int bs) {
+__global__ __launch_bounds__(256) void k_per_sample(int64_t size, double beta, const double* __restrict__ u, uint64_t seed,
+                                                    uint64_t counter, PerTree tr, int64_t* __restrict__ idx,
+                                                    float* __restrict__ w, int bs) {
     const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (j >= bs) return;  // wave-uniform
-    const int64_t size = sz.get();
     double uj;
     if (u) uj = u[j];
     else { const U4 r = philox64((uint32_t)j, TAG_PER, counter, seed); uj = u53(r.x, r.y); }
     int64_t i;
     float wr;
-    per_sample_one(prios, size, bsum, alpha, beta, uj, i, wr);
+    per_sample_one(size, tr, PushRange{0, 0, size, 0.f}, beta, uj, i, wr);
     if ((threadIdx.x & 63) == 0) { idx[j] = i; w[j] = wr; }
 }
 
@@ -84,11 +80,19 @@ __global__ __launch_bounds__(256) void k_per_update(float* __restrict__ prios, c
 extern "C" int64_t pm_per_work_bytes(int64_t cap) { return per_work_bytes(cap); }
 
 namespace pm {
-int per_launch_reduce(const float* prios, PerSize sz, int64_t cap, float alpha, double* bsum, hipStream_t st) {
-    const int64_t nb = (cap + PER_CHUNK - 1) / PER_CHUNK;
-    const unsigned grid = (unsigned)(nb < 4096 ? (nb > 0 ? nb : 1) : 4096);
-    hipLaunchKernelGGL(k_per_reduce, dim3(grid), dim3(256), 0, st, prios, sz, alpha, bsum);
-    PM_LAUNCHED("k_per_reduce");
+int per_launch_build(const float* prios, int64_t cap, float alpha, const pm_ctrl* ctrl, int64_t n_push, void* work,
+                     hipStream_t st) {
+    const PerTree tr = per_tree(work, cap);
+    const auto grid = [](int64_t n) {
+        const int64_t b = (n + 255) / 256;
+        return (unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+    };
+    hipLaunchKernelGGL(k_per_leaves, dim3(grid(cap)), dim3(256), 0, st, prios, cap, alpha, tr.leaf);
+    PM_LAUNCHED("k_per_leaves");
+    hipLaunchKernelGGL(k_per_subs, dim3(grid(tr.nsub)), dim3(256), 0, st, cap, alpha, ctrl, n_push, tr);
+    PM_LAUNCHED("k_per_subs");
+    hipLaunchKernelGGL(k_per_chunks, dim3(grid(tr.nchunk)), dim3(256), 0, st, tr);
+    PM_LAUNCHED("k_per_chunks");
     return PM_OK;
 }
 int per_launch_update(float* prios, const int64_t* idx, const float* err, int bs, hipStream_t st) {
@@ -103,12 +107,12 @@ extern "C" int pm_per_sample(const float* prios, int64_t size, float alpha, floa
     PM_REQUIRE(prios && idx && w && work, PM_E_ARG, "pm_per_sample: null buffer");
     PM_REQUIRE(size > 0 && bs > 0, PM_E_SIZE, "pm_per_sample: size=%lld bs=%d", (long long)size, bs);
     hipStream_t st = pm_stream(stream);
-    double* bsum = reinterpret_cast<double*>(work);
-    PerSize sz{size, nullptr, 0, 0};
-    int rc = per_launch_reduce(prios, sz, size, alpha, bsum, st);
+    const PerTree tr = per_tree(work, size);
+    PM_REQUIRE(((uintptr_t)work & 15) == 0, PM_E_ARG, "pm_per_sample: work must be 16-byte aligned");
+    int rc = per_launch_build(prios, size, alpha, nullptr, 0, work, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_per_sample, dim3(pm_blocks(bs, 4)), dim3(256), 0, st, prios, sz, alpha, (double)beta, u, seed,
-                       counter, bsum, idx, w, bs);
+    hipLaunchKernelGGL(k_per_sample, dim3(pm_blocks(bs, 4)), dim3(256), 0, st, size, (double)beta, u, seed, counter, tr,
+                       idx, w, bs);
     PM_LAUNCHED("k_per_sample");
     hipLaunchKernelGGL(k_per_normalize, dim3(1), dim3(1024), 0, st, w, bs);
     PM_LAUNCHED("k_per_normalize");

@@ -1,18 +1,18 @@
-// The batched self-play learner: one vector step of scripts/train_iterative.py:239-245 for n arenas.
+// The batched self-play learner: one vector step of scripts/train_iterative.py:239-245 for n arenas,
+// three kernels, nothing returns to the host:
 //
-//   k_act_sp    (MFMA tiles)   both players' QNet forward + eps-greedy / argmax (pm_mfma.h)
-//   k_env       (n lanes)      env tick + replay push + episode bookkeeping + serves
-//   k_per_refresh              per-1024 block sums of prio^alpha for the blocks that changed
-//   k_sp_sample (batch waves)  proportional sample + un-normalised IS weights
-//   k_dqn_fwd   (MFMA tiles)   Q_B(s), Q_B(s'), Q_T(s') and features of s for the sampled batch
-//   k_dqn       (1 WG)         double-DQN targets, IS-weighted MSE, head grads, priority update
-//   ----------------------------- (sharded: RCCL all-reduce of sp.grad here)
-//   k_adam      (1 WG)         Adam on the 520 head params, target sync, epsilon decay,
-//                              replay/step counters, next step's acting noise and next update's
-//                              heads (fused into k_dqn when unsharded)
+//   k_act_sp (MFMA tiles)  both players' QNet forward + eps-greedy / argmax (pm_mfma.h); its first
+//                          ceil(batch/4) blocks draw this step's PER sample (one wave per sample) off
+//                          the sum tree, which already accounts for the push k_env is about to make
+//   k_env    (n lanes)     env tick + replay push + episode bookkeeping + serves
+//   k_learn  (1 WG, 1024)  Q_B(s), Q_B(s'), Q_T(s') on the matrix cores into LDS, double-DQN targets,
+//                          IS-weighted MSE, priority scatter, sum-tree refresh (scattered sub-blocks +
+//                          next push range), head grads [+ Adam / target sync / epsilon decay /
+//                          counters / next weights when unsharded]
+//   ----------------------- (sharded: RCCL all-reduce of sp.grad, then k_adam)
 //
-// Nothing returns to the host: every loop counter lives in the device control block (pm_ctrl), so
-// a whole vector step can be replayed from a captured graph.
+// Every loop counter lives in the device control block (pm_ctrl), so a whole vector step can be
+// replayed from a captured graph.
 #include "pm_host.h"
 #include "pm_mfma.h"
 #include "pm_per.h"
@@ -22,22 +22,61 @@ using namespace pm;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kGradN = PM_QNET_NHEAD;  // grad[520] = finished episodes, grad[521] = updated flag
+constexpr int kLearn = 1024;              // k_learn / k_adam / k_prepare block
+constexpr int kGradN = PM_QNET_NHEAD;     // grad[520] = finished episodes, grad[521] = updated flag
+constexpr uint32_t kHashEmpty = 0xFFFFFFFFu;
 
 __device__ __forceinline__ bool learner_active(const pm_selfplay& sp) {
     const int64_t s = sp.ctrl->size + sp.n;
     return (s < sp.cap ? s : sp.cap) >= sp.batch;
 }
 
+__device__ __forceinline__ double beta_of(const pm_selfplay& sp, int64_t frame) {  // :137
+    const double b = sp.beta_start + (double)frame * (1.0 - sp.beta_start) / (double)sp.beta_frames;
+    return b < 1.0 ? b : 1.0;
+}
+
+// The push k_env makes this step: [pos, pos + n) mod cap at max(prios) (1.0 into an empty buffer, :57).
+__device__ __forceinline__ float push_prio(int64_t size, float max_prio) { return size == 0 ? 1.0f : max_prio; }
+__device__ __forceinline__ PushRange push_of(const pm_selfplay& sp, int64_t pos, int64_t size, float max_prio) {
+    return PushRange{pos, sp.n, sp.cap, prio_pow(push_prio(size, max_prio), (float)sp.alpha)};
+}
+}  // namespace
+
 // ------------------------------------------------------------------------------------ rollout
+// PrioritizedReplay.sample (:64-73) for update sample j: proportional draw + un-normalised IS weight.
+__device__ __forceinline__ void sample_wave(const pm_selfplay& sp, int j) {
+    if (j >= sp.batch || !learner_active(sp)) return;  // wave-uniform
+    const pm_ctrl* c = sp.ctrl;
+    const int64_t s = c->size + sp.n;
+    const int64_t size = s < sp.cap ? s : sp.cap;
+    const int64_t frame = c->frame_idx + 1;  // frame_idx += 1 before sampling (:136)
+    const U4 r = philox64((uint32_t)j, TAG_PER, (uint64_t)frame, sp.seed_env);
+    int64_t idx;
+    float wr;
+    per_sample_one(size, per_tree(sp.per_work, sp.cap), push_of(sp, c->pos, c->size, c->max_prio), beta_of(sp, frame),
+                   u53(r.x, r.y), idx, wr);
+    if ((threadIdx.x & 63) == 0) { sp.idx[j] = idx; sp.isw[j] = wr; }
+}
+
 // Both players act (train_iterative.py:240-241) on the matrix cores: ActGrid blocks, modelB tiles
 // with epsilon-greedy, opponent tiles grouped by net (modelA / pool) so weights are tile-uniform.
+// Blocks [0, ceil(batch/4)) sample the update's batch instead (latency-bound, hidden under the act).
 __global__ __launch_bounds__(kActBlock, 2) void k_act_sp(const pm_selfplay sp) {
     __shared__ __attribute__((aligned(16))) ActShared sh;
+    const int nsb = (sp.batch + 3) / 4;
+    if ((int)blockIdx.x < nsb) {
+        PM_STAMP(64);
+        sample_wave(sp, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+        PM_STAMP(65);
+        return;
+    }
+    if ((int)blockIdx.x == nsb) PM_STAMP_ANY(70);
     const ActGrid g{sp.n, sp.n_pool + 1, sp.chunk_A, sp.chunk_P, 1};
     const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
     const TileOut outB{sp.aB, nullptr, sp.ctrl->epsilon, sp.seed_env, sp.ctrl->step};
-    act_block(sh, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, sp.w_B, sp.obsA, sp.obsB, outA, outB);
+    act_block(sh, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, sp.w_B, sp.obsA, sp.obsB, outA, outB,
+              (int)blockIdx.x - nsb);
 }
 
 // env.step (:242) + memory.push (:243) + episode bookkeeping (:245-249) + next opponent (:235-236)
@@ -50,8 +89,11 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
     const bool valid = i < sp.n;
     const int ii = valid ? i : sp.n - 1;
     const pm_ctrl* c = sp.ctrl;
+    PM_STAMP(72);
     const int64_t pos = c->pos, size = c->size;
-    const float maxp = size == 0 ? 1.0f : c->max_prio;  // max(prios) if buffer else 1.0 (:57)
+    const float maxp = push_prio(size, c->max_prio);  // max(prios) if buffer else 1.0 (:57)
+    float* leaf = per_tree(sp.per_work, sp.cap).leaf;
+    const float pval = prio_pow(maxp, (float)sp.alpha);  // its PER leaf
 
     Arena a = load_arena(sp.st, ii);
     const int aA = sp.aA[ii], aB = sp.aB[ii];
@@ -86,6 +128,7 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
         row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
         row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
         sp.prios[slot] = maxp;
+        leaf[slot] = pval;
         int onew = o;
         float ernew = er;
         if (d) {  // next episode: opponent draw then env.reset()
@@ -137,70 +180,33 @@ __global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
 }
 
 // ------------------------------------------------------------------------------------ learner
-__device__ __forceinline__ double beta_of(const pm_selfplay& sp, int64_t frame) {  // :137
-    const double b = sp.beta_start + (double)frame * (1.0 - sp.beta_start) / (double)sp.beta_frames;
-    return b < 1.0 ? b : 1.0;
-}
-
-__global__ __launch_bounds__(256) void k_sp_sample(const pm_selfplay sp, const double* __restrict__ bsum) {
-    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= sp.batch || !learner_active(sp)) return;  // wave-uniform
-    const int64_t s = sp.ctrl->size + sp.n;
-    const int64_t size = s < sp.cap ? s : sp.cap;
-    const int64_t frame = sp.ctrl->frame_idx + 1;  // frame_idx += 1 before sampling (:136)
-    const U4 r = philox64((uint32_t)j, TAG_PER, (uint64_t)frame, sp.seed_env);
-    int64_t idx;
-    float wr;
-    per_sample_one(sp.prios, size, bsum, (float)sp.alpha, beta_of(sp, frame), u53(r.x, r.y), idx, wr);
-    if ((threadIdx.x & 63) == 0) { sp.idx[j] = idx; sp.isw[j] = wr; }
-}
-
-// Priority block sums, incremental: only the 1024-entry blocks this step's push wrote ([pos, pos+n)
-// mod cap) and the blocks the previous update's priority scatter touched (sp.idx still holds its
-// indices) changed since they were last summed. Each is recomputed from scratch in the same fixed
-// order as a full pass (k_per_reduce), so the sums are identical to a full recompute.
-__global__ __launch_bounds__(256) void k_per_refresh(const pm_selfplay sp, double* __restrict__ bsum) {
-    __shared__ double part[4];
-    if (!learner_active(sp)) return;
-    const int64_t nbc = (sp.cap + PER_CHUNK - 1) / PER_CHUNK;
-    const int64_t npush = (int64_t)(sp.n + PER_CHUNK - 1) / PER_CHUNK + 2;
-    int64_t blk;
-    if ((int64_t)blockIdx.x < npush) {
-        const int64_t pos = sp.ctrl->pos;  // not yet committed: the push of this step started here
-        const int64_t first = pos / PER_CHUNK, last = (pos + sp.n - 1) / PER_CHUNK;
-        if (first + (int64_t)blockIdx.x > last) return;
-        blk = (first + blockIdx.x) % nbc;
-    } else {
-        blk = sp.idx[blockIdx.x - npush] / PER_CHUNK;
-    }
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const float alpha = (float)sp.alpha;
-    double acc = 0.0;
-    const int64_t base = blk * PER_CHUNK;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int64_t e = base + t + k * 256;
-        if (e < sp.cap) acc += (double)powf(sp.prios[e], alpha);
-    }
-    acc = wave_sum(acc);
-    if (lane == 0) part[wv] = acc;
-    __syncthreads();
-    if (t == 0) bsum[blk] = ((part[0] + part[1]) + part[2]) + part[3];
-}
-
 // ------------------------------------------------------------------------------------ apply
 struct ApplySmem {
     float hp[PM_QNET_NHEAD];   // modelB head parameters (after the optimizer step)
     float tmu[PM_QNET_NHEAD];  // targetB head parameters (mu used)
+    float m[PM_QNET_NHEAD], v[PM_QNET_NHEAD];  // Adam moments
+    float g[PM_QNET_NHEAD + 2];                // shard-summed grads | finished episodes | updated flag
     float nact[132], ntrain[132];
     float heads[260];
 };
 
+// Block-wide: the optimizer's inputs into LDS (one load round trip). g: from LDS already when fused.
+__device__ __forceinline__ void load_apply_inputs(const pm_selfplay& sp, ApplySmem& sm, bool with_grad) {
+    for (int k = threadIdx.x; k < PM_QNET_NHEAD; k += blockDim.x) {
+        sm.hp[k] = sp.paramsB[PM_QNET_HEAD_OFF + k];
+        sm.tmu[k] = sp.paramsT[PM_QNET_HEAD_OFF + k];
+        sm.m[k] = sp.adam_m[k];
+        sm.v[k] = sp.adam_v[k];
+    }
+    if (with_grad)
+        for (int k = threadIdx.x; k < PM_QNET_NHEAD + 2; k += blockDim.x) sm.g[k] = sp.grad[k];
+}
+
 // Everything that follows from the head parameters once they are final for this step, from LDS:
-// acting weights for vector step `act_ctr` (select_action_B -> reset_noise, :125; the noise lands
-// in modelB's epsilon buffers), the next update's modelB heads with fresh noise `train_ctr`
-// (reset_noise, :142) and targetB heads (eval mode: mu, :100), both in MFMA fragment order in
-// learn_heads, plus that update's noise. Block-wide; noise already in sm.nact / sm.ntrain.
+// acting weights for the next vector step (select_action_B -> reset_noise, :125; the noise lands
+// in modelB's epsilon buffers), the next update's modelB heads with fresh noise (reset_noise, :142)
+// and targetB heads (eval mode: mu, :100), both in MFMA fragment order in learn_heads, plus that
+// update's noise. Block-wide; noise already in sm.nact / sm.ntrain.
 __device__ __forceinline__ void derive_weights(const pm_selfplay& sp, ApplySmem& sm) {
     const int t = threadIdx.x, nt = blockDim.x;
     float* lh = sp.learn_heads;
@@ -226,24 +232,22 @@ __device__ __forceinline__ void gen_both_noises(const pm_selfplay& sp, ApplySmem
 }
 
 // optimizer.step() (:161) on the shard-summed grads, target sync (:166-168), epsilon decay (:261),
-// replay / step counters, then derive_weights for the next step. One global load round trip:
-// grads, Adam moments, modelB and targetB heads are read together; the rest runs from LDS.
-__device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& sm) {
+// replay / step counters, then derive_weights for the next step. All inputs in LDS (sm) and `cs`
+// (the control block as the kernel found it); only stores go to global memory.
+__device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& sm, const pm_ctrl& cs) {
     const int t = threadIdx.x, nt = blockDim.x;
-    pm_ctrl* c = sp.ctrl;
-    const bool train = sp.grad[kGradN + 1] > 0.5f;
-    const int64_t ts = c->train_steps + (train ? 1 : 0);
-    const uint64_t step = c->step;
-    const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
-    const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
-    const float step_size = (float)(sp.lr / bc1);
-    const float bc2s = (float)sqrt(bc2);
-    for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
-        float p = sp.paramsB[PM_QNET_HEAD_OFF + k];
-        sm.tmu[k] = sp.paramsT[PM_QNET_HEAD_OFF + k];
-        if (train) {
-            const float g = sp.grad[k] / (float)sp.world;
-            float m = sp.adam_m[k], v = sp.adam_v[k];
+    const bool train = sm.g[kGradN + 1] > 0.5f;
+    const int64_t ts = cs.train_steps + (train ? 1 : 0);
+    const uint64_t step = cs.step;
+    gen_both_noises(sp, sm, step + 1, (uint64_t)ts + 1);
+    if (train) {
+        const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
+        const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
+        const float step_size = (float)(sp.lr / bc1);
+        const float bc2s = (float)sqrt(bc2);
+        for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
+            const float g = sm.g[k] / (float)sp.world;
+            float m = sm.m[k], v = sm.v[k], p = sm.hp[k];
             m = m + (float)(1.0 - sp.beta1) * (g - m);                  // exp_avg.lerp_(grad, 1-beta1)
             v = v * (float)sp.beta2 + (float)(1.0 - sp.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
             const float denom = sqrtf(v) / bc2s + (float)sp.adam_eps;
@@ -251,165 +255,201 @@ __device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& s
             sp.paramsB[PM_QNET_HEAD_OFF + k] = p;
             sp.adam_m[k] = m;
             sp.adam_v[k] = v;
+            sm.hp[k] = p;
         }
-        sm.hp[k] = p;
     }
-    gen_both_noises(sp, sm, step + 1, (uint64_t)ts + 1);
     __syncthreads();
+    PM_STAMP(20);
     if (train && ts % sp.target_update_interval == 0) {  // targetB.load_state_dict(modelB) (:166-168)
         for (int k = t; k < PM_QNET_NHEAD; k += nt) sm.tmu[k] = sm.hp[k];
         for (int k = t; k < PM_QNET_NP; k += nt) {
             const int h = k - PM_QNET_HEAD_OFF;
             sp.paramsT[k] = (h >= 0 && h < PM_QNET_NHEAD) ? sm.hp[h] : sp.paramsB[k];
         }
+        __syncthreads();
     }
-    __syncthreads();
     derive_weights(sp, sm);
+    PM_STAMP(21);
     if (t == 0) {
-        const double D = (double)sp.grad[kGradN];  // finished episodes (all shards)
-        const double e = c->epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
+        pm_ctrl* c = sp.ctrl;
+        const double D = (double)sm.g[kGradN];  // finished episodes (all shards)
+        const double e = cs.epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
         c->epsilon = e > sp.min_epsilon ? e : sp.min_epsilon;
-        if (train) { c->train_steps = ts; c->frame_idx += 1; }
-        c->pos = (c->pos + sp.n) % sp.cap;
-        const int64_t s = c->size + sp.n;
+        if (train) { c->train_steps = ts; c->frame_idx = cs.frame_idx + 1; }
+        c->pos = (cs.pos + sp.n) % sp.cap;
+        const int64_t s = cs.size + sp.n;
         c->size = s < sp.cap ? s : sp.cap;
         c->step = step + 1;
     }
 }
 
 // ------------------------------------------------------------------------------------ learner
-// The three QNet evaluations of train_step (:152-155) for the sampled batch on the matrix cores:
-// rows [0, B) are s, rows [B, 2B) are s'. Heads come precomputed in learn_heads (modelB with the
-// update's fresh noise, targetB with mu). Writes h2 = ReLU(features(s)) for the gradient and, per
-// sample j, q[j*16 + 0..2] = Q_B(s), [4..6] = Q_B(s'), [8..10] = Q_T(s'). One tile per wave.
-__global__ __launch_bounds__(256) void k_dqn_fwd(const pm_selfplay sp) {
-    __shared__ __attribute__((aligned(16))) float lw[F_SIZE];
-    __shared__ __attribute__((aligned(16))) float hf[2][264];
-    if (!learner_active(sp)) return;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
-    const int B = sp.batch;
-    stage_frags(sp.w_B, lw);  // modelB.features fragments (frozen; == targetB.features)
-    for (int k = threadIdx.x; k < 2 * 264; k += blockDim.x) hf[k / 264][k % 264] = sp.learn_heads[k];
-    if (blockIdx.x == 0)  // the update's noise in modelB's epsilon buffers, as reset_noise leaves them
-        for (int k = threadIdx.x; k < 260; k += blockDim.x) sp.paramsB[PM_QNET_EPS_OFF + k] = sp.learn_heads[528 + k];
-    __syncthreads();
-    const int tile = blockIdx.x * 4 + wave;
-    if (tile * 32 >= 2 * B) return;  // wave-uniform
+struct LearnSmem {
+    union {
+        struct {  // forward phase
+            float lw[F_SIZE];  // modelB.features fragments (== targetB.features: frozen)
+            float hf[2][264];  // modelB (update noise) / targetB (mu) head fragments
+        } f;
+        float gpart[16][256];  // gradient phase: per-wave partial sums
+    } u;
+    float Hs[PM_MAX_BATCH][65];  // ReLU(features(s)) of the batch
+    float qv[PM_MAX_BATCH][12];  // Q_B(s) 0..2 | Q_B(s') 4..6 | Q_T(s') 8..10
+    float coef[PM_MAX_BATCH][4]; // dL/d(V, A0, A1, A2) per sample
+    float eps_tr[260];           // the update's noise (eps section layout)
+    int64_t sidx[PM_MAX_BATCH];
+    uint32_t hkey[512];          // open-addressing set of sampled indices (last-duplicate-wins)
+    int hwin[512];
+    float red[16][8];
+    long long cnt[16][6];
+    ApplySmem ap;
+};
+
+// One tile of 32 rows of the batch forward: rows [0, B) are s, [B, 2B) are s'.
+__device__ __forceinline__ void learn_tile(const pm_selfplay& sp, LearnSmem& sm, int tile, int lane) {
+    const int h = lane >> 5, col = lane & 31, B = sp.batch;
     const int g = tile * 32 + col;
     const bool valid = g < 2 * B;
     const int gg = valid ? g : 2 * B - 1;
     const bool nxt = gg >= B;
     const int j = nxt ? gg - B : gg;
     float xs[4];
-    tile_inputs(sp.trans + sp.idx[j] * PM_TRANS_F + (nxt ? 8 : 0), h, xs);
+    tile_inputs(sp.trans + sm.sidx[j] * PM_TRANS_F + (nxt ? 8 : 0), h, xs);
     f32x16 c2[2];
-    tile_hidden(lw, xs, lane, c2);
+    tile_hidden(sm.u.f.lw, xs, lane, c2);
     float qb[3], qt[3];
-    tile_heads(hf[0], c2, lane, qb);
-    tile_heads(hf[1], c2, lane, qt);
-    float* hs = sp.hfeat + (size_t)j * 64;
-    float* q = sp.hfeat + (size_t)B * 64 + (size_t)j * 16;
+    tile_heads(sm.u.f.hf[0], c2, lane, qb);
+    tile_heads(sm.u.f.hf[1], c2, lane, qt);
     if (valid && !nxt) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) hs[32 * t + rho(r) + 4 * h] = fmaxf(c2[t][r], 0.f);
+            for (int r = 0; r < 16; ++r) sm.Hs[j][32 * t + rho(r) + 4 * h] = fmaxf(c2[t][r], 0.f);
     }
     if (valid && h == 0) {
+        float* q = sp.hfeat + (size_t)j * 16;  // inspection copy
         if (!nxt) {
+            sm.qv[j][0] = qb[0]; sm.qv[j][1] = qb[1]; sm.qv[j][2] = qb[2];
             q[0] = qb[0]; q[1] = qb[1]; q[2] = qb[2];
         } else {
+            sm.qv[j][4] = qb[0]; sm.qv[j][5] = qb[1]; sm.qv[j][6] = qb[2];
+            sm.qv[j][8] = qt[0]; sm.qv[j][9] = qt[1]; sm.qv[j][10] = qt[2];
             q[4] = qb[0]; q[5] = qb[1]; q[6] = qb[2];
             q[8] = qt[0]; q[9] = qt[1]; q[10] = qt[2];
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
-    __shared__ float Hs[PM_MAX_BATCH][65];
-    __shared__ float coef[PM_MAX_BATCH][4];
-    __shared__ int64_t sidx[PM_MAX_BATCH];
-    __shared__ float red[4][2];
-    __shared__ float red2[4][8];
-    __shared__ long long cnt[4][6];
-    __shared__ ApplySmem asm_;
+// train_step (:134-168) for the batch k_act_sp sampled, plus the episode counters of the rollout and
+// the sum-tree refresh. Single workgroup of 1024 threads; global loads are issued up front.
+__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
+    __shared__ __attribute__((aligned(16))) LearnSmem sm;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int B = sp.batch;
     pm_ctrl* c = sp.ctrl;
+    PM_STAMP(0);
+    const pm_ctrl cs = *c;  // loop counters as the step found them (only this kernel / k_adam commit)
+    const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
+    const bool train = s_after >= B;
+    const PerTree tree = per_tree(sp.per_work, sp.cap);
 
-    // ---- rollout partials -> episode counters: one block row per thread, then a fixed-order tree
+    // ---- phase 0: every independent load
+    long long part[6] = {0, 0, 0, 0, 0, 0};
     {
         const int nbr = (sp.n + kBlock - 1) / kBlock;
-        long long v[6] = {0, 0, 0, 0, 0, 0};
-        for (int b = t; b < nbr; b += 256)
+        for (int b = t; b < nbr; b += kLearn)
 #pragma unroll
-            for (int k = 0; k < 6; ++k) v[k] += sp.partials[(size_t)b * 8 + k];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
-            if (lane == 0) cnt[wv][k] = v[k];
-        }
+            for (int k = 0; k < 6; ++k) part[k] += sp.partials[(size_t)b * 8 + k];
     }
-    __syncthreads();
-    const bool train = learner_active(sp);
-    if (t == 0) {
-        long long s[6];
-        for (int k = 0; k < 6; ++k) s[k] = ((cnt[0][k] + cnt[1][k]) + cnt[2][k]) + cnt[3][k];
-        c->ep_step = s[0];
-        c->episodes += s[0];
-        c->ep_A += s[1]; c->win_A += s[2];
-        c->ep_P += s[3]; c->win_P += s[4];
-        c->reward_B += (double)s[5];
-        sp.grad[kGradN] = (float)s[0];
-        sp.grad[kGradN + 1] = train ? 1.f : 0.f;
-    }
+    const bool act = train && t < B;
+    const float wraw = act ? sp.isw[t] : 0.f;
+    const int64_t id = act ? sp.idx[t] : 0;
     if (train) {
-        const int B = sp.batch;
-        const bool act = t < B;
-        {   // features of s (k_dqn_fwd) -> LDS, coalesced
-            const float4* src = reinterpret_cast<const float4*>(sp.hfeat);
-            for (int k = t; k < B * 16; k += 256) {
-                const float4 v = src[k];
-                const int row = k >> 4, c4 = (k & 15) * 4;
-                Hs[row][c4 + 0] = v.x; Hs[row][c4 + 1] = v.y; Hs[row][c4 + 2] = v.z; Hs[row][c4 + 3] = v.w;
-            }
+        stage_frags(sp.w_B, sm.u.f.lw);
+        for (int k = t; k < 2 * 264; k += kLearn) sm.u.f.hf[k / 264][k % 264] = sp.learn_heads[k];
+        for (int k = t; k < 260; k += kLearn) {  // the update's noise, left in modelB's buffers by reset_noise
+            const float e = sp.learn_heads[528 + k];
+            sm.eps_tr[k] = e;
+            sp.paramsB[PM_QNET_EPS_OFF + k] = e;
         }
-        // ---- IS weights: w /= max(w) over the batch (:72)
-        const float wraw = act ? sp.isw[t] : 0.f;
+    }
+    if (sp.fuse_apply) load_apply_inputs(sp, sm.ap, false);
+    for (int k = t; k < 512; k += kLearn) { sm.hkey[k] = kHashEmpty; sm.hwin[k] = -1; }
+    if (act) sm.sidx[t] = id;
+    float rwd = 0.f;
+    int bits = 0;
+    if (act) {
+        const float* tr = sp.trans + id * PM_TRANS_F;
+        rwd = tr[7];
+        bits = __float_as_int(tr[15]);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) part[k] += __shfl_xor(part[k], o);
+        if (lane == 0) sm.cnt[wv][k] = part[k];
+    }
+    {
         float m = wraw;
 #pragma unroll
-        for (int s = 32; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
-        if (lane == 0) red[wv][0] = m;
-        __syncthreads();
-        const float wmax = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
-        float lossp = 0.f, prio = 0.f;
-        float cf[4] = {0.f, 0.f, 0.f, 0.f};
-        if (act) {
-            const int64_t id = sp.idx[t];
-            sidx[t] = id;
-            const float* tr = sp.trans + id * PM_TRANS_F;
-            const float rwd = tr[7];
-            const int bits = __float_as_int(tr[15]);
-            const int a = bits & 0xff, dn = (bits >> 8) & 1;
-            const float* qq = sp.hfeat + (size_t)B * 64 + (size_t)t * 16;
-            const float qs[3] = {qq[0], qq[1], qq[2]};
-            const float qn[3] = {qq[4], qq[5], qq[6]};
-            const float qt[3] = {qq[8], qq[9], qq[10]};
-            const float q = qs[a];                                            // modelB(s).gather(a)   (:152)
-            const float nq = qt[argmax3(qn)];                                 // targetB(ns)[argmax modelB(ns)]
-            const float tgt = rwd + (float)sp.gamma * nq * (dn ? 0.f : 1.f);  // r + gamma*nq*(~d)     (:156)
-            const float diff = q - tgt;
-            const float w = wraw / wmax;
-            lossp = w * (diff * diff);
-            const float g = 2.f * w * diff / (float)B;  // d mean(w (q-t)^2) / dq
-            cf[0] = g;
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        if (lane == 0) sm.red[wv][0] = m;
+    }
+    __syncthreads();
+    PM_STAMP(1);
+
+    // ---- phase 1: counters; the batch forward on the matrix cores (one 32-row tile per wave)
+    long long ep_fin = 0;
+    if (t < 6) {
+        long long s = 0;
+        for (int w = 0; w < 16; ++w) s += sm.cnt[w][t];
+        sm.cnt[0][t] = s;  // read after the next barrier
+    }
+    if (train && wv * 32 < 2 * B) learn_tile(sp, sm, wv, lane);
+    float wmax = sm.red[0][0];
+    for (int w = 1; w < 16; ++w) wmax = fmaxf(wmax, sm.red[w][0]);
+    __syncthreads();
+    PM_STAMP(2);
+    ep_fin = sm.cnt[0][0];
+    if (t == 0) {  // rollout bookkeeping (:245-249)
+        c->ep_step = ep_fin;
+        c->episodes = cs.episodes + ep_fin;
+        c->ep_A = cs.ep_A + sm.cnt[0][1]; c->win_A = cs.win_A + sm.cnt[0][2];
+        c->ep_P = cs.ep_P + sm.cnt[0][3]; c->win_P = cs.win_P + sm.cnt[0][4];
+        c->reward_B = cs.reward_B + (double)sm.cnt[0][5];
+    }
+
+    // ---- phase 2: double-DQN targets, loss, priorities, bias grads
+    float lossp = 0.f, prio = 0.f;
+    float cf[4] = {0.f, 0.f, 0.f, 0.f};
+    int slot = 0;
+    if (act) {
+        const int a = bits & 0xff, dn = (bits >> 8) & 1;
+        const float qs[3] = {sm.qv[t][0], sm.qv[t][1], sm.qv[t][2]};
+        const float qn[3] = {sm.qv[t][4], sm.qv[t][5], sm.qv[t][6]};
+        const float qt[3] = {sm.qv[t][8], sm.qv[t][9], sm.qv[t][10]};
+        const float q = qs[a];                                            // modelB(s).gather(a)   (:152)
+        const float nq = qt[argmax3(qn)];                                 // targetB(ns)[argmax modelB(ns)]
+        const float tgt = rwd + (float)sp.gamma * nq * (dn ? 0.f : 1.f);  // r + gamma*nq*(~d)     (:156)
+        const float diff = q - tgt;
+        const float w = wraw / wmax;                                      // w /= w.max() (:72)
+        lossp = w * (diff * diff);
+        const float g = 2.f * w * diff / (float)B;  // d mean(w (q-t)^2) / dq
+        cf[0] = g;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) cf[1 + k] = g * ((k == a ? 1.f : 0.f) - 1.f / 3.f);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) coef[t][k] = cf[k];
-            prio = fabsf(diff) + 1e-6f;  // |err| + 1e-6 (:76)
+        for (int k = 0; k < 3; ++k) cf[1 + k] = g * ((k == a ? 1.f : 0.f) - 1.f / 3.f);
+        *reinterpret_cast<float4*>(sm.coef[t]) = make_float4(cf[0], cf[1], cf[2], cf[3]);
+        prio = fabsf(diff) + 1e-6f;  // |err| + 1e-6 (:76)
+        // update_priorities runs sequentially (:74-76): the last duplicate of an index wins
+        const uint32_t key = (uint32_t)id;
+        slot = (int)((key * 2654435761u) >> 23);
+        for (;;) {
+            const uint32_t old = atomicCAS(&sm.hkey[slot], kHashEmpty, key);
+            if (old == kHashEmpty || old == key) break;
+            slot = (slot + 1) & 511;
         }
-        // loss, max priority and the 4 bias gradients (sum_j coef_j) as block reductions
+        atomicMax(&sm.hwin[slot], t);
+    }
+    {
         float s = lossp, mp = prio;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -418,107 +458,185 @@ __global__ __launch_bounds__(256) void k_dqn(const pm_selfplay sp) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) cf[k] += __shfl_xor(cf[k], o);
         }
-        __syncthreads();
         if (lane == 0) {
-            red[wv][0] = s; red[wv][1] = mp;
+            sm.red[wv][1] = s; sm.red[wv][2] = mp;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) red2[wv][k] = cf[k];
+            for (int k = 0; k < 4; ++k) sm.red[wv][3 + k] = cf[k];
         }
-        __syncthreads();
-        if (act) {  // update_priorities: sequential order, the last duplicate wins (:74-76)
-            const int64_t mine = sidx[t];
-            bool last = true;
-#pragma unroll 8
-            for (int k = 0; k < B; ++k) last &= !(k > t && sidx[k] == mine);  // uniform k: broadcast reads
-            if (last) sp.prios[mine] = prio;
+    }
+    __syncthreads();
+    PM_STAMP(3);
+
+    // ---- phase 3: priority scatter; head gradients (16 waves x 16 samples, fixed-order combine)
+    float mpx = 0.f;
+    if (train) {
+        if (act && sm.hwin[slot] == t) {
+            sp.prios[id] = prio;
+            tree.leaf[id] = prio_pow(prio, (float)sp.alpha);
         }
+        mpx = sm.red[0][2];
+        for (int w = 1; w < 16; ++w) mpx = fmaxf(mpx, sm.red[w][2]);
         if (t == 0) {
-            c->last_loss = (((red[0][0] + red[1][0]) + red[2][0]) + red[3][0]) / (float)B;
-            const float mpx = fmaxf(fmaxf(red[0][1], red[1][1]), fmaxf(red[2][1], red[3][1]));
-            c->max_prio = fmaxf(c->max_prio, mpx);  // n > batch pushes of max_prio survive the scatter
+            float l = 0.f;
+            for (int w = 0; w < 16; ++w) l += sm.red[w][1];
+            c->last_loss = l / (float)B;
+            c->max_prio = fmaxf(cs.max_prio, mpx);  // n > batch pushes of max_prio survive the scatter
         }
-        // ---- head gradients: dL/dW_mu = sum_j coef_j h_j (one output per thread), dL/db_mu = sum_j
-        // coef_j; dL/dW_sigma = dL/dW_mu * eps with the update's noise (learn_heads[528..])
-        const float* ep = sp.learn_heads + 528;
-        {
-            const int row = t >> 6, col = t & 63;  // 256 weight outputs, row uniform per wave
+        const int col = t & 63;
+        float g[4] = {0.f, 0.f, 0.f, 0.f};
+        const int j0 = wv * 16, j1 = min(j0 + 16, B);
+        for (int j = j0; j < j1; ++j) {
+            const float4 k4 = *reinterpret_cast<const float4*>(sm.coef[j]);
+            const float h = sm.Hs[j][col];
+            g[0] = fmaf(k4.x, h, g[0]);
+            g[1] = fmaf(k4.y, h, g[1]);
+            g[2] = fmaf(k4.z, h, g[2]);
+            g[3] = fmaf(k4.w, h, g[3]);
+        }
+        // lw / hf are dead: the forward finished before the last barrier
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm.u.gpart[wv][r * 64 + col] = g[r];
+    }
+    const float max_prio_next = train ? fmaxf(cs.max_prio, mpx) : cs.max_prio;
+    __threadfence_block();  // readers are this workgroup: no agent-scope L2 writeback
+    __syncthreads();
+    PM_STAMP(4);
+
+    // ---- phase 4: gradients out; sum tree: sub-blocks of the scatter and of the next push range
+    const PushRange next = push_of(sp, (cs.pos + sp.n) % sp.cap, s_after, max_prio_next);
+    if (train) {
+        if (t < 256) {  // dL/dW_mu = sum_j coef_j h_j; dL/dW_sigma = dL/dW_mu * eps (the update's noise)
             float g = 0.f;
-#pragma unroll 8
-            for (int j = 0; j < B; ++j) g = fmaf(coef[j][row], Hs[j][col], g);
+#pragma unroll
+            for (int w = 0; w < 16; ++w) g += sm.u.gpart[w][t];
+            const int row = t >> 6, col = t & 63;
+            float* gs = sm.ap.g;
             if (row == 0) {
-                sp.grad[col] = g;                                                  // fc_V.weight_mu
-                sp.grad[65 + col] = g * ep[P_VWEP - PM_QNET_EPS_OFF + col];          // fc_V.weight_sigma
+                gs[col] = g;                                                   // fc_V.weight_mu
+                gs[65 + col] = g * sm.eps_tr[P_VWEP - PM_QNET_EPS_OFF + col];  // fc_V.weight_sigma
             } else {
                 const int a = row - 1;
-                sp.grad[130 + a * 64 + col] = g;                                   // fc_A.weight_mu
-                sp.grad[325 + a * 64 + col] = g * ep[P_AWEP - PM_QNET_EPS_OFF + a * 64 + col];  // fc_A.weight_sigma
+                gs[130 + a * 64 + col] = g;                                               // fc_A.weight_mu
+                gs[325 + a * 64 + col] = g * sm.eps_tr[P_AWEP - PM_QNET_EPS_OFF + a * 64 + col];  // fc_A.weight_sigma
             }
-        }
-        if (t < 4) {
-            const float g = ((red2[0][t] + red2[1][t]) + red2[2][t]) + red2[3][t];
-            if (t == 0) {
-                sp.grad[64] = g;                                                   // fc_V.bias_mu
-                sp.grad[129] = g * ep[P_VBEP - PM_QNET_EPS_OFF];                     // fc_V.bias_sigma
+        } else if (t < 260) {  // dL/db_mu = sum_j coef_j
+            const int k = t - 256;
+            float g = 0.f;
+            for (int w = 0; w < 16; ++w) g += sm.red[w][3 + k];
+            float* gs = sm.ap.g;
+            if (k == 0) {
+                gs[64] = g;                                             // fc_V.bias_mu
+                gs[129] = g * sm.eps_tr[P_VBEP - PM_QNET_EPS_OFF];      // fc_V.bias_sigma
             } else {
-                sp.grad[322 + t - 1] = g;                                          // fc_A.bias_mu
-                sp.grad[517 + t - 1] = g * ep[P_ABEP - PM_QNET_EPS_OFF + t - 1];     // fc_A.bias_sigma
+                gs[322 + k - 1] = g;                                    // fc_A.bias_mu
+                gs[517 + k - 1] = g * sm.eps_tr[P_ABEP - PM_QNET_EPS_OFF + k - 1];  // fc_A.bias_sigma
             }
         }
+        PM_STAMP(8); PM_STAMP_T(9, 960);
+        // level-1 nodes of the scatter: 4 lanes per sampled index (duplicates recompute the same
+        // node from the same leaves: identical values)
+        const int j = min(t >> 2, B - 1);
+        const int64_t sb = sm.sidx[j] / PER_SUB;
+        const double v = per_sub_sum4(tree.leaf, sb, next);
+        if ((t & 3) == 0) tree.sub[sb] = v;
+        PM_STAMP(10); PM_STAMP_T(11, 960);
     } else {
-        for (int k = t; k < kGradN; k += 256) sp.grad[k] = 0.f;
+        for (int k = t; k < kGradN; k += kLearn) sm.ap.g[k] = 0.f;
     }
+    if (t == 0) { sm.ap.g[kGradN] = (float)ep_fin; sm.ap.g[kGradN + 1] = train ? 1.f : 0.f; }
+    {   // level-1 nodes of the next push: wholly pushed ones are one constant; the <= 4 partially
+        // pushed ones at the segment ends are summed from the leaves by 4 lanes of wave 0 each
+        const RingNodes rn = ring_nodes(next, PER_SUB);
+        const double csub = per_sub_pushed_sum(next);
+        for (int64_t k = t; k < rn.count(); k += kLearn) {
+            const int64_t sb = rn.at(k);
+            if (per_sub_pushed(sb, next)) tree.sub[sb] = csub;
+        }
+        PM_STAMP(12); PM_STAMP_T(13, 960);
+        if (wv == 0) {
+            const int g = lane >> 2;
+            const bool ok = g < 4 && (g < 2 ? rn.na : rn.nb) > 0;
+            const int64_t sb = !ok ? 0 : g == 0 ? rn.a0 : g == 1 ? rn.a0 + rn.na - 1 : g == 2 ? 0 : rn.nb - 1;
+            const double v = per_sub_sum4(tree.leaf, sb, next);
+            if (ok && (lane & 3) == 0 && !per_sub_pushed(sb, next)) tree.sub[sb] = v;
+        }
+    }
+    PM_STAMP(14); PM_STAMP_T(15, 960);
+    __threadfence_block();  // readers are this workgroup: no agent-scope L2 writeback
+    __syncthreads();
+    PM_STAMP(5);
+    for (int k = t; k < kGradN + 2; k += kLearn) sp.grad[k] = sm.ap.g[k];
+    // ---- phase 5: level-2 nodes over the refreshed sub-blocks
+    if (act && sm.hwin[slot] == t) {
+        const int64_t ch = id / PER_CHUNK;
+        tree.chunk[ch] = per_chunk_sum(tree, ch);
+    }
+    {
+        const RingNodes rn = ring_nodes(next, PER_CHUNK);
+        for (int64_t k = t; k < rn.count(); k += kLearn) {
+            const int64_t ch = rn.at(k);
+            tree.chunk[ch] = per_chunk_sum(tree, ch);
+        }
+    }
+    PM_STAMP(6);
     if (sp.fuse_apply) {  // unsharded: no all-reduce between the gradient and the optimizer step
-        __threadfence_block();
         __syncthreads();
-        apply_update(sp, asm_);
+        apply_update(sp, sm.ap, cs);
     }
+    PM_STAMP(7);
 }
 
 // ------------------------------------------------------------------------------------ Adam + commit
-__global__ __launch_bounds__(1024) void k_adam(const pm_selfplay sp) {
+__global__ __launch_bounds__(kLearn) void k_adam(const pm_selfplay sp) {
     __shared__ ApplySmem sm;
-    apply_update(sp, sm);
+    const pm_ctrl cs = *sp.ctrl;
+    load_apply_inputs(sp, sm, true);
+    __syncthreads();
+    apply_update(sp, sm, cs);
 }
 
 // pm_selfplay_prepare: features + acting weights of the current step + next update's heads
-__global__ __launch_bounds__(256) void k_prepare(const pm_selfplay sp) {
+__global__ __launch_bounds__(kLearn) void k_prepare(const pm_selfplay sp) {
     __shared__ ApplySmem sm;
     write_feature_frags(sp.paramsB, sp.w_B);
-    for (int k = threadIdx.x; k < PM_QNET_NHEAD; k += blockDim.x) {
-        sm.hp[k] = sp.paramsB[PM_QNET_HEAD_OFF + k];
-        sm.tmu[k] = sp.paramsT[PM_QNET_HEAD_OFF + k];
-    }
+    load_apply_inputs(sp, sm, false);
     gen_both_noises(sp, sm, sp.ctrl->step, (uint64_t)sp.ctrl->train_steps + 1);
     __syncthreads();
     derive_weights(sp, sm);
 }
 
+namespace {
 int check(const pm_selfplay* sp) {
     PM_REQUIRE(sp && sp->ctrl && sp->trans && sp->prios && sp->per_work && sp->idx && sp->isw && sp->grad &&
                    sp->partials && sp->hfeat && sp->w_opp && sp->paramsB && sp->paramsT && sp->w_B && sp->adam_m &&
                    sp->adam_v && sp->opp && sp->ep_reward,
                PM_E_ARG, "pm_selfplay: null buffer");
-    PM_REQUIRE(sp->n > 0 && sp->batch >= 1 && sp->batch <= PM_MAX_BATCH && sp->n > sp->batch && sp->cap >= sp->n,
+    PM_REQUIRE(sp->n > 0 && sp->batch >= 1 && sp->batch <= PM_MAX_BATCH && sp->n > sp->batch && sp->cap >= sp->n &&
+                   sp->cap < 0xFFFFFFFFll,
                PM_E_SIZE, "pm_selfplay: n=%d batch=%d cap=%lld", sp->n, sp->batch, (long long)sp->cap);
     PM_REQUIRE(sp->n_pool >= 0 && sp->n_pool <= 4096 && sp->world >= 1, PM_E_SIZE, "pm_selfplay: n_pool/world");
     PM_REQUIRE(sp->obsA && sp->obsB && sp->aA && sp->aB && sp->learn_heads, PM_E_ARG, "pm_selfplay: null buffer");
     PM_REQUIRE(!sp->fuse_apply || sp->world == 1, PM_E_ARG, "pm_selfplay: fuse_apply needs world == 1");
     PM_REQUIRE(sp->chunk_A > 0 && sp->chunk_A <= kListMax && sp->chunk_P > 0 && sp->chunk_P <= kListMax, PM_E_SIZE,
                "pm_selfplay: chunk_A/chunk_P must be in [1, %d]", kListMax);
-    PM_REQUIRE(((((uintptr_t)sp->w_opp) | ((uintptr_t)sp->w_B)) & 15) == 0, PM_E_ARG, "pm_selfplay: weights alignment");
+    PM_REQUIRE(((((uintptr_t)sp->w_opp) | ((uintptr_t)sp->w_B) | ((uintptr_t)sp->prios) | ((uintptr_t)sp->per_work)) &
+                15) == 0,
+               PM_E_ARG, "pm_selfplay: w_opp / w_B / prios / per_work must be 16-byte aligned");
     PM_REQUIRE(sp->env.speed_scale_every > 0 && sp->target_update_interval > 0 && sp->beta_frames > 0, PM_E_ARG,
                "pm_selfplay: zero interval");
     return PM_OK;
 }
-
 }  // namespace
 
+// prepare: derived weights + a full rebuild of the PER sum tree (with the coming push substituted).
+// Call after init and after any host-side change of parameters, priorities or counters.
 extern "C" int pm_selfplay_prepare(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_prepare, dim3(1), dim3(256), 0, pm_stream(stream), *sp);
+    hipStream_t st = pm_stream(stream);
+    hipLaunchKernelGGL(k_prepare, dim3(1), dim3(kLearn), 0, st, *sp);
     PM_LAUNCHED("k_prepare");
-    return PM_OK;
+    return per_launch_build(sp->prios, sp->cap, (float)sp->alpha, sp->ctrl, sp->n, sp->per_work, st);
 }
 
 extern "C" int pm_selfplay_init(const pm_selfplay* sp, void* stream) {
@@ -534,7 +652,8 @@ extern "C" int pm_selfplay_act(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
     const ActGrid g{sp->n, sp->n_pool + 1, sp->chunk_A, sp->chunk_P, 1};
-    hipLaunchKernelGGL(k_act_sp, dim3(g.blocks()), dim3(kActBlock), 0, pm_stream(stream), *sp);
+    const int nsb = (sp->batch + 3) / 4;
+    hipLaunchKernelGGL(k_act_sp, dim3(nsb + g.blocks()), dim3(kActBlock), 0, pm_stream(stream), *sp);
     PM_LAUNCHED("k_act_sp");
     return PM_OK;
 }
@@ -555,17 +674,8 @@ extern "C" int pm_selfplay_rollout(const pm_selfplay* sp, void* stream) {
 extern "C" int pm_selfplay_learn(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
-    hipStream_t st = pm_stream(stream);
-    double* bsum = reinterpret_cast<double*>(sp->per_work);
-    const int npush = (sp->n + PER_CHUNK - 1) / PER_CHUNK + 2;
-    hipLaunchKernelGGL(k_per_refresh, dim3(npush + sp->batch), dim3(256), 0, st, *sp, bsum);
-    PM_LAUNCHED("k_per_refresh");
-    hipLaunchKernelGGL(k_sp_sample, dim3(pm_blocks(sp->batch, 4)), dim3(256), 0, st, *sp, bsum);
-    PM_LAUNCHED("k_sp_sample");
-    hipLaunchKernelGGL(k_dqn_fwd, dim3(pm_blocks(2 * sp->batch, 128)), dim3(256), 0, st, *sp);
-    PM_LAUNCHED("k_dqn_fwd");
-    hipLaunchKernelGGL(k_dqn, dim3(1), dim3(256), 0, st, *sp);
-    PM_LAUNCHED("k_dqn");
+    hipLaunchKernelGGL(k_learn, dim3(1), dim3(kLearn), 0, pm_stream(stream), *sp);
+    PM_LAUNCHED("k_learn");
     return PM_OK;
 }
 
@@ -573,7 +683,7 @@ extern "C" int pm_selfplay_apply(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
     if (sp->fuse_apply) return PM_OK;  // learn already applied (unsharded, fused)
-    hipLaunchKernelGGL(k_adam, dim3(1), dim3(1024), 0, pm_stream(stream), *sp);
+    hipLaunchKernelGGL(k_adam, dim3(1), dim3(kLearn), 0, pm_stream(stream), *sp);
     PM_LAUNCHED("k_adam");
     return PM_OK;
 }
@@ -583,3 +693,14 @@ extern "C" int pm_selfplay_step(const pm_selfplay* sp, void* stream) {
     if (!rc) rc = pm_selfplay_learn(sp, stream);
     return rc ? rc : pm_selfplay_apply(sp, stream);
 }
+
+#ifdef PM_DIAG
+extern "C" int pm_diag_read(uint64_t* out, int32_t n) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_buf), sizeof(uint64_t) * (n < 256 ? n : 256));
+    return e == hipSuccess ? 0 : (int)e;
+}
+extern "C" int pm_diag_clear(void) {
+    static const unsigned long long z[256] = {0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(pm_diag_buf), z, sizeof(z));
+}
+#endif

@@ -51,7 +51,9 @@ def test_entry_points_reject_bad_arguments_without_a_gpu():
     assert L.pm_qnet_fold(None, None, 7, 0, 0, None, None, 1, None) == -1
     assert b"mode" in L.pm_last_error()
     assert L.pm_selfplay_step(None, None) == -1
-    assert L.pm_per_work_bytes(1_000_000) == 7936  # 977 fp64 block sums, 256-byte rounded
+    # 977 fp64 chunk sums (1024 leaves) + 15625 fp64 sub-block sums (64 leaves) + 1e6 fp32 leaves,
+    # each 256-byte rounded
+    assert L.pm_per_work_bytes(1_000_000) == 7936 + 125184 + 4_000_000
     assert L.pm_env_reset(None, None, None, None, 0, 0, None, None, None, 0, None) == 0  # n = 0 is a no-op
 
 

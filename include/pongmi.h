@@ -191,7 +191,7 @@ typedef struct pm_selfplay {
     int64_t *partials;       /* [ceil(n/256)][8] per-block episode counters of the rollout          */
     float *obsA, *obsB;      /* [n][7] observations of the current step (written by the env kernel) */
     int8_t *aA, *aB;         /* [n] actions of the current step (written by the act kernel)        */
-    float *hfeat;            /* [batch][16] last update's Q_B(s) 0..2, Q_B(s') 4..6, Q_T(s') 8..10 */
+    float *hfeat;            /* [batch][80] batch forward scratch: features of s, Q values at 64.. */
     float *learn_heads;      /* [3][264] next update's modelB heads (fresh noise) and targetB heads in
                                 MFMA fragment order, and that noise (epsilon-buffer layout)        */
     pm_ctrl *ctrl;

@@ -24,11 +24,32 @@ static __device__ unsigned long long pm_diag_buf[256];
     do {                                                                               \
         if (threadIdx.x == 0) pm_diag_buf[(slot)] = __builtin_amdgcn_s_memrealtime();  \
     } while (0)
+// per-block timeline of one kernel: [0] begin, [1] ready (inputs staged), [2] end (all waves),
+// [3] placement: CU id (__smid) | XCC id << 16, [4..7] kernel-specific mid points
+static __device__ unsigned long long pm_diag_blk[8][4096];
+#define PM_BLK_END()                                                                              \
+    do {                                                                                          \
+        __syncthreads();                                                                          \
+        PM_BLK(2);                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                                                \
+            pm_diag_blk[3][blockIdx.x] =                                                          \
+                (unsigned long long)__smid() | ((unsigned long long)(__builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15) << 16); \
+    } while (0)
+#define PM_BLK(k)                                                                                  \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) pm_diag_blk[(k)][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 #define PM_STAMP_T(slot, tid)                                                                            \
     do {                                                                                                 \
         if (threadIdx.x == (tid) && blockIdx.x == 0) pm_diag_buf[(slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
+#define PM_BLK(k) \
+    do {          \
+    } while (0)
+#define PM_BLK_END() \
+    do {             \
+    } while (0)
 #define PM_STAMP_T(slot, tid) \
     do {                      \
     } while (0)

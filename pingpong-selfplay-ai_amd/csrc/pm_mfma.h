@@ -18,6 +18,7 @@
 namespace pm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;  // LDS destination of global_load_lds
 
 constexpr int PLAIN = 4936;  // plain effective weights (4932) padded to 16 B
 // fragment image (floats, from w + PLAIN)
@@ -70,37 +71,71 @@ __device__ __forceinline__ void write_head_frags(const float* heads, float* __re
 }
 
 // ----------------------------------------------------------------------------- block helpers
-// Stage one net's fragment image (F_SIZE floats) into LDS. Block-wide; caller syncs.
-__device__ __forceinline__ void stage_frags(const float* __restrict__ w, float* lw) {
+constexpr int kLwChunks = (F_SIZE / 4 + 63) / 64;  // 1 KB chunks of the fragment image (20)
+constexpr int kLwFloats = kLwChunks * 256;          // LDS image size: whole 1 KB wave chunks
+
+// Stage one net's fragment image global -> LDS directly (global_load_lds: 1 KB per wave
+// instruction, no registers, no wait until the caller's barrier). `lw` holds kLwFloats floats.
+// Chunk order starts at `rot` so concurrent blocks reading the same image spread over L2 channels.
+// Block-wide; the caller's __syncthreads() (which waits vmcnt(0)) publishes the image.
+__device__ __forceinline__ void stage_frags_lds(const float* __restrict__ w, float* lw, int rot) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const float4* src = reinterpret_cast<const float4*>(w + PLAIN);
-    float4* dst = reinterpret_cast<float4*>(lw);
-    for (int k = threadIdx.x; k < F_SIZE / 4; k += blockDim.x) dst[k] = src[k];
+    float4* lw4 = reinterpret_cast<float4*>(lw);
+    rot %= kLwChunks;
+    for (int c0 = wv; c0 < kLwChunks; c0 += nw) {
+        const int c = c0 + rot < kLwChunks ? c0 + rot : c0 + rot - kLwChunks;
+        const int k = min(c * 64 + lane, F_SIZE / 4 - 1);  // the pad tail re-reads the last float4
+        __builtin_amdgcn_global_load_lds((const void*)(src + k), (lds_void*)(lw4 + c * 64), 16, 0, 0);
+    }
 }
 
-// Append the arenas i in [lo, hi) with id[i] == net to the LDS list (order unspecified: every row
-// is computed independently, so the tile composition never changes a result). All of a thread's
-// ids are loaded before the first ballot, so a chunk costs one memory round trip. Block-wide;
-// hi - lo <= kListMax (16 ids per thread at 256 threads).
-__device__ __forceinline__ void compact_rows(const int32_t* __restrict__ id, int net, int lo, int hi, int* list,
-                                             int* count) {
-    const int lane = threadIdx.x & 63, nt = blockDim.x;
-    int ids[16];
+// Compaction of the arenas i in [lo, hi) with id[i] == net, in ascending order, into an LDS list.
+// Thread t owns ids [lo + 16 t, lo + 16 t + 16): compact_load issues its loads (four int4 when
+// aligned; the caller overlaps them with other loads), compact_scan counts matches and places them
+// with one block-wide exclusive scan. hi - lo <= 16 * blockDim.x (kListMax at 256 threads);
+// `wtot` = LDS scratch of blockDim.x / 64 ints; *count = total. Block-wide.
+__device__ __forceinline__ void compact_load(const int32_t* __restrict__ id, int lo, int hi, int (&v)[16]) {
+    const int base = lo + 16 * (int)threadIdx.x;
+    if (base + 16 <= hi && (reinterpret_cast<uintptr_t>(id + base) & 15) == 0) {
+        const int4* p4 = reinterpret_cast<const int4*>(id + base);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int i = lo + r * nt + (int)threadIdx.x;
-        ids[r] = i < hi ? id[i] : -1;
-    }
+        for (int q = 0; q < 4; ++q) {
+            const int4 x = p4[q];
+            v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+        }
+    } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        if (lo + r * nt >= hi) break;  // block-uniform
-        const int i = lo + r * nt + (int)threadIdx.x;
-        const bool m = ids[r] == net;
-        const unsigned long long b = __ballot(m);
-        int pos = 0;
-        if (lane == 0 && b) pos = atomicAdd(count, __popcll(b));
-        pos = __shfl(pos, 0);
-        if (m) list[pos + __popcll(b & ((1ull << lane) - 1ull))] = i;
+        for (int r = 0; r < 16; ++r) v[r] = base + r < hi ? id[base + r] : -1;
     }
+}
+__device__ __forceinline__ void compact_scan(const int (&v)[16], int net, int lo, int* list, int* count, int* wtot) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = blockDim.x >> 6;
+    const int base = lo + 16 * t;
+    unsigned mask = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mask |= (v[r] == net ? 1u : 0u) << r;
+    const int c = __popc(mask);
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    int off = 0, total = 0;
+    for (int w = 0; w < nw; ++w) {
+        off += w < wv ? wtot[w] : 0;
+        total += wtot[w];
+    }
+    int p = off + incl - c;
+    while (mask) {
+        const int r = __ffs(mask) - 1;
+        mask &= mask - 1;
+        list[p++] = base + r;
+    }
+    if (t == 0) *count = total;
 }
 
 struct TileOut {
@@ -238,9 +273,21 @@ __device__ __forceinline__ void run_tiles(const float* lw, const float* __restri
             tile_inputs(obs + (size_t)arena_n * 7, h, xn);
         }
         f32x16 c2[2];
+#ifdef PM_DIAG
+        if (tl == wave) {  // first tile: operands in registers
+            __builtin_amdgcn_s_waitcnt(0);
+            PM_BLK(5);
+        }
+#endif
         tile_hidden(lw, xs, lane, c2);
+#ifdef PM_DIAG
+        if (tl == wave) PM_BLK(6);
+#endif
         float q[3];
         tile_heads(lw + F_H, c2, lane, q);
+#ifdef PM_DIAG
+        if (tl == wave) PM_BLK(7);
+#endif
         int a = argmax3(q);
         if (out.eps >= 0.0) {  // random.random() < eps ? randint(0,2) : argmax (train_iterative.py:126-130)
             const U4 rr = philox64((uint32_t)arena, TAG_ACT, out.ctr, out.seed);
@@ -261,12 +308,14 @@ __device__ __forceinline__ void run_tiles(const float* lw, const float* __restri
 }
 
 // ----------------------------------------------------------------------------- grouped act grid
-// Block -> work: [0, nB) chunks of 256 arenas for side B (one net: w_B); then side A: net 0 in
+// Block -> work: [0, nB) chunks of kChunkB arenas for side B (one net: w_B); then side A: net 0 in
 // chunks of chunk0 arenas, nets 1..n_opp-1 in chunks of chunk1 arenas each, rows compacted by
 // opponent id so every tile has uniform weights.
+constexpr int kChunkB = 128;  // side-B rows per block: 4 tiles, one per wave (A-side chunks aim at ~96-128 rows)
+
 struct ActGrid {
     int n, n_opp, chunk0, chunk1, side_b;
-    __host__ __device__ int nb() const { return side_b ? (n + 255) / 256 : 0; }
+    __host__ __device__ int nb() const { return side_b ? (n + kChunkB - 1) / kChunkB : 0; }
     __host__ __device__ int na0() const { return (n + chunk0 - 1) / chunk0; }
     __host__ __device__ int na1() const { return (n + chunk1 - 1) / chunk1; }
     __host__ __device__ int blocks() const { return nb() + na0() + (n_opp - 1) * na1(); }
@@ -276,13 +325,15 @@ constexpr int kActBlock = 256;
 constexpr int kListMax = 4096;  // max chunk size
 
 struct ActShared {
-    float lw[F_SIZE];
+    float lw[kLwFloats];  // fragment image, padded to whole 1 KB wave chunks
     int list[kListMax];
     int count;
+    int wtot[kActBlock / 64];
 };
 
-// Block-wide body of the grouped act kernel for grid block b. side B: eps-greedy on obsB with w_B;
-// side A: greedy on obsA with w_opp[net]. opp == nullptr -> every arena plays net 0.
+// Block-wide body of the grouped act kernel for grid block b (blockDim.x == kActBlock). side B:
+// eps-greedy on obsB with w_B; side A: greedy on obsA with w_opp[net]. opp == nullptr -> every
+// arena plays net 0.
 __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const float* __restrict__ w_opp,
                                           const int32_t* __restrict__ opp, const float* __restrict__ w_B,
                                           const float* __restrict__ obsA, const float* __restrict__ obsB,
@@ -293,7 +344,7 @@ __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const
     int net, lo, hi;
     bool compact;
     if (b < g.nb()) {
-        w = w_B; obs = obsB; out = outB; net = -1; lo = b * 256; hi = min(lo + 256, g.n); compact = false;
+        w = w_B; obs = obsB; out = outB; net = -1; lo = b * kChunkB; hi = min(lo + kChunkB, g.n); compact = false;
     } else {
         b -= g.nb();
         if (b < g.na0()) { net = 0; lo = b * g.chunk0; hi = min(lo + g.chunk0, g.n); }
@@ -302,12 +353,25 @@ __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const
         compact = opp != nullptr;
         if (!compact && net != 0) return;  // block-uniform
     }
-    stage_frags(w, sh.lw);
-    if (threadIdx.x == 0) sh.count = compact ? 0 : hi - lo;
+    // prologue: the fragment image (20 KB) goes global -> LDS directly (global_load_lds, 1 KB per
+    // wave instruction, no registers) while this block's opponent ids load into registers: one
+    // memory round trip. Each block starts at a different 1 KB chunk so concurrent blocks reading
+    // the same image spread over L2 channels. Staging / compaction run at raised priority (their
+    // VALU/LDS work loses arbitration to co-resident waves' f32 MFMA streams), the tiles at normal.
+    __builtin_amdgcn_s_setprio(2);
+    stage_frags_lds(w, sh.lw, b);
+    int ids[16];
+    if (compact) compact_load(opp, lo, hi, ids);
+    PM_BLK(4);
+    if (compact) {
+        compact_scan(ids, net, lo, sh.list, &sh.count, sh.wtot);
+    } else {
+        if (threadIdx.x == 0) sh.count = hi - lo;
+        for (int k = threadIdx.x; k < hi - lo; k += blockDim.x) sh.list[k] = lo + k;
+    }
     __syncthreads();
-    if (compact) compact_rows(opp, net, lo, hi, sh.list, &sh.count);
-    else for (int k = threadIdx.x; k < hi - lo; k += blockDim.x) sh.list[k] = lo + k;
-    __syncthreads();
+    PM_BLK(1);
+    __builtin_amdgcn_s_setprio(0);
     run_tiles(sh.lw, obs, sh.list, sh.count, out);
 }
 

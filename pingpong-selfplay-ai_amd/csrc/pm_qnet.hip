@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void k_fold(const float* params, float* params
     write_head_frags(heads, wb);
 }
 
-__global__ __launch_bounds__(kActBlock, 2) void k_act(ActGrid g, const float* __restrict__ w_opp,
+__global__ __launch_bounds__(kActBlock, 4) void k_act(ActGrid g, const float* __restrict__ w_opp,
                                                    const int32_t* __restrict__ opp, const float* __restrict__ w_B,
                                                    const float* __restrict__ obsA, const float* __restrict__ obsB,
                                                    TileOut outA, TileOut outB, const double* __restrict__ eps_dev,

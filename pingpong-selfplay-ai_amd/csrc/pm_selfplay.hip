@@ -62,13 +62,15 @@ __device__ __forceinline__ void sample_wave(const pm_selfplay& sp, int j) {
 // Both players act (train_iterative.py:240-241) on the matrix cores: ActGrid blocks, modelB tiles
 // with epsilon-greedy, opponent tiles grouped by net (modelA / pool) so weights are tile-uniform.
 // Blocks [0, ceil(batch/4)) sample the update's batch instead (latency-bound, hidden under the act).
-__global__ __launch_bounds__(kActBlock, 2) void k_act_sp(const pm_selfplay sp) {
+__global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp) {
     __shared__ __attribute__((aligned(16))) ActShared sh;
+    PM_BLK(0);
     const int nsb = (sp.batch + 3) / 4;
     if ((int)blockIdx.x < nsb) {
         PM_STAMP(64);
         sample_wave(sp, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
         PM_STAMP(65);
+        PM_BLK_END();
         return;
     }
     if ((int)blockIdx.x == nsb) PM_STAMP_ANY(70);
@@ -77,11 +79,74 @@ __global__ __launch_bounds__(kActBlock, 2) void k_act_sp(const pm_selfplay sp) {
     const TileOut outB{sp.aB, nullptr, sp.ctrl->epsilon, sp.seed_env, sp.ctrl->step};
     act_block(sh, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, sp.w_B, sp.obsA, sp.obsB, outA, outB,
               (int)blockIdx.x - nsb);
+    PM_BLK_END();
+}
+
+// The three QNet evaluations of train_step (:152-155) for one 32-row tile of the sampled batch on
+// the matrix cores: row r < B is s of sample r, row r >= B is s' of sample r - B (the same replay
+// row). This lane's row: trans row `id`, `nxt` selects s'. Returns the pre-ReLU features (MFMA
+// accumulator layout) and Q_B / Q_T of the row (heads from learn_heads, staged in hf0 / hf1).
+// Every output column depends only on its own row, so which tile or kernel computes a row never
+// changes a bit of it.
+__device__ __forceinline__ void batch_row_fwd(const pm_selfplay& sp, const float* lw, const float* hf0, const float* hf1,
+                                              int64_t id, bool nxt, int lane, f32x16 (&c2)[2], float (&qb)[3],
+                                              float (&qt)[3]) {
+    float xs[4];
+    tile_inputs(sp.trans + id * PM_TRANS_F + (nxt ? 8 : 0), lane >> 5, xs);
+    tile_hidden(lw, xs, lane, c2);
+    tile_heads(hf0, c2, lane, qb);
+    tile_heads(hf1, c2, lane, qt);
+}
+
+// Rows of the batch whose replay row is NOT in this step's push range are stable while k_env runs:
+// k_env's last ceil(2B/128) blocks compute them (one tile per wave) into hfeat [B][80] (features
+// of s | Q_B(s) 0..2, Q_B(s') 4..6, Q_T(s') 8..10 at 64..); k_learn computes the rest.
+__device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f) {
+    __shared__ __attribute__((aligned(16))) float lw[kLwFloats];
+    __shared__ __attribute__((aligned(16))) float hf[2][264];
+    if (!learner_active(sp)) return;  // block-uniform
+    stage_frags_lds(sp.w_B, lw, f * 5);
+    for (int k = threadIdx.x; k < 2 * 264; k += blockDim.x) hf[k / 264][k % 264] = sp.learn_heads[k];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, B = sp.batch;
+    const int r0 = f * 128 + (int)(threadIdx.x >> 6) * 32;
+    if (r0 >= 2 * B) return;  // wave-uniform
+    const int r = min(r0 + (lane & 31), 2 * B - 1);
+    const bool nxt = r >= B;
+    const int j = nxt ? r - B : r;
+    const int64_t id = sp.idx[j];
+    const pm_ctrl* c = sp.ctrl;
+    const bool mine = r0 + (lane & 31) < 2 * B && !push_of(sp, c->pos, c->size, c->max_prio).covers(id);
+    f32x16 c2[2];
+    float qb[3], qt[3];
+    batch_row_fwd(sp, lw, hf[0], hf[1], id, nxt, lane, c2, qb, qt);
+    if (!mine) return;
+    float* row = sp.hfeat + (size_t)j * 80;
+    const int h = lane >> 5;
+    if (!nxt) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) row[32 * t + rho(q) + 4 * h] = fmaxf(c2[t][q], 0.f);
+    }
+    if (h == 0) {
+        if (!nxt) {
+            row[64] = qb[0]; row[65] = qb[1]; row[66] = qb[2];
+        } else {
+            row[68] = qb[0]; row[69] = qb[1]; row[70] = qb[2];
+            row[72] = qt[0]; row[73] = qt[1]; row[74] = qt[2];
+        }
+    }
 }
 
 // env.step (:242) + memory.push (:243) + episode bookkeeping (:245-249) + next opponent (:235-236)
 // and env.reset (:238) for finished arenas; writes next step's observations. HBM-bound.
 __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
+    const int nenv = (sp.n + kBlock - 1) / kBlock;
+    if ((int)blockIdx.x >= nenv) {
+        env_fwd_block(sp, (int)blockIdx.x - nenv);
+        return;
+    }
     __shared__ float lds[kBlock][7];
     __shared__ long long red[kBlock / 64][6];
     const int i0 = blockIdx.x * kBlock;
@@ -287,7 +352,7 @@ __device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& s
 struct LearnSmem {
     union {
         struct {  // forward phase
-            float lw[F_SIZE];  // modelB.features fragments (== targetB.features: frozen)
+            float lw[kLwFloats];  // modelB.features fragments (== targetB.features: frozen)
             float hf[2][264];  // modelB (update noise) / targetB (mu) head fragments
         } f;
         float gpart[16][256];  // gradient phase: per-wave partial sums
@@ -301,43 +366,10 @@ struct LearnSmem {
     int hwin[512];
     float red[16][8];
     long long cnt[16][6];
+    int plist[PM_MAX_BATCH];     // samples whose row is in this step's push range, per wave slot
+    int pcnt[16];
     ApplySmem ap;
 };
-
-// One tile of 32 rows of the batch forward: rows [0, B) are s, [B, 2B) are s'.
-__device__ __forceinline__ void learn_tile(const pm_selfplay& sp, LearnSmem& sm, int tile, int lane) {
-    const int h = lane >> 5, col = lane & 31, B = sp.batch;
-    const int g = tile * 32 + col;
-    const bool valid = g < 2 * B;
-    const int gg = valid ? g : 2 * B - 1;
-    const bool nxt = gg >= B;
-    const int j = nxt ? gg - B : gg;
-    float xs[4];
-    tile_inputs(sp.trans + sm.sidx[j] * PM_TRANS_F + (nxt ? 8 : 0), h, xs);
-    f32x16 c2[2];
-    tile_hidden(sm.u.f.lw, xs, lane, c2);
-    float qb[3], qt[3];
-    tile_heads(sm.u.f.hf[0], c2, lane, qb);
-    tile_heads(sm.u.f.hf[1], c2, lane, qt);
-    if (valid && !nxt) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sm.Hs[j][32 * t + rho(r) + 4 * h] = fmaxf(c2[t][r], 0.f);
-    }
-    if (valid && h == 0) {
-        float* q = sp.hfeat + (size_t)j * 16;  // inspection copy
-        if (!nxt) {
-            sm.qv[j][0] = qb[0]; sm.qv[j][1] = qb[1]; sm.qv[j][2] = qb[2];
-            q[0] = qb[0]; q[1] = qb[1]; q[2] = qb[2];
-        } else {
-            sm.qv[j][4] = qb[0]; sm.qv[j][5] = qb[1]; sm.qv[j][6] = qb[2];
-            sm.qv[j][8] = qt[0]; sm.qv[j][9] = qt[1]; sm.qv[j][10] = qt[2];
-            q[4] = qb[0]; q[5] = qb[1]; q[6] = qb[2];
-            q[8] = qt[0]; q[9] = qt[1]; q[10] = qt[2];
-        }
-    }
-}
 
 // train_step (:134-168) for the batch k_act_sp sampled, plus the episode counters of the rollout and
 // the sum-tree refresh. Single workgroup of 1024 threads; global loads are issued up front.
@@ -364,7 +396,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
     const float wraw = act ? sp.isw[t] : 0.f;
     const int64_t id = act ? sp.idx[t] : 0;
     if (train) {
-        stage_frags(sp.w_B, sm.u.f.lw);
+        stage_frags_lds(sp.w_B, sm.u.f.lw, 0);
         for (int k = t; k < 2 * 264; k += kLearn) sm.u.f.hf[k / 264][k % 264] = sp.learn_heads[k];
         for (int k = t; k < 260; k += kLearn) {  // the update's noise, left in modelB's buffers by reset_noise
             const float e = sp.learn_heads[528 + k];
@@ -374,7 +406,32 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
     }
     if (sp.fuse_apply) load_apply_inputs(sp, sm.ap, false);
     for (int k = t; k < 512; k += kLearn) { sm.hkey[k] = kHashEmpty; sm.hwin[k] = -1; }
+    // the rows k_env's forward blocks computed (hfeat [B][80]): a quarter of sample t/4 per thread
+    const int hj = t >> 2, hq = (t & 3) * 20;
+    float hv[20];
+    if (train && hj < B) {
+        const float4* src = reinterpret_cast<const float4*>(sp.hfeat + (size_t)hj * 80 + hq);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const float4 v = src[k];
+            hv[4 * k] = v.x; hv[4 * k + 1] = v.y; hv[4 * k + 2] = v.z; hv[4 * k + 3] = v.w;
+        }
+    }
     if (act) sm.sidx[t] = id;
+    {   // samples whose replay row k_env was writing: computed here (phase 1)
+        const bool ip = act && push_of(sp, cs.pos, cs.size, cs.max_prio).covers(id);
+        const unsigned long long m = __ballot(ip);
+        if (ip) sm.plist[wv * 64 + __popcll(m & ((1ull << lane) - 1ull))] = t;
+        if (lane == 0) sm.pcnt[wv] = __popcll(m);
+    }
+    if (train && hj < B) {
+#pragma unroll
+        for (int k = 0; k < 20; ++k) {
+            const int f = hq + k;
+            if (f < 64) sm.Hs[hj][f] = hv[k];
+            else if (f < 76) sm.qv[hj][f - 64] = hv[k];
+        }
+    }
     float rwd = 0.f;
     int bits = 0;
     if (act) {
@@ -404,7 +461,39 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][t];
         sm.cnt[0][t] = s;  // read after the next barrier
     }
-    if (train && wv * 32 < 2 * B) learn_tile(sp, sm, wv, lane);
+    if (train) {  // rows in the push range: one 32-row tile per wave (s rows then s' rows)
+        int pre[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) pre[w + 1] = pre[w] + sm.pcnt[w];  // B <= 256: waves 0..3
+        const int np = pre[4];
+        if (wv * 32 < 2 * np) {  // wave-uniform
+            const int rr = min(wv * 32 + (lane & 31), 2 * np - 1);
+            const bool nxt = rr >= np;
+            const int k = nxt ? rr - np : rr;
+            const int w = k >= pre[3] ? 3 : k >= pre[2] ? 2 : k >= pre[1] ? 1 : 0;
+            const int j = sm.plist[w * 64 + k - pre[w]];
+            f32x16 c2[2];
+            float qb[3], qt[3];
+            batch_row_fwd(sp, sm.u.f.lw, sm.u.f.hf[0], sm.u.f.hf[1], sm.sidx[j], nxt, lane, c2, qb, qt);
+            if (wv * 32 + (lane & 31) < 2 * np) {
+                const int h = lane >> 5;
+                if (!nxt) {
+#pragma unroll
+                    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) sm.Hs[j][32 * tt + rho(r) + 4 * h] = fmaxf(c2[tt][r], 0.f);
+                }
+                if (h == 0) {
+                    if (!nxt) {
+                        sm.qv[j][0] = qb[0]; sm.qv[j][1] = qb[1]; sm.qv[j][2] = qb[2];
+                    } else {
+                        sm.qv[j][4] = qb[0]; sm.qv[j][5] = qb[1]; sm.qv[j][6] = qb[2];
+                        sm.qv[j][8] = qt[0]; sm.qv[j][9] = qt[1]; sm.qv[j][10] = qt[2];
+                    }
+                }
+            }
+        }
+    }
     float wmax = sm.red[0][0];
     for (int w = 1; w < 16; ++w) wmax = fmaxf(wmax, sm.red[w][0]);
     __syncthreads();
@@ -661,7 +750,8 @@ extern "C" int pm_selfplay_act(const pm_selfplay* sp, void* stream) {
 extern "C" int pm_selfplay_env(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_env, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *sp);
+    const unsigned nfwd = pm_blocks(2 * sp->batch, 128);  // batch rows not in the push range (env_fwd_block)
+    hipLaunchKernelGGL(k_env, dim3(pm_blocks(sp->n, kBlock) + nfwd), dim3(kBlock), 0, pm_stream(stream), *sp);
     PM_LAUNCHED("k_env");
     return PM_OK;
 }
@@ -698,6 +788,9 @@ extern "C" int pm_selfplay_step(const pm_selfplay* sp, void* stream) {
 extern "C" int pm_diag_read(uint64_t* out, int32_t n) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_buf), sizeof(uint64_t) * (n < 256 ? n : 256));
     return e == hipSuccess ? 0 : (int)e;
+}
+extern "C" int pm_diag_read_blk(uint64_t* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_blk), sizeof(uint64_t) * 8 * 4096);
 }
 extern "C" int pm_diag_clear(void) {
     static const unsigned long long z[256] = {0};

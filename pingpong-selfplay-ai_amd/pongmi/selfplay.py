@@ -83,7 +83,7 @@ class SelfPlayLearner:
         self.isw = torch.zeros(self.batch, **f32)
         self.grad = torch.zeros(PM_QNET_NHEAD + 8, **f32)
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
-        self.hfeat = torch.zeros((self.batch, 16), **f32)
+        self.hfeat = torch.zeros((self.batch, 80), **f32)
         self.learn_heads = torch.zeros(3 * 264, **f32)
         self.obsA = torch.zeros((n, 7), **f32)
         self.obsB = torch.zeros((n, 7), **f32)

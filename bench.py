@@ -9,11 +9,14 @@ push + proportional sample, double-DQN update with target net, Adam), weak-scale
 
 A step = one vector step: every arena on every rank advances one env step and every rank runs one
 PER update of batch 256. value = total env-steps (all ranks) / max-over-ranks wall time of K steps.
-Rank 0 prints one JSON line. Also reported (rank 0, N=1 only):
-  roofline      the dominant kernel (k_rollout: 2 QNet forwards + env tick per arena) timed with
-                HIP events on the stream it runs on, FP32 FLOP/s vs the 157.3 TF FP32 peak
-  env_step_roofline  K1 (pm_env_step) alone at the same n: algorithmic 203 B / env-step vs 8 TB/s
-  cpu_baseline  the oracle's CPU port of the same vector step, 1 core, bounded sample
+Rank 0 prints one JSON line. Also reported:
+  roofline      the dominant kernel, k_act_sp (both players' QNet forwards on the matrix cores, plus
+                the PER sample blocks), timed with HIP events on the stream it runs on: FP32 FLOP/s
+                vs the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per launch from the
+                committed counter profile (profiles/r1_pmc.json, same workload), null without it
+  env_roofline  k_env (env tick + replay push + bookkeeping, 282 algorithmic B / env-step) vs 8 TB/s
+  env_step_roofline  K1 (pm_env_step) alone at the same n: 203 B / env-step vs 8 TB/s (N=1 only)
+  cpu_baseline  the oracle's CPU port of the same vector step, 1 core, bounded sample (N=1 only)
 """
 import argparse
 import json
@@ -35,10 +38,20 @@ ENV_KW = dict(paddle_width=0.2, paddle_speed=0.03, max_score=3, enable_spin=True
 FLOP_PER_ARENA = 2 * 2 * (7 * 64 + 64 * 64 + 64 * 4)  # two QNet forwards (MACs x 2)
 ENV_BYTES = 203  # K1 algorithmic bytes per env-step
 # k_env (self-play tick): state 7x8 + 3x4 read and written (136), actions 2, opp 4 + ep_reward 4 read and
-# written (16), replay row 64 + priority 4 written, next observations 2x28 written
-SP_ENV_BYTES = 136 + 2 + 16 + 68 + 56
+# written (16), replay row 64 + priority 4 + PER leaf 4 written, next observations 2x28 written
+SP_ENV_BYTES = 136 + 2 + 16 + 72 + 56
 PEAK_FP32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 counter profile, or None."""
+    path = os.path.join(ROOT, "profiles", "r1_pmc.json")
+    try:
+        with open(path) as fh:
+            return json.load(fh)["kernels"][kernel]["hbm_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def synthetic_qnet(seed):
@@ -179,10 +192,11 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "k_act_sp", "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; "
                                                                           "dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": pmc_traffic("k_act_sp"),
                          "avg_us": round(act_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
             "env_roofline": {"bound": "hbm", "kernel": "k_env", "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS,
-                             "unit": "GB/s", "frac": round(env_gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                             "unit": "GB/s", "frac": round(env_gbs / PEAK_HBM_GBS, 4),
+                             "traffic": pmc_traffic("k_env"),
                              "avg_us": round(env_s * 1e6, 2), "bytes_per_env_step": SP_ENV_BYTES},
             "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
                         "last_loss": c["last_loss"]},

@@ -6,7 +6,7 @@ TAG=${1:-r1}
 STEPS=${STEPS:-40}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-RX='k_(act_sp|env|dqn|dqn_fwd|sp_sample|per_refresh|prepare|env_step|act)\b'
+
 run() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv \

@@ -11,7 +11,8 @@ A step = one vector step: every arena on every rank advances one env step and ev
 PER update of batch 256. value = total env-steps (all ranks) / max-over-ranks wall time of K steps.
 Rank 0 prints one JSON line. Also reported:
   roofline      the dominant kernel, k_act_sp (both players' QNet forwards on the matrix cores, plus
-                the PER sample blocks), timed with HIP events on the stream it runs on: FP32 FLOP/s
+                the PER sample blocks), timed with HIP events on the stream it runs on, around every
+                10th step of the timed region (the others run the uninstrumented step): FP32 FLOP/s
                 vs the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per launch from the
                 committed counter profile (profiles/r1_pmc.json, same workload), null without it
   env_roofline  k_env (env tick + replay push + bookkeeping, 282 algorithmic B / env-step) vs 8 TB/s
@@ -41,6 +42,7 @@ ENV_BYTES = 203  # K1 algorithmic bytes per env-step
 # written (16), replay row 64 + priority 4 + PER leaf 4 written, next observations 2x28 written
 SP_ENV_BYTES = 136 + 2 + 16 + 72 + 56
 PEAK_FP32_TFLOPS = 157.3
+INSTR = 10  # one instrumented (event-bracketed) step per INSTR timed steps
 PEAK_HBM_GBS = 8000.0
 
 
@@ -138,14 +140,20 @@ def main():
                         epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce)
 
     def one_step(ev=None):
-        if ev is not None:
-            ev[0].record()
+        if ev is None:  # the production path: one C call (three launches) per vector step
+            if dist is None:
+                L.step()
+            else:
+                L.rollout()
+                L.learn()
+                dist.all_reduce(L.grad)
+                L.apply()
+            return
+        ev[0].record()  # instrumented step: the same kernels, bracketed for the per-kernel rooflines
         L.act()
-        if ev is not None:
-            ev[1].record()
+        ev[1].record()
         L.env_step()
-        if ev is not None:
-            ev[2].record()
+        ev[2].record()
         L.learn()
         if dist is not None:
             dist.all_reduce(L.grad)
@@ -154,13 +162,16 @@ def main():
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
-    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    # every INSTR-th step of the timed region carries HIP events around k_act_sp and k_env (an event
+    # marker costs GPU time on ROCm; bracketing every step would slow the loop ~15 %)
+    inst = set(range(0, args.steps, INSTR))
+    evs = {k: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for k in inst}
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(evs[k])
+        one_step(evs.get(k))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -169,8 +180,8 @@ def main():
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    act_s = sum(e[0].elapsed_time(e[1]) for e in evs) * 1e-3 / args.steps
-    env_s = sum(e[1].elapsed_time(e[2]) for e in evs) * 1e-3 / args.steps
+    act_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
+    env_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)
     c = L.counters()
 
     if rank == 0:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 1
+#define PM_ABI_VERSION 2
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -195,8 +195,12 @@ typedef struct pm_selfplay {
     float *learn_heads;      /* [3][264] next update's modelB heads (fresh noise) and targetB heads in
                                 MFMA fragment order, and that noise (epsilon-buffer layout)        */
     pm_ctrl *ctrl;
+    int32_t *opp_list;       /* [n] per 256-arena block: its arenas grouped by opponent net (ascending)  */
+    int32_t *opp_cnt;        /* [ceil(n/256)][n_pool+1] (offset << 16 | count) of each net in the block;
+                                written by the env kernel (and init) for the next act, n_pool < 64   */
     int32_t n, n_pool, batch, world;
-    int32_t chunk_A, chunk_P;  /* act grouping: arenas per compaction chunk for modelA / pool nets */
+    int32_t chunk_A, chunk_P;  /* act grouping: arenas per chunk for modelA / pool nets (multiples of
+                                  256 use opp_list; others compact opp in the act kernel)        */
     int32_t fuse_apply;        /* world == 1: learn also applies (pm_selfplay_apply is then a no-op) */
     int32_t _pad0;
     int64_t cap;

@@ -23,7 +23,8 @@ typedef __attribute__((address_space(3))) void lds_void;  // LDS destination of 
 constexpr int PLAIN = 4936;  // plain effective weights (4932) padded to 16 B
 // fragment image (floats, from w + PLAIN)
 enum : int {
-    F_W1 = 0,      // [jt 2][lane 64][s 4]            W1[32jt + (l&31)][2s + (l>>5)] (k = 7 -> 0)
+    F_W1 = 0,      // [jt 2][lane 64][s 4]            k' = 2s + (l>>5): k' = 0 -> b1[32jt + (l&31)],
+                   //                                 else W1[32jt + (l&31)][k' - 1] (input k' = 0 is 1.0)
     F_W2 = 512,    // [jt 2][t 2][rq 4][lane 64][e 4] W2[32jt + (l&31)][32t + rho(4rq+e) + 4(l>>5)]
     F_B1 = 4608,   // [jt 2][h 2][r 16]               b1[32jt + rho(r) + 4h]
     F_B2 = 4672,   // [jt 2][h 2][r 16]               b2[32jt + rho(r) + 4h]
@@ -35,6 +36,11 @@ static_assert(PLAIN + F_SIZE == PM_QNET_NW, "effective weight block size");
 
 __device__ __forceinline__ int rho(int r) { return (r & 3) + 8 * (r >> 2); }
 
+// ReLU as one v_max_i32 on the float's bits: every negative float (sign bit set) is a negative
+// int and becomes +0, every non-negative float is unchanged. fmaxf(x, 0) costs two VALU ops in
+// IEEE mode (a canonicalize per max), and VALU time adds to MFMA time on a gfx950 SIMD.
+__device__ __forceinline__ float relu(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
 // ----------------------------------------------------------------------------- fragment writers
 // Feature fragments (W1, W2, b1, b2) + the plain feature copy, from a parameter block. Block-wide.
 __device__ __forceinline__ void write_feature_frags(const float* __restrict__ p, float* __restrict__ w) {
@@ -44,7 +50,7 @@ __device__ __forceinline__ void write_feature_frags(const float* __restrict__ p,
     for (int k = t; k < 512; k += nt) {  // W1
         const int jt = k >> 8, lane = (k >> 2) & 63, s = k & 3;
         const int row = 32 * jt + (lane & 31), kk = 2 * s + (lane >> 5);
-        f[F_W1 + k] = kk < 7 ? p[W1 + row * 7 + kk] : 0.f;
+        f[F_W1 + k] = kk == 0 ? p[B1 + row] : p[W1 + row * 7 + kk - 1];  // bias rides input k' = 0
     }
     for (int k = t; k < 4096; k += nt) {  // W2
         const int e = k & 3, lane = (k >> 2) & 63, rq = (k >> 8) & 3, tt = (k >> 10) & 1, jt = k >> 11;
@@ -158,20 +164,17 @@ __device__ __forceinline__ void heads_to_frags(const float* heads, float* hf) {
 }
 
 // Layer 1 (7 -> 64) + ReLU + layer 2 (64 -> 64, pre-ReLU) for one 32-row tile on the matrix cores.
-// xs: this lane's layer-1 B operands obs[row][2s + (lane>>5)] (index 7 = 0). lw: staged fragments.
+// xs: this lane's layer-1 B operands, input k' = 2s + (lane>>5) with k' = 0 the constant 1.0 (its
+// weight column is b1) and k' = 1..7 the observation. The fma chain per output is b1 + W·x in
+// k order, as with a bias-initialised accumulator. lw: staged fragments.
 __device__ __forceinline__ void tile_hidden(const float* lw, const float (&xs)[4], int lane, f32x16 (&c2)[2]) {
     const int h = lane >> 5;
     f32x16 c1[2];
+    const f32x16 zero = {};
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {  // bias as the initial accumulator
-        const float4* b = reinterpret_cast<const float4*>(lw + F_B1 + (jt * 2 + h) * 16);
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-            const float4 v = b[q4];
-            c1[jt][4 * q4 + 0] = v.x; c1[jt][4 * q4 + 1] = v.y; c1[jt][4 * q4 + 2] = v.z; c1[jt][4 * q4 + 3] = v.w;
-        }
+    for (int jt = 0; jt < 2; ++jt) {
         const float4 w = reinterpret_cast<const float4*>(lw + F_W1)[jt * 64 + lane];
-        c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, xs[0], c1[jt], 0, 0, 0);
+        c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, xs[0], zero, 0, 0, 0);
         c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, xs[1], c1[jt], 0, 0, 0);
         c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, xs[2], c1[jt], 0, 0, 0);
         c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, xs[3], c1[jt], 0, 0, 0);
@@ -179,7 +182,7 @@ __device__ __forceinline__ void tile_hidden(const float* lw, const float (&xs)[4
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) c1[jt][r] = fmaxf(c1[jt][r], 0.f);
+        for (int r = 0; r < 16; ++r) c1[jt][r] = relu(c1[jt][r]);
     // layer 2: the layer-1 accumulators are the B operands. Operand fragments are read one group
     // (4 MFMAs = 256 cycles) ahead; sched_barrier keeps the scheduler from hoisting all 16 reads
     // (64 registers) to the top.
@@ -218,7 +221,7 @@ __device__ __forceinline__ void tile_heads(const float* hf, const f32x16 (&c2)[2
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const float x = fmaxf(c2[t][r], 0.f);
+            const float x = relu(c2[t][r]);
             const float4 w = hw[t * 16 + r];
             v = fmaf(w.x, x, v);
             a0 = fmaf(w.y, x, a0);
@@ -241,12 +244,13 @@ __device__ __forceinline__ void tile_heads(const float* hf, const f32x16 (&c2)[2
     q[2] = v + (a2 - mean);
 }
 
-// layer-1 B operands of this lane for observation row o (obs[2s + h], index 7 -> 0)
+// layer-1 B operands of this lane for observation row o: input k' = 2s + h, k' = 0 -> 1.0 (bias),
+// k' >= 1 -> o[k' - 1]
 __device__ __forceinline__ void tile_inputs(const float* __restrict__ o, int h, float (&xs)[4]) {
-    xs[0] = o[h];
-    xs[1] = o[2 + h];
-    xs[2] = o[4 + h];
-    xs[3] = h ? 0.f : o[6];
+    xs[0] = h ? o[0] : 1.0f;
+    xs[1] = o[1 + h];
+    xs[2] = o[3 + h];
+    xs[3] = o[5 + h];
 }
 
 // QNet forward + action for `count` arenas listed in LDS `list` (arena indices), weights staged in
@@ -329,6 +333,7 @@ struct ActShared {
     int list[kListMax];
     int count;
     int wtot[kActBlock / 64];
+    int lpre[16], loff[16], lcnt[16];  // per 256-arena segment of the env kernel's opponent lists
 };
 
 // Block-wide body of the grouped act kernel for grid block b (blockDim.x == kActBlock). side B:
@@ -337,7 +342,9 @@ struct ActShared {
 __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const float* __restrict__ w_opp,
                                           const int32_t* __restrict__ opp, const float* __restrict__ w_B,
                                           const float* __restrict__ obsA, const float* __restrict__ obsB,
-                                          TileOut outA, TileOut outB, int b) {
+                                          TileOut outA, TileOut outB, int b,
+                                          const int32_t* __restrict__ opp_list = nullptr,
+                                          const int32_t* __restrict__ opp_cnt = nullptr) {
     const float* w;
     const float* obs;
     TileOut out;
@@ -360,10 +367,39 @@ __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const
     // VALU/LDS work loses arbitration to co-resident waves' f32 MFMA streams), the tiles at normal.
     __builtin_amdgcn_s_setprio(2);
     stage_frags_lds(w, sh.lw, b);
+    // opponent rows: from the env kernel's per-block lists when the chunk is whole 256-arena blocks
+    const bool lists = compact && opp_list != nullptr && (lo & 255) == 0 && (((hi - lo) & 255) == 0 || hi == g.n);
     int ids[16];
-    if (compact) compact_load(opp, lo, hi, ids);
+    if (compact && !lists) compact_load(opp, lo, hi, ids);
     PM_BLK(4);
-    if (compact) {
+    if (lists) {
+        const int g0 = lo >> 8, G = (hi - lo + 255) >> 8;  // <= kListMax / 256 = 16 segments
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            const int v = lane < G ? opp_cnt[(size_t)(g0 + lane) * g.n_opp + net] : 0;
+            const int c = v & 0xFFFF;
+            int incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int u = __shfl_up(incl, o);
+                if (lane >= o) incl += u;
+            }
+            if (lane < G) { sh.lpre[lane] = incl - c; sh.loff[lane] = v >> 16; sh.lcnt[lane] = c; }
+            if (lane == 63) sh.count = incl;
+        }
+        __syncthreads();
+        const int seg = threadIdx.x >> 4, j0 = threadIdx.x & 15;  // 16 threads per segment
+        if (seg < G) {
+            const int c = sh.lcnt[seg], dst = sh.lpre[seg];
+            const int32_t* src = opp_list + (size_t)(g0 + seg) * 256 + sh.loff[seg];
+            int v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = j0 + 16 * r < c ? src[j0 + 16 * r] : 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (j0 + 16 * r < c) sh.list[dst + j0 + 16 * r] = v[r];
+        }
+    } else if (compact) {
         compact_scan(ids, net, lo, sh.list, &sh.count, sh.wtot);
     } else {
         if (threadIdx.x == 0) sh.count = hi - lo;

@@ -24,6 +24,7 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kLearn = 1024;              // k_learn / k_adam / k_prepare block
 constexpr int kGradN = PM_QNET_NHEAD;     // grad[520] = finished episodes, grad[521] = updated flag
+constexpr int kListNets = 64;             // opponent nets the env kernel keeps per-block lists for
 constexpr uint32_t kHashEmpty = 0xFFFFFFFFu;
 
 __device__ __forceinline__ bool learner_active(const pm_selfplay& sp) {
@@ -76,9 +77,9 @@ __global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp) {
     if ((int)blockIdx.x == nsb) PM_STAMP_ANY(70);
     const ActGrid g{sp.n, sp.n_pool + 1, sp.chunk_A, sp.chunk_P, 1};
     const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
-    const TileOut outB{sp.aB, nullptr, sp.ctrl->epsilon, sp.seed_env, sp.ctrl->step};
+    const TileOut outB{sp.aB, nullptr, -1.0, 0, 0};  // greedy here; k_env applies the epsilon draw
     act_block(sh, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, sp.w_B, sp.obsA, sp.obsB, outA, outB,
-              (int)blockIdx.x - nsb);
+              (int)blockIdx.x - nsb, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
     PM_BLK_END();
 }
 
@@ -127,7 +128,7 @@ __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) row[32 * t + rho(q) + 4 * h] = fmaxf(c2[t][q], 0.f);
+            for (int q = 0; q < 16; ++q) row[32 * t + rho(q) + 4 * h] = relu(c2[t][q]);
     }
     if (h == 0) {
         if (!nxt) {
@@ -137,6 +138,47 @@ __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f) {
             row[72] = qt[0]; row[73] = qt[1]; row[74] = qt[2];
         }
     }
+}
+
+// Per 256-arena block: its arenas grouped by opponent net for the next act (ascending within a
+// net), and (offset << 16 | count) per net, so the act kernel's opponent tiles read their rows with
+// two small loads instead of compacting ids next to MFMA waves (VALU there waits for the matrix
+// cores). Block-wide (kBlock threads); more than kListNets nets: no lists (the act kernel compacts).
+struct OppListSmem {
+    int woff[kBlock / 64][kListNets];  // per-wave count, then per-wave offset within the net
+    int noff[kListNets], ncnt[kListNets];
+};
+__device__ __forceinline__ void write_opp_lists(const pm_selfplay& sp, OppListSmem& sm, int blk, int i, bool valid,
+                                                int net) {
+    const int nn = sp.n_pool + 1;
+    if (nn > kListNets) return;  // uniform
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int rank = 0;
+    for (int k = 0; k < nn; ++k) {
+        const bool m = valid && net == k;
+        const unsigned long long b = __ballot(m);
+        if (m) rank = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) sm.woff[wv][k] = __popcll(b);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nn) {
+        const int k = threadIdx.x;
+        int acc = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const int c = sm.woff[w][k];
+            sm.woff[w][k] = acc;
+            acc += c;
+        }
+        sm.ncnt[k] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int k = 0; k < nn; ++k) { sm.noff[k] = acc; acc += sm.ncnt[k]; }
+    }
+    __syncthreads();
+    if (valid) sp.opp_list[(size_t)blk * kBlock + sm.noff[net] + sm.woff[wv][net] + rank] = i;
+    if ((int)threadIdx.x < nn) sp.opp_cnt[(size_t)blk * nn + threadIdx.x] = (sm.noff[threadIdx.x] << 16) | sm.ncnt[threadIdx.x];
 }
 
 // env.step (:242) + memory.push (:243) + episode bookkeeping (:245-249) + next opponent (:235-236)
@@ -161,7 +203,13 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
     const float pval = prio_pow(maxp, (float)sp.alpha);  // its PER leaf
 
     Arena a = load_arena(sp.st, ii);
-    const int aA = sp.aA[ii], aB = sp.aB[ii];
+    const int aA = sp.aA[ii];
+    int aB = sp.aB[ii];
+    {   // select_action_B (:126-130): random.random() < eps ? randint(0, 2) : argmax. The act kernel
+        // wrote the argmax; the draw is per-arena VALU work, cheaper here than beside the MFMAs.
+        const U4 rr = philox64((uint32_t)ii, TAG_ACT, c->step, sp.seed_env);
+        if (u53(rr.x, rr.y) < c->epsilon) aB = (int)below(rr.z, 3u);
+    }
     const int o = sp.opp[ii];
     float oA[7], oB[7];
     observe(a, oA, oB);  // the state the actions were chosen on (= obs of the previous env kernel)
@@ -184,6 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
             red[wv][3] = __popcll(mP); red[wv][4] = __popcll(mwP); red[wv][5] = rs;
         }
     }
+    int onew = o;
     if (valid) {
         // memory.push((oB, aB, rB, nB, done)) (:243, :56-63)
         const int64_t slot = (pos + i) % sp.cap;
@@ -194,7 +243,6 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
         row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
         sp.prios[slot] = maxp;
         leaf[slot] = pval;
-        int onew = o;
         float ernew = er;
         if (d) {  // next episode: opponent draw then env.reset()
             const uint32_t ns = (uint32_t)sp.st.serves[i];
@@ -209,6 +257,7 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
         }
         store_arena(sp.st, i, a);
         sp.opp[i] = onew;
+        sp.aB[i] = (int8_t)aB;  // the action taken
         sp.ep_reward[i] = ernew;
     }
     __syncthreads();
@@ -216,6 +265,10 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
         long long t = 0;
         for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
         sp.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = t;
+    }
+    {
+        __shared__ OppListSmem ol;
+        write_opp_lists(sp, ol, blockIdx.x, i, valid, onew);
     }
     store_rows7(sp.obsA, lds, nA, i0, sp.n);
     store_rows7(sp.obsB, lds, nB, i0, sp.n);
@@ -227,10 +280,12 @@ __global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
     const int i0 = blockIdx.x * kBlock;
     const int i = i0 + threadIdx.x;
     float oA[7] = {0}, oB[7] = {0};
+    int net = 0;
     if (i < sp.n) {
         const uint32_t ns = (uint32_t)sp.st.serves[i];
         const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
-        sp.opp[i] = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
+        net = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
+        sp.opp[i] = net;
         Arena a;
         double vx, vy, spn;
         philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
@@ -239,6 +294,10 @@ __global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
         sp.st.serves[i] = (int32_t)ns + 1;
         sp.ep_reward[i] = 0.f;
         observe(a, oA, oB);
+    }
+    {
+        __shared__ OppListSmem ol;
+        write_opp_lists(sp, ol, blockIdx.x, i, i < sp.n, net);
     }
     store_rows7(sp.obsA, lds, oA, i0, sp.n);
     store_rows7(sp.obsB, lds, oB, i0, sp.n);
@@ -251,9 +310,19 @@ struct ApplySmem {
     float tmu[PM_QNET_NHEAD];  // targetB head parameters (mu used)
     float m[PM_QNET_NHEAD], v[PM_QNET_NHEAD];  // Adam moments
     float g[PM_QNET_NHEAD + 2];                // shard-summed grads | finished episodes | updated flag
+    float ak[2];                               // Adam step size lr / (1 - b1^t), sqrt(1 - b2^t)
     float nact[132], ntrain[132];
     float heads[260];
 };
+
+// torch.optim.Adam's bias corrections for update number ts, computed in fp64 as torch does (Python
+// floats), once per block (two fp64 pow per thread cost ~3 us of VALU in a 1024-thread block).
+__device__ __forceinline__ void adam_consts(const pm_selfplay& sp, int64_t ts, ApplySmem& sm) {
+    const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
+    const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
+    sm.ak[0] = (float)(sp.lr / bc1);
+    sm.ak[1] = (float)sqrt(bc2);
+}
 
 // Block-wide: the optimizer's inputs into LDS (one load round trip). g: from LDS already when fused.
 __device__ __forceinline__ void load_apply_inputs(const pm_selfplay& sp, ApplySmem& sm, bool with_grad) {
@@ -306,10 +375,7 @@ __device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& s
     const uint64_t step = cs.step;
     gen_both_noises(sp, sm, step + 1, (uint64_t)ts + 1);
     if (train) {
-        const double bc1 = 1.0 - pow(sp.beta1, (double)ts);
-        const double bc2 = 1.0 - pow(sp.beta2, (double)ts);
-        const float step_size = (float)(sp.lr / bc1);
-        const float bc2s = (float)sqrt(bc2);
+        const float step_size = sm.ak[0], bc2s = sm.ak[1];  // adam_consts, published before a barrier
         for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
             const float g = sm.g[k] / (float)sp.world;
             float m = sm.m[k], v = sm.v[k], p = sm.hp[k];
@@ -404,7 +470,10 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
             sp.paramsB[PM_QNET_EPS_OFF + k] = e;
         }
     }
-    if (sp.fuse_apply) load_apply_inputs(sp, sm.ap, false);
+    if (sp.fuse_apply) {
+        load_apply_inputs(sp, sm.ap, false);
+        if (t == 0) adam_consts(sp, cs.train_steps + 1, sm.ap);
+    }
     for (int k = t; k < 512; k += kLearn) { sm.hkey[k] = kHashEmpty; sm.hwin[k] = -1; }
     // the rows k_env's forward blocks computed (hfeat [B][80]): a quarter of sample t/4 per thread
     const int hj = t >> 2, hq = (t & 3) * 20;
@@ -481,7 +550,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
 #pragma unroll
                     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) sm.Hs[j][32 * tt + rho(r) + 4 * h] = fmaxf(c2[tt][r], 0.f);
+                        for (int r = 0; r < 16; ++r) sm.Hs[j][32 * tt + rho(r) + 4 * h] = relu(c2[tt][r]);
                 }
                 if (h == 0) {
                     if (!nxt) {
@@ -680,6 +749,7 @@ __global__ __launch_bounds__(kLearn) void k_adam(const pm_selfplay sp) {
     __shared__ ApplySmem sm;
     const pm_ctrl cs = *sp.ctrl;
     load_apply_inputs(sp, sm, true);
+    if (threadIdx.x == 0) adam_consts(sp, cs.train_steps + 1, sm);
     __syncthreads();
     apply_update(sp, sm, cs);
 }
@@ -704,7 +774,8 @@ int check(const pm_selfplay* sp) {
                    sp->cap < 0xFFFFFFFFll,
                PM_E_SIZE, "pm_selfplay: n=%d batch=%d cap=%lld", sp->n, sp->batch, (long long)sp->cap);
     PM_REQUIRE(sp->n_pool >= 0 && sp->n_pool <= 4096 && sp->world >= 1, PM_E_SIZE, "pm_selfplay: n_pool/world");
-    PM_REQUIRE(sp->obsA && sp->obsB && sp->aA && sp->aB && sp->learn_heads, PM_E_ARG, "pm_selfplay: null buffer");
+    PM_REQUIRE(sp->obsA && sp->obsB && sp->aA && sp->aB && sp->learn_heads && sp->opp_list && sp->opp_cnt, PM_E_ARG,
+               "pm_selfplay: null buffer");
     PM_REQUIRE(!sp->fuse_apply || sp->world == 1, PM_E_ARG, "pm_selfplay: fuse_apply needs world == 1");
     PM_REQUIRE(sp->chunk_A > 0 && sp->chunk_A <= kListMax && sp->chunk_P > 0 && sp->chunk_P <= kListMax, PM_E_SIZE,
                "pm_selfplay: chunk_A/chunk_P must be in [1, %d]", kListMax);

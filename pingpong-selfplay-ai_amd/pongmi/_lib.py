@@ -28,7 +28,7 @@ PM_QNET_PLAIN = 4936
 PM_TRANS_F = 16
 PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class EnvParams(ctypes.Structure):
@@ -55,7 +55,7 @@ class SelfPlay(ctypes.Structure):
     _fields_ = [("env", EnvParams), ("st", EnvState)] + \
         [(n, c_void_p) for n in ("opp", "ep_reward", "w_opp", "paramsB", "paramsT", "w_B", "adam_m", "adam_v",
                                  "trans", "prios", "per_work", "idx", "isw", "grad", "partials", "obsA", "obsB", "aA",
-                                 "aB", "hfeat", "learn_heads", "ctrl")] + \
+                                 "aB", "hfeat", "learn_heads", "ctrl", "opp_list", "opp_cnt")] + \
         [("n", c_i32), ("n_pool", c_i32), ("batch", c_i32), ("world", c_i32), ("chunk_A", c_i32), ("chunk_P", c_i32),
          ("fuse_apply", c_i32), ("_pad0", c_i32), ("cap", c_i64)] + \
         [(n, c_double) for n in ("gamma", "alpha", "lr", "beta1", "beta2", "adam_eps", "min_epsilon", "epsilon_decay",

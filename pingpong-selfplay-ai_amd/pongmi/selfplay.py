@@ -27,12 +27,13 @@ from .env import env_config, env_params
 from .qnet import HEAD_KEYS, fold, pack_state_dict, unpack_state_dict
 
 
-def act_chunk(p, rows=96, cap=4096):
-    """Arenas per compaction chunk of an opponent played with probability p: the smallest power of
-    two expected to hold >= `rows` of its arenas (so its 32-row MFMA tiles are mostly full)."""
+def act_chunk(p, rows=96, cap=4096, lo=256):
+    """Arenas per act chunk of an opponent played with probability p: the smallest power of two
+    >= `lo` expected to hold >= `rows` of its arenas (so its 32-row MFMA tiles are mostly full).
+    Multiples of 256 let the act kernel read the env kernel's per-block opponent lists."""
     if p <= 0:
         return cap
-    c = 64
+    c = lo
     while c < cap and c * p < rows:
         c *= 2
     return c
@@ -61,6 +62,8 @@ class SelfPlayLearner:
         self.f64 = torch.zeros((7, n), dtype=torch.float64, device=dev)
         self.i32 = torch.zeros((4, n), dtype=torch.int32, device=dev)
         self.opp = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.opp_list = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.opp_cnt = torch.zeros(((n + 255) // 256) * (len(pool_states) + 1), dtype=torch.int32, device=dev)
         self.ep_reward = torch.zeros(n, **f32)
         # ---- networks
         self.paramsB = pack_state_dict(modelB_state, dev)
@@ -102,7 +105,7 @@ class SelfPlayLearner:
         sp.st = _lib.EnvState(*[ptr(self.f64[k]) for k in range(7)], *[ptr(self.i32[k]) for k in range(4)])
         for name in ("opp", "ep_reward", "w_opp", "paramsB", "paramsT", "w_B", "adam_m", "adam_v", "trans", "prios",
                      "per_work", "idx", "isw", "grad", "partials", "obsA", "obsB", "aA", "aB", "hfeat", "learn_heads",
-                     "ctrl"):
+                     "ctrl", "opp_list", "opp_cnt"):
             setattr(sp, name, ptr(getattr(self, name)))
         sp.n, sp.n_pool, sp.batch, sp.world, sp.cap = n, self.n_pool, self.batch, self.world, self.cap
         sp.fuse_apply = int(bool(fuse_apply) and self.world == 1)

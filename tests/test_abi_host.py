@@ -108,11 +108,12 @@ def test_qnet_pack_roundtrip_and_layout(golden):
 
 def test_act_chunk_sizing():
     from pongmi.selfplay import act_chunk
-    assert act_chunk(1.0) == 128 and act_chunk(0.67) == 256
+    assert act_chunk(1.0) == 256 and act_chunk(0.67) == 256  # >= 256: the env kernel's per-block lists
     assert act_chunk(0.33 / 8) == 4096 and act_chunk(0.0) == 4096
+    assert act_chunk(1.0, lo=64) == 128
     for p in (0.5, 0.1, 0.01):
         c = act_chunk(p)
-        assert c <= 4096 and (c * p >= 96 or c == 4096)
+        assert c <= 4096 and c % 256 == 0 and (c * p >= 96 or c == 4096)
 
 
 def test_drop_in_modules_import_with_reference_names():

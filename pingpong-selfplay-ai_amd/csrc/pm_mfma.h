@@ -80,6 +80,19 @@ __device__ __forceinline__ void write_head_frags(const float* heads, float* __re
 constexpr int kLwChunks = (F_SIZE / 4 + 63) / 64;  // 1 KB chunks of the fragment image (20)
 constexpr int kLwFloats = kLwChunks * 256;          // LDS image size: whole 1 KB wave chunks
 
+// Copy n floats global -> LDS with global_load_lds (4 B per lane, one wave instruction per 64
+// floats, no registers); dst must hold n rounded up to a multiple of 64 (the tail re-reads the
+// last element). Block-wide; published by the caller's __syncthreads().
+template <int N>
+__device__ __forceinline__ void copy_lds_f32(const float* __restrict__ src, float* dst) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int c = wv; c * 64 < N; c += nw) {
+        const int k = min(c * 64 + lane, N - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(src + k), (lds_void*)(dst + c * 64), 4, 0, 0);
+    }
+}
+constexpr int pad64(int n) { return (n + 63) / 64 * 64; }
+
 // Stage one net's fragment image global -> LDS directly (global_load_lds: 1 KB per wave
 // instruction, no registers, no wait until the caller's barrier). `lw` holds kLwFloats floats.
 // Chunk order starts at `rot` so concurrent blocks reading the same image spread over L2 channels.

@@ -305,10 +305,10 @@ __global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
 
 // ------------------------------------------------------------------------------------ learner
 // ------------------------------------------------------------------------------------ apply
-struct ApplySmem {
-    float hp[PM_QNET_NHEAD];   // modelB head parameters (after the optimizer step)
-    float tmu[PM_QNET_NHEAD];  // targetB head parameters (mu used)
-    float m[PM_QNET_NHEAD], v[PM_QNET_NHEAD];  // Adam moments
+struct ApplySmem {  // the 520-float arrays are padded to whole 64-float global_load_lds chunks
+    float hp[pad64(PM_QNET_NHEAD)];   // modelB head parameters (after the optimizer step)
+    float tmu[pad64(PM_QNET_NHEAD)];  // targetB head parameters (mu used)
+    float m[pad64(PM_QNET_NHEAD)], v[pad64(PM_QNET_NHEAD)];  // Adam moments
     float g[PM_QNET_NHEAD + 2];                // shard-summed grads | finished episodes | updated flag
     float ak[2];                               // Adam step size lr / (1 - b1^t), sqrt(1 - b2^t)
     float nact[132], ntrain[132];
@@ -324,14 +324,13 @@ __device__ __forceinline__ void adam_consts(const pm_selfplay& sp, int64_t ts, A
     sm.ak[1] = (float)sqrt(bc2);
 }
 
-// Block-wide: the optimizer's inputs into LDS (one load round trip). g: from LDS already when fused.
+// Block-wide: the optimizer's inputs global -> LDS directly (global_load_lds, no wait until the
+// caller's barrier). g: from LDS already when fused.
 __device__ __forceinline__ void load_apply_inputs(const pm_selfplay& sp, ApplySmem& sm, bool with_grad) {
-    for (int k = threadIdx.x; k < PM_QNET_NHEAD; k += blockDim.x) {
-        sm.hp[k] = sp.paramsB[PM_QNET_HEAD_OFF + k];
-        sm.tmu[k] = sp.paramsT[PM_QNET_HEAD_OFF + k];
-        sm.m[k] = sp.adam_m[k];
-        sm.v[k] = sp.adam_v[k];
-    }
+    copy_lds_f32<PM_QNET_NHEAD>(sp.paramsB + PM_QNET_HEAD_OFF, sm.hp);
+    copy_lds_f32<PM_QNET_NHEAD>(sp.paramsT + PM_QNET_HEAD_OFF, sm.tmu);
+    copy_lds_f32<PM_QNET_NHEAD>(sp.adam_m, sm.m);
+    copy_lds_f32<PM_QNET_NHEAD>(sp.adam_v, sm.v);
     if (with_grad)
         for (int k = threadIdx.x; k < PM_QNET_NHEAD + 2; k += blockDim.x) sm.g[k] = sp.grad[k];
 }
@@ -419,14 +418,14 @@ struct LearnSmem {
     union {
         struct {  // forward phase
             float lw[kLwFloats];  // modelB.features fragments (== targetB.features: frozen)
-            float hf[2][264];  // modelB (update noise) / targetB (mu) head fragments
+            float hf[pad64(2 * 264)];  // modelB (update noise) [0, 264) / targetB (mu) [264, 528) head fragments
         } f;
         float gpart[16][256];  // gradient phase: per-wave partial sums
     } u;
     float Hs[PM_MAX_BATCH][65];  // ReLU(features(s)) of the batch
     float qv[PM_MAX_BATCH][12];  // Q_B(s) 0..2 | Q_B(s') 4..6 | Q_T(s') 8..10
     float coef[PM_MAX_BATCH][4]; // dL/d(V, A0, A1, A2) per sample
-    float eps_tr[260];           // the update's noise (eps section layout)
+    float eps_tr[pad64(260)];    // the update's noise (eps section layout)
     int64_t sidx[PM_MAX_BATCH];
     uint32_t hkey[512];          // open-addressing set of sampled indices (last-duplicate-wins)
     int hwin[512];
@@ -450,42 +449,50 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
     const bool train = s_after >= B;
     const PerTree tree = per_tree(sp.per_work, sp.cap);
 
-    // ---- phase 0: every independent load
-    long long part[6] = {0, 0, 0, 0, 0, 0};
-    {
-        const int nbr = (sp.n + kBlock - 1) / kBlock;
-        for (int b = t; b < nbr; b += kLearn)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) part[k] += sp.partials[(size_t)b * 8 + k];
-    }
+    // ---- phase 0: every independent load, issued before any use. LDS-bound arrays go global ->
+    // LDS directly (global_load_lds); register loads are issued unconditionally (gating them on the
+    // control block, or storing each to LDS right away, costs one round trip per load).
     const bool act = train && t < B;
-    const float wraw = act ? sp.isw[t] : 0.f;
-    const int64_t id = act ? sp.idx[t] : 0;
-    if (train) {
-        stage_frags_lds(sp.w_B, sm.u.f.lw, 0);
-        for (int k = t; k < 2 * 264; k += kLearn) sm.u.f.hf[k / 264][k % 264] = sp.learn_heads[k];
-        for (int k = t; k < 260; k += kLearn) {  // the update's noise, left in modelB's buffers by reset_noise
-            const float e = sp.learn_heads[528 + k];
-            sm.eps_tr[k] = e;
-            sp.paramsB[PM_QNET_EPS_OFF + k] = e;
-        }
+    const int nbr = (sp.n + kBlock - 1) / kBlock;
+    stage_frags_lds(sp.w_B, sm.u.f.lw, 0);
+    copy_lds_f32<2 * 264>(sp.learn_heads, sm.u.f.hf);
+    copy_lds_f32<260>(sp.learn_heads + 528, sm.eps_tr);
+    if (sp.fuse_apply) load_apply_inputs(sp, sm.ap, false);
+    long long part[6] = {0, 0, 0, 0, 0, 0};
+    if (t < nbr) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) part[k] = sp.partials[(size_t)t * 8 + k];
     }
-    if (sp.fuse_apply) {
-        load_apply_inputs(sp, sm.ap, false);
-        if (t == 0) adam_consts(sp, cs.train_steps + 1, sm.ap);
-    }
-    for (int k = t; k < 512; k += kLearn) { sm.hkey[k] = kHashEmpty; sm.hwin[k] = -1; }
+    const float wraw_l = t < B ? sp.isw[t] : 0.f;
+    const int64_t id_l = t < B ? sp.idx[t] : 0;
+    const float eps_v = t < 260 ? sp.learn_heads[528 + t] : 0.f;
     // the rows k_env's forward blocks computed (hfeat [B][80]): a quarter of sample t/4 per thread
     const int hj = t >> 2, hq = (t & 3) * 20;
     float hv[20];
-    if (train && hj < B) {
-        const float4* src = reinterpret_cast<const float4*>(sp.hfeat + (size_t)hj * 80 + hq);
+    {
+        const float4* src = reinterpret_cast<const float4*>(sp.hfeat + (size_t)min(hj, B - 1) * 80 + hq);
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             const float4 v = src[k];
             hv[4 * k] = v.x; hv[4 * k + 1] = v.y; hv[4 * k + 2] = v.z; hv[4 * k + 3] = v.w;
         }
     }
+    for (int b = t + kLearn; b < nbr; b += kLearn)  // n > 256 * 1024 arenas only
+#pragma unroll
+        for (int k = 0; k < 6; ++k) part[k] += sp.partials[(size_t)b * 8 + k];
+    // first uses: the replay rows of the sample (dependent on idx: the second round trip)
+    float rwd = 0.f;
+    int bits = 0;
+    if (t < B) {
+        const float* tr = sp.trans + id_l * PM_TRANS_F;
+        rwd = tr[7];
+        bits = __float_as_int(tr[15]);
+    }
+    if (sp.fuse_apply && t == 0) adam_consts(sp, cs.train_steps + 1, sm.ap);
+    if (train && t < 260) sp.paramsB[PM_QNET_EPS_OFF + t] = eps_v;  // reset_noise leaves it in modelB
+    const float wraw = act ? wraw_l : 0.f;
+    const int64_t id = act ? id_l : 0;
+    for (int k = t; k < 512; k += kLearn) { sm.hkey[k] = kHashEmpty; sm.hwin[k] = -1; }
     if (act) sm.sidx[t] = id;
     {   // samples whose replay row k_env was writing: computed here (phase 1)
         const bool ip = act && push_of(sp, cs.pos, cs.size, cs.max_prio).covers(id);
@@ -501,13 +508,15 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
             else if (f < 76) sm.qv[hj][f - 64] = hv[k];
         }
     }
-    float rwd = 0.f;
-    int bits = 0;
-    if (act) {
-        const float* tr = sp.trans + id * PM_TRANS_F;
-        rwd = tr[7];
-        bits = __float_as_int(tr[15]);
-    }
+#ifdef PM_DIAG
+    PM_STAMP(30);
+    asm volatile("" ::"v"(wraw_l), "v"((int)id_l));
+    PM_STAMP(31);
+    asm volatile("" ::"v"(hv[0]), "v"(hv[19]));
+    PM_STAMP(32);
+    asm volatile("" ::"v"(rwd), "v"(bits));
+    PM_STAMP(33);
+#endif
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
 #pragma unroll
@@ -543,7 +552,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
             const int j = sm.plist[w * 64 + k - pre[w]];
             f32x16 c2[2];
             float qb[3], qt[3];
-            batch_row_fwd(sp, sm.u.f.lw, sm.u.f.hf[0], sm.u.f.hf[1], sm.sidx[j], nxt, lane, c2, qb, qt);
+            batch_row_fwd(sp, sm.u.f.lw, sm.u.f.hf, sm.u.f.hf + 264, sm.sidx[j], nxt, lane, c2, qb, qt);
             if (wv * 32 + (lane & 31) < 2 * np) {
                 const int h = lane >> 5;
                 if (!nxt) {

@@ -22,7 +22,8 @@ import torch  # noqa: E402
 
 NAMES = {
     70: "act start (1st act blk)", 64: "sample start", 65: "sample blk0 end", 72: "env start",
-    0: "learn start", 1: "learn loads", 2: "learn fwd (MFMA)", 3: "learn td/loss", 4: "learn scatter+grad",
+    0: "learn start", 30: "ph0 issued", 31: "ph0 idx/isw in", 32: "ph0 hfeat in", 33: "ph0 trans in",
+    1: "learn loads", 2: "learn fwd (MFMA)", 3: "learn td/loss", 4: "learn scatter+grad",
     8: "ph4 grads out w0", 9: "ph4 grads out w15", 10: "ph4 scatter subs w0", 11: "ph4 scatter subs w15",
     12: "ph4 push subs w0", 13: "ph4 push subs w15", 14: "ph4 edges w0", 15: "ph4 edges w15",
     5: "learn tree level1", 6: "learn tree level2", 20: "apply adam", 21: "apply derive", 7: "learn end",

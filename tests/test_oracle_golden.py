@@ -125,3 +125,25 @@ def test_dqn_steps_match_reference(orc, golden):
         if (s + 1) % 2 == 0:
             target = heads.copy()
         np.testing.assert_allclose(target, g[k + "target_heads_after"], rtol=3e-7, atol=2e-6)
+
+
+def test_rnn_forward_matches_reference(golden, orc):
+    """QNetRNN restatement vs the reference module (act step, T=8 sequences, 12-step carry)."""
+    g = golden("rnn")
+    sd = {k[7:]: v for k, v in g.items() if k.startswith("params.")}
+    for mode in ("train", "eval"):
+        eff = orc.rnn_effective(sd, mode == "train")
+        q, h, c = orc.rnn_forward(eff, g["act_x"], g["act_h0"][0], g["act_c0"][0])
+        np.testing.assert_allclose(q, g[f"act_q_{mode}"], rtol=1e-4, atol=2e-6)
+        np.testing.assert_allclose(h, g[f"act_h1_{mode}"][0], rtol=1e-4, atol=2e-6)
+        np.testing.assert_allclose(c, g[f"act_c1_{mode}"][0], rtol=1e-4, atol=2e-6)
+        z = np.zeros((16, 128))
+        q, h, c = orc.rnn_forward(eff, g["seq_x"], z, z)
+        np.testing.assert_allclose(q, g[f"seq_q_{mode}"], rtol=1e-4, atol=2e-6)
+        np.testing.assert_allclose(h, g[f"seq_h_{mode}"][0], rtol=1e-4, atol=2e-6)
+    eff = orc.rnn_effective(sd, True)
+    h = c = np.zeros((16, 128))
+    for t in range(12):
+        q, h, c = orc.rnn_forward(eff, g["roll_x"][t][:, None, :], h, c)
+        np.testing.assert_allclose(q, g["roll_q"][t], rtol=1e-4, atol=3e-6)
+    np.testing.assert_allclose(c, g["roll_c"][0], rtol=1e-4, atol=3e-6)

@@ -133,6 +133,39 @@ int pm_qnet_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const 
                 const uint64_t* counter_dev, int8_t* aA, int8_t* aB, float* qA, float* qB, int32_t n,
                 int32_t chunk0, int32_t chunk1, void* stream);
 
+/* ---------------------------------------------------------------- QNetRNN (K5) */
+
+/* Packed QNetRNN parameter block (models/qnet_rnn.py:58-101), PM_RNN_NP floats: the state_dict
+ * tensors in modelB.parameters() order (features_extractor.{0,2}.{weight,bias}, lstm.{weight_ih_l0,
+ * weight_hh_l0, bias_ih_l0, bias_hh_l0}, fc_shared_head.0 / fc_V / fc_A {weight_mu, bias_mu,
+ * weight_sigma, bias_sigma}: 174 984 floats), then the NoisyLinear epsilon buffers (shared head,
+ * V, A; weight then bias). Effective weights, PM_RNN_NW floats: an opaque MFMA fragment image. */
+#define PM_RNN_NP 192012
+#define PM_RNN_NPARAM 174984
+#define PM_RNN_NW 157456
+
+/* Fold `count` QNetRNN blocks [count][PM_RNN_NP] into effective weights [count][PM_RNN_NW]; modes
+ * as pm_qnet_fold (NoisyLinear eval: mu; train: mu + sigma*eps; train_fresh: reset_noise() first,
+ * Philox(seed, counter + *counter_dev) per net, written back into params_out when non-NULL). */
+int pm_rnn_fold(const float* params, float* params_out, int32_t mode, uint64_t seed, uint64_t counter,
+                const uint64_t* counter_dev, float* w_eff, int32_t count, void* stream);
+
+/* One QNetRNN.forward step (models/qnet_rnn.py:107-144, T = 1) for n rows: x [n][7], (h, c)
+ * [n][128] each read and overwritten with (h_n, c_n); reset[i] != 0 (nullable) starts row i from
+ * init_hidden (zeros, :146-152); q [n][3]. */
+int pm_rnn_q(const float* w_eff, const float* x, float* h, float* c, const uint8_t* reset, float* q, int32_t n,
+             void* stream);
+
+/* Both players' QNetRNN action selection (train_rnn_iterative.py:371-389, :571-581) for n arenas,
+ * fused on the matrix cores: A greedy with w_opp[opp_id[i]] (opp_id NULL = net 0) on obsA and
+ * (hA, cA); B on obsB and (hB, cB): random.random() < epsilon ? randint(0,2) : argmax, the forward
+ * advancing (hB, cB) either way. reset (nullable) zeroes both players' state first (episode
+ * start). Grouping as pm_qnet_act. */
+int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B, const float* obsA,
+               const float* obsB, float* hA, float* cA, float* hB, float* cB, const uint8_t* reset, float epsilon,
+               const double* eps_dev, uint64_t seed, uint64_t counter, const uint64_t* counter_dev, int8_t* aA,
+               int8_t* aB, float* qA, float* qB, int32_t n, int32_t chunk0, int32_t chunk1, void* stream);
+
 /* ---------------------------------------------------------------- replay + PER (K4) */
 
 /* Transition record, PM_TRANS_F floats per row (64 B): s [7] | r | s' [7] | bits(a | done << 8).

@@ -264,7 +264,7 @@ def argmax_first(q):
 
 # ----------------------------------------------------------------------------- QNetRNN (numpy)
 def _sigmoid(x):
-    return 1.0 / (1.0 + np.exp(-x))
+    return 0.5 * (1.0 + np.tanh(0.5 * np.asarray(x)))  # = 1 / (1 + e^-x), no overflow
 
 
 def rnn_effective(sd, train):

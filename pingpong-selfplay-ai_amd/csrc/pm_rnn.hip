@@ -1,0 +1,282 @@
+// K5 — QNetRNN acting (models/qnet_rnn.py, scripts/train_rnn_iterative.py:371-389) on the matrix
+// cores: fold (NoisyLinear mu + sigma * eps into the fragment-ordered block), single-net step
+// (pm_rnn_q: parity / the drop-in module's forward) and the fused two-player act (pm_rnn_act).
+#include "pm_host.h"
+#include "pm_rnn.h"
+
+using namespace pm;
+
+namespace {
+
+constexpr int kRnnBlock = 256;  // 4 waves, one 32-arena tile each at a time
+constexpr int kRnnRows = 128;   // arenas per block on the ungrouped side
+
+// reset_noise() (models/qnet_rnn.py:33-41) for fc_shared_head.0, fc_V, fc_A after _scale_noise:
+// [0,128) f(eps_in) S | [128,256) f(eps_out) S | [256,384) f(eps_in) V | [384] f(eps_out) V |
+// [385,513) f(eps_in) A | [513,516) f(eps_out) A. Philox(seed) counter (index, tag, ctr).
+__device__ __forceinline__ void rnn_noise(uint64_t seed, uint64_t ctr, float* noise) {
+    for (int k = threadIdx.x; k < R_NOISE; k += blockDim.x) {
+        uint32_t layer, which, e;
+        if (k < 256) { layer = 0; which = k >= 128; e = (uint32_t)(k & 127); }
+        else if (k < 385) { layer = 1; which = k >= 384; e = which ? 0u : (uint32_t)(k - 256); }
+        else { layer = 2; which = k >= 513; e = which ? (uint32_t)(k - 513) : (uint32_t)(k - 385); }
+        const U4 r = philox64(e, TAG_NOISE_RNN | (layer << 8) | (which << 12), ctr, seed);
+        noise[k] = scale_noise(normal(r.x, r.y, false));
+    }
+}
+
+// NoisyLinear weight / bias as the forward uses them (qnet_rnn.py:43-50), torch float32 order.
+struct RnnFold {
+    const float* p;
+    const float* noise;  // fresh draws (mode FRESH) or nullptr
+    int mode;
+    // layer: 0 S (128 x 128), 1 V (1 x 128), 2 A (3 x 128)
+    __device__ __forceinline__ float weight(int layer, int row, int k) const {
+        const int wmu = layer == 0 ? R_P_SWMU : layer == 1 ? R_P_VWMU : R_P_AWMU;
+        const int wsg = layer == 0 ? R_P_SWSG : layer == 1 ? R_P_VWSG : R_P_AWSG;
+        const int wep = layer == 0 ? R_P_SWEP : layer == 1 ? R_P_VWEP : R_P_AWEP;
+        const int idx = row * 128 + k;
+        if (mode == PM_FOLD_EVAL) return p[wmu + idx];
+        float eps;
+        if (mode == PM_FOLD_TRAIN) {
+            eps = p[wep + idx];
+        } else {
+            const int in0 = layer == 0 ? 0 : layer == 1 ? 256 : 385;
+            const int out0 = layer == 0 ? 128 : layer == 1 ? 384 : 513;
+            eps = noise[out0 + row] * noise[in0 + k];  // eps_out.ger(eps_in)
+        }
+        return p[wmu + idx] + p[wsg + idx] * eps;
+    }
+    __device__ __forceinline__ float bias(int layer, int row) const {
+        const int bmu = layer == 0 ? R_P_SBMU : layer == 1 ? R_P_VBMU : R_P_ABMU;
+        const int bsg = layer == 0 ? R_P_SBSG : layer == 1 ? R_P_VBSG : R_P_ABSG;
+        const int bep = layer == 0 ? R_P_SBEP : layer == 1 ? R_P_VBEP : R_P_ABEP;
+        if (mode == PM_FOLD_EVAL) return p[bmu + row];
+        const float eps = mode == PM_FOLD_TRAIN ? p[bep + row]
+                                                : noise[(layer == 0 ? 128 : layer == 1 ? 384 : 513) + row];
+        return p[bmu + row] + p[bsg + row] * eps;
+    }
+};
+
+__global__ __launch_bounds__(256) void k_rnn_fold(const float* __restrict__ params, float* __restrict__ params_out,
+                                                  int mode, uint64_t seed, uint64_t counter,
+                                                  const uint64_t* __restrict__ counter_dev, float* __restrict__ w_eff) {
+    __shared__ float noise[R_NOISE];
+    const int net = blockIdx.y;
+    const float* p = params + (size_t)net * PM_RNN_NP;
+    float* w = w_eff + (size_t)net * PM_RNN_NW;
+    if (mode == PM_FOLD_TRAIN_FRESH) {
+        rnn_noise(seed, counter + (counter_dev ? *counter_dev : 0ull) + (uint64_t)net * 0x10000ull, noise);
+        __syncthreads();
+    }
+    const RnnFold F{p, noise, mode};
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < PM_RNN_NW; e += gridDim.x * blockDim.x) {
+        float v;
+        if (e < R_F2) {
+            const int k = e - R_F1, s = k & 3, lane = (k >> 2) & 63, jt = k >> 8;
+            const int row = 32 * jt + (lane & 31), kk = 2 * s + (lane >> 5);
+            v = kk == 0 ? p[R_P_F1B + row] : p[R_P_F1W + row * 7 + kk - 1];
+        } else if (e < R_B2) {
+            const int k = e - R_F2, ee = k & 3, lane = (k >> 2) & 63, rq = (k >> 8) & 3, t = (k >> 10) & 1, mt = k >> 11;
+            v = p[R_P_F2W + (32 * mt + (lane & 31)) * 64 + 32 * t + rho(4 * rq + ee) + 4 * (lane >> 5)];
+        } else if (e < R_G) {
+            const int k = e - R_B2, r = k & 15, h = (k >> 4) & 1, mt = k >> 5;
+            v = p[R_P_F2B + 32 * mt + rho(r) + 4 * h];
+        } else if (e < R_BG) {
+            const int k = e - R_G, ee = k & 3, lane = (k >> 2) & 63, rq = (k >> 8) & 3, t = (k >> 10) & 7;
+            const int m = (k >> 13) & 3, gq = k >> 15;
+            const int row = 128 * gq + 32 * m + (lane & 31), kk = 32 * (t & 3) + rho(4 * rq + ee) + 4 * (lane >> 5);
+            v = t < 4 ? p[R_P_WIH + row * 128 + kk] : p[R_P_WHH + row * 128 + kk];
+        } else if (e < R_S) {
+            const int k = e - R_BG, r = k & 15, h = (k >> 4) & 1, m = (k >> 5) & 3, gq = k >> 7;
+            const int row = 128 * gq + 32 * m + rho(r) + 4 * h;
+            v = p[R_P_BIH + row] + p[R_P_BHH + row];
+        } else if (e < R_BS) {
+            const int k = e - R_S, ee = k & 3, lane = (k >> 2) & 63, rq = (k >> 8) & 3, t = (k >> 10) & 3, mt = k >> 12;
+            v = F.weight(0, 32 * mt + (lane & 31), 32 * t + rho(4 * rq + ee) + 4 * (lane >> 5));
+        } else if (e < R_H) {
+            const int k = e - R_BS, r = k & 15, h = (k >> 4) & 1, mt = k >> 5;
+            v = F.bias(0, 32 * mt + rho(r) + 4 * h);
+        } else if (e < R_BH) {
+            const int k = e - R_H, c = k & 3, r = (k >> 2) & 15, t = (k >> 6) & 3, h = k >> 8;
+            const int unit = 32 * t + rho(r) + 4 * h;
+            v = c == 0 ? F.weight(1, 0, unit) : F.weight(2, c - 1, unit);
+        } else {
+            const int c = e - R_BH;
+            v = c == 0 ? F.bias(1, 0) : c < 4 ? F.bias(2, c - 1) : 0.f;
+        }
+        w[e] = v;
+    }
+    if (mode == PM_FOLD_TRAIN_FRESH && params_out && blockIdx.x == 0) {  // reset_noise leaves the buffers
+        float* po = params_out + (size_t)net * PM_RNN_NP;
+        for (int k = threadIdx.x; k < 128 * 128; k += blockDim.x) po[R_P_SWEP + k] = noise[128 + (k >> 7)] * noise[k & 127];
+        for (int k = threadIdx.x; k < 128; k += blockDim.x) {
+            po[R_P_SBEP + k] = noise[128 + k];
+            po[R_P_VWEP + k] = noise[384] * noise[256 + k];
+            for (int a = 0; a < 3; ++a) po[R_P_AWEP + a * 128 + k] = noise[513 + a] * noise[385 + k];
+        }
+        if (threadIdx.x < 3) po[R_P_ABEP + threadIdx.x] = noise[513 + threadIdx.x];
+        if (threadIdx.x == 0) po[R_P_VBEP] = noise[384];
+    }
+}
+
+__device__ __forceinline__ void stage_heads(const float* __restrict__ w, float* hw) {
+    for (int k = threadIdx.x; k < 516; k += blockDim.x) hw[k] = w[R_H + k];
+}
+
+// One acting step for `count` arenas listed in `list` (LDS) with weights w; wave-uniform loop.
+__device__ __forceinline__ void rnn_rows(const float* __restrict__ w, const float* hw, float* xl_block,
+                                         const float* __restrict__ obs, float* hst, float* cst,
+                                         const uint8_t* __restrict__ reset, const int* list, int count,
+                                         const TileOut& out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int ntiles = (count + 31) >> 5;
+    for (int tl = wave; tl < ntiles; tl += nw) {
+        const int row = tl * 32 + (lane & 31);
+        const bool valid = row < count;
+        const int arena = list[min(row, count - 1)];
+        float xs[4];
+        tile_inputs(obs + (size_t)arena * 7, lane >> 5, xs);
+        const bool zero = reset != nullptr && reset[arena] != 0;
+        float q[3];
+        rnn_tile(w, xs, hst + (size_t)arena * 128, cst + (size_t)arena * 128, zero, valid, hw,
+                 xl_block + wave * 32 * kXStride, lane, q);
+        int a = argmax3(q);
+        if (out.eps >= 0.0) {  // random.random() < eps ? randint(0, 2) (forward still advances h, c: :376-380)
+            const U4 rr = philox64((uint32_t)arena, TAG_ACT, out.ctr, out.seed);
+            if (u53(rr.x, rr.y) < out.eps) a = below(rr.z, 3u);
+        }
+        if ((lane >> 5) == 0 && valid) {
+            if (out.act) out.act[arena] = (int8_t)a;
+            if (out.q) {
+                out.q[(size_t)arena * 3 + 0] = q[0];
+                out.q[(size_t)arena * 3 + 1] = q[1];
+                out.q[(size_t)arena * 3 + 2] = q[2];
+            }
+        }
+    }
+}
+
+constexpr int kRnnList = 2048;  // max arenas per grouped chunk
+
+struct RnnShared {
+    float hw[528];
+    float x[kRnnBlock / 64][32 * kXStride];  // per-wave gate input rows (features | h_prev)
+    int list[kRnnList];
+    int count;
+    int wtot[kRnnBlock / 64];
+};
+
+__global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_q(const float* __restrict__ w, const float* __restrict__ x,
+                                                        float* h, float* c, const uint8_t* __restrict__ reset,
+                                                        float* __restrict__ q, int n) {
+    __shared__ RnnShared sh;
+    const int lo = blockIdx.x * kRnnRows, hi = min(lo + kRnnRows, n);
+    stage_heads(w, sh.hw);
+    for (int k = threadIdx.x; k < hi - lo; k += blockDim.x) sh.list[k] = lo + k;
+    __syncthreads();
+    rnn_rows(w, sh.hw, &sh.x[0][0], x, h, c, reset, sh.list, hi - lo, TileOut{nullptr, q, -1.0, 0, 0});
+}
+
+struct RnnActArgs {
+    const float* w_opp;
+    const int32_t* opp;
+    const float* w_B;
+    const float *obsA, *obsB;
+    float *hA, *cA, *hB, *cB;
+    const uint8_t* reset;
+    int8_t *aA, *aB;
+    float *qA, *qB;
+    double eps;
+    const double* eps_dev;
+    uint64_t seed, counter;
+    const uint64_t* counter_dev;
+};
+
+// Grid as ActGrid (pm_mfma.h) with kRnnRows-arena chunks on side B; side A grouped by opponent net.
+__global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs A) {
+    __shared__ RnnShared sh;
+    int b = blockIdx.x;
+    const int nb = (g.n + kRnnRows - 1) / kRnnRows;
+    const float* w;
+    int net = -1, lo, hi;
+    bool compact = false;
+    if (b < nb) {
+        w = A.w_B; lo = b * kRnnRows; hi = min(lo + kRnnRows, g.n);
+    } else {
+        b -= nb;
+        if (b < g.na0()) { net = 0; lo = b * g.chunk0; hi = min(lo + g.chunk0, g.n); }
+        else { b -= g.na0(); net = 1 + b / g.na1(); lo = (b % g.na1()) * g.chunk1; hi = min(lo + g.chunk1, g.n); }
+        w = A.w_opp + (size_t)net * PM_RNN_NW;
+        compact = A.opp != nullptr;
+        if (!compact && net != 0) return;  // block-uniform
+    }
+    stage_heads(w, sh.hw);
+    int ids[16];
+    if (compact) compact_load(A.opp, lo, hi, ids);
+    if (compact) {
+        compact_scan(ids, net, lo, sh.list, &sh.count, sh.wtot);
+    } else {
+        if (threadIdx.x == 0) sh.count = hi - lo;
+        for (int k = threadIdx.x; k < hi - lo; k += blockDim.x) sh.list[k] = lo + k;
+    }
+    __syncthreads();
+    const uint64_t ctr = A.counter + (A.counter_dev ? *A.counter_dev : 0ull);
+    if (net < 0) {
+        const double eps = A.eps_dev ? *A.eps_dev : A.eps;
+        rnn_rows(w, sh.hw, &sh.x[0][0], A.obsB, A.hB, A.cB, A.reset, sh.list, sh.count,
+                 TileOut{A.aB, A.qB, eps, A.seed, ctr});
+    } else {
+        rnn_rows(w, sh.hw, &sh.x[0][0], A.obsA, A.hA, A.cA, A.reset, sh.list, sh.count,
+                 TileOut{A.aA, A.qA, -1.0, 0, 0});
+    }
+}
+
+}  // namespace
+
+extern "C" int pm_rnn_fold(const float* params, float* params_out, int32_t mode, uint64_t seed, uint64_t counter,
+                           const uint64_t* counter_dev, float* w_eff, int32_t count, void* stream) {
+    if (count == 0) return PM_OK;
+    PM_REQUIRE(params && w_eff && count > 0, PM_E_ARG, "pm_rnn_fold: null buffer or count");
+    PM_REQUIRE(mode >= PM_FOLD_EVAL && mode <= PM_FOLD_TRAIN_FRESH, PM_E_ARG, "pm_rnn_fold: mode %d", mode);
+    PM_REQUIRE((((uintptr_t)w_eff) & 15) == 0, PM_E_ARG, "pm_rnn_fold: w_eff must be 16-byte aligned");
+    hipLaunchKernelGGL(k_rnn_fold, dim3(pm_blocks(PM_RNN_NW, 256), count), dim3(256), 0, pm_stream(stream), params,
+                       params_out, mode, seed, counter, counter_dev, w_eff);
+    PM_LAUNCHED("k_rnn_fold");
+    return PM_OK;
+}
+
+extern "C" int pm_rnn_q(const float* w_eff, const float* x, float* h, float* c, const uint8_t* reset, float* q,
+                        int32_t n, void* stream) {
+    if (n == 0) return PM_OK;
+    PM_REQUIRE(w_eff && x && h && c && q && n > 0, PM_E_ARG, "pm_rnn_q: null buffer or n");
+    PM_REQUIRE(((((uintptr_t)w_eff) | ((uintptr_t)h) | ((uintptr_t)c)) & 15) == 0, PM_E_ARG,
+               "pm_rnn_q: w_eff / h / c must be 16-byte aligned");
+    hipLaunchKernelGGL(k_rnn_q, dim3(pm_blocks(n, kRnnRows)), dim3(kRnnBlock), 0, pm_stream(stream), w_eff, x, h, c,
+                       reset, q, n);
+    PM_LAUNCHED("k_rnn_q");
+    return PM_OK;
+}
+
+extern "C" int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B,
+                          const float* obsA, const float* obsB, float* hA, float* cA, float* hB, float* cB,
+                          const uint8_t* reset, float epsilon, const double* eps_dev, uint64_t seed, uint64_t counter,
+                          const uint64_t* counter_dev, int8_t* aA, int8_t* aB, float* qA, float* qB, int32_t n,
+                          int32_t chunk0, int32_t chunk1, void* stream) {
+    if (n == 0) return PM_OK;
+    PM_REQUIRE(w_opp && w_B && obsA && obsB && hA && cA && hB && cB && aA && aB && n > 0 && n_opp >= 1, PM_E_ARG,
+               "pm_rnn_act: null buffer or size");
+    PM_REQUIRE(((((uintptr_t)w_opp) | ((uintptr_t)w_B) | ((uintptr_t)hA) | ((uintptr_t)cA) | ((uintptr_t)hB) |
+                 ((uintptr_t)cB)) & 15) == 0,
+               PM_E_ARG, "pm_rnn_act: weights and hidden states must be 16-byte aligned");
+    if (chunk0 <= 0) chunk0 = 256;
+    if (chunk1 <= 0) chunk1 = kRnnList;
+    PM_REQUIRE(chunk0 <= kRnnList && chunk1 <= kRnnList, PM_E_SIZE, "pm_rnn_act: chunk > %d", kRnnList);
+    const ActGrid g{n, opp_id ? n_opp : 1, chunk0, chunk1, 0};
+    const int nb = (n + kRnnRows - 1) / kRnnRows;
+    const RnnActArgs a{w_opp, opp_id, w_B, obsA, obsB, hA, cA, hB, cB, reset, aA, aB, qA, qB,
+                       (double)epsilon, eps_dev, seed, counter, counter_dev};
+    hipLaunchKernelGGL(k_rnn_act, dim3(nb + g.blocks()), dim3(kRnnBlock), 0, pm_stream(stream), g, a);
+    PM_LAUNCHED("k_rnn_act");
+    return PM_OK;
+}

@@ -25,6 +25,9 @@ PM_QNET_HEAD_OFF = 4672
 PM_QNET_EPS_OFF = 5192
 PM_QNET_NW = 9944
 PM_QNET_PLAIN = 4936
+PM_RNN_NP = 192012
+PM_RNN_NPARAM = 174984
+PM_RNN_NW = 157456
 PM_TRANS_F = 16
 PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
@@ -76,6 +79,11 @@ _SIGS = {
     "pm_qnet_q": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_qnet_act": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p]),
+    "pm_rnn_fold": (c_i32, [c_void_p, c_void_p, c_i32, c_u64, c_u64, c_void_p, c_void_p, c_i32, c_void_p]),
+    "pm_rnn_q": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
+    "pm_rnn_act": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_i32, c_i32, c_i32, c_void_p]),
     "pm_per_work_bytes": (c_i64, [c_i64]),
     "pm_per_sample": (c_i32, [c_void_p, c_i64, c_float, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_i32,
                               c_void_p, c_void_p]),

@@ -166,6 +166,49 @@ int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const f
                const double* eps_dev, uint64_t seed, uint64_t counter, const uint64_t* counter_dev, int8_t* aA,
                int8_t* aB, float* qA, float* qB, int32_t n, int32_t chunk0, int32_t chunk1, void* stream);
 
+/* ---------------------------------------------------------------- DRQN update (K6) */
+
+/* train_step_rnn (scripts/train_rnn_iterative.py:400-531) on a sampled batch of `batch` sequences
+ * of length T: zero initial state; q = Q_B(obs)[last step][act[:, T-1]]; double-DQN target
+ * y = rew[:, T-1] + gamma * Q_T(next)[argmax Q_B(next)] * (1 - done[:, T-1]) with modelB in train
+ * mode (NoisyLinear mu + sigma * its epsilon buffers) and targetB in eval mode (mu);
+ * loss = smooth_l1(q, y) (mean); gradients of all PM_RNN_NPARAM parameters by BPTT;
+ * clip_grad_norm_(max_norm); Adam; targetB <- modelB every target_update_interval steps. */
+typedef struct pm_drqn_stats {
+    int64_t steps;  /* Adam steps taken (train_steps_count) */
+    float loss;     /* smooth_l1 loss of the last update */
+    float norm;     /* pre-clip total gradient norm of the last update (after the world mean) */
+    float q_mean;   /* mean q of the last batch */
+    int32_t status;
+} pm_drqn_stats;
+
+typedef struct pm_drqn {
+    float *params;          /* [PM_RNN_NP] modelB, updated in place */
+    float *target;          /* [PM_RNN_NP] targetB */
+    float *adam_m, *adam_v; /* [PM_RNN_NPARAM] */
+    float *grad;            /* [PM_RNN_NPARAM] gradients, packed parameter order (sum over ranks) */
+    void *work;             /* pm_drqn_work_bytes(batch, T) bytes, 16-byte aligned */
+    pm_drqn_stats *stats;
+    const float *obs, *next; /* [batch][T][7] */
+    const int32_t *act;      /* [batch][T] */
+    const float *rew;        /* [batch][T] */
+    const uint8_t *done;     /* [batch][T] */
+    int32_t batch;           /* multiple of 32, <= 256 */
+    int32_t T;               /* 1 .. 64 */
+    int32_t world;           /* ranks whose gradients `grad` sums (1 = single replica) */
+    int32_t _pad;
+    int64_t target_update_interval;
+    double gamma, lr, beta1, beta2, adam_eps, max_norm;
+} pm_drqn;
+
+int64_t pm_drqn_work_bytes(int32_t batch, int32_t T);
+/* Forward + BPTT: grad <- d loss / d params of this replica's batch. */
+int pm_drqn_grads(const pm_drqn *d, void *stream);
+/* grad / world -> clip_grad_norm_ -> Adam step -> target sync; stats updated. */
+int pm_drqn_apply(const pm_drqn *d, void *stream);
+/* pm_drqn_grads then pm_drqn_apply. */
+int pm_drqn_update(const pm_drqn *d, void *stream);
+
 /* ---------------------------------------------------------------- replay + PER (K4) */
 
 /* Transition record, PM_TRANS_F floats per row (64 B): s [7] | r | s' [7] | bits(a | done << 8).
@@ -279,7 +322,8 @@ int pm_selfplay_step(const pm_selfplay* sp, void* stream);
 /* ---------------------------------------------------------------- misc */
 const char* pm_last_error(void);
 int pm_abi_version(void);
-int32_t pm_sizeof(int32_t which); /* 0: pm_env_params 1: pm_env_state 2: pm_ctrl 3: pm_selfplay */
+int32_t pm_sizeof(int32_t which); /* 0: pm_env_params 1: pm_env_state 2: pm_ctrl 3: pm_selfplay 4: pm_drqn
+                                     5: pm_drqn_stats */
 
 #ifdef __cplusplus
 }

@@ -313,6 +313,117 @@ def rnn_forward(eff, xseq, h0, c0):
     return rnn_head(eff, h), h, c
 
 
+RNN_PARAM_KEYS = (  # modelB.parameters() order (models/qnet_rnn.py:71-99)
+    "features_extractor.0.weight", "features_extractor.0.bias", "features_extractor.2.weight",
+    "features_extractor.2.bias", "lstm.weight_ih_l0", "lstm.weight_hh_l0", "lstm.bias_ih_l0", "lstm.bias_hh_l0") + tuple(
+    f"{m}.{s}" for m in ("fc_shared_head.0", "fc_V", "fc_A") for s in ("weight_mu", "bias_mu", "weight_sigma", "bias_sigma"))
+
+
+def drqn_grads(sd, target_sd, obs, act, rew, nxt, done, gamma=0.99):
+    """train_step_rnn's loss and gradients (scripts/train_rnn_iterative.py:424-513), float64: zero
+    initial state; q = Q_B(obs)[last step][a_last]; a* = argmax Q_B(next) (first max); y = r_last +
+    gamma * Q_T(next)[a*] * (1 - done_last) with targetB in eval mode; loss = smooth_l1(q, y) (beta 1,
+    mean); gradients of every modelB parameter by hand-written BPTT (NoisyLinear: d mu = dW,
+    d sigma = dW * eps). obs/next [B,T,7], act/rew/done [B,T]. Returns dict(loss, q, y, grads)."""
+    eB = rnn_effective(sd, True)
+    eT = rnn_effective(target_sd, False)
+    B, T, _ = obs.shape
+    z = np.zeros((B, 128))
+    qn = rnn_forward(eB, nxt, z, z)[0]
+    qt = rnn_forward(eT, nxt, z, z)[0]
+    a_star = argmax_first(qn)
+    y = rew[:, -1].astype(np.float64) + gamma * qt[np.arange(B), a_star] * (~done[:, -1].astype(bool))
+    # forward with caches
+    x = np.asarray(obs, np.float64)
+    f1s, f2s, gs, cs, hs = [], [], [], [z], [z]
+    for t in range(T):
+        f1 = np.maximum(x[:, t] @ eB["W1"].T + eB["b1"], 0.0)
+        f2 = np.maximum(f1 @ eB["W2"].T + eB["b2"], 0.0)
+        zt = f2 @ eB["Wih"].T + eB["bih"] + hs[-1] @ eB["Whh"].T + eB["bhh"]
+        i, f, g, o = np.split(zt, 4, axis=1)
+        i, f, g, o = _sigmoid(i), _sigmoid(f), np.tanh(g), _sigmoid(o)
+        c = f * cs[-1] + i * g
+        h = o * np.tanh(c)
+        f1s.append(f1); f2s.append(f2); gs.append((i, f, g, o)); cs.append(c); hs.append(h)
+    hT = hs[-1]
+    spre = hT @ eB["S.W"].T + eB["S.b"]
+    s = np.maximum(spre, 0.0)
+    V = s @ eB["V.W"].T + eB["V.b"]
+    A = s @ eB["A.W"].T + eB["A.b"]
+    Q = V + (A - A.mean(axis=1, keepdims=True))
+    a = np.asarray(act[:, -1], np.int64)
+    q = Q[np.arange(B), a]
+    d = q - y
+    ad = np.abs(d)
+    loss = np.mean(np.where(ad < 1.0, 0.5 * d * d, ad - 0.5))
+    gq = np.clip(d, -1.0, 1.0) / B
+    dQ = np.zeros((B, 3))
+    dQ[np.arange(B), a] = gq
+    dV = dQ.sum(axis=1, keepdims=True)
+    dA = dQ - dQ.sum(axis=1, keepdims=True) / 3.0
+    G = {"V.W": dV.T @ s, "V.b": dV.sum(0), "A.W": dA.T @ s, "A.b": dA.sum(0)}
+    ds = (dV @ eB["V.W"] + dA @ eB["A.W"]) * (spre > 0)
+    G["S.W"], G["S.b"] = ds.T @ hT, ds.sum(0)
+    dh = ds @ eB["S.W"]
+    dc = np.zeros_like(dh)
+    for k in ("Wih", "Whh", "b", "W2", "b2", "W1", "b1"):
+        G[k] = 0.0
+    for t in range(T - 1, -1, -1):
+        i, f, g, o = gs[t]
+        tc = np.tanh(cs[t + 1])
+        do = dh * tc
+        dc = dc + dh * o * (1.0 - tc * tc)
+        dzi, dzf, dzg = dc * g * i * (1.0 - i), dc * cs[t] * f * (1.0 - f), dc * i * (1.0 - g * g)
+        dzo = do * o * (1.0 - o)
+        dz = np.concatenate([dzi, dzf, dzg, dzo], axis=1)
+        dc = dc * f
+        G["Wih"] = G["Wih"] + dz.T @ f2s[t]
+        G["Whh"] = G["Whh"] + dz.T @ hs[t]
+        G["b"] = G["b"] + dz.sum(0)
+        dh = dz @ eB["Whh"]
+        dp2 = (dz @ eB["Wih"]) * (f2s[t] > 0)
+        G["W2"] = G["W2"] + dp2.T @ f1s[t]
+        G["b2"] = G["b2"] + dp2.sum(0)
+        dp1 = (dp2 @ eB["W2"]) * (f1s[t] > 0)
+        G["W1"] = G["W1"] + dp1.T @ x[:, t]
+        G["b1"] = G["b1"] + dp1.sum(0)
+    eps = lambda k: np.asarray(sd[k], np.float64)  # noqa: E731
+    grads = {"features_extractor.0.weight": G["W1"], "features_extractor.0.bias": G["b1"],
+             "features_extractor.2.weight": G["W2"], "features_extractor.2.bias": G["b2"],
+             "lstm.weight_ih_l0": G["Wih"], "lstm.weight_hh_l0": G["Whh"],
+             "lstm.bias_ih_l0": G["b"], "lstm.bias_hh_l0": G["b"].copy()}
+    for name, key in (("S", "fc_shared_head.0"), ("V", "fc_V"), ("A", "fc_A")):
+        grads[f"{key}.weight_mu"] = G[name + ".W"]
+        grads[f"{key}.bias_mu"] = G[name + ".b"]
+        grads[f"{key}.weight_sigma"] = G[name + ".W"] * eps(f"{key}.weight_epsilon")
+        grads[f"{key}.bias_sigma"] = G[name + ".b"] * eps(f"{key}.bias_epsilon")
+    return dict(loss=loss, q=q, y=y, grads=grads)
+
+
+def clip_grad_norm(grads, max_norm=1.0):
+    """torch.nn.utils.clip_grad_norm_ (L2 over all tensors): scale by min(1, max_norm / (norm + 1e-6));
+    returns (clipped grads, the pre-clip total norm)."""
+    norm = float(np.sqrt(sum(float(np.sum(np.square(g))) for g in grads.values())))
+    coef = min(1.0, max_norm / (norm + 1e-6))
+    return {k: g * coef for k, g in grads.items()}, norm
+
+
+def drqn_update(sd, target_sd, adam, step, batch, lr=1e-4, gamma=0.99, max_norm=1.0):
+    """One train_step_rnn (:400-531): grads, clip_grad_norm_(1.0), Adam(lr) on every modelB
+    parameter. adam: {name: (m, v)} (updated in place); step: the Adam step count after this update.
+    Returns (new state_dict, info)."""
+    info = drqn_grads(sd, target_sd, *batch, gamma=gamma)
+    grads, norm = clip_grad_norm(info["grads"], max_norm)
+    new = dict(sd)
+    for k in RNN_PARAM_KEYS:
+        m, v = adam.get(k, (np.zeros_like(grads[k]), np.zeros_like(grads[k])))
+        p, m, v = adam_step(np.asarray(sd[k], np.float64), grads[k], m, v, step, lr)
+        adam[k] = (m, v)
+        new[k] = p
+    info["norm"] = norm
+    return new, info
+
+
 # ----------------------------------------------------------------------------- PER (numpy)
 def per_sample(prios, size, bs, beta, uniforms, alpha=0.6):
     """PrioritizedReplay.sample (scripts/train_iterative.py:64-73) with np.random.choice's own

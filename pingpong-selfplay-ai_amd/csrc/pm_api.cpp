@@ -26,6 +26,8 @@ extern "C" int32_t pm_sizeof(int32_t which) {
         case 1: return (int32_t)sizeof(pm_env_state);
         case 2: return (int32_t)sizeof(pm_ctrl);
         case 3: return (int32_t)sizeof(pm_selfplay);
+        case 4: return (int32_t)sizeof(pm_drqn);
+        case 5: return (int32_t)sizeof(pm_drqn_stats);
         default: return -1;
     }
 }

@@ -66,6 +66,17 @@ class SelfPlay(ctypes.Structure):
         [("beta_frames", c_i64), ("target_update_interval", c_i64), ("seed_env", c_u64), ("seed_net", c_u64)]
 
 
+class DrqnStats(ctypes.Structure):
+    _fields_ = [("steps", c_i64), ("loss", c_float), ("norm", c_float), ("q_mean", c_float), ("status", c_i32)]
+
+
+class Drqn(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("params", "target", "adam_m", "adam_v", "grad", "work", "stats", "obs", "next",
+                                        "act", "rew", "done")] + \
+        [("batch", c_i32), ("T", c_i32), ("world", c_i32), ("_pad", c_i32), ("target_update_interval", c_i64)] + \
+        [(n, c_double) for n in ("gamma", "lr", "beta1", "beta2", "adam_eps", "max_norm")]
+
+
 CTRL_DTYPE_BYTES = ctypes.sizeof(Ctrl)
 
 # name -> (restype, argtypes)
@@ -84,6 +95,10 @@ _SIGS = {
     "pm_rnn_act": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_i32, c_i32, c_i32, c_void_p]),
+    "pm_drqn_work_bytes": (c_i64, [c_i32, c_i32]),
+    "pm_drqn_grads": (c_i32, [c_void_p, c_void_p]),
+    "pm_drqn_apply": (c_i32, [c_void_p, c_void_p]),
+    "pm_drqn_update": (c_i32, [c_void_p, c_void_p]),
     "pm_per_work_bytes": (c_i64, [c_i64]),
     "pm_per_sample": (c_i32, [c_void_p, c_i64, c_float, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_i32,
                               c_void_p, c_void_p]),
@@ -124,7 +139,7 @@ def load():
         f.argtypes = args
     if L.pm_abi_version() != ABI_VERSION:
         raise PongmiError(f"libpongmi ABI {L.pm_abi_version()} != {ABI_VERSION}")
-    for which, cls in ((0, EnvParams), (1, EnvState), (2, Ctrl), (3, SelfPlay)):
+    for which, cls in ((0, EnvParams), (1, EnvState), (2, Ctrl), (3, SelfPlay), (4, Drqn), (5, DrqnStats)):
         if L.pm_sizeof(which) != ctypes.sizeof(cls):
             raise PongmiError(f"struct layout mismatch for {cls.__name__}: C {L.pm_sizeof(which)} "
                               f"vs ctypes {ctypes.sizeof(cls)}")

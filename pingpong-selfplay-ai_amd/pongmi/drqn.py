@@ -1,0 +1,98 @@
+"""The DRQN learner (K6): train_step_rnn (scripts/train_rnn_iterative.py:400-531) on device buffers.
+
+DRQNLearner owns modelB's and targetB's packed QNetRNN blocks (pongmi.rnn layout), the Adam moments
+and the update workspace; update() runs one train_step_rnn on a sampled batch of sequences
+(obs / next [B, T, 7], act / rew / done [B, T]) as one pm_drqn_update call: forward of modelB on obs
+and next and targetB on next from zero state, double-DQN target, smooth-L1, BPTT, clip_grad_norm_,
+Adam, target sync every target_update_interval steps — no host synchronisation.
+
+For data-parallel training, grads() / apply() split the update around the gradient all-reduce:
+every rank computes its gradient, the ranks sum `grad` (pongmi.dist), then apply() divides by the
+world size and runs the clip on the global norm and the identical Adam step on every rank.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import PM_RNN_NP, PM_RNN_NPARAM, check, stream_ptr
+from .rnn import pack_state_dict, unpack_state_dict
+
+
+class DRQNLearner:
+    def __init__(self, modelB, target=None, *, batch=64, T=8, gamma=0.99, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
+                 max_norm=1.0, target_update_interval=2000, world=1, device="cuda"):
+        """modelB / target: a QNetRNN module, its state_dict, or a packed [PM_RNN_NP] tensor;
+        target None = a copy of modelB (targetB.load_state_dict(modelB.state_dict()), :336-338)."""
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        self.params = self._block(modelB)
+        self.target = self._block(target) if target is not None else self.params.clone()
+        self.adam_m = torch.zeros(PM_RNN_NPARAM, dtype=torch.float32, device=self.device)
+        self.adam_v = torch.zeros(PM_RNN_NPARAM, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(PM_RNN_NPARAM, dtype=torch.float32, device=self.device)
+        self.batch, self.T = int(batch), int(T)
+        nbytes = self.lib.pm_drqn_work_bytes(self.batch, self.T)
+        if nbytes < 0:
+            raise ValueError("invalid batch / T")
+        self.work = torch.empty((nbytes + 15) // 16 * 4, dtype=torch.float32, device=self.device)
+        self.stats_buf = torch.zeros(ctypes.sizeof(_lib.DrqnStats), dtype=torch.uint8, device=self.device)
+        self.obs = torch.zeros((self.batch, self.T, 7), dtype=torch.float32, device=self.device)
+        self.next = torch.zeros_like(self.obs)
+        self.act = torch.zeros((self.batch, self.T), dtype=torch.int32, device=self.device)
+        self.rew = torch.zeros((self.batch, self.T), dtype=torch.float32, device=self.device)
+        self.done = torch.zeros((self.batch, self.T), dtype=torch.uint8, device=self.device)
+        d = _lib.Drqn()
+        for name in ("params", "target", "adam_m", "adam_v", "grad", "work", "obs", "next", "act", "rew", "done"):
+            setattr(d, name, getattr(self, name).data_ptr())
+        d.stats = self.stats_buf.data_ptr()
+        d.batch, d.T, d.world = self.batch, self.T, int(world)
+        d.target_update_interval = int(target_update_interval)
+        d.gamma, d.lr, d.beta1, d.beta2, d.adam_eps, d.max_norm = float(gamma), float(lr), float(betas[0]), \
+            float(betas[1]), float(eps), float(max_norm)
+        self.desc = d
+
+    def _block(self, m):
+        if isinstance(m, torch.Tensor):
+            if m.numel() != PM_RNN_NP:
+                raise ValueError(f"packed QNetRNN block must have {PM_RNN_NP} floats")
+            return m.detach().to(self.device, torch.float32).reshape(-1).clone()
+        sd = m.state_dict() if hasattr(m, "state_dict") else m
+        return pack_state_dict(sd, self.device)
+
+    def load_batch(self, obs, act, rew, next_obs, done):
+        """Copy a sampled batch (any device / dtype) into the learner's input buffers."""
+        self.obs.copy_(torch.as_tensor(obs).reshape(self.obs.shape))
+        self.next.copy_(torch.as_tensor(next_obs).reshape(self.next.shape))
+        self.act.copy_(torch.as_tensor(act).reshape(self.act.shape))
+        self.rew.copy_(torch.as_tensor(rew).reshape(self.rew.shape))
+        self.done.copy_(torch.as_tensor(done).reshape(self.done.shape))
+
+    def _call(self, fn, stream=None):
+        check(fn(ctypes.byref(self.desc), stream_ptr(stream)), fn.__name__)
+
+    def update(self, *batch, stream=None):
+        """One train_step_rnn; batch = (obs, act, rew, next_obs, done) or nothing (buffers already filled)."""
+        if batch:
+            self.load_batch(*batch)
+        self._call(self.lib.pm_drqn_update, stream)
+
+    def grads(self, *batch, stream=None):
+        if batch:
+            self.load_batch(*batch)
+        self._call(self.lib.pm_drqn_grads, stream)
+
+    def apply(self, stream=None):
+        self._call(self.lib.pm_drqn_apply, stream)
+
+    def stats(self):
+        """(steps, loss, pre-clip grad norm, mean q) of the last update (host sync)."""
+        s = _lib.DrqnStats.from_buffer_copy(bytes(self.stats_buf.cpu().numpy()))
+        return dict(steps=s.steps, loss=s.loss, norm=s.norm, q_mean=s.q_mean)
+
+    def state_dict(self):
+        """modelB's state_dict (reference key names)."""
+        return unpack_state_dict(self.params)
+
+    def target_state_dict(self):
+        return unpack_state_dict(self.target)

@@ -1,0 +1,118 @@
+"""K6 — the DRQN update (pm_drqn_update) against train_step_rnn run on the reference QNetRNN with
+torch autograd (tests/golden/drqn.npz) and against the float64 oracle (oracle.drqn_update).
+
+Tolerances (fp32 on the device; exact-f32 MFMA sums in a different order than torch's CPU GEMMs):
+loss / pre-clip norm rtol 1e-4; gradients rtol 1e-3 with atol 1e-5 x the tensor's largest
+magnitude (the same bar the oracle meets against the reference); parameters after three clipped
+Adam steps: Adam normalises every element's step to ~lr = 1e-4, so an element whose gradient is
+at fp32 rounding level moves by +-lr in a direction the rounding decides — every element within
+3 steps x lr, and all but < 0.5 % within rtol 1e-5 / atol 1e-6.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _sd(g):
+    return {k[7:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("params.")}
+
+
+def _batch(gd, k):
+    return tuple(gd[f"b{k}_{n}"] for n in ("obs", "act", "rew", "next", "done"))
+
+
+def _grads(L):
+    from pongmi.rnn import PARAM_LAYOUT
+    out, o = {}, 0
+    g = L.grad.cpu().numpy()
+    for k, s in PARAM_LAYOUT:
+        n = int(np.prod(s))
+        if "epsilon" not in k:
+            out[k] = g[o:o + n].reshape(s)
+        o += n
+    return out
+
+
+def _assert_params(got, ref, what, steps):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=steps * 1e-4 * 1.01, err_msg=what)
+    off = np.abs(got - ref) > 1e-6 + 1e-5 * np.abs(ref)
+    assert off.mean() < 0.005, f"{what}: {off.sum()} of {off.size} elements beyond 1e-6"
+
+
+def _assert_grads(got, ref, what):
+    for k, r in ref.items():
+        np.testing.assert_allclose(got[k], r, rtol=1e-3, atol=1e-5 * np.abs(r).max() + 1e-9, err_msg=f"{what}: {k}")
+
+
+def test_drqn_update_matches_reference(golden):
+    from pongmi.drqn import DRQNLearner
+    gr, gd = golden("rnn"), golden("drqn")
+    L = DRQNLearner(_sd(gr), batch=64, T=8)
+    for k in range(3):
+        L.update(*(torch.from_numpy(x) for x in _batch(gd, k)))
+        st = L.stats()
+        assert st["steps"] == k + 1
+        np.testing.assert_allclose(st["loss"], gd[f"u{k}_loss"], rtol=1e-4)
+        np.testing.assert_allclose(st["norm"], gd[f"u{k}_norm"], rtol=1e-4)
+        if k == 0:
+            _assert_grads(_grads(L), {k2[len("u0_grad."):]: v for k2, v in gd.items() if k2.startswith("u0_grad.")},
+                          "update 0")
+    sd = L.state_dict()
+    for k in (n[len("final_sub."):] for n in gd if n.startswith("final_sub.")):
+        _assert_params(sd[k].numpy().reshape(-1)[::8], gd["final_sub." + k], k, 3)
+    # targetB untouched (interval 2000), epsilon buffers unchanged
+    assert torch.equal(L.target_state_dict()["lstm.weight_hh_l0"], _sd(gr)["lstm.weight_hh_l0"])
+    assert torch.equal(sd["fc_A.weight_epsilon"], _sd(gr)["fc_A.weight_epsilon"])
+
+
+@pytest.mark.parametrize("B,T", [(32, 3), (96, 5), (64, 1)])
+def test_drqn_against_oracle_ragged(golden, orc, B, T):
+    """Other batch / sequence sizes against the oracle, with a target net that differs from modelB."""
+    from pongmi.drqn import DRQNLearner
+    gr = golden("rnn")
+    sd = {k[7:]: v for k, v in gr.items() if k.startswith("params.")}
+    rng = np.random.default_rng(B * 100 + T)
+    tsd = {k: (v + rng.normal(0, 0.02, v.shape).astype(np.float32)) if "epsilon" not in k else v for k, v in sd.items()}
+    obs = rng.uniform(0, 1, (B, T, 7)).astype(np.float32)
+    nxt = rng.uniform(0, 1, (B, T, 7)).astype(np.float32)
+    act = rng.integers(0, 3, (B, T)).astype(np.int64)
+    rew = rng.choice(np.array([-1, 0, 1], np.float32), (B, T)).astype(np.float32)
+    done = rng.random((B, T)) < 0.3
+    L = DRQNLearner({k: torch.from_numpy(v) for k, v in sd.items()}, {k: torch.from_numpy(v) for k, v in tsd.items()},
+                    batch=B, T=T)
+    L.grads(torch.from_numpy(obs), torch.from_numpy(act), torch.from_numpy(rew), torch.from_numpy(nxt),
+            torch.from_numpy(done))
+    info = orc.drqn_grads({k: v.astype(np.float64) for k, v in sd.items()},
+                          {k: v.astype(np.float64) for k, v in tsd.items()}, obs, act, rew, nxt, done)
+    _assert_grads(_grads(L), info["grads"], f"B={B} T={T}")
+    np.testing.assert_allclose(L.stats()["loss"], info["loss"], rtol=1e-4)
+    L.apply()
+    new, _ = orc.drqn_update({k: v.astype(np.float64) for k, v in sd.items()},
+                             {k: v.astype(np.float64) for k, v in tsd.items()}, {}, 1, (obs, act, rew, nxt, done))
+    got = L.state_dict()
+    for k in orc.RNN_PARAM_KEYS:
+        _assert_params(got[k].numpy(), new[k], k, 1)
+
+
+def test_drqn_deterministic_world_and_target_sync(golden):
+    """Bit-identical across runs; a gradient summed over 2 ranks with world = 2 gives the same step;
+    targetB <- modelB (all of it, epsilon buffers included) at every target_update_interval-th step."""
+    from pongmi.drqn import DRQNLearner
+    gr, gd = golden("rnn"), golden("drqn")
+    b = tuple(torch.from_numpy(x) for x in _batch(gd, 1))
+    runs = []
+    for world in (1, 1, 2):
+        L = DRQNLearner(_sd(gr), batch=64, T=8, world=world, target_update_interval=2)
+        for step in (1, 2):
+            L.grads(*b)
+            if world == 2:
+                L.grad.mul_(2.0)  # what the all-reduce of two identical replicas leaves
+            L.apply()
+            assert torch.equal(L.params, L.target) == (step == 2)  # synced at step 2
+        runs.append((L.params.clone(), L.adam_m.clone(), L.adam_v.clone(), L.stats()))
+    for r in runs[1:]:
+        assert torch.equal(r[0], runs[0][0]) and torch.equal(r[1], runs[0][1]) and torch.equal(r[2], runs[0][2])
+        assert r[3] == runs[0][3]

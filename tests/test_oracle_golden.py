@@ -147,3 +147,27 @@ def test_rnn_forward_matches_reference(golden, orc):
         q, h, c = orc.rnn_forward(eff, g["roll_x"][t][:, None, :], h, c)
         np.testing.assert_allclose(q, g["roll_q"][t], rtol=1e-4, atol=3e-6)
     np.testing.assert_allclose(c, g["roll_c"][0], rtol=1e-4, atol=3e-6)
+
+
+def test_drqn_update_matches_reference(golden, orc):
+    """The DRQN update restatement (hand-written BPTT + clip + Adam, float64) vs train_step_rnn run
+    on the reference QNetRNN with torch autograd (tests/golden/drqn.npz)."""
+    gr = golden("rnn")
+    gd = golden("drqn")
+    sd = {k[7:]: v.astype(np.float64) for k, v in gr.items() if k.startswith("params.")}
+    target = dict(sd)
+    batch = lambda k: tuple(gd[f"b{k}_{n}"] for n in ("obs", "act", "rew", "next", "done"))  # noqa: E731
+    info = orc.drqn_grads(sd, target, *batch(0))
+    np.testing.assert_allclose(info["q"], gd["u0_q"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(info["y"], gd["u0_target"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(info["loss"], gd["u0_loss"], rtol=1e-5)
+    for k in orc.RNN_PARAM_KEYS:
+        g = gd["u0_grad." + k]
+        np.testing.assert_allclose(info["grads"][k], g, rtol=1e-3, atol=1e-5 * np.abs(g).max() + 1e-9, err_msg=k)
+    adam = {}
+    for k in range(3):
+        sd, info = orc.drqn_update(sd, target, adam, k + 1, batch(k))
+        np.testing.assert_allclose(info["loss"], gd[f"u{k}_loss"], rtol=1e-4)
+        np.testing.assert_allclose(info["norm"], gd[f"u{k}_norm"], rtol=1e-4)
+    for k in orc.RNN_PARAM_KEYS:
+        np.testing.assert_allclose(np.ravel(sd[k])[::8], gd["final_sub." + k], rtol=1e-5, atol=1e-6, err_msg=k)

@@ -177,7 +177,7 @@ int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const f
 typedef struct pm_drqn_stats {
     int64_t steps;  /* Adam steps taken (train_steps_count) */
     float loss;     /* smooth_l1 loss of the last update */
-    float norm;     /* pre-clip total gradient norm of the last update (after the world mean) */
+    float norm;     /* pre-clip total gradient norm of the last update (of the rank mean) */
     float q_mean;   /* mean q of the last batch */
     int32_t status;
 } pm_drqn_stats;
@@ -186,28 +186,83 @@ typedef struct pm_drqn {
     float *params;          /* [PM_RNN_NP] modelB, updated in place */
     float *target;          /* [PM_RNN_NP] targetB */
     float *adam_m, *adam_v; /* [PM_RNN_NPARAM] */
-    float *grad;            /* [PM_RNN_NPARAM] gradients, packed parameter order (sum over ranks) */
+    float *grad;            /* [PM_RNN_NPARAM + 4] gradients in packed parameter order, then at
+                             * [PM_RNN_NPARAM] the number of ranks that contributed (1 per enabled
+                             * replica) — both summed by the all-reduce; apply divides by it */
     void *work;             /* pm_drqn_work_bytes(batch, T) bytes, 16-byte aligned */
     pm_drqn_stats *stats;
     const float *obs, *next; /* [batch][T][7] */
     const int32_t *act;      /* [batch][T] */
     const float *rew;        /* [batch][T] */
     const uint8_t *done;     /* [batch][T] */
+    const int32_t *enable;   /* nullable device flag: 0 = this replica skips the update (grads -> 0) */
     int32_t batch;           /* multiple of 32, <= 256 */
     int32_t T;               /* 1 .. 64 */
-    int32_t world;           /* ranks whose gradients `grad` sums (1 = single replica) */
-    int32_t _pad;
     int64_t target_update_interval;
     double gamma, lr, beta1, beta2, adam_eps, max_norm;
 } pm_drqn;
 
 int64_t pm_drqn_work_bytes(int32_t batch, int32_t T);
-/* Forward + BPTT: grad <- d loss / d params of this replica's batch. */
+/* Forward + BPTT: grad <- d loss / d params of this replica's batch, grad[PM_RNN_NPARAM] <- 1
+ * (all zero when *enable == 0). */
 int pm_drqn_grads(const pm_drqn *d, void *stream);
-/* grad / world -> clip_grad_norm_ -> Adam step -> target sync; stats updated. */
+/* grad / grad[PM_RNN_NPARAM] -> clip_grad_norm_ -> Adam step -> target sync; stats updated.
+ * Nothing happens when grad[PM_RNN_NPARAM] == 0. */
 int pm_drqn_apply(const pm_drqn *d, void *stream);
 /* pm_drqn_grads then pm_drqn_apply. */
 int pm_drqn_update(const pm_drqn *d, void *stream);
+
+/* ---------------------------------------------------------------- QNetRNN self-play (K7) */
+
+/* scripts/train_rnn_iterative.py's hot loop (:731-798) for n arenas: both players act with their
+ * QNetRNN and (h, c) carried per arena (A greedy: modelA or a pool net, both eval mode; B
+ * epsilon-greedy with fresh noise per vector step), env.step, SequenceReplayBuffer.push_step
+ * (:107-116: whole episodes of length >= T are kept, the latest seq_cap of them), episode
+ * bookkeeping and the next opponent / serve for finished arenas, then 64 sequences sampled
+ * (:118-173) into a pm_drqn batch and train_step_rnn once the buffer holds > min_episodes. */
+typedef struct pm_rnn_ctrl {
+    uint64_t step;       /* vector steps taken */
+    int64_t episodes;    /* finished episodes (global_episode_count) */
+    int64_t seq_count;   /* episodes ever stored (length >= T) */
+    int64_t seq_size;    /* episodes held: min(seq_count, seq_cap) */
+    double epsilon;
+    int64_t win_A, ep_A, win_P, ep_P;
+    double reward_B;     /* summed rewards of finished episodes */
+    int32_t status;      /* bit 0: a sampled step had been overwritten in its arena's ring */
+    int32_t train;       /* 1 when this step's DRQN update was enabled */
+} pm_rnn_ctrl;
+
+typedef struct pm_rnn_selfplay {
+    pm_env_params env;
+    pm_env_state st;
+    int32_t *opp;          /* [n] 0 = modelA, k >= 1 = pool net k */
+    float *ep_reward;      /* [n] */
+    int32_t *ep_len;       /* [n] steps into the current episode */
+    uint8_t *reset;        /* [n] 1: zero both players' (h, c) before the next act (episode start) */
+    const float *w_opp;    /* [1 + n_pool][PM_RNN_NW] modelA, pool nets (eval-mode folds) */
+    float *paramsB;        /* [PM_RNN_NP] modelB (the pm_drqn params); fresh noise written back */
+    float *w_B;            /* [PM_RNN_NW] */
+    float *hA, *cA, *hB, *cB;  /* [n][128] */
+    float *obsA, *obsB;    /* [n][7] */
+    int8_t *aA, *aB;       /* [n] */
+    float *trans;          /* [depth][n][PM_TRANS_F] per-arena transition rings (s, r, s', a | done << 8) */
+    int64_t *seq_eps;      /* [seq_cap][2]: arena | length << 32, first step */
+    int32_t *fin;          /* [n] scratch */
+    int64_t *partials;     /* [ceil(n / 256)][8] */
+    int32_t *enable;       /* [1] set by the sampler: seq_size > min_episodes */
+    pm_rnn_ctrl *ctrl;
+    int32_t n, n_pool, depth, T, chunk_A, chunk_P;
+    int64_t seq_cap, min_episodes;
+    double min_epsilon, epsilon_decay, pool_ratio;
+    uint64_t seed_env, seed_net;
+} pm_rnn_selfplay;
+
+/* Serve every arena, draw its first opponent, zero (h, c). */
+int pm_rnn_selfplay_init(const pm_rnn_selfplay *sp, void *stream);
+/* fold (fresh noise) + act + env + sequence store; then, when d != NULL, sample d's batch. */
+int pm_rnn_selfplay_rollout(const pm_rnn_selfplay *sp, const pm_drqn *d, void *stream);
+/* rollout then pm_drqn_update(d) (d->enable should be sp->enable). */
+int pm_rnn_selfplay_step(const pm_rnn_selfplay *sp, const pm_drqn *d, void *stream);
 
 /* ---------------------------------------------------------------- replay + PER (K4) */
 
@@ -323,7 +378,7 @@ int pm_selfplay_step(const pm_selfplay* sp, void* stream);
 const char* pm_last_error(void);
 int pm_abi_version(void);
 int32_t pm_sizeof(int32_t which); /* 0: pm_env_params 1: pm_env_state 2: pm_ctrl 3: pm_selfplay 4: pm_drqn
-                                     5: pm_drqn_stats */
+                                     5: pm_drqn_stats 6: pm_rnn_ctrl 7: pm_rnn_selfplay */
 
 #ifdef __cplusplus
 }

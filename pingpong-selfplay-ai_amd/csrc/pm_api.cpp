@@ -28,6 +28,8 @@ extern "C" int32_t pm_sizeof(int32_t which) {
         case 3: return (int32_t)sizeof(pm_selfplay);
         case 4: return (int32_t)sizeof(pm_drqn);
         case 5: return (int32_t)sizeof(pm_drqn_stats);
+        case 6: return (int32_t)sizeof(pm_rnn_ctrl);
+        case 7: return (int32_t)sizeof(pm_rnn_selfplay);
         default: return -1;
     }
 }

@@ -64,7 +64,7 @@ static __device__ unsigned long long pm_diag_blk[8][4096];
 namespace pm {
 
 // ----------------------------------------------------------------------------- RNG
-enum : uint32_t { TAG_SERVE = 1, TAG_ACT = 2, TAG_OPP = 3, TAG_NOISE_ACT = 4, TAG_PER = 5, TAG_NOISE_TRAIN = 6, TAG_NOISE_RNN = 7 };
+enum : uint32_t { TAG_SERVE = 1, TAG_ACT = 2, TAG_OPP = 3, TAG_NOISE_ACT = 4, TAG_PER = 5, TAG_NOISE_TRAIN = 6, TAG_NOISE_RNN = 7, TAG_SEQ = 8 };
 
 struct U4 {
     uint32_t x, y, z, w;

@@ -44,6 +44,7 @@ struct DrqnArgs {
     const float *rew;
     const uint8_t *done;
     pm_drqn_stats *stats;
+    const int32_t* enable;
     float gamma;
 };
 
@@ -91,8 +92,15 @@ inline int64_t drqn_layout(int B, int T, DrqnArgs* a, void* work) {
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ---------------------------------------------------------------- prep
+__device__ __forceinline__ bool skipped(const DrqnArgs& a) { return a.enable && *a.enable == 0; }
+
 __global__ __launch_bounds__(256) void k_drqn_prep(DrqnArgs a) {
     const int tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+    if (skipped(a)) {  // this replica contributes nothing to the all-reduce
+        for (int i = tid; i < PM_RNN_NPARAM + 4; i += nt) a.grad[i] = 0.f;
+        return;
+    }
+    if (tid == 0) a.grad[PM_RNN_NPARAM] = 1.0f;
     // effective heads: modelB train (mu + sigma * eps, NoisyLinear.forward :44-46), targetB eval (mu)
     for (int i = tid; i < 2 * E_N; i += nt) {
         const bool T = i >= E_N;
@@ -128,6 +136,7 @@ __global__ __launch_bounds__(256) void k_drqn_prep(DrqnArgs a) {
 // ---------------------------------------------------------------- forward LSTM step
 // grid: 3 streams x (B/32) column tiles x 4 hidden blocks; wave q = gate q (torch order i, f, g, o)
 __global__ __launch_bounds__(256) void k_drqn_fwd(DrqnArgs a, int t) {
+    if (skipped(a)) return;
     __shared__ float gate[4][32][33];
     const int B = a.B, C0 = a.C0, ldh = a.ldh, nct = B / 32;
     const int mb = blockIdx.x & 3, ct = (blockIdx.x >> 2) % nct, s = blockIdx.x / (4 * nct);
@@ -181,6 +190,7 @@ __global__ __launch_bounds__(256) void k_drqn_fwd(DrqnArgs a, int t) {
 
 // ---------------------------------------------------------------- heads: Q, TD target, loss, dQ
 __global__ __launch_bounds__(256) void k_drqn_q(DrqnArgs a) {
+    if (skipped(a)) return;
     __shared__ float Q[3][256][3];
     __shared__ float dV[256], dA[256][3], lv[256], qv[256];
     const int B = a.B, tid = threadIdx.x;
@@ -253,6 +263,7 @@ __global__ __launch_bounds__(256) void k_drqn_q(DrqnArgs a) {
 // grid: 4 unit tiles x (B/32) column tiles. dz_t for all 512 gate rows of the block's columns in
 // LDS; the block writes dz_t / dc_{t-1} for its own 32 units and dh_{t-1} = Whh^T dz_t for them.
 __global__ __launch_bounds__(256) void k_drqn_bwd(DrqnArgs a, int t) {
+    if (skipped(a)) return;
     __shared__ float dz[512][33];
     __shared__ float red[4][16][64];
     const int B = a.B, C0 = a.C0, ldh = a.ldh, Tn = a.T;
@@ -307,6 +318,7 @@ __global__ __launch_bounds__(256) void k_drqn_bwd(DrqnArgs a, int t) {
 
 // ---------------------------------------------------------------- NoisyLinear sigma gradients
 __global__ __launch_bounds__(256) void k_drqn_sigma(DrqnArgs a) {
+    if (skipped(a)) return;
     const int n = 16384 + 128 + 128 + 1 + 384 + 3;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         int mu, sg, ep;
@@ -321,8 +333,11 @@ __global__ __launch_bounds__(256) void k_drqn_sigma(DrqnArgs a) {
 }
 
 // ---------------------------------------------------------------- clip + Adam
-__global__ __launch_bounds__(256) void k_drqn_norm(DrqnArgs a, float inv_world) {
+__global__ __launch_bounds__(256) void k_drqn_norm(DrqnArgs a) {
     __shared__ double red[256];
+    const float ranks = a.grad[PM_RNN_NPARAM];  // replicas that contributed (summed by the all-reduce)
+    if (!(ranks > 0.f)) return;
+    const float inv_world = 1.0f / ranks;
     const int n = PM_RNN_NPARAM, per = (n + kNormBlocks - 1) / kNormBlocks;
     const int lo = blockIdx.x * per, hi = min(n, lo + per);
     double s = 0.0;
@@ -345,16 +360,17 @@ __global__ __launch_bounds__(256) void k_drqn_norm(DrqnArgs a, float inv_world) 
 }
 
 struct AdamK {
-    float lr_unused;
     double lr, beta1, beta2, eps, max_norm;
     int64_t interval;
-    float inv_world;
 };
 
 __global__ __launch_bounds__(256) void k_drqn_adam(DrqnArgs a, AdamK k, float* params, float* target, float* m_,
                                                    float* v_) {
     __shared__ float cf[3];
     __shared__ int64_t ts_s;
+    const float ranks = a.grad[PM_RNN_NPARAM];
+    if (!(ranks > 0.f)) return;
+    const float inv_world = 1.0f / ranks;
     if (threadIdx.x == 0) {
         double ss = 0.0;
         for (int j = 0; j < kNormBlocks; ++j) ss += a.part[j];
@@ -373,7 +389,7 @@ __global__ __launch_bounds__(256) void k_drqn_adam(DrqnArgs a, AdamK k, float* p
     const bool sync = ts_s % k.interval == 0;  // targetB.load_state_dict(modelB.state_dict()) (:529-530)
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < PM_RNN_NP; i += gridDim.x * blockDim.x) {
         if (i < PM_RNN_NPARAM) {
-            const float g = (a.grad[i] * k.inv_world) * coef;
+            const float g = (a.grad[i] * inv_world) * coef;
             float m = m_[i], v = v_[i], p = params[i];
             m = m + (float)(1.0 - k.beta1) * (g - m);                 // exp_avg.lerp_(grad, 1-beta1)
             v = v * (float)k.beta2 + (float)(1.0 - k.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
@@ -396,7 +412,6 @@ int check(const pm_drqn* d) {
     PM_REQUIRE(d->batch >= 32 && d->batch <= 256 && d->batch % 32 == 0, PM_E_SIZE,
                "pm_drqn: batch %d (multiple of 32 in [32, 256])", d->batch);
     PM_REQUIRE(d->T >= 1 && d->T <= 64, PM_E_SIZE, "pm_drqn: T %d (1..64)", d->T);
-    PM_REQUIRE(d->world >= 1, PM_E_ARG, "pm_drqn: world %d", d->world);
     PM_REQUIRE(d->target_update_interval >= 1, PM_E_ARG, "pm_drqn: target_update_interval");
     PM_REQUIRE(((((uintptr_t)d->params) | ((uintptr_t)d->target) | ((uintptr_t)d->grad) | ((uintptr_t)d->work)) & 15) == 0,
                PM_E_ARG, "pm_drqn: params / target / grad / work must be 16-byte aligned");
@@ -419,7 +434,7 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     hipStream_t st = pm_stream(stream);
     DrqnArgs a{};
     drqn_layout(d->batch, d->T, &a, d->work);
-    a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats;
+    a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats; a.enable = d->enable;
     a.obs = d->obs; a.next = d->next; a.act = d->act; a.rew = d->rew; a.done = d->done;
     a.gamma = (float)d->gamma;
     const int B = a.B, C0 = a.C0, ldh = a.ldh, T = a.T, nct = B / 32;
@@ -431,14 +446,14 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     GemmProb p[kGemmMax];
     p[0] = gemm_prob(PB + R_P_F1W, 7, 1, a.X, 2 * C0, 1, a.F1B, 2 * C0, 1, 64, 2 * C0, 7, GF_RELU, PB + R_P_F1B);
     p[1] = gemm_prob(PT + R_P_F1W, 7, 1, a.X + C0, 2 * C0, 1, a.F1T, C0, 1, 64, C0, 7, GF_RELU, PT + R_P_F1B);
-    PM_REQUIRE(gemm_launch(p, 2, st) == hipSuccess, PM_E_LAUNCH, "k_gemm (F1)");
+    PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (F1)");
     p[0] = gemm_prob(PB + R_P_F2W, 64, 1, a.F1B, 2 * C0, 1, a.F2B, 2 * C0, 1, 128, 2 * C0, 64, GF_RELU, PB + R_P_F2B);
     p[1] = gemm_prob(PT + R_P_F2W, 64, 1, a.F1T, C0, 1, a.F2T, C0, 1, 128, C0, 64, GF_RELU, PT + R_P_F2B);
-    PM_REQUIRE(gemm_launch(p, 2, st) == hipSuccess, PM_E_LAUNCH, "k_gemm (F2)");
+    PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (F2)");
     p[0] = gemm_prob(PB + R_P_WIH, 128, 1, a.F2B, 2 * C0, 1, a.ZxB, 2 * C0, 1, 512, 2 * C0, 128, 0, PB + R_P_BIH,
                      PB + R_P_BHH);
     p[1] = gemm_prob(PT + R_P_WIH, 128, 1, a.F2T, C0, 1, a.ZxT, C0, 1, 512, C0, 128, 0, PT + R_P_BIH, PT + R_P_BHH);
-    PM_REQUIRE(gemm_launch(p, 2, st) == hipSuccess, PM_E_LAUNCH, "k_gemm (Zx)");
+    PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (Zx)");
     for (int t = 0; t < T; ++t) {
         hipLaunchKernelGGL(k_drqn_fwd, dim3(3 * nct * 4), dim3(256), 0, st, a, t);
         PM_LAUNCHED("k_drqn_fwd");
@@ -448,13 +463,13 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     p[0] = gemm_prob(a.effB + E_S, 128, 1, a.Hp0 + hT, ldh, 1, a.S0, B, 1, 128, B, 128, GF_RELU, a.effB + E_SB);
     p[1] = gemm_prob(a.effB + E_S, 128, 1, a.Hp1 + hT, ldh, 1, a.S1, B, 1, 128, B, 128, GF_RELU, a.effB + E_SB);
     p[2] = gemm_prob(a.effT + E_S, 128, 1, a.Hp2 + hT, ldh, 1, a.S2, B, 1, 128, B, 128, GF_RELU, a.effT + E_SB);
-    PM_REQUIRE(gemm_launch(p, 3, st) == hipSuccess, PM_E_LAUNCH, "k_gemm (S)");
+    PM_REQUIRE(gemm_launch(p, 3, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (S)");
     hipLaunchKernelGGL(k_drqn_q, dim3(1), dim3(256), 0, st, a);
     PM_LAUNCHED("k_drqn_q");
     p[0] = gemm_prob(a.dS, B, 1, a.Hp0 + hT, 1, ldh, g + R_P_SWMU, 128, 1, 128, 128, B);  // dW_S = dS h_T^T
     p[1] = gemm_prob(a.dS, B, 1, a.one, 0, 0, g + R_P_SBMU, 1, 0, 128, 1, B);             // db_S
     p[2] = gemm_prob(a.effB + E_S, 1, 128, a.dS, B, 1, a.dH0, B, 1, 128, B, 128);          // dh_T = W_S^T dS
-    PM_REQUIRE(gemm_launch(p, 3, st) == hipSuccess, PM_E_LAUNCH, "k_gemm (dS)");
+    PM_REQUIRE(gemm_launch(p, 3, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dS)");
     for (int t = T - 1; t >= 0; --t) {
         hipLaunchKernelGGL(k_drqn_bwd, dim3(4 * nct), dim3(256), 0, st, a, t);
         PM_LAUNCHED("k_drqn_bwd");
@@ -466,15 +481,15 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     p[3] = gemm_prob(a.dZ, C0, 1, a.one, 0, 0, g + R_P_BHH, 1, 0, 512, 1, C0);           // db_hh
     p[4] = gemm_prob(PB + R_P_WIH, 1, 128, a.dZ, C0, 1, a.dP2, C0, 1, 128, C0, 512, 0, nullptr, nullptr, a.F2B,
                      2 * C0, 1);  // dF2 = Wih^T dZ, through the ReLU
-    PM_REQUIRE(gemm_launch(p, 5, st) == hipSuccess, PM_E_LAUNCH, "k_gemm (dZ)");
+    PM_REQUIRE(gemm_launch(p, 5, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dZ)");
     p[0] = gemm_prob(a.dP2, C0, 1, a.F1B, 1, 2 * C0, g + R_P_F2W, 64, 1, 128, 64, C0);  // dW2
     p[1] = gemm_prob(a.dP2, C0, 1, a.one, 0, 0, g + R_P_F2B, 1, 0, 128, 1, C0);         // db2
     p[2] = gemm_prob(PB + R_P_F2W, 1, 64, a.dP2, C0, 1, a.dP1, C0, 1, 64, C0, 128, 0, nullptr, nullptr, a.F1B, 2 * C0,
                      1);  // dF1 = W2^T dF2, through the ReLU
-    PM_REQUIRE(gemm_launch(p, 3, st) == hipSuccess, PM_E_LAUNCH, "k_gemm (dP2)");
+    PM_REQUIRE(gemm_launch(p, 3, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dP2)");
     p[0] = gemm_prob(a.dP1, C0, 1, a.X, 1, 2 * C0, g + R_P_F1W, 7, 1, 64, 7, C0);  // dW1
     p[1] = gemm_prob(a.dP1, C0, 1, a.one, 0, 0, g + R_P_F1B, 1, 0, 64, 1, C0);     // db1
-    PM_REQUIRE(gemm_launch(p, 2, st) == hipSuccess, PM_E_LAUNCH, "k_gemm (dP1)");
+    PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dP1)");
     hipLaunchKernelGGL(k_drqn_sigma, dim3(pm_blocks(17028, 256)), dim3(256), 0, st, a);
     PM_LAUNCHED("k_drqn_sigma");
     return PM_OK;
@@ -486,10 +501,9 @@ extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) {
     DrqnArgs a{};
     drqn_layout(d->batch, d->T, &a, d->work);
     a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats;
-    const float inv_world = 1.0f / (float)d->world;
-    hipLaunchKernelGGL(k_drqn_norm, dim3(kNormBlocks), dim3(256), 0, st, a, inv_world);
+    hipLaunchKernelGGL(k_drqn_norm, dim3(kNormBlocks), dim3(256), 0, st, a);
     PM_LAUNCHED("k_drqn_norm");
-    AdamK k{0.f, d->lr, d->beta1, d->beta2, d->adam_eps, d->max_norm, d->target_update_interval, inv_world};
+    AdamK k{d->lr, d->beta1, d->beta2, d->adam_eps, d->max_norm, d->target_update_interval};
     hipLaunchKernelGGL(k_drqn_adam, dim3(pm_blocks(PM_RNN_NP, 256)), dim3(256), 0, st, a, k, d->params, d->target,
                        d->adam_m, d->adam_v);
     PM_LAUNCHED("k_drqn_adam");

@@ -32,6 +32,7 @@ struct GemmProb {
 constexpr int kGemmMax = 6;
 struct GemmBatch {
     GemmProb p[kGemmMax];
+    const int32_t* enable;  // nullable device flag: 0 = skip the whole launch
     int np, nblk;
 };
 
@@ -88,6 +89,7 @@ __device__ __forceinline__ void gemm_tile(const GemmProb& P, int tile, float (*r
 
 __global__ __launch_bounds__(256) void k_gemm(GemmBatch g) {
     __shared__ float red[4][16][64];
+    if (g.enable && *g.enable == 0) return;
     int pi = 0;
 #pragma unroll
     for (int j = 1; j < kGemmMax; ++j)
@@ -116,9 +118,10 @@ inline GemmProb gemm_prob(const float* A, int64_t sam, int64_t sak, const float*
 }
 
 // Launch up to kGemmMax problems as one grid.
-inline hipError_t gemm_launch(const GemmProb* probs, int np, hipStream_t st) {
+inline hipError_t gemm_launch(const GemmProb* probs, int np, hipStream_t st, const int32_t* enable = nullptr) {
     GemmBatch g{};
     g.np = np;
+    g.enable = enable;
     int blk = 0;
     for (int i = 0; i < np; ++i) {
         g.p[i] = probs[i];

@@ -1,0 +1,266 @@
+// K7 — QNetRNN self-play: scripts/train_rnn_iterative.py's hot loop (:731-798) for n arenas.
+//
+// One vector step = one env step in every arena, on one stream:
+//   pm_rnn_fold   modelB's NoisyLinear layers with fresh noise (select_action_for_model's
+//                 reset_noise, :385), written back into modelB's epsilon buffers
+//   pm_rnn_act    both players on the matrix cores, (h, c) carried per arena (K5)
+//   k_rsp_env     env.step, SequenceReplayBuffer.push_step into the arena's transition ring,
+//                 ep reward / length, next opponent + env.reset() for finished arenas (HBM-bound)
+//   k_rsp_append  finished episodes of length >= T appended to the episode table in arena order
+//                 (deque(maxlen=capacity).append, :114), counters, epsilon decay (:798)
+//   k_rsp_sample  SequenceReplayBuffer.sample(64) (:118-173) into the DRQN batch, and the enable
+//                 flag (len(memory) > batch * min_episodes_for_training_start, :768)
+// then pm_drqn_update (K6). Transition rings are [depth][n] records of 64 B written by step
+// (coalesced); an episode is (arena, first step, length), its steps read back from the ring.
+#include "pm_dev.h"
+#include "pm_host.h"
+
+using namespace pm;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ int draw_opponent(const pm_rnn_selfplay& sp, int i, uint32_t ns) {
+    // use_pool_opponent = pool and random() < ratio; opponent = random.choice(pool) (:735-736)
+    const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
+    return (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rsp_init(const pm_rnn_selfplay sp) {
+    __shared__ float lds[kBlock][7];
+    const int i0 = blockIdx.x * kBlock;
+    const int i = i0 + threadIdx.x;
+    float oA[7] = {0}, oB[7] = {0};
+    if (i < sp.n) {
+        const uint32_t ns = (uint32_t)sp.st.serves[i];
+        sp.opp[i] = draw_opponent(sp, i, ns);
+        Arena a;
+        double vx, vy, spn;
+        philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
+        serve(a, vx, vy, spn);
+        store_arena(sp.st, i, a);
+        sp.st.serves[i] = (int32_t)ns + 1;
+        sp.ep_reward[i] = 0.f;
+        sp.ep_len[i] = 0;
+        sp.reset[i] = 1;  // init_hidden for both players (:744-746)
+        observe(a, oA, oB);
+    }
+    store_rows7(sp.obsA, lds, oA, i0, sp.n);
+    store_rows7(sp.obsB, lds, oB, i0, sp.n);
+}
+
+__global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
+    __shared__ float lds[kBlock][7];
+    __shared__ long long red[kBlock / 64][6];
+    const int i0 = blockIdx.x * kBlock;
+    const int i = i0 + threadIdx.x;
+    const bool valid = i < sp.n;
+    const int ii = valid ? i : sp.n - 1;
+    const uint64_t step = sp.ctrl->step;
+    Arena a = load_arena(sp.st, ii);
+    const int aA = sp.aA[ii], aB = sp.aB[ii], o = sp.opp[ii];
+    float oA[7], oB[7];
+    observe(a, oA, oB);  // the observation the actions were chosen on
+    float rA, rB;
+    const int d = tick(sp.env, a, aA, aB, rA, rB);
+    float nA[7], nB[7];
+    observe(a, nA, nB);
+    const float er = sp.ep_reward[ii] + rB;  // episode_reward_b += reward_B (:765)
+    const int len = sp.ep_len[ii] + 1;
+    const bool fin = valid && d;
+    {   // per-block partials, no atomics: finished, vs-A, wins vs A, vs-pool, wins vs pool, reward
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const bool win = er > 0.f;  // win_flag = episode_reward_b > 0 (:783)
+        const unsigned long long mf = __ballot(fin), mA = __ballot(fin && o == 0), mwA = __ballot(fin && o == 0 && win);
+        const unsigned long long mP = __ballot(fin && o != 0), mwP = __ballot(fin && o != 0 && win);
+        int rs = fin ? (int)er : 0;
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) rs += __shfl_xor(rs, s);
+        if (lane == 0) {
+            red[wv][0] = __popcll(mf); red[wv][1] = __popcll(mA); red[wv][2] = __popcll(mwA);
+            red[wv][3] = __popcll(mP); red[wv][4] = __popcll(mwP); red[wv][5] = rs;
+        }
+    }
+    if (valid) {
+        // memory.push_step(obs_B, act_B, reward_B, next_obs_B, done) (:770, :107-110)
+        float4* row = reinterpret_cast<float4*>(sp.trans + ((int64_t)(step % (uint64_t)sp.depth) * sp.n + i) * PM_TRANS_F);
+        row[0] = make_float4(oB[0], oB[1], oB[2], oB[3]);
+        row[1] = make_float4(oB[4], oB[5], oB[6], rB);
+        row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
+        row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
+        int keep = 0;
+        if (d) {  // episode over: stored when len >= trace_length (:112-115); next opponent, env.reset()
+            keep = len >= sp.T ? len : 0;
+            const uint32_t ns = (uint32_t)sp.st.serves[i];
+            sp.opp[i] = draw_opponent(sp, i, ns);
+            double vx, vy, spn;
+            philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
+            serve(a, vx, vy, spn);
+            sp.st.serves[i] = (int32_t)ns + 1;
+            observe(a, nA, nB);
+        }
+        store_arena(sp.st, i, a);
+        sp.ep_reward[i] = d ? 0.f : er;
+        sp.ep_len[i] = d ? 0 : len;
+        sp.reset[i] = (uint8_t)d;
+        sp.fin[i] = keep;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        long long t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
+        sp.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = t;
+    }
+    store_rows7(sp.obsA, lds, nA, i0, sp.n);
+    store_rows7(sp.obsB, lds, nB, i0, sp.n);
+}
+
+constexpr int kAppend = 1024;
+
+__global__ __launch_bounds__(kAppend) void k_rsp_append(const pm_rnn_selfplay sp) {
+    __shared__ int cnt[kAppend];
+    __shared__ long long tot[6];
+    const int t = threadIdx.x;
+    pm_rnn_ctrl* c = sp.ctrl;
+    const int nblk = (sp.n + kBlock - 1) / kBlock;
+    if (t < 6) {
+        long long s = 0;
+        for (int b = 0; b < nblk; ++b) s += sp.partials[(size_t)b * 8 + t];
+        tot[t] = s;
+    }
+    const int per = (sp.n + kAppend - 1) / kAppend;
+    const int lo = min(sp.n, t * per), hi = min(sp.n, lo + per);
+    int k = 0;
+    for (int j = lo; j < hi; ++j) k += sp.fin[j] > 0;
+    cnt[t] = k;
+    __syncthreads();
+    for (int s = 1; s < kAppend; s <<= 1) {  // inclusive scan
+        const int v = t >= s ? cnt[t - s] : 0;
+        __syncthreads();
+        cnt[t] += v;
+        __syncthreads();
+    }
+    const int64_t base = c->seq_count;
+    const uint64_t step = c->step;
+    int64_t e = base + cnt[t] - k;
+    for (int j = lo; j < hi; ++j) {
+        const int L = sp.fin[j];
+        if (L > 0) {
+            const int64_t slot = e % sp.seq_cap;
+            sp.seq_eps[2 * slot] = (int64_t)(uint32_t)j | ((int64_t)L << 32);
+            sp.seq_eps[2 * slot + 1] = (int64_t)step - L + 1;
+            ++e;
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        const int64_t total = cnt[kAppend - 1];
+        c->seq_count = base + total;
+        c->seq_size = c->seq_count < sp.seq_cap ? c->seq_count : sp.seq_cap;
+        c->episodes += tot[0];
+        c->ep_A += tot[1]; c->win_A += tot[2]; c->ep_P += tot[3]; c->win_P += tot[4];
+        c->reward_B += (double)tot[5];
+        double eps = c->epsilon;
+        for (long long q = 0; q < tot[0]; ++q) {  // epsilon = max(min_epsilon, epsilon * decay), per episode
+            eps = eps * sp.epsilon_decay;
+            if (eps < sp.min_epsilon) eps = sp.min_epsilon;
+        }
+        c->epsilon = eps;
+        c->step = step + 1;
+    }
+}
+
+struct SampleOut {
+    float *obs, *next, *rew;
+    int32_t* act;
+    uint8_t* done;
+    int B, T;
+};
+
+__global__ __launch_bounds__(256) void k_rsp_sample(const pm_rnn_selfplay sp, SampleOut o) {
+    pm_rnn_ctrl* c = sp.ctrl;
+    const int64_t size = c->seq_size;
+    const bool en = size > sp.min_episodes && size > 0;
+    if (threadIdx.x == 0) { *sp.enable = en; c->train = en; }
+    if (!en) return;
+    const uint64_t now = c->step;  // steps [0, now) written; slot s % depth holds the latest s
+    const int64_t first = c->seq_count - size;
+    for (int b = threadIdx.x; b < o.B; b += blockDim.x) {
+        // np.random.choice(len(buffer), batch, replace=True), then randint(0, len - T + 1) (:131, :147)
+        const U4 r = philox64((uint32_t)b, TAG_SEQ, now, sp.seed_env);
+        const int64_t j = below(r.x, (uint32_t)size);
+        const int64_t slot = (first + j) % sp.seq_cap;
+        const int64_t packed = sp.seq_eps[2 * slot];
+        const int arena = (int)(packed & 0xffffffff), L = (int)(packed >> 32);
+        const int64_t start = sp.seq_eps[2 * slot + 1] + below(r.y, (uint32_t)(L - o.T + 1));
+        for (int tau = 0; tau < o.T; ++tau) {
+            const int64_t s = start + tau;
+            if ((int64_t)now - 1 - s >= sp.depth) atomicOr(&c->status, 1);  // overwritten
+            const float4* row =
+                reinterpret_cast<const float4*>(sp.trans + ((s % sp.depth) * (int64_t)sp.n + arena) * PM_TRANS_F);
+            const float4 r0 = row[0], r1 = row[1], r2 = row[2], r3 = row[3];
+            float* ob = o.obs + ((int64_t)b * o.T + tau) * 7;
+            float* nx = o.next + ((int64_t)b * o.T + tau) * 7;
+            ob[0] = r0.x; ob[1] = r0.y; ob[2] = r0.z; ob[3] = r0.w; ob[4] = r1.x; ob[5] = r1.y; ob[6] = r1.z;
+            nx[0] = r2.x; nx[1] = r2.y; nx[2] = r2.z; nx[3] = r2.w; nx[4] = r3.x; nx[5] = r3.y; nx[6] = r3.z;
+            const int bits = __float_as_int(r3.w);
+            o.rew[(int64_t)b * o.T + tau] = r1.w;
+            o.act[(int64_t)b * o.T + tau] = bits & 0xff;
+            o.done[(int64_t)b * o.T + tau] = (uint8_t)(bits >> 8);
+        }
+    }
+}
+
+int check(const pm_rnn_selfplay* sp) {
+    PM_REQUIRE(sp, PM_E_ARG, "pm_rnn_selfplay: null descriptor");
+    PM_REQUIRE(sp->n > 0 && sp->n_pool >= 0, PM_E_SIZE, "pm_rnn_selfplay: n %d, n_pool %d", sp->n, sp->n_pool);
+    PM_REQUIRE(sp->T >= 1 && sp->depth > sp->T && sp->seq_cap >= 1, PM_E_SIZE, "pm_rnn_selfplay: T %d depth %d",
+               sp->T, sp->depth);
+    PM_REQUIRE(sp->opp && sp->ep_reward && sp->ep_len && sp->reset && sp->w_opp && sp->paramsB && sp->w_B && sp->hA &&
+                   sp->cA && sp->hB && sp->cB && sp->obsA && sp->obsB && sp->aA && sp->aB && sp->trans && sp->seq_eps &&
+                   sp->fin && sp->partials && sp->enable && sp->ctrl,
+               PM_E_ARG, "pm_rnn_selfplay: null buffer");
+    PM_REQUIRE((((uintptr_t)sp->trans) & 15) == 0, PM_E_ARG, "pm_rnn_selfplay: trans must be 16-byte aligned");
+    return PM_OK;
+}
+
+}  // namespace
+
+extern "C" int pm_rnn_selfplay_init(const pm_rnn_selfplay* sp, void* stream) {
+    if (int rc = check(sp)) return rc;
+    hipLaunchKernelGGL(k_rsp_init, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *sp);
+    PM_LAUNCHED("k_rsp_init");
+    return PM_OK;
+}
+
+extern "C" int pm_rnn_selfplay_rollout(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {
+    if (int rc = check(sp)) return rc;
+    hipStream_t st = pm_stream(stream);
+    const uint64_t* ctr = &sp->ctrl->step;
+    // modelB.reset_noise() then act (:385-387): one noise draw per vector step for all arenas
+    if (int rc = pm_rnn_fold(sp->paramsB, sp->paramsB, PM_FOLD_TRAIN_FRESH, sp->seed_net, 0, ctr, sp->w_B, 1, stream))
+        return rc;
+    if (int rc = pm_rnn_act(sp->w_opp, sp->opp, 1 + sp->n_pool, sp->w_B, sp->obsA, sp->obsB, sp->hA, sp->cA, sp->hB,
+                            sp->cB, sp->reset, 0.f, &sp->ctrl->epsilon, sp->seed_env, 0, ctr, sp->aA, sp->aB, nullptr,
+                            nullptr, sp->n, sp->chunk_A, sp->chunk_P, stream))
+        return rc;
+    hipLaunchKernelGGL(k_rsp_env, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, st, *sp);
+    PM_LAUNCHED("k_rsp_env");
+    hipLaunchKernelGGL(k_rsp_append, dim3(1), dim3(kAppend), 0, st, *sp);
+    PM_LAUNCHED("k_rsp_append");
+    if (d) {
+        PM_REQUIRE(d->T == sp->T, PM_E_ARG, "pm_rnn_selfplay: learner T %d != %d", d->T, sp->T);
+        const SampleOut o{const_cast<float*>(d->obs), const_cast<float*>(d->next), const_cast<float*>(d->rew),
+                          const_cast<int32_t*>(d->act), const_cast<uint8_t*>(d->done), d->batch, d->T};
+        hipLaunchKernelGGL(k_rsp_sample, dim3(1), dim3(256), 0, st, *sp, o);
+        PM_LAUNCHED("k_rsp_sample");
+    }
+    return PM_OK;
+}
+
+extern "C" int pm_rnn_selfplay_step(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {
+    PM_REQUIRE(d, PM_E_ARG, "pm_rnn_selfplay_step: null learner");
+    if (int rc = pm_rnn_selfplay_rollout(sp, d, stream)) return rc;
+    return pm_drqn_update(d, stream);
+}

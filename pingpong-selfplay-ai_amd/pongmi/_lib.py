@@ -72,9 +72,26 @@ class DrqnStats(ctypes.Structure):
 
 class Drqn(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("params", "target", "adam_m", "adam_v", "grad", "work", "stats", "obs", "next",
-                                        "act", "rew", "done")] + \
-        [("batch", c_i32), ("T", c_i32), ("world", c_i32), ("_pad", c_i32), ("target_update_interval", c_i64)] + \
+                                        "act", "rew", "done", "enable")] + \
+        [("batch", c_i32), ("T", c_i32), ("target_update_interval", c_i64)] + \
         [(n, c_double) for n in ("gamma", "lr", "beta1", "beta2", "adam_eps", "max_norm")]
+
+
+class RnnCtrl(ctypes.Structure):
+    _fields_ = [("step", c_u64), ("episodes", c_i64), ("seq_count", c_i64), ("seq_size", c_i64), ("epsilon", c_double),
+                ("win_A", c_i64), ("ep_A", c_i64), ("win_P", c_i64), ("ep_P", c_i64), ("reward_B", c_double),
+                ("status", c_i32), ("train", c_i32)]
+
+
+class RnnSelfPlay(ctypes.Structure):
+    _fields_ = [("env", EnvParams), ("st", EnvState)] + \
+        [(n, c_void_p) for n in ("opp", "ep_reward", "ep_len", "reset", "w_opp", "paramsB", "w_B", "hA", "cA", "hB",
+                                 "cB", "obsA", "obsB", "aA", "aB", "trans", "seq_eps", "fin", "partials", "enable",
+                                 "ctrl")] + \
+        [(n, c_i32) for n in ("n", "n_pool", "depth", "T", "chunk_A", "chunk_P")] + \
+        [("seq_cap", c_i64), ("min_episodes", c_i64)] + \
+        [(n, c_double) for n in ("min_epsilon", "epsilon_decay", "pool_ratio")] + \
+        [("seed_env", c_u64), ("seed_net", c_u64)]
 
 
 CTRL_DTYPE_BYTES = ctypes.sizeof(Ctrl)
@@ -99,6 +116,9 @@ _SIGS = {
     "pm_drqn_grads": (c_i32, [c_void_p, c_void_p]),
     "pm_drqn_apply": (c_i32, [c_void_p, c_void_p]),
     "pm_drqn_update": (c_i32, [c_void_p, c_void_p]),
+    "pm_rnn_selfplay_init": (c_i32, [c_void_p, c_void_p]),
+    "pm_rnn_selfplay_rollout": (c_i32, [c_void_p, c_void_p, c_void_p]),
+    "pm_rnn_selfplay_step": (c_i32, [c_void_p, c_void_p, c_void_p]),
     "pm_per_work_bytes": (c_i64, [c_i64]),
     "pm_per_sample": (c_i32, [c_void_p, c_i64, c_float, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_i32,
                               c_void_p, c_void_p]),
@@ -139,7 +159,8 @@ def load():
         f.argtypes = args
     if L.pm_abi_version() != ABI_VERSION:
         raise PongmiError(f"libpongmi ABI {L.pm_abi_version()} != {ABI_VERSION}")
-    for which, cls in ((0, EnvParams), (1, EnvState), (2, Ctrl), (3, SelfPlay), (4, Drqn), (5, DrqnStats)):
+    for which, cls in ((0, EnvParams), (1, EnvState), (2, Ctrl), (3, SelfPlay), (4, Drqn), (5, DrqnStats), (6, RnnCtrl),
+                       (7, RnnSelfPlay)):
         if L.pm_sizeof(which) != ctypes.sizeof(cls):
             raise PongmiError(f"struct layout mismatch for {cls.__name__}: C {L.pm_sizeof(which)} "
                               f"vs ctypes {ctypes.sizeof(cls)}")

@@ -7,8 +7,10 @@ and next and targetB on next from zero state, double-DQN target, smooth-L1, BPTT
 Adam, target sync every target_update_interval steps — no host synchronisation.
 
 For data-parallel training, grads() / apply() split the update around the gradient all-reduce:
-every rank computes its gradient, the ranks sum `grad` (pongmi.dist), then apply() divides by the
-world size and runs the clip on the global norm and the identical Adam step on every rank.
+every rank computes its gradient into `grad` ([PM_RNN_NPARAM] gradients, then a 1 marking a
+contributing rank), the ranks sum `grad` (one all-reduce), then apply() divides by the number of
+contributing ranks and runs the clip on the global norm and the identical Adam step on every rank.
+A rank whose `enable` flag is 0 (its sequence buffer not yet full enough) contributes zeros.
 """
 import ctypes
 
@@ -21,7 +23,7 @@ from .rnn import pack_state_dict, unpack_state_dict
 
 class DRQNLearner:
     def __init__(self, modelB, target=None, *, batch=64, T=8, gamma=0.99, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
-                 max_norm=1.0, target_update_interval=2000, world=1, device="cuda"):
+                 max_norm=1.0, target_update_interval=2000, enable=None, device="cuda"):
         """modelB / target: a QNetRNN module, its state_dict, or a packed [PM_RNN_NP] tensor;
         target None = a copy of modelB (targetB.load_state_dict(modelB.state_dict()), :336-338)."""
         self.lib = _lib.load()
@@ -30,7 +32,7 @@ class DRQNLearner:
         self.target = self._block(target) if target is not None else self.params.clone()
         self.adam_m = torch.zeros(PM_RNN_NPARAM, dtype=torch.float32, device=self.device)
         self.adam_v = torch.zeros(PM_RNN_NPARAM, dtype=torch.float32, device=self.device)
-        self.grad = torch.zeros(PM_RNN_NPARAM, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(PM_RNN_NPARAM + 4, dtype=torch.float32, device=self.device)
         self.batch, self.T = int(batch), int(T)
         nbytes = self.lib.pm_drqn_work_bytes(self.batch, self.T)
         if nbytes < 0:
@@ -46,7 +48,9 @@ class DRQNLearner:
         for name in ("params", "target", "adam_m", "adam_v", "grad", "work", "obs", "next", "act", "rew", "done"):
             setattr(d, name, getattr(self, name).data_ptr())
         d.stats = self.stats_buf.data_ptr()
-        d.batch, d.T, d.world = self.batch, self.T, int(world)
+        self.enable = enable  # optional int32 device flag (the self-play sampler's)
+        d.enable = enable.data_ptr() if enable is not None else None
+        d.batch, d.T = self.batch, self.T
         d.target_update_interval = int(target_update_interval)
         d.gamma, d.lr, d.beta1, d.beta2, d.adam_eps, d.max_norm = float(gamma), float(lr), float(betas[0]), \
             float(betas[1]), float(eps), float(max_norm)

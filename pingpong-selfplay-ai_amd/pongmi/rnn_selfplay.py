@@ -1,0 +1,167 @@
+"""The batched QNetRNN self-play learner: scripts/train_rnn_iterative.py's hot loop (:731-798) for n
+arenas per device — fold + act (K5) + env / sequence store (K7) + DRQN update (K6) per vector step
+on one stream, every loop counter in a device control block (no host synchronisation).
+
+Semantics the batching fixes (the reference steps ONE env and runs train_step_rnn once per step):
+  * one vector step = one env step in every arena, then one DRQN update of `batch` sequences once
+    the sequence buffer holds > batch * min_episodes_for_training_start episodes (:768);
+  * modelB's acting noise is drawn fresh once per vector step and shared by all arenas (the
+    reference resets it before each greedy action, :385); the update uses modelB's epsilon buffers
+    as that draw left them (train_step_rnn does not reset noise);
+  * epsilon decays once per finished episode (:798), applied after the vector step;
+  * each episode plays modelA or (p = opponent_pool_ratio) a uniformly drawn pool net (:735-736),
+    every opponent in eval mode (:344, :615); both players start each episode from zero (h, c);
+  * the sequence buffer keeps the latest `memory_size` episodes of length >= trace_length
+    (deque(maxlen), :104, :112-115); their steps live in per-arena rings of `depth` steps.
+    The reference's max_episode_steps cut (:751, 1000 steps) is not applied (episodes average
+    ~38 steps).
+Sharded (world > 1): every rank owns n arenas and its own sequence buffer; the gradient (+ the
+contributing-rank count) is summed by one all-reduce per update and every rank applies the
+identical clip + Adam step (pongmi.drqn).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import PM_RNN_NW, PM_TRANS_F, check, ptr, stream_ptr
+from .dist import shard_seeds
+from .drqn import DRQNLearner
+from .env import env_config, env_params
+from .rnn import fold, pack_state_dict, unpack_state_dict
+from .selfplay import act_chunk
+
+
+def ring_depth(n, memory_size, mean_len=40, margin=512):
+    """Steps per arena ring: the span of the newest `memory_size` episodes (~memory_size * mean_len / n
+    vector steps) with 50 % headroom, plus room for long episodes; a power of two."""
+    need = int(1.5 * memory_size * mean_len / max(n, 1)) + margin
+    d = 64
+    while d < need:
+        d *= 2
+    return d
+
+
+class RNNSelfPlayLearner:
+    def __init__(self, env_kw, n_arenas, modelB_state, modelA_state=None, pool_states=(), *, batch=64, trace_length=8,
+                 memory_size=200_000, min_episodes_for_training_start=10, depth=None, gamma=0.99, lr=1e-4,
+                 epsilon=1.0, min_epsilon=0.05, epsilon_decay=0.999, target_update_interval=2000, pool_ratio=0.4,
+                 grad_clip_norm=1.0, episode=0, seed=0, rank=0, world=1, allreduce=None, device=None):
+        self.lib = _lib.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise _lib.PongmiError("RNNSelfPlayLearner runs on a ROCm device only")
+        self.n, self.T, self.cap = int(n_arenas), int(trace_length), int(memory_size)
+        self.world, self.rank = int(world), int(rank)
+        if self.world > 1 and allreduce is None:
+            raise ValueError("world > 1 needs an allreduce(tensor) callable (torch.distributed.all_reduce)")
+        self.allreduce = allreduce
+        self.env_cfg = env_config(**env_kw)
+        self.depth = int(depth) if depth else ring_depth(self.n, self.cap)
+        dev, n = self.device, self.n
+        f32 = dict(dtype=torch.float32, device=dev)
+        # ---- environment SoA + per-arena bookkeeping
+        self.f64 = torch.zeros((7, n), dtype=torch.float64, device=dev)
+        self.i32 = torch.zeros((4, n), dtype=torch.int32, device=dev)
+        self.opp = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.ep_reward = torch.zeros(n, **f32)
+        self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.reset = torch.ones(n, dtype=torch.uint8, device=dev)
+        self.hA, self.cA, self.hB, self.cB = (torch.zeros((n, 128), **f32) for _ in range(4))
+        self.obsA = torch.zeros((n, 7), **f32)
+        self.obsB = torch.zeros((n, 7), **f32)
+        self.aA = torch.zeros(n, dtype=torch.int8, device=dev)
+        self.aB = torch.zeros(n, dtype=torch.int8, device=dev)
+        # ---- sequence buffer
+        self.trans = torch.zeros((self.depth, n, PM_TRANS_F), **f32)
+        self.seq_eps = torch.zeros((self.cap, 2), dtype=torch.int64, device=dev)
+        self.fin = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
+        self.enable = torch.zeros(1, dtype=torch.int32, device=dev)
+        # ---- networks
+        self.learner = DRQNLearner(modelB_state, batch=batch, T=self.T, gamma=gamma, lr=lr, max_norm=grad_clip_norm,
+                                   target_update_interval=target_update_interval, enable=self.enable, device=dev)
+        self.batch = self.learner.batch
+        self.w_B = torch.zeros(PM_RNN_NW, **f32)
+        self.n_pool = len(pool_states)
+        self.w_opp = torch.zeros((1 + self.n_pool, PM_RNN_NW), **f32)
+        self.set_modelA(modelA_state if modelA_state is not None else modelB_state)
+        if self.n_pool:
+            pool = torch.stack([pack_state_dict(s, dev) for s in pool_states])
+            self.w_opp[1:] = fold(pool, _lib.PM_FOLD_EVAL)  # m_rnn.eval() (:615-617)
+        # ---- control block
+        c = _lib.RnnCtrl()
+        c.epsilon = float(epsilon)
+        c.episodes = int(episode)
+        self.ctrl = torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8).to(dev)
+
+        sp = _lib.RnnSelfPlay()
+        sp.env = env_params(**env_kw)
+        sp.st = _lib.EnvState(*[ptr(self.f64[k]) for k in range(7)], *[ptr(self.i32[k]) for k in range(4)])
+        for name in ("opp", "ep_reward", "ep_len", "reset", "w_opp", "w_B", "hA", "cA", "hB", "cB", "obsA", "obsB", "aA",
+                     "aB", "trans", "seq_eps", "fin", "partials", "enable", "ctrl"):
+            setattr(sp, name, ptr(getattr(self, name)))
+        sp.paramsB = ptr(self.learner.params)
+        sp.n, sp.n_pool, sp.depth, sp.T = n, self.n_pool, self.depth, self.T
+        p_pool = pool_ratio if self.n_pool else 0.0
+        sp.chunk_A = act_chunk(1.0 - p_pool, cap=2048)
+        sp.chunk_P = act_chunk(p_pool / self.n_pool, cap=2048) if self.n_pool else 256
+        sp.seq_cap = self.cap
+        sp.min_episodes = int(self.batch * min_episodes_for_training_start)
+        sp.min_epsilon, sp.epsilon_decay, sp.pool_ratio = float(min_epsilon), float(epsilon_decay), float(pool_ratio)
+        self.seed = int(seed)
+        sp.seed_env, sp.seed_net = shard_seeds(self.seed, self.rank)
+        self.sp = sp
+        check(self.lib.pm_rnn_selfplay_init(ctypes.byref(sp), stream_ptr()), "pm_rnn_selfplay_init")
+
+    # ------------------------------------------------------------------ stepping
+    def rollout(self):
+        """fold + act + env + sequence store + batch sample (no update)."""
+        check(self.lib.pm_rnn_selfplay_rollout(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),
+              "pm_rnn_selfplay_rollout")
+
+    def step(self):
+        """One vector step (n env-steps on this rank) including the DRQN update when enabled."""
+        if self.world == 1:
+            check(self.lib.pm_rnn_selfplay_step(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),
+                  "pm_rnn_selfplay_step")
+            return
+        self.rollout()
+        self.learner.grads()
+        self.allreduce(self.learner.grad)  # one RCCL all-reduce per update: 174 984 grads + rank count
+        self.learner.apply()
+
+    # ------------------------------------------------------------------ state readout (syncs)
+    def counters(self):
+        c = _lib.RnnCtrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))
+        out = {k: getattr(c, k) for k, _ in _lib.RnnCtrl._fields_}
+        out["train_steps"] = self.learner.stats()["steps"]
+        return out
+
+    def set_epsilon(self, eps):
+        c = _lib.RnnCtrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))
+        c.epsilon = float(eps)
+        self.ctrl.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
+
+    def set_modelA(self, state):
+        """Opponent slot 0: modelA, frozen and in eval mode (train_rnn_iterative.py:343-344)."""
+        self.paramsA = pack_state_dict(state, self.device)
+        self.w_opp[0] = fold(self.paramsA, _lib.PM_FOLD_EVAL)[0]
+
+    def modelB_state_dict(self):
+        return unpack_state_dict(self.learner.params)
+
+    def targetB_state_dict(self):
+        return unpack_state_dict(self.learner.target)
+
+    def modelA_state_dict(self):
+        return unpack_state_dict(self.paramsA)
+
+    def episodes(self):
+        """The stored episodes, oldest first: (arena, first step, length) int64 [seq_size, 3] (host)."""
+        c = self.counters()
+        size, count = c["seq_size"], c["seq_count"]
+        raw = self.seq_eps.cpu()
+        idx = (torch.arange(count - size, count) % self.cap)
+        e = raw[idx]
+        return torch.stack([e[:, 0] & 0xFFFFFFFF, e[:, 1], e[:, 0] >> 32], 1)

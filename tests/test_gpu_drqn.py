@@ -105,14 +105,31 @@ def test_drqn_deterministic_world_and_target_sync(golden):
     b = tuple(torch.from_numpy(x) for x in _batch(gd, 1))
     runs = []
     for world in (1, 1, 2):
-        L = DRQNLearner(_sd(gr), batch=64, T=8, world=world, target_update_interval=2)
+        L = DRQNLearner(_sd(gr), batch=64, T=8, target_update_interval=2)
         for step in (1, 2):
             L.grads(*b)
             if world == 2:
-                L.grad.mul_(2.0)  # what the all-reduce of two identical replicas leaves
+                L.grad.mul_(2.0)  # what the all-reduce of two identical replicas leaves (flag slot: 2 ranks)
             L.apply()
             assert torch.equal(L.params, L.target) == (step == 2)  # synced at step 2
         runs.append((L.params.clone(), L.adam_m.clone(), L.adam_v.clone(), L.stats()))
     for r in runs[1:]:
         assert torch.equal(r[0], runs[0][0]) and torch.equal(r[1], runs[0][1]) and torch.equal(r[2], runs[0][2])
         assert r[3] == runs[0][3]
+
+
+def test_drqn_disabled_replica_contributes_nothing(golden):
+    """enable = 0: grads() zeroes the gradient and the rank count; apply() then leaves everything
+    untouched — a rank whose sequence buffer is not ready yet sits out an all-reduce."""
+    from pongmi.drqn import DRQNLearner
+    gr, gd = golden("rnn"), golden("drqn")
+    en = torch.zeros(1, dtype=torch.int32, device="cuda")
+    L = DRQNLearner(_sd(gr), batch=64, T=8, enable=en)
+    p0 = L.params.clone()
+    L.grad.fill_(3.0)
+    L.update(*(torch.from_numpy(x) for x in _batch(gd, 0)))
+    assert torch.count_nonzero(L.grad) == 0 and torch.equal(L.params, p0) and L.stats()["steps"] == 0
+    en.fill_(1)
+    L.update()
+    assert L.grad[-4].item() == 1.0 and L.stats()["steps"] == 1 and not torch.equal(L.params, p0)
+    np.testing.assert_allclose(L.stats()["loss"], gd["u0_loss"], rtol=1e-4)

@@ -1,0 +1,198 @@
+"""The QNetRNN self-play loop (pm_rnn_selfplay_*, K7) — train_rnn_iterative.py:731-798 batched:
+
+1. step by step against the oracle env + pm_rnn_q: actions are the argmax of each player's QNetRNN
+   with (h, c) carried and zeroed at episode start, the transition ring records
+   push_step(obs_B, act_B, reward_B, next_obs_B, done) exactly, finished arenas redraw their
+   opponent and re-serve (Philox), bookkeeping matches;
+2. the sequence buffer: every stored episode is one contiguous trajectory of >= T steps ending in
+   done, the latest memory_size are kept, sampled sequences are windows of stored episodes, the
+   update runs exactly when len(memory) > batch * min_episodes_for_training_start, epsilon decays
+   once per finished episode;
+3. determinism, and two data-parallel ranks (gradient sum + contributing-rank count) stay identical.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ENV_KW = dict(paddle_width=0.2, paddle_speed=0.03, max_score=3, enable_spin=True, magnus_factor=0.025, restitution=1.0,
+              friction=0.6, ball_mass=1.0, world_ball_radius=0.03, ball_speed_range=[0.03, 0.05],
+              spin_range=[-5, 5], ball_angle_intervals=[[-60, -30], [30, 60]], speed_scale_every=5,
+              speed_increment=0.2)  # config_rnn.yaml:6-28
+
+
+def _rnn_sd(seed):
+    from models.qnet_rnn import QNetRNN
+    torch.manual_seed(seed)
+    return {k: v.clone() for k, v in QNetRNN(7, 3).state_dict().items()}
+
+
+def _golden_sd(g):
+    return {k[7:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("params.")}
+
+
+def _learner(golden, n=256, n_pool=2, **kw):
+    from pongmi.rnn_selfplay import RNNSelfPlayLearner
+    g = golden("rnn")
+    pool = [_rnn_sd(200 + k) for k in range(n_pool)]
+    return RNNSelfPlayLearner(ENV_KW, n, _golden_sd(g), _rnn_sd(7), pool, **kw)
+
+
+def _snap(L):
+    torch.cuda.synchronize()
+    t = lambda x: x.detach().cpu().numpy().copy()  # noqa: E731
+    return dict(f64=t(L.f64), i32=t(L.i32), opp=t(L.opp), er=t(L.ep_reward), el=t(L.ep_len), reset=t(L.reset),
+                obsA=t(L.obsA), obsB=t(L.obsB), hA=L.hA.clone(), cA=L.cA.clone(), hB=L.hB.clone(), cB=L.cB.clone(),
+                ctrl=L.counters())
+
+
+def test_rnn_selfplay_steps_match_oracle(golden, orc):
+    from pongmi import rnn
+    L = _learner(golden, n=256, n_pool=2, epsilon=0.0, min_epsilon=0.0, pool_ratio=0.5,
+                 min_episodes_for_training_start=10 ** 6, memory_size=4096, seed=3)
+    n, sp = L.n, L.sp
+    pv = orc.env_params_from_kwargs(**ENV_KW)
+    P = orc.make_params(pv)
+    names = ("x", "y", "vx", "vy", "spin", "top", "bot")
+    finished = 0
+    for k in range(60):
+        pre = _snap(L)
+        L.step()
+        post = _snap(L)
+        aA = L.aA.cpu().numpy().astype(np.int64)
+        aB = L.aB.cpu().numpy().astype(np.int64)
+        # ---- acting: the same kernel path on the tracked states
+        z = torch.from_numpy(pre["reset"].astype(bool)).cuda()
+        hA, cA, hB, cB = (pre[s].clone() for s in ("hA", "cA", "hB", "cB"))
+        for s in (hA, cA, hB, cB):
+            s[z] = 0
+        qB = rnn.q_step(L.w_B, torch.from_numpy(pre["obsB"]).cuda(), hB, cB)
+        qA = torch.empty_like(qB)
+        oppt = torch.from_numpy(pre["opp"]).cuda().long()
+        obsA = torch.from_numpy(pre["obsA"]).cuda()
+        for j in range(L.n_pool + 1):
+            sel = (oppt == j).nonzero().flatten()
+            if sel.numel():
+                h, c = hA[sel].contiguous(), cA[sel].contiguous()
+                qA[sel] = rnn.q_step(L.w_opp[j], obsA[sel], h, c)
+                hA[sel], cA[sel] = h, c
+        assert np.array_equal(aA, qA.argmax(1).cpu().numpy()), f"step {k}: aA"
+        assert np.array_equal(aB, qB.argmax(1).cpu().numpy()), f"step {k}: aB (epsilon 0: greedy)"
+        for s, ref in (("hA", hA), ("cA", cA), ("hB", hB), ("cB", cB)):
+            assert torch.equal(post[s], ref), f"step {k}: {s}"
+        # ---- env tick on the oracle
+        arr = np.zeros(n, orc.ARENA_DTYPE)
+        for j, nm in enumerate(names):
+            arr[nm] = pre["f64"][j]
+        for j, nm in enumerate(("scoreA", "scoreB", "bounces")):
+            arr[nm] = pre["i32"][j]
+        oA, oB = orc.obs_of_arenas(arr)
+        assert np.array_equal(oB, pre["obsB"]) and np.array_equal(oA, pre["obsA"])
+        nA, nB, rew, done = orc.step_arenas(P, arr, aA.astype(np.int8), aB.astype(np.int8))
+        d = done.astype(bool)
+        rows = L.trans[k % L.depth].cpu().numpy()
+        assert np.array_equal(rows[:, 0:7], oB) and np.array_equal(rows[:, 7], rew[:, 1])
+        assert np.array_equal(rows[:, 8:15], nB)
+        bits = rows[:, 15].view(np.int32)
+        assert np.array_equal(bits & 0xFF, aB) and np.array_equal(bits >> 8, done.astype(np.int32))
+        # ---- bookkeeping, next opponent, serve
+        er = pre["er"] + rew[:, 1]
+        ln = pre["el"] + 1
+        ns = pre["i32"][3]
+        q = orc.philox(np.arange(n), orc.TAG_OPP, ns, 0, sp.seed_env)
+        use_pool = orc.u53(q[0], q[1]) < sp.pool_ratio
+        newopp = np.where(use_pool, 1 + orc.below(q[2], L.n_pool), 0)
+        vx, vy, spn = orc.philox_serve(pv, np.arange(n), ns, sp.seed_env)
+        assert np.array_equal(post["opp"][d], newopp[d]) and np.array_equal(post["opp"][~d], pre["opp"][~d])
+        assert np.all(post["er"][d] == 0) and np.array_equal(post["er"][~d], er[~d])
+        assert np.all(post["el"][d] == 0) and np.array_equal(post["el"][~d], ln[~d])
+        assert np.array_equal(post["reset"].astype(bool), d)
+        assert np.all(post["i32"][3][d] == ns[d] + 1) and np.array_equal(post["i32"][3][~d], ns[~d])
+        np.testing.assert_allclose(post["f64"][2][d], vx[d], rtol=4e-16, atol=1e-18)
+        np.testing.assert_allclose(post["f64"][3][d], vy[d], rtol=4e-16, atol=1e-18)
+        assert np.array_equal(post["f64"][4][d], spn[d]) and np.all(post["f64"][0][d] == 0.5)
+        for j, nm in enumerate(names):
+            assert np.array_equal(post["f64"][j][~d], arr[nm][~d]), nm
+        c0, c1 = pre["ctrl"], post["ctrl"]
+        assert c1["step"] == c0["step"] + 1 and c1["episodes"] == c0["episodes"] + d.sum()
+        assert c1["ep_A"] - c0["ep_A"] == (d & (pre["opp"] == 0)).sum()
+        assert c1["win_A"] - c0["win_A"] == (d & (pre["opp"] == 0) & (er > 0)).sum()
+        assert c1["ep_P"] - c0["ep_P"] == (d & (pre["opp"] != 0)).sum()
+        assert c1["seq_count"] - c0["seq_count"] == (d & (ln >= L.T)).sum()
+        finished += int(d.sum())
+    assert finished > 50  # episodes did end and restart during the run
+    assert L.counters()["train_steps"] == 0
+
+
+def test_rnn_sequence_buffer_and_training(golden):
+    T, B, cap = 8, 64, 3000
+    L = _learner(golden, n=2048, n_pool=2, epsilon=1.0, min_epsilon=0.05, epsilon_decay=0.999, memory_size=cap,
+                 min_episodes_for_training_start=1, seed=11)
+    trained = 0
+    for k in range(140):
+        L.step()
+        c = L.counters()
+        trained += c["train"]
+        assert c["train"] == int(c["seq_size"] > B), f"step {k}"
+        assert c["train_steps"] == trained
+    c = L.counters()
+    assert c["status"] == 0 and c["seq_count"] > cap and c["seq_size"] == cap  # wrapped around
+    assert c["episodes"] == c["ep_A"] + c["ep_P"] and c["seq_count"] <= c["episodes"]
+    eps = 1.0
+    for _ in range(c["episodes"]):
+        eps = max(0.05, eps * 0.999)
+    assert c["epsilon"] == eps
+    st = L.learner.stats()
+    assert trained > 50 and st["steps"] == trained and np.isfinite(st["loss"]) and st["norm"] > 0
+    # every stored episode: one contiguous trajectory in its arena's ring, done only on its last step
+    ring = L.trans.cpu().numpy()
+    eps_tab = L.episodes().numpy()
+    assert len(eps_tab) == cap
+    now = c["step"]
+    for arena, start, length in eps_tab[::7]:
+        assert length >= T and start + length - 1 <= now - 1 and now - 1 - start < L.depth
+        rec = ring[(start + np.arange(length)) % L.depth, arena]
+        bits = rec[:, 15].view(np.int32)
+        assert np.all(bits[:-1] >> 8 == 0) and bits[-1] >> 8 == 1
+        assert np.array_equal(rec[1:, 0:7], rec[:-1, 8:15])  # next_obs[t] == obs[t+1]
+    # the sampled batch: windows of stored episodes
+    obs, nxt = L.learner.obs.cpu().numpy(), L.learner.next.cpu().numpy()
+    done = L.learner.done.cpu().numpy()
+    assert np.array_equal(obs[:, 1:], nxt[:, :-1]) and np.all(done[:, :-1] == 0)
+
+
+def test_rnn_selfplay_deterministic(golden):
+    runs = []
+    for _ in range(2):
+        L = _learner(golden, n=1024, n_pool=1, epsilon=0.5, memory_size=2000, min_episodes_for_training_start=1,
+                     seed=4)
+        for _ in range(60):
+            L.step()
+        runs.append((L.learner.params.clone(), L.trans.clone(), L.counters()))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1]) and runs[0][2] == runs[1][2]
+
+
+def test_two_ranks_stay_identical(golden):
+    """world = 2 on one device: each rank its own arenas / buffer (rank-specific env seed), the
+    gradients (+ rank count) summed as the all-reduce would, the same Adam step on both."""
+    from pongmi.rnn_selfplay import RNNSelfPlayLearner
+    g = golden("rnn")
+    Ls = [RNNSelfPlayLearner(ENV_KW, 1024, _golden_sd(g), _rnn_sd(7), [], epsilon=0.5, memory_size=2000,
+                             min_episodes_for_training_start=1, seed=9, rank=r, world=2, allreduce=lambda t: None)
+          for r in range(2)]
+    both = 0
+    for _ in range(70):
+        for L in Ls:
+            L.rollout()
+            L.learner.grads()
+        s = Ls[0].learner.grad + Ls[1].learner.grad
+        ranks = s[-4].item()
+        for L in Ls:
+            L.learner.grad.copy_(s)
+            L.learner.apply()
+        both += ranks == 2
+        assert torch.equal(Ls[0].learner.params, Ls[1].learner.params)
+    assert both > 10
+    assert not torch.equal(Ls[0].trans, Ls[1].trans)  # different arenas per rank
+    assert Ls[0].learner.stats()["steps"] == Ls[1].learner.stats()["steps"] > 0

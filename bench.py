@@ -109,13 +109,140 @@ def cpu_baseline(n, seconds=12.0):
                       f"batch 256), {dt:.1f} s on 1 host core"}
 
 
+ENV_KW_RNN = dict(ENV_KW, restitution=1.0, speed_scale_every=5, speed_increment=0.2)  # config_rnn.yaml:6-28
+# QNetRNN multiply-adds per row: 7(+bias)x64 + 64x128 + 256x512 (LSTM gates) + 128x128 + 128x4 heads
+RNN_MAC = 8 * 64 + 64 * 128 + 256 * 512 + 128 * 128 + 128 * 4
+RNN_FLOP_PER_ARENA = 2 * 2 * RNN_MAC  # both players
+# k_rsp_env: state 136, actions 2, opp 4 + ep_reward 4 + ep_len 4 read, + reset 1 + fin 4 written (21 B),
+# ring record 64 written, next observations 2 x 28 written
+RNN_ENV_BYTES = 136 + 2 + 12 + 21 + 64 + 56
+
+
+def synthetic_rnn(seed):
+    from models.qnet_rnn import QNetRNN
+    torch.manual_seed(seed)
+    return {k: v.clone() for k, v in QNetRNN(7, 3).state_dict().items()}
+
+
+def cpu_baseline_rnn(seconds=12.0, n=2048):
+    from threadpoolctl import threadpool_limits
+    from oracle.cpu_rnn_selfplay import CpuRnnSelfPlay
+    np_sd = lambda s: {k: v.numpy() for k, v in s.items()}  # noqa: E731
+    with threadpool_limits(1):
+        cpu = CpuRnnSelfPlay(ENV_KW_RNN, n, np_sd(synthetic_rnn(1)), np_sd(synthetic_rnn(2)),
+                             [np_sd(synthetic_rnn(100 + k)) for k in range(4)], min_episodes=640)
+        while cpu.t == 0:  # fill the sequence buffer until updates run
+            cpu.step()
+        t0 = time.perf_counter()
+        steps = 0
+        while time.perf_counter() - t0 < seconds:
+            cpu.step()
+            steps += 1
+        dt = time.perf_counter() - t0
+    return {"value": round(n * steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/cpu_rnn_selfplay.py: {steps} vector steps x {n} arenas (QNetRNN acting both players "
+                      f"+ env + sequence buffer + DRQN update 64x8 every step), {dt:.1f} s on 1 host core"}
+
+
+def run_rnn(args, dist, rank, world):
+    """configs[4]: 32768 arenas/GPU, the train_rnn_iterative loop (QNetRNN both players with (h, c)
+    per arena, sequence buffer, DRQN update 64 x 8 with BPTT + clip + Adam every vector step)."""
+    from pongmi.rnn_selfplay import RNNSelfPlayLearner
+    n = args.arenas or 32768
+    pool_n = 4 if args.pool is None else args.pool
+    allreduce = (lambda t: dist.all_reduce(t)) if dist else None
+    L = RNNSelfPlayLearner(ENV_KW_RNN, n, synthetic_rnn(1), synthetic_rnn(2),
+                           [synthetic_rnn(100 + k) for k in range(pool_n)], epsilon=0.05, seed=7, rank=rank,
+                           world=world, allreduce=allreduce)
+
+    def one_step(ev=None):
+        if ev is None:
+            L.step()
+            return
+        ev[0].record()
+        L.act()
+        ev[1].record()
+        L.env_step()
+        ev[2].record()
+        if dist is None:
+            L.learner.update()
+        else:
+            L.learner.grads()
+            dist.all_reduce(L.learner.grad)
+            L.learner.apply()
+        ev[3].record()
+
+    warm = max(args.warmup, 60)  # the sequence buffer holds > 640 episodes (updates run) from ~step 20
+    for _ in range(warm):
+        one_step()
+    torch.cuda.synchronize()
+    c0 = L.counters()
+    inst = set(range(0, args.steps, INSTR))
+    evs = {k: tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for k in inst}
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(evs.get(k))
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    act_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
+    env_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)
+    upd_s = sum(e[2].elapsed_time(e[3]) for e in evs.values()) * 1e-3 / len(evs)
+    c = L.counters()
+    if rank == 0:
+        value = n * world * args.steps / dt
+        achieved = n * RNN_FLOP_PER_ARENA / act_s / 1e12
+        env_gbs = n * RNN_ENV_BYTES / env_s / 1e9
+        out = {
+            "metric": "env-steps/sec (whole node), QNetRNN self-play + DRQN (configs[4])",
+            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": warm,
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64 env state / f32 QNetRNN",
+            "data": "synthetic (random-init QNetRNN weights of the reference architecture, Philox serves)",
+            "config": {"workload": "configs[4]: 32768 arenas/GPU, train_rnn_iterative loop (QNetRNN act both players "
+                                   "with (h, c) per arena + env tick + sequence buffer + DRQN update 64x8 BPTT + "
+                                   "clip + Adam every vector step)",
+                       "arenas_per_gpu": n, "global_arenas": n * world, "pool": pool_n, "batch": 64, "trace_length": 8,
+                       "memory_size": L.cap, "ring_depth": L.depth,
+                       "updates_in_timed_region": c["train_steps"] - c0["train_steps"],
+                       "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)"},
+            "roofline": {"bound": "mfma", "kernel": "k_rnn_act (+ k_rnn_fold)",
+                         "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
+                         "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "avg_us": round(act_s * 1e6, 2), "flop_per_arena": RNN_FLOP_PER_ARENA, "n": n},
+            "env_roofline": {"bound": "hbm", "kernel": "k_rsp_env + k_rsp_append + k_rsp_sample",
+                             "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(env_gbs / PEAK_HBM_GBS, 4), "avg_us": round(env_s * 1e6, 2),
+                             "bytes_per_env_step": RNN_ENV_BYTES},
+            "drqn_update_us": round(upd_s * 1e6, 2),
+            "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
+                        "seq_size": c["seq_size"], "status": c["status"], **L.learner.stats()},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_rnn(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--arenas", type=int, default=65536, help="arenas per GPU")
-    ap.add_argument("--pool", type=int, default=8, help="opponent pool size (synthetic nets)")
+    ap.add_argument("--workload", choices=("dqn", "rnn"), default="dqn",
+                    help="dqn: configs[2] (the headline); rnn: configs[4], the QNetRNN / DRQN loop")
+    ap.add_argument("--arenas", type=int, default=None, help="arenas per GPU (65536 dqn, 32768 rnn)")
+    ap.add_argument("--pool", type=int, default=None, help="opponent pool size (synthetic nets; 8 dqn, 4 rnn)")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--memory", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -131,6 +258,10 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if args.workload == "rnn":
+        return run_rnn(args, dist, rank, world)
+    args.arenas = args.arenas or 65536
+    args.pool = 8 if args.pool is None else args.pool
     from pongmi.selfplay import SelfPlayLearner
 
     sdB, sdA = synthetic_qnet(1), synthetic_qnet(2)

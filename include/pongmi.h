@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 2
+#define PM_ABI_VERSION 3
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -160,11 +160,14 @@ int pm_rnn_q(const float* w_eff, const float* x, float* h, float* c, const uint8
  * fused on the matrix cores: A greedy with w_opp[opp_id[i]] (opp_id NULL = net 0) on obsA and
  * (hA, cA); B on obsB and (hB, cB): random.random() < epsilon ? randint(0,2) : argmax, the forward
  * advancing (hB, cB) either way. reset (nullable) zeroes both players' state first (episode
- * start). Grouping as pm_qnet_act. */
+ * start). Side A is grouped per net: with opp_list / opp_cnt (nullable; per-256-arena-block lists
+ * as pm_selfplay's, consistent with opp_id) every net's arenas are packed into full 128-row groups,
+ * otherwise chunks of chunk0 (net 0) / chunk1 (others) arenas are compacted (0 = 256 / 2048). */
 int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B, const float* obsA,
                const float* obsB, float* hA, float* cA, float* hB, float* cB, const uint8_t* reset, float epsilon,
                const double* eps_dev, uint64_t seed, uint64_t counter, const uint64_t* counter_dev, int8_t* aA,
-               int8_t* aB, float* qA, float* qB, int32_t n, int32_t chunk0, int32_t chunk1, void* stream);
+               int8_t* aB, float* qA, float* qB, int32_t n, int32_t chunk0, int32_t chunk1, const int32_t* opp_list,
+               const int32_t* opp_cnt, void* stream);
 
 /* ---------------------------------------------------------------- DRQN update (K6) */
 
@@ -204,7 +207,8 @@ typedef struct pm_drqn {
 
 int64_t pm_drqn_work_bytes(int32_t batch, int32_t T);
 /* Forward + BPTT: grad <- d loss / d params of this replica's batch, grad[PM_RNN_NPARAM] <- 1
- * (all zero when *enable == 0). */
+ * (all zero when *enable == 0). The NoisyLinear sigma slots are left for pm_drqn_apply, which
+ * forms them as mu gradient x epsilon (linear, identical epsilon on every rank). */
 int pm_drqn_grads(const pm_drqn *d, void *stream);
 /* grad / grad[PM_RNN_NPARAM] -> clip_grad_norm_ -> Adam step -> target sync; stats updated.
  * Nothing happens when grad[PM_RNN_NPARAM] == 0. */
@@ -247,8 +251,10 @@ typedef struct pm_rnn_selfplay {
     int8_t *aA, *aB;       /* [n] */
     float *trans;          /* [depth][n][PM_TRANS_F] per-arena transition rings (s, r, s', a | done << 8) */
     int64_t *seq_eps;      /* [seq_cap][2]: arena | length << 32, first step */
-    int32_t *fin;          /* [n] scratch */
+    int64_t *fin;          /* [ceil(n / 256) * 256][2] scratch: stored episodes staged per env block */
     int64_t *partials;     /* [ceil(n / 256)][8] */
+    int32_t *opp_list;     /* [n] per-256-arena-block opponent lists (written by the env kernel) */
+    int32_t *opp_cnt;      /* [ceil(n / 256)][1 + n_pool] (offset << 16 | count) */
     int32_t *enable;       /* [1] set by the sampler: seq_size > min_episodes */
     pm_rnn_ctrl *ctrl;
     int32_t n, n_pool, depth, T, chunk_A, chunk_P;
@@ -259,7 +265,11 @@ typedef struct pm_rnn_selfplay {
 
 /* Serve every arena, draw its first opponent, zero (h, c). */
 int pm_rnn_selfplay_init(const pm_rnn_selfplay *sp, void *stream);
-/* fold (fresh noise) + act + env + sequence store; then, when d != NULL, sample d's batch. */
+/* modelB's fold with fresh noise + both players' act (K5). */
+int pm_rnn_selfplay_act(const pm_rnn_selfplay *sp, void *stream);
+/* env tick + sequence store + counters; then, when d != NULL, sample d's batch and set *enable. */
+int pm_rnn_selfplay_env(const pm_rnn_selfplay *sp, const pm_drqn *d, void *stream);
+/* pm_rnn_selfplay_act then pm_rnn_selfplay_env. */
 int pm_rnn_selfplay_rollout(const pm_rnn_selfplay *sp, const pm_drqn *d, void *stream);
 /* rollout then pm_drqn_update(d) (d->enable should be sp->enable). */
 int pm_rnn_selfplay_step(const pm_rnn_selfplay *sp, const pm_drqn *d, void *stream);

@@ -13,7 +13,7 @@
 //   bwd   xT    one BPTT step: dz_t from (dh_t, dc_t, the cached gates) into LDS, dh_{t-1} = Whh^T dz_t
 //   wgrad x3    dWih = dZ F2^T, dWhh = dZ H_{t-1}^T, db = rowsum dZ, dF2 = Wih^T dZ (masked by the
 //               ReLU) -> dW2, db2, dF1 -> dW1, db1
-//   sigma       NoisyLinear sigma grads = mu grads * epsilon
+//   (apply)     NoisyLinear sigma grads = mu grads * epsilon, formed in the norm pass
 // then (pm_drqn_apply) the global-norm clip (fp64 partials, fixed order) and torch's Adam.
 // Nothing uses atomics: the update is bit-reproducible run to run.
 #include "pm_gemm.h"
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void k_drqn_prep(DrqnArgs a) {
 
 // ---------------------------------------------------------------- forward LSTM step
 // grid: 3 streams x (B/32) column tiles x 4 hidden blocks; wave q = gate q (torch order i, f, g, o)
-__global__ __launch_bounds__(256) void k_drqn_fwd(DrqnArgs a, int t) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_drqn_fwd(DrqnArgs a, int t) {
     if (skipped(a)) return;
     __shared__ float gate[4][32][33];
     const int B = a.B, C0 = a.C0, ldh = a.ldh, nct = B / 32;
@@ -151,16 +151,25 @@ __global__ __launch_bounds__(256) void k_drqn_fwd(DrqnArgs a, int t) {
     gemm_f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = Zx[(int64_t)(g0 + (r & 3) + 8 * (r >> 2) + 4 * h) * ldz + zc + r32];
-    if (t > 0) {  // + Whh h_{t-1}
+    if (t > 0) {  // + Whh h_{t-1}: all 16 + 64 operand loads of the wave issued before the 64 MFMAs
         const float* __restrict__ Wr = P + R_P_WHH + (int64_t)(g0 + r32) * 128;
         const float* __restrict__ Hc = Hp + t * B + ct * 32 + r32;
-        for (int kb = 0; kb < 128; kb += 8) {
-            const int k0 = kb + 4 * h;
-            const float4 w4 = *reinterpret_cast<const float4*>(Wr + k0);
-            const float wa[4] = {w4.x, w4.y, w4.z, w4.w};
+        float4 w4[16];
+        float hb[64];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[e], Hc[(int64_t)(k0 + e) * ldh], acc, 0, 0, 0);
+        for (int j = 0; j < 16; ++j) {
+            const int k0 = 8 * j + 4 * h;
+            w4[j] = *reinterpret_cast<const float4*>(Wr + k0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) hb[4 * j + e] = Hc[(int64_t)(k0 + e) * ldh];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep every load ahead of the MFMA chain
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w4[j].x, hb[4 * j], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w4[j].y, hb[4 * j + 1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w4[j].z, hb[4 * j + 2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w4[j].w, hb[4 * j + 3], acc, 0, 0, 0);
         }
     }
 #pragma unroll
@@ -199,6 +208,7 @@ __global__ __launch_bounds__(256) void k_drqn_q(DrqnArgs a) {
         const float* eff = s == 2 ? a.effT : a.effB;
         const float* S = s == 0 ? a.S0 : (s == 1 ? a.S1 : a.S2);
         float v = 0.f, x0 = 0.f, x1 = 0.f, x2 = 0.f;
+#pragma unroll 16
         for (int u = 0; u < 128; ++u) {
             const float su = S[u * B + b];
             v += eff[E_V + u] * su;
@@ -238,6 +248,7 @@ __global__ __launch_bounds__(256) void k_drqn_q(DrqnArgs a) {
     if (tid < 128) {
         const int u = tid;
         float gv = 0.f, g0 = 0.f, g1 = 0.f, g2 = 0.f;
+#pragma unroll 16
         for (int b = 0; b < B; ++b) {
             const float su = a.S0[u * B + b];
             gv += dV[b] * su; g0 += dA[b][0] * su; g1 += dA[b][1] * su; g2 += dA[b][2] * su;
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(256) void k_drqn_q(DrqnArgs a) {
 // ---------------------------------------------------------------- one BPTT step
 // grid: 4 unit tiles x (B/32) column tiles. dz_t for all 512 gate rows of the block's columns in
 // LDS; the block writes dz_t / dc_{t-1} for its own 32 units and dh_{t-1} = Whh^T dz_t for them.
-__global__ __launch_bounds__(256) void k_drqn_bwd(DrqnArgs a, int t) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_drqn_bwd(DrqnArgs a, int t) {
     if (skipped(a)) return;
     __shared__ float dz[512][33];
     __shared__ float red[4][16][64];
@@ -272,39 +283,69 @@ __global__ __launch_bounds__(256) void k_drqn_bwd(DrqnArgs a, int t) {
     float* dHout = ((Tn - t) & 1) ? a.dH1 : a.dH0;
     const float* dCin = ((Tn - 1 - t) & 1) ? a.dC1 : a.dC0;
     float* dCout = ((Tn - t) & 1) ? a.dC1 : a.dC0;
-    for (int e = threadIdx.x; e < 4096; e += 256) {
-        const int u = e >> 5, c = e & 31, col = ct * 32 + c;
-        const int64_t gc = (int64_t)t * B + col;
-        const float dh = dHin[u * B + col];
-        const float dcc = t == Tn - 1 ? 0.f : dCin[u * B + col];
-        const float gi = a.G0[(int64_t)u * C0 + gc], gf = a.G0[(int64_t)(128 + u) * C0 + gc];
-        const float gg = a.G0[(int64_t)(256 + u) * C0 + gc], go = a.G0[(int64_t)(384 + u) * C0 + gc];
-        const float cT = a.Cs0[(int64_t)u * ldh + (t + 1) * B + col], cp = a.Cs0[(int64_t)u * ldh + t * B + col];
-        const float tc = tanhf(cT);
-        const float dc = dcc + dh * go * (1.0f - tc * tc);
-        const float dzi = dc * gg * (gi * (1.0f - gi));
-        const float dzf = dc * cp * (gf * (1.0f - gf));
-        const float dzg = dc * gi * (1.0f - gg * gg);
-        const float dzo = dh * tc * (go * (1.0f - go));
-        dz[u][c] = dzi; dz[128 + u][c] = dzf; dz[256 + u][c] = dzg; dz[384 + u][c] = dzo;
-        if ((u >> 5) == mu) {
-            a.dZ[(int64_t)u * C0 + gc] = dzi;
-            a.dZ[(int64_t)(128 + u) * C0 + gc] = dzf;
-            a.dZ[(int64_t)(256 + u) * C0 + gc] = dzg;
-            a.dZ[(int64_t)(384 + u) * C0 + gc] = dzo;
-            dCout[u * B + col] = dc * gf;
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const float* __restrict__ Wc = a.params + R_P_WHH + 32 * mu + (ln & 31);  // A(m = u_out, k = g) = Whh[g][u_out]
+    float wa[64];  // this wave's K quarter of the Whh column, loaded before the elementwise pass
+    if (t > 0) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) wa[4 * j + e] = Wc[(int64_t)(128 * wv + 8 * j + 4 * (ln >> 5) + e) * 128];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 16 (unit, column) pairs per thread in two halves: the 8 operand loads of 8 pairs are issued
+    // before any of their stores (the workspace pointers may alias, so the compiler would not)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        float v[8][8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = threadIdx.x + 256 * (8 * half + q);
+            const int u = e >> 5, col = ct * 32 + (e & 31);
+            const int64_t gc = (int64_t)t * B + col;
+            v[q][0] = dHin[u * B + col];
+            v[q][1] = t == Tn - 1 ? 0.f : dCin[u * B + col];
+            v[q][2] = a.G0[(int64_t)u * C0 + gc];
+            v[q][3] = a.G0[(int64_t)(128 + u) * C0 + gc];
+            v[q][4] = a.G0[(int64_t)(256 + u) * C0 + gc];
+            v[q][5] = a.G0[(int64_t)(384 + u) * C0 + gc];
+            v[q][6] = a.Cs0[(int64_t)u * ldh + (t + 1) * B + col];
+            v[q][7] = a.Cs0[(int64_t)u * ldh + t * B + col];
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = threadIdx.x + 256 * (8 * half + q);
+            const int u = e >> 5, c = e & 31, col = ct * 32 + c;
+            const int64_t gc = (int64_t)t * B + col;
+            const float dh = v[q][0], dcc = v[q][1], gi = v[q][2], gf = v[q][3], gg = v[q][4], go = v[q][5];
+            const float cT = v[q][6], cp = v[q][7];
+            const float tc = tanhf(cT);
+            const float dc = dcc + dh * go * (1.0f - tc * tc);
+            const float dzi = dc * gg * (gi * (1.0f - gi));
+            const float dzf = dc * cp * (gf * (1.0f - gf));
+            const float dzg = dc * gi * (1.0f - gg * gg);
+            const float dzo = dh * tc * (go * (1.0f - go));
+            dz[u][c] = dzi; dz[128 + u][c] = dzf; dz[256 + u][c] = dzg; dz[384 + u][c] = dzo;
+            if ((u >> 5) == mu) {
+                a.dZ[(int64_t)u * C0 + gc] = dzi;
+                a.dZ[(int64_t)(128 + u) * C0 + gc] = dzf;
+                a.dZ[(int64_t)(256 + u) * C0 + gc] = dzg;
+                a.dZ[(int64_t)(384 + u) * C0 + gc] = dzo;
+                dCout[u * B + col] = dc * gf;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
     if (t == 0) return;  // dh_{-1} is not needed
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r32 = lane & 31, h = lane >> 5;
-    const float* __restrict__ Wc = a.params + R_P_WHH + 32 * mu + r32;  // A(m = u_out, k = g) = Whh[g][u_out]
+    const int w = wv, lane = ln, r32 = lane & 31, h = lane >> 5;
     gemm_f32x16 acc = {};
-    for (int kb = 128 * w; kb < 128 * w + 128; kb += 8) {
-        const int k0 = kb + 4 * h;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Wc[(int64_t)(k0 + e) * 128], dz[k0 + e][r32], acc, 0, 0, 0);
+    for (int j = 0; j < 16; ++j) {
+        const int k0 = 128 * w + 8 * j + 4 * h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + e], dz[k0 + e][r32], acc, 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[w][r][lane] = acc[r];
@@ -316,20 +357,16 @@ __global__ __launch_bounds__(256) void k_drqn_bwd(DrqnArgs a, int t) {
     }
 }
 
-// ---------------------------------------------------------------- NoisyLinear sigma gradients
-__global__ __launch_bounds__(256) void k_drqn_sigma(DrqnArgs a) {
-    if (skipped(a)) return;
-    const int n = 16384 + 128 + 128 + 1 + 384 + 3;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        int mu, sg, ep;
-        if (i < 16384) { mu = R_P_SWMU + i; sg = R_P_SWSG + i; ep = R_P_SWEP + i; }
-        else if (i < 16512) { const int k = i - 16384; mu = R_P_SBMU + k; sg = R_P_SBSG + k; ep = R_P_SBEP + k; }
-        else if (i < 16640) { const int k = i - 16512; mu = R_P_VWMU + k; sg = R_P_VWSG + k; ep = R_P_VWEP + k; }
-        else if (i == 16640) { mu = R_P_VBMU; sg = R_P_VBSG; ep = R_P_VBEP; }
-        else if (i < 17025) { const int k = i - 16641; mu = R_P_AWMU + k; sg = R_P_AWSG + k; ep = R_P_AWEP + k; }
-        else { const int k = i - 17025; mu = R_P_ABMU + k; sg = R_P_ABSG + k; ep = R_P_ABEP + k; }
-        a.grad[sg] = a.grad[mu] * a.params[ep];  // d sigma = dW * epsilon (NoisyLinear.forward :45-46)
-    }
+// NoisyLinear sigma gradients: d sigma = dW * epsilon (NoisyLinear.forward :45-46). Linear in the
+// mu gradient with the same epsilon on every rank, so it is formed after the all-reduce (apply).
+__device__ __forceinline__ int sigma_source(int i, int& ep) {
+    if (i >= R_P_SWSG && i < R_P_SWSG + 16384) { ep = R_P_SWEP + i - R_P_SWSG; return R_P_SWMU + i - R_P_SWSG; }
+    if (i >= R_P_SBSG && i < R_P_SBSG + 128) { ep = R_P_SBEP + i - R_P_SBSG; return R_P_SBMU + i - R_P_SBSG; }
+    if (i >= R_P_VWSG && i < R_P_VWSG + 128) { ep = R_P_VWEP + i - R_P_VWSG; return R_P_VWMU + i - R_P_VWSG; }
+    if (i == R_P_VBSG) { ep = R_P_VBEP; return R_P_VBMU; }
+    if (i >= R_P_AWSG && i < R_P_AWSG + 384) { ep = R_P_AWEP + i - R_P_AWSG; return R_P_AWMU + i - R_P_AWSG; }
+    if (i >= R_P_ABSG && i < R_P_ABSG + 3) { ep = R_P_ABEP + i - R_P_ABSG; return R_P_ABMU + i - R_P_ABSG; }
+    return -1;
 }
 
 // ---------------------------------------------------------------- clip + Adam
@@ -341,8 +378,16 @@ __global__ __launch_bounds__(256) void k_drqn_norm(DrqnArgs a) {
     const int n = PM_RNN_NPARAM, per = (n + kNormBlocks - 1) / kNormBlocks;
     const int lo = blockIdx.x * per, hi = min(n, lo + per);
     double s = 0.0;
+#pragma unroll 4
     for (int i = lo + threadIdx.x; i < hi; i += 256) {
-        const float g = a.grad[i] * inv_world;
+        int ep;
+        const int src = i >= R_P_SWSG ? sigma_source(i, ep) : -1;
+        float graw = a.grad[i];
+        if (src >= 0) {
+            graw = a.grad[src] * a.params[ep];
+            a.grad[i] = graw;
+        }
+        const float g = graw * inv_world;
         s += (double)g * (double)g;
     }
     red[threadIdx.x] = s;
@@ -371,9 +416,12 @@ __global__ __launch_bounds__(256) void k_drqn_adam(DrqnArgs a, AdamK k, float* p
     const float ranks = a.grad[PM_RNN_NPARAM];
     if (!(ranks > 0.f)) return;
     const float inv_world = 1.0f / ranks;
+    __shared__ double ps[kNormBlocks];
+    if (threadIdx.x < kNormBlocks) ps[threadIdx.x] = a.part[threadIdx.x];
+    __syncthreads();
     if (threadIdx.x == 0) {
         double ss = 0.0;
-        for (int j = 0; j < kNormBlocks; ++j) ss += a.part[j];
+        for (int j = 0; j < kNormBlocks; ++j) ss += ps[j];
         const float norm = (float)sqrt(ss);
         const float coef = (float)(k.max_norm / ((double)norm + 1e-6));  // clip_coef
         const int64_t ts = *a.tstep;
@@ -490,8 +538,6 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     p[0] = gemm_prob(a.dP1, C0, 1, a.X, 1, 2 * C0, g + R_P_F1W, 7, 1, 64, 7, C0);  // dW1
     p[1] = gemm_prob(a.dP1, C0, 1, a.one, 0, 0, g + R_P_F1B, 1, 0, 64, 1, C0);     // db1
     PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dP1)");
-    hipLaunchKernelGGL(k_drqn_sigma, dim3(pm_blocks(17028, 256)), dim3(256), 0, st, a);
-    PM_LAUNCHED("k_drqn_sigma");
     return PM_OK;
 }
 

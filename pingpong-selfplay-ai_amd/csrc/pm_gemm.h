@@ -48,25 +48,31 @@ __device__ __forceinline__ void gemm_tile(const GemmProb& P, int tile, float (*r
     const float* __restrict__ Bc = P.B + (int64_t)(nv ? n : 0) * P.sbn;
     const bool avec = P.flags & GF_AVEC, bvec = P.flags & GF_BVEC;
     gemm_f32x16 acc = {};
-    for (int kb = kbeg; kb < kend; kb += 8) {
-        const int k0 = kb + 4 * h;
-        float a[4], b[4];
-        if (avec) {
-            const float4 v = (mv && k0 < K) ? *reinterpret_cast<const float4*>(Ar + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
-            a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-        } else {
+    // chunks of 4 k-steps (32 k): every operand load of the chunk is issued before its 16 MFMAs
+    for (int kc = kbeg; kc < kend; kc += 32) {
+        float a[16], b[16];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) a[e] = (mv && k0 + e < K) ? Ar[(int64_t)(k0 + e) * P.sak] : 0.f;
+        for (int j = 0; j < 4; ++j) {
+            const int k0 = kc + 8 * j + 4 * h;
+            const bool kin = k0 < kend;
+            if (avec) {
+                const float4 v = (mv && kin) ? *reinterpret_cast<const float4*>(Ar + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+                a[4 * j] = v.x; a[4 * j + 1] = v.y; a[4 * j + 2] = v.z; a[4 * j + 3] = v.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a[4 * j + e] = (mv && k0 + e < kend) ? Ar[(int64_t)(k0 + e) * P.sak] : 0.f;
+            }
+            if (bvec) {
+                const float4 v = (nv && kin) ? *reinterpret_cast<const float4*>(Bc + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+                b[4 * j] = v.x; b[4 * j + 1] = v.y; b[4 * j + 2] = v.z; b[4 * j + 3] = v.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) b[4 * j + e] = (nv && k0 + e < kend) ? Bc[(int64_t)(k0 + e) * P.sbk] : 0.f;
+            }
         }
-        if (bvec) {
-            const float4 v = (nv && k0 < K) ? *reinterpret_cast<const float4*>(Bc + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
-            b[0] = v.x; b[1] = v.y; b[2] = v.z; b[3] = v.w;
-        } else {
+        __builtin_amdgcn_sched_barrier(0);  // the chunk's loads stay ahead of its MFMAs
 #pragma unroll
-            for (int e = 0; e < 4; ++e) b[e] = (nv && k0 + e < K) ? Bc[(int64_t)(k0 + e) * P.sbk] : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e], b[e], acc, 0, 0, 0);
+        for (int e = 0; e < 16; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e], b[e], acc, 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[w][r][lane] = acc[r];

@@ -109,6 +109,49 @@ __device__ __forceinline__ void stage_frags_lds(const float* __restrict__ w, flo
     }
 }
 
+// Per-env-block opponent lists. Per 256-arena block: its arenas grouped by opponent net for the
+// next act (ascending within a net), and (offset << 16 | count) per net, so the act kernel's
+// opponent tiles read their rows with two small loads instead of compacting ids next to MFMA waves
+// (VALU there waits for the matrix cores). Block-wide (kListBlock threads); more than kListNets
+// nets: no lists (the act kernel compacts).
+constexpr int kListNets = 64;
+constexpr int kListBlock = 256;
+struct OppListSmem {
+    int woff[kListBlock / 64][kListNets];  // per-wave count, then per-wave offset within the net
+    int noff[kListNets], ncnt[kListNets];
+};
+__device__ __forceinline__ void write_opp_lists(int nn, int32_t* opp_list, int32_t* opp_cnt, OppListSmem& sm, int blk,
+                                                int i, bool valid, int net) {
+    if (nn > kListNets) return;  // uniform
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int rank = 0;
+    for (int k = 0; k < nn; ++k) {
+        const bool m = valid && net == k;
+        const unsigned long long b = __ballot(m);
+        if (m) rank = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) sm.woff[wv][k] = __popcll(b);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nn) {
+        const int k = threadIdx.x;
+        int acc = 0;
+        for (int w = 0; w < kListBlock / 64; ++w) {
+            const int c = sm.woff[w][k];
+            sm.woff[w][k] = acc;
+            acc += c;
+        }
+        sm.ncnt[k] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int k = 0; k < nn; ++k) { sm.noff[k] = acc; acc += sm.ncnt[k]; }
+    }
+    __syncthreads();
+    if (valid) opp_list[(size_t)blk * kListBlock + sm.noff[net] + sm.woff[wv][net] + rank] = i;
+    if ((int)threadIdx.x < nn) opp_cnt[(size_t)blk * nn + threadIdx.x] = (sm.noff[threadIdx.x] << 16) | sm.ncnt[threadIdx.x];
+}
+
 // Compaction of the arenas i in [lo, hi) with id[i] == net, in ascending order, into an LDS list.
 // Thread t owns ids [lo + 16 t, lo + 16 t + 16): compact_load issues its loads (four int4 when
 // aligned; the caller overlaps them with other loads), compact_scan counts matches and places them

@@ -10,7 +10,7 @@
 // (h, c) per arena live in HBM [n][128], read and written as float4 in that same unit order.
 //
 // The effective-weight block (PM_RNN_NW floats) is pre-arranged in fragment order: 615 KB per net,
-// streamed from L2 by each wave (one float4 per lane = 1 KB per 4 MFMAs), one step ahead.
+// streamed through a block-shared LDS ring (see rnn_group).
 #pragma once
 #include "pm_mfma.h"
 
@@ -46,6 +46,13 @@ constexpr int R_NOISE = 128 + 128 + 128 + 1 + 128 + 3;  // eps_in / eps_out of S
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Hardware-rate activations for the acting path (v_exp_f32, v_rcp_f32: ~1 ulp each, a few ulp
+// composed; the accurate forms above cost ~6x the VALU, which the f32 MFMA stream serialises with).
+__device__ __forceinline__ float sig_hw(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+__device__ __forceinline__ float tanh_hw(float x) { return 2.0f * sig_hw(2.0f * x) - 1.0f; }
+
 __device__ __forceinline__ void load_acc_bias(const float* __restrict__ b, f32x16& acc) {
     const float4* p = reinterpret_cast<const float4*>(b);
 #pragma unroll
@@ -55,25 +62,144 @@ __device__ __forceinline__ void load_acc_bias(const float* __restrict__ b, f32x1
     }
 }
 
-constexpr int kXStride = 260;  // LDS row (one arena) of the gate input [features 128 | h_prev 128] + pad
+// ---------------------------------------------------------------- the weight ring
+// A workgroup of 4 waves runs 4 tiles (128 arenas) of the same net in lockstep. The weights stream
+// through a double-buffered LDS ring in 16 KB stages, each stage four 4 KB pieces (one gate, or one
+// 32-row tile of a layer) loaded by one wave each with global_load_lds (no registers) while the
+// previous stage computes; every wave's MFMA A operands then come from LDS (ds_read_b128), its B
+// operands from registers. Per 128 arenas: F2 in 2 stages, then per 32-unit hidden block m the 8
+// K-steps of its four gates (t = 0..3: features, 4..7: h_prev) and the shared head's k-tile m.
+constexpr int kStageFloats = 4096;  // 16 KB
+constexpr int kRingStages = 2 + 4 * 9;
 
-// One acting step of QNetRNN for the 32 arenas of this wave's tile (column = lane & 31).
-// xs: layer-1 B operands (tile_inputs); hs/cs: this arena's (h, c) rows [128] (read, then written
-// with the new state when `valid`); zero_state: start from h = c = 0 (episode start). xl: this
-// wave's LDS gate-input rows [32][kXStride]; hw_lds: heads (R_H.. R_BH) staged in LDS. q: Q values.
-__device__ __forceinline__ void rnn_tile(const float* __restrict__ w, const float (&xs)[4], float* hs, float* cs,
-                                         bool zero_state, bool valid, const float* hw_lds, float* xl, int lane,
-                                         float (&q)[3]) {
-    const int h = lane >> 5, col = lane & 31;
-    float* xrow = xl + col * kXStride;  // this lane's arena: units [0,128) features, [128,256) h_prev
-    // ---- features 7 -> 64 -> 128
+#ifdef PM_DIAG
+// diagnostic builds: s_memrealtime after each ring barrier of a block's first group (blocks < 1024)
+static __device__ unsigned long long pm_diag_stage[48][1024];
+#define PM_STG(k)                                                                                   \
+    do {                                                                                            \
+        if (threadIdx.x == 0 && blockIdx.x < 1024 && g == 0) pm_diag_stage[(k)][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+// shader-clock counter (s_memtime) beside the 100 MHz one: slots 40 (begin) and 47 (end)
+#define PM_STG_CLK(k)                                                                               \
+    do {                                                                                            \
+        if (threadIdx.x == 0 && blockIdx.x < 1024 && g == 0) pm_diag_stage[(k)][blockIdx.x] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define PM_STG(k) \
+    do {          \
+    } while (0)
+#define PM_STG_CLK(k) \
+    do {              \
+    } while (0)
+#endif
+
+__device__ __forceinline__ const float* stage_piece(const float* __restrict__ w, int s, int piece) {
+    if (s < 2) return w + R_F2 + (piece * 2 + s) * 4 * 256;  // F2: [mt][t = s]
+    s -= 2;
+    const int m = s / 9, t = s - 9 * m;
+    if (t < 8) return w + R_G + ((piece * 4 + m) * 8 + t) * 4 * 256;  // gate q = piece, block m, K-step t
+    return w + R_S + (piece * 4 + m) * 4 * 256;                         // shared head tile mt = piece, k-tile m
+}
+
+// Issue stage s into `slot`: wave w loads piece w (4 KB = 4 wave instructions of 1 KB). Landed at
+// the caller's next __syncthreads() (which waits vmcnt(0)).
+__device__ __forceinline__ void stage_issue(const float* __restrict__ w, int s, float* slot) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const float4* src = reinterpret_cast<const float4*>(stage_piece(w, s, wv)) + lane;
+    float4* dst = reinterpret_cast<float4*>(slot) + wv * 256;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        __builtin_amdgcn_global_load_lds((const void*)(src + 64 * k), (lds_void*)(dst + 64 * k), 16, 0, 0);
+}
+
+// 64 MFMAs of one stage: acc[p] += piece p (A, LDS) x b[4 rq + e] (B, registers).
+__device__ __forceinline__ void stage_mfma(const float* slot, const float (&b)[16], f32x16 (&acc)[4], int lane) {
+    const float4* a4 = reinterpret_cast<const float4*>(slot) + lane;
+#pragma unroll
+    for (int rq = 0; rq < 4; ++rq) {
+        float4 a[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) a[p] = a4[(p * 4 + rq) * 64];
+        // the four accumulator chains interleaved: consecutive MFMAs never depend on each other
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[p].x, b[4 * rq + 0], acc[p], 0, 0, 0);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[p].y, b[4 * rq + 1], acc[p], 0, 0, 0);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[p].z, b[4 * rq + 2], acc[p], 0, 0, 0);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[p].w, b[4 * rq + 3], acc[p], 0, 0, 0);
+    }
+}
+
+// F2 stage t: one K half (32 units) of all four 32-row feature tiles: b = the layer-1 tile t.
+__device__ __forceinline__ void stage_mfma_f2(const float* slot, const f32x16& c1t, f32x16 (&acc)[4], int lane) {
+    float b[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) b[r] = c1t[r];
+    stage_mfma(slot, b, acc, lane);
+}
+
+// Block-shared LDS copy of the small per-net tables: heads (R_H .. R_H + 516) then the biases of
+// F2 (R_B2, 128), the gates (R_BG, 512) and the shared head (R_BS, 128).
+constexpr int kHwHeads = 0, kHwB2 = 528, kHwBG = kHwB2 + 128, kHwBS = kHwBG + 512, kHwFloats = kHwBS + 128;
+
+__device__ __forceinline__ void stage_tables(const float* __restrict__ w, float* hw) {
+    for (int k = threadIdx.x; k < kHwFloats; k += blockDim.x) {
+        float v = 0.f;
+        if (k < 516) v = w[R_H + k];
+        else if (k >= kHwB2 && k < kHwBG) v = w[R_B2 + k - kHwB2];
+        else if (k >= kHwBG && k < kHwBS) v = w[R_BG + k - kHwBG];
+        else if (k >= kHwBS) v = w[R_BS + k - kHwBS];
+        hw[k] = v;
+    }
+}
+
+__device__ __forceinline__ void add_bias_lds(const float* b, f32x16& acc) {
+    const float4* p = reinterpret_cast<const float4*>(b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float4 v = p[j];
+        acc[4 * j] += v.x; acc[4 * j + 1] += v.y; acc[4 * j + 2] += v.z; acc[4 * j + 3] += v.w;
+    }
+}
+
+// One acting step of QNetRNN for group g of a block's arena list (tiles 4g .. 4g+3, one per wave):
+// q values out through `out`, (h, c) rows updated in HBM. Block-wide (all 4 waves, barriers).
+template <typename Out>
+__device__ __forceinline__ void rnn_group(const float* __restrict__ w, float* ring, const float* hw,
+                                          const float* __restrict__ obs, float* hst, float* cst,
+                                          const uint8_t* __restrict__ reset, const int* list, int count, int g,
+                                          const Out& out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+    const int row = (4 * g + wave) * 32 + (lane & 31);
+    const bool valid = row < count;
+    const int arena = list[min(row, count - 1)];
+    float* hs = hst + (size_t)arena * 128;
+    float* cs = cst + (size_t)arena * 128;
+    const bool zero = reset != nullptr && reset[arena] != 0;
+    PM_STG(0);
+    PM_STG_CLK(40);
+    stage_issue(w, 0, ring);  // F2 first half lands while the prologue runs
+    // ---- prologue: inputs, layer 1, biases, h_prev into the B-operand registers
+    float xs[4];
+    tile_inputs(obs + (size_t)arena * 7, h, xs);
+    float xb[8][16];  // gate K-steps t = 0..7: B operands (features 0..3, h_prev 4..7)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            const float4 v = zero ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                  : *reinterpret_cast<const float4*>(hs + 32 * t + 8 * rq + 4 * h);
+            xb[4 + t][4 * rq] = v.x; xb[4 + t][4 * rq + 1] = v.y; xb[4 + t][4 * rq + 2] = v.z; xb[4 + t][4 * rq + 3] = v.w;
+        }
+    f32x16 c1[2];
     {
-        f32x16 c1[2];
-        const f32x16 zero = {};
+        const f32x16 zero16 = {};
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
             const float4 a = reinterpret_cast<const float4*>(w + R_F1)[jt * 64 + lane];
-            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, xs[0], zero, 0, 0, 0);
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, xs[0], zero16, 0, 0, 0);
             c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, xs[1], c1[jt], 0, 0, 0);
             c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, xs[2], c1[jt], 0, 0, 0);
             c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, xs[3], c1[jt], 0, 0, 0);
@@ -82,127 +208,92 @@ __device__ __forceinline__ void rnn_tile(const float* __restrict__ w, const floa
         for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) c1[jt][r] = relu(c1[jt][r]);
-        const float4* w2 = reinterpret_cast<const float4*>(w + R_F2) + lane;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            f32x16 acc;
-            load_acc_bias(w + R_B2 + (mt * 2 + h) * 16, acc);
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int rq = 0; rq < 4; ++rq) {
-                    const float4 a = w2[((mt * 2 + t) * 4 + rq) * 64];
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, c1[t][4 * rq + 0], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, c1[t][4 * rq + 1], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, c1[t][4 * rq + 2], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, c1[t][4 * rq + 3], acc, 0, 0, 0);
-                }
-            // units 32mt + 8j + 4h + e live in register 4j + e
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                *reinterpret_cast<float4*>(xrow + 32 * mt + 8 * j + 4 * h) =
-                    make_float4(relu(acc[4 * j]), relu(acc[4 * j + 1]), relu(acc[4 * j + 2]), relu(acc[4 * j + 3]));
-        }
     }
-    // h_prev into the same rows
+    f32x16 acc[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x16{};
+    __syncthreads();
+    PM_STG(1);
+    // ---- F2 (stages 0, 1)
+    stage_issue(w, 1, ring + kStageFloats);
+    stage_mfma_f2(ring, c1[0], acc, lane);
+    __syncthreads();
+    PM_STG(2);
+    stage_issue(w, 2, ring);
+    stage_mfma_f2(ring + kStageFloats, c1[1], acc, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int u = 32 * t + 8 * j + 4 * h;
-            const float4 v = zero_state ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(hs + u);
-            *reinterpret_cast<float4*>(xrow + 128 + u) = v;
-        }
-    // the wave's rows are written by all its lanes: wave-level LDS visibility before the reads
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-    // ---- LSTM gates per 32-unit hidden block m (the four gates interleaved), cell update in place;
-    // the shared head's k-tile m consumes that block's h' right away (its K runs over the same blocks)
+    for (int mt = 0; mt < 4; ++mt) {
+        add_bias_lds(hw + kHwB2 + (mt * 2 + h) * 16, acc[mt]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xb[mt][r] = relu(acc[mt][r]);
+    }
     f32x16 sacc[4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) load_acc_bias(w + R_BS + (mt * 2 + h) * 16, sacc[mt]);
-    const float4* g4 = reinterpret_cast<const float4*>(w + R_G) + lane;
-    const float4* s4 = reinterpret_cast<const float4*>(w + R_S) + lane;
+    for (int mt = 0; mt < 4; ++mt) sacc[mt] = f32x16{};
+    __syncthreads();
+    PM_STG(3);
+    // ---- LSTM: stage s = 2 + 9m + t lives in slot s & 1 = (m + t) & 1
 #pragma unroll 1
     for (int m = 0; m < 4; ++m) {
         float4 cp[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            cp[j] = zero_state ? make_float4(0.f, 0.f, 0.f, 0.f)
-                               : *reinterpret_cast<const float4*>(cs + 32 * m + 8 * j + 4 * h);
-        f32x16 acc[4];
+            cp[j] = zero ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(cs + 32 * m + 8 * j + 4 * h);
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) load_acc_bias(w + R_BG + ((gq * 4 + m) * 2 + h) * 16, acc[gq]);
-        // weights for (t, rq): g4[(((gq*4 + m)*8 + t)*4 + rq)*64]; software-pipelined one rq-step ahead
-        float4 a[4];
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) a[gq] = g4[(((gq * 4 + m) * 8 + 0) * 4 + 0) * 64];
+        for (int q = 0; q < 4; ++q) acc[q] = f32x16{};
+        const int s0 = 2 + 9 * m;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
+            const int s = s0 + t;
+            stage_issue(w, s + 1, ring + ((s + 1) & 1) * kStageFloats);
+            stage_mfma(ring + (s & 1) * kStageFloats, xb[t], acc, lane);
+            __syncthreads();
+            PM_STG(s + 2);
+        }
+        // cell update: c' = s(f) c + s(i) tanh(g), h' = s(o) tanh(c') (torch gate order i, f, g, o)
 #pragma unroll
-            for (int rq = 0; rq < 4; ++rq) {
-                const int nt = rq < 3 ? t : t + 1, nrq = rq < 3 ? rq + 1 : 0;
-                float4 an[4];
-                if (nt < 8) {
+        for (int q = 0; q < 4; ++q) add_bias_lds(hw + kHwBG + ((q * 4 + m) * 2 + h) * 16, acc[q]);
+        float hb[16];
+        {
+            float cn[16];
 #pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) an[gq] = g4[(((gq * 4 + m) * 8 + nt) * 4 + nrq) * 64];
+            for (int r = 0; r < 16; ++r) {
+                const float cprev = (&cp[r >> 2].x)[r & 3];
+                const float ig = sig_hw(acc[0][r]), fg = sig_hw(acc[1][r]);
+                const float gg = tanh_hw(acc[2][r]), og = sig_hw(acc[3][r]);
+                cn[r] = fg * cprev + ig * gg;
+                hb[r] = og * tanh_hw(cn[r]);
+            }
+            if (valid) {  // h_prev is in registers: the rows can take the new state now
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    *reinterpret_cast<float4*>(cs + 32 * m + 8 * j + 4 * h) =
+                        make_float4(cn[4 * j], cn[4 * j + 1], cn[4 * j + 2], cn[4 * j + 3]);
+                    *reinterpret_cast<float4*>(hs + 32 * m + 8 * j + 4 * h) =
+                        make_float4(hb[4 * j], hb[4 * j + 1], hb[4 * j + 2], hb[4 * j + 3]);
                 }
-                // B operands: units 32t + 8rq + 4h + (0..3) of this arena (k-steps 4rq .. 4rq+3)
-                const float4 b = *reinterpret_cast<const float4*>(xrow + 32 * t + 8 * rq + 4 * h);
-#pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    acc[gq] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[gq].x, b.x, acc[gq], 0, 0, 0);
-                    acc[gq] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[gq].y, b.y, acc[gq], 0, 0, 0);
-                    acc[gq] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[gq].z, b.z, acc[gq], 0, 0, 0);
-                    acc[gq] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[gq].w, b.w, acc[gq], 0, 0, 0);
-                }
-                if (nt < 8) {
-#pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) a[gq] = an[gq];
-                }
-                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        float hb[16], cn[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float cprev = (&cp[r >> 2].x)[r & 3];
-            const float ig = sigmoidf_(acc[0][r]), fg = sigmoidf_(acc[1][r]);
-            const float gg = tanhf(acc[2][r]), og = sigmoidf_(acc[3][r]);
-            cn[r] = fg * cprev + ig * gg;
-            hb[r] = og * tanhf(cn[r]);
+        // shared head k-tile m (stage s0 + 8): sacc[mt] += W_S[32mt.., 32m + rho(r) + 4h] h'
+        {
+            const int s = s0 + 8;
+            if (s + 1 < kRingStages) stage_issue(w, s + 1, ring + ((s + 1) & 1) * kStageFloats);
+            PM_STG(42 + m);  // cell update done
+            stage_mfma(ring + (s & 1) * kStageFloats, hb, sacc, lane);
+            __syncthreads();
+            PM_STG(s + 2);
         }
-        if (valid) {  // h_prev was copied to LDS: the global rows can take the new state now
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                *reinterpret_cast<float4*>(cs + 32 * m + 8 * j + 4 * h) =
-                    make_float4(cn[4 * j], cn[4 * j + 1], cn[4 * j + 2], cn[4 * j + 3]);
-                *reinterpret_cast<float4*>(hs + 32 * m + 8 * j + 4 * h) =
-                    make_float4(hb[4 * j], hb[4 * j + 1], hb[4 * j + 2], hb[4 * j + 3]);
-            }
-        }
-        // shared head, k-tile m: sacc[mt] += W_S[32mt.., 32m + rho(r) + 4h] * h'
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int rq = 0; rq < 4; ++rq) {
-                const float4 a4 = s4[((mt * 4 + m) * 4 + rq) * 64];
-                sacc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, hb[4 * rq + 0], sacc[mt], 0, 0, 0);
-                sacc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, hb[4 * rq + 1], sacc[mt], 0, 0, 0);
-                sacc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, hb[4 * rq + 2], sacc[mt], 0, 0, 0);
-                sacc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, hb[4 * rq + 3], sacc[mt], 0, 0, 0);
-            }
     }
     // ---- ReLU(shared head) and the dueling heads (VALU, weights from LDS)
     float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-        const f32x16& acc = sacc[mt];
-        const float4* hw = reinterpret_cast<const float4*>(hw_lds) + (h * 4 + mt) * 16;
+        add_bias_lds(hw + kHwBS + (mt * 2 + h) * 16, sacc[mt]);
+        const float4* hw4 = reinterpret_cast<const float4*>(hw + kHwHeads) + (h * 4 + mt) * 16;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const float x = relu(acc[r]);
-            const float4 wv = hw[r];
+            const float x = relu(sacc[mt][r]);
+            const float4 wv = hw4[r];
             v = fmaf(wv.x, x, v);
             a0 = fmaf(wv.y, x, a0);
             a1 = fmaf(wv.z, x, a1);
@@ -213,15 +304,15 @@ __device__ __forceinline__ void rnn_tile(const float* __restrict__ w, const floa
     a0 += __shfl_xor(a0, 32);
     a1 += __shfl_xor(a1, 32);
     a2 += __shfl_xor(a2, 32);
-    v += hw_lds[512];
-    a0 += hw_lds[513];
-    a1 += hw_lds[514];
-    a2 += hw_lds[515];
+    v += hw[512];
+    a0 += hw[513];
+    a1 += hw[514];
+    a2 += hw[515];
     const float mean = ((a0 + a1) + a2) / 3.0f;
-    q[0] = v + (a0 - mean);
-    q[1] = v + (a1 - mean);
-    q[2] = v + (a2 - mean);
-    __builtin_amdgcn_wave_barrier();  // this wave may overwrite its rows for the next tile
+    const float q[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
+    out(arena, valid && h == 0, q);
+    PM_STG(46);
+    PM_STG_CLK(47);
 }
 
 }  // namespace pm

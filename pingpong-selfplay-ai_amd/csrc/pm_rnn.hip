@@ -120,67 +120,127 @@ __global__ __launch_bounds__(256) void k_rnn_fold(const float* __restrict__ para
     }
 }
 
-__device__ __forceinline__ void stage_heads(const float* __restrict__ w, float* hw) {
-    for (int k = threadIdx.x; k < 516; k += blockDim.x) hw[k] = w[R_H + k];
-}
-
-// One acting step for `count` arenas listed in `list` (LDS) with weights w; wave-uniform loop.
-__device__ __forceinline__ void rnn_rows(const float* __restrict__ w, const float* hw, float* xl_block,
-                                         const float* __restrict__ obs, float* hst, float* cst,
-                                         const uint8_t* __restrict__ reset, const int* list, int count,
-                                         const TileOut& out) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int ntiles = (count + 31) >> 5;
-    for (int tl = wave; tl < ntiles; tl += nw) {
-        const int row = tl * 32 + (lane & 31);
-        const bool valid = row < count;
-        const int arena = list[min(row, count - 1)];
-        float xs[4];
-        tile_inputs(obs + (size_t)arena * 7, lane >> 5, xs);
-        const bool zero = reset != nullptr && reset[arena] != 0;
-        float q[3];
-        rnn_tile(w, xs, hst + (size_t)arena * 128, cst + (size_t)arena * 128, zero, valid, hw,
-                 xl_block + wave * 32 * kXStride, lane, q);
-        int a = argmax3(q);
-        if (out.eps >= 0.0) {  // random.random() < eps ? randint(0, 2) (forward still advances h, c: :376-380)
-            const U4 rr = philox64((uint32_t)arena, TAG_ACT, out.ctr, out.seed);
-            if (u53(rr.x, rr.y) < out.eps) a = below(rr.z, 3u);
+// Action selection and stores for one row: argmax (first max), then the epsilon branch
+// (random.random() < eps ? randint(0, 2); the forward still advanced (h, c), :376-380).
+struct RowOut {
+    int8_t* act;
+    float* q;
+    double eps;
+    uint64_t seed, ctr;
+    __device__ __forceinline__ void operator()(int arena, bool store, const float (&qv)[3]) const {
+        int a = argmax3(qv);
+        if (eps >= 0.0) {
+            const U4 rr = philox64((uint32_t)arena, TAG_ACT, ctr, seed);
+            if (u53(rr.x, rr.y) < eps) a = below(rr.z, 3u);
         }
-        if ((lane >> 5) == 0 && valid) {
-            if (out.act) out.act[arena] = (int8_t)a;
-            if (out.q) {
-                out.q[(size_t)arena * 3 + 0] = q[0];
-                out.q[(size_t)arena * 3 + 1] = q[1];
-                out.q[(size_t)arena * 3 + 2] = q[2];
+        if (store) {
+            if (act) act[arena] = (int8_t)a;
+            if (q) {
+                q[(size_t)arena * 3 + 0] = qv[0];
+                q[(size_t)arena * 3 + 1] = qv[1];
+                q[(size_t)arena * 3 + 2] = qv[2];
             }
         }
     }
-}
+};
 
 constexpr int kRnnList = 2048;  // max arenas per grouped chunk
 
 struct RnnShared {
-    float hw[528];
-    float x[kRnnBlock / 64][32 * kXStride];  // per-wave gate input rows (features | h_prev)
+    float ring[2 * kStageFloats];  // the weight ring (32 KB)
+    float hw[kHwFloats];           // heads + biases (stage_tables)
     int list[kRnnList];
     int count;
     int wtot[kRnnBlock / 64];
+    int tot[kListNets], gpre[kListNets + 1], scan[kRnnBlock], net;
 };
+
+// Side A from the env kernel's per-block opponent lists (write_opp_lists): every net's arenas are
+// packed globally into 128-row groups, block b taking group b of the concatenation over nets (only
+// each net's last group is partial). Fills sh.list / sh.count; returns the net, or -1 past the end.
+// Block-wide; LDS scratch: sh.tot / gpre / scan, sh.list[kRnnRows ..] for the env-block prefix.
+constexpr int kMaxEnvBlocks = kRnnList - kRnnRows - 1;  // n <= kMaxEnvBlocks * kListBlock
+__device__ __forceinline__ int packed_rows(const int32_t* __restrict__ opp_list, const int32_t* __restrict__ opp_cnt,
+                                           int n, int nn, int b, RnnShared& sh) {
+    const int t = threadIdx.x, neb = (n + kListBlock - 1) / kListBlock;
+    if (t < nn) sh.tot[t] = 0;
+    __syncthreads();
+    for (int idx = t; idx < neb * nn; idx += blockDim.x) atomicAdd(&sh.tot[idx % nn], opp_cnt[idx] & 0xFFFF);
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0, k = -1;
+        for (int j = 0; j < nn; ++j) {
+            sh.gpre[j] = acc;
+            if (b >= acc) k = j;
+            acc += (sh.tot[j] + kRnnRows - 1) / kRnnRows;
+        }
+        sh.gpre[nn] = acc;
+        sh.net = b < acc ? k : -1;
+        while (sh.net >= 0 && sh.tot[sh.net] == 0) --sh.net;  // skip nets without arenas
+    }
+    __syncthreads();
+    const int k = sh.net;
+    if (k < 0) return -1;
+    const int g = b - sh.gpre[k];
+    // exclusive prefix over env blocks of net k's counts: pre[e] in sh.list[kRnnRows + e]
+    int* pre = sh.list + kRnnRows;
+    const int per = (neb + blockDim.x - 1) / blockDim.x, e0 = min(neb, t * per), e1 = min(neb, e0 + per);
+    int cnt = 0;
+    for (int e = e0; e < e1; ++e) cnt += opp_cnt[(size_t)e * nn + k] & 0xFFFF;
+    sh.scan[t] = cnt;
+    __syncthreads();
+    for (int s = 1; s < (int)blockDim.x; s <<= 1) {
+        const int v = t >= s ? sh.scan[t - s] : 0;
+        __syncthreads();
+        sh.scan[t] += v;
+        __syncthreads();
+    }
+    int acc = sh.scan[t] - cnt;
+    for (int e = e0; e < e1; ++e) {
+        pre[e] = acc;
+        acc += opp_cnt[(size_t)e * nn + k] & 0xFFFF;
+    }
+    if (t == 0) pre[neb] = sh.tot[k];
+    __syncthreads();
+    const int count = min(kRnnRows, sh.tot[k] - g * kRnnRows);
+    for (int j = t; j < count; j += blockDim.x) {
+        const int r = g * kRnnRows + j;
+        int lo = 0, hi = neb;  // pre[lo] <= r < pre[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (pre[mid] <= r) lo = mid; else hi = mid;
+        }
+        const int v = opp_cnt[(size_t)lo * nn + k];
+        sh.list[j] = opp_list[(size_t)lo * kListBlock + (v >> 16) + (r - pre[lo])];
+    }
+    if (t == 0) sh.count = count;
+    __syncthreads();
+    return k;
+}
+
+// All rows of the block's list, 128 per group (block-uniform loop: every wave takes every barrier).
+__device__ __forceinline__ void rnn_rows(const float* __restrict__ w, RnnShared& sh, const float* __restrict__ obs,
+                                         float* hst, float* cst, const uint8_t* __restrict__ reset, int count,
+                                         const RowOut& out) {
+    for (int g = 0; g * kRnnRows < count; ++g)
+        rnn_group(w, sh.ring, sh.hw, obs, hst, cst, reset, sh.list, count, g, out);
+}
 
 __global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_q(const float* __restrict__ w, const float* __restrict__ x,
                                                         float* h, float* c, const uint8_t* __restrict__ reset,
                                                         float* __restrict__ q, int n) {
     __shared__ RnnShared sh;
     const int lo = blockIdx.x * kRnnRows, hi = min(lo + kRnnRows, n);
-    stage_heads(w, sh.hw);
+    stage_tables(w, sh.hw);
     for (int k = threadIdx.x; k < hi - lo; k += blockDim.x) sh.list[k] = lo + k;
     __syncthreads();
-    rnn_rows(w, sh.hw, &sh.x[0][0], x, h, c, reset, sh.list, hi - lo, TileOut{nullptr, q, -1.0, 0, 0});
+    rnn_rows(w, sh, x, h, c, reset, hi - lo, RowOut{nullptr, q, -1.0, 0, 0});
 }
 
 struct RnnActArgs {
     const float* w_opp;
     const int32_t* opp;
+    const int32_t *opp_list, *opp_cnt;  // per-env-block lists (packed side A) or null
     const float* w_B;
     const float *obsA, *obsB;
     float *hA, *cA, *hB, *cB;
@@ -201,6 +261,15 @@ __global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs 
     const float* w;
     int net = -1, lo, hi;
     bool compact = false;
+    if (b >= nb && A.opp_list) {  // side A packed over the env kernel's lists
+        const int k = packed_rows(A.opp_list, A.opp_cnt, g.n, g.n_opp, b - nb, sh);
+        if (k < 0) return;  // block-uniform: past the last group
+        w = A.w_opp + (size_t)k * PM_RNN_NW;
+        stage_tables(w, sh.hw);
+        __syncthreads();
+        rnn_rows(w, sh, A.obsA, A.hA, A.cA, A.reset, sh.count, RowOut{A.aA, A.qA, -1.0, 0, 0});
+        return;
+    }
     if (b < nb) {
         w = A.w_B; lo = b * kRnnRows; hi = min(lo + kRnnRows, g.n);
     } else {
@@ -211,7 +280,7 @@ __global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs 
         compact = A.opp != nullptr;
         if (!compact && net != 0) return;  // block-uniform
     }
-    stage_heads(w, sh.hw);
+    stage_tables(w, sh.hw);
     int ids[16];
     if (compact) compact_load(A.opp, lo, hi, ids);
     if (compact) {
@@ -222,13 +291,12 @@ __global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs 
     }
     __syncthreads();
     const uint64_t ctr = A.counter + (A.counter_dev ? *A.counter_dev : 0ull);
+    const int count = sh.count;
     if (net < 0) {
         const double eps = A.eps_dev ? *A.eps_dev : A.eps;
-        rnn_rows(w, sh.hw, &sh.x[0][0], A.obsB, A.hB, A.cB, A.reset, sh.list, sh.count,
-                 TileOut{A.aB, A.qB, eps, A.seed, ctr});
+        rnn_rows(w, sh, A.obsB, A.hB, A.cB, A.reset, count, RowOut{A.aB, A.qB, eps, A.seed, ctr});
     } else {
-        rnn_rows(w, sh.hw, &sh.x[0][0], A.obsA, A.hA, A.cA, A.reset, sh.list, sh.count,
-                 TileOut{A.aA, A.qA, -1.0, 0, 0});
+        rnn_rows(w, sh, A.obsA, A.hA, A.cA, A.reset, count, RowOut{A.aA, A.qA, -1.0, 0, 0});
     }
 }
 
@@ -262,7 +330,8 @@ extern "C" int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_o
                           const float* obsA, const float* obsB, float* hA, float* cA, float* hB, float* cB,
                           const uint8_t* reset, float epsilon, const double* eps_dev, uint64_t seed, uint64_t counter,
                           const uint64_t* counter_dev, int8_t* aA, int8_t* aB, float* qA, float* qB, int32_t n,
-                          int32_t chunk0, int32_t chunk1, void* stream) {
+                          int32_t chunk0, int32_t chunk1, const int32_t* opp_list, const int32_t* opp_cnt,
+                          void* stream) {
     if (n == 0) return PM_OK;
     PM_REQUIRE(w_opp && w_B && obsA && obsB && hA && cA && hB && cB && aA && aB && n > 0 && n_opp >= 1, PM_E_ARG,
                "pm_rnn_act: null buffer or size");
@@ -272,11 +341,25 @@ extern "C" int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_o
     if (chunk0 <= 0) chunk0 = 256;
     if (chunk1 <= 0) chunk1 = kRnnList;
     PM_REQUIRE(chunk0 <= kRnnList && chunk1 <= kRnnList, PM_E_SIZE, "pm_rnn_act: chunk > %d", kRnnList);
+    const bool lists = opp_list && opp_cnt && opp_id && n_opp <= kListNets;
+    PM_REQUIRE(!lists || (n + kListBlock - 1) / kListBlock <= kMaxEnvBlocks, PM_E_SIZE,
+               "pm_rnn_act: n %d too large for opponent lists", n);
     const ActGrid g{n, opp_id ? n_opp : 1, chunk0, chunk1, 0};
     const int nb = (n + kRnnRows - 1) / kRnnRows;
-    const RnnActArgs a{w_opp, opp_id, w_B, obsA, obsB, hA, cA, hB, cB, reset, aA, aB, qA, qB,
-                       (double)epsilon, eps_dev, seed, counter, counter_dev};
-    hipLaunchKernelGGL(k_rnn_act, dim3(nb + g.blocks()), dim3(kRnnBlock), 0, pm_stream(stream), g, a);
+    const RnnActArgs a{w_opp, opp_id, lists ? opp_list : nullptr, lists ? opp_cnt : nullptr, w_B, obsA, obsB, hA, cA,
+                       hB, cB, reset, aA, aB, qA, qB, (double)epsilon, eps_dev, seed, counter, counter_dev};
+    const int na = lists ? nb + n_opp : g.blocks();  // packed: sum over nets of ceil(rows / 128) <= nb + nets
+    hipLaunchKernelGGL(k_rnn_act, dim3(nb + na), dim3(kRnnBlock), 0, pm_stream(stream), g, a);
     PM_LAUNCHED("k_rnn_act");
     return PM_OK;
 }
+
+#ifdef PM_DIAG
+extern "C" int pm_diag_read_rnn(uint64_t* out) {  // [48][1024] ring-stage stamps
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_stage), sizeof(pm_diag_stage));
+}
+extern "C" int pm_diag_clear_rnn(void) {
+    static unsigned long long z[48][1024];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(pm_diag_stage), z, sizeof(z));
+}
+#endif

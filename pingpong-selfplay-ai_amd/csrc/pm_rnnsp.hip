@@ -12,8 +12,8 @@
 //                 flag (len(memory) > batch * min_episodes_for_training_start, :768)
 // then pm_drqn_update (K6). Transition rings are [depth][n] records of 64 B written by step
 // (coalesced); an episode is (arena, first step, length), its steps read back from the ring.
-#include "pm_dev.h"
 #include "pm_host.h"
+#include "pm_mfma.h"
 
 using namespace pm;
 
@@ -46,6 +46,10 @@ __global__ __launch_bounds__(kBlock) void k_rsp_init(const pm_rnn_selfplay sp) {
         sp.reset[i] = 1;  // init_hidden for both players (:744-746)
         observe(a, oA, oB);
     }
+    {
+        __shared__ OppListSmem ol;
+        write_opp_lists(sp.n_pool + 1, sp.opp_list, sp.opp_cnt, ol, blockIdx.x, i, i < sp.n, i < sp.n ? sp.opp[i] : 0);
+    }
     store_rows7(sp.obsA, lds, oA, i0, sp.n);
     store_rows7(sp.obsB, lds, oB, i0, sp.n);
 }
@@ -53,6 +57,7 @@ __global__ __launch_bounds__(kBlock) void k_rsp_init(const pm_rnn_selfplay sp) {
 __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
     __shared__ float lds[kBlock][7];
     __shared__ long long red[kBlock / 64][6];
+    __shared__ int red_st[kBlock / 64];
     const int i0 = blockIdx.x * kBlock;
     const int i = i0 + threadIdx.x;
     const bool valid = i < sp.n;
@@ -82,6 +87,7 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
             red[wv][3] = __popcll(mP); red[wv][4] = __popcll(mwP); red[wv][5] = rs;
         }
     }
+    int onew = o;
     if (valid) {
         // memory.push_step(obs_B, act_B, reward_B, next_obs_B, done) (:770, :107-110)
         float4* row = reinterpret_cast<float4*>(sp.trans + ((int64_t)(step % (uint64_t)sp.depth) * sp.n + i) * PM_TRANS_F);
@@ -89,11 +95,10 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
         row[1] = make_float4(oB[4], oB[5], oB[6], rB);
         row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
         row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
-        int keep = 0;
         if (d) {  // episode over: stored when len >= trace_length (:112-115); next opponent, env.reset()
-            keep = len >= sp.T ? len : 0;
             const uint32_t ns = (uint32_t)sp.st.serves[i];
-            sp.opp[i] = draw_opponent(sp, i, ns);
+            onew = draw_opponent(sp, i, ns);
+            sp.opp[i] = onew;
             double vx, vy, spn;
             philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
             serve(a, vx, vy, spn);
@@ -104,70 +109,97 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
         sp.ep_reward[i] = d ? 0.f : er;
         sp.ep_len[i] = d ? 0 : len;
         sp.reset[i] = (uint8_t)d;
-        sp.fin[i] = keep;
     }
-    __syncthreads();
-    if (threadIdx.x < 6) {
+    {   // episodes to store, ranked in arena order within the block -> the block's staging slots
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const bool st = valid && d && len >= sp.T;
+        const unsigned long long m = __ballot(st);
+        if (lane == 0) red_st[wv] = __popcll(m);
+        __syncthreads();
+        int rank = __popcll(m & ((1ull << lane) - 1ull));
+        for (int w = 0; w < wv; ++w) rank += red_st[w];
+        if (st) {
+            int64_t* slot = sp.fin + 2 * ((int64_t)blockIdx.x * kBlock + rank);
+            slot[0] = (int64_t)(uint32_t)i | ((int64_t)len << 32);
+            slot[1] = (int64_t)step - len + 1;
+        }
+    }
+    if (threadIdx.x < 7) {
         long long t = 0;
-        for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
+        for (int w = 0; w < kBlock / 64; ++w) t += threadIdx.x < 6 ? red[w][threadIdx.x] : red_st[w];
         sp.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = t;
+    }
+    {   // the next act's per-block opponent lists
+        __shared__ OppListSmem ol;
+        write_opp_lists(sp.n_pool + 1, sp.opp_list, sp.opp_cnt, ol, blockIdx.x, i, valid, onew);
     }
     store_rows7(sp.obsA, lds, nA, i0, sp.n);
     store_rows7(sp.obsB, lds, nB, i0, sp.n);
 }
 
-constexpr int kAppend = 1024;
+constexpr int kAppend = 1024;  // one thread per env block: n <= kAppend * kBlock
 
+// The env blocks' staged episodes appended to the table in arena order (block prefix sums), the
+// bookkeeping partials summed, epsilon decayed once per finished episode, the step advanced.
 __global__ __launch_bounds__(kAppend) void k_rsp_append(const pm_rnn_selfplay sp) {
-    __shared__ int cnt[kAppend];
-    __shared__ long long tot[6];
-    const int t = threadIdx.x;
+    __shared__ int off[kAppend + 1];
+    __shared__ long long wred[kAppend / 64][7];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     pm_rnn_ctrl* c = sp.ctrl;
     const int nblk = (sp.n + kBlock - 1) / kBlock;
-    if (t < 6) {
-        long long s = 0;
-        for (int b = 0; b < nblk; ++b) s += sp.partials[(size_t)b * 8 + t];
-        tot[t] = s;
+    long long p[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (t < nblk) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) p[k] = sp.partials[(size_t)t * 8 + k];
     }
-    const int per = (sp.n + kAppend - 1) / kAppend;
-    const int lo = min(sp.n, t * per), hi = min(sp.n, lo + per);
-    int k = 0;
-    for (int j = lo; j < hi; ++j) k += sp.fin[j] > 0;
-    cnt[t] = k;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        long long v = p[k];
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
+        if (lane == 0) wred[wv][k] = v;
+    }
+    off[t + 1] = (int)p[6];  // stored episodes of env block t
+    if (t == 0) off[0] = 0;
     __syncthreads();
-    for (int s = 1; s < kAppend; s <<= 1) {  // inclusive scan
-        const int v = t >= s ? cnt[t - s] : 0;
+    for (int s = 1; s <= kAppend; s <<= 1) {  // inclusive scan of off[1..kAppend]
+        const int v = t + 1 > s ? off[t + 1 - s] : 0;
         __syncthreads();
-        cnt[t] += v;
+        off[t + 1] += v;
         __syncthreads();
     }
+    const int total = off[kAppend];
     const int64_t base = c->seq_count;
-    const uint64_t step = c->step;
-    int64_t e = base + cnt[t] - k;
-    for (int j = lo; j < hi; ++j) {
-        const int L = sp.fin[j];
-        if (L > 0) {
-            const int64_t slot = e % sp.seq_cap;
-            sp.seq_eps[2 * slot] = (int64_t)(uint32_t)j | ((int64_t)L << 32);
-            sp.seq_eps[2 * slot + 1] = (int64_t)step - L + 1;
-            ++e;
+    for (int e = t; e < total; e += kAppend) {  // entry e: env block b with off[b] <= e < off[b + 1]
+        int lo = 0, hi = kAppend;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (off[mid] <= e) lo = mid; else hi = mid;
         }
+        const int64_t* src = sp.fin + 2 * ((int64_t)lo * kBlock + (e - off[lo]));
+        const int64_t slot = (base + e) % sp.seq_cap;
+        sp.seq_eps[2 * slot] = src[0];
+        sp.seq_eps[2 * slot + 1] = src[1];
     }
-    __syncthreads();
     if (t == 0) {
-        const int64_t total = cnt[kAppend - 1];
+        long long tot[6];
+        for (int k = 0; k < 6; ++k) {
+            long long v = 0;
+            for (int w = 0; w < kAppend / 64; ++w) v += wred[w][k];
+            tot[k] = v;
+        }
         c->seq_count = base + total;
         c->seq_size = c->seq_count < sp.seq_cap ? c->seq_count : sp.seq_cap;
         c->episodes += tot[0];
         c->ep_A += tot[1]; c->win_A += tot[2]; c->ep_P += tot[3]; c->win_P += tot[4];
         c->reward_B += (double)tot[5];
         double eps = c->epsilon;
-        for (long long q = 0; q < tot[0]; ++q) {  // epsilon = max(min_epsilon, epsilon * decay), per episode
+        for (long long q = 0; q < tot[0] && eps > sp.min_epsilon; ++q) {  // max(min_epsilon, eps * decay) per episode
             eps = eps * sp.epsilon_decay;
             if (eps < sp.min_epsilon) eps = sp.min_epsilon;
         }
         c->epsilon = eps;
-        c->step = step + 1;
+        c->step = c->step + 1;
     }
 }
 
@@ -178,7 +210,7 @@ struct SampleOut {
     int B, T;
 };
 
-__global__ __launch_bounds__(256) void k_rsp_sample(const pm_rnn_selfplay sp, SampleOut o) {
+__global__ __launch_bounds__(512) void k_rsp_sample(const pm_rnn_selfplay sp, SampleOut o) {
     pm_rnn_ctrl* c = sp.ctrl;
     const int64_t size = c->seq_size;
     const bool en = size > sp.min_episodes && size > 0;
@@ -186,29 +218,27 @@ __global__ __launch_bounds__(256) void k_rsp_sample(const pm_rnn_selfplay sp, Sa
     if (!en) return;
     const uint64_t now = c->step;  // steps [0, now) written; slot s % depth holds the latest s
     const int64_t first = c->seq_count - size;
-    for (int b = threadIdx.x; b < o.B; b += blockDim.x) {
+    for (int e = threadIdx.x; e < o.B * o.T; e += blockDim.x) {  // one (sequence, step) per thread
+        const int b = e / o.T, tau = e % o.T;
         // np.random.choice(len(buffer), batch, replace=True), then randint(0, len - T + 1) (:131, :147)
         const U4 r = philox64((uint32_t)b, TAG_SEQ, now, sp.seed_env);
         const int64_t j = below(r.x, (uint32_t)size);
         const int64_t slot = (first + j) % sp.seq_cap;
         const int64_t packed = sp.seq_eps[2 * slot];
         const int arena = (int)(packed & 0xffffffff), L = (int)(packed >> 32);
-        const int64_t start = sp.seq_eps[2 * slot + 1] + below(r.y, (uint32_t)(L - o.T + 1));
-        for (int tau = 0; tau < o.T; ++tau) {
-            const int64_t s = start + tau;
-            if ((int64_t)now - 1 - s >= sp.depth) atomicOr(&c->status, 1);  // overwritten
-            const float4* row =
-                reinterpret_cast<const float4*>(sp.trans + ((s % sp.depth) * (int64_t)sp.n + arena) * PM_TRANS_F);
-            const float4 r0 = row[0], r1 = row[1], r2 = row[2], r3 = row[3];
-            float* ob = o.obs + ((int64_t)b * o.T + tau) * 7;
-            float* nx = o.next + ((int64_t)b * o.T + tau) * 7;
-            ob[0] = r0.x; ob[1] = r0.y; ob[2] = r0.z; ob[3] = r0.w; ob[4] = r1.x; ob[5] = r1.y; ob[6] = r1.z;
-            nx[0] = r2.x; nx[1] = r2.y; nx[2] = r2.z; nx[3] = r2.w; nx[4] = r3.x; nx[5] = r3.y; nx[6] = r3.z;
-            const int bits = __float_as_int(r3.w);
-            o.rew[(int64_t)b * o.T + tau] = r1.w;
-            o.act[(int64_t)b * o.T + tau] = bits & 0xff;
-            o.done[(int64_t)b * o.T + tau] = (uint8_t)(bits >> 8);
-        }
+        const int64_t s = sp.seq_eps[2 * slot + 1] + below(r.y, (uint32_t)(L - o.T + 1)) + tau;
+        if ((int64_t)now - 1 - s >= sp.depth) atomicOr(&c->status, 1);  // overwritten
+        const float4* row =
+            reinterpret_cast<const float4*>(sp.trans + ((s % sp.depth) * (int64_t)sp.n + arena) * PM_TRANS_F);
+        const float4 r0 = row[0], r1 = row[1], r2 = row[2], r3 = row[3];
+        float* ob = o.obs + (int64_t)e * 7;
+        float* nx = o.next + (int64_t)e * 7;
+        ob[0] = r0.x; ob[1] = r0.y; ob[2] = r0.z; ob[3] = r0.w; ob[4] = r1.x; ob[5] = r1.y; ob[6] = r1.z;
+        nx[0] = r2.x; nx[1] = r2.y; nx[2] = r2.z; nx[3] = r2.w; nx[4] = r3.x; nx[5] = r3.y; nx[6] = r3.z;
+        const int bits = __float_as_int(r3.w);
+        o.rew[e] = r1.w;
+        o.act[e] = bits & 0xff;
+        o.done[e] = (uint8_t)(bits >> 8);
     }
 }
 
@@ -219,9 +249,10 @@ int check(const pm_rnn_selfplay* sp) {
                sp->T, sp->depth);
     PM_REQUIRE(sp->opp && sp->ep_reward && sp->ep_len && sp->reset && sp->w_opp && sp->paramsB && sp->w_B && sp->hA &&
                    sp->cA && sp->hB && sp->cB && sp->obsA && sp->obsB && sp->aA && sp->aB && sp->trans && sp->seq_eps &&
-                   sp->fin && sp->partials && sp->enable && sp->ctrl,
+                   sp->fin && sp->partials && sp->opp_list && sp->opp_cnt && sp->enable && sp->ctrl,
                PM_E_ARG, "pm_rnn_selfplay: null buffer");
     PM_REQUIRE((((uintptr_t)sp->trans) & 15) == 0, PM_E_ARG, "pm_rnn_selfplay: trans must be 16-byte aligned");
+    PM_REQUIRE(sp->n <= kAppend * kBlock, PM_E_SIZE, "pm_rnn_selfplay: n %d > %d", sp->n, kAppend * kBlock);
     return PM_OK;
 }
 
@@ -234,17 +265,22 @@ extern "C" int pm_rnn_selfplay_init(const pm_rnn_selfplay* sp, void* stream) {
     return PM_OK;
 }
 
-extern "C" int pm_rnn_selfplay_rollout(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {
+extern "C" int pm_rnn_selfplay_act(const pm_rnn_selfplay* sp, void* stream) {
     if (int rc = check(sp)) return rc;
-    hipStream_t st = pm_stream(stream);
     const uint64_t* ctr = &sp->ctrl->step;
     // modelB.reset_noise() then act (:385-387): one noise draw per vector step for all arenas
     if (int rc = pm_rnn_fold(sp->paramsB, sp->paramsB, PM_FOLD_TRAIN_FRESH, sp->seed_net, 0, ctr, sp->w_B, 1, stream))
         return rc;
     if (int rc = pm_rnn_act(sp->w_opp, sp->opp, 1 + sp->n_pool, sp->w_B, sp->obsA, sp->obsB, sp->hA, sp->cA, sp->hB,
                             sp->cB, sp->reset, 0.f, &sp->ctrl->epsilon, sp->seed_env, 0, ctr, sp->aA, sp->aB, nullptr,
-                            nullptr, sp->n, sp->chunk_A, sp->chunk_P, stream))
+                            nullptr, sp->n, sp->chunk_A, sp->chunk_P, sp->opp_list, sp->opp_cnt, stream))
         return rc;
+    return PM_OK;
+}
+
+extern "C" int pm_rnn_selfplay_env(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {
+    if (int rc = check(sp)) return rc;
+    hipStream_t st = pm_stream(stream);
     hipLaunchKernelGGL(k_rsp_env, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, st, *sp);
     PM_LAUNCHED("k_rsp_env");
     hipLaunchKernelGGL(k_rsp_append, dim3(1), dim3(kAppend), 0, st, *sp);
@@ -253,10 +289,15 @@ extern "C" int pm_rnn_selfplay_rollout(const pm_rnn_selfplay* sp, const pm_drqn*
         PM_REQUIRE(d->T == sp->T, PM_E_ARG, "pm_rnn_selfplay: learner T %d != %d", d->T, sp->T);
         const SampleOut o{const_cast<float*>(d->obs), const_cast<float*>(d->next), const_cast<float*>(d->rew),
                           const_cast<int32_t*>(d->act), const_cast<uint8_t*>(d->done), d->batch, d->T};
-        hipLaunchKernelGGL(k_rsp_sample, dim3(1), dim3(256), 0, st, *sp, o);
+        hipLaunchKernelGGL(k_rsp_sample, dim3(1), dim3(512), 0, st, *sp, o);
         PM_LAUNCHED("k_rsp_sample");
     }
     return PM_OK;
+}
+
+extern "C" int pm_rnn_selfplay_rollout(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {
+    if (int rc = pm_rnn_selfplay_act(sp, stream)) return rc;
+    return pm_rnn_selfplay_env(sp, d, stream);
 }
 
 extern "C" int pm_rnn_selfplay_step(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {

@@ -24,7 +24,6 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kLearn = 1024;              // k_learn / k_adam / k_prepare block
 constexpr int kGradN = PM_QNET_NHEAD;     // grad[520] = finished episodes, grad[521] = updated flag
-constexpr int kListNets = 64;             // opponent nets the env kernel keeps per-block lists for
 constexpr uint32_t kHashEmpty = 0xFFFFFFFFu;
 
 __device__ __forceinline__ bool learner_active(const pm_selfplay& sp) {
@@ -140,45 +139,9 @@ __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f) {
     }
 }
 
-// Per 256-arena block: its arenas grouped by opponent net for the next act (ascending within a
-// net), and (offset << 16 | count) per net, so the act kernel's opponent tiles read their rows with
-// two small loads instead of compacting ids next to MFMA waves (VALU there waits for the matrix
-// cores). Block-wide (kBlock threads); more than kListNets nets: no lists (the act kernel compacts).
-struct OppListSmem {
-    int woff[kBlock / 64][kListNets];  // per-wave count, then per-wave offset within the net
-    int noff[kListNets], ncnt[kListNets];
-};
 __device__ __forceinline__ void write_opp_lists(const pm_selfplay& sp, OppListSmem& sm, int blk, int i, bool valid,
                                                 int net) {
-    const int nn = sp.n_pool + 1;
-    if (nn > kListNets) return;  // uniform
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int rank = 0;
-    for (int k = 0; k < nn; ++k) {
-        const bool m = valid && net == k;
-        const unsigned long long b = __ballot(m);
-        if (m) rank = __popcll(b & ((1ull << lane) - 1ull));
-        if (lane == 0) sm.woff[wv][k] = __popcll(b);
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < nn) {
-        const int k = threadIdx.x;
-        int acc = 0;
-        for (int w = 0; w < kBlock / 64; ++w) {
-            const int c = sm.woff[w][k];
-            sm.woff[w][k] = acc;
-            acc += c;
-        }
-        sm.ncnt[k] = acc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int k = 0; k < nn; ++k) { sm.noff[k] = acc; acc += sm.ncnt[k]; }
-    }
-    __syncthreads();
-    if (valid) sp.opp_list[(size_t)blk * kBlock + sm.noff[net] + sm.woff[wv][net] + rank] = i;
-    if ((int)threadIdx.x < nn) sp.opp_cnt[(size_t)blk * nn + threadIdx.x] = (sm.noff[threadIdx.x] << 16) | sm.ncnt[threadIdx.x];
+    write_opp_lists(sp.n_pool + 1, sp.opp_list, sp.opp_cnt, sm, blk, i, valid, net);
 }
 
 // env.step (:242) + memory.push (:243) + episode bookkeeping (:245-249) + next opponent (:235-236)

@@ -31,7 +31,7 @@ PM_RNN_NW = 157456
 PM_TRANS_F = 16
 PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class EnvParams(ctypes.Structure):
@@ -86,8 +86,8 @@ class RnnCtrl(ctypes.Structure):
 class RnnSelfPlay(ctypes.Structure):
     _fields_ = [("env", EnvParams), ("st", EnvState)] + \
         [(n, c_void_p) for n in ("opp", "ep_reward", "ep_len", "reset", "w_opp", "paramsB", "w_B", "hA", "cA", "hB",
-                                 "cB", "obsA", "obsB", "aA", "aB", "trans", "seq_eps", "fin", "partials", "enable",
-                                 "ctrl")] + \
+                                 "cB", "obsA", "obsB", "aA", "aB", "trans", "seq_eps", "fin", "partials", "opp_list",
+                                 "opp_cnt", "enable", "ctrl")] + \
         [(n, c_i32) for n in ("n", "n_pool", "depth", "T", "chunk_A", "chunk_P")] + \
         [("seq_cap", c_i64), ("min_episodes", c_i64)] + \
         [(n, c_double) for n in ("min_epsilon", "epsilon_decay", "pool_ratio")] + \
@@ -111,12 +111,14 @@ _SIGS = {
     "pm_rnn_q": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_rnn_act": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_void_p, c_void_p,
-                           c_void_p, c_i32, c_i32, c_i32, c_void_p]),
+                           c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
     "pm_drqn_work_bytes": (c_i64, [c_i32, c_i32]),
     "pm_drqn_grads": (c_i32, [c_void_p, c_void_p]),
     "pm_drqn_apply": (c_i32, [c_void_p, c_void_p]),
     "pm_drqn_update": (c_i32, [c_void_p, c_void_p]),
     "pm_rnn_selfplay_init": (c_i32, [c_void_p, c_void_p]),
+    "pm_rnn_selfplay_act": (c_i32, [c_void_p, c_void_p]),
+    "pm_rnn_selfplay_env": (c_i32, [c_void_p, c_void_p, c_void_p]),
     "pm_rnn_selfplay_rollout": (c_i32, [c_void_p, c_void_p, c_void_p]),
     "pm_rnn_selfplay_step": (c_i32, [c_void_p, c_void_p, c_void_p]),
     "pm_per_work_bytes": (c_i64, [c_i64]),

@@ -129,7 +129,7 @@ def forward(w_eff, x_seq, h0=None, c0=None, stream=None):
 
 
 def act(w_opp, opp_id, w_B, obsA, obsB, stA, stB, reset=None, epsilon=0.0, seed=0, counter=0, eps_dev=None,
-        counter_dev=None, want_q=False, chunk0=0, chunk1=0, stream=None):
+        counter_dev=None, want_q=False, chunk0=0, chunk1=0, opp_list=None, opp_cnt=None, stream=None):
     """Both players' QNetRNN actions (fused K5): aA = argmax Q_opp(obsA; stA) greedy,
     aB = eps-greedy argmax Q_B(obsB; stB); stA = (hA, cA), stB = (hB, cB) advance in place."""
     lib = _lib.load()
@@ -149,5 +149,5 @@ def act(w_opp, opp_id, w_B, obsA, obsB, stA, stB, reset=None, epsilon=0.0, seed=
     check(lib.pm_rnn_act(ptr(w_opp), ptr(opp_id), w_opp.shape[0], ptr(w_B.contiguous()), ptr(obsA.contiguous()),
                          ptr(obsB.contiguous()), ptr(hA), ptr(cA), ptr(hB), ptr(cB), ptr(reset), float(epsilon),
                          ptr(eps_dev), int(seed), int(counter), ptr(counter_dev), ptr(aA), ptr(aB), ptr(qA), ptr(qB),
-                         n, int(chunk0), int(chunk1), stream_ptr(stream)), "pm_rnn_act")
+                         n, int(chunk0), int(chunk1), ptr(opp_list), ptr(opp_cnt), stream_ptr(stream)), "pm_rnn_act")
     return (aA, aB, qA, qB) if want_q else (aA, aB)

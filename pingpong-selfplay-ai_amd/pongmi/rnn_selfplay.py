@@ -75,8 +75,10 @@ class RNNSelfPlayLearner:
         # ---- sequence buffer
         self.trans = torch.zeros((self.depth, n, PM_TRANS_F), **f32)
         self.seq_eps = torch.zeros((self.cap, 2), dtype=torch.int64, device=dev)
-        self.fin = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.fin = torch.zeros((((n + 255) // 256) * 256, 2), dtype=torch.int64, device=dev)  # staging
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
+        self.opp_list = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.opp_cnt = torch.zeros(((n + 255) // 256) * (len(pool_states) + 1), dtype=torch.int32, device=dev)
         self.enable = torch.zeros(1, dtype=torch.int32, device=dev)
         # ---- networks
         self.learner = DRQNLearner(modelB_state, batch=batch, T=self.T, gamma=gamma, lr=lr, max_norm=grad_clip_norm,
@@ -99,7 +101,7 @@ class RNNSelfPlayLearner:
         sp.env = env_params(**env_kw)
         sp.st = _lib.EnvState(*[ptr(self.f64[k]) for k in range(7)], *[ptr(self.i32[k]) for k in range(4)])
         for name in ("opp", "ep_reward", "ep_len", "reset", "w_opp", "w_B", "hA", "cA", "hB", "cB", "obsA", "obsB", "aA",
-                     "aB", "trans", "seq_eps", "fin", "partials", "enable", "ctrl"):
+                     "aB", "trans", "seq_eps", "fin", "partials", "opp_list", "opp_cnt", "enable", "ctrl"):
             setattr(sp, name, ptr(getattr(self, name)))
         sp.paramsB = ptr(self.learner.params)
         sp.n, sp.n_pool, sp.depth, sp.T = n, self.n_pool, self.depth, self.T
@@ -115,6 +117,15 @@ class RNNSelfPlayLearner:
         check(self.lib.pm_rnn_selfplay_init(ctypes.byref(sp), stream_ptr()), "pm_rnn_selfplay_init")
 
     # ------------------------------------------------------------------ stepping
+    def act(self):
+        """modelB fold with fresh noise + both players' act."""
+        check(self.lib.pm_rnn_selfplay_act(ctypes.byref(self.sp), stream_ptr()), "pm_rnn_selfplay_act")
+
+    def env_step(self):
+        """env tick + sequence store + counters + batch sample / enable flag."""
+        check(self.lib.pm_rnn_selfplay_env(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),
+              "pm_rnn_selfplay_env")
+
     def rollout(self):
         """fold + act + env + sequence store + batch sample (no update)."""
         check(self.lib.pm_rnn_selfplay_rollout(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),

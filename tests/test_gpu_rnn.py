@@ -129,8 +129,26 @@ def test_rnn_reset_rows_start_from_zero(golden):
     assert torch.equal(q, q2) and torch.equal(h, hz) and torch.equal(c, cz)
 
 
-@pytest.mark.parametrize("n,n_opp", [(1000, 1), (5000, 3), (257, 9)])
-def test_rnn_act_matches_q_step(golden, n, n_opp):
+def _host_lists(opp, nn):
+    """Per-256-arena-block opponent lists as the env kernels write them (write_opp_lists)."""
+    n = len(opp)
+    neb = (n + 255) // 256
+    lst = np.zeros(n, np.int32)
+    cnt = np.zeros(neb * nn, np.int32)
+    for e in range(neb):
+        ids = opp[e * 256:(e + 1) * 256]
+        off = 0
+        for k in range(nn):
+            sel = np.nonzero(ids == k)[0] + e * 256
+            lst[e * 256 + off:e * 256 + off + len(sel)] = sel
+            cnt[e * nn + k] = (off << 16) | len(sel)
+            off += len(sel)
+    return lst, cnt
+
+
+@pytest.mark.parametrize("n,n_opp,lists", [(1000, 1, False), (5000, 3, False), (257, 9, False), (5000, 3, True),
+                                           (33000, 5, True), (300, 9, True)])
+def test_rnn_act_matches_q_step(golden, n, n_opp, lists):
     """The fused two-player act: A greedy with its opponent's net, B greedy (eps = 0) — actions are
     the first-max argmax of the same Q values pm_rnn_q returns, states advance identically."""
     from pongmi import _lib, rnn
@@ -148,7 +166,14 @@ def test_rnn_act_matches_q_step(golden, n, n_opp):
     stB = [torch.from_numpy(rng.normal(0, 0.4, (n, 128)).astype(np.float32)).cuda() for _ in range(2)]
     refA = [t.clone() for t in stA]
     refB = [t.clone() for t in stB]
-    aA, aB, qA, qB = rnn.act(w_opp, opp, wB, obsA, obsB, stA, stB, epsilon=0.0, want_q=True, chunk1=1024)
+    kw = {}
+    if lists:  # side A packed over per-block lists (the self-play loop's path)
+        oid_h = opp.cpu().numpy() if opp is not None else np.zeros(n, np.int32)
+        if opp is None:
+            opp = torch.zeros(n, dtype=torch.int32, device="cuda")
+        lst, cnt = _host_lists(oid_h, n_opp)
+        kw = dict(opp_list=torch.from_numpy(lst).cuda(), opp_cnt=torch.from_numpy(cnt).cuda())
+    aA, aB, qA, qB = rnn.act(w_opp, opp, wB, obsA, obsB, stA, stB, epsilon=0.0, want_q=True, chunk1=1024, **kw)
     qB_ref = rnn.q_step(wB, obsB, *refB)
     qA_ref = torch.empty_like(qA)
     hA, cA = torch.empty_like(refA[0]), torch.empty_like(refA[1])

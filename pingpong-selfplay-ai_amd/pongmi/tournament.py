@@ -1,0 +1,200 @@
+"""Batched round-robin tournament: tests/test_round_robin.py (:117-386) with every (pair, episode)
+as one arena of a PongEnv2PBatch advanced in lockstep.
+
+The reference plays the pairs (i < j, participant order) one episode after another on one
+PongEnv2P: each episode is env.reset() (its serve drawn from the global `random` stream) and greedy
+play until done; the winner is decided by the final scoreA / scoreB (:317-321). Here the host draws
+every episode's serve from the same stream in the same order, so episode e of pair p sees exactly
+the serve the reference's would, and all episodes run at once:
+
+  * QNet participants act through pm_qnet_q on their arenas (eval mode: NoisyLinear mu, as
+    load_model_universal leaves them, :181-185);
+  * QNetRNN participants through pm_rnn_q with (h, c) per arena and side, from zero state;
+  * HardcodedBallFollower through the same comparison as :207-228 (float32, numpy 2 semantics).
+
+load_model_universal keeps the reference's checkpoint key order, its legacy fc.* -> dueling mapping
+(:144-168) and strictness, and loads with torch.load(weights_only=True). The returned frames have
+the reference's columns and order (match records: pair-major, episode 1..E; summary: by win_rate).
+"""
+import itertools
+import random as _pyrandom
+from pathlib import Path
+
+import torch
+
+from . import _lib
+from . import qnet as _qnet
+from . import rnn as _rnn
+from .env import PongEnv2PBatch, draw_serve, env_config
+
+STATE_KEYS = ["modelB_state", "modelA_state", "modelB", "modelA", "model", "state_dict"]
+HARDCODED = "HardcodedBallFollower"
+
+
+def _state_dict_of(ckpt, name, path):
+    for key in STATE_KEYS:
+        if key in ckpt:
+            return ckpt[key]
+    if all(not isinstance(v, dict) for v in ckpt.values()) and any(
+            k.startswith("fc.") or k.startswith("features.") for k in ckpt.keys()):
+        return ckpt
+    raise KeyError(f"no model state dict in checkpoint of '{name}' ({path}); tried {STATE_KEYS}, "
+                   f"keys {list(ckpt.keys())}")
+
+
+def load_model_universal(model_info, rnn_arch_config, device):
+    """A QNet / QNetRNN drop-in module in eval mode (test_round_robin.py:117-185), or the string
+    "HardcodedAgent" for the ball follower."""
+    from models.qnet import QNet
+    from models.qnet_rnn import QNetRNN
+    typ = model_info["type"]
+    name = model_info.get("name", Path(model_info["path"]).stem)
+    if typ == HARDCODED:
+        return "HardcodedAgent"
+    path = Path(model_info["path"])
+    if not path.exists():
+        raise FileNotFoundError(f"model '{name}' not found at {path}")
+    sd = _state_dict_of(torch.load(path, map_location="cpu", weights_only=True), name, path)
+    if typ == "QNet":
+        net = QNet(input_dim=7, output_dim=3)
+        if any(k.startswith(("features.", "fc_V.", "fc_A.")) for k in sd):
+            net.load_state_dict(sd, strict=True)
+        else:  # legacy fc.0 / fc.2 / fc.4 checkpoints: features copied, fc.4 becomes the advantage mu
+            mapped = {}
+            for k, v in sd.items():
+                if k.startswith("fc.0."):
+                    mapped[k.replace("fc.0.", "features.0.")] = v
+                elif k.startswith("fc.2."):
+                    mapped[k.replace("fc.2.", "features.2.")] = v
+            if "fc.4.weight" in sd and "fc.4.bias" in sd:
+                w4, b4 = sd["fc.4.weight"], sd["fc.4.bias"]
+                mapped["fc_A.weight_mu"], mapped["fc_A.bias_mu"] = w4, b4
+                mapped["fc_V.weight_mu"], mapped["fc_V.bias_mu"] = w4.mean(dim=0, keepdim=True), b4.mean().unsqueeze(0)
+            net.load_state_dict(mapped, strict=False)
+    elif typ == "QNetRNN":
+        cfg = rnn_arch_config or {}
+        net = QNetRNN(input_dim=7, output_dim=3, feature_dim=cfg.get("feature_dim", 128),
+                      lstm_hidden_dim=cfg.get("lstm_hidden_dim", 128), lstm_layers=cfg.get("lstm_layers", 1),
+                      head_hidden_dim=cfg.get("head_hidden_dim", 128))
+        net.load_state_dict(sd)
+    else:
+        raise ValueError(f"unsupported model type '{typ}' (model {name})")
+    net.eval()
+    net.reset_noise()
+    return net.to(device)
+
+
+class _Player:
+    """One participant's acting on the arenas where it plays side A and side B."""
+
+    def __init__(self, model, typ, rows_A, rows_B, device):
+        self.typ = typ
+        self.rows = (rows_A, rows_B)
+        if typ == "QNet":
+            self.w = _qnet.fold(model.packed().to(device), _lib.PM_FOLD_EVAL)[0]
+        elif typ == "QNetRNN":
+            self.w = _rnn.fold(model.packed().to(device), _lib.PM_FOLD_EVAL)[0]
+            self.state = [_rnn.init_state(int(r.numel()), device) for r in self.rows]
+
+    def act(self, side, obs, out):
+        rows = self.rows[side]
+        if rows.numel() == 0:
+            return
+        x = obs.index_select(0, rows)
+        if self.typ == "QNet":
+            a = _qnet.q_values(self.w, x).argmax(1)
+        elif self.typ == "QNetRNN":
+            h, c = self.state[side]
+            a = _rnn.q_step(self.w, x, h, c).argmax(1)
+        else:  # ball follower: obs = (ball_x, ball_y, vx, vy, my_paddle_x, other_paddle_x, spin)
+            ball, mine = x[:, 0], x[:, 4]
+            tol = torch.tensor(0.01, dtype=torch.float32, device=x.device)
+            a = torch.where(ball < mine - tol, 0, torch.where(ball > mine + tol, 2, 1))
+        out.index_copy_(0, rows, a.to(out.dtype))
+
+
+def run_round_robin_tournament(env_params, rnn_arch_params, models_to_compete, episodes_per_match, device="cuda",
+                               verbose_progress=False, rng=None, max_steps=1_000_000):
+    """(match_df, summary_df) as test_round_robin.py:238-386 returns them."""
+    import pandas as pd
+    rng = _pyrandom if rng is None else rng
+    participants = {}
+    for info in models_to_compete:
+        try:
+            participants[info["name"]] = {"model": load_model_universal(info, rnn_arch_params, device),
+                                          "type": info["type"], "path": info["path"]}
+        except Exception as e:  # the reference skips models that fail to load (:259-261)
+            print(f"  [error] loading '{info['name']}' failed: {e}")
+    if len(participants) < 2:
+        return pd.DataFrame(), pd.DataFrame(columns=["name", "win", "lose", "draw", "games_played", "win_rate"])
+    names = list(participants)
+    env_kw = {k: v for k, v in dict(env_params).items() if k not in ("render_size", "enable_render")}
+    cfg = env_config(**env_kw)
+    E = int(episodes_per_match)
+    pairs = list(itertools.combinations(range(len(names)), 2))
+    n = len(pairs) * E
+    serves = torch.tensor([draw_serve(rng, cfg) for _ in range(n)], dtype=torch.float64)  # pair-major, episode-minor
+    ida = torch.tensor([i for i, _ in pairs for _ in range(E)], dtype=torch.int64, device=device)
+    idb = torch.tensor([j for _, j in pairs for _ in range(E)], dtype=torch.int64, device=device)
+    players = [_Player(participants[nm]["model"], participants[nm]["type"], (ida == k).nonzero().flatten(),
+                       (idb == k).nonzero().flatten(), device) for k, nm in enumerate(names)]
+    env = PongEnv2PBatch(n, device=device, serve_table=serves.numpy().reshape(n, 1, 3), autoreset=False, **env_kw)
+    obsA, obsB = env.reset()
+    aA = torch.zeros(n, dtype=torch.int8, device=device)
+    aB = torch.zeros(n, dtype=torch.int8, device=device)
+    finished = torch.zeros(n, dtype=torch.bool, device=device)
+    score = torch.zeros((n, 2), dtype=torch.int32, device=device)
+    for t in range(max_steps):
+        for p in players:
+            p.act(0, obsA, aA)
+            p.act(1, obsB, aB)
+        (obsA, obsB), _, done, _ = env.step(aA, aB)
+        new = done.bool() & ~finished
+        score = torch.where(new.unsqueeze(1), env.i32[0:2].t(), score)
+        finished |= new
+        if (t + 1) % 16 == 0 and bool(finished.all()):
+            break
+    if not bool(finished.all()):
+        raise RuntimeError(f"tournament did not finish within {max_steps} steps")
+    score = score.cpu().numpy()
+    records = []
+    for p, (i, j) in enumerate(pairs):
+        for ep in range(E):
+            sA, sB = int(score[p * E + ep, 0]), int(score[p * E + ep, 1])
+            winner = names[i] if sA > sB else names[j] if sB > sA else "draw"
+            records.append({"episode": ep + 1, "player_A_name": names[i], "player_B_name": names[j],
+                            "player_A_type": participants[names[i]]["type"],
+                            "player_B_type": participants[names[j]]["type"], "score_A": sA, "score_B": sB,
+                            "winner_name": winner})
+            if verbose_progress:
+                print(f"  {names[i]} vs {names[j]} episode {ep + 1}: {sA}-{sB}, winner {winner}")
+    match_df = pd.DataFrame(records)
+    stats = {nm: {"win": 0, "lose": 0, "draw": 0, "games_played": 0} for nm in names}
+    for r in records:
+        a, b, w = r["player_A_name"], r["player_B_name"], r["winner_name"]
+        stats[a]["games_played"] += 1
+        stats[b]["games_played"] += 1
+        if w == a:
+            stats[a]["win"] += 1
+            stats[b]["lose"] += 1
+        elif w == b:
+            stats[b]["win"] += 1
+            stats[a]["lose"] += 1
+        else:
+            stats[a]["draw"] += 1
+            stats[b]["draw"] += 1
+    rows = [{"name": nm, **s, "win_rate": (s["win"] / s["games_played"]) if s["games_played"] else 0}
+            for nm, s in stats.items()]
+    summary_df = pd.DataFrame(rows).sort_values("win_rate", ascending=False).set_index("name")
+    return match_df, summary_df
+
+
+def save_results(match_df, summary_df, output_dir, timestamp):
+    """match_records_<ts>.csv and summary_ranking_<ts>.csv as the reference writes them (:497-501)."""
+    out = Path(output_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    match_path = out / f"match_records_{timestamp}.csv"
+    summary_path = out / f"summary_ranking_{timestamp}.csv"
+    match_df.to_csv(match_path, index=False)
+    summary_df.to_csv(summary_path)
+    return match_path, summary_path

@@ -113,31 +113,25 @@ class _Player:
         out.index_copy_(0, rows, a.to(out.dtype))
 
 
-def run_round_robin_tournament(env_params, rnn_arch_params, models_to_compete, episodes_per_match, device="cuda",
-                               verbose_progress=False, rng=None, max_steps=1_000_000):
-    """(match_df, summary_df) as test_round_robin.py:238-386 returns them."""
-    import pandas as pd
+def play_matches(env_params, models, plan, device="cuda", rng=None, max_steps=1_000_000):
+    """Play every episode of `plan` at once. models: name -> (module or "HardcodedAgent", type);
+    plan: [(name_A, name_B, episodes)] in the order the reference plays them (its serves are drawn
+    from `rng` / the global random stream in that order, one env.reset() per episode).
+    Returns [(name_A, name_B, score_A, score_B)] per episode, in plan order."""
     rng = _pyrandom if rng is None else rng
-    participants = {}
-    for info in models_to_compete:
-        try:
-            participants[info["name"]] = {"model": load_model_universal(info, rnn_arch_params, device),
-                                          "type": info["type"], "path": info["path"]}
-        except Exception as e:  # the reference skips models that fail to load (:259-261)
-            print(f"  [error] loading '{info['name']}' failed: {e}")
-    if len(participants) < 2:
-        return pd.DataFrame(), pd.DataFrame(columns=["name", "win", "lose", "draw", "games_played", "win_rate"])
-    names = list(participants)
     env_kw = {k: v for k, v in dict(env_params).items() if k not in ("render_size", "enable_render")}
     cfg = env_config(**env_kw)
-    E = int(episodes_per_match)
-    pairs = list(itertools.combinations(range(len(names)), 2))
-    n = len(pairs) * E
-    serves = torch.tensor([draw_serve(rng, cfg) for _ in range(n)], dtype=torch.float64)  # pair-major, episode-minor
-    ida = torch.tensor([i for i, _ in pairs for _ in range(E)], dtype=torch.int64, device=device)
-    idb = torch.tensor([j for _, j in pairs for _ in range(E)], dtype=torch.int64, device=device)
-    players = [_Player(participants[nm]["model"], participants[nm]["type"], (ida == k).nonzero().flatten(),
-                       (idb == k).nonzero().flatten(), device) for k, nm in enumerate(names)]
+    names = list(models)
+    index = {nm: k for k, nm in enumerate(names)}
+    eps = [(a, b) for a, b, e in plan for _ in range(int(e))]
+    n = len(eps)
+    if n == 0:
+        return []
+    serves = torch.tensor([draw_serve(rng, cfg) for _ in range(n)], dtype=torch.float64)
+    ida = torch.tensor([index[a] for a, _ in eps], dtype=torch.int64, device=device)
+    idb = torch.tensor([index[b] for _, b in eps], dtype=torch.int64, device=device)
+    players = [_Player(models[nm][0], models[nm][1], (ida == k).nonzero().flatten(), (idb == k).nonzero().flatten(),
+                       device) for k, nm in enumerate(names)]
     env = PongEnv2PBatch(n, device=device, serve_table=serves.numpy().reshape(n, 1, 3), autoreset=False, **env_kw)
     obsA, obsB = env.reset()
     aA = torch.zeros(n, dtype=torch.int8, device=device)
@@ -145,9 +139,9 @@ def run_round_robin_tournament(env_params, rnn_arch_params, models_to_compete, e
     finished = torch.zeros(n, dtype=torch.bool, device=device)
     score = torch.zeros((n, 2), dtype=torch.int32, device=device)
     for t in range(max_steps):
-        for p in players:
-            p.act(0, obsA, aA)
-            p.act(1, obsB, aB)
+        for pl in players:
+            pl.act(0, obsA, aA)
+            pl.act(1, obsB, aB)
         (obsA, obsB), _, done, _ = env.step(aA, aB)
         new = done.bool() & ~finished
         score = torch.where(new.unsqueeze(1), env.i32[0:2].t(), score)
@@ -155,23 +149,16 @@ def run_round_robin_tournament(env_params, rnn_arch_params, models_to_compete, e
         if (t + 1) % 16 == 0 and bool(finished.all()):
             break
     if not bool(finished.all()):
-        raise RuntimeError(f"tournament did not finish within {max_steps} steps")
+        raise RuntimeError(f"matches did not finish within {max_steps} steps")
     score = score.cpu().numpy()
-    records = []
-    for p, (i, j) in enumerate(pairs):
-        for ep in range(E):
-            sA, sB = int(score[p * E + ep, 0]), int(score[p * E + ep, 1])
-            winner = names[i] if sA > sB else names[j] if sB > sA else "draw"
-            records.append({"episode": ep + 1, "player_A_name": names[i], "player_B_name": names[j],
-                            "player_A_type": participants[names[i]]["type"],
-                            "player_B_type": participants[names[j]]["type"], "score_A": sA, "score_B": sB,
-                            "winner_name": winner})
-            if verbose_progress:
-                print(f"  {names[i]} vs {names[j]} episode {ep + 1}: {sA}-{sB}, winner {winner}")
-    match_df = pd.DataFrame(records)
+    return [(a, b, int(score[k, 0]), int(score[k, 1])) for k, (a, b) in enumerate(eps)]
+
+
+def summarize(records, names, key="name"):
+    """win / lose / draw / games_played / win_rate per participant, sorted by win_rate (:351-386)."""
+    import pandas as pd
     stats = {nm: {"win": 0, "lose": 0, "draw": 0, "games_played": 0} for nm in names}
-    for r in records:
-        a, b, w = r["player_A_name"], r["player_B_name"], r["winner_name"]
+    for a, b, w in records:
         stats[a]["games_played"] += 1
         stats[b]["games_played"] += 1
         if w == a:
@@ -183,9 +170,40 @@ def run_round_robin_tournament(env_params, rnn_arch_params, models_to_compete, e
         else:
             stats[a]["draw"] += 1
             stats[b]["draw"] += 1
-    rows = [{"name": nm, **s, "win_rate": (s["win"] / s["games_played"]) if s["games_played"] else 0}
+    rows = [{key: nm, **s, "win_rate": (s["win"] / s["games_played"]) if s["games_played"] else 0}
             for nm, s in stats.items()]
-    summary_df = pd.DataFrame(rows).sort_values("win_rate", ascending=False).set_index("name")
+    return pd.DataFrame(rows).sort_values("win_rate", ascending=False).set_index(key)
+
+
+def run_round_robin_tournament(env_params, rnn_arch_params, models_to_compete, episodes_per_match, device="cuda",
+                               verbose_progress=False, rng=None, max_steps=1_000_000):
+    """(match_df, summary_df) as test_round_robin.py:238-386 returns them."""
+    import pandas as pd
+    participants = {}
+    for info in models_to_compete:
+        try:
+            participants[info["name"]] = (load_model_universal(info, rnn_arch_params, device), info["type"])
+        except Exception as e:  # the reference skips models that fail to load (:259-261)
+            print(f"  [error] loading '{info['name']}' failed: {e}")
+    if len(participants) < 2:
+        return pd.DataFrame(), pd.DataFrame(columns=["name", "win", "lose", "draw", "games_played", "win_rate"])
+    names = list(participants)
+    E = int(episodes_per_match)
+    plan = [(a, b, E) for a, b in itertools.combinations(names, 2)]
+    played = play_matches(env_params, participants, plan, device, rng, max_steps)
+    records, k = [], 0
+    for a, b, e in plan:
+        for ep in range(e):
+            _, _, sA, sB = played[k]
+            k += 1
+            winner = a if sA > sB else b if sB > sA else "draw"
+            records.append({"episode": ep + 1, "player_A_name": a, "player_B_name": b,
+                            "player_A_type": participants[a][1], "player_B_type": participants[b][1],
+                            "score_A": sA, "score_B": sB, "winner_name": winner})
+            if verbose_progress:
+                print(f"  {a} vs {b} episode {ep + 1}: {sA}-{sB}, winner {winner}")
+    match_df = pd.DataFrame(records)
+    summary_df = summarize([(r["player_A_name"], r["player_B_name"], r["winner_name"]) for r in records], names)
     return match_df, summary_df
 
 

@@ -78,3 +78,25 @@ def test_tournament_skips_unloadable_and_writes_csvs(golden, tmp_path):
     back = pd.read_csv(s, index_col=0)
     assert list(back.columns) == ["win", "lose", "draw", "games_played", "win_rate"]
     assert pd.read_csv(m)["winner_name"].isin(list(summary_df.index) + ["draw"]).all()
+
+
+def test_arena_runs_only_missing_episodes(golden, tmp_path):
+    """pongmi.arena (tests/arena.py): register -> plan -> batched run -> database; a second run with a
+    higher target plays only the missing episodes of each pair."""
+    from pongmi.arena import create_match_plan, generate_summary_report, load_database, register_models, run_arena
+    _, infos = _write_checkpoints(golden, tmp_path)
+    cands = [{"id": i["name"], "type": i["type"], "path": i["path"], "description": ""} for i in infos[2:]]
+    db_path = tmp_path / "arena_database.json"
+    db = load_database(db_path)
+    assert register_models(db, cands)
+    assert run_arena(ENV, db, db_path, create_match_plan(db, 6), {}, rng=random.Random(3)) == 3 * 6
+    db = load_database(db_path)
+    assert len(db["match_history"]) == 18 and create_match_plan(db, 6) == []
+    plan = create_match_plan(db, 8)
+    assert [p["episodes_to_run"] for p in plan] == [2, 2, 2]
+    assert run_arena(ENV, db, db_path, plan, {}, rng=random.Random(4)) == 6
+    db = load_database(db_path)
+    rep = generate_summary_report(db)
+    assert (rep["games_played"] == 16).all() and rep["win"].sum() + rep["draw"].sum() // 2 == 24
+    for r in db["match_history"]:
+        assert r["winner"] in (r["p1"], r["p2"], "draw") and max(r["p1_score"], r["p2_score"]) == 3

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 3
+#define PM_ABI_VERSION 4
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -178,7 +178,8 @@ int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const f
  * loss = smooth_l1(q, y) (mean); gradients of all PM_RNN_NPARAM parameters by BPTT;
  * clip_grad_norm_(max_norm); Adam; targetB <- modelB every target_update_interval steps. */
 typedef struct pm_drqn_stats {
-    int64_t steps;  /* Adam steps taken (train_steps_count) */
+    int64_t steps;  /* updates taken (train_steps_count: target sync every target_update_interval) */
+    int64_t adam_t; /* the optimizer's step count (bias correction); a new optimizer restarts it at 0 */
     float loss;     /* smooth_l1 loss of the last update */
     float norm;     /* pre-clip total gradient norm of the last update (of the rank mean) */
     float q_mean;   /* mean q of the last batch */

@@ -71,7 +71,7 @@ inline int64_t drqn_layout(int B, int T, DrqnArgs* a, void* work) {
                   odS = L.add(128 * B), odH0 = L.add(128 * B), odH1 = L.add(128 * B), odC0 = L.add(128 * B),
                   odC1 = L.add(128 * B), odZ = L.add(512 * C0), odP2 = L.add(128 * C0), odP1 = L.add(64 * C0),
                   oEB = L.add(E_N), oET = L.add(E_N), oA = L.add(B), oR = L.add(B), oD = L.add(B), oOne = L.add(4),
-                  oPart = L.add(2 * kNormBlocks), oTs = L.add(2);
+                  oPart = L.add(2 * kNormBlocks), oTs = L.add(4);
     const int64_t bytes = L.total * 4;
     if (a && work) {
         float* w = static_cast<float*>(work);
@@ -397,10 +397,12 @@ __global__ __launch_bounds__(256) void k_drqn_norm(DrqnArgs a) {
         __syncthreads();
     }
     if (threadIdx.x == 0) a.part[blockIdx.x] = red[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const int64_t ts = a.stats->steps + 1;
-        *a.tstep = ts;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // tstep[0]: train step (target sync), tstep[1]: Adam t
+        const int64_t ts = a.stats->steps + 1, at = a.stats->adam_t + 1;
+        a.tstep[0] = ts;
+        a.tstep[1] = at;
         a.stats->steps = ts;
+        a.stats->adam_t = at;
     }
 }
 
@@ -424,8 +426,8 @@ __global__ __launch_bounds__(256) void k_drqn_adam(DrqnArgs a, AdamK k, float* p
         for (int j = 0; j < kNormBlocks; ++j) ss += ps[j];
         const float norm = (float)sqrt(ss);
         const float coef = (float)(k.max_norm / ((double)norm + 1e-6));  // clip_coef
-        const int64_t ts = *a.tstep;
-        const double bc1 = 1.0 - pow(k.beta1, (double)ts), bc2 = 1.0 - pow(k.beta2, (double)ts);
+        const int64_t ts = a.tstep[0], at = a.tstep[1];
+        const double bc1 = 1.0 - pow(k.beta1, (double)at), bc2 = 1.0 - pow(k.beta2, (double)at);
         cf[0] = coef < 1.0f ? coef : 1.0f;  // clamp(clip_coef, max=1)
         cf[1] = (float)(k.lr / bc1);
         cf[2] = (float)sqrt(bc2);

@@ -31,7 +31,7 @@ PM_RNN_NW = 157456
 PM_TRANS_F = 16
 PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class EnvParams(ctypes.Structure):
@@ -67,7 +67,8 @@ class SelfPlay(ctypes.Structure):
 
 
 class DrqnStats(ctypes.Structure):
-    _fields_ = [("steps", c_i64), ("loss", c_float), ("norm", c_float), ("q_mean", c_float), ("status", c_i32)]
+    _fields_ = [("steps", c_i64), ("adam_t", c_i64), ("loss", c_float), ("norm", c_float), ("q_mean", c_float),
+                ("status", c_i32)]
 
 
 class Drqn(ctypes.Structure):

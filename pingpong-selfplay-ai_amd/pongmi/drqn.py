@@ -18,7 +18,10 @@ import torch
 
 from . import _lib
 from ._lib import PM_RNN_NP, PM_RNN_NPARAM, check, stream_ptr
-from .rnn import pack_state_dict, unpack_state_dict
+from .checkpoint import adam_moments, adam_state_dict
+from .rnn import PARAM_LAYOUT, PARAM_KEYS, pack_state_dict, unpack_state_dict
+
+PARAM_SHAPES = [s for k, s in PARAM_LAYOUT if k in PARAM_KEYS]  # modelB.parameters() order
 
 
 class DRQNLearner:
@@ -92,11 +95,46 @@ class DRQNLearner:
     def stats(self):
         """(steps, loss, pre-clip grad norm, mean q) of the last update (host sync)."""
         s = _lib.DrqnStats.from_buffer_copy(bytes(self.stats_buf.cpu().numpy()))
-        return dict(steps=s.steps, loss=s.loss, norm=s.norm, q_mean=s.q_mean)
+        return dict(steps=s.steps, adam_t=s.adam_t, loss=s.loss, norm=s.norm, q_mean=s.q_mean)
 
     def state_dict(self):
         """modelB's state_dict (reference key names)."""
         return unpack_state_dict(self.params)
+
+    # ------------------------------------------------------------------ optimizer / counters
+    def _stats(self):
+        return _lib.DrqnStats.from_buffer_copy(bytes(self.stats_buf.cpu().numpy()))
+
+    def _set_stats(self, **kw):
+        s = self._stats()
+        for k, v in kw.items():
+            setattr(s, k, v)
+        self.stats_buf.copy_(torch.frombuffer(bytearray(bytes(s)), dtype=torch.uint8))
+
+    def optimizer_state_dict(self):
+        """torch.optim.Adam(modelB.parameters(), lr).state_dict() equivalent (train_rnn_iterative.py:335)."""
+        return adam_state_dict(PARAM_SHAPES, self.adam_m, self.adam_v, self._stats().adam_t, self.desc.lr,
+                               (self.desc.beta1, self.desc.beta2), self.desc.adam_eps)
+
+    def load_optimizer_state_dict(self, sd):
+        m, v, step = adam_moments(sd, PARAM_SHAPES)
+        self.adam_m.copy_(m)
+        self.adam_v.copy_(v)
+        self._set_stats(adam_t=step)
+
+    def new_optimizer(self):
+        """optimizerB = optim.Adam(modelB.parameters(), lr=lr): zero moments, step 0."""
+        self.adam_m.zero_()
+        self.adam_v.zero_()
+        self._set_stats(adam_t=0)
+
+    def set_train_steps(self, steps):
+        self._set_stats(steps=int(steps))
+
+    def load_params(self, modelB, target=None):
+        """modelB <- state; targetB <- target (default: a copy of the new modelB)."""
+        self.params.copy_(self._block(modelB))
+        self.target.copy_(self._block(target) if target is not None else self.params)
 
     def target_state_dict(self):
         return unpack_state_dict(self.target)

@@ -21,6 +21,7 @@ identical clip + Adam step (pongmi.drqn).
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -167,6 +168,55 @@ class RNNSelfPlayLearner:
 
     def modelA_state_dict(self):
         return unpack_state_dict(self.paramsA)
+
+    # ------------------------------------------------------------------ generation controller hooks
+    def reset_B(self, state, epsilon=1.0, reset_train_steps=True):
+        """modelB <- state with a new Adam, targetB <- modelB, epsilon reset (reset_model_b_for_new_attempt,
+        train_rnn_iterative.py:669-702; also the new-generation start, :711-722, which keeps
+        train_steps_count: reset_train_steps=False). The sequence buffer is kept, as there."""
+        self.learner.load_params(state)
+        self.learner.new_optimizer()
+        if reset_train_steps:
+            self.learner.set_train_steps(0)
+        self.set_epsilon(epsilon)
+
+    def add_pool_model(self, state):
+        """pool_models.append(net in eval mode) (:855-859): opponent slot n_pool + 1 for later draws."""
+        w = fold(pack_state_dict(state, self.device), _lib.PM_FOLD_EVAL)
+        self.w_opp = torch.cat([self.w_opp, w], 0).contiguous()
+        self.n_pool += 1
+        n = self.n
+        self.opp_cnt = torch.zeros(((n + 255) // 256) * (self.n_pool + 1), dtype=torch.int32, device=self.device)
+        sp = self.sp
+        sp.w_opp, sp.opp_cnt, sp.n_pool = ptr(self.w_opp), ptr(self.opp_cnt), self.n_pool
+        p_pool = sp.pool_ratio
+        sp.chunk_A = act_chunk(1.0 - p_pool, cap=2048)
+        sp.chunk_P = act_chunk(p_pool / self.n_pool, cap=2048)
+        self._rebuild_lists()
+
+    def _rebuild_lists(self):
+        """Per-block opponent lists for the current opponent ids (the env kernel keeps them after this)."""
+        opp = self.opp.cpu().numpy()
+        nn = self.n_pool + 1
+        neb = (self.n + 255) // 256
+        lst = np.zeros(self.n, np.int32)
+        cnt = np.zeros(neb * nn, np.int32)
+        for e in range(neb):
+            ids = opp[e * 256:(e + 1) * 256]
+            off = 0
+            for k in range(nn):
+                sel = np.nonzero(ids == k)[0] + e * 256
+                lst[e * 256 + off:e * 256 + off + len(sel)] = sel
+                cnt[e * nn + k] = (off << 16) | len(sel)
+                off += len(sel)
+        self.opp_list.copy_(torch.from_numpy(lst))
+        self.opp_cnt.copy_(torch.from_numpy(cnt))
+
+    def set_counters(self, **kw):
+        c = _lib.RnnCtrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))
+        for k, v in kw.items():
+            setattr(c, k, v)
+        self.ctrl.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
 
     def episodes(self):
         """The stored episodes, oldest first: (arena, first step, length) int64 [seq_size, 3] (host)."""

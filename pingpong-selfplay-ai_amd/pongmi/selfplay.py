@@ -20,7 +20,7 @@ import ctypes
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, checkpoint
 from ._lib import PM_QNET_NHEAD, PM_QNET_NP, PM_QNET_NW, PM_TRANS_F, check, ptr, stream_ptr
 from .dist import shard_seeds, splitmix64  # noqa: F401
 from .env import env_config, env_params
@@ -176,20 +176,9 @@ class SelfPlayLearner:
 
     def optimizer_state_dict(self):
         """torch.optim.Adam state_dict for the 8 head tensors (train_iterative.py:101-104)."""
-        c = self.counters()
-        m, v = self.adam_m.cpu(), self.adam_v.cpu()
-        state, o = {}, 0
         shapes = [(1, 64), (1,), (1, 64), (1,), (3, 64), (3,), (3, 64), (3,)]
-        for i, s in enumerate(shapes):
-            k = int(np.prod(s))
-            if c["train_steps"] > 0:
-                state[i] = {"step": torch.tensor(float(c["train_steps"])), "exp_avg": m[o:o + k].reshape(s).clone(),
-                            "exp_avg_sq": v[o:o + k].reshape(s).clone()}
-            o += k
-        return {"state": state, "param_groups": [{
-            "lr": self.hparams["lr"], "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 0, "amsgrad": False,
-            "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
-            "decoupled_weight_decay": False, "params": list(range(8))}]}
+        return checkpoint.adam_state_dict(shapes, self.adam_m, self.adam_v, self.counters()["train_steps"],
+                                          self.hparams["lr"])
 
     def reset_B(self, state, epsilon=1.0):
         """reset_B (train_iterative.py:213-224): fresh modelB from `state`, new Adam, empty replay,

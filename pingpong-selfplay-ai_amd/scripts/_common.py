@@ -1,0 +1,23 @@
+"""Shared entry-point plumbing for the training scripts: import paths, config, CLI."""
+import argparse
+import os
+import sys
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+
+def parse(description, default_arenas):
+    ap = argparse.ArgumentParser(description=description)
+    ap.add_argument("--arenas", type=int, default=default_arenas, help="arenas stepped in lockstep on the device")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--check-every", type=int, default=4, help="vector steps between episode-budget checks")
+    ap.add_argument("--config", default=None, help="config file (default: the reference's name, in the CWD)")
+    return ap.parse_args()
+
+
+def load_config(path):
+    import yaml
+    with open(path, "r") as f:
+        return yaml.safe_load(f)

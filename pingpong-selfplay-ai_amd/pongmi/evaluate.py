@@ -8,7 +8,8 @@ eval_vs_pool draws `random.choice(pool)` first) followed by ticks until a score 
 Here every episode is an arena of one PongEnv2PBatch, all advanced in lockstep (K1 + the fused
 two-player act K2, both players greedy): the host draws the per-episode opponent and serve from
 the same `random` stream in the reference's order, so episode e sees exactly the serve and the
-opponent the reference's e-th episode would. The nets act as their modules would: a QNet in
+opponent the reference's e-th episode would. The episodes run inside the match megakernel (K8,
+pongmi.play): one launch plays every episode to the end with the arenas in registers. The nets act as their modules would: a QNet in
 train mode uses mu + sigma * (its current epsilon buffers), in eval mode mu (models/qnet.py:43-50).
 """
 import random as _pyrandom
@@ -46,10 +47,22 @@ def folded_weights(net, device):
     return fold(block, mode)[0]
 
 
-def run_episodes(env_kw, w_opp, opp_id, w_B, serves, device="cuda", max_steps=1_000_000, check_every=16):
-    """One greedy episode per arena. serves [E, 3] (vx, vy, spin) per episode; w_opp [nets, NW] with
-    opp_id [E] (None: net 0) for player A, w_B for player B. Returns (wins [E] bool: rB > rA on the
-    episode's last step, lengths [E] int) as host numpy arrays."""
+def run_episodes(env_kw, w_opp, opp_id, w_B, serves, device="cuda", max_steps=1_000_000):
+    """One greedy episode per arena, each played start to finish inside the match megakernel
+    (K8, pongmi.play). serves [E, 3] (vx, vy, spin) per episode; w_opp [nets, NW] with opp_id [E]
+    (None: net 0) for player A, w_B for player B. Returns (wins [E] bool: rB > rA on the episode's
+    last step, lengths [E] int) as host numpy arrays."""
+    from .play import play
+    E = int(np.asarray(serves).reshape(-1, 3).shape[0])
+    n_opp = int(w_opp.shape[0])
+    w_nets = torch.cat([w_opp.reshape(n_opp, -1), w_B.reshape(1, -1)]).to(device)
+    netA = np.zeros(E, np.int64) if opp_id is None else np.asarray(torch.as_tensor(opp_id).cpu(), np.int64)
+    _, _, length, last = play(env_kw, w_nets, netA, np.full(E, n_opp), serves, device, max_steps)
+    return last > 0, length
+
+
+def run_episodes_stepped(env_kw, w_opp, opp_id, w_B, serves, device="cuda", max_steps=1_000_000, check_every=16):
+    """run_episodes as one act launch (K2) + one env launch (K1) per tick, all arenas in lockstep."""
     E = int(serves.shape[0])
     env = PongEnv2PBatch(E, device=device, serve_table=np.asarray(serves, np.float64).reshape(E, 1, 3),
                          autoreset=False, **env_kw)

@@ -7,8 +7,10 @@ play until done; the winner is decided by the final scoreA / scoreB (:317-321). 
 every episode's serve from the same stream in the same order, so episode e of pair p sees exactly
 the serve the reference's would, and all episodes run at once:
 
-  * QNet participants act through pm_qnet_q on their arenas (eval mode: NoisyLinear mu, as
-    load_model_universal leaves them, :181-185);
+  * episodes between QNet / ball-follower players run start to finish in the match megakernel
+    (K8, pongmi.play: both nets staged per block, arenas in registers, one launch);
+  * in episodes with a QNetRNN player, QNet participants act through pm_qnet_q on their arenas
+    (eval mode: NoisyLinear mu, as load_model_universal leaves them, :181-185);
   * QNetRNN participants through pm_rnn_q with (h, c) per arena and side, from zero state;
   * HardcodedBallFollower through the same comparison as :207-228 (float32, numpy 2 semantics).
 
@@ -20,6 +22,7 @@ import itertools
 import random as _pyrandom
 from pathlib import Path
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -117,22 +120,56 @@ def play_matches(env_params, models, plan, device="cuda", rng=None, max_steps=1_
     """Play every episode of `plan` at once. models: name -> (module or "HardcodedAgent", type);
     plan: [(name_A, name_B, episodes)] in the order the reference plays them (its serves are drawn
     from `rng` / the global random stream in that order, one env.reset() per episode).
+    Episodes between QNet / ball-follower players run in the match megakernel (K8, pongmi.play);
+    episodes with a QNetRNN player step all their arenas in lockstep (K5 + K1 per tick).
     Returns [(name_A, name_B, score_A, score_B)] per episode, in plan order."""
     rng = _pyrandom if rng is None else rng
     env_kw = {k: v for k, v in dict(env_params).items() if k not in ("render_size", "enable_render")}
     cfg = env_config(**env_kw)
-    names = list(models)
-    index = {nm: k for k, nm in enumerate(names)}
     eps = [(a, b) for a, b, e in plan for _ in range(int(e))]
     n = len(eps)
     if n == 0:
         return []
-    serves = torch.tensor([draw_serve(rng, cfg) for _ in range(n)], dtype=torch.float64)
+    serves = np.array([draw_serve(rng, cfg) for _ in range(n)], np.float64).reshape(n, 3)
+    score = np.zeros((n, 2), np.int64)
+    rnn = {nm for nm, (_, typ) in models.items() if typ == "QNetRNN"}
+    stepped = np.array([a in rnn or b in rnn for a, b in eps], bool)
+    if (~stepped).any():
+        score[~stepped] = _play_fused(env_kw, models, [eps[k] for k in np.nonzero(~stepped)[0]], serves[~stepped],
+                                      device, max_steps)
+    if stepped.any():
+        score[stepped] = _play_stepped(env_kw, models, [eps[k] for k in np.nonzero(stepped)[0]], serves[stepped],
+                                       device, max_steps)
+    return [(a, b, int(score[k, 0]), int(score[k, 1])) for k, (a, b) in enumerate(eps)]
+
+
+def _play_fused(env_kw, models, eps, serves, device, max_steps):
+    """QNet / ball-follower episodes in the match megakernel: [E, 2] final scores."""
+    from .play import FOLLOWER, play
+    ids, weights = {}, []
+    for nm in dict.fromkeys([x for ab in eps for x in ab]):
+        module, typ = models[nm]
+        if typ == HARDCODED:
+            ids[nm] = FOLLOWER
+        else:  # eval mode: NoisyLinear mu (load_model_universal leaves the nets in eval, :181-185)
+            ids[nm] = len(weights)
+            weights.append(_qnet.fold(module.packed().to(device), _lib.PM_FOLD_EVAL)[0])
+    w = torch.stack(weights) if weights else None
+    sA, sB, _, _ = play(env_kw, w, [ids[a] for a, _ in eps], [ids[b] for _, b in eps], serves, device, max_steps)
+    return np.stack([sA, sB], 1)
+
+
+def _play_stepped(env_kw, models, eps, serves, device, max_steps):
+    """Episodes with a QNetRNN player: all arenas in lockstep, one act per participant and side plus
+    one env launch per tick: [E, 2] final scores."""
+    n = len(eps)
+    names = list(dict.fromkeys([x for ab in eps for x in ab]))
+    index = {nm: k for k, nm in enumerate(names)}
     ida = torch.tensor([index[a] for a, _ in eps], dtype=torch.int64, device=device)
     idb = torch.tensor([index[b] for _, b in eps], dtype=torch.int64, device=device)
     players = [_Player(models[nm][0], models[nm][1], (ida == k).nonzero().flatten(), (idb == k).nonzero().flatten(),
                        device) for k, nm in enumerate(names)]
-    env = PongEnv2PBatch(n, device=device, serve_table=serves.numpy().reshape(n, 1, 3), autoreset=False, **env_kw)
+    env = PongEnv2PBatch(n, device=device, serve_table=serves.reshape(n, 1, 3), autoreset=False, **env_kw)
     obsA, obsB = env.reset()
     aA = torch.zeros(n, dtype=torch.int8, device=device)
     aB = torch.zeros(n, dtype=torch.int8, device=device)
@@ -150,8 +187,7 @@ def play_matches(env_params, models, plan, device="cuda", rng=None, max_steps=1_
             break
     if not bool(finished.all()):
         raise RuntimeError(f"matches did not finish within {max_steps} steps")
-    score = score.cpu().numpy()
-    return [(a, b, int(score[k, 0]), int(score[k, 1])) for k, (a, b) in enumerate(eps)]
+    return score.cpu().numpy()
 
 
 def summarize(records, names, key="name"):

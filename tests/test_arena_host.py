@@ -46,3 +46,22 @@ def test_plan_register_roundtrip(golden, tmp_path):
     (tmp_path / "bad.json").write_text("{not json")
     assert load_database(tmp_path / "bad.json") == {"models": [], "match_history": []}
     assert load_database(tmp_path / "missing.json") == {"models": [], "match_history": []}
+
+
+def test_play_plan_blocks_groups_pairs():
+    """pongmi.play.plan_blocks: arenas grouped by (net A, net B) in first-appearance order, ascending
+    within a pair, each group padded to whole 128-slot blocks."""
+    import numpy as np
+    from pongmi.play import BLOCK, plan_blocks
+    blk, slots = plan_blocks([0, 1, 0, 1, 0], [2, 2, 2, 2, 2])
+    assert blk.tolist() == [[0, 2], [1, 2]] and slots.shape == (2 * BLOCK,)
+    assert slots[:4].tolist() == [0, 2, 4, -1] and slots[BLOCK:BLOCK + 3].tolist() == [1, 3, -1]
+    rng = np.random.default_rng(0)
+    a, b = rng.integers(-1, 3, 1000), rng.integers(-1, 3, 1000)
+    blk, slots = plan_blocks(a, b)
+    assert sorted(slots[slots >= 0].tolist()) == list(range(1000))
+    for k, (na, nb) in enumerate(blk):
+        idx = slots[k * BLOCK:(k + 1) * BLOCK]
+        idx = idx[idx >= 0]
+        assert len(idx) and (a[idx] == na).all() and (b[idx] == nb).all() and (np.diff(idx) > 0).all()
+    assert plan_blocks([], [])[0].shape == (0, 2)

@@ -136,16 +136,21 @@ int pm_qnet_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const 
 /* K8 — whole greedy matches in one launch (the match megakernel, csrc/pm_play.hip). Replaces the
  * per-episode loops of scripts/train_iterative.py:171-196 (eval_vs_model / eval_vs_pool),
  * tests/test_round_robin.py:290-330 and tests/arena.py:294-320 for QNet and ball-follower players.
- * Arena i resets with serves[i] = (vx, vy, spin) and plays until a score reaches max_score, both
+ * Every arena resets with its serve (vx, vy, spin) and plays until a score reaches max_score, both
  * players greedy (argmax, first max) on effective weights w_nets[net] (PM_QNET_NW floats each,
- * 16-B aligned; net -1 = HardcodedBallFollower). Work is given per block of 128 arena slots sharing
- * one pair: blk_nets[2b], blk_nets[2b+1] = (net A, net B) of block b, arenas[128 b + s] = arena
- * index or -1 (padding). Outputs per arena: final scores, length (-1: not done within max_steps)
- * and last[i] = sign(rB - rA) of the final tick. *status (device, zeroed by the caller) counts
- * arenas not finished plus invalid net / arena ids. All device pointers except p. */
+ * 16-B aligned; net -1 = HardcodedBallFollower). Work is given as slots: order[s] = arena of slot
+ * s, serves[s] = its serve ([m][3] f64, slot order). Block b plays slots
+ * [blk_range[2b], blk_range[2b] + blk_range[2b+1]) (at most 1024 slots) with nets
+ * (blk_nets[2b], blk_nets[2b+1]) for (A, B), 128 at a time, a finished slot's column taking the
+ * next one. max_steps bounds the ticks of each wave over all its slots. Outputs per arena: final
+ * scores, length and last[i] = sign(rB - rA) of the final tick; arenas not finished keep the
+ * caller's length (initialise it to -1). *status (device, zeroed by the caller) counts invalid net /
+ * arena ids, invalid ranges and episodes cut by max_steps. All pointers except p are device
+ * pointers. */
 int pm_play(const pm_env_params* p, const float* w_nets, int32_t n_nets, const int32_t* blk_nets,
-            const int32_t* arenas, int32_t n_blocks, const double* serves, int32_t n, int32_t max_steps,
-            int32_t* scoreA, int32_t* scoreB, int32_t* length, int8_t* last, int32_t* status, void* stream);
+            const int32_t* blk_range, int32_t n_blocks, const int32_t* order, const double* serves, int32_t n,
+            int32_t max_steps, int32_t* scoreA, int32_t* scoreB, int32_t* length, int8_t* last, int32_t* status,
+            void* stream);
 
 /* ---------------------------------------------------------------- QNetRNN (K5) */
 

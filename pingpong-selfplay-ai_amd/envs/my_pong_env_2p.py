@@ -10,8 +10,8 @@ pm_env_reset / pm_env_step kernels). The scalar API is the reference's:
 Serves are drawn on the host from the global `random` module with the reference's own draw order
 and expressions (:94-110) and handed to the kernel, so a script that seeds `random` sees the
 reference's trajectories bit for bit. The readable attributes (ball_x, ..., bounce_count) are
-fetched from the device on access. Rendering (:265-306) is not part of this path: it needs pygame,
-which is imported lazily only when enable_render=True.
+fetched from the device on access. render() (:265-306) draws the reference's scene through
+pongmi.viewer.ArenaView; pygame is imported lazily, only when enable_render=True.
 """
 import random
 
@@ -86,8 +86,15 @@ class PongEnv2P:
         return obsA, obsB
 
     def render(self):
+        """The reference's scene (:265-306) through pongmi.viewer (pygame window; frame() is headless)."""
         if not self.enable_render:
             return
+        if getattr(self, "_view", None) is None:
+            from pongmi.viewer import ArenaView
+            self._view = ArenaView(self._env, 0, self.render_size)
+        self._view.spin_angle = self.spin_angle
+        self._view.render()
+        self.spin_angle = self._view.spin_angle
 
     def close(self):
         pass

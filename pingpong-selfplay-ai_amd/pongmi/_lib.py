@@ -113,8 +113,8 @@ _SIGS = {
     "pm_rnn_act": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
-    "pm_play": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_i32, c_void_p, c_void_p,
-                        c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pm_play": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_i32,
+                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pm_drqn_work_bytes": (c_i64, [c_i32, c_i32]),
     "pm_drqn_grads": (c_i32, [c_void_p, c_void_p]),
     "pm_drqn_apply": (c_i32, [c_void_p, c_void_p]),

@@ -50,18 +50,23 @@ def test_plan_register_roundtrip(golden, tmp_path):
 
 def test_play_plan_blocks_groups_pairs():
     """pongmi.play.plan_blocks: arenas grouped by (net A, net B) in first-appearance order, ascending
-    within a pair, each group padded to whole 128-slot blocks."""
+    within a pair, each group split into block ranges of per_block slots."""
     import numpy as np
-    from pongmi.play import BLOCK, plan_blocks
-    blk, slots = plan_blocks([0, 1, 0, 1, 0], [2, 2, 2, 2, 2])
-    assert blk.tolist() == [[0, 2], [1, 2]] and slots.shape == (2 * BLOCK,)
-    assert slots[:4].tolist() == [0, 2, 4, -1] and slots[BLOCK:BLOCK + 3].tolist() == [1, 3, -1]
-    rng = np.random.default_rng(0)
-    a, b = rng.integers(-1, 3, 1000), rng.integers(-1, 3, 1000)
-    blk, slots = plan_blocks(a, b)
-    assert sorted(slots[slots >= 0].tolist()) == list(range(1000))
-    for k, (na, nb) in enumerate(blk):
-        idx = slots[k * BLOCK:(k + 1) * BLOCK]
-        idx = idx[idx >= 0]
-        assert len(idx) and (a[idx] == na).all() and (b[idx] == nb).all() and (np.diff(idx) > 0).all()
+    from pongmi.play import COLUMNS, MAX_SLOTS, TARGET_BLOCKS, plan_blocks
+    blk, rng_, order = plan_blocks([0, 1, 0, 1, 0], [2, 2, 2, 2, 2])
+    assert blk.tolist() == [[0, 2], [1, 2]] and rng_.tolist() == [[0, 3], [3, 2]] and order.tolist() == [0, 2, 4, 1, 3]
+    r = np.random.default_rng(0)
+    a, b = r.integers(-1, 3, 1000), r.integers(-1, 3, 1000)
+    for per_block in (None, 7, 128):
+        blk, rng_, order = plan_blocks(a, b, per_block)
+        assert sorted(order.tolist()) == list(range(1000))
+        assert rng_[:, 1].sum() == 1000 and (rng_[1:, 0] == np.cumsum(rng_[:, 1])[:-1]).all()
+        for (na, nb), (s0, c) in zip(blk, rng_):
+            idx = order[s0:s0 + c]
+            assert 0 < c <= (per_block or COLUMNS)
+            assert (a[idx] == na).all() and (b[idx] == nb).all() and (np.diff(idx) > 0).all()
+    big = plan_blocks(np.zeros(COLUMNS * TARGET_BLOCKS * 3), np.ones(COLUMNS * TARGET_BLOCKS * 3))
+    assert big[0].shape[0] == TARGET_BLOCKS and (big[1][:, 1] == 3 * COLUMNS).all()
+    huge = plan_blocks(np.zeros(MAX_SLOTS * TARGET_BLOCKS * 2), np.ones(MAX_SLOTS * TARGET_BLOCKS * 2))
+    assert huge[0].shape[0] == 2 * TARGET_BLOCKS and (huge[1][:, 1] == MAX_SLOTS).all()
     assert plan_blocks([], [])[0].shape == (0, 2)

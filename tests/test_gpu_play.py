@@ -51,6 +51,22 @@ def test_play_matches_stepped_episodes(E, n_opp):
     assert (length > 0).all()
 
 
+@pytest.mark.parametrize("per_block", [128, 640, 1024])
+def test_play_lane_refill_matches_stepped(per_block):
+    """Blocks with more slots than columns: finished columns take the next slot of the range (1, 5
+    and 8 slots per column). Every episode must equal the stepped loop's."""
+    from pongmi.evaluate import run_episodes_stepped
+    from pongmi.play import play
+    E, n_opp = 8192, 3
+    w = _nets(n_opp + 1, seed=77)
+    opp = np.random.default_rng(1).integers(0, n_opp, E).astype(np.int32)
+    serves = _serves(E, 21)
+    sA, sB, length, last = play(ENV_KW, w, opp, np.full(E, n_opp), serves, per_block=per_block)
+    wins_s, length_s = run_episodes_stepped(ENV_KW, w[:n_opp], opp, w[n_opp], serves)
+    assert np.array_equal(length, length_s) and np.array_equal(last > 0, wins_s)
+    assert (np.maximum(sA, sB) == 3).all()
+
+
 def test_play_scores_and_follower_pairs_match_stepped():
     """Tournament shapes: QNet-QNet, QNet-follower, follower-QNet, follower-follower pairs, ragged."""
     from models.qnet import QNet

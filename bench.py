@@ -16,7 +16,8 @@ Rank 0 prints one JSON line. Also reported:
                 vs the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per launch from the
                 committed counter profile (profiles/r1_pmc.json, same workload), null without it
   env_roofline  k_env (env tick + replay push + bookkeeping, 282 algorithmic B / env-step) vs 8 TB/s
-  env_step_roofline  K1 (pm_env_step) alone at the same n: 203 B / env-step vs 8 TB/s (N=1 only)
+  env_step_roofline  K1 (pm_env_step, autoreset of done arenas) alone at the same n: 203 B / env-step
+                vs 8 TB/s, timed over graph-replayed back-to-back launches (N=1 only)
   cpu_baseline  the oracle's CPU port of the same vector step, 1 core, bounded sample (N=1 only)
 """
 import argparse
@@ -62,30 +63,43 @@ def synthetic_qnet(seed):
     return {k: v.clone() for k, v in QNet(7, 3).state_dict().items()}
 
 
-def time_env_step(n, reps=200):
+def time_env_step(n, per_graph=50, replays=20):
+    """K1 alone: pm_env_step with autoreset of done arenas (term rows for done arenas only: the
+    203 B / env-step of SURVEY.md 8d). `per_graph` back-to-back launches are captured in one HIP
+    graph so the host launch rate (ctypes, ~8 us per call) does not pace the queue; HIP events on
+    the replay stream bracket `replays` replays. avg_us = elapsed / launches."""
     from pongmi.env import PongEnv2PBatch
-    env = PongEnv2PBatch(n, seed=3, autoreset=True, **ENV_KW)
+    env = PongEnv2PBatch(n, seed=3, autoreset="done", **ENV_KW)
     env.reset()
-    g = torch.Generator(device="cuda").manual_seed(0)
-    aA = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=g)
-    aB = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=g)
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    aA = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=gen)
+    aB = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=gen)
     for _ in range(20):
         env.step(aA, aB)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    total = 0.0
-    for _ in range(reps):
-        torch.cuda._sleep(200_000)  # keep the queue busy so the events bracket the kernel, not the host launch
-        e0.record()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
         env.step(aA, aB)
-        e1.record()
-        e1.synchronize()
-        total += e0.elapsed_time(e1)
-    t = total / reps * 1e-3
+        s.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(per_graph):
+                env.step(aA, aB)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(3):
+            g.replay()
+        e0.record(s)
+        for _ in range(replays):
+            g.replay()
+        e1.record(s)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) * 1e-3 / (per_graph * replays)
     achieved = n * ENV_BYTES / t / 1e9
     return {"bound": "hbm", "kernel": "k_env_step", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
-            "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-            "avg_us": round(t * 1e6, 2), "bytes_per_env_step": ENV_BYTES, "n": n}
+            "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic("k_env_step"),
+            "avg_us": round(t * 1e6, 2), "bytes_per_env_step": ENV_BYTES, "n": n,
+            "timing": f"HIP events over {replays} graph replays x {per_graph} launches, autoreset='done'"}
 
 
 def cpu_baseline(n, seconds=12.0):

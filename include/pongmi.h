@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 4
+#define PM_ABI_VERSION 5
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -38,18 +38,21 @@ extern "C" {
 
 /* ---------------------------------------------------------------- environment (K1) */
 
-/* PongEnv2P constructor parameters (envs/my_pong_env_2p.py:19-81). The last four doubles are
+/* PongEnv2P constructor parameters (envs/my_pong_env_2p.py:19-81). The last six doubles are
  * derived constants the HOST computes with the reference's own Python expressions so the device
  * reproduces them bit for bit:
  *   half_width   = paddle_width/2                     (:152,190)
  *   speed_scale  = 1.0 + speed_increment              (:230)
  *   inertia      = (2/5) * ball_mass * radius**2      (envs/physics.py:9)
- *   jt_coef      = 2*ball_mass/7.0                    (envs/physics.py:10)                  */
+ *   jt_coef      = 2*ball_mass/7.0                    (envs/physics.py:10)
+ *   inv_mass     = 1.0/ball_mass, inv_inertia = 1.0/inertia (correctly rounded reciprocals: the
+ *                  device divides by ball_mass and inertia as q = a*inv; q + fma(-q, b, a)*inv,
+ *                  which is the correctly rounded a/b, the quotient physics.py:20-21 computes)  */
 typedef struct pm_env_params {
     double paddle_width, paddle_speed, magnus_factor, restitution, friction, ball_mass, radius;
     double speed_lo, speed_hi, spin_lo, spin_hi;
     double ang0_lo, ang0_hi, ang1_lo, ang1_hi;
-    double half_width, speed_scale, inertia, jt_coef;
+    double half_width, speed_scale, inertia, jt_coef, inv_mass, inv_inertia;
     int32_t max_score, speed_scale_every, enable_spin, _pad;
 } pm_env_params;
 
@@ -76,8 +79,12 @@ int pm_env_reset(const pm_env_params* p, const pm_env_state* s, const uint8_t* m
  * _get_obs :235-263) for n arenas: aA/aB [n] in {0,1,2}; writes obsA/obsB [n][7], rA/rB [n]
  * (values -1/0/+1), done [n]. With autoreset != 0, done arenas are then reset as pm_env_reset
  * (inject / seed as above); obsA/obsB then hold the post-reset observation, and term_obsA /
- * term_obsB (nullable) the observation returned by the terminal step (the `nB` the reference
- * stores in replay, scripts/train_iterative.py:242-243). */
+ * term_obsB (nullable, both or neither) the observation returned by the terminal step (the `nB`
+ * the reference stores in replay, scripts/train_iterative.py:242-243):
+ *   autoreset 1: every term row is written (the step's pre-reset observation of every arena);
+ *   autoreset 2: only the rows of arenas with done[i] != 0 are written, the others keep their
+ *                contents (next state for replay = done ? term_obs : obs; SURVEY.md §8d's 203 B
+ *                per env-step). With autoreset 0 the term rows, if given, equal obs. */
 int pm_env_step(const pm_env_params* p, const pm_env_state* s, const int8_t* aA, const int8_t* aB, float* obsA,
                 float* obsB, float* rA, float* rB, uint8_t* done, float* term_obsA, float* term_obsB,
                 int32_t autoreset, const double* inject, int32_t inject_cap, uint64_t seed, int32_t* status,

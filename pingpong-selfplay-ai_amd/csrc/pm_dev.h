@@ -160,6 +160,22 @@ __device__ __forceinline__ void store_rows7(float* __restrict__ dst, float (*lds
     __syncthreads();
 }
 
+// The copy-out half of store_rows7 for rows the caller already staged in LDS (and fenced with a
+// barrier): several outputs can share one barrier. No barrier inside.
+__device__ __forceinline__ void copy_rows7(float* __restrict__ dst, const float (*lds)[7], int i0, int n) {
+    const int t = threadIdx.x;
+    const int rows = min((int)blockDim.x, n - i0);
+    float* base = dst + (size_t)i0 * 7;
+    const float* src = &lds[0][0];
+    if (rows == (int)blockDim.x && (((uintptr_t)base) & 15) == 0) {
+        float4* d4 = reinterpret_cast<float4*>(base);
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        for (int f = t; f < rows * 7 / 4; f += blockDim.x) d4[f] = s4[f];
+    } else {
+        for (int f = t; f < rows * 7; f += blockDim.x) base[f] = src[f];
+    }
+}
+
 // reset() (:83-114) with a given serve (vx, vy, spin)
 __device__ __forceinline__ void serve(Arena& a, double vx, double vy, double spin) {
     a.sA = 0; a.sB = 0; a.bounces = 0;
@@ -169,6 +185,7 @@ __device__ __forceinline__ void serve(Arena& a, double vx, double vy, double spi
 
 // Production serve draws from Philox: speed = U(lo,hi), coin < 0.5 picks the angle interval,
 // angle = U(interval) degrees -> radians (math.radians: deg * (pi/180)), spin = U(lo,hi).
+// sincos shares one argument reduction between the two (OCML, same values as cos and sin).
 __device__ __forceinline__ void philox_serve(const pm_env_params& p, uint32_t i, uint32_t nserve, uint64_t seed,
                                              double& vx, double& vy, double& spin) {
     const U4 r0 = philox(i, TAG_SERVE, nserve, 0u, seed);
@@ -178,12 +195,25 @@ __device__ __forceinline__ void philox_serve(const pm_env_params& p, uint32_t i,
     if (u53(r0.z, r0.w) < 0.5) ang = p.ang0_lo + (p.ang0_hi - p.ang0_lo) * u53(r1.x, r1.y);
     else ang = p.ang1_lo + (p.ang1_hi - p.ang1_lo) * u53(r1.x, r1.y);
     const double rad = ang * (3.141592653589793 / 180.0);
-    vx = speed * cos(rad);
-    vy = speed * sin(rad);
+    double sn, cs;
+    sincos(rad, &sn, &cs);
+    vx = speed * cs;
+    vy = speed * sn;
     spin = p.spin_lo + (p.spin_hi - p.spin_lo) * u53(r1.z, r1.w);
 }
 
 __device__ __forceinline__ double clip01(double v) { return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v); }
+
+// a / b for a divisor b with correctly rounded reciprocal inv = RN(1/b): q = RN(a*inv) is within an
+// ulp of a/b, and one FMA residual step q + RN(a - b*q)*inv rounds correctly (Markstein's theorem,
+// for results clear of under/overflow; checked against IEEE division on 2.4e8 random operands for
+// the divisors the configs produce). Zero dividends keep their sign, as a/b does.
+__device__ __forceinline__ double div_by(double a, double b, double inv) {
+    const double q = a * inv;
+    const double r = __builtin_fma(-q, b, a);
+    const double q2 = __builtin_fma(r, inv, q);
+    return a == 0.0 ? q : q2;
+}
 
 // collide_sphere_with_moving_plane (envs/physics.py:3-23)
 __device__ __forceinline__ void collide(const pm_env_params& p, double vn, double vt, double u, double om,
@@ -200,11 +230,14 @@ __device__ __forceinline__ void collide(const pm_env_params& p, double vn, doubl
         const double vrel = (vt - u) - R * om;
         Jt = (-mf) * copysign(1.0, vrel);
     }
-    vt2 = vt + (Jt / m);
-    om2 = om - (R * Jt) / p.inertia;
+    vt2 = vt + div_by(Jt, m, p.inv_mass);
+    om2 = om - div_by(R * Jt, p.inertia, p.inv_inertia);
 }
 
-// One PongEnv2P.step. Returns done; rewards are exactly -1/0/+1.
+// One PongEnv2P.step. Returns done; rewards are exactly -1/0/+1. A paddle hit at the top (y < 0,
+// player A) and at the bottom (y > 1, player B) share one collide path: the bottom case is the top
+// case with vn = -vy and vy' = -vn' (exact negations), so a wave with hits on both sides runs the
+// impulse arithmetic once.
 __device__ __forceinline__ int tick(const pm_env_params& p, Arena& a, int aA, int aB, float& rA, float& rB) {
     if (aA == 0) a.top = a.top - p.paddle_speed;
     else if (aA == 2) a.top = a.top + p.paddle_speed;
@@ -221,31 +254,25 @@ __device__ __forceinline__ int tick(const pm_env_params& p, Arena& a, int aA, in
     if (a.x < 0.0) { a.x = -a.x; a.vx = -a.vx; }
     else if (a.x > 1.0) { a.x = 2.0 - a.x; a.vx = -a.vx; }
 
-    if (a.y < 0.0) {
-        const double lo = a.top - p.half_width, hi = a.top + p.half_width;
+    const bool low = a.y < 0.0, high = a.y > 1.0;
+    if (low || high) {
+        const double pad = low ? a.top : a.bot;
+        const double lo = pad - p.half_width, hi = pad + p.half_width;
         if (lo <= a.x && a.x <= hi) {
-            const double u = aA == 0 ? -p.paddle_speed : (aA == 2 ? p.paddle_speed : 0.0);
+            const int act = low ? aA : aB;
+            const double u = act == 0 ? -p.paddle_speed : (act == 2 ? p.paddle_speed : 0.0);
             double vn2, vt2, om2;
-            collide(p, a.vy, a.vx, u, a.spin, vn2, vt2, om2);
-            a.vy = vn2; a.vx = vt2; a.spin = om2;
-            a.y = 0.0;
+            collide(p, low ? a.vy : -a.vy, a.vx, u, a.spin, vn2, vt2, om2);
+            a.vy = low ? vn2 : -vn2; a.vx = vt2; a.spin = om2;
+            a.y = low ? 0.0 : 1.0;
             a.bounces += 1;
-            if (a.bounces % p.speed_scale_every == 0) { a.vx = a.vx * p.speed_scale; a.vy = a.vy * p.speed_scale; }
-        } else {
+            if (p.speed_scale_every == 1 || a.bounces % p.speed_scale_every == 0) {
+                a.vx = a.vx * p.speed_scale; a.vy = a.vy * p.speed_scale;
+            }
+        } else if (low) {
             rA = -1.f; rB = 1.f;
             a.sB += 1;
             done = a.sB >= p.max_score;
-        }
-    } else if (a.y > 1.0) {
-        const double lo = a.bot - p.half_width, hi = a.bot + p.half_width;
-        if (lo <= a.x && a.x <= hi) {
-            const double u = aB == 0 ? -p.paddle_speed : (aB == 2 ? p.paddle_speed : 0.0);
-            double vn2, vt2, om2;
-            collide(p, -a.vy, a.vx, u, a.spin, vn2, vt2, om2);
-            a.vy = -vn2; a.vx = vt2; a.spin = om2;
-            a.y = 1.0;
-            a.bounces += 1;
-            if (a.bounces % p.speed_scale_every == 0) { a.vx = a.vx * p.speed_scale; a.vy = a.vy * p.speed_scale; }
         } else {
             rA = 1.f; rB = -1.f;
             a.sA += 1;

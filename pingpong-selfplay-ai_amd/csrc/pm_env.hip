@@ -47,6 +47,15 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(pm_env_params p, pm_env_st
     if (obsB) store_rows7(obsB, lds, oB, i0, n);
 }
 
+// One lane per arena, one wave per SIMD at 65 536 arenas: the kernel is a single load -> tick ->
+// store pass, so its time is the serial latency of that pass. Three things keep it short:
+//   - the serve counter is loaded first and the next production serve (two Philox draws + sincos)
+//     is drawn for every lane while the state loads are still in flight; done lanes use it;
+//   - tick() runs one shared collide path with reciprocal-multiply division (pm_dev.h);
+//   - every observation row of the block is staged in LDS once, behind one barrier, and leaves as
+//     full float4 stores.
+// autoreset: 0 none, 1 reset + full term rows (term row = the step's pre-reset observation),
+// 2 reset + term rows written for done arenas only (the other rows are left as they were).
 __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
                                                      const int8_t* __restrict__ aB, float* __restrict__ obsA,
                                                      float* __restrict__ obsB, float* __restrict__ rA,
@@ -54,20 +63,42 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
                                                      float* __restrict__ tobsA, float* __restrict__ tobsB,
                                                      int autoreset, const double* __restrict__ inject, int inject_cap,
                                                      uint64_t seed, int32_t* status, int n) {
-    __shared__ float lds[kBlock][7];
+    __shared__ float lds[4][kBlock][7];
     const int i0 = blockIdx.x * kBlock;
-    const int i = i0 + threadIdx.x;
+    const int t = threadIdx.x;
+    const int i = i0 + t;
+    const bool full_term = tobsA && autoreset != 2;  // tobsA and tobsB are both set or both null
     float oA[7] = {0}, oB[7] = {0};
-    float tA[7] = {0}, tB[7] = {0};
     if (i < n) {
+        int32_t ns = 0;
+        double vx = 0.0, vy = 0.0, spn = 0.0;
+        if (autoreset) {
+            ns = __builtin_nontemporal_load(&s.serves[i]);
+            __builtin_amdgcn_sched_barrier(0);  // issue it ahead of the state loads
+        }
         Arena a = load_arena(s, i);
+        const int xa = aA[i], xb = aB[i];
+        if (autoreset && !inject) philox_serve(p, (uint32_t)i, (uint32_t)ns, seed, vx, vy, spn);
         float ra, rb;
-        const int d = tick(p, a, aA[i], aB[i], ra, rb);
+        const int d = tick(p, a, xa, xb, ra, rb);
         observe(a, oA, oB);
+        if (full_term) {
 #pragma unroll
-        for (int k = 0; k < 7; ++k) { tA[k] = oA[k]; tB[k] = oB[k]; }
+            for (int k = 0; k < 7; ++k) { lds[2][t][k] = oA[k]; lds[3][t][k] = oB[k]; }
+        }
         if (autoreset && d) {
-            do_serve(p, s, a, i, inject, inject_cap, seed, status);
+            if (autoreset == 2 && tobsA) {
+                float* ta = tobsA + (size_t)i * 7;
+                float* tb = tobsB + (size_t)i * 7;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) { ta[k] = oA[k]; tb[k] = oB[k]; }
+            }
+            if (inject) {
+                const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
+                vx = r[0]; vy = r[1]; spn = r[2];
+            }
+            serve(a, vx, vy, spn);
+            s.serves[i] = ns + 1;
             observe(a, oA, oB);
         }
         store_arena(s, i, a);
@@ -75,10 +106,15 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
         rB[i] = rb;
         done[i] = (uint8_t)d;
     }
-    store_rows7(obsA, lds, oA, i0, n);
-    store_rows7(obsB, lds, oB, i0, n);
-    if (tobsA) store_rows7(tobsA, lds, tA, i0, n);
-    if (tobsB) store_rows7(tobsB, lds, tB, i0, n);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { lds[0][t][k] = oA[k]; lds[1][t][k] = oB[k]; }
+    __syncthreads();
+    copy_rows7(obsA, lds[0], i0, n);
+    copy_rows7(obsB, lds[1], i0, n);
+    if (full_term) {
+        copy_rows7(tobsA, lds[2], i0, n);
+        copy_rows7(tobsB, lds[3], i0, n);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_collide(const double* __restrict__ in, const double* __restrict__ inertia,
@@ -90,6 +126,8 @@ __global__ __launch_bounds__(kBlock) void k_collide(const double* __restrict__ i
     p.restitution = r[4]; p.friction = r[5]; p.ball_mass = r[6]; p.radius = r[7];
     p.inertia = inertia[i];
     p.jt_coef = (2.0 * r[6]) / 7.0;
+    p.inv_mass = 1.0 / r[6];
+    p.inv_inertia = 1.0 / p.inertia;
     double vn2, vt2, om2;
     collide(p, r[0], r[1], r[2], r[3], vn2, vt2, om2);
     out[(size_t)i * 3 + 0] = vn2;
@@ -127,6 +165,8 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
     if (n == 0) return PM_OK;
     PM_REQUIRE(p && state_ok(s), PM_E_ARG, "pm_env_step: null params/state");
     PM_REQUIRE(aA && aB && obsA && obsB && rA && rB && done, PM_E_ARG, "pm_env_step: null buffer");
+    PM_REQUIRE(!term_obsA == !term_obsB, PM_E_ARG, "pm_env_step: term_obsA and term_obsB must both be set or both NULL");
+    PM_REQUIRE(autoreset >= 0 && autoreset <= 2, PM_E_ARG, "pm_env_step: autoreset=%d not in {0,1,2}", autoreset);
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
     if (n == 0) return PM_OK;

@@ -132,20 +132,22 @@ __device__ __forceinline__ void write_opp_lists(int nn, int32_t* opp_list, int32
         if (lane == 0) sm.woff[wv][k] = __popcll(b);
     }
     __syncthreads();
-    if ((int)threadIdx.x < nn) {
-        const int k = threadIdx.x;
+    if (wv == 0) {  // lane k < nn: per-wave offsets within net k, then an exclusive scan over nets
         int acc = 0;
-        for (int w = 0; w < kListBlock / 64; ++w) {
-            const int c = sm.woff[w][k];
-            sm.woff[w][k] = acc;
-            acc += c;
+        if (lane < nn) {
+            for (int w = 0; w < kListBlock / 64; ++w) {
+                const int c = sm.woff[w][lane];
+                sm.woff[w][lane] = acc;
+                acc += c;
+            }
         }
-        sm.ncnt[k] = acc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int k = 0; k < nn; ++k) { sm.noff[k] = acc; acc += sm.ncnt[k]; }
+        int inc = acc;  // inclusive scan of the net counts across the wave (nn <= 64)
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(inc, d);
+            if (lane >= d) inc += v;
+        }
+        if (lane < nn) { sm.ncnt[lane] = acc; sm.noff[lane] = inc - acc; }
     }
     __syncthreads();
     if (valid) opp_list[(size_t)blk * kListBlock + sm.noff[net] + sm.woff[wv][net] + rank] = i;

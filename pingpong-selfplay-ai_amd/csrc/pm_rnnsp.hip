@@ -55,7 +55,7 @@ __global__ __launch_bounds__(kBlock) void k_rsp_init(const pm_rnn_selfplay sp) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
-    __shared__ float lds[kBlock][7];
+    __shared__ float lds[2][kBlock][7];
     __shared__ long long red[kBlock / 64][6];
     __shared__ int red_st[kBlock / 64];
     const int i0 = blockIdx.x * kBlock;
@@ -63,8 +63,14 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
     const bool valid = i < sp.n;
     const int ii = valid ? i : sp.n - 1;
     const uint64_t step = sp.ctrl->step;
+    // serve counter first; the next opponent and serve are drawn while the state loads land
+    const uint32_t ns = (uint32_t)__builtin_nontemporal_load(&sp.st.serves[ii]);
+    __builtin_amdgcn_sched_barrier(0);
     Arena a = load_arena(sp.st, ii);
     const int aA = sp.aA[ii], aB = sp.aB[ii], o = sp.opp[ii];
+    const int onext = draw_opponent(sp, ii, ns);
+    double svx, svy, sspn;
+    philox_serve(sp.env, (uint32_t)ii, ns, sp.seed_env, svx, svy, sspn);
     float oA[7], oB[7];
     observe(a, oA, oB);  // the observation the actions were chosen on
     float rA, rB;
@@ -96,12 +102,9 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
         row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
         row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
         if (d) {  // episode over: stored when len >= trace_length (:112-115); next opponent, env.reset()
-            const uint32_t ns = (uint32_t)sp.st.serves[i];
-            onew = draw_opponent(sp, i, ns);
+            onew = onext;
             sp.opp[i] = onew;
-            double vx, vy, spn;
-            philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
-            serve(a, vx, vy, spn);
+            serve(a, svx, svy, sspn);
             sp.st.serves[i] = (int32_t)ns + 1;
             observe(a, nA, nB);
         }
@@ -110,6 +113,8 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
         sp.ep_len[i] = d ? 0 : len;
         sp.reset[i] = (uint8_t)d;
     }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { lds[0][threadIdx.x][k] = nA[k]; lds[1][threadIdx.x][k] = nB[k]; }
     {   // episodes to store, ranked in arena order within the block -> the block's staging slots
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         const bool st = valid && d && len >= sp.T;
@@ -133,8 +138,8 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
         __shared__ OppListSmem ol;
         write_opp_lists(sp.n_pool + 1, sp.opp_list, sp.opp_cnt, ol, blockIdx.x, i, valid, onew);
     }
-    store_rows7(sp.obsA, lds, nA, i0, sp.n);
-    store_rows7(sp.obsB, lds, nB, i0, sp.n);
+    copy_rows7(sp.obsA, lds[0], i0, sp.n);  // staged before the ranking barrier
+    copy_rows7(sp.obsB, lds[1], i0, sp.n);
 }
 
 constexpr int kAppend = 1024;  // one thread per env block: n <= kAppend * kBlock

@@ -19,6 +19,30 @@
 
 using namespace pm;
 
+#ifdef PM_DIAG
+// k_env phase timeline (diagnostic build only): wave 0 of each env block. A stamp records when the
+// wave's instruction stream reaches it (no drain: stores still in flight are not waited for);
+// PM_ENV_STAMP_DRAIN first waits for every outstanding memory operation of the wave.
+static __device__ unsigned long long pm_diag_env[8][1024];
+#define PM_ENV_STAMP(k, blk)                                                                   \
+    do {                                                                                       \
+        asm volatile("" ::: "memory");                                                         \
+        if (threadIdx.x == 0 && (blk) < 1024) pm_diag_env[(k)][(blk)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define PM_ENV_STAMP_DRAIN(k, blk)                                                             \
+    do {                                                                                       \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                            \
+        if (threadIdx.x == 0 && (blk) < 1024) pm_diag_env[(k)][(blk)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PM_ENV_STAMP(k, blk) \
+    do {                     \
+    } while (0)
+#define PM_ENV_STAMP_DRAIN(k, blk) \
+    do {                           \
+    } while (0)
+#endif
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -147,40 +171,75 @@ __device__ __forceinline__ void write_opp_lists(const pm_selfplay& sp, OppListSm
 // env.step (:242) + memory.push (:243) + episode bookkeeping (:245-249) + next opponent (:235-236)
 // and env.reset (:238) for finished arenas; writes next step's observations. HBM-bound.
 __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
+    // env blocks first, then the learner-forward blocks (measured: dispatching the forward blocks
+    // first lengthens the kernel by ~1 us; last, they finish inside the env blocks' time)
+    const int blk = (int)blockIdx.x;
     const int nenv = (sp.n + kBlock - 1) / kBlock;
-    if ((int)blockIdx.x >= nenv) {
-        env_fwd_block(sp, (int)blockIdx.x - nenv);
+    if (blk >= nenv) {
+        env_fwd_block(sp, blk - nenv);
         return;
     }
-    __shared__ float lds[kBlock][7];
+    __shared__ float lds[2][kBlock][7];
     __shared__ long long red[kBlock / 64][6];
-    const int i0 = blockIdx.x * kBlock;
+    const int i0 = blk * kBlock;
     const int i = i0 + threadIdx.x;
     const bool valid = i < sp.n;
     const int ii = valid ? i : sp.n - 1;
     const pm_ctrl* c = sp.ctrl;
-    PM_STAMP(72);
+    if (blk == 0) PM_STAMP_ANY(72);
+    PM_ENV_STAMP(0, blk);
+    // Every per-arena load is issued here, in one basic block, before any branch (loads placed after
+    // a branch were issued only after it, one more HBM round trip). The serve counter goes first:
+    // the next episode's opponent and serve are drawn for every lane while the state loads are in
+    // flight (lanes that finish use them; see k_env_step).
+    // The control block is read before them (vmcnt retires in issue order: what only needs ns and
+    // the control words can then run while the state is still in flight).
+    const uint32_t ns = (uint32_t)__builtin_nontemporal_load(&sp.st.serves[ii]);
     const int64_t pos = c->pos, size = c->size;
-    const float maxp = push_prio(size, c->max_prio);  // max(prios) if buffer else 1.0 (:57)
-    float* leaf = per_tree(sp.per_work, sp.cap).leaf;
-    const float pval = prio_pow(maxp, (float)sp.alpha);  // its PER leaf
-
+    const float cmaxp = c->max_prio;
+    const uint64_t cstep = c->step;
+    const double ceps = c->epsilon;
+    const int o = sp.opp[ii];
+    const float er0 = sp.ep_reward[ii];
     Arena a = load_arena(sp.st, ii);
     const int aA = sp.aA[ii];
     int aB = sp.aB[ii];
-    {   // select_action_B (:126-130): random.random() < eps ? randint(0, 2) : argmax. The act kernel
-        // wrote the argmax; the draw is per-arena VALU work, cheaper here than beside the MFMAs.
-        const U4 rr = philox64((uint32_t)ii, TAG_ACT, c->step, sp.seed_env);
-        if (u53(rr.x, rr.y) < c->epsilon) aB = (int)below(rr.z, 3u);
+    __builtin_amdgcn_sched_barrier(0);
+    const float maxp = push_prio(size, cmaxp);  // max(prios) if buffer else 1.0 (:57)
+    float* leaf = per_tree(sp.per_work, sp.cap).leaf;
+    const float pval = prio_pow(maxp, (float)sp.alpha);  // its PER leaf
+
+    // Draws that need only the serve counter and the control block, pinned ahead of everything that
+    // waits for the state loads:
+    //   select_action_B (:126-130): random.random() < eps ? randint(0, 2) : argmax (the act kernel
+    //   wrote the argmax; the draw is per-arena VALU work, cheaper here than beside the MFMAs);
+    //   the next episode's opponent (:235-236) and serve (env.reset(), :238), used if this one ends.
+    int onext, eps_a;
+    bool eps_hit;
+    double svx, svy, sspn;
+    {
+        const U4 rr = philox64((uint32_t)ii, TAG_ACT, cstep, sp.seed_env);
+        eps_hit = u53(rr.x, rr.y) < ceps;
+        eps_a = (int)below(rr.z, 3u);
+        const U4 q = philox((uint32_t)ii, TAG_OPP, ns, 0u, sp.seed_env);
+        onext = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
+        philox_serve(sp.env, (uint32_t)ii, ns, sp.seed_env, svx, svy, sspn);
+        asm volatile("" ::"v"(onext), "v"(svx), "v"(svy), "v"(sspn), "v"(eps_hit), "v"(eps_a));
+        __builtin_amdgcn_sched_barrier(0);
     }
-    const int o = sp.opp[ii];
+    PM_ENV_STAMP(1, blk);
+    if (eps_hit) aB = eps_a;
     float oA[7], oB[7];
     observe(a, oA, oB);  // the state the actions were chosen on (= obs of the previous env kernel)
     float rA, rB;
     const int d = tick(sp.env, a, aA, aB, rA, rB);
     float nA[7], nB[7];
     observe(a, nA, nB);
-    const float er = sp.ep_reward[ii] + rB;  // ep_reward += rB (:245)
+#ifdef PM_DIAG
+    asm volatile("" ::"v"(nA[0]), "v"(nB[1]), "v"(d));
+#endif
+    PM_ENV_STAMP(2, blk);
+    const float er = er0 + rB;  // ep_reward += rB (:245)
     const bool fin = valid && d;
     {   // per-block partials, no atomics (:247-249)
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -207,13 +266,9 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
         sp.prios[slot] = maxp;
         leaf[slot] = pval;
         float ernew = er;
-        if (d) {  // next episode: opponent draw then env.reset()
-            const uint32_t ns = (uint32_t)sp.st.serves[i];
-            const U4 q = philox((uint32_t)i, TAG_OPP, ns, 0u, sp.seed_env);
-            onew = (sp.n_pool > 0 && u53(q.x, q.y) < sp.pool_ratio) ? 1 + below(q.z, (uint32_t)sp.n_pool) : 0;
-            double vx, vy, spn;
-            philox_serve(sp.env, (uint32_t)i, ns, sp.seed_env, vx, vy, spn);
-            serve(a, vx, vy, spn);
+        if (d) {  // next episode: the opponent and serve drawn above
+            onew = onext;
+            serve(a, svx, svy, sspn);
             sp.st.serves[i] = (int32_t)ns + 1;
             ernew = 0.f;
             observe(a, nA, nB);
@@ -223,18 +278,24 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
         sp.aB[i] = (int8_t)aB;  // the action taken
         sp.ep_reward[i] = ernew;
     }
+    PM_ENV_STAMP(3, blk);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { lds[0][threadIdx.x][k] = nA[k]; lds[1][threadIdx.x][k] = nB[k]; }
     __syncthreads();
+    PM_ENV_STAMP(4, blk);
     if (threadIdx.x < 6) {
         long long t = 0;
         for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
-        sp.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = t;
+        sp.partials[(size_t)blk * 8 + threadIdx.x] = t;
     }
     {
         __shared__ OppListSmem ol;
-        write_opp_lists(sp, ol, blockIdx.x, i, valid, onew);
+        write_opp_lists(sp, ol, blk, i, valid, onew);
     }
-    store_rows7(sp.obsA, lds, nA, i0, sp.n);
-    store_rows7(sp.obsB, lds, nB, i0, sp.n);
+    PM_ENV_STAMP(5, blk);
+    copy_rows7(sp.obsA, lds[0], i0, sp.n);
+    copy_rows7(sp.obsB, lds[1], i0, sp.n);
+    PM_ENV_STAMP_DRAIN(6, blk);
 }
 
 // ------------------------------------------------------------------------------------ init
@@ -834,6 +895,9 @@ extern "C" int pm_diag_read(uint64_t* out, int32_t n) {
 }
 extern "C" int pm_diag_read_blk(uint64_t* out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_blk), sizeof(uint64_t) * 8 * 4096);
+}
+extern "C" int pm_diag_read_env(uint64_t* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_env), sizeof(uint64_t) * 8 * 1024);
 }
 extern "C" int pm_diag_clear(void) {
     static const unsigned long long z[256] = {0};

@@ -31,14 +31,14 @@ PM_RNN_NW = 157456
 PM_TRANS_F = 16
 PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class EnvParams(ctypes.Structure):
     _fields_ = [(n, c_double) for n in (
         "paddle_width", "paddle_speed", "magnus_factor", "restitution", "friction", "ball_mass", "radius",
         "speed_lo", "speed_hi", "spin_lo", "spin_hi", "ang0_lo", "ang0_hi", "ang1_lo", "ang1_hi",
-        "half_width", "speed_scale", "inertia", "jt_coef")] + \
+        "half_width", "speed_scale", "inertia", "jt_coef", "inv_mass", "inv_inertia")] + \
         [("max_score", c_i32), ("speed_scale_every", c_i32), ("enable_spin", c_i32), ("_pad", c_i32)]
 
 

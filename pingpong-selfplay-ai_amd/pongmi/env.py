@@ -62,6 +62,8 @@ def env_params(**kw):
     p.speed_scale = 1.0 + c["speed_increment"]           # :230
     p.inertia = (2 / 5) * m * R ** 2                     # envs/physics.py:9
     p.jt_coef = 2 * m / 7.0                              # envs/physics.py:10
+    p.inv_mass = 1.0 / m if m else float("inf")          # divisors of physics.py:20-21 (see pongmi.h)
+    p.inv_inertia = 1.0 / p.inertia if p.inertia else float("inf")
     p.max_score = int(c["max_score"])
     p.speed_scale_every = int(c["speed_scale_every"])
     p.enable_spin = int(bool(c["enable_spin"]))
@@ -98,7 +100,9 @@ class PongEnv2PBatch:
     step(aA, aB) -> ((obsA, obsB), (rA, rB), done, info), all device tensors: obs [n, 7] f32,
     rewards [n] f32, done [n] u8. With autoreset=True finished arenas are served again inside the
     same kernel; obs then holds the post-reset observation and info['term_obsA'/'term_obsB'] the
-    terminal one (what the reference pushes to replay as next state)."""
+    observation the step returned before the reset (what the reference pushes to replay as next
+    state). autoreset="done" writes the term rows of finished arenas only (the others keep old
+    contents: next state = where(done, term_obs, obs)), which saves 56 B of stores per env-step."""
 
     def __init__(self, n, device="cuda", seed=0, serve_table=None, autoreset=False, **env_kw):
         self.lib = _lib.load()
@@ -109,7 +113,9 @@ class PongEnv2PBatch:
         self.cfg = env_config(**env_kw)
         self.params = env_params(**env_kw)
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
-        self.autoreset = bool(autoreset)
+        if autoreset not in (False, True, 0, 1, "done"):
+            raise ValueError(f"autoreset must be False, True or 'done', got {autoreset!r}")
+        self.autoreset = 2 if autoreset == "done" else int(bool(autoreset))
         n, dev = self.n, self.device
         self.f64 = torch.zeros((7, n), dtype=torch.float64, device=dev)
         self.i32 = torch.zeros((4, n), dtype=torch.int32, device=dev)
@@ -149,7 +155,7 @@ class PongEnv2PBatch:
         aB = _as_actions(aB, self.n, self.device)
         check(self.lib.pm_env_step(ctypes_ref(self.params), ctypes_ref(self.state), ptr(aA), ptr(aB), ptr(self.obsA),
                                    ptr(self.obsB), ptr(self.rA), ptr(self.rB), ptr(self.done), ptr(self.term_obsA),
-                                   ptr(self.term_obsB), int(self.autoreset), ptr(self.inject), self.inject_cap,
+                                   ptr(self.term_obsB), self.autoreset, ptr(self.inject), self.inject_cap,
                                    self.seed, None, self.n, stream_ptr()), "pm_env_step")
         info = {}
         if self.autoreset:

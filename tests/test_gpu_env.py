@@ -54,14 +54,23 @@ def test_env_matches_reference_trajectories_bit_exact(golden, name):
         assert np.array_equal(oA.cpu().numpy(), exp_oA) and np.array_equal(oB.cpu().numpy(), exp_oB)
 
 
-@pytest.mark.parametrize("n", [1, 255, 65536])
-def test_env_step_matches_oracle_at_scale(orc, n):
+AT_SCALE_KW = {
+    "cfg": dict(paddle_speed=0.03, max_score=3, magnus_factor=0.025, restitution=1, friction=0.6,
+                ball_speed_range=[0.03, 0.05], spin_range=[-5, 5], speed_scale_every=1, speed_increment=0.1),
+    # mass != 1 and an odd radius: the device divides by mass and inertia through their reciprocals
+    "mass": dict(paddle_speed=0.041, max_score=5, magnus_factor=0.031, restitution=0.83, friction=0.35,
+                 ball_mass=1.7, world_ball_radius=0.0123, ball_speed_range=[0.03, 0.05], spin_range=[-5, 5],
+                 speed_scale_every=3, speed_increment=0.07),
+}
+
+
+@pytest.mark.parametrize("n,cfg", [(1, "cfg"), (255, "cfg"), (65536, "cfg"), (65536, "mass")])
+def test_env_step_matches_oracle_at_scale(orc, n, cfg):
     """n arenas from random mid-game states (including y beyond the lines, paddles at the walls),
     random actions, 40 ticks without reset: bit-exact with the C oracle."""
     from pongmi.env import PongEnv2PBatch
 
-    kw = dict(paddle_speed=0.03, max_score=3, magnus_factor=0.025, restitution=1, friction=0.6,
-              ball_speed_range=[0.03, 0.05], spin_range=[-5, 5], speed_scale_every=1, speed_increment=0.1)
+    kw = AT_SCALE_KW[cfg]
     P = orc.make_params(orc.env_params_from_kwargs(**kw))
     rng = np.random.RandomState(n)
     st = dict(x=rng.uniform(-0.02, 1.02, n), y=rng.uniform(-0.05, 1.05, n), vx=rng.uniform(-0.08, 0.08, n),
@@ -84,6 +93,39 @@ def test_env_step_matches_oracle_at_scale(orc, n):
         assert np.array_equal(got[k], arr[k]), k
 
 
+def test_autoreset_done_rows_only():
+    """autoreset='done' (ABI mode 2) against autoreset=True on the same Philox serves: identical
+    state, obs, rewards and done every step; term rows written exactly for done arenas, with the
+    full-mode values; every other row keeps its previous contents."""
+    from pongmi.env import PongEnv2PBatch
+
+    n = 65536
+    full = PongEnv2PBatch(n, seed=5, autoreset=True)
+    part = PongEnv2PBatch(n, seed=5, autoreset="done")
+    full.reset()
+    part.reset()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    fill = torch.full((n, 7), -7.0, device="cuda")
+    part.term_obsA.copy_(fill)
+    part.term_obsB.copy_(fill)
+    seen = 0
+    for t in range(120):
+        aA = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=g)
+        aB = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=g)
+        prevA, prevB = part.term_obsA.clone(), part.term_obsB.clone()
+        (fA, fB), (frA, frB), fd, finfo = full.step(aA, aB)
+        (pA, pB), (prA, prB), pd, pinfo = part.step(aA, aB)
+        assert torch.equal(fA, pA) and torch.equal(fB, pB) and torch.equal(fd, pd)
+        assert torch.equal(frA, prA) and torch.equal(frB, prB)
+        d = pd.bool()
+        seen += int(d.sum())
+        for side, prev in (("term_obsA", prevA), ("term_obsB", prevB)):
+            exp = torch.where(d[:, None], finfo[side], prev)
+            assert torch.equal(pinfo[side], exp), (t, side)
+    assert np.array_equal(_state_matrix(full), _state_matrix(part))
+    assert seen > 1000
+
+
 def test_env_empty_and_bad_arguments():
     from pongmi import _lib
     from pongmi.env import PongEnv2PBatch, env_params
@@ -97,6 +139,8 @@ def test_env_empty_and_bad_arguments():
         env_params(bogus=1)
     with pytest.raises(ValueError):
         PongEnv2PBatch(4).step(np.zeros(3), np.zeros(4))
+    with pytest.raises(ValueError):
+        PongEnv2PBatch(4, autoreset="sometimes")
     with pytest.raises(_lib.PongmiError):
         _lib.check(_lib.load().pm_env_step(None, None, None, None, None, None, None, None, None, None, None, 0, None,
                                            0, 0, None, 4, None))

@@ -1,0 +1,63 @@
+"""Phase timeline of k_env (env tick + replay push + bookkeeping) per env block, from the
+diagnostic library's PM_ENV_STAMP stamps (s_memrealtime, 10 ns; each stamp first drains the wave's
+memory operations only at the end: a phase is the time the wave's instruction stream takes to get
+through it, waits the compiler placed in it included).
+
+    make -C pingpong-selfplay-ai_amd/csrc diag && python tools/env_blocks.py
+
+Diagnostic only (libpongmi_diag.so, never the product library).
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["PONGMI_LIB"] = os.path.join(ROOT, "pingpong-selfplay-ai_amd", "pongmi", "libpongmi_diag.so")
+sys.path.insert(0, os.path.join(ROOT, "pingpong-selfplay-ai_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PHASES = ["begin", "loads issued + speculative draws", "state wait + tick + obs", "bookkeeping + replay/state stores",
+          "LDS staging + barrier", "partials + opponent lists", "obs stores + drain of all stores (end)"]
+
+
+def main():
+    import bench
+    from pongmi import _lib
+    from pongmi.selfplay import SelfPlayLearner
+    lib = _lib.load()
+    lib.pm_diag_read_env.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    n = 65536
+    sdB, sdA = bench.synthetic_qnet(1), bench.synthetic_qnet(2)
+    pool = [bench.synthetic_qnet(100 + k) for k in range(8)]
+    L = SelfPlayLearner(bench.ENV_KW, n, sdB, sdA, pool, batch=256, memory_size=1_000_000, epsilon=0.08, seed=7)
+    for _ in range(40):
+        L.step()
+    torch.cuda.synchronize()
+    nb = (n + 255) // 256
+    buf = (ctypes.c_uint64 * (8 * 1024))()
+    acc = []
+    for _ in range(20):
+        L.step()
+        torch.cuda.synchronize()
+        lib.pm_diag_read_env(buf)
+        a = np.array(buf[:], dtype=np.int64).reshape(8, 1024)[:7, :nb]
+        acc.append(a)
+    spans, deltas = [], [[] for _ in PHASES]
+    for a in acc:
+        t0 = a[0].min()
+        spans.append((a[6].max() - t0) * 0.01)
+        deltas[0].extend((a[0] - t0) * 0.01)
+        for k in range(1, 7):
+            deltas[k].extend((a[k] - a[k - 1]) * 0.01)
+    print(f"k_env env blocks: {nb}; span first begin -> last end: median {np.median(spans):.2f} us")
+    for k, name in enumerate(PHASES):
+        v = np.array(deltas[k])
+        label = "begin offset" if k == 0 else name
+        print(f"  {label:44s} p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -138,42 +138,47 @@ __device__ __forceinline__ void observe(const Arena& a, float* oA, float* oB) {
     oB[4] = (float)a.bot; oB[5] = (float)a.top; oB[6] = (float)a.spin;
 }
 
-// Stage [blockDim][7] floats per block in LDS and write them back as contiguous float4s (a row-per-lane
-// store of 28-byte rows would be seven 4-byte stores per lane). Block-wide, includes two barriers.
+// Row staging for [n][7] f32 outputs. Every kernel that stages rows runs kRowBlock-thread blocks and
+// declares its staging array 16-byte aligned, so a block's rows leave LDS as ds_read_b128 and reach
+// HBM as full global_store_dwordx4 (BLOCK * 7 / 4 float4s, two per thread), with no runtime trip
+// count (a row-per-lane store of 28-byte rows would be seven 4-byte stores per lane).
+constexpr int kRowBlock = 256;
+
+// The copy-out of rows the caller already staged in LDS (and fenced with a barrier): several outputs
+// can share one barrier. No barrier inside.
+__device__ __forceinline__ void copy_rows7(float* __restrict__ dst, const float (*lds)[7], int i0, int n) {
+    const int t = threadIdx.x;
+    const int rows = min(kRowBlock, n - i0);
+    float* base = dst + (size_t)i0 * 7;
+    const float* src = &lds[0][0];
+    if (rows == kRowBlock && (((uintptr_t)base) & 15) == 0) {
+        float4* d4 = reinterpret_cast<float4*>(base);
+        const float4* s4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(src, 16));
+#pragma unroll
+        for (int f = t; f < kRowBlock * 7 / 4; f += kRowBlock) d4[f] = s4[f];
+    } else {
+        for (int f = t; f < rows * 7; f += kRowBlock) base[f] = src[f];
+    }
+}
+
+// Stage one row per thread in LDS and copy the block's rows out. Block-wide, two barriers.
 __device__ __forceinline__ void store_rows7(float* __restrict__ dst, float (*lds)[7], const float* row, int i0,
                                             int n) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int k = 0; k < 7; ++k) lds[t][k] = row[k];
     __syncthreads();
-    const int rows = min((int)blockDim.x, n - i0);
-    const int nf = rows * 7;
-    float* base = dst + (size_t)i0 * 7;
-    const float* src = &lds[0][0];
-    if (rows == (int)blockDim.x && (((uintptr_t)base) & 15) == 0) {
-        float4* d4 = reinterpret_cast<float4*>(base);
-        const float4* s4 = reinterpret_cast<const float4*>(src);
-        for (int f = t; f < nf / 4; f += blockDim.x) d4[f] = s4[f];
-    } else {
-        for (int f = t; f < nf; f += blockDim.x) base[f] = src[f];
-    }
+    copy_rows7(dst, lds, i0, n);
     __syncthreads();
 }
 
-// The copy-out half of store_rows7 for rows the caller already staged in LDS (and fenced with a
-// barrier): several outputs can share one barrier. No barrier inside.
-__device__ __forceinline__ void copy_rows7(float* __restrict__ dst, const float (*lds)[7], int i0, int n) {
-    const int t = threadIdx.x;
-    const int rows = min((int)blockDim.x, n - i0);
-    float* base = dst + (size_t)i0 * 7;
-    const float* src = &lds[0][0];
-    if (rows == (int)blockDim.x && (((uintptr_t)base) & 15) == 0) {
-        float4* d4 = reinterpret_cast<float4*>(base);
-        const float4* s4 = reinterpret_cast<const float4*>(src);
-        for (int f = t; f < rows * 7 / 4; f += blockDim.x) d4[f] = s4[f];
-    } else {
-        for (int f = t; f < rows * 7; f += blockDim.x) base[f] = src[f];
-    }
+// One 28-byte row written by its own lane as dwordx4 + dwordx3 (4-byte aligned: gfx950 global
+// stores take unaligned addresses), for scattered rows that are not worth an LDS round trip.
+typedef float pm_f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float pm_f3u __attribute__((ext_vector_type(3), aligned(4)));
+__device__ __forceinline__ void store_row7(float* __restrict__ dst, const float* v) {
+    *reinterpret_cast<pm_f4u*>(dst) = pm_f4u{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<pm_f3u*>(dst + 4) = pm_f3u{v[4], v[5], v[6]};
 }
 
 // reset() (:83-114) with a given serve (vx, vy, spin)
@@ -223,63 +228,62 @@ __device__ __forceinline__ void collide(const pm_env_params& p, double vn, doubl
     const double Jn = (m * (1.0 + e)) * fabs(vn);
     const double Jt_star = p.jt_coef * ((u + R * om) - vt);
     const double mf = p.friction * Jn;
-    double Jt;
-    if (fabs(Jt_star) <= mf) {
-        Jt = Jt_star;
-    } else {
-        const double vrel = (vt - u) - R * om;
-        Jt = (-mf) * copysign(1.0, vrel);
-    }
+    const double vrel = (vt - u) - R * om;  // used only when sliding (|Jt*| > mu Jn)
+    const double Jt = fabs(Jt_star) <= mf ? Jt_star : (-mf) * copysign(1.0, vrel);
     vt2 = vt + div_by(Jt, m, p.inv_mass);
     om2 = om - div_by(R * Jt, p.inertia, p.inv_inertia);
 }
 
-// One PongEnv2P.step. Returns done; rewards are exactly -1/0/+1. A paddle hit at the top (y < 0,
-// player A) and at the bottom (y > 1, player B) share one collide path: the bottom case is the top
-// case with vn = -vy and vy' = -vn' (exact negations), so a wave with hits on both sides runs the
-// impulse arithmetic once.
+// One PongEnv2P.step. Returns done; rewards are exactly -1/0/+1.
+// Straight-line code: every branch of the reference is evaluated and the taken side selected
+// (v_cndmask), so the whole tick is one basic block the scheduler can interleave with other
+// independent work (the next serve's draw) and no lane waits on another lane's side of a branch.
+// Every selected value is computed by the reference's own expression in its order, so selection
+// changes no bit. A paddle hit at the top (y < 0, player A) and at the bottom (y > 1, player B)
+// share one collide evaluation: the bottom case is the top case with vn = -vy and vy' = -vn' (exact
+// negations). `bounces % every == 0` is true for every == 1, as the reference's `every == 1 or`.
 __device__ __forceinline__ int tick(const pm_env_params& p, Arena& a, int aA, int aB, float& rA, float& rB) {
-    if (aA == 0) a.top = a.top - p.paddle_speed;
-    else if (aA == 2) a.top = a.top + p.paddle_speed;
-    a.top = clip01(a.top);
-    if (aB == 0) a.bot = a.bot - p.paddle_speed;
-    else if (aB == 2) a.bot = a.bot + p.paddle_speed;
-    a.bot = clip01(a.bot);
+    // paddle: top - ps == top + (-ps) exactly, and top + 0.0 == top for the paddle's range (never
+    // -0.0: it starts at 0.5 and x - x rounds to +0.0), so one add of a selected step is the
+    // reference's if/elif
+    const double ps = p.paddle_speed;
+    a.top = clip01(a.top + (aA == 0 ? -ps : (aA == 2 ? ps : 0.0)));
+    a.bot = clip01(a.bot + (aB == 0 ? -ps : (aB == 2 ? ps : 0.0)));
 
-    int done = 0;
-    rA = 0.f; rB = 0.f;
-    if (p.enable_spin) a.vx = a.vx + (p.magnus_factor * a.spin) * a.vy;
-    a.x = a.x + a.vx;
-    a.y = a.y + a.vy;
-    if (a.x < 0.0) { a.x = -a.x; a.vx = -a.vx; }
-    else if (a.x > 1.0) { a.x = 2.0 - a.x; a.vx = -a.vx; }
+    double vx = p.enable_spin ? a.vx + (p.magnus_factor * a.spin) * a.vy : a.vx;
+    double x = a.x + vx;
+    const double y = a.y + a.vy;
+    const bool wl = x < 0.0, wr = x > 1.0;
+    x = wl ? -x : (wr ? 2.0 - x : x);
+    vx = (wl || wr) ? -vx : vx;
 
-    const bool low = a.y < 0.0, high = a.y > 1.0;
-    if (low || high) {
-        const double pad = low ? a.top : a.bot;
-        const double lo = pad - p.half_width, hi = pad + p.half_width;
-        if (lo <= a.x && a.x <= hi) {
-            const int act = low ? aA : aB;
-            const double u = act == 0 ? -p.paddle_speed : (act == 2 ? p.paddle_speed : 0.0);
-            double vn2, vt2, om2;
-            collide(p, low ? a.vy : -a.vy, a.vx, u, a.spin, vn2, vt2, om2);
-            a.vy = low ? vn2 : -vn2; a.vx = vt2; a.spin = om2;
-            a.y = low ? 0.0 : 1.0;
-            a.bounces += 1;
-            if (p.speed_scale_every == 1 || a.bounces % p.speed_scale_every == 0) {
-                a.vx = a.vx * p.speed_scale; a.vy = a.vy * p.speed_scale;
-            }
-        } else if (low) {
-            rA = -1.f; rB = 1.f;
-            a.sB += 1;
-            done = a.sB >= p.max_score;
-        } else {
-            rA = 1.f; rB = -1.f;
-            a.sA += 1;
-            done = a.sA >= p.max_score;
-        }
-    }
-    return done;
+    const bool low = y < 0.0, high = y > 1.0;
+    const double pad = low ? a.top : a.bot;
+    const bool inside = (pad - p.half_width) <= x && x <= (pad + p.half_width);
+    const bool hit = (low || high) && inside;
+    const int act = low ? aA : aB;
+    const double u = act == 0 ? -ps : (act == 2 ? ps : 0.0);
+    double vn2, vt2, om2;
+    collide(p, low ? a.vy : -a.vy, vx, u, a.spin, vn2, vt2, om2);
+    // materialise the impulse for every lane here: otherwise the compiler sinks it into a branch
+    // on `hit`, which splits the tick into separately scheduled blocks
+    asm volatile("" : "+v"(vn2), "+v"(vt2), "+v"(om2));
+    const int nb = a.bounces + 1;
+    const bool scale = nb % p.speed_scale_every == 0;
+    const double hvy = low ? vn2 : -vn2;
+    a.x = x;
+    a.vx = hit ? (scale ? vt2 * p.speed_scale : vt2) : vx;
+    a.vy = hit ? (scale ? hvy * p.speed_scale : hvy) : a.vy;
+    a.spin = hit ? om2 : a.spin;
+    a.y = hit ? (low ? 0.0 : 1.0) : y;
+    a.bounces = hit ? nb : a.bounces;
+
+    const bool missA = low && !inside, missB = high && !inside;  // A defends y < 0, B defends y > 1
+    a.sB += missA ? 1 : 0;
+    a.sA += missB ? 1 : 0;
+    rA = missA ? -1.f : (missB ? 1.f : 0.f);
+    rB = missA ? 1.f : (missB ? -1.f : 0.f);
+    return missA ? (a.sB >= p.max_score) : (missB ? (a.sA >= p.max_score) : 0);
 }
 
 // ----------------------------------------------------------------------------- QNet

@@ -11,6 +11,7 @@ using namespace pm;
 namespace {
 
 constexpr int kBlock = 256;
+static_assert(kBlock == kRowBlock, "row staging assumes kRowBlock-thread blocks");
 
 __device__ __forceinline__ void do_serve(const pm_env_params& p, const pm_env_state& s, Arena& a, int i,
                                          const double* __restrict__ inject, int inject_cap, uint64_t seed,
@@ -31,7 +32,7 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(pm_env_params p, pm_env_st
                                                       const double* __restrict__ inject, int inject_cap, uint64_t seed,
                                                       float* __restrict__ obsA, float* __restrict__ obsB,
                                                       int32_t* status, int n) {
-    __shared__ float lds[kBlock][7];
+    __shared__ __attribute__((aligned(16))) float lds[kBlock][7];
     const int i0 = blockIdx.x * kBlock;
     const int i = i0 + threadIdx.x;
     float oA[7] = {0}, oB[7] = {0};
@@ -48,52 +49,54 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(pm_env_params p, pm_env_st
 }
 
 // One lane per arena, one wave per SIMD at 65 536 arenas: the kernel is a single load -> tick ->
-// store pass, so its time is the serial latency of that pass. Three things keep it short:
-//   - the serve counter is loaded first and the next production serve (two Philox draws + sincos)
-//     is drawn for every lane while the state loads are still in flight; done lanes use it;
-//   - tick() runs one shared collide path with reciprocal-multiply division (pm_dev.h);
+// store pass, so its time is the serial latency of that pass. Four things keep it short:
+//   - the serve counter is loaded first; the next production serve (two Philox draws + sincos) is
+//     drawn for every lane (done lanes use it) in the same scheduling region as the straight-line
+//     tick, so the two independent dependency chains interleave instead of running back to back;
+//   - tick() is branch-free, with one shared collide path and reciprocal-multiply division;
 //   - every observation row of the block is staged in LDS once, behind one barrier, and leaves as
-//     full float4 stores.
-// autoreset: 0 none, 1 reset + full term rows (term row = the step's pre-reset observation),
+//     full float4 stores; term rows of done arenas leave as one dwordx4 + dwordx3 per row;
+//   - the autoreset mode and parity-mode injection are template parameters, so no uniform branch
+//     splits the hot block.
+// AR (autoreset): 0 none, 1 reset + full term rows (term row = the step's pre-reset observation),
 // 2 reset + term rows written for done arenas only (the other rows are left as they were).
+template <int AR, bool INJ>
 __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
                                                      const int8_t* __restrict__ aB, float* __restrict__ obsA,
                                                      float* __restrict__ obsB, float* __restrict__ rA,
                                                      float* __restrict__ rB, uint8_t* __restrict__ done,
                                                      float* __restrict__ tobsA, float* __restrict__ tobsB,
-                                                     int autoreset, const double* __restrict__ inject, int inject_cap,
+                                                     const double* __restrict__ inject, int inject_cap,
                                                      uint64_t seed, int32_t* status, int n) {
-    __shared__ float lds[4][kBlock][7];
+    __shared__ __attribute__((aligned(16))) float lds[4][kBlock][7];
     const int i0 = blockIdx.x * kBlock;
     const int t = threadIdx.x;
     const int i = i0 + t;
-    const bool full_term = tobsA && autoreset != 2;  // tobsA and tobsB are both set or both null
+    const bool full_term = tobsA && AR != 2;  // tobsA and tobsB are both set or both null
     float oA[7] = {0}, oB[7] = {0};
     if (i < n) {
         int32_t ns = 0;
         double vx = 0.0, vy = 0.0, spn = 0.0;
-        if (autoreset) {
-            ns = __builtin_nontemporal_load(&s.serves[i]);
-            __builtin_amdgcn_sched_barrier(0);  // issue it ahead of the state loads
-        }
+        if (AR) ns = __builtin_nontemporal_load(&s.serves[i]);
         Arena a = load_arena(s, i);
         const int xa = aA[i], xb = aB[i];
-        if (autoreset && !inject) philox_serve(p, (uint32_t)i, (uint32_t)ns, seed, vx, vy, spn);
+        if (AR && !INJ) philox_serve(p, (uint32_t)i, (uint32_t)ns, seed, vx, vy, spn);
         float ra, rb;
         const int d = tick(p, a, xa, xb, ra, rb);
+        // every lane's draw is complete here, ahead of the done branch (the compiler would sink it
+        // into that branch, behind the term-row stores)
+        if (AR && !INJ) asm volatile("" ::"v"(vx), "v"(vy), "v"(spn));
         observe(a, oA, oB);
         if (full_term) {
 #pragma unroll
             for (int k = 0; k < 7; ++k) { lds[2][t][k] = oA[k]; lds[3][t][k] = oB[k]; }
         }
-        if (autoreset && d) {
-            if (autoreset == 2 && tobsA) {
-                float* ta = tobsA + (size_t)i * 7;
-                float* tb = tobsB + (size_t)i * 7;
-#pragma unroll
-                for (int k = 0; k < 7; ++k) { ta[k] = oA[k]; tb[k] = oB[k]; }
+        if (AR && d) {
+            if (AR == 2 && tobsA) {
+                store_row7(tobsA + (size_t)i * 7, oA);
+                store_row7(tobsB + (size_t)i * 7, oB);
             }
-            if (inject) {
+            if (INJ) {
                 const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
                 vx = r[0]; vy = r[1]; spn = r[2];
             }
@@ -170,8 +173,13 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
     if (n == 0) return PM_OK;
-    hipLaunchKernelGGL(k_env_step, dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *p, *s, aA, aB,
-                       obsA, obsB, rA, rB, done, term_obsA, term_obsB, autoreset, inject, inject_cap, seed, status, n);
+    using K = decltype(&k_env_step<0, false>);
+    static const K kernels[3][2] = {{k_env_step<0, false>, k_env_step<0, true>},
+                                    {k_env_step<1, false>, k_env_step<1, true>},
+                                    {k_env_step<2, false>, k_env_step<2, true>}};
+    hipLaunchKernelGGL(kernels[autoreset][inject != nullptr], dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0,
+                       pm_stream(stream), *p, *s, aA, aB, obsA, obsB, rA, rB, done, term_obsA, term_obsB, inject,
+                       inject_cap, seed, status, n);
     PM_LAUNCHED("k_env_step");
     return PM_OK;
 }

@@ -20,6 +20,7 @@ using namespace pm;
 namespace {
 
 constexpr int kBlock = 256;
+static_assert(kBlock == kRowBlock, "row staging assumes kRowBlock-thread blocks");
 
 __device__ __forceinline__ int draw_opponent(const pm_rnn_selfplay& sp, int i, uint32_t ns) {
     // use_pool_opponent = pool and random() < ratio; opponent = random.choice(pool) (:735-736)
@@ -28,7 +29,7 @@ __device__ __forceinline__ int draw_opponent(const pm_rnn_selfplay& sp, int i, u
 }
 
 __global__ __launch_bounds__(kBlock) void k_rsp_init(const pm_rnn_selfplay sp) {
-    __shared__ float lds[kBlock][7];
+    __shared__ __attribute__((aligned(16))) float lds[kBlock][7];
     const int i0 = blockIdx.x * kBlock;
     const int i = i0 + threadIdx.x;
     float oA[7] = {0}, oB[7] = {0};
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(kBlock) void k_rsp_init(const pm_rnn_selfplay sp) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
-    __shared__ float lds[2][kBlock][7];
+    __shared__ __attribute__((aligned(16))) float lds[2][kBlock][7];
     __shared__ long long red[kBlock / 64][6];
     __shared__ int red_st[kBlock / 64];
     const int i0 = blockIdx.x * kBlock;

@@ -46,6 +46,7 @@ static __device__ unsigned long long pm_diag_env[8][1024];
 namespace {
 
 constexpr int kBlock = 256;
+static_assert(kBlock == kRowBlock, "row staging assumes kRowBlock-thread blocks");
 constexpr int kLearn = 1024;              // k_learn / k_adam / k_prepare block
 constexpr int kGradN = PM_QNET_NHEAD;     // grad[520] = finished episodes, grad[521] = updated flag
 constexpr uint32_t kHashEmpty = 0xFFFFFFFFu;
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
         env_fwd_block(sp, blk - nenv);
         return;
     }
-    __shared__ float lds[2][kBlock][7];
+    __shared__ __attribute__((aligned(16))) float lds[2][kBlock][7];
     __shared__ long long red[kBlock / 64][6];
     const int i0 = blk * kBlock;
     const int i = i0 + threadIdx.x;
@@ -300,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
 
 // ------------------------------------------------------------------------------------ init
 __global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
-    __shared__ float lds[kBlock][7];
+    __shared__ __attribute__((aligned(16))) float lds[kBlock][7];
     const int i0 = blockIdx.x * kBlock;
     const int i = i0 + threadIdx.x;
     float oA[7] = {0}, oB[7] = {0};

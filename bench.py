@@ -261,6 +261,7 @@ def main():
     ap.add_argument("--memory", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-overlap", action="store_true", help="dqn: plain step (opponent act in k_act_sp, not in the learner launch)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -282,24 +283,22 @@ def main():
     pool = [synthetic_qnet(100 + k) for k in range(args.pool)]
     allreduce = (lambda t: dist.all_reduce(t)) if dist else None
     L = SelfPlayLearner(ENV_KW, args.arenas, sdB, sdA, pool, batch=args.batch, memory_size=args.memory,
-                        epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce)
+                        epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce,
+                        overlap=not args.no_overlap)
 
     def one_step(ev=None):
-        if ev is None:  # the production path: one C call (three launches) per vector step
-            if dist is None:
-                L.step()
-            else:
-                L.rollout()
-                L.learn()
-                dist.all_reduce(L.grad)
-                L.apply()
+        if ev is None:  # the production path: the overlapped vector step (L.step)
+            L.step()
             return
-        ev[0].record()  # instrumented step: the same kernels, bracketed for the per-kernel rooflines
+        # instrumented step: the same kernels, bracketed for the per-kernel rooflines (both players'
+        # act in one k_act_sp launch; the learner launch computes the next step's opponent act, as
+        # in the production step)
+        ev[0].record()
         L.act()
         ev[1].record()
         L.env_step()
         ev[2].record()
-        L.learn()
+        L.learn(act_next=True)
         if dist is not None:
             dist.all_reduce(L.grad)
         L.apply()

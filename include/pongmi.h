@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 5
+#define PM_ABI_VERSION 6
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -410,6 +410,25 @@ int pm_selfplay_env(const pm_selfplay* sp, void* stream);     /* tick + push + b
 int pm_selfplay_learn(const pm_selfplay* sp, void* stream);
 int pm_selfplay_apply(const pm_selfplay* sp, void* stream);
 int pm_selfplay_step(const pm_selfplay* sp, void* stream);
+
+/* Overlapped stepping. The opponents' greedy actions (side A: modelA / pool nets, :240) depend only
+ * on the observations and opponent ids k_env writes, not on anything the learner updates, and the
+ * learner is a single workgroup, so the next vector step's side-A act rides in the learner's launch
+ * on otherwise idle CUs.
+ *   pm_selfplay_act_part: part PM_ACT_ALL = pm_selfplay_act; PM_ACT_B = PER sample + modelB's
+ *     epsilon-greedy act (select_action_B, :124-130) only; PM_ACT_A = side A only.
+ *   pm_selfplay_learn_act: pm_selfplay_learn, plus side-A actions for the observations the last
+ *     pm_selfplay_env wrote (the next vector step's), into sp->aA.
+ *   pm_selfplay_step_overlap = act_part(B) + env + learn_act + apply (unsharded).
+ * Contract: before act_part(B) / step_overlap, sp->aA must hold side-A actions for the current
+ * observations (pm_selfplay_act_part(A), or learn_act after the last env). Results are
+ * bit-identical to pm_selfplay_step. */
+#define PM_ACT_ALL 0
+#define PM_ACT_B 1
+#define PM_ACT_A 2
+int pm_selfplay_act_part(const pm_selfplay* sp, int32_t part, void* stream);
+int pm_selfplay_learn_act(const pm_selfplay* sp, void* stream);
+int pm_selfplay_step_overlap(const pm_selfplay* sp, void* stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* pm_last_error(void);

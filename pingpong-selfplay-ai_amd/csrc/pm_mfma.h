@@ -390,7 +390,7 @@ struct ActShared {
     float lw[kLwFloats];  // fragment image, padded to whole 1 KB wave chunks
     int list[kListMax];
     int count;
-    int wtot[kActBlock / 64];
+    int wtot[16];  // one per wave: up to 1024-thread blocks (k_learn's side-A act blocks)
     int lpre[16], loff[16], lcnt[16];  // per 256-arena segment of the env kernel's opponent lists
 };
 

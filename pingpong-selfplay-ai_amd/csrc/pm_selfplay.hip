@@ -13,6 +13,8 @@
 //
 // Every loop counter lives in the device control block (pm_ctrl), so a whole vector step can be
 // replayed from a captured graph.
+#include <algorithm>
+
 #include "pm_host.h"
 #include "pm_mfma.h"
 #include "pm_per.h"
@@ -87,10 +89,13 @@ __device__ __forceinline__ void sample_wave(const pm_selfplay& sp, int j) {
 // Both players act (train_iterative.py:240-241) on the matrix cores: ActGrid blocks, modelB tiles
 // with epsilon-greedy, opponent tiles grouped by net (modelA / pool) so weights are tile-uniform.
 // Blocks [0, ceil(batch/4)) sample the update's batch instead (latency-bound, hidden under the act).
-__global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp) {
+// part: PM_ACT_ALL (sample + side B + side A), PM_ACT_B (sample + side B), PM_ACT_A (side A only:
+// the opponents' greedy actions depend on nothing the learner writes, so the overlapped step runs
+// them for the next vector step beside k_learn).
+__global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp, int part) {
     __shared__ __attribute__((aligned(16))) ActShared sh;
     PM_BLK(0);
-    const int nsb = (sp.batch + 3) / 4;
+    const int nsb = part == PM_ACT_A ? 0 : (sp.batch + 3) / 4;
     if ((int)blockIdx.x < nsb) {
         PM_STAMP(64);
         sample_wave(sp, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
@@ -99,7 +104,7 @@ __global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp) {
         return;
     }
     if ((int)blockIdx.x == nsb) PM_STAMP_ANY(70);
-    const ActGrid g{sp.n, sp.n_pool + 1, sp.chunk_A, sp.chunk_P, 1};
+    const ActGrid g{sp.n, sp.n_pool + 1, sp.chunk_A, sp.chunk_P, part == PM_ACT_A ? 0 : 1};
     const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
     const TileOut outB{sp.aB, nullptr, -1.0, 0, 0};  // greedy here; k_env applies the epsilon draw
     act_block(sh, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, sp.w_B, sp.obsA, sp.obsB, outA, outB,
@@ -463,8 +468,27 @@ struct LearnSmem {
 
 // train_step (:134-168) for the batch k_act_sp sampled, plus the episode counters of the rollout and
 // the sum-tree refresh. Single workgroup of 1024 threads; global loads are issued up front.
-__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp) {
-    __shared__ __attribute__((aligned(16))) LearnSmem sm;
+union LearnShared {
+    LearnSmem learn;
+    ActShared act;
+};
+static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
+
+// Block 0 is the learner. Blocks 1.. (pm_selfplay_learn_act) run the opponents' greedy act for the
+// NEXT vector step (train_iterative.py:240, side A) on the observations k_env just wrote: those
+// actions depend on nothing the learner changes, and the learner occupies one CU, so they ride in
+// this launch on otherwise idle CUs instead of lengthening the next k_act_sp. act_block is
+// block-size agnostic: a 1024-thread block stages, compacts and tiles a 4x larger chunk.
+__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP) {
+    __shared__ __attribute__((aligned(16))) LearnShared shm;
+    if (blockIdx.x > 0) {
+        const ActGrid g{sp.n, sp.n_pool + 1, chunkA, chunkP, 0};
+        const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
+        act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,
+                  (int)blockIdx.x - 1, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
+        return;
+    }
+    LearnSmem& sm = shm.learn;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int B = sp.batch;
     pm_ctrl* c = sp.ctrl;
@@ -842,14 +866,40 @@ extern "C" int pm_selfplay_init(const pm_selfplay* sp, void* stream) {
     return pm_selfplay_prepare(sp, stream);
 }
 
-extern "C" int pm_selfplay_act(const pm_selfplay* sp, void* stream) {
-    int rc = check(sp);
-    if (rc) return rc;
-    const ActGrid g{sp->n, sp->n_pool + 1, sp->chunk_A, sp->chunk_P, 1};
-    const int nsb = (sp->batch + 3) / 4;
-    hipLaunchKernelGGL(k_act_sp, dim3(nsb + g.blocks()), dim3(kActBlock), 0, pm_stream(stream), *sp);
+namespace {
+int launch_act(const pm_selfplay* sp, int part, hipStream_t st) {
+    const ActGrid g{sp->n, sp->n_pool + 1, sp->chunk_A, sp->chunk_P, part == PM_ACT_A ? 0 : 1};
+    const int nsb = part == PM_ACT_A ? 0 : (sp->batch + 3) / 4;
+    const int blocks = part == PM_ACT_B ? nsb + g.nb() : nsb + g.blocks();
+    hipLaunchKernelGGL(k_act_sp, dim3(blocks), dim3(kActBlock), 0, st, *sp, part);
     PM_LAUNCHED("k_act_sp");
     return PM_OK;
+}
+
+// The side-A act grid of k_learn's extra blocks (1024 threads: four act blocks' worth each).
+ActGrid learn_act_grid(const pm_selfplay* sp) {
+    return ActGrid{sp->n, sp->n_pool + 1, std::min(4 * sp->chunk_A, kListMax), std::min(4 * sp->chunk_P, kListMax), 0};
+}
+
+int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st) {
+    const ActGrid g = learn_act_grid(sp);
+    const unsigned blocks = 1u + (with_act ? (unsigned)g.blocks() : 0u);
+    hipLaunchKernelGGL(k_learn, dim3(blocks), dim3(kLearn), 0, st, *sp, g.chunk0, g.chunk1);
+    PM_LAUNCHED("k_learn");
+    return PM_OK;
+}
+}  // namespace
+
+extern "C" int pm_selfplay_act(const pm_selfplay* sp, void* stream) {
+    return pm_selfplay_act_part(sp, PM_ACT_ALL, stream);
+}
+
+extern "C" int pm_selfplay_act_part(const pm_selfplay* sp, int32_t part, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    PM_REQUIRE(part == PM_ACT_ALL || part == PM_ACT_B || part == PM_ACT_A, PM_E_ARG,
+               "pm_selfplay_act_part: part=%d", part);
+    return launch_act(sp, part, pm_stream(stream));
 }
 
 extern "C" int pm_selfplay_env(const pm_selfplay* sp, void* stream) {
@@ -868,10 +918,12 @@ extern "C" int pm_selfplay_rollout(const pm_selfplay* sp, void* stream) {
 
 extern "C" int pm_selfplay_learn(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_learn, dim3(1), dim3(kLearn), 0, pm_stream(stream), *sp);
-    PM_LAUNCHED("k_learn");
-    return PM_OK;
+    return rc ? rc : launch_learn(sp, false, pm_stream(stream));
+}
+
+extern "C" int pm_selfplay_learn_act(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    return rc ? rc : launch_learn(sp, true, pm_stream(stream));
 }
 
 extern "C" int pm_selfplay_apply(const pm_selfplay* sp, void* stream) {
@@ -886,6 +938,13 @@ extern "C" int pm_selfplay_apply(const pm_selfplay* sp, void* stream) {
 extern "C" int pm_selfplay_step(const pm_selfplay* sp, void* stream) {
     int rc = pm_selfplay_rollout(sp, stream);
     if (!rc) rc = pm_selfplay_learn(sp, stream);
+    return rc ? rc : pm_selfplay_apply(sp, stream);
+}
+
+extern "C" int pm_selfplay_step_overlap(const pm_selfplay* sp, void* stream) {
+    int rc = pm_selfplay_act_part(sp, PM_ACT_B, stream);
+    if (!rc) rc = pm_selfplay_env(sp, stream);
+    if (!rc) rc = pm_selfplay_learn_act(sp, stream);
     return rc ? rc : pm_selfplay_apply(sp, stream);
 }
 

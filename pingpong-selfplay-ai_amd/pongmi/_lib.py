@@ -31,7 +31,8 @@ PM_RNN_NW = 157456
 PM_TRANS_F = 16
 PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
-ABI_VERSION = 5
+PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
+ABI_VERSION = 6
 
 
 class EnvParams(ctypes.Structure):
@@ -136,6 +137,9 @@ _SIGS = {
     "pm_selfplay_learn": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_apply": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_step": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_act_part": (c_i32, [c_void_p, c_i32, c_void_p]),
+    "pm_selfplay_learn_act": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_step_overlap": (c_i32, [c_void_p, c_void_p]),
     "pm_last_error": (ctypes.c_char_p, []),
     "pm_abi_version": (c_i32, []),
     "pm_sizeof": (c_i32, [c_i32]),

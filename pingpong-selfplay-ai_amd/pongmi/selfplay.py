@@ -44,8 +44,10 @@ class SelfPlayLearner:
                  memory_size=1_000_000, gamma=0.99, lr=2.5e-4, epsilon=0.02, min_epsilon=0.02, epsilon_decay=0.995,
                  target_update_interval=1000, pool_ratio=0.33, alpha=0.6, beta_start=0.4, beta_frames=100000,
                  episode=0, seed=0, rank=0, world=1, allreduce=None, device=None, modelA_noisy=True,
-                 fuse_apply=True):
+                 fuse_apply=True, overlap=True):
         self.lib = _lib.load()
+        self.overlap = bool(overlap)
+        self._aA_ready = False
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise _lib.PongmiError("SelfPlayLearner runs on a ROCm device only")
@@ -124,29 +126,56 @@ class SelfPlayLearner:
         check(self.lib.pm_selfplay_init(ctypes.byref(sp), stream_ptr()), "pm_selfplay_init")
 
     # ------------------------------------------------------------------ stepping
+    # `_aA_ready`: sp.aA holds the opponents' actions for the current observations (computed by a
+    # side-A act, or by the extra blocks of the previous step's learner launch). Anything that
+    # changes the observations, opponent ids or opponent weights clears it.
     def rollout(self):
+        self._aA_ready = False
         check(self.lib.pm_selfplay_rollout(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_rollout")
 
-    def act(self):
-        check(self.lib.pm_selfplay_act(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_act")
+    def act(self, part=_lib.PM_ACT_ALL):
+        check(self.lib.pm_selfplay_act_part(ctypes.byref(self.sp), int(part), stream_ptr()), "pm_selfplay_act_part")
+        if part != _lib.PM_ACT_B:
+            self._aA_ready = True
 
     def env_step(self):
+        self._aA_ready = False
         check(self.lib.pm_selfplay_env(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_env")
 
-    def learn(self):
-        check(self.lib.pm_selfplay_learn(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_learn")
+    def learn(self, act_next=False):
+        """train_step; with act_next the same launch also computes the next vector step's opponent
+        actions (after env_step: for the observations it wrote)."""
+        if act_next:
+            check(self.lib.pm_selfplay_learn_act(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_learn_act")
+            self._aA_ready = True
+        else:
+            check(self.lib.pm_selfplay_learn(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_learn")
 
     def apply(self):
         check(self.lib.pm_selfplay_apply(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_apply")
 
     def step(self):
-        """One vector step (n env-steps on this rank)."""
-        if self.world == 1:
-            check(self.lib.pm_selfplay_step(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step")
+        """One vector step (n env-steps on this rank). With `overlap` the opponents' act for the
+        next step runs inside the learner's launch (bit-identical results)."""
+        if not self.overlap:
+            if self.world == 1:
+                check(self.lib.pm_selfplay_step(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step")
+                return
+            self.rollout()
+            self.learn()
+            self.allreduce(self.grad)  # one RCCL all-reduce per update: 520 grads + counters
+            self.apply()
             return
-        self.rollout()
-        self.learn()
-        self.allreduce(self.grad)  # one RCCL all-reduce per update: 520 grads + counters
+        if not self._aA_ready:
+            self.act(_lib.PM_ACT_A)
+        if self.world == 1:
+            check(self.lib.pm_selfplay_step_overlap(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step_overlap")
+            self._aA_ready = True
+            return
+        self.act(_lib.PM_ACT_B)
+        self.env_step()
+        self.learn(act_next=True)
+        self.allreduce(self.grad)
         self.apply()
 
     # ------------------------------------------------------------------ state readout (syncs)
@@ -168,6 +197,7 @@ class SelfPlayLearner:
     def set_modelA(self, state):
         """Opponent slot 0. modelA is never put in eval() by the reference (train_iterative.py:90-92),
         so it acts with its frozen epsilon buffers: W = mu + sigma*eps."""
+        self._aA_ready = False
         self.paramsA = pack_state_dict(state, self.device)
         self.w_opp[0] = fold(self.paramsA, _lib.PM_FOLD_TRAIN if self.modelA_noisy else _lib.PM_FOLD_EVAL)[0]
 
@@ -198,6 +228,7 @@ class SelfPlayLearner:
 
     def prepare(self):
         """Re-derive acting weights / next-update heads after the host replaced parameters."""
+        self._aA_ready = False
         check(self.lib.pm_selfplay_prepare(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_prepare")
 
 

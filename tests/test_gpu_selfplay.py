@@ -282,3 +282,31 @@ def test_sum_tree_incremental_equals_rebuild(golden, n, cap):
     ref = np.array([np.sum((pr[k * 1024:(k + 1) * 1024] ** np.float32(0.6)).astype(np.float64))
                     for k in range(nch)])
     np.testing.assert_allclose(chunks, ref, rtol=1e-6)  # device powf vs numpy float32 pow
+
+
+def test_overlapped_step_is_bitwise_identical(golden):
+    """pm_selfplay_step_overlap (the next step's side-A act in the learner's launch) must equal the
+    plain step bit for bit, also across host changes of modelA (which invalidate the precomputed
+    actions) and the bench's instrumented step shape (full act -> env -> learn_act -> apply)."""
+    from pongmi import _lib
+    A = _learner(golden, n=4096, batch=256, cap=16384, seed=21, n_pool=3)
+    B = _learner(golden, n=4096, batch=256, cap=16384, seed=21, n_pool=3, overlap=False)
+    for k in range(24):
+        if k == 9:
+            sd = _random_qnet_sd(77)
+            A.set_modelA(sd)
+            B.set_modelA(sd)
+        if k % 5 == 3:  # instrumented shape
+            A.act()
+            A.env_step()
+            A.learn(act_next=True)
+            A.apply()
+        else:
+            A.step()
+        B.step()
+    B.act(_lib.PM_ACT_A)  # A already holds the next step's side-A actions
+    torch.cuda.synchronize()
+    for name in ("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "opp", "w_B",
+                 "learn_heads", "per_work", "idx", "isw", "aA", "aB", "obsA", "obsB", "ep_reward"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    assert A.counters() == B.counters()

@@ -19,11 +19,19 @@ tag = args[0] if args else "r1"
 root = args[1] if len(args) > 1 else "gpurun_out"
 out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
 acc = defaultdict(lambda: defaultdict(list))
+grids = defaultdict(set)
 for f in sorted(glob.glob(os.path.join(root, f"pmc_{tag}_*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         short = name.split("::")[-1].split("(")[0] if "::" in name else name.split("(")[0]
-        acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        short = short.split("<")[0].strip()  # template arguments (k_env_step<2, false>)
+        grid = r.get("Grid_Size") or r.get("Grid_Size_X") or "0"
+        acc[f"{short}@{grid}"][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        grids[short].add(int(grid))
+# a kernel launched with several grids (k_act_sp: full act / side B only; k_learn: with and without
+# the side-A act blocks) is listed per grid as name@grid; the bare name is its LARGEST grid
+for short, gs in grids.items():
+    acc[short] = acc[f"{short}@{max(gs)}"]
 keys = ["k_act_sp", "k_env", "k_learn", "k_env_step"]
 summary = {}
 for k in keys + sorted(set(acc) - set(keys)):

@@ -188,23 +188,75 @@ __device__ __forceinline__ void serve(Arena& a, double vx, double vy, double spi
     a.vx = vx; a.vy = vy; a.spin = spin;
 }
 
+// sin and cos of x for |x| < 3*pi/4 (serve angles are within +-135 degrees for any sane config;
+// the caller falls back to OCML otherwise), straight-line: one Cody-Waite step by pi/2 with a
+// two-part constant (fdlibm __ieee754_rem_pio2's first case) and fdlibm's __kernel_sin /
+// __kernel_cos polynomials on the reduced pair (y0, y1), the quadrant applied by selects. Error
+// < 1 ulp, as OCML's sincos; no branch, so the draw schedules together with the env tick.
+__device__ __forceinline__ void sincos_serve(double x, double& s, double& c) {
+    const double pio4 = 7.85398163397448278999e-01;
+    const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
+    const int n = x > pio4 ? 1 : (x < -pio4 ? -1 : 0);
+    const double z0 = n > 0 ? x - pio2_1 : x + pio2_1;
+    const double t = n > 0 ? pio2_1t : -pio2_1t;
+    double y0 = z0 - t;
+    double y1 = (z0 - y0) - t;
+    y0 = n == 0 ? x : y0;
+    y1 = n == 0 ? 0.0 : y1;
+    // __kernel_sin(y0, y1, 1)
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double z = y0 * y0, v = z * y0;
+    const double rs = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    const double ks = y0 - ((z * (0.5 * y1 - v * rs) - y1) - v * S1);
+    // __kernel_cos(y0, y1): |y0| <= pi/4 < 0.78125, fdlibm's plain branch
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double rc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double kc = w + (((1.0 - w) - hz) + (z * rc - y0 * y1));
+    s = n == 0 ? ks : (n > 0 ? kc : -kc);
+    c = n == 0 ? kc : (n > 0 ? -ks : ks);
+}
+
 // Production serve draws from Philox: speed = U(lo,hi), coin < 0.5 picks the angle interval,
 // angle = U(interval) degrees -> radians (math.radians: deg * (pi/180)), spin = U(lo,hi).
-// sincos shares one argument reduction between the two (OCML, same values as cos and sin).
-__device__ __forceinline__ void philox_serve(const pm_env_params& p, uint32_t i, uint32_t nserve, uint64_t seed,
-                                             double& vx, double& vy, double& spin) {
+// serve_draw is straight-line (hot kernels draw it for every lane beside the tick); serve_finish
+// redoes the rare |angle| >= 135 degree case with OCML's sincos, where the serve is applied.
+struct ServeDraw {
+    double speed, rad, vx, vy, spin;
+};
+__device__ __forceinline__ ServeDraw serve_draw(const pm_env_params& p, uint32_t i, uint32_t nserve, uint64_t seed) {
     const U4 r0 = philox(i, TAG_SERVE, nserve, 0u, seed);
     const U4 r1 = philox(i, TAG_SERVE | 0x100u, nserve, 0u, seed);
-    const double speed = p.speed_lo + (p.speed_hi - p.speed_lo) * u53(r0.x, r0.y);
-    double ang;
-    if (u53(r0.z, r0.w) < 0.5) ang = p.ang0_lo + (p.ang0_hi - p.ang0_lo) * u53(r1.x, r1.y);
-    else ang = p.ang1_lo + (p.ang1_hi - p.ang1_lo) * u53(r1.x, r1.y);
-    const double rad = ang * (3.141592653589793 / 180.0);
+    ServeDraw d;
+    d.speed = p.speed_lo + (p.speed_hi - p.speed_lo) * u53(r0.x, r0.y);
+    const bool first = u53(r0.z, r0.w) < 0.5;
+    const double lo = first ? p.ang0_lo : p.ang1_lo, hi = first ? p.ang0_hi : p.ang1_hi;
+    const double ang = lo + (hi - lo) * u53(r1.x, r1.y);
+    d.rad = ang * (3.141592653589793 / 180.0);
     double sn, cs;
-    sincos(rad, &sn, &cs);
-    vx = speed * cs;
-    vy = speed * sn;
-    spin = p.spin_lo + (p.spin_hi - p.spin_lo) * u53(r1.z, r1.w);
+    sincos_serve(d.rad, sn, cs);
+    d.vx = d.speed * cs;
+    d.vy = d.speed * sn;
+    d.spin = p.spin_lo + (p.spin_hi - p.spin_lo) * u53(r1.z, r1.w);
+    return d;
+}
+__device__ __forceinline__ void serve_finish(ServeDraw& d) {
+    if (!(fabs(d.rad) < 2.35619449019234483700)) {
+        double sn, cs;
+        sincos(d.rad, &sn, &cs);
+        d.vx = d.speed * cs;
+        d.vy = d.speed * sn;
+    }
+}
+__device__ __forceinline__ void philox_serve(const pm_env_params& p, uint32_t i, uint32_t nserve, uint64_t seed,
+                                             double& vx, double& vy, double& spin) {
+    ServeDraw d = serve_draw(p, i, nserve, seed);
+    serve_finish(d);
+    vx = d.vx; vy = d.vy; spin = d.spin;
 }
 
 __device__ __forceinline__ double clip01(double v) { return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v); }

@@ -76,16 +76,16 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
     float oA[7] = {0}, oB[7] = {0};
     if (i < n) {
         int32_t ns = 0;
-        double vx = 0.0, vy = 0.0, spn = 0.0;
+        ServeDraw sv{};
         if (AR) ns = __builtin_nontemporal_load(&s.serves[i]);
         Arena a = load_arena(s, i);
         const int xa = aA[i], xb = aB[i];
-        if (AR && !INJ) philox_serve(p, (uint32_t)i, (uint32_t)ns, seed, vx, vy, spn);
+        if (AR && !INJ) sv = serve_draw(p, (uint32_t)i, (uint32_t)ns, seed);
         float ra, rb;
         const int d = tick(p, a, xa, xb, ra, rb);
         // every lane's draw is complete here, ahead of the done branch (the compiler would sink it
         // into that branch, behind the term-row stores)
-        if (AR && !INJ) asm volatile("" ::"v"(vx), "v"(vy), "v"(spn));
+        if (AR && !INJ) asm volatile("" ::"v"(sv.vx), "v"(sv.vy), "v"(sv.spin), "v"(sv.rad));
         observe(a, oA, oB);
         if (full_term) {
 #pragma unroll
@@ -98,9 +98,11 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
             }
             if (INJ) {
                 const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
-                vx = r[0]; vy = r[1]; spn = r[2];
+                sv.vx = r[0]; sv.vy = r[1]; sv.spin = r[2];
+            } else {
+                serve_finish(sv);
             }
-            serve(a, vx, vy, spn);
+            serve(a, sv.vx, sv.vy, sv.spin);
             s.serves[i] = ns + 1;
             observe(a, oA, oB);
         }

@@ -342,7 +342,8 @@ struct ApplySmem {  // the 520-float arrays are padded to whole 64-float global_
     float g[PM_QNET_NHEAD + 2];                // shard-summed grads | finished episodes | updated flag
     float ak[2];                               // Adam step size lr / (1 - b1^t), sqrt(1 - b2^t)
     float nact[132], ntrain[132];
-    float heads[260];
+    float heads[3][260];                       // folded acting / next-update / target heads
+    double eps_next;                           // fused learner: eps * decay^D, computed early
 };
 
 // torch.optim.Adam's bias corrections for update number ts, computed in fp64 as torch does (Python
@@ -371,19 +372,21 @@ __device__ __forceinline__ void load_apply_inputs(const pm_selfplay& sp, ApplySm
 // and targetB heads (eval mode: mu, :100), both in MFMA fragment order in learn_heads, plus that
 // update's noise. Block-wide; noise already in sm.nact / sm.ntrain.
 __device__ __forceinline__ void derive_weights(const pm_selfplay& sp, ApplySmem& sm) {
-    const int t = threadIdx.x, nt = blockDim.x;
+    const int t = threadIdx.x;
     float* lh = sp.learn_heads;
-    fold_heads_from(sm.hp, nullptr, sm.nact, PM_FOLD_TRAIN_FRESH, sm.heads, sp.paramsB + PM_QNET_EPS_OFF, t, nt);
+    // the three folds are independent: one pass on three 260-thread groups, one barrier, then the
+    // three fragment writes
+    if (t < 260) {
+        fold_heads_from(sm.hp, nullptr, sm.nact, PM_FOLD_TRAIN_FRESH, sm.heads[0], sp.paramsB + PM_QNET_EPS_OFF, t, 260);
+    } else if (t < 520) {
+        fold_heads_from(sm.hp, nullptr, sm.ntrain, PM_FOLD_TRAIN_FRESH, sm.heads[1], lh + 528, t - 260, 260);
+    } else if (t < 780) {
+        fold_heads_from(sm.tmu, nullptr, nullptr, PM_FOLD_EVAL, sm.heads[2], nullptr, t - 520, 260);
+    }
     __syncthreads();
-    write_head_frags(sm.heads, sp.w_B);
-    __syncthreads();
-    fold_heads_from(sm.hp, nullptr, sm.ntrain, PM_FOLD_TRAIN_FRESH, sm.heads, lh + 528, t, nt);
-    __syncthreads();
-    heads_to_frags(sm.heads, lh);
-    __syncthreads();
-    fold_heads_from(sm.tmu, nullptr, nullptr, PM_FOLD_EVAL, sm.heads, nullptr, t, nt);
-    __syncthreads();
-    heads_to_frags(sm.heads, lh + 264);
+    write_head_frags(sm.heads[0], sp.w_B);
+    heads_to_frags(sm.heads[1], lh);
+    heads_to_frags(sm.heads[2], lh + 264);
 }
 
 // Both noise draws at once, half of the block each.
@@ -393,16 +396,27 @@ __device__ __forceinline__ void gen_both_noises(const pm_selfplay& sp, ApplySmem
     if (t < half) gen_noise(sp.seed_net, TAG_NOISE_ACT, act_ctr, sm.nact, t, half);
     else gen_noise(sp.seed_net, TAG_NOISE_TRAIN, train_ctr, sm.ntrain, t - half, half);
 }
+// The same draws on threads [t0, t0 + 512) only (the fused learner's waves with slack in its load
+// phase). Same values: every noise element depends only on (seed, tag, counter, index).
+__device__ __forceinline__ void gen_both_noises_on(const pm_selfplay& sp, ApplySmem& sm, uint64_t act_ctr,
+                                                   uint64_t train_ctr, int t0) {
+    const int u = (int)threadIdx.x - t0;
+    if (u < 0 || u >= 512) return;
+    if (u < 256) gen_noise(sp.seed_net, TAG_NOISE_ACT, act_ctr, sm.nact, u, 256);
+    else gen_noise(sp.seed_net, TAG_NOISE_TRAIN, train_ctr, sm.ntrain, u - 256, 256);
+}
 
 // optimizer.step() (:161) on the shard-summed grads, target sync (:166-168), epsilon decay (:261),
 // replay / step counters, then derive_weights for the next step. All inputs in LDS (sm) and `cs`
-// (the control block as the kernel found it); only stores go to global memory.
-__device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& sm, const pm_ctrl& cs) {
+// (the control block as the kernel found it); only stores go to global memory. `early`: the fused
+// learner already drew both noises into sm and computed sm.eps_next (the same values) off its
+// critical path.
+__device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& sm, const pm_ctrl& cs, bool early) {
     const int t = threadIdx.x, nt = blockDim.x;
     const bool train = sm.g[kGradN + 1] > 0.5f;
     const int64_t ts = cs.train_steps + (train ? 1 : 0);
     const uint64_t step = cs.step;
-    gen_both_noises(sp, sm, step + 1, (uint64_t)ts + 1);
+    if (!early) gen_both_noises(sp, sm, step + 1, (uint64_t)ts + 1);
     if (train) {
         const float step_size = sm.ak[0], bc2s = sm.ak[1];  // adam_consts, published before a barrier
         for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
@@ -433,7 +447,7 @@ __device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& s
     if (t == 0) {
         pm_ctrl* c = sp.ctrl;
         const double D = (double)sm.g[kGradN];  // finished episodes (all shards)
-        const double e = cs.epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
+        const double e = early ? sm.eps_next : cs.epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
         c->epsilon = e > sp.min_epsilon ? e : sp.min_epsilon;
         if (train) { c->train_steps = ts; c->frame_idx = cs.frame_idx + 1; }
         c->pos = (cs.pos + sp.n) % sp.cap;
@@ -537,7 +551,15 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         rwd = tr[7];
         bits = __float_as_int(tr[15]);
     }
-    if (sp.fuse_apply && t == 0) adam_consts(sp, cs.train_steps + 1, sm.ap);
+    // fused: the optimizer's scalar prologue on waves with slack in this load phase (they are not
+    // on the dependent idx -> replay-row path of waves 0-3): the Adam bias corrections (two fp64
+    // pow) on the last thread, both NoisyNet draws of the apply on the upper half of the block
+    PM_STAMP(35);
+    if (sp.fuse_apply) {
+        if (t == kLearn - 1) adam_consts(sp, cs.train_steps + 1, sm.ap);
+        gen_both_noises_on(sp, sm.ap, cs.step + 1, (uint64_t)(cs.train_steps + (train ? 1 : 0)) + 1, kLearn / 2);
+    }
+    PM_STAMP(34);
     if (train && t < 260) sp.paramsB[PM_QNET_EPS_OFF + t] = eps_v;  // reset_noise leaves it in modelB
     const float wraw = act ? wraw_l : 0.f;
     const int64_t id = act ? id_l : 0;
@@ -578,6 +600,10 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
         if (lane == 0) sm.red[wv][0] = m;
     }
+#ifdef PM_DIAG
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's loads (incl. LDS DMA) landed
+    PM_STAMP_T(40, 0); PM_STAMP_T(41, 256); PM_STAMP_T(42, 512); PM_STAMP_T(43, 960);
+#endif
     __syncthreads();
     PM_STAMP(1);
 
@@ -626,6 +652,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     __syncthreads();
     PM_STAMP(2);
     ep_fin = sm.cnt[0][0];
+    if (sp.fuse_apply && t == kLearn - 1)  // idle in phase 2: the per-episode epsilon decay (:261)
+        sm.ap.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)(float)ep_fin);
     if (t == 0) {  // rollout bookkeeping (:245-249)
         c->ep_step = ep_fin;
         c->episodes = cs.episodes + ep_fin;
@@ -797,7 +825,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     PM_STAMP(6);
     if (sp.fuse_apply) {  // unsharded: no all-reduce between the gradient and the optimizer step
         __syncthreads();
-        apply_update(sp, sm.ap, cs);
+        apply_update(sp, sm.ap, cs, true);
     }
     PM_STAMP(7);
 }
@@ -809,7 +837,7 @@ __global__ __launch_bounds__(kLearn) void k_adam(const pm_selfplay sp) {
     load_apply_inputs(sp, sm, true);
     if (threadIdx.x == 0) adam_consts(sp, cs.train_steps + 1, sm);
     __syncthreads();
-    apply_update(sp, sm, cs);
+    apply_update(sp, sm, cs, false);
 }
 
 // pm_selfplay_prepare: features + acting weights of the current step + next update's heads

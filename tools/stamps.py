@@ -26,6 +26,8 @@ NAMES = {
     1: "learn loads", 2: "learn fwd (MFMA)", 3: "learn td/loss", 4: "learn scatter+grad",
     8: "ph4 grads out w0", 9: "ph4 grads out w15", 10: "ph4 scatter subs w0", 11: "ph4 scatter subs w15",
     12: "ph4 push subs w0", 13: "ph4 push subs w15", 14: "ph4 edges w0", 15: "ph4 edges w15",
+    35: "ph0 before prologue", 34: "ph0 after prologue", 40: "ph0 w0 loads landed",
+    41: "ph0 w4 loads landed", 42: "ph0 w8 loads landed", 43: "ph0 w15 loads landed",
     5: "learn tree level1", 6: "learn tree level2", 20: "apply adam", 21: "apply derive", 7: "learn end",
 }
 

@@ -311,10 +311,17 @@ __device__ __forceinline__ void tile_inputs(const float* __restrict__ o, int h, 
     xs[3] = o[5 + h];
 }
 
+// The first tile's layer-1 operands when the caller could load them before its staging barrier
+// (rows lo + k, no list needed): the observation load then shares the weight staging's round trip.
+struct TilePre {
+    bool have;
+    float xs[4];
+};
+
 // QNet forward + action for `count` arenas listed in LDS `list` (arena indices), weights staged in
 // LDS `lw`. Each wave takes tiles wave, wave + nwaves, ... Wave-uniform control flow throughout.
 __device__ __forceinline__ void run_tiles(const float* lw, const float* __restrict__ obs, const int* list, int count,
-                                          const TileOut& out) {
+                                          const TileOut& out, const TilePre& pre) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int h = lane >> 5, col = lane & 31;
     const int ntiles = (count + 31) >> 5;
@@ -322,7 +329,12 @@ __device__ __forceinline__ void run_tiles(const float* lw, const float* __restri
     if (tl >= ntiles) return;  // wave-uniform
     int arena = list[min(tl * 32 + col, count - 1)];
     float xs[4];
-    tile_inputs(obs + (size_t)arena * 7, h, xs);
+    if (pre.have) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xs[k] = pre.xs[k];
+    } else {
+        tile_inputs(obs + (size_t)arena * 7, h, xs);
+    }
     for (; tl < ntiles; tl += nw) {
         const int row = tl * 32 + col;
         const bool valid = row < count;
@@ -373,7 +385,7 @@ __device__ __forceinline__ void run_tiles(const float* lw, const float* __restri
 // Block -> work: [0, nB) chunks of kChunkB arenas for side B (one net: w_B); then side A: net 0 in
 // chunks of chunk0 arenas, nets 1..n_opp-1 in chunks of chunk1 arenas each, rows compacted by
 // opponent id so every tile has uniform weights.
-constexpr int kChunkB = 128;  // side-B rows per block: 4 tiles, one per wave (A-side chunks aim at ~96-128 rows)
+constexpr int kChunkB = 256;  // side-B rows per block: 8 tiles, two per wave (A-side chunks aim at ~96-128 rows)
 
 struct ActGrid {
     int n, n_opp, chunk0, chunk1, side_b;
@@ -463,10 +475,20 @@ __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const
         if (threadIdx.x == 0) sh.count = hi - lo;
         for (int k = threadIdx.x; k < hi - lo; k += blockDim.x) sh.list[k] = lo + k;
     }
+    // rows lo + k (side B, or a single opponent net): this wave's first tile of observations loads
+    // now, in the same round trip as the weight staging (the barrier below waits for both)
+    TilePre pre{false, {0.f, 0.f, 0.f, 0.f}};
+    if (!compact && !lists) {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, cnt = hi - lo;
+        if (wave * 32 < cnt) {  // wave-uniform
+            pre.have = true;
+            tile_inputs(obs + (size_t)(lo + min(wave * 32 + (lane & 31), cnt - 1)) * 7, lane >> 5, pre.xs);
+        }
+    }
     __syncthreads();
     PM_BLK(1);
     __builtin_amdgcn_s_setprio(0);
-    run_tiles(sh.lw, obs, sh.list, sh.count, out);
+    run_tiles(sh.lw, obs, sh.list, sh.count, out, pre);
 }
 
 }  // namespace pm

@@ -225,6 +225,7 @@ __device__ inline void per_sample_one(int64_t size, const PerTree& tr, const Pus
         total = __shfl(incl, 63);
         t = u * total;
         blk = chunk_find(vals, part, incl, 0.0, t, lane, before);
+        PM_BLK(4);
     } else {
         total = 0.0;
         for (int64_t c0 = 0; c0 < nb; c0 += 1024) {
@@ -273,13 +274,19 @@ __device__ inline void per_sample_one(int64_t size, const PerTree& tr, const Pus
     const int64_t s0 = blk * PER_FAN;
     const double sv = (lane < PER_FAN && s0 + lane < tr.nsub) ? tr.sub[s0 + lane] : 0.0;
     const int64_t sb = s0 + lane_find(sv, t - before, lane, b1, v1);
+    PM_BLK(5);
     // level 0: 64 leaves
     const int64_t e = sb * PER_SUB + lane;
     const double pv = e < size ? (double)per_leaf(tr.leaf, e, pr) : 0.0;
     double b0, pa;
     const int k = lane_find(pv, t - before - b1, lane, b0, pa);
+    PM_BLK(6);
     idx_out = sb * PER_SUB + k;
     wraw_out = (float)pow((double)size * (pa / total), -beta);
+#ifdef PM_DIAG
+    asm volatile("" ::"v"(wraw_out));
+#endif
+    PM_BLK(7);
 }
 
 // Full rebuild over prios[0, cap): leaves, then level-1 and level-2 nodes with the pending push

@@ -92,6 +92,20 @@ __device__ __forceinline__ void copy_lds_f32(const float* __restrict__ src, floa
     }
 }
 constexpr int pad64(int n) { return (n + 63) / 64 * 64; }
+// The same copy as 16-byte lanes (1 KB per wave instruction, a quarter of the instructions): src and
+// dst 16-byte aligned, N a multiple of 4, dst holding N rounded up to 256 floats. The 4-byte form
+// was the last thing to land in the learner's load phase (~2 us after its plain loads).
+template <int N>
+__device__ __forceinline__ void copy_lds_f32x4(const float* __restrict__ src, float* dst) {
+    static_assert(N % 4 == 0, "whole float4s");
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    for (int c = wv; c * 256 < N; c += nw) {
+        const int k = min(c * 64 + lane, N / 4 - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(s4 + k), (lds_void*)(dst + c * 256), 16, 0, 0);
+    }
+}
+constexpr int pad256(int n) { return (n + 255) / 256 * 256; }
 
 // Stage one net's fragment image global -> LDS directly (global_load_lds: 1 KB per wave
 // instruction, no registers, no wait until the caller's barrier). `lw` holds kLwFloats floats.

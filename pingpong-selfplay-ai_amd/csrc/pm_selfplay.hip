@@ -336,9 +336,9 @@ __global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
 // ------------------------------------------------------------------------------------ learner
 // ------------------------------------------------------------------------------------ apply
 struct ApplySmem {  // the 520-float arrays are padded to whole 64-float global_load_lds chunks
-    float hp[pad64(PM_QNET_NHEAD)];   // modelB head parameters (after the optimizer step)
-    float tmu[pad64(PM_QNET_NHEAD)];  // targetB head parameters (mu used)
-    float m[pad64(PM_QNET_NHEAD)], v[pad64(PM_QNET_NHEAD)];  // Adam moments
+    float hp[pad256(PM_QNET_NHEAD)];   // modelB head parameters (after the optimizer step)
+    float tmu[pad256(PM_QNET_NHEAD)];  // targetB head parameters (mu used)
+    float m[pad256(PM_QNET_NHEAD)], v[pad256(PM_QNET_NHEAD)];  // Adam moments
     float g[PM_QNET_NHEAD + 2];                // shard-summed grads | finished episodes | updated flag
     float ak[2];                               // Adam step size lr / (1 - b1^t), sqrt(1 - b2^t)
     float nact[132], ntrain[132];
@@ -354,14 +354,20 @@ __device__ __forceinline__ void adam_consts(const pm_selfplay& sp, int64_t ts, A
     sm.ak[0] = (float)(sp.lr / bc1);
     sm.ak[1] = (float)sqrt(bc2);
 }
+// The same two constants from two lanes of one wave (lane `which` = 0: step size, 1: sqrt(bc2)), so
+// the two fp64 pow run side by side instead of back to back.
+__device__ __forceinline__ void adam_const_lane(const pm_selfplay& sp, int64_t ts, ApplySmem& sm, int which) {
+    const double bc = 1.0 - pow(which ? sp.beta2 : sp.beta1, (double)ts);
+    sm.ak[which] = which ? (float)sqrt(bc) : (float)(sp.lr / bc);
+}
 
 // Block-wide: the optimizer's inputs global -> LDS directly (global_load_lds, no wait until the
 // caller's barrier). g: from LDS already when fused.
 __device__ __forceinline__ void load_apply_inputs(const pm_selfplay& sp, ApplySmem& sm, bool with_grad) {
-    copy_lds_f32<PM_QNET_NHEAD>(sp.paramsB + PM_QNET_HEAD_OFF, sm.hp);
-    copy_lds_f32<PM_QNET_NHEAD>(sp.paramsT + PM_QNET_HEAD_OFF, sm.tmu);
-    copy_lds_f32<PM_QNET_NHEAD>(sp.adam_m, sm.m);
-    copy_lds_f32<PM_QNET_NHEAD>(sp.adam_v, sm.v);
+    copy_lds_f32x4<PM_QNET_NHEAD>(sp.paramsB + PM_QNET_HEAD_OFF, sm.hp);
+    copy_lds_f32x4<PM_QNET_NHEAD>(sp.paramsT + PM_QNET_HEAD_OFF, sm.tmu);
+    copy_lds_f32x4<PM_QNET_NHEAD>(sp.adam_m, sm.m);
+    copy_lds_f32x4<PM_QNET_NHEAD>(sp.adam_v, sm.v);
     if (with_grad)
         for (int k = threadIdx.x; k < PM_QNET_NHEAD + 2; k += blockDim.x) sm.g[k] = sp.grad[k];
 }
@@ -462,14 +468,14 @@ struct LearnSmem {
     union {
         struct {  // forward phase
             float lw[kLwFloats];  // modelB.features fragments (== targetB.features: frozen)
-            float hf[pad64(2 * 264)];  // modelB (update noise) [0, 264) / targetB (mu) [264, 528) head fragments
+            float hf[pad256(2 * 264)];  // modelB (update noise) [0, 264) / targetB (mu) [264, 528) head fragments
         } f;
         float gpart[16][256];  // gradient phase: per-wave partial sums
     } u;
     float Hs[PM_MAX_BATCH][65];  // ReLU(features(s)) of the batch
     float qv[PM_MAX_BATCH][12];  // Q_B(s) 0..2 | Q_B(s') 4..6 | Q_T(s') 8..10
     float coef[PM_MAX_BATCH][4]; // dL/d(V, A0, A1, A2) per sample
-    float eps_tr[pad64(260)];    // the update's noise (eps section layout)
+    float eps_tr[pad256(260)];    // the update's noise (eps section layout)
     int64_t sidx[PM_MAX_BATCH];
     uint32_t hkey[512];          // open-addressing set of sampled indices (last-duplicate-wins)
     int hwin[512];
@@ -518,8 +524,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     const bool act = train && t < B;
     const int nbr = (sp.n + kBlock - 1) / kBlock;
     stage_frags_lds(sp.w_B, sm.u.f.lw, 0);
-    copy_lds_f32<2 * 264>(sp.learn_heads, sm.u.f.hf);
-    copy_lds_f32<260>(sp.learn_heads + 528, sm.eps_tr);
+    copy_lds_f32x4<2 * 264>(sp.learn_heads, sm.u.f.hf);
+    copy_lds_f32x4<260>(sp.learn_heads + 528, sm.eps_tr);
     if (sp.fuse_apply) load_apply_inputs(sp, sm.ap, false);
     long long part[6] = {0, 0, 0, 0, 0, 0};
     if (t < nbr) {
@@ -556,7 +562,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     // pow) on the last thread, both NoisyNet draws of the apply on the upper half of the block
     PM_STAMP(35);
     if (sp.fuse_apply) {
-        if (t == kLearn - 1) adam_consts(sp, cs.train_steps + 1, sm.ap);
+        if (t >= kLearn - 2) adam_const_lane(sp, cs.train_steps + 1, sm.ap, t - (kLearn - 2));
         gen_both_noises_on(sp, sm.ap, cs.step + 1, (uint64_t)(cs.train_steps + (train ? 1 : 0)) + 1, kLearn / 2);
     }
     PM_STAMP(34);
@@ -865,9 +871,12 @@ int check(const pm_selfplay* sp) {
     PM_REQUIRE(!sp->fuse_apply || sp->world == 1, PM_E_ARG, "pm_selfplay: fuse_apply needs world == 1");
     PM_REQUIRE(sp->chunk_A > 0 && sp->chunk_A <= kListMax && sp->chunk_P > 0 && sp->chunk_P <= kListMax, PM_E_SIZE,
                "pm_selfplay: chunk_A/chunk_P must be in [1, %d]", kListMax);
-    PM_REQUIRE(((((uintptr_t)sp->w_opp) | ((uintptr_t)sp->w_B) | ((uintptr_t)sp->prios) | ((uintptr_t)sp->per_work)) &
+    PM_REQUIRE(((((uintptr_t)sp->w_opp) | ((uintptr_t)sp->w_B) | ((uintptr_t)sp->prios) | ((uintptr_t)sp->per_work) |
+                 ((uintptr_t)sp->paramsB) | ((uintptr_t)sp->paramsT) | ((uintptr_t)sp->adam_m) | ((uintptr_t)sp->adam_v) |
+                 ((uintptr_t)sp->learn_heads)) &
                 15) == 0,
-               PM_E_ARG, "pm_selfplay: w_opp / w_B / prios / per_work must be 16-byte aligned");
+               PM_E_ARG, "pm_selfplay: w_opp / w_B / prios / per_work / paramsB / paramsT / adam_m / adam_v / "
+                         "learn_heads must be 16-byte aligned");
     PM_REQUIRE(sp->env.speed_scale_every > 0 && sp->target_update_interval > 0 && sp->beta_frames > 0, PM_E_ARG,
                "pm_selfplay: zero interval");
     return PM_OK;

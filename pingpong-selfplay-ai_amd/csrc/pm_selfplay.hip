@@ -263,7 +263,8 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
     int onew = o;
     if (valid) {
         // memory.push((oB, aB, rB, nB, done)) (:243, :56-63)
-        const int64_t slot = (pos + i) % sp.cap;
+        int64_t slot = pos + i;  // pos < cap and i < n <= cap: one conditional subtract is the modulo
+        if (slot >= sp.cap) slot -= sp.cap;  // (a per-lane 64-bit % is a ~100-instruction expansion)
         float4* row = reinterpret_cast<float4*>(sp.trans + slot * PM_TRANS_F);
         row[0] = make_float4(oB[0], oB[1], oB[2], oB[3]);
         row[1] = make_float4(oB[4], oB[5], oB[6], rB);
@@ -480,7 +481,8 @@ struct LearnSmem {
     uint32_t hkey[512];          // open-addressing set of sampled indices (last-duplicate-wins)
     int hwin[512];
     float red[16][8];
-    long long cnt[16][6];
+    long long cnt[16][6];        // per-wave episode counters of the rollout (phase 0)
+    long long ctot[6];           // their sums (phase 1)
     int plist[PM_MAX_BATCH];     // samples whose row is in this step's push range, per wave slot
     int pcnt[16];
     ApplySmem ap;
@@ -618,7 +620,12 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     if (t < 6) {
         long long s = 0;
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][t];
-        sm.cnt[0][t] = s;  // read after the next barrier
+        sm.ctot[t] = s;  // read after the next barrier
+    }
+    if (sp.fuse_apply && t == kLearn - 1) {  // the per-episode epsilon decay (:261) beside the forward
+        long long s = 0;                     // (same sum, same order as thread 0's ctot[0])
+        for (int w = 0; w < 16; ++w) s += sm.cnt[w][0];
+        sm.ap.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)(float)s);
     }
     if (train) {  // rows in the push range: one 32-row tile per wave (s rows then s' rows)
         int pre[5] = {0, 0, 0, 0, 0};
@@ -657,15 +664,13 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     for (int w = 1; w < 16; ++w) wmax = fmaxf(wmax, sm.red[w][0]);
     __syncthreads();
     PM_STAMP(2);
-    ep_fin = sm.cnt[0][0];
-    if (sp.fuse_apply && t == kLearn - 1)  // idle in phase 2: the per-episode epsilon decay (:261)
-        sm.ap.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)(float)ep_fin);
+    ep_fin = sm.ctot[0];
     if (t == 0) {  // rollout bookkeeping (:245-249)
         c->ep_step = ep_fin;
         c->episodes = cs.episodes + ep_fin;
-        c->ep_A = cs.ep_A + sm.cnt[0][1]; c->win_A = cs.win_A + sm.cnt[0][2];
-        c->ep_P = cs.ep_P + sm.cnt[0][3]; c->win_P = cs.win_P + sm.cnt[0][4];
-        c->reward_B = cs.reward_B + (double)sm.cnt[0][5];
+        c->ep_A = cs.ep_A + sm.ctot[1]; c->win_A = cs.win_A + sm.ctot[2];
+        c->ep_P = cs.ep_P + sm.ctot[3]; c->win_P = cs.win_P + sm.ctot[4];
+        c->reward_B = cs.reward_B + (double)sm.ctot[5];
     }
 
     // ---- phase 2: double-DQN targets, loss, priorities, bias grads

@@ -10,12 +10,15 @@ push + proportional sample, double-DQN update with target net, Adam), weak-scale
 A step = one vector step: every arena on every rank advances one env step and every rank runs one
 PER update of batch 256. value = total env-steps (all ranks) / max-over-ranks wall time of K steps.
 Rank 0 prints one JSON line. Also reported:
-  roofline      the dominant kernel, k_act_sp (both players' QNet forwards on the matrix cores, plus
-                the PER sample blocks), timed with HIP events on the stream it runs on, around every
-                10th step of the timed region (the others run the uninstrumented step): FP32 FLOP/s
-                vs the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per launch from the
+  roofline      the matrix-core act kernel of the production step, k_act_sp(PM_ACT_B): modelB's QNet
+                forward for every arena + eps-greedy, plus the PER sample blocks (the opponents' act
+                rides in the learner's launch), timed with HIP events on the stream it runs on around
+                every 10th step of the timed region (the others run uninstrumented): FP32 FLOP/s vs
+                the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per launch from the
                 committed counter profile (profiles/r1_pmc.json, same workload), null without it
   env_roofline  k_env (env tick + replay push + bookkeeping, 282 algorithmic B / env-step) vs 8 TB/s
+  act_full_roofline  k_act_sp with both players' act in one launch (PM_ACT_ALL), back to back after the
+                timed region (N=1 only)
   env_step_roofline  K1 (pm_env_step, autoreset of done arenas) alone at the same n: 203 B / env-step
                 vs 8 TB/s, timed over graph-replayed back-to-back launches (N=1 only)
   cpu_baseline  the oracle's CPU port of the same vector step, 1 core, bounded sample (N=1 only)
@@ -37,7 +40,7 @@ ENV_KW = dict(paddle_width=0.2, paddle_speed=0.03, max_score=3, enable_spin=True
               restitution=1, friction=0.6, ball_mass=1.0, world_ball_radius=0.03, ball_speed_range=[0.03, 0.05],
               spin_range=[-5, 5], ball_angle_intervals=[[-60, -30], [30, 60]], speed_scale_every=1,
               speed_increment=0.1)  # config.yaml env (render keys dropped)
-FLOP_PER_ARENA = 2 * 2 * (7 * 64 + 64 * 64 + 64 * 4)  # two QNet forwards (MACs x 2)
+FLOP_PER_ARENA = 2 * (7 * 64 + 64 * 64 + 64 * 4)  # one QNet forward (MACs x 2): side B, the production act kernel
 ENV_BYTES = 203  # K1 algorithmic bytes per env-step
 # k_env (self-play tick): state 7x8 + 3x4 read and written (136), actions 2, opp 4 + ep_reward 4 read and
 # written (16), replay row 64 + priority 4 + PER leaf 4 written, next observations 2x28 written
@@ -100,6 +103,27 @@ def time_env_step(n, per_graph=50, replays=20):
             "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic("k_env_step"),
             "avg_us": round(t * 1e6, 2), "bytes_per_env_step": ENV_BYTES, "n": n,
             "timing": f"HIP events over {replays} graph replays x {per_graph} launches, autoreset='done'"}
+
+
+def time_act_full(L, launches=50):
+    """k_act_sp with both players in one launch (PM_ACT_ALL: what the plain step and pm_selfplay_act
+    run), back to back on the learner's state after the timed region (idempotent: same observations,
+    same actions), HIP events on its stream: both QNet forwards per arena, 19 200 FLOP."""
+    from pongmi import _lib
+    for _ in range(5):
+        L.act(_lib.PM_ACT_ALL)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(launches):
+        L.act(_lib.PM_ACT_ALL)
+    e1.record()
+    e1.synchronize()
+    t = e0.elapsed_time(e1) * 1e-3 / launches
+    achieved = L.n * 2 * FLOP_PER_ARENA / t / 1e12
+    return {"bound": "mfma", "kernel": "k_act_sp (PM_ACT_ALL: both players, no PER sample)",
+            "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "avg_us": round(t * 1e6, 2),
+            "flop_per_arena": 2 * FLOP_PER_ARENA, "n": L.n, "timing": f"HIP events over {launches} back-to-back launches"}
 
 
 def cpu_baseline(n, seconds=12.0):
@@ -277,6 +301,7 @@ def main():
         return run_rnn(args, dist, rank, world)
     args.arenas = args.arenas or 65536
     args.pool = 8 if args.pool is None else args.pool
+    from pongmi import _lib
     from pongmi.selfplay import SelfPlayLearner
 
     sdB, sdA = synthetic_qnet(1), synthetic_qnet(2)
@@ -290,11 +315,13 @@ def main():
         if ev is None:  # the production path: the overlapped vector step (L.step)
             L.step()
             return
-        # instrumented step: the same kernels, bracketed for the per-kernel rooflines (both players'
-        # act in one k_act_sp launch; the learner launch computes the next step's opponent act, as
-        # in the production step)
+        # instrumented step: the production step's kernels (pm_selfplay_step_overlap), bracketed for
+        # the per-kernel rooflines: k_act_sp side B (+ PER sample blocks), k_env, then the learner
+        # launch that also acts for the next step's opponents
+        if not L._aA_ready:
+            L.act(_lib.PM_ACT_A)
         ev[0].record()
-        L.act()
+        L.act(_lib.PM_ACT_B)
         ev[1].record()
         L.env_step()
         ev[2].record()
@@ -344,8 +371,8 @@ def main():
                        "arenas_per_gpu": args.arenas, "global_arenas": args.arenas * world,
                        "pool": args.pool, "batch": args.batch, "updates_per_vector_step": 1,
                        "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)"},
-            "roofline": {"bound": "mfma", "kernel": "k_act_sp", "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; "
-                                                                          "dense FP32 matrix peak 157.3 TF)",
+            "roofline": {"bound": "mfma", "kernel": "k_act_sp (PM_ACT_B: modelB's act + the PER sample blocks)",
+                         "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": pmc_traffic("k_act_sp"),
                          "avg_us": round(act_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
@@ -357,6 +384,7 @@ def main():
                         "last_loss": c["last_loss"]},
         }
         if world == 1:
+            out["act_full_roofline"] = time_act_full(L)
             out["env_step_roofline"] = time_env_step(args.arenas)
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline(args.arenas, args.cpu_seconds)

@@ -336,7 +336,7 @@ __global__ __launch_bounds__(kBlock) void k_sp_init(const pm_selfplay sp) {
 
 // ------------------------------------------------------------------------------------ learner
 // ------------------------------------------------------------------------------------ apply
-struct ApplySmem {  // the 520-float arrays are padded to whole 64-float global_load_lds chunks
+struct __attribute__((aligned(16))) ApplySmem {  // 520-float arrays padded to whole 1 KB (16-B lane) global_load_lds chunks
     float hp[pad256(PM_QNET_NHEAD)];   // modelB head parameters (after the optimizer step)
     float tmu[pad256(PM_QNET_NHEAD)];  // targetB head parameters (mu used)
     float m[pad256(PM_QNET_NHEAD)], v[pad256(PM_QNET_NHEAD)];  // Adam moments
@@ -842,13 +842,20 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
 }
 
 // ------------------------------------------------------------------------------------ Adam + commit
+// The scalar prologue (both noises, the bias-correction and epsilon-decay pows) runs while the
+// loads are in flight: every thread reads the all-reduced updated flag and episode count itself.
 __global__ __launch_bounds__(kLearn) void k_adam(const pm_selfplay sp) {
     __shared__ ApplySmem sm;
+    const int t = threadIdx.x;
     const pm_ctrl cs = *sp.ctrl;
     load_apply_inputs(sp, sm, true);
-    if (threadIdx.x == 0) adam_consts(sp, cs.train_steps + 1, sm);
+    const float D = sp.grad[kGradN], upd = sp.grad[kGradN + 1];  // finished episodes | updated flag (all shards)
+    const int64_t ts = cs.train_steps + (upd > 0.5f ? 1 : 0);
+    gen_both_noises_on(sp, sm, cs.step + 1, (uint64_t)ts + 1, kLearn / 2);
+    if (t >= kLearn - 2) adam_const_lane(sp, cs.train_steps + 1, sm, t - (kLearn - 2));
+    if (t == kLearn / 2 - 1) sm.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)D);  // as apply_update's D
     __syncthreads();
-    apply_update(sp, sm, cs, false);
+    apply_update(sp, sm, cs, true);
 }
 
 // pm_selfplay_prepare: features + acting weights of the current step + next update's heads

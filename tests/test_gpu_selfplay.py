@@ -310,3 +310,43 @@ def test_overlapped_step_is_bitwise_identical(golden):
                  "learn_heads", "per_work", "idx", "isw", "aA", "aB", "obsA", "obsB", "ep_reward"):
         assert torch.equal(getattr(A, name), getattr(B, name)), name
     assert A.counters() == B.counters()
+
+
+def test_sharded_world2_overlap_equals_plain(golden):
+    """world = 2 on one device (rank-specific arenas / replay, one summed gradient): the overlapped
+    sharded step (act B -> env -> learn with the next side-A act -> all-reduce -> k_adam) equals the
+    plain sharded step (rollout -> learn -> all-reduce -> k_adam) bit for bit, and the two replicas'
+    networks stay identical."""
+    from pongmi import _lib
+
+    def make(rank, overlap):
+        return _learner(golden, n=2048, batch=256, cap=8192, seed=13, rank=rank, world=2, allreduce=lambda t: None,
+                        overlap=overlap)
+
+    ov = [make(0, True), make(1, True)]
+    pl = [make(0, False), make(1, False)]
+    for _ in range(14):
+        for L in ov:
+            if not L._aA_ready:
+                L.act(_lib.PM_ACT_A)
+            L.act(_lib.PM_ACT_B)
+            L.env_step()
+            L.learn(act_next=True)
+        for L in pl:
+            L.rollout()
+            L.learn()
+        for pair in (ov, pl):
+            g = pair[0].grad + pair[1].grad  # the all-reduce (SUM)
+            for L in pair:
+                L.grad.copy_(g)
+                L.apply()
+    torch.cuda.synchronize()
+    for r in range(2):
+        for name in ("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "opp", "w_B",
+                     "learn_heads", "per_work", "idx", "isw", "aB", "obsA", "obsB", "ep_reward"):
+            assert torch.equal(getattr(ov[r], name), getattr(pl[r], name)), (r, name)
+        assert ov[r].counters() == pl[r].counters()
+    for name in ("paramsB", "paramsT", "adam_m", "adam_v", "w_B", "learn_heads"):
+        assert torch.equal(getattr(ov[0], name), getattr(ov[1], name)), name
+    assert not torch.equal(ov[0].f64, ov[1].f64)  # rank-specific arenas
+    assert ov[0].counters()["train_steps"] == 14

@@ -415,16 +415,13 @@ __device__ __forceinline__ void gen_both_noises_on(const pm_selfplay& sp, ApplyS
 
 // optimizer.step() (:161) on the shard-summed grads, target sync (:166-168), epsilon decay (:261),
 // replay / step counters, then derive_weights for the next step. All inputs in LDS (sm) and `cs`
-// (the control block as the kernel found it); only stores go to global memory. `early`: the fused
-// learner already drew both noises into sm and computed sm.eps_next (the same values) off its
-// critical path.
-__device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& sm, const pm_ctrl& cs, bool early) {
+// (the control block as the kernel found it); only stores go to global memory. Both noises are in
+// sm.nact / sm.ntrain and sm.eps_next holds eps * decay^D already (drawn / computed by idle waves
+// while the callers' loads were in flight). Two parts: apply_adam (per-thread, no barrier: the fused
+// learner runs it beside the sum-tree's level-2 refresh) and apply_finish (behind a barrier).
+__device__ __forceinline__ void apply_adam(const pm_selfplay& sp, ApplySmem& sm) {
     const int t = threadIdx.x, nt = blockDim.x;
-    const bool train = sm.g[kGradN + 1] > 0.5f;
-    const int64_t ts = cs.train_steps + (train ? 1 : 0);
-    const uint64_t step = cs.step;
-    if (!early) gen_both_noises(sp, sm, step + 1, (uint64_t)ts + 1);
-    if (train) {
+    if (sm.g[kGradN + 1] > 0.5f) {
         const float step_size = sm.ak[0], bc2s = sm.ak[1];  // adam_consts, published before a barrier
         for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
             const float g = sm.g[k] / (float)sp.world;
@@ -439,7 +436,12 @@ __device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& s
             sm.hp[k] = p;
         }
     }
-    __syncthreads();
+}
+__device__ __forceinline__ void apply_finish(const pm_selfplay& sp, ApplySmem& sm, const pm_ctrl& cs) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    const bool train = sm.g[kGradN + 1] > 0.5f;
+    const int64_t ts = cs.train_steps + (train ? 1 : 0);
+    const uint64_t step = cs.step;
     PM_STAMP(20);
     if (train && ts % sp.target_update_interval == 0) {  // targetB.load_state_dict(modelB) (:166-168)
         for (int k = t; k < PM_QNET_NHEAD; k += nt) sm.tmu[k] = sm.hp[k];
@@ -453,8 +455,7 @@ __device__ __forceinline__ void apply_update(const pm_selfplay& sp, ApplySmem& s
     PM_STAMP(21);
     if (t == 0) {
         pm_ctrl* c = sp.ctrl;
-        const double D = (double)sm.g[kGradN];  // finished episodes (all shards)
-        const double e = early ? sm.eps_next : cs.epsilon * pow(sp.epsilon_decay, D);  // per-episode decay (:261)
+        const double e = sm.eps_next;  // eps * decay^D, D = finished episodes (all shards) (:261)
         c->epsilon = e > sp.min_epsilon ? e : sp.min_epsilon;
         if (train) { c->train_steps = ts; c->frame_idx = cs.frame_idx + 1; }
         c->pos = (cs.pos + sp.n) % sp.cap;
@@ -821,7 +822,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     __syncthreads();
     PM_STAMP(5);
     for (int k = t; k < kGradN + 2; k += kLearn) sp.grad[k] = sm.ap.g[k];
-    // ---- phase 5: level-2 nodes over the refreshed sub-blocks
+    // ---- phase 5: level-2 nodes over the refreshed sub-blocks; beside them, the fused optimizer step
+    if (sp.fuse_apply) apply_adam(sp, sm.ap);
     if (act && sm.hwin[slot] == t) {
         const int64_t ch = id / PER_CHUNK;
         tree.chunk[ch] = per_chunk_sum(tree, ch);
@@ -836,7 +838,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     PM_STAMP(6);
     if (sp.fuse_apply) {  // unsharded: no all-reduce between the gradient and the optimizer step
         __syncthreads();
-        apply_update(sp, sm.ap, cs, true);
+        apply_finish(sp, sm.ap, cs);
     }
     PM_STAMP(7);
 }
@@ -855,7 +857,9 @@ __global__ __launch_bounds__(kLearn) void k_adam(const pm_selfplay sp) {
     if (t >= kLearn - 2) adam_const_lane(sp, cs.train_steps + 1, sm, t - (kLearn - 2));
     if (t == kLearn / 2 - 1) sm.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)D);  // as apply_update's D
     __syncthreads();
-    apply_update(sp, sm, cs, true);
+    apply_adam(sp, sm);
+    __syncthreads();
+    apply_finish(sp, sm, cs);
 }
 
 // pm_selfplay_prepare: features + acting weights of the current step + next update's heads

@@ -383,12 +383,14 @@ __device__ __forceinline__ void derive_weights(const pm_selfplay& sp, ApplySmem&
     float* lh = sp.learn_heads;
     // the three folds are independent: one pass on three 260-thread groups, one barrier, then the
     // three fragment writes
-    if (t < 260) {
-        fold_heads_from(sm.hp, nullptr, sm.nact, PM_FOLD_TRAIN_FRESH, sm.heads[0], sp.paramsB + PM_QNET_EPS_OFF, t, 260);
-    } else if (t < 520) {
-        fold_heads_from(sm.hp, nullptr, sm.ntrain, PM_FOLD_TRAIN_FRESH, sm.heads[1], lh + 528, t - 260, 260);
-    } else if (t < 780) {
-        fold_heads_from(sm.tmu, nullptr, nullptr, PM_FOLD_EVAL, sm.heads[2], nullptr, t - 520, 260);
+    // (threads 256..1023: in the fused learner threads < 256 are still refreshing level-2 tree nodes)
+    const int g = (t - 256) >> 8, u = (t - 256) & 255;
+    if (t >= 256 && g == 0) {
+        fold_heads_from(sm.hp, nullptr, sm.nact, PM_FOLD_TRAIN_FRESH, sm.heads[0], sp.paramsB + PM_QNET_EPS_OFF, u, 256);
+    } else if (t >= 256 && g == 1) {
+        fold_heads_from(sm.hp, nullptr, sm.ntrain, PM_FOLD_TRAIN_FRESH, sm.heads[1], lh + 528, u, 256);
+    } else if (t >= 256 && g == 2) {
+        fold_heads_from(sm.tmu, nullptr, nullptr, PM_FOLD_EVAL, sm.heads[2], nullptr, u, 256);
     }
     __syncthreads();
     write_head_frags(sm.heads[0], sp.w_B);
@@ -419,23 +421,24 @@ __device__ __forceinline__ void gen_both_noises_on(const pm_selfplay& sp, ApplyS
 // sm.nact / sm.ntrain and sm.eps_next holds eps * decay^D already (drawn / computed by idle waves
 // while the callers' loads were in flight). Two parts: apply_adam (per-thread, no barrier: the fused
 // learner runs it beside the sum-tree's level-2 refresh) and apply_finish (behind a barrier).
+// torch.optim.Adam (single-tensor path) on head parameter k with gradient g (summed over shards).
+__device__ __forceinline__ void adam_one(const pm_selfplay& sp, ApplySmem& sm, int k, float gsum) {
+    const float step_size = sm.ak[0], bc2s = sm.ak[1];  // adam_consts, published before a barrier
+    const float g = gsum / (float)sp.world;
+    float m = sm.m[k], v = sm.v[k], p = sm.hp[k];
+    m = m + (float)(1.0 - sp.beta1) * (g - m);                  // exp_avg.lerp_(grad, 1-beta1)
+    v = v * (float)sp.beta2 + (float)(1.0 - sp.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
+    const float denom = sqrtf(v) / bc2s + (float)sp.adam_eps;
+    p = p - step_size * (m / denom);
+    sp.paramsB[PM_QNET_HEAD_OFF + k] = p;
+    sp.adam_m[k] = m;
+    sp.adam_v[k] = v;
+    sm.hp[k] = p;
+}
 __device__ __forceinline__ void apply_adam(const pm_selfplay& sp, ApplySmem& sm) {
     const int t = threadIdx.x, nt = blockDim.x;
-    if (sm.g[kGradN + 1] > 0.5f) {
-        const float step_size = sm.ak[0], bc2s = sm.ak[1];  // adam_consts, published before a barrier
-        for (int k = t; k < PM_QNET_NHEAD; k += nt) {  // torch.optim.Adam, single-tensor path
-            const float g = sm.g[k] / (float)sp.world;
-            float m = sm.m[k], v = sm.v[k], p = sm.hp[k];
-            m = m + (float)(1.0 - sp.beta1) * (g - m);                  // exp_avg.lerp_(grad, 1-beta1)
-            v = v * (float)sp.beta2 + (float)(1.0 - sp.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
-            const float denom = sqrtf(v) / bc2s + (float)sp.adam_eps;
-            p = p - step_size * (m / denom);
-            sp.paramsB[PM_QNET_HEAD_OFF + k] = p;
-            sp.adam_m[k] = m;
-            sp.adam_v[k] = v;
-            sm.hp[k] = p;
-        }
-    }
+    if (sm.g[kGradN + 1] > 0.5f)
+        for (int k = t; k < PM_QNET_NHEAD; k += nt) adam_one(sp, sm, k, sm.g[k]);
 }
 __device__ __forceinline__ void apply_finish(const pm_selfplay& sp, ApplySmem& sm, const pm_ctrl& cs) {
     const int t = threadIdx.x, nt = blockDim.x;
@@ -767,25 +770,29 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             for (int w = 0; w < 16; ++w) g += sm.u.gpart[w][t];
             const int row = t >> 6, col = t & 63;
             float* gs = sm.ap.g;
-            if (row == 0) {
-                gs[col] = g;                                                   // fc_V.weight_mu
-                gs[65 + col] = g * sm.eps_tr[P_VWEP - PM_QNET_EPS_OFF + col];  // fc_V.weight_sigma
-            } else {
-                const int a = row - 1;
-                gs[130 + a * 64 + col] = g;                                               // fc_A.weight_mu
-                gs[325 + a * 64 + col] = g * sm.eps_tr[P_AWEP - PM_QNET_EPS_OFF + a * 64 + col];  // fc_A.weight_sigma
+            const int a = row - 1;  // fc_V.weight_mu / _sigma, or fc_A.weight_mu / _sigma (row a)
+            const int kmu = row == 0 ? col : 130 + a * 64 + col, ksg = row == 0 ? 65 + col : 325 + a * 64 + col;
+            const float gsg = g * sm.eps_tr[row == 0 ? P_VWEP - PM_QNET_EPS_OFF + col
+                                                     : P_AWEP - PM_QNET_EPS_OFF + a * 64 + col];
+            gs[kmu] = g;
+            gs[ksg] = gsg;
+            if (sp.fuse_apply) {  // the optimizer step on the two parameters this thread owns
+                adam_one(sp, sm.ap, kmu, g);
+                adam_one(sp, sm.ap, ksg, gsg);
             }
         } else if (t < 260) {  // dL/db_mu = sum_j coef_j
             const int k = t - 256;
             float g = 0.f;
             for (int w = 0; w < 16; ++w) g += sm.red[w][3 + k];
             float* gs = sm.ap.g;
-            if (k == 0) {
-                gs[64] = g;                                             // fc_V.bias_mu
-                gs[129] = g * sm.eps_tr[P_VBEP - PM_QNET_EPS_OFF];      // fc_V.bias_sigma
-            } else {
-                gs[322 + k - 1] = g;                                    // fc_A.bias_mu
-                gs[517 + k - 1] = g * sm.eps_tr[P_ABEP - PM_QNET_EPS_OFF + k - 1];  // fc_A.bias_sigma
+            // fc_V.bias_mu / _sigma, or fc_A.bias_mu / _sigma (k - 1)
+            const int kmu = k == 0 ? 64 : 322 + k - 1, ksg = k == 0 ? 129 : 517 + k - 1;
+            const float gsg = g * sm.eps_tr[k == 0 ? P_VBEP - PM_QNET_EPS_OFF : P_ABEP - PM_QNET_EPS_OFF + k - 1];
+            gs[kmu] = g;
+            gs[ksg] = gsg;
+            if (sp.fuse_apply) {
+                adam_one(sp, sm.ap, kmu, g);
+                adam_one(sp, sm.ap, ksg, gsg);
             }
         }
         PM_STAMP(8); PM_STAMP_T(9, 960);
@@ -822,8 +829,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     __syncthreads();
     PM_STAMP(5);
     for (int k = t; k < kGradN + 2; k += kLearn) sp.grad[k] = sm.ap.g[k];
-    // ---- phase 5: level-2 nodes over the refreshed sub-blocks; beside them, the fused optimizer step
-    if (sp.fuse_apply) apply_adam(sp, sm.ap);
+    // ---- phase 5: level-2 nodes over the refreshed sub-blocks; beside them (fused) the target sync
+    // and the three head folds of derive_weights, which run on threads 256.. (level 2's are < 256)
     if (act && sm.hwin[slot] == t) {
         const int64_t ch = id / PER_CHUNK;
         tree.chunk[ch] = per_chunk_sum(tree, ch);
@@ -836,10 +843,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         }
     }
     PM_STAMP(6);
-    if (sp.fuse_apply) {  // unsharded: no all-reduce between the gradient and the optimizer step
-        __syncthreads();
-        apply_finish(sp, sm.ap, cs);
-    }
+    if (sp.fuse_apply) apply_finish(sp, sm.ap, cs);  // unsharded: Adam ran with the gradients (phase 4)
     PM_STAMP(7);
 }
 

@@ -17,8 +17,8 @@ Rank 0 prints one JSON line. Also reported:
                 the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per launch from the
                 committed counter profile (profiles/r1_pmc.json, same workload), null without it
   env_roofline  k_env (env tick + replay push + bookkeeping, 282 algorithmic B / env-step) vs 8 TB/s
-  act_full_roofline  k_act_sp with both players' act in one launch (PM_ACT_ALL), back to back after the
-                timed region (N=1 only)
+  act_full_roofline  k_act_sp with both players' act (+ the PER sample blocks) in one launch
+                (PM_ACT_ALL), back to back after the timed region (N=1 only)
   env_step_roofline  K1 (pm_env_step, autoreset of done arenas) alone at the same n: 203 B / env-step
                 vs 8 TB/s, timed over graph-replayed back-to-back launches (N=1 only)
   cpu_baseline  the oracle's CPU port of the same vector step, 1 core, bounded sample (N=1 only)
@@ -51,7 +51,8 @@ PEAK_HBM_GBS = 8000.0
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 counter profile, or None."""
+    """HBM bytes per launch of `kernel` (`name`, or `name@grid` for one of its launch grids) from the
+    committed rocprofv3 counter profile, or None."""
     path = os.path.join(ROOT, "profiles", "r1_pmc.json")
     try:
         with open(path) as fh:
@@ -107,8 +108,9 @@ def time_env_step(n, per_graph=50, replays=20):
 
 def time_act_full(L, launches=50):
     """k_act_sp with both players in one launch (PM_ACT_ALL: what the plain step and pm_selfplay_act
-    run), back to back on the learner's state after the timed region (idempotent: same observations,
-    same actions), HIP events on its stream: both QNet forwards per arena, 19 200 FLOP."""
+    run, PER sample blocks included), back to back on the learner's state after the timed region
+    (idempotent: same observations, same sample, same actions), HIP events on its stream: both QNet
+    forwards per arena, 19 200 FLOP."""
     from pongmi import _lib
     for _ in range(5):
         L.act(_lib.PM_ACT_ALL)
@@ -120,10 +122,11 @@ def time_act_full(L, launches=50):
     e1.synchronize()
     t = e0.elapsed_time(e1) * 1e-3 / launches
     achieved = L.n * 2 * FLOP_PER_ARENA / t / 1e12
-    return {"bound": "mfma", "kernel": "k_act_sp (PM_ACT_ALL: both players, no PER sample)",
+    return {"bound": "mfma", "kernel": "k_act_sp (PM_ACT_ALL: both players + the PER sample blocks)",
             "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "avg_us": round(t * 1e6, 2),
-            "flop_per_arena": 2 * FLOP_PER_ARENA, "n": L.n, "timing": f"HIP events over {launches} back-to-back launches"}
+            "flop_per_arena": 2 * FLOP_PER_ARENA, "n": L.n, "traffic": pmc_traffic("k_act_sp"),
+            "timing": f"HIP events over {launches} back-to-back launches"}
 
 
 def cpu_baseline(n, seconds=12.0):
@@ -374,7 +377,8 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "k_act_sp (PM_ACT_B: modelB's act + the PER sample blocks)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": pmc_traffic("k_act_sp"),
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         "traffic": pmc_traffic(f"k_act_sp@{((args.batch + 3) // 4 + (args.arenas + 255) // 256) * 256}"),
                          "avg_us": round(act_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
             "env_roofline": {"bound": "hbm", "kernel": "k_env", "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS,
                              "unit": "GB/s", "frac": round(env_gbs / PEAK_HBM_GBS, 4),

@@ -13,7 +13,7 @@ Rank 0 prints one JSON line. Also reported:
   roofline      the matrix-core act kernel of the production step, k_act_sp(PM_ACT_B): modelB's QNet
                 forward for every arena + eps-greedy, plus the PER sample blocks (the opponents' act
                 rides in the learner's launch), timed with HIP events on the stream it runs on around
-                every 10th step of the timed region (the others run uninstrumented): FP32 FLOP/s vs
+                every 20th step of the timed region (the others run uninstrumented): FP32 FLOP/s vs
                 the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per launch from the
                 committed counter profile (profiles/r1_pmc.json, same workload), null without it
   env_roofline  k_env (env tick + replay push + bookkeeping, 282 algorithmic B / env-step) vs 8 TB/s
@@ -46,7 +46,7 @@ ENV_BYTES = 203  # K1 algorithmic bytes per env-step
 # written (16), replay row 64 + priority 4 + PER leaf 4 written, next observations 2x28 written
 SP_ENV_BYTES = 136 + 2 + 16 + 72 + 56
 PEAK_FP32_TFLOPS = 157.3
-INSTR = 10  # one instrumented (event-bracketed) step per INSTR timed steps
+INSTR = 20  # one instrumented (event-bracketed) step per INSTR timed steps (events cost GPU time on ROCm)
 PEAK_HBM_GBS = 8000.0
 
 

@@ -130,7 +130,8 @@ __device__ __forceinline__ void batch_row_fwd(const pm_selfplay& sp, const float
 
 // Rows of the batch whose replay row is NOT in this step's push range are stable while k_env runs:
 // k_env's last ceil(2B/128) blocks compute them (one tile per wave) into hfeat [B][80] (features
-// of s | Q_B(s) 0..2, Q_B(s') 4..6, Q_T(s') 8..10 at 64..); k_learn computes the rest.
+// of s | Q_B(s) 0..2, r at 3, Q_B(s') 4..6, action|done bits at 7, Q_T(s') 8..10 at 64..); k_learn
+// computes the rest. Carrying r and the bits here spares k_learn a load that depends on idx.
 __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f) {
     __shared__ __attribute__((aligned(16))) float lw[kLwFloats];
     __shared__ __attribute__((aligned(16))) float hf[2][264];
@@ -161,7 +162,10 @@ __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f) {
     }
     if (h == 0) {
         if (!nxt) {
+            const float* tr = sp.trans + id * PM_TRANS_F;
             row[64] = qb[0]; row[65] = qb[1]; row[66] = qb[2];
+            row[67] = tr[7];   // reward
+            row[71] = tr[15];  // action | done << 8 (float bits)
         } else {
             row[68] = qb[0]; row[69] = qb[1]; row[70] = qb[2];
             row[72] = qt[0]; row[73] = qt[1]; row[74] = qt[2];
@@ -555,14 +559,6 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     for (int b = t + kLearn; b < nbr; b += kLearn)  // n > 256 * 1024 arenas only
 #pragma unroll
         for (int k = 0; k < 6; ++k) part[k] += sp.partials[(size_t)b * 8 + k];
-    // first uses: the replay rows of the sample (dependent on idx: the second round trip)
-    float rwd = 0.f;
-    int bits = 0;
-    if (t < B) {
-        const float* tr = sp.trans + id_l * PM_TRANS_F;
-        rwd = tr[7];
-        bits = __float_as_int(tr[15]);
-    }
     // fused: the optimizer's scalar prologue on waves with slack in this load phase (they are not
     // on the dependent idx -> replay-row path of waves 0-3): the Adam bias corrections (two fp64
     // pow) on the last thread, both NoisyNet draws of the apply on the upper half of the block
@@ -597,7 +593,6 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     PM_STAMP(31);
     asm volatile("" ::"v"(hv[0]), "v"(hv[19]));
     PM_STAMP(32);
-    asm volatile("" ::"v"(rwd), "v"(bits));
     PM_STAMP(33);
 #endif
 #pragma unroll
@@ -655,7 +650,9 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
                 }
                 if (h == 0) {
                     if (!nxt) {
+                        const float* tr = sp.trans + sm.sidx[j] * PM_TRANS_F;  // written by this step's k_env
                         sm.qv[j][0] = qb[0]; sm.qv[j][1] = qb[1]; sm.qv[j][2] = qb[2];
+                        sm.qv[j][3] = tr[7]; sm.qv[j][7] = tr[15];
                     } else {
                         sm.qv[j][4] = qb[0]; sm.qv[j][5] = qb[1]; sm.qv[j][6] = qb[2];
                         sm.qv[j][8] = qt[0]; sm.qv[j][9] = qt[1]; sm.qv[j][10] = qt[2];
@@ -682,6 +679,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     float cf[4] = {0.f, 0.f, 0.f, 0.f};
     int slot = 0;
     if (act) {
+        const float rwd = sm.qv[t][3];
+        const int bits = __float_as_int(sm.qv[t][7]);
         const int a = bits & 0xff, dn = (bits >> 8) & 1;
         const float qs[3] = {sm.qv[t][0], sm.qv[t][1], sm.qv[t][2]};
         const float qn[3] = {sm.qv[t][4], sm.qv[t][5], sm.qv[t][6]};

@@ -512,6 +512,9 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     if (blockIdx.x > 0) {
+        // the learner's load phase is latency-bound under these blocks' staging burst; they have slack
+        // (the learner is the longer of the two), so they start after its loads are in flight
+        __builtin_amdgcn_s_sleep(127);
         const ActGrid g{sp.n, sp.n_pool + 1, chunkA, chunkP, 0};
         const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
         act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,

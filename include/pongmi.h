@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 6
+#define PM_ABI_VERSION 7
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -336,7 +336,7 @@ typedef struct pm_ctrl {
     int64_t win_A, ep_A, win_P, ep_P; /* wins / episodes of B vs modelA and vs pool (:247-248) */
     double reward_B;         /* sum of rB over finished episodes                          */
     int32_t status;          /* error bits                                               */
-    int32_t _pad;
+    int32_t max_bits;        /* pm_selfplay_commit scratch: float bits of max(prios); 0 between steps */
 } pm_ctrl;
 
 /* One shard of the batched self-play learner: every buffer is a device pointer, [n] = per arena. */
@@ -429,6 +429,29 @@ int pm_selfplay_step(const pm_selfplay* sp, void* stream);
 int pm_selfplay_act_part(const pm_selfplay* sp, int32_t part, void* stream);
 int pm_selfplay_learn_act(const pm_selfplay* sp, void* stream);
 int pm_selfplay_step_overlap(const pm_selfplay* sp, void* stream);
+
+/* Replay ratio: U >= 1 double-DQN updates per vector step. The reference trains once per env step
+ * (train_iterative.py:243-244), i.e. once per pushed transition; U = n keeps that ratio for n arenas.
+ *   update 0 (mode PM_UPD_FIRST) trains on the batch k_act_sp drew with this step's push pending, as
+ *     the U = 1 step does, and carries the step's episode counters and epsilon decay (:245-261);
+ *   updates 1..U-1 draw their batch with pm_selfplay_resample (PER sample + batch forward over the
+ *     replay as this step's push left it; frame_idx, hence beta and the Philox draw, advance per
+ *     update, :136-137) and run pm_selfplay_learn_ex / _apply_ex in mode 0;
+ *   pm_selfplay_commit closes the step: max_prio = max(prios) over the replay (memory.push stores
+ *     prios.max(), :57 — U * batch >= n scatters can lower the array maximum below the running
+ *     maximum the U = 1 step tracks), the sum tree's nodes over the next push range, pos/size/step.
+ * PM_UPD_FIRST | PM_UPD_LAST is the U = 1 update (pm_selfplay_learn / pm_selfplay_apply).
+ * pm_selfplay_step_multi = act_part(B) + env + learn_ex(FIRST, side-A act) + (U - 1) x [resample +
+ * learn_ex(0)] + commit, unsharded, under step_overlap's contract (sp->aA holds side-A actions for
+ * the current observations); U = 1 is pm_selfplay_step_overlap. Sharded callers run the same sequence
+ * with an all-reduce of sp->grad and pm_selfplay_apply_ex after every learn_ex. */
+#define PM_UPD_FIRST 1
+#define PM_UPD_LAST 2
+int pm_selfplay_learn_ex(const pm_selfplay* sp, int32_t mode, int32_t with_act, void* stream);
+int pm_selfplay_apply_ex(const pm_selfplay* sp, int32_t mode, void* stream);
+int pm_selfplay_resample(const pm_selfplay* sp, void* stream);
+int pm_selfplay_commit(const pm_selfplay* sp, void* stream);
+int pm_selfplay_step_multi(const pm_selfplay* sp, int32_t updates, void* stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* pm_last_error(void);

@@ -72,7 +72,10 @@ __device__ __forceinline__ PushRange push_of(const pm_selfplay& sp, int64_t pos,
 
 // ------------------------------------------------------------------------------------ rollout
 // PrioritizedReplay.sample (:64-73) for update sample j: proportional draw + un-normalised IS weight.
-__device__ __forceinline__ void sample_wave(const pm_selfplay& sp, int j) {
+// pending: the step's push has not landed yet (update 0, drawn beside k_env: the tree accounts for it
+// and its leaves read as the pushed value); otherwise (updates 1..U-1) the replay is as k_env left it.
+// The fill is the post-push one either way: pos/size advance only when the step commits.
+__device__ __forceinline__ void sample_wave(const pm_selfplay& sp, int j, bool pending) {
     if (j >= sp.batch || !learner_active(sp)) return;  // wave-uniform
     const pm_ctrl* c = sp.ctrl;
     const int64_t s = c->size + sp.n;
@@ -81,8 +84,8 @@ __device__ __forceinline__ void sample_wave(const pm_selfplay& sp, int j) {
     const U4 r = philox64((uint32_t)j, TAG_PER, (uint64_t)frame, sp.seed_env);
     int64_t idx;
     float wr;
-    per_sample_one(size, per_tree(sp.per_work, sp.cap), push_of(sp, c->pos, c->size, c->max_prio), beta_of(sp, frame),
-                   u53(r.x, r.y), idx, wr);
+    const PushRange pr = pending ? push_of(sp, c->pos, c->size, c->max_prio) : PushRange{0, 0, sp.cap, 0.f};
+    per_sample_one(size, per_tree(sp.per_work, sp.cap), pr, beta_of(sp, frame), u53(r.x, r.y), idx, wr);
     if ((threadIdx.x & 63) == 0) { sp.idx[j] = idx; sp.isw[j] = wr; }
 }
 
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp, i
     const int nsb = part == PM_ACT_A ? 0 : (sp.batch + 3) / 4;
     if ((int)blockIdx.x < nsb) {
         PM_STAMP(64);
-        sample_wave(sp, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+        sample_wave(sp, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), true);
         PM_STAMP(65);
         PM_BLK_END();
         return;
@@ -132,7 +135,8 @@ __device__ __forceinline__ void batch_row_fwd(const pm_selfplay& sp, const float
 // k_env's last ceil(2B/128) blocks compute them (one tile per wave) into hfeat [B][80] (features
 // of s | Q_B(s) 0..2, r at 3, Q_B(s') 4..6, action|done bits at 7, Q_T(s') 8..10 at 64..); k_learn
 // computes the rest. Carrying r and the bits here spares k_learn a load that depends on idx.
-__device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f) {
+// pending = false (updates 1..U-1, k_batch_fwd): no push is in flight, this block computes every row.
+__device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f, bool pending = true) {
     __shared__ __attribute__((aligned(16))) float lw[kLwFloats];
     __shared__ __attribute__((aligned(16))) float hf[2][264];
     if (!learner_active(sp)) return;  // block-uniform
@@ -147,7 +151,7 @@ __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f) {
     const int j = nxt ? r - B : r;
     const int64_t id = sp.idx[j];
     const pm_ctrl* c = sp.ctrl;
-    const bool mine = r0 + (lane & 31) < 2 * B && !push_of(sp, c->pos, c->size, c->max_prio).covers(id);
+    const bool mine = r0 + (lane & 31) < 2 * B && !(pending && push_of(sp, c->pos, c->size, c->max_prio).covers(id));
     f32x16 c2[2];
     float qb[3], qt[3];
     batch_row_fwd(sp, lw, hf[0], hf[1], id, nxt, lane, c2, qb, qt);
@@ -444,7 +448,9 @@ __device__ __forceinline__ void apply_adam(const pm_selfplay& sp, ApplySmem& sm)
     if (sm.g[kGradN + 1] > 0.5f)
         for (int k = t; k < PM_QNET_NHEAD; k += nt) adam_one(sp, sm, k, sm.g[k]);
 }
-__device__ __forceinline__ void apply_finish(const pm_selfplay& sp, ApplySmem& sm, const pm_ctrl& cs) {
+// mode (PM_UPD_*): FIRST commits the epsilon decay of the step's finished episodes, LAST the replay
+// and step counters (with U > 1 updates per step pm_selfplay_commit does that after the last one).
+__device__ __forceinline__ void apply_finish(const pm_selfplay& sp, ApplySmem& sm, const pm_ctrl& cs, int mode) {
     const int t = threadIdx.x, nt = blockDim.x;
     const bool train = sm.g[kGradN + 1] > 0.5f;
     const int64_t ts = cs.train_steps + (train ? 1 : 0);
@@ -462,13 +468,17 @@ __device__ __forceinline__ void apply_finish(const pm_selfplay& sp, ApplySmem& s
     PM_STAMP(21);
     if (t == 0) {
         pm_ctrl* c = sp.ctrl;
-        const double e = sm.eps_next;  // eps * decay^D, D = finished episodes (all shards) (:261)
-        c->epsilon = e > sp.min_epsilon ? e : sp.min_epsilon;
+        if (mode & PM_UPD_FIRST) {
+            const double e = sm.eps_next;  // eps * decay^D, D = finished episodes (all shards) (:261)
+            c->epsilon = e > sp.min_epsilon ? e : sp.min_epsilon;
+        }
         if (train) { c->train_steps = ts; c->frame_idx = cs.frame_idx + 1; }
-        c->pos = (cs.pos + sp.n) % sp.cap;
-        const int64_t s = cs.size + sp.n;
-        c->size = s < sp.cap ? s : sp.cap;
-        c->step = step + 1;
+        if (mode & PM_UPD_LAST) {
+            c->pos = (cs.pos + sp.n) % sp.cap;
+            const int64_t s = cs.size + sp.n;
+            c->size = s < sp.cap ? s : sp.cap;
+            c->step = step + 1;
+        }
     }
 }
 
@@ -509,7 +519,10 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // actions depend on nothing the learner changes, and the learner occupies one CU, so they ride in
 // this launch on otherwise idle CUs instead of lengthening the next k_act_sp. act_block is
 // block-size agnostic: a 1024-thread block stages, compacts and tiles a 4x larger chunk.
-__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP) {
+// mode (PM_UPD_*): FIRST = the update that follows this step's k_env (its batch may hold rows of the
+// push k_env just made, which this kernel computes; it sums the rollout's episode counters); LAST =
+// the step's last update (refreshes the sum tree for the next push, commits the step). U = 1: both.
+__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     if (blockIdx.x > 0) {
         // the learner's load phase is latency-bound under these blocks' staging burst; they have slack
@@ -530,6 +543,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
     const bool train = s_after >= B;
     const PerTree tree = per_tree(sp.per_work, sp.cap);
+    const bool first = mode & PM_UPD_FIRST, last = mode & PM_UPD_LAST;
 
     // ---- phase 0: every independent load, issued before any use. LDS-bound arrays go global ->
     // LDS directly (global_load_lds); register loads are issued unconditionally (gating them on the
@@ -541,7 +555,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     copy_lds_f32x4<260>(sp.learn_heads + 528, sm.eps_tr);
     if (sp.fuse_apply) load_apply_inputs(sp, sm.ap, false);
     long long part[6] = {0, 0, 0, 0, 0, 0};
-    if (t < nbr) {
+    if (first && t < nbr) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) part[k] = sp.partials[(size_t)t * 8 + k];
     }
@@ -559,7 +573,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             hv[4 * k] = v.x; hv[4 * k + 1] = v.y; hv[4 * k + 2] = v.z; hv[4 * k + 3] = v.w;
         }
     }
-    for (int b = t + kLearn; b < nbr; b += kLearn)  // n > 256 * 1024 arenas only
+    for (int b = t + kLearn; first && b < nbr; b += kLearn)  // n > 256 * 1024 arenas only
 #pragma unroll
         for (int k = 0; k < 6; ++k) part[k] += sp.partials[(size_t)b * 8 + k];
     // fused: the optimizer's scalar prologue on waves with slack in this load phase (they are not
@@ -577,7 +591,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     for (int k = t; k < 512; k += kLearn) { sm.hkey[k] = kHashEmpty; sm.hwin[k] = -1; }
     if (act) sm.sidx[t] = id;
     {   // samples whose replay row k_env was writing: computed here (phase 1)
-        const bool ip = act && push_of(sp, cs.pos, cs.size, cs.max_prio).covers(id);
+        const bool ip = first && act && push_of(sp, cs.pos, cs.size, cs.max_prio).covers(id);
         const unsigned long long m = __ballot(ip);
         if (ip) sm.plist[wv * 64 + __popcll(m & ((1ull << lane) - 1ull))] = t;
         if (lane == 0) sm.pcnt[wv] = __popcll(m);
@@ -624,7 +638,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][t];
         sm.ctot[t] = s;  // read after the next barrier
     }
-    if (sp.fuse_apply && t == kLearn - 1) {  // the per-episode epsilon decay (:261) beside the forward
+    if (sp.fuse_apply && first && t == kLearn - 1) {  // the per-episode epsilon decay (:261) beside the forward
         long long s = 0;                     // (same sum, same order as thread 0's ctot[0])
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][0];
         sm.ap.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)(float)s);
@@ -669,7 +683,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     __syncthreads();
     PM_STAMP(2);
     ep_fin = sm.ctot[0];
-    if (t == 0) {  // rollout bookkeeping (:245-249)
+    if (first && t == 0) {  // rollout bookkeeping (:245-249)
         c->ep_step = ep_fin;
         c->episodes = cs.episodes + ep_fin;
         c->ep_A = cs.ep_A + sm.ctot[1]; c->win_A = cs.win_A + sm.ctot[2];
@@ -764,7 +778,9 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     PM_STAMP(4);
 
     // ---- phase 4: gradients out; sum tree: sub-blocks of the scatter and of the next push range
-    const PushRange next = push_of(sp, (cs.pos + sp.n) % sp.cap, s_after, max_prio_next);
+    // not the last update: no pending push (empty range: refreshed nodes are plain sums of the leaves)
+    const PushRange next = last ? push_of(sp, (cs.pos + sp.n) % sp.cap, s_after, max_prio_next)
+                                : PushRange{0, 0, sp.cap, 0.f};
     if (train) {
         if (t < 256) {  // dL/dW_mu = sum_j coef_j h_j; dL/dW_sigma = dL/dW_mu * eps (the update's noise)
             float g = 0.f;
@@ -845,14 +861,14 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         }
     }
     PM_STAMP(6);
-    if (sp.fuse_apply) apply_finish(sp, sm.ap, cs);  // unsharded: Adam ran with the gradients (phase 4)
+    if (sp.fuse_apply) apply_finish(sp, sm.ap, cs, mode);  // unsharded: Adam ran with the gradients (phase 4)
     PM_STAMP(7);
 }
 
 // ------------------------------------------------------------------------------------ Adam + commit
 // The scalar prologue (both noises, the bias-correction and epsilon-decay pows) runs while the
 // loads are in flight: every thread reads the all-reduced updated flag and episode count itself.
-__global__ __launch_bounds__(kLearn) void k_adam(const pm_selfplay sp) {
+__global__ __launch_bounds__(kLearn) void k_adam(const pm_selfplay sp, int mode) {
     __shared__ ApplySmem sm;
     const int t = threadIdx.x;
     const pm_ctrl cs = *sp.ctrl;
@@ -865,7 +881,7 @@ __global__ __launch_bounds__(kLearn) void k_adam(const pm_selfplay sp) {
     __syncthreads();
     apply_adam(sp, sm);
     __syncthreads();
-    apply_finish(sp, sm, cs);
+    apply_finish(sp, sm, cs, mode);
 }
 
 // pm_selfplay_prepare: features + acting weights of the current step + next update's heads
@@ -876,6 +892,86 @@ __global__ __launch_bounds__(kLearn) void k_prepare(const pm_selfplay sp) {
     gen_both_noises(sp, sm, sp.ctrl->step, (uint64_t)sp.ctrl->train_steps + 1);
     __syncthreads();
     derive_weights(sp, sm);
+}
+
+// ------------------------------------------------------------------------------------ U > 1 updates
+// Updates 1..U-1 of a vector step: the PER sample over the replay as this step's push left it (one
+// wave per sample), then the batch forward of every row (no pending push: k_env's forward blocks'
+// job, on their own launch).
+__global__ __launch_bounds__(256) void k_resample(const pm_selfplay sp) {
+    sample_wave(sp, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), false);
+}
+__global__ __launch_bounds__(kBlock) void k_batch_fwd(const pm_selfplay sp) { env_fwd_block(sp, (int)blockIdx.x, false); }
+
+// pm_selfplay_commit, pass 1: max(prios[0, size)) (memory.push: prios.max(), :57) as float bits into
+// ctrl->max_bits (priorities are > 0, so the int order of the bits is the float order).
+constexpr int kMaxBlocks = 512;
+__global__ __launch_bounds__(256) void k_prio_max(const pm_selfplay sp) {
+    __shared__ float red[4];
+    const pm_ctrl* c = sp.ctrl;
+    const int64_t s = c->size + sp.n;
+    const int64_t size = s < sp.cap ? s : sp.cap;
+    const int64_t n4 = size / 4;
+    const float4* p4 = reinterpret_cast<const float4*>(sp.prios);
+    float m = 0.f;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n4; k += (int64_t)gridDim.x * 256) {
+        const float4 v = p4[k];
+        m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    }
+    if (blockIdx.x == 0 && threadIdx.x < size - 4 * n4) m = fmaxf(m, sp.prios[4 * n4 + threadIdx.x]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        atomicMax(&sp.ctrl->max_bits, __float_as_int(m));
+    }
+}
+
+// pm_selfplay_commit, pass 2 (one workgroup): max_prio = that maximum; the sum tree's level-1 then
+// level-2 nodes over the next push range with the push substituted (as k_learn's LAST update does);
+// pos / size / step advance.
+__global__ __launch_bounds__(kLearn) void k_commit(const pm_selfplay sp) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    pm_ctrl* c = sp.ctrl;
+    const pm_ctrl cs = *c;
+    const PerTree tree = per_tree(sp.per_work, sp.cap);
+    const int64_t s = cs.size + sp.n;
+    const int64_t s_after = s < sp.cap ? s : sp.cap;
+    const float mp = __int_as_float(cs.max_bits);
+    const PushRange next = push_of(sp, (cs.pos + sp.n) % sp.cap, s_after, mp);
+    {
+        const RingNodes rn = ring_nodes(next, PER_SUB);
+        const double csub = per_sub_pushed_sum(next);
+        for (int64_t k = t; k < rn.count(); k += kLearn) {
+            const int64_t sb = rn.at(k);
+            if (per_sub_pushed(sb, next)) tree.sub[sb] = csub;
+        }
+        if (wv == 0) {  // the <= 4 partially pushed nodes at the segment ends, 4 lanes each
+            const int g = lane >> 2;
+            const bool ok = g < 4 && (g < 2 ? rn.na : rn.nb) > 0;
+            const int64_t sb = !ok ? 0 : g == 0 ? rn.a0 : g == 1 ? rn.a0 + rn.na - 1 : g == 2 ? 0 : rn.nb - 1;
+            const double v = per_sub_sum4(tree.leaf, sb, next);
+            if (ok && (lane & 3) == 0 && !per_sub_pushed(sb, next)) tree.sub[sb] = v;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    {
+        const RingNodes rn = ring_nodes(next, PER_CHUNK);
+        for (int64_t k = t; k < rn.count(); k += kLearn) {
+            const int64_t ch = rn.at(k);
+            tree.chunk[ch] = per_chunk_sum(tree, ch);
+        }
+    }
+    if (t == 0) {
+        c->max_prio = mp;
+        c->max_bits = 0;
+        c->pos = (cs.pos + sp.n) % sp.cap;
+        c->size = s_after;
+        c->step = cs.step + 1;
+    }
 }
 
 namespace {
@@ -940,10 +1036,10 @@ ActGrid learn_act_grid(const pm_selfplay* sp) {
     return ActGrid{sp->n, sp->n_pool + 1, std::min(4 * sp->chunk_A, kListMax), std::min(4 * sp->chunk_P, kListMax), 0};
 }
 
-int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st) {
+int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st, int mode = PM_UPD_FIRST | PM_UPD_LAST) {
     const ActGrid g = learn_act_grid(sp);
     const unsigned blocks = 1u + (with_act ? (unsigned)g.blocks() : 0u);
-    hipLaunchKernelGGL(k_learn, dim3(blocks), dim3(kLearn), 0, st, *sp, g.chunk0, g.chunk1);
+    hipLaunchKernelGGL(k_learn, dim3(blocks), dim3(kLearn), 0, st, *sp, g.chunk0, g.chunk1, mode);
     PM_LAUNCHED("k_learn");
     return PM_OK;
 }
@@ -986,12 +1082,66 @@ extern "C" int pm_selfplay_learn_act(const pm_selfplay* sp, void* stream) {
 }
 
 extern "C" int pm_selfplay_apply(const pm_selfplay* sp, void* stream) {
+    return pm_selfplay_apply_ex(sp, PM_UPD_FIRST | PM_UPD_LAST, stream);
+}
+
+extern "C" int pm_selfplay_apply_ex(const pm_selfplay* sp, int32_t mode, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
+    PM_REQUIRE(mode >= 0 && mode <= (PM_UPD_FIRST | PM_UPD_LAST), PM_E_ARG, "pm_selfplay_apply_ex: mode=%d", mode);
     if (sp->fuse_apply) return PM_OK;  // learn already applied (unsharded, fused)
-    hipLaunchKernelGGL(k_adam, dim3(1), dim3(kLearn), 0, pm_stream(stream), *sp);
+    hipLaunchKernelGGL(k_adam, dim3(1), dim3(kLearn), 0, pm_stream(stream), *sp, (int)mode);
     PM_LAUNCHED("k_adam");
     return PM_OK;
+}
+
+extern "C" int pm_selfplay_learn_ex(const pm_selfplay* sp, int32_t mode, int32_t with_act, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    PM_REQUIRE(mode >= 0 && mode <= (PM_UPD_FIRST | PM_UPD_LAST), PM_E_ARG, "pm_selfplay_learn_ex: mode=%d", mode);
+    return launch_learn(sp, with_act != 0, pm_stream(stream), (int)mode);
+}
+
+extern "C" int pm_selfplay_resample(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipStream_t st = pm_stream(stream);
+    hipLaunchKernelGGL(k_resample, dim3((sp->batch + 3) / 4), dim3(256), 0, st, *sp);
+    PM_LAUNCHED("k_resample");
+    hipLaunchKernelGGL(k_batch_fwd, dim3(pm_blocks(2 * sp->batch, 128)), dim3(kBlock), 0, st, *sp);
+    PM_LAUNCHED("k_batch_fwd");
+    return PM_OK;
+}
+
+extern "C" int pm_selfplay_commit(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipStream_t st = pm_stream(stream);
+    const int64_t blocks = std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (sp->cap + 4095) / 4096));
+    hipLaunchKernelGGL(k_prio_max, dim3((unsigned)blocks), dim3(256), 0, st, *sp);
+    PM_LAUNCHED("k_prio_max");
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(kLearn), 0, st, *sp);
+    PM_LAUNCHED("k_commit");
+    return PM_OK;
+}
+
+extern "C" int pm_selfplay_step_multi(const pm_selfplay* sp, int32_t updates, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    PM_REQUIRE(updates >= 1, PM_E_ARG, "pm_selfplay_step_multi: updates=%d", updates);
+    PM_REQUIRE(sp->world == 1, PM_E_ARG, "pm_selfplay_step_multi: unsharded only (world=%d)", sp->world);
+    if (updates == 1) return pm_selfplay_step_overlap(sp, stream);
+    hipStream_t st = pm_stream(stream);
+    if ((rc = launch_act(sp, PM_ACT_B, st))) return rc;
+    if ((rc = pm_selfplay_env(sp, stream))) return rc;
+    if ((rc = launch_learn(sp, true, st, PM_UPD_FIRST))) return rc;
+    if ((rc = pm_selfplay_apply_ex(sp, PM_UPD_FIRST, stream))) return rc;
+    for (int u = 1; u < updates; ++u) {
+        if ((rc = pm_selfplay_resample(sp, stream))) return rc;
+        if ((rc = launch_learn(sp, false, st, 0))) return rc;
+        if ((rc = pm_selfplay_apply_ex(sp, 0, stream))) return rc;
+    }
+    return pm_selfplay_commit(sp, stream);
 }
 
 extern "C" int pm_selfplay_step(const pm_selfplay* sp, void* stream) {

@@ -32,7 +32,8 @@ PM_TRANS_F = 16
 PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
-ABI_VERSION = 6
+PM_UPD_FIRST, PM_UPD_LAST = 1, 2
+ABI_VERSION = 7
 
 
 class EnvParams(ctypes.Structure):
@@ -52,7 +53,7 @@ class Ctrl(ctypes.Structure):
     _fields_ = [("step", c_u64), ("pos", c_i64), ("size", c_i64), ("train_steps", c_i64), ("frame_idx", c_i64),
                 ("episodes", c_i64), ("epsilon", c_double), ("max_prio", c_float), ("last_loss", c_float),
                 ("ep_step", c_i64), ("win_A", c_i64), ("ep_A", c_i64), ("win_P", c_i64), ("ep_P", c_i64),
-                ("reward_B", c_double), ("status", c_i32), ("_pad", c_i32)]
+                ("reward_B", c_double), ("status", c_i32), ("max_bits", c_i32)]
 
 
 class SelfPlay(ctypes.Structure):
@@ -140,6 +141,11 @@ _SIGS = {
     "pm_selfplay_act_part": (c_i32, [c_void_p, c_i32, c_void_p]),
     "pm_selfplay_learn_act": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_step_overlap": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_learn_ex": (c_i32, [c_void_p, c_i32, c_i32, c_void_p]),
+    "pm_selfplay_apply_ex": (c_i32, [c_void_p, c_i32, c_void_p]),
+    "pm_selfplay_resample": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_commit": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_step_multi": (c_i32, [c_void_p, c_i32, c_void_p]),
     "pm_last_error": (ctypes.c_char_p, []),
     "pm_abi_version": (c_i32, []),
     "pm_sizeof": (c_i32, [c_i32]),

@@ -3,8 +3,12 @@ per device, as four libpongmi launches sequences per vector step (rollout / lear
 apply) on one stream, with every loop counter in a device control block.
 
 Semantics the batching fixes (the reference steps ONE env and updates once per env step):
-  * one vector step = one env step in every arena; one PER update of `batch` per vector step
-    (`updates_per_step` repeats learn+apply);
+  * one vector step = one env step in every arena, then `updates_per_step` (U) PER updates of
+    `batch`. The reference's replay ratio is one update per pushed transition (:243-244): U = n
+    keeps it (the generation controllers do, with a few hundred arenas); U = 1, the throughput
+    setting the bench measures, trains once per n transitions. With U > 1, update 0 samples with
+    the step's push pending (as U = 1) and updates 1..U-1 resample the replay after it; every
+    update advances frame_idx (beta), the noise counter, train_steps and the target sync;
   * NoisyNet acting noise is fresh per vector step and shared by all arenas (reset_noise per
     select_action_B, :125), the update draws its own fresh noise (:142);
   * epsilon decays once per finished episode: eps <- max(min_eps, eps * decay^D) for the D
@@ -44,8 +48,11 @@ class SelfPlayLearner:
                  memory_size=1_000_000, gamma=0.99, lr=2.5e-4, epsilon=0.02, min_epsilon=0.02, epsilon_decay=0.995,
                  target_update_interval=1000, pool_ratio=0.33, alpha=0.6, beta_start=0.4, beta_frames=100000,
                  episode=0, seed=0, rank=0, world=1, allreduce=None, device=None, modelA_noisy=True,
-                 fuse_apply=True, overlap=True):
+                 fuse_apply=True, overlap=True, updates_per_step=1):
         self.lib = _lib.load()
+        self.updates_per_step = int(updates_per_step)
+        if self.updates_per_step < 1:
+            raise ValueError("updates_per_step must be >= 1")
         self.overlap = bool(overlap)
         self._aA_ready = False
         self.device = torch.device(device if device is not None else "cuda")
@@ -154,9 +161,55 @@ class SelfPlayLearner:
     def apply(self):
         check(self.lib.pm_selfplay_apply(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_apply")
 
+    def learn_ex(self, mode, act_next=False):
+        check(self.lib.pm_selfplay_learn_ex(ctypes.byref(self.sp), int(mode), int(bool(act_next)), stream_ptr()),
+              "pm_selfplay_learn_ex")
+        if act_next:
+            self._aA_ready = True
+
+    def apply_ex(self, mode):
+        check(self.lib.pm_selfplay_apply_ex(ctypes.byref(self.sp), int(mode), stream_ptr()), "pm_selfplay_apply_ex")
+
+    def resample(self):
+        """The PER sample + batch forward of updates 1..U-1 of a vector step."""
+        check(self.lib.pm_selfplay_resample(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_resample")
+
+    def commit(self):
+        """Close a vector step of U > 1 updates: max_prio = max(prios), next-push tree nodes, counters."""
+        check(self.lib.pm_selfplay_commit(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_commit")
+
+    def _step_multi(self):
+        U = self.updates_per_step
+        if self.world == 1 and self.overlap:
+            if not self._aA_ready:
+                self.act(_lib.PM_ACT_A)
+            check(self.lib.pm_selfplay_step_multi(ctypes.byref(self.sp), U, stream_ptr()), "pm_selfplay_step_multi")
+            self._aA_ready = True
+            return
+        if self.overlap:
+            if not self._aA_ready:
+                self.act(_lib.PM_ACT_A)
+            self.act(_lib.PM_ACT_B)
+            self.env_step()
+        else:
+            self.rollout()
+        for u in range(U):
+            mode = _lib.PM_UPD_FIRST if u == 0 else 0
+            if u:
+                self.resample()
+            self.learn_ex(mode, act_next=self.overlap and u == 0)
+            if self.world > 1:
+                self.allreduce(self.grad)
+            self.apply_ex(mode)
+        self.commit()
+
     def step(self):
-        """One vector step (n env-steps on this rank). With `overlap` the opponents' act for the
-        next step runs inside the learner's launch (bit-identical results)."""
+        """One vector step (n env-steps on this rank) and its `updates_per_step` updates. With
+        `overlap` the opponents' act for the next step runs inside the learner's launch
+        (bit-identical results)."""
+        if self.updates_per_step > 1:
+            self._step_multi()
+            return
         if not self.overlap:
             if self.world == 1:
                 check(self.lib.pm_selfplay_step(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step")

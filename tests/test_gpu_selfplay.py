@@ -350,3 +350,143 @@ def test_sharded_world2_overlap_equals_plain(golden):
         assert torch.equal(getattr(ov[0], name), getattr(ov[1], name)), name
     assert not torch.equal(ov[0].f64, ov[1].f64)  # rank-specific arenas
     assert ov[0].counters()["train_steps"] == 14
+
+
+# ------------------------------------------------------------------------------ U > 1 updates per step
+def _drive_split(L, U):
+    """One vector step of U updates through the split entry points (rollout, learn_ex / apply_ex per
+    update, resample for updates 1..U-1, commit)."""
+    from pongmi import _lib
+    L.rollout()
+    for u in range(U):
+        mode = _lib.PM_UPD_FIRST if u == 0 else 0
+        if u:
+            L.resample()
+        L.learn_ex(mode)
+        L.apply_ex(mode)
+    L.commit()
+
+
+def test_multi_update_step_matches_oracle(orc, golden):
+    """U = 3 updates per vector step (replay ratio): update 0 samples with the push pending, updates
+    1..2 resample the replay after it with their own frame (beta, Philox draw) and the update noise
+    of their own train step; every update matches the oracle's double-DQN restatement and Adam; the
+    commit sets max_prio to the array maximum exactly (U * batch >= n here, so scatters can lower it)
+    and leaves the sum tree bit-identical to a full rebuild."""
+    from pongmi import _lib
+    from pongmi.qnet import unpack_state_dict
+    U = 3
+    L = _learner(golden, n=512, batch=256, cap=2048, epsilon=0.5, target_update_interval=4, fuse_apply=False,
+                 overlap=False, updates_per_step=U)
+    sp = L.sp
+    m_ref, v_ref = np.zeros(520), np.zeros(520)
+    updates = 0
+    for step in range(6):
+        c0 = L.counters()
+        L.rollout()
+        for u in range(U):
+            mode = _lib.PM_UPD_FIRST if u == 0 else 0
+            if u:
+                L.resample()
+            pre = _snap(L)
+            L.learn_ex(mode)
+            torch.cuda.synchronize()
+            c = pre["ctrl"]
+            assert c["step"] == c0["step"] and c["pos"] == c0["pos"]  # the step commits after its last update
+            size = min(c["size"] + L.n, L.cap)
+            frame = c["frame_idx"] + 1
+            assert frame == updates + 1
+            beta = min(1.0, 0.4 + frame * 0.6 / 100000)
+            r = orc.philox64(np.arange(L.batch), orc.TAG_PER, np.full(L.batch, frame, np.uint64), sp.seed_env)
+            # update 0's batch was drawn beside k_env with the push pending: the pushed priorities
+            # are in pre["prios"] already, so every update samples from its snapshot
+            ref_idx, ref_w = orc.per_sample(pre["prios"], size, L.batch, beta, orc.u53(r[0], r[1]))
+            idx = L.idx.cpu().numpy()
+            assert np.mean(idx == ref_idx) > 0.99, (step, u)
+            rows = pre["trans"][idx]
+            bits = rows[:, 15].view(np.int32)
+            isw = L.isw.cpu().numpy()
+            w = isw / isw.max()
+            sdB = {k: v.numpy() for k, v in unpack_state_dict(L.paramsB).items()}
+            fVi, fVo, fAi, fAo = orc.philox_noise(sp.seed_net, orc.TAG_NOISE_TRAIN, c["train_steps"] + 1)
+            np.testing.assert_allclose(sdB["fc_A.weight_epsilon"], np.outer(fAo, fAi), rtol=2e-6, atol=1e-7)
+            heads = orc.pack_heads(sdB)
+            theads = orc.pack_heads({k: v.numpy() for k, v in unpack_state_dict(L.paramsT).items()})
+            res = orc.dqn_loss_grads(sdB, heads, theads, sdB, rows[:, 0:7], bits & 0xFF, rows[:, 7], rows[:, 8:15],
+                                     ((bits >> 8) & 1).astype(bool), w, 0.99)
+            grad = L.grad.cpu().numpy()
+            np.testing.assert_allclose(grad[:520], res["grads"], rtol=2e-4, atol=2e-6)
+            exp_pr = pre["prios"].copy()
+            orc.per_update(exp_pr, idx, res["errors"])
+            np.testing.assert_allclose(L.prios.cpu().numpy(), exp_pr, rtol=2e-5, atol=3e-5)
+            if u > 0:
+                assert grad[520] == 0  # the step's episodes are counted by update 0 only
+            L.apply_ex(mode)
+            updates += 1
+            p_ref, m_ref, v_ref = orc.adam_step(heads, grad[:520].astype(np.float64), m_ref, v_ref, updates, 2.5e-4)
+            np.testing.assert_allclose(L.paramsB.cpu().numpy()[4672:5192], p_ref, rtol=1e-5, atol=1e-7)
+            after = L.counters()
+            assert after["train_steps"] == updates and after["frame_idx"] == updates
+            if updates % 4 == 0:
+                assert np.array_equal(L.paramsT.cpu().numpy()[:5192], L.paramsB.cpu().numpy()[:5192])
+            if u == 0:
+                assert np.isclose(after["epsilon"], max(0.02, c["epsilon"] * 0.995 ** grad[520]), rtol=1e-12)
+            else:
+                assert after["epsilon"] == c["epsilon"]
+        L.commit()
+        torch.cuda.synchronize()
+        c = L.counters()
+        pr = L.prios.cpu().numpy()
+        assert c["max_prio"] == pr.max() and c["max_bits"] == 0
+        assert c["step"] == c0["step"] + 1 and c["pos"] == (c0["pos"] + L.n) % L.cap
+        assert c["size"] == min(c0["size"] + L.n, L.cap)
+        inc = L.per_work.clone()
+        L.prepare()
+        torch.cuda.synchronize()
+        assert torch.equal(inc, L.per_work), step
+
+
+def test_multi_update_fused_equals_split(golden):
+    """pm_selfplay_step_multi (overlapped, fused Adam) equals the split path bit for bit."""
+    U = 4
+    A = _learner(golden, n=1024, batch=256, cap=4096, seed=8, updates_per_step=U)
+    B = _learner(golden, n=1024, batch=256, cap=4096, seed=8, updates_per_step=U, fuse_apply=False, overlap=False)
+    for _ in range(9):
+        A.step()
+        _drive_split(B, U)
+    torch.cuda.synchronize()
+    for name in ("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "opp", "w_B",
+                 "learn_heads", "per_work", "idx", "isw", "aB", "ep_reward"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    assert A.counters() == B.counters()
+    assert A.counters()["train_steps"] == 9 * U
+
+
+def test_multi_update_sharded_replicas(golden):
+    """world = 2 with U = 3: all-reduce after every update keeps the replicas identical."""
+    from pongmi import _lib
+    U = 3
+    Ls = [_learner(golden, n=1024, batch=256, cap=4096, seed=13, rank=r, world=2, allreduce=lambda t: None,
+                   updates_per_step=U, overlap=False) for r in range(2)]
+    for _ in range(5):
+        for L in Ls:
+            L.rollout()
+        for u in range(U):
+            mode = _lib.PM_UPD_FIRST if u == 0 else 0
+            for L in Ls:
+                if u:
+                    L.resample()
+                L.learn_ex(mode)
+            g = Ls[0].grad + Ls[1].grad
+            for L in Ls:
+                L.grad.copy_(g)
+                L.apply_ex(mode)
+        for L in Ls:
+            L.commit()
+    torch.cuda.synchronize()
+    for name in ("paramsB", "paramsT", "adam_m", "adam_v", "w_B", "learn_heads"):
+        assert torch.equal(getattr(Ls[0], name), getattr(Ls[1], name)), name
+    c0, c1 = Ls[0].counters(), Ls[1].counters()
+    assert c0["train_steps"] == c1["train_steps"] == 5 * U and c0["epsilon"] == c1["epsilon"]
+    for L in Ls:
+        assert L.counters()["max_prio"] == L.prios.cpu().numpy().max()

@@ -255,11 +255,15 @@ typedef struct pm_rnn_ctrl {
     uint64_t step;       /* vector steps taken */
     int64_t episodes;    /* finished episodes (global_episode_count) */
     int64_t seq_count;   /* episodes ever stored (length >= T) */
-    int64_t seq_size;    /* episodes held: min(seq_count, seq_cap) */
+    int64_t seq_size;    /* episodes held: the newest min(seq_count, seq_cap), less any evicted by age */
     double epsilon;
     int64_t win_A, ep_A, win_P, ep_P;
     double reward_B;     /* summed rewards of finished episodes */
-    int32_t status;      /* bit 0: a sampled step had been overwritten in its arena's ring */
+    int32_t status;      /* bit 0: a sampled step had been overwritten in its arena's ring (never, by
+                            construction: kept for the check); bit 1: episodes left the buffer by age
+                            before seq_cap newer ones did (their steps would leave the ring: depth is
+                            too small for the episode lengths seen); bit 2: a finished trajectory
+                            longer than depth / 2 steps was not stored */
     int32_t train;       /* 1 when this step's DRQN update was enabled */
 } pm_rnn_ctrl;
 
@@ -268,7 +272,9 @@ typedef struct pm_rnn_selfplay {
     pm_env_state st;
     int32_t *opp;          /* [n] 0 = modelA, k >= 1 = pool net k */
     float *ep_reward;      /* [n] */
-    int32_t *ep_len;       /* [n] steps into the current episode */
+    int32_t *ep_len;       /* [n] steps into the current trajectory (the episode steps push_step
+                              collected since the last done; a max_steps cut does not end it) */
+    int32_t *ep_steps;     /* [n] steps into the current env episode (the max_steps cut)           */
     uint8_t *reset;        /* [n] 1: zero both players' (h, c) before the next act (episode start) */
     const float *w_opp;    /* [1 + n_pool][PM_RNN_NW] modelA, pool nets (eval-mode folds) */
     float *paramsB;        /* [PM_RNN_NP] modelB (the pm_drqn params); fresh noise written back */
@@ -278,6 +284,7 @@ typedef struct pm_rnn_selfplay {
     int8_t *aA, *aB;       /* [n] */
     float *trans;          /* [depth][n][PM_TRANS_F] per-arena transition rings (s, r, s', a | done << 8) */
     int64_t *seq_eps;      /* [seq_cap][2]: arena | length << 32, first step */
+    int64_t *seq_mark;     /* [depth] seq_count after step s's append, at s % depth (age eviction) */
     int64_t *fin;          /* [ceil(n / 256) * 256][2] scratch: stored episodes staged per env block */
     int64_t *partials;     /* [ceil(n / 256)][8] */
     int32_t *opp_list;     /* [n] per-256-arena-block opponent lists (written by the env kernel) */
@@ -285,11 +292,21 @@ typedef struct pm_rnn_selfplay {
     int32_t *enable;       /* [1] set by the sampler: seq_size > min_episodes */
     pm_rnn_ctrl *ctrl;
     int32_t n, n_pool, depth, T, chunk_A, chunk_P;
+    int32_t max_steps;     /* max_episode_steps (:751, config default 1000; 0 = no cut): an episode still
+                              running after max_steps steps ends (counters, epsilon decay, new opponent,
+                              env.reset, zero (h, c)) but its trajectory does not: push_step's
+                              current_episode_trajectory keeps collecting until a done (:107-116) */
+    int32_t _pad;
     int64_t seq_cap, min_episodes;
     double min_epsilon, epsilon_decay, pool_ratio;
     uint64_t seed_env, seed_net;
 } pm_rnn_selfplay;
 
+/* Ring safety: a stored trajectory is at most depth / 2 steps long (longer ones are dropped, status bit
+ * 2), and an episode leaves the buffer once depth / 2 steps have passed since it finished (status bit
+ * 1 if that happens before seq_cap newer episodes push it out), so every step a sample can reach is
+ * still in its arena's ring. Size depth >= 2 x (the steps seq_cap episodes span + the longest
+ * trajectory expected) and neither bit is ever set. */
 /* Serve every arena, draw its first opponent, zero (h, c). */
 int pm_rnn_selfplay_init(const pm_rnn_selfplay *sp, void *stream);
 /* modelB's fold with fresh noise + both players' act (K5). */
@@ -300,6 +317,12 @@ int pm_rnn_selfplay_env(const pm_rnn_selfplay *sp, const pm_drqn *d, void *strea
 int pm_rnn_selfplay_rollout(const pm_rnn_selfplay *sp, const pm_drqn *d, void *stream);
 /* rollout then pm_drqn_update(d) (d->enable should be sp->enable). */
 int pm_rnn_selfplay_step(const pm_rnn_selfplay *sp, const pm_drqn *d, void *stream);
+/* Replay ratio: the reference runs train_step_rnn once per env step (:776-777). Update u >= 1 of a
+ * vector step samples its own batch (Philox counter (step, u); u = 0 is the env call's draw):
+ * pm_rnn_selfplay_sample then pm_drqn_update. pm_rnn_selfplay_step_multi = rollout + update + (U - 1)
+ * x [sample(u) + update]; U = 1 is pm_rnn_selfplay_step. */
+int pm_rnn_selfplay_sample(const pm_rnn_selfplay *sp, const pm_drqn *d, int32_t u, void *stream);
+int pm_rnn_selfplay_step_multi(const pm_rnn_selfplay *sp, const pm_drqn *d, int32_t updates, void *stream);
 
 /* ---------------------------------------------------------------- replay + PER (K4) */
 

@@ -44,6 +44,7 @@ __global__ __launch_bounds__(kBlock) void k_rsp_init(const pm_rnn_selfplay sp) {
         sp.st.serves[i] = (int32_t)ns + 1;
         sp.ep_reward[i] = 0.f;
         sp.ep_len[i] = 0;
+        sp.ep_steps[i] = 0;
         sp.reset[i] = 1;  // init_hidden for both players (:744-746)
         observe(a, oA, oB);
     }
@@ -79,8 +80,11 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
     float nA[7], nB[7];
     observe(a, nA, nB);
     const float er = sp.ep_reward[ii] + rB;  // episode_reward_b += reward_B (:765)
-    const int len = sp.ep_len[ii] + 1;
-    const bool fin = valid && d;
+    const int len = sp.ep_len[ii] + 1;       // the trajectory push_step is collecting (:107-110)
+    const int steps = sp.ep_steps[ii] + 1;   // for step_in_episode in range(max_episode_steps) (:751)
+    // the episode ends on done or at the step cut; the trajectory only on done (:111-116)
+    const bool end = d || (sp.max_steps > 0 && steps >= sp.max_steps);
+    const bool fin = valid && end;
     {   // per-block partials, no atomics: finished, vs-A, wins vs A, vs-pool, wins vs pool, reward
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         const bool win = er > 0.f;  // win_flag = episode_reward_b > 0 (:783)
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
         row[1] = make_float4(oB[4], oB[5], oB[6], rB);
         row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
         row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
-        if (d) {  // episode over: stored when len >= trace_length (:112-115); next opponent, env.reset()
+        if (end) {  // episode over (done or cut): next opponent, env.reset() (:735-740)
             onew = onext;
             sp.opp[i] = onew;
             serve(a, svx, svy, sspn);
@@ -110,15 +114,18 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
             observe(a, nA, nB);
         }
         store_arena(sp.st, i, a);
-        sp.ep_reward[i] = d ? 0.f : er;
+        sp.ep_reward[i] = end ? 0.f : er;
         sp.ep_len[i] = d ? 0 : len;
-        sp.reset[i] = (uint8_t)d;
+        sp.ep_steps[i] = end ? 0 : steps;
+        sp.reset[i] = (uint8_t)end;  // init_hidden for both players at the next episode (:744-746)
     }
 #pragma unroll
     for (int k = 0; k < 7; ++k) { lds[0][threadIdx.x][k] = nA[k]; lds[1][threadIdx.x][k] = nB[k]; }
     {   // episodes to store, ranked in arena order within the block -> the block's staging slots
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        const bool st = valid && d && len >= sp.T;
+        // stored when len >= trace_length (:112-115) and short enough to stay in the ring (header)
+        const bool st = valid && d && len >= sp.T && len <= sp.depth / 2;
+        if (valid && d && len > sp.depth / 2) atomicOr(&sp.ctrl->status, 4);
         const unsigned long long m = __ballot(st);
         if (lane == 0) red_st[wv] = __popcll(m);
         __syncthreads();
@@ -194,8 +201,18 @@ __global__ __launch_bounds__(kAppend) void k_rsp_append(const pm_rnn_selfplay sp
             for (int w = 0; w < kAppend / 64; ++w) v += wred[w][k];
             tot[k] = v;
         }
-        c->seq_count = base + total;
-        c->seq_size = c->seq_count < sp.seq_cap ? c->seq_count : sp.seq_cap;
+        // deque(maxlen=seq_cap) keeps the newest seq_cap episodes; an episode that finished more than
+        // depth / 2 steps ago also leaves (its steps are about to leave the ring): entries [0, E(s))
+        // finished at or before step s, E(s) = seq_mark[s % depth] (header: ring safety)
+        const uint64_t now = c->step;
+        const int64_t count = base + total;
+        sp.seq_mark[now % (uint64_t)sp.depth] = count;
+        const int64_t h = sp.depth / 2;
+        const int64_t by_cap = count > sp.seq_cap ? count - sp.seq_cap : 0;
+        const int64_t by_age = (int64_t)now >= h + 1 ? sp.seq_mark[(now - h - 1) % (uint64_t)sp.depth] : 0;
+        if (by_age > by_cap) c->status |= 2;
+        c->seq_count = count;
+        c->seq_size = count - (by_age > by_cap ? by_age : by_cap);
         c->episodes += tot[0];
         c->ep_A += tot[1]; c->win_A += tot[2]; c->ep_P += tot[3]; c->win_P += tot[4];
         c->reward_B += (double)tot[5];
@@ -216,7 +233,8 @@ struct SampleOut {
     int B, T;
 };
 
-__global__ __launch_bounds__(512) void k_rsp_sample(const pm_rnn_selfplay sp, SampleOut o) {
+// u: the update of this vector step (0: the env call's draw; 1..U-1: pm_rnn_selfplay_sample).
+__global__ __launch_bounds__(512) void k_rsp_sample(const pm_rnn_selfplay sp, SampleOut o, int u) {
     pm_rnn_ctrl* c = sp.ctrl;
     const int64_t size = c->seq_size;
     const bool en = size > sp.min_episodes && size > 0;
@@ -227,7 +245,7 @@ __global__ __launch_bounds__(512) void k_rsp_sample(const pm_rnn_selfplay sp, Sa
     for (int e = threadIdx.x; e < o.B * o.T; e += blockDim.x) {  // one (sequence, step) per thread
         const int b = e / o.T, tau = e % o.T;
         // np.random.choice(len(buffer), batch, replace=True), then randint(0, len - T + 1) (:131, :147)
-        const U4 r = philox64((uint32_t)b, TAG_SEQ, now, sp.seed_env);
+        const U4 r = philox64((uint32_t)b, TAG_SEQ, now | ((uint64_t)u << 48), sp.seed_env);
         const int64_t j = below(r.x, (uint32_t)size);
         const int64_t slot = (first + j) % sp.seq_cap;
         const int64_t packed = sp.seq_eps[2 * slot];
@@ -253,7 +271,7 @@ int check(const pm_rnn_selfplay* sp) {
     PM_REQUIRE(sp->n > 0 && sp->n_pool >= 0, PM_E_SIZE, "pm_rnn_selfplay: n %d, n_pool %d", sp->n, sp->n_pool);
     PM_REQUIRE(sp->T >= 1 && sp->depth > sp->T && sp->seq_cap >= 1, PM_E_SIZE, "pm_rnn_selfplay: T %d depth %d",
                sp->T, sp->depth);
-    PM_REQUIRE(sp->opp && sp->ep_reward && sp->ep_len && sp->reset && sp->w_opp && sp->paramsB && sp->w_B && sp->hA &&
+    PM_REQUIRE(sp->opp && sp->ep_reward && sp->ep_len && sp->ep_steps && sp->seq_mark && sp->max_steps >= 0 && sp->reset && sp->w_opp && sp->paramsB && sp->w_B && sp->hA &&
                    sp->cA && sp->hB && sp->cB && sp->obsA && sp->obsB && sp->aA && sp->aB && sp->trans && sp->seq_eps &&
                    sp->fin && sp->partials && sp->opp_list && sp->opp_cnt && sp->enable && sp->ctrl,
                PM_E_ARG, "pm_rnn_selfplay: null buffer");
@@ -295,9 +313,20 @@ extern "C" int pm_rnn_selfplay_env(const pm_rnn_selfplay* sp, const pm_drqn* d, 
         PM_REQUIRE(d->T == sp->T, PM_E_ARG, "pm_rnn_selfplay: learner T %d != %d", d->T, sp->T);
         const SampleOut o{const_cast<float*>(d->obs), const_cast<float*>(d->next), const_cast<float*>(d->rew),
                           const_cast<int32_t*>(d->act), const_cast<uint8_t*>(d->done), d->batch, d->T};
-        hipLaunchKernelGGL(k_rsp_sample, dim3(1), dim3(512), 0, st, *sp, o);
+        hipLaunchKernelGGL(k_rsp_sample, dim3(1), dim3(512), 0, st, *sp, o, 0);
         PM_LAUNCHED("k_rsp_sample");
     }
+    return PM_OK;
+}
+
+extern "C" int pm_rnn_selfplay_sample(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t u, void* stream) {
+    if (int rc = check(sp)) return rc;
+    PM_REQUIRE(d && d->T == sp->T, PM_E_ARG, "pm_rnn_selfplay_sample: learner missing or T mismatch");
+    PM_REQUIRE(u >= 0 && u < (1 << 15), PM_E_ARG, "pm_rnn_selfplay_sample: u=%d", u);
+    const SampleOut o{const_cast<float*>(d->obs), const_cast<float*>(d->next), const_cast<float*>(d->rew),
+                      const_cast<int32_t*>(d->act), const_cast<uint8_t*>(d->done), d->batch, d->T};
+    hipLaunchKernelGGL(k_rsp_sample, dim3(1), dim3(512), 0, pm_stream(stream), *sp, o, (int)u);
+    PM_LAUNCHED("k_rsp_sample");
     return PM_OK;
 }
 
@@ -310,4 +339,14 @@ extern "C" int pm_rnn_selfplay_step(const pm_rnn_selfplay* sp, const pm_drqn* d,
     PM_REQUIRE(d, PM_E_ARG, "pm_rnn_selfplay_step: null learner");
     if (int rc = pm_rnn_selfplay_rollout(sp, d, stream)) return rc;
     return pm_drqn_update(d, stream);
+}
+
+extern "C" int pm_rnn_selfplay_step_multi(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates, void* stream) {
+    PM_REQUIRE(updates >= 1, PM_E_ARG, "pm_rnn_selfplay_step_multi: updates=%d", updates);
+    if (int rc = pm_rnn_selfplay_step(sp, d, stream)) return rc;
+    for (int u = 1; u < updates; ++u) {
+        if (int rc = pm_rnn_selfplay_sample(sp, d, u, stream)) return rc;
+        if (int rc = pm_drqn_update(d, stream)) return rc;
+    }
+    return PM_OK;
 }

@@ -88,10 +88,10 @@ class RnnCtrl(ctypes.Structure):
 
 class RnnSelfPlay(ctypes.Structure):
     _fields_ = [("env", EnvParams), ("st", EnvState)] + \
-        [(n, c_void_p) for n in ("opp", "ep_reward", "ep_len", "reset", "w_opp", "paramsB", "w_B", "hA", "cA", "hB",
-                                 "cB", "obsA", "obsB", "aA", "aB", "trans", "seq_eps", "fin", "partials", "opp_list",
-                                 "opp_cnt", "enable", "ctrl")] + \
-        [(n, c_i32) for n in ("n", "n_pool", "depth", "T", "chunk_A", "chunk_P")] + \
+        [(n, c_void_p) for n in ("opp", "ep_reward", "ep_len", "ep_steps", "reset", "w_opp", "paramsB", "w_B", "hA",
+                                 "cA", "hB", "cB", "obsA", "obsB", "aA", "aB", "trans", "seq_eps", "seq_mark", "fin",
+                                 "partials", "opp_list", "opp_cnt", "enable", "ctrl")] + \
+        [(n, c_i32) for n in ("n", "n_pool", "depth", "T", "chunk_A", "chunk_P", "max_steps", "_pad")] + \
         [("seq_cap", c_i64), ("min_episodes", c_i64)] + \
         [(n, c_double) for n in ("min_epsilon", "epsilon_decay", "pool_ratio")] + \
         [("seed_env", c_u64), ("seed_net", c_u64)]
@@ -126,6 +126,8 @@ _SIGS = {
     "pm_rnn_selfplay_env": (c_i32, [c_void_p, c_void_p, c_void_p]),
     "pm_rnn_selfplay_rollout": (c_i32, [c_void_p, c_void_p, c_void_p]),
     "pm_rnn_selfplay_step": (c_i32, [c_void_p, c_void_p, c_void_p]),
+    "pm_rnn_selfplay_sample": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p]),
+    "pm_rnn_selfplay_step_multi": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_per_work_bytes": (c_i64, [c_i64]),
     "pm_per_sample": (c_i32, [c_void_p, c_i64, c_float, c_float, c_void_p, c_u64, c_u64, c_void_p, c_void_p, c_i32,
                               c_void_p, c_void_p]),

@@ -4,9 +4,19 @@ learners (SelfPlayLearner, RNNSelfPlayLearner) and evaluators.
 
 Each training try plays until `episodes_per_generation` more episodes have finished across the
 arenas (counted on the device, read every `check_every` vector steps; the reference plays exactly
-that many episodes one after another). Then modelB is evaluated against modelA and the pool with
-the batched evaluators (serves and pool draws from the global `random` stream, as the reference),
-and promoted, retried or saved as a fault exactly as the reference decides. Checkpoints are the
+that many episodes one after another).
+
+Replay ratio. The reference trains once per env step (train_iterative.py:243-244,
+train_rnn_iterative.py:776-777): one update per pushed transition, ~episodes x mean length
+(~38 steps) updates per try, which is what lets its double-DQN target sync every 1000 / 2000
+updates within a generation. A vector step pushes n transitions, so the controllers run
+U = round(replay_ratio * n) updates per vector step (replay_ratio = 1.0: the reference's ratio) on
+a few hundred arenas by default (QNet 512, QNetRNN 64) rather than the bench's 65 536: a try then
+costs ~episodes x 38 updates, as the reference's does, and finishes in seconds on the device.
+
+After a try, modelB is evaluated against modelA and the pool with the batched evaluators (serves
+and pool draws from the global `random` stream, as the reference), and promoted, retried or saved
+as a fault exactly as the reference decides. Checkpoints are the
 reference's dicts (same keys, same order, state_dicts with the reference's key names and an Adam
 state_dict), written with torch.save and loadable by the reference's scripts and tests/arena.py.
 Console lines keep the reference's formats (win rates in the interval lines are over the episodes
@@ -55,11 +65,19 @@ class _Progress:
         self.next_mark = (c["episodes"] // self.interval + 1) * self.interval
 
 
-def _play_episodes(L, episodes, progress, check_every, on_check=None):
+def updates_for(n_arenas, replay_ratio=1.0, updates_per_step=None):
+    """Updates per vector step: explicit, or replay_ratio updates per pushed transition."""
+    if updates_per_step is not None:
+        return max(1, int(updates_per_step))
+    return max(1, int(round(float(replay_ratio) * int(n_arenas))))
+
+
+def _play_episodes(L, episodes, progress, check_every, on_check=None, step=None):
     e0 = L.counters()["episodes"]
+    step = step or L.step
     while True:
         for _ in range(check_every):
-            L.step()
+            step()
         c = L.counters()
         progress.tick(c)
         if on_check:
@@ -73,7 +91,8 @@ class QNetGenerations:
     """scripts/train_iterative.py: generations of modelB (NoisyNet heads, PER double DQN) against a
     frozen modelA and a pool read once from the init checkpoint's directory."""
 
-    def __init__(self, cfg, n_arenas=65536, device="cuda", seed=0, log=print, check_every=4):
+    def __init__(self, cfg, n_arenas=512, device="cuda", seed=0, log=print, check_every=4, replay_ratio=1.0,
+                 updates_per_step=None):
         from models.qnet import QNet
         from .selfplay import SelfPlayLearner
         t = cfg["training"]
@@ -105,7 +124,8 @@ class QNetGenerations:
                                  batch=t["batch_size"], memory_size=t["memory_size"], gamma=t["gamma"], lr=t["lr"],
                                  epsilon=epsilon, min_epsilon=t["min_epsilon"], epsilon_decay=t["epsilon_decay"],
                                  target_update_interval=t["target_update_interval"],
-                                 pool_ratio=t["opponent_pool_ratio"], episode=episode, seed=seed, device=device)
+                                 pool_ratio=t["opponent_pool_ratio"], episode=episode, seed=seed, device=device,
+                                 updates_per_step=updates_for(n_arenas, replay_ratio, updates_per_step))
         self.done_generations = 0
         self.current_generation = 0
 
@@ -165,7 +185,8 @@ class RNNGenerations:
     from the latest-state checkpoint, per-generation restart of B from A, and promoted models joining
     the runtime pool."""
 
-    def __init__(self, cfg, n_arenas=32768, device="cuda", seed=0, log=print, check_every=4):
+    def __init__(self, cfg, n_arenas=64, device="cuda", seed=0, log=print, check_every=4, replay_ratio=1.0,
+                 updates_per_step=None):
         from models.qnet_rnn import QNetRNN
         from .rnn_selfplay import RNNSelfPlayLearner
         t = cfg["training"]
@@ -258,14 +279,23 @@ class RNNGenerations:
                                     epsilon_decay=t["epsilon_decay"],
                                     target_update_interval=t["target_update_interval"],
                                     pool_ratio=t["opponent_pool_ratio"] or 0.0, grad_clip_norm=g("grad_clip_norm", 1.0),
-                                    episode=episodes, seed=seed, device=device)
+                                    episode=episodes, seed=seed, device=device,
+                                    updates_per_step=updates_for(n_arenas, replay_ratio, updates_per_step),
+                                    max_episode_steps=cfg["env"].get("max_episode_steps", 1000))
         if opt:
             self.L.learner.load_optimizer_state_dict(opt)
         self.L.learner.set_train_steps(train_steps)
         # the main loop starts from generation 0 whatever was resumed (:625-626)
         self.done_generations = 0
         self.current_generation = 0
-        self._next_save = (train_steps // self.save_every + 1) * self.save_every if self.save_every > 0 else None
+        self._next_save = None
+        self._sync_save_mark(train_steps)
+
+    def _sync_save_mark(self, train_steps):
+        """Next latest-state save: after update number k * interval (k*interval > train_steps)."""
+        self._steps_hi = int(train_steps)  # upper bound of train steps since the last host read
+        self._next_save = ((self._steps_hi // self.save_every + 1) * self.save_every if self.save_every > 0
+                           else None)
 
     # ------------------------------------------------------------------ checkpoints
     def _base(self):
@@ -275,18 +305,50 @@ class RNNGenerations:
                       "modelB_state": checkpoint.cpu_state(L.modelB_state_dict()),
                       "optimizer_B_state": L.learner.optimizer_state_dict()}
 
-    def save_latest(self):
-        """save_latest_training_checkpoint (:630-667)."""
+    def save_latest(self, train_steps=None):
+        """save_latest_training_checkpoint (:630-667). train_steps: the count to record (default: the
+        current one)."""
         L, c, d = self._base()
+        ts = c["train_steps"] if train_steps is None else int(train_steps)
         torch.save({**d, "epsilon": c["epsilon"], "global_episode_count": c["episodes"],
                     "current_generation_active": self.current_generation,
-                    "done_generations_count": self.done_generations, "train_steps_count": c["train_steps"],
+                    "done_generations_count": self.done_generations, "train_steps_count": ts,
                     "old_state_for_reset": checkpoint.cpu_state(self.old_state)}, self.latest)
 
-    def _maybe_save_latest(self, c):
-        if self._next_save is not None and c["train_steps"] >= self._next_save:
-            self.save_latest()
-            self._next_save = (c["train_steps"] // self.save_every + 1) * self.save_every
+    def _step(self):
+        """One vector step. The reference saves the latest state right after the optimizer step of
+        update number k * interval, recording train_steps_count = k * interval - 1 (the count before
+        that update's increment, :519-528). When update k * interval may fall inside this vector
+        step's U updates, the step runs its updates in runs that end exactly there (one host read of
+        the train-step count and the enable flag after the rollout: every update of a vector step
+        trains or none does) and saves between them; otherwise it is one fused device sequence."""
+        L = self.L
+        U = L.updates_per_step
+        if self._next_save is None or self._steps_hi + U < self._next_save:
+            L.step()
+            self._steps_hi += U
+            return
+        L.rollout()
+        st = L.learner.stats()["steps"]
+        enabled = bool(L.enable.item())
+        u = 0
+        while u < U:
+            run = min(U - u, self._next_save - st) if enabled else U - u
+            for _ in range(run):
+                if u:
+                    L.sample(u)
+                L.learner.update()
+                u += 1
+            if enabled:
+                st += run
+                if st == self._next_save:
+                    self.save_latest(train_steps=st - 1)
+                    self._sync_save_mark(st)
+        self._steps_hi = st
+
+    def _on_check(self, c):
+        self.L.check_status(c, self.log)
+        self._steps_hi = int(c["train_steps"])
 
     def _save_success(self, fn):
         L, c, d = self._base()
@@ -346,7 +408,7 @@ class RNNGenerations:
             for i_try in range(1, max_retries + 1):
                 log(f"  [Gen {gen}] Attempt {i_try}/{max_retries}")
                 _play_episodes(L, t["episodes_per_generation"], _Progress(L, t["win_rate_interval"], "rnn", log),
-                               self.check_every, self._maybe_save_latest)
+                               self.check_every, self._on_check, self._step)
                 log(f"  [Gen {gen}, Try {i_try}] Evaluating modelB...")
                 wA, wP = self.evaluate(rng)
                 c = L.counters()
@@ -388,3 +450,4 @@ class RNNGenerations:
             state = self.L.modelA_state_dict()
             self.log("[INFO] modelB reset to current modelA's state.")
         self.L.reset_B(state, epsilon=1.0, reset_train_steps=True)
+        self._sync_save_mark(0)

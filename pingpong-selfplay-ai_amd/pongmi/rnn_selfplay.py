@@ -3,8 +3,10 @@ arenas per device — fold + act (K5) + env / sequence store (K7) + DRQN update 
 on one stream, every loop counter in a device control block (no host synchronisation).
 
 Semantics the batching fixes (the reference steps ONE env and runs train_step_rnn once per step):
-  * one vector step = one env step in every arena, then one DRQN update of `batch` sequences once
-    the sequence buffer holds > batch * min_episodes_for_training_start episodes (:768);
+  * one vector step = one env step in every arena, then `updates_per_step` (U) DRQN updates of
+    `batch` sequences once the sequence buffer holds > batch * min_episodes_for_training_start
+    episodes (:776-777), each on its own sampled batch. U = n keeps the reference's one update per
+    env step (the generation controller's setting); U = 1 is the throughput setting;
   * modelB's acting noise is drawn fresh once per vector step and shared by all arenas (the
     reference resets it before each greedy action, :385); the update uses modelB's epsilon buffers
     as that draw left them (train_step_rnn does not reset noise);
@@ -12,9 +14,14 @@ Semantics the batching fixes (the reference steps ONE env and runs train_step_rn
   * each episode plays modelA or (p = opponent_pool_ratio) a uniformly drawn pool net (:735-736),
     every opponent in eval mode (:344, :615); both players start each episode from zero (h, c);
   * the sequence buffer keeps the latest `memory_size` episodes of length >= trace_length
-    (deque(maxlen), :104, :112-115); their steps live in per-arena rings of `depth` steps.
-    The reference's max_episode_steps cut (:751, 1000 steps) is not applied (episodes average
-    ~38 steps).
+    (deque(maxlen), :104, :112-115); their steps live in per-arena rings of `depth` steps. So that
+    no sample can reach an overwritten step, a trajectory longer than depth / 2 is not stored and
+    an episode leaves once depth / 2 steps have passed since it finished; `ring_depth` sizes depth
+    so neither happens at the expected episode lengths, and `check_status` raises / warns if the
+    device saw otherwise;
+  * max_episode_steps (:751, default 1000): an episode still running after that many steps ends
+    (counters, epsilon decay, new opponent, env.reset, zero (h, c)) while its trajectory goes on
+    collecting steps until a done, as push_step's current_episode_trajectory does.
 Sharded (world > 1): every rank owns n arenas and its own sequence buffer; the gradient (+ the
 contributing-rank count) is summed by one all-reduce per update and every rank applies the
 identical clip + Adam step (pongmi.drqn).
@@ -34,9 +41,10 @@ from .selfplay import act_chunk
 
 
 def ring_depth(n, memory_size, mean_len=40, margin=512):
-    """Steps per arena ring: the span of the newest `memory_size` episodes (~memory_size * mean_len / n
-    vector steps) with 50 % headroom, plus room for long episodes; a power of two."""
-    need = int(1.5 * memory_size * mean_len / max(n, 1)) + margin
+    """Steps per arena ring, a power of two: depth / 2 (the age an episode may reach in the buffer, and
+    the longest trajectory stored) covers the span of the newest `memory_size` episodes (~memory_size
+    * mean_len / n vector steps) with 50 % headroom, plus `margin` steps for long episodes."""
+    need = 2 * (int(1.5 * memory_size * mean_len / max(n, 1)) + margin)
     d = 64
     while d < need:
         d *= 2
@@ -47,8 +55,13 @@ class RNNSelfPlayLearner:
     def __init__(self, env_kw, n_arenas, modelB_state, modelA_state=None, pool_states=(), *, batch=64, trace_length=8,
                  memory_size=200_000, min_episodes_for_training_start=10, depth=None, gamma=0.99, lr=1e-4,
                  epsilon=1.0, min_epsilon=0.05, epsilon_decay=0.999, target_update_interval=2000, pool_ratio=0.4,
-                 grad_clip_norm=1.0, episode=0, seed=0, rank=0, world=1, allreduce=None, device=None):
+                 grad_clip_norm=1.0, episode=0, seed=0, rank=0, world=1, allreduce=None, device=None,
+                 updates_per_step=1, max_episode_steps=1000):
         self.lib = _lib.load()
+        self.updates_per_step = int(updates_per_step)
+        if self.updates_per_step < 1:
+            raise ValueError("updates_per_step must be >= 1")
+        self._warned = 0
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise _lib.PongmiError("RNNSelfPlayLearner runs on a ROCm device only")
@@ -67,6 +80,7 @@ class RNNSelfPlayLearner:
         self.opp = torch.zeros(n, dtype=torch.int32, device=dev)
         self.ep_reward = torch.zeros(n, **f32)
         self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.ep_steps = torch.zeros(n, dtype=torch.int32, device=dev)
         self.reset = torch.ones(n, dtype=torch.uint8, device=dev)
         self.hA, self.cA, self.hB, self.cB = (torch.zeros((n, 128), **f32) for _ in range(4))
         self.obsA = torch.zeros((n, 7), **f32)
@@ -76,6 +90,7 @@ class RNNSelfPlayLearner:
         # ---- sequence buffer
         self.trans = torch.zeros((self.depth, n, PM_TRANS_F), **f32)
         self.seq_eps = torch.zeros((self.cap, 2), dtype=torch.int64, device=dev)
+        self.seq_mark = torch.zeros(self.depth, dtype=torch.int64, device=dev)
         self.fin = torch.zeros((((n + 255) // 256) * 256, 2), dtype=torch.int64, device=dev)  # staging
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
         self.opp_list = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -101,11 +116,13 @@ class RNNSelfPlayLearner:
         sp = _lib.RnnSelfPlay()
         sp.env = env_params(**env_kw)
         sp.st = _lib.EnvState(*[ptr(self.f64[k]) for k in range(7)], *[ptr(self.i32[k]) for k in range(4)])
-        for name in ("opp", "ep_reward", "ep_len", "reset", "w_opp", "w_B", "hA", "cA", "hB", "cB", "obsA", "obsB", "aA",
-                     "aB", "trans", "seq_eps", "fin", "partials", "opp_list", "opp_cnt", "enable", "ctrl"):
+        for name in ("opp", "ep_reward", "ep_len", "ep_steps", "reset", "w_opp", "w_B", "hA", "cA", "hB", "cB", "obsA",
+                     "obsB", "aA", "aB", "trans", "seq_eps", "seq_mark", "fin", "partials", "opp_list", "opp_cnt",
+                     "enable", "ctrl"):
             setattr(sp, name, ptr(getattr(self, name)))
         sp.paramsB = ptr(self.learner.params)
         sp.n, sp.n_pool, sp.depth, sp.T = n, self.n_pool, self.depth, self.T
+        sp.max_steps = int(max_episode_steps or 0)
         p_pool = pool_ratio if self.n_pool else 0.0
         sp.chunk_A = act_chunk(1.0 - p_pool, cap=2048)
         sp.chunk_P = act_chunk(p_pool / self.n_pool, cap=2048) if self.n_pool else 256
@@ -132,16 +149,44 @@ class RNNSelfPlayLearner:
         check(self.lib.pm_rnn_selfplay_rollout(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),
               "pm_rnn_selfplay_rollout")
 
+    def sample(self, u):
+        """Batch of update u >= 1 of the current vector step (update 0's is drawn by env_step)."""
+        check(self.lib.pm_rnn_selfplay_sample(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), int(u),
+                                              stream_ptr()), "pm_rnn_selfplay_sample")
+
     def step(self):
-        """One vector step (n env-steps on this rank) including the DRQN update when enabled."""
+        """One vector step (n env-steps on this rank) and its `updates_per_step` DRQN updates when
+        enabled."""
+        U = self.updates_per_step
         if self.world == 1:
-            check(self.lib.pm_rnn_selfplay_step(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),
-                  "pm_rnn_selfplay_step")
+            check(self.lib.pm_rnn_selfplay_step_multi(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), U,
+                                                      stream_ptr()), "pm_rnn_selfplay_step_multi")
             return
         self.rollout()
-        self.learner.grads()
-        self.allreduce(self.learner.grad)  # one RCCL all-reduce per update: 174 984 grads + rank count
-        self.learner.apply()
+        for u in range(U):
+            if u:
+                self.sample(u)
+            self.learner.grads()
+            self.allreduce(self.learner.grad)  # one RCCL all-reduce per update: 174 984 grads + rank count
+            self.learner.apply()
+
+    def check_status(self, c=None, log=print):
+        """Device error bits (pm_rnn_ctrl.status): bit 0 (a sample read an overwritten ring step) means
+        corrupted training data and raises; bits 1 / 2 (episodes evicted by age / a trajectory longer
+        than depth / 2 dropped: `depth` is too small for the episode lengths seen) warn once each."""
+        st = int((c or self.counters())["status"])
+        if st & 1:
+            raise _lib.PongmiError(f"RNN sequence buffer: a sampled step had been overwritten (status {st}); "
+                                   f"depth {self.depth} is too small")
+        new = st & 6 & ~self._warned
+        if new & 2:
+            log(f"[WARNING] sequence buffer: episodes older than depth/2 = {self.depth // 2} steps were evicted "
+                f"before {self.cap} newer ones; raise depth (ring_depth) for longer episodes")
+        if new & 4:
+            log(f"[WARNING] sequence buffer: a trajectory longer than depth/2 = {self.depth // 2} steps was not "
+                f"stored; raise depth for longer rallies")
+        self._warned |= new
+        return st
 
     # ------------------------------------------------------------------ state readout (syncs)
     def counters(self):

@@ -15,7 +15,9 @@ Semantics the batching fixes (the reference steps ONE env and updates once per e
     episodes finished in a vector step (:261);
   * each episode independently plays modelA or (p = opponent_pool_ratio) a uniformly drawn pool
     net (:235-236);
-  * pushes of a vector step all receive the max priority held before the step (:57).
+  * pushes of a vector step all receive the max priority held before the step (:57): the running
+    maximum when U = 1 (exact, since n > batch pushes survive the scatter), the array maximum
+    recomputed by pm_selfplay_commit when U > 1.
 Sharded (world > 1): every rank owns n arenas and its own replay; `sp.grad` (520 head grads +
 counters) is summed by one all-reduce per update and every rank applies the identical Adam step.
 """

@@ -14,6 +14,10 @@ def parse(description, default_arenas):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--check-every", type=int, default=4, help="vector steps between episode-budget checks")
     ap.add_argument("--config", default=None, help="config file (default: the reference's name, in the CWD)")
+    ap.add_argument("--replay-ratio", type=float, default=1.0,
+                    help="updates per pushed transition (1.0 = the reference's one update per env step)")
+    ap.add_argument("--updates-per-step", type=int, default=None,
+                    help="updates per vector step (overrides --replay-ratio)")
     return ap.parse_args()
 
 

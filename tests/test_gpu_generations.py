@@ -62,8 +62,8 @@ def test_qnet_generations_promote(tmp_path):
     from pongmi.generations import QNetGenerations
     cfg, d, init = _qnet_cfg(tmp_path)
     lines = []
-    G = QNetGenerations(cfg, n_arenas=1024, seed=1, log=lines.append)
-    assert len(G.pool) == 2 and G.L.counters()["episodes"] == 7
+    G = QNetGenerations(cfg, n_arenas=512, seed=1, log=lines.append)
+    assert len(G.pool) == 2 and G.L.counters()["episodes"] == 7 and G.L.updates_per_step == 512
     G.run(rng=random.Random(0))
     assert G.done_generations == 2
     for gen in (1, 2):
@@ -79,7 +79,7 @@ def test_qnet_generations_fault_resets_b(tmp_path):
     from pongmi.generations import QNetGenerations
     cfg, d, init = _qnet_cfg(tmp_path, max_generations=1, curr_win_threshold=1.1, episodes_per_generation=150)
     lines = []
-    G = QNetGenerations(cfg, n_arenas=1024, seed=2, log=lines.append)
+    G = QNetGenerations(cfg, n_arenas=512, seed=2, log=lines.append)
     G.run(rng=random.Random(1))
     assert lines.count("未達标，继续尝试…") == 1 and "[Fault] model9-1_fault.pth" in lines
     cp = _check_qnet_ckpt(d / "model9-1_fault.pth")
@@ -90,6 +90,29 @@ def test_qnet_generations_fault_resets_b(tmp_path):
     assert all(torch.equal(got[k].cpu(), init[k]) for k in init if "epsilon" not in k)
 
 
+def test_qnet_generations_replay_ratio(tmp_path):
+    """The reference trains once per env step: a try of E episodes runs ~E x mean episode length
+    updates and its target network (interval 1000) syncs within the try. The controller's default
+    (replay_ratio 1: U = n updates per vector step) keeps that: train_steps per try equals the env
+    steps the try played, and the target follows modelB at the sync points."""
+    from pongmi.generations import QNetGenerations, _Progress, _play_episodes
+    cfg, d, init = _qnet_cfg(tmp_path, max_generations=1, episodes_per_generation=400, target_update_interval=1000,
+                             batch_size=256)
+    G = QNetGenerations(cfg, n_arenas=512, seed=4, log=lambda *_: None)
+    L = G.L
+    c0 = L.counters()
+    c = _play_episodes(L, 400, _Progress(L, 100, "qnet", lambda *_: None), G.check_every)
+    env_steps = (c["step"] - c0["step"]) * L.n
+    eps = c["episodes"] - c0["episodes"]
+    assert c["train_steps"] == env_steps  # one update per pushed transition
+    assert eps >= 400 and 15 * eps <= c["train_steps"] <= 120 * eps  # ~mean episode length (~38) per episode
+    assert c["train_steps"] >= 1000
+    from pongmi.qnet import pack_state_dict
+    p0 = pack_state_dict(G.old_state, "cpu")
+    assert not torch.equal(L.paramsT.cpu()[4672:5192], p0[4672:5192])  # the target synced with a trained modelB
+    assert c["max_prio"] == float(L.prios.max())  # U * batch >= n: the commit keeps the array maximum
+
+
 # ---------------------------------------------------------------------------------------- QNetRNN
 def _rnn_cfg(tmp_path, **kw):
     d = tmp_path / "checkpoints_rnn"
@@ -98,7 +121,7 @@ def _rnn_cfg(tmp_path, **kw):
              batch_size=32, memory_size=40000, min_episodes_for_training_start=2,
              initial_epsilon_per_generation=0.7, epsilon_decay=0.999, min_epsilon=0.05, target_update_interval=100,
              model_id_prefix="rnn_t_", init_model_path_rnn=None, ckpt_dir_rnn=str(d), opponent_pool_ratio=0.4,
-             win_rate_interval=100, save_latest_checkpoint_interval_steps=10,
+             win_rate_interval=100, save_latest_checkpoint_interval_steps=300,
              latest_checkpoint_filename="latest_rnn_training_state.pth")
     t.update(kw)
     return {"env": {**ENV, "speed_scale_every": 5, "speed_increment": 0.2}, "training": t}, d
@@ -121,7 +144,8 @@ def test_rnn_generations_promote_pool_and_resume(tmp_path):
     from pongmi.generations import RNNGenerations
     cfg, d = _rnn_cfg(tmp_path)
     lines = []
-    G = RNNGenerations(cfg, n_arenas=1024, seed=3, log=lines.append)
+    G = RNNGenerations(cfg, n_arenas=128, seed=3, log=lines.append)
+    assert G.L.updates_per_step == 128  # replay ratio 1: one DRQN update per env step
     assert G.L.n_pool == 0 and "[WARNING] Opponent pool is empty! ModelB will only train against ModelA." in lines
     G.run(rng=random.Random(2))
     assert G.done_generations == 2 and G.L.n_pool == 2  # promoted nets join the runtime pool (:855-859)
@@ -130,17 +154,17 @@ def test_rnn_generations_promote_pool_and_resume(tmp_path):
         cp = _check_rnn_ckpt(d / f"rnn_t_{gen}.pth", RNN_OK_KEYS)
         assert cp["generation"] == gen and cp["train_steps_count"] > 0
         assert _equal_sd(cp["modelA_state"], cp["modelB_state"]) and _equal_sd(cp["old_state_for_reset"], cp["modelA_state"])
-    # gen 2's redraws pick the promoted nets (slots 1..n_pool); with ~1024 episodes in flight, few of
-    # them finish within a 300-episode budget, so count the draws rather than the finished episodes
+    # gen 2's redraws pick the promoted nets (slots 1..n_pool); few of the episodes in flight finish
+    # within a 300-episode budget, so count the draws rather than the finished episodes
     assert int((G.L.opp > 0).sum()) > 0 and int(G.L.opp.max()) <= 2
     latest = _check_rnn_ckpt(d / "latest_rnn_training_state.pth", RNN_LATEST_KEYS)
-    # saved at the first budget check after each multiple of 10 train steps (one update per vector step)
-    assert latest["train_steps_count"] % 10 < 4 and latest["train_steps_count"] >= 10
+    # saved right after update k * 300, recording k * 300 - 1 as the reference does (:519-528)
+    assert latest["train_steps_count"] % 300 == 299
 
     # resume: B, A, Adam, epsilon, counters from the latest checkpoint; pool = every non-fault .pth
     torch.save({"modelB_state": latest["modelB_state"]}, d / "rnn_t_3_fault.pth")
     lines2 = []
-    G2 = RNNGenerations(cfg, n_arenas=1024, seed=4, log=lines2.append)
+    G2 = RNNGenerations(cfg, n_arenas=128, seed=4, log=lines2.append)
     assert any(s.startswith("[INFO] Resumed from latest checkpoint.") for s in lines2)
     assert G2.L.n_pool == 3 and not any("fault" in s for s in lines2 if "Loaded RNN pool model" in s)
     assert _equal_sd(G2.L.modelB_state_dict(), latest["modelB_state"])
@@ -159,7 +183,7 @@ def test_rnn_generations_fault_resets_b(tmp_path):
     cfg, d = _rnn_cfg(tmp_path, max_generations=1, max_retries_for_generation=1, curr_win_threshold=1.1,
                       episodes_per_generation=200, save_latest_checkpoint_interval_steps=0)
     lines = []
-    G = RNNGenerations(cfg, n_arenas=1024, seed=5, log=lines.append)
+    G = RNNGenerations(cfg, n_arenas=128, seed=5, log=lines.append)
     G.run(rng=random.Random(3))
     cp = _check_rnn_ckpt(d / "rnn_t_1_fault.pth", RNN_FAULT_KEYS)
     assert cp["train_steps_count"] > 0 and not (d / "latest_rnn_training_state.pth").exists()
@@ -183,12 +207,36 @@ def test_training_scripts_read_config_from_cwd(tmp_path):
     qcfg, d, _ = _qnet_cfg(tmp_path, max_generations=1, episodes_per_generation=100)
     qcfg["training"]["init_model_path"] = "checkpoints/model4-12.pth"  # relative to the CWD, as in config.yaml
     rcfg, rd = _rnn_cfg(tmp_path, max_generations=1, episodes_per_generation=100)
+    qcfg["training"]["batch_size"] = 64
     rcfg["training"]["ckpt_dir_rnn"] = "checkpoints_rnn"
     (tmp_path / "config.yaml").write_text(yaml.safe_dump(qcfg))
     (tmp_path / "config_rnn.yaml").write_text(yaml.safe_dump(rcfg))
     for script, made in (("train_iterative.py", d / "model9-1.pth"), ("train_rnn_iterative.py", rd / "rnn_t_1.pth")):
-        out = subprocess.run([sys.executable, os.path.join(scripts, script), "--arenas", "1024"], cwd=tmp_path,
+        out = subprocess.run([sys.executable, os.path.join(scripts, script), "--arenas", "256"], cwd=tmp_path,
                              capture_output=True, text=True, timeout=600)
         assert out.returncode == 0, out.stderr[-2000:]
         assert made.exists(), out.stdout[-2000:]
     assert "=== RNN Training: Generation 1/1 ===" in out.stdout
+
+
+def test_rnn_generations_replay_ratio_and_exact_saves(tmp_path):
+    """RNN controller at its defaults (64 arenas, one DRQN update per env step): train steps follow
+    the env steps once training is enabled, the target syncs (interval 100 here), and every
+    latest-state save lands exactly after update k * interval with k * interval - 1 recorded."""
+    from pongmi.generations import RNNGenerations, _Progress, _play_episodes
+    cfg, d = _rnn_cfg(tmp_path, max_generations=1, episodes_per_generation=150, save_latest_checkpoint_interval_steps=700)
+    saves = []
+    G = RNNGenerations(cfg, seed=6, log=lambda *_: None)
+    assert G.L.n == 64 and G.L.updates_per_step == 64
+    orig = G.save_latest
+    G.save_latest = lambda train_steps=None: (saves.append((train_steps, G.L.learner.stats()["steps"])),
+                                              orig(train_steps))
+    L = G.L
+    target0 = L.learner.target.cpu().clone()
+    c = _play_episodes(L, 150, _Progress(L, 100, "rnn", lambda *_: None), G.check_every, G._on_check, G._step)
+    st = L.learner.stats()["steps"]
+    assert st % 64 == 0 and st >= 150 * 10 and st <= c["step"] * 64
+    assert saves and all(ts == after - 1 and after % 700 == 0 for ts, after in saves)
+    assert len(saves) == st // 700
+    assert not torch.equal(L.learner.target.cpu(), target0)  # synced every 100 updates (interval)
+    assert c["status"] == 0

@@ -42,20 +42,24 @@ def _learner(golden, n=256, n_pool=2, **kw):
 def _snap(L):
     torch.cuda.synchronize()
     t = lambda x: x.detach().cpu().numpy().copy()  # noqa: E731
-    return dict(f64=t(L.f64), i32=t(L.i32), opp=t(L.opp), er=t(L.ep_reward), el=t(L.ep_len), reset=t(L.reset),
+    return dict(f64=t(L.f64), i32=t(L.i32), opp=t(L.opp), er=t(L.ep_reward), el=t(L.ep_len), es=t(L.ep_steps),
+                reset=t(L.reset),
                 obsA=t(L.obsA), obsB=t(L.obsB), hA=L.hA.clone(), cA=L.cA.clone(), hB=L.hB.clone(), cB=L.cB.clone(),
                 ctrl=L.counters())
 
 
-def test_rnn_selfplay_steps_match_oracle(golden, orc):
+@pytest.mark.parametrize("max_steps", [1000, 24])
+def test_rnn_selfplay_steps_match_oracle(golden, orc, max_steps):
+    """max_steps = 24 exercises the max_episode_steps cut (:751): the episode ends (new opponent,
+    serve, zero (h, c), counters) but the trajectory goes on until a done."""
     from pongmi import rnn
     L = _learner(golden, n=256, n_pool=2, epsilon=0.0, min_epsilon=0.0, pool_ratio=0.5,
-                 min_episodes_for_training_start=10 ** 6, memory_size=4096, seed=3)
+                 min_episodes_for_training_start=10 ** 6, memory_size=4096, seed=3, max_episode_steps=max_steps)
     n, sp = L.n, L.sp
     pv = orc.env_params_from_kwargs(**ENV_KW)
     P = orc.make_params(pv)
     names = ("x", "y", "vx", "vy", "spin", "top", "bot")
-    finished = 0
+    finished = cut = long_traj = 0
     for k in range(60):
         pre = _snap(L)
         L.step()
@@ -91,6 +95,7 @@ def test_rnn_selfplay_steps_match_oracle(golden, orc):
         assert np.array_equal(oB, pre["obsB"]) and np.array_equal(oA, pre["obsA"])
         nA, nB, rew, done = orc.step_arenas(P, arr, aA.astype(np.int8), aB.astype(np.int8))
         d = done.astype(bool)
+        e = d | (pre["es"] + 1 >= max_steps)  # episode end: done or the step cut
         rows = L.trans[k % L.depth].cpu().numpy()
         assert np.array_equal(rows[:, 0:7], oB) and np.array_equal(rows[:, 7], rew[:, 1])
         assert np.array_equal(rows[:, 8:15], nB)
@@ -104,24 +109,31 @@ def test_rnn_selfplay_steps_match_oracle(golden, orc):
         use_pool = orc.u53(q[0], q[1]) < sp.pool_ratio
         newopp = np.where(use_pool, 1 + orc.below(q[2], L.n_pool), 0)
         vx, vy, spn = orc.philox_serve(pv, np.arange(n), ns, sp.seed_env)
-        assert np.array_equal(post["opp"][d], newopp[d]) and np.array_equal(post["opp"][~d], pre["opp"][~d])
-        assert np.all(post["er"][d] == 0) and np.array_equal(post["er"][~d], er[~d])
-        assert np.all(post["el"][d] == 0) and np.array_equal(post["el"][~d], ln[~d])
-        assert np.array_equal(post["reset"].astype(bool), d)
-        assert np.all(post["i32"][3][d] == ns[d] + 1) and np.array_equal(post["i32"][3][~d], ns[~d])
-        np.testing.assert_allclose(post["f64"][2][d], vx[d], rtol=4e-16, atol=1e-18)
-        np.testing.assert_allclose(post["f64"][3][d], vy[d], rtol=4e-16, atol=1e-18)
-        assert np.array_equal(post["f64"][4][d], spn[d]) and np.all(post["f64"][0][d] == 0.5)
+        assert np.array_equal(post["opp"][e], newopp[e]) and np.array_equal(post["opp"][~e], pre["opp"][~e])
+        assert np.all(post["er"][e] == 0) and np.array_equal(post["er"][~e], er[~e])
+        assert np.all(post["el"][d] == 0) and np.array_equal(post["el"][~d], ln[~d])  # trajectory: done only
+        assert np.all(post["es"][e] == 0) and np.array_equal(post["es"][~e], pre["es"][~e] + 1)
+        assert np.array_equal(post["reset"].astype(bool), e)
+        assert np.all(post["i32"][3][e] == ns[e] + 1) and np.array_equal(post["i32"][3][~e], ns[~e])
+        np.testing.assert_allclose(post["f64"][2][e], vx[e], rtol=4e-16, atol=1e-18)
+        np.testing.assert_allclose(post["f64"][3][e], vy[e], rtol=4e-16, atol=1e-18)
+        assert np.array_equal(post["f64"][4][e], spn[e]) and np.all(post["f64"][0][e] == 0.5)
         for j, nm in enumerate(names):
-            assert np.array_equal(post["f64"][j][~d], arr[nm][~d]), nm
+            assert np.array_equal(post["f64"][j][~e], arr[nm][~e]), nm
         c0, c1 = pre["ctrl"], post["ctrl"]
-        assert c1["step"] == c0["step"] + 1 and c1["episodes"] == c0["episodes"] + d.sum()
-        assert c1["ep_A"] - c0["ep_A"] == (d & (pre["opp"] == 0)).sum()
-        assert c1["win_A"] - c0["win_A"] == (d & (pre["opp"] == 0) & (er > 0)).sum()
-        assert c1["ep_P"] - c0["ep_P"] == (d & (pre["opp"] != 0)).sum()
+        assert c1["step"] == c0["step"] + 1 and c1["episodes"] == c0["episodes"] + e.sum()
+        assert c1["ep_A"] - c0["ep_A"] == (e & (pre["opp"] == 0)).sum()
+        assert c1["win_A"] - c0["win_A"] == (e & (pre["opp"] == 0) & (er > 0)).sum()
+        assert c1["ep_P"] - c0["ep_P"] == (e & (pre["opp"] != 0)).sum()
         assert c1["seq_count"] - c0["seq_count"] == (d & (ln >= L.T)).sum()
         finished += int(d.sum())
-    assert finished > 50  # episodes did end and restart during the run
+        cut += int((e & ~d).sum())
+        long_traj = max(long_traj, int(ln[d].max()) if d.any() else 0)
+    assert finished > (50 if max_steps == 1000 else 10)  # episodes did end and restart during the run
+    if max_steps < 1000:
+        assert cut > 100 and long_traj > max_steps  # cuts happened; a stored trajectory spanned a cut
+    else:
+        assert cut == 0
     assert L.counters()["train_steps"] == 0
 
 
@@ -196,3 +208,60 @@ def test_two_ranks_stay_identical(golden):
     assert both > 10
     assert not torch.equal(Ls[0].trans, Ls[1].trans)  # different arenas per rank
     assert Ls[0].learner.stats()["steps"] == Ls[1].learner.stats()["steps"] > 0
+
+
+def test_rnn_ring_safety(golden):
+    """A ring too shallow for the episodes (depth 64: trajectories up to 32 steps, episodes leave
+    the buffer 32 steps after they finish): nothing a sample reads was overwritten (status bit 0
+    never set), every held episode is intact in its ring, long trajectories are dropped (bit 2) and
+    age eviction is reported (bit 1); check_status raises only on bit 0."""
+    from pongmi import _lib
+    L = _learner(golden, n=512, n_pool=1, epsilon=0.3, memory_size=100_000, min_episodes_for_training_start=1,
+                 seed=6, depth=64)
+    for _ in range(150):
+        L.step()
+    c = L.counters()
+    assert c["status"] & 1 == 0 and c["status"] & 2 and c["seq_size"] < c["seq_count"] < 100_000
+    now = c["step"]
+    ring = L.trans.cpu().numpy()
+    for arena, start, length in L.episodes().numpy():
+        assert _storable(length, L) and now - 1 - start < L.depth
+        rec = ring[(start + np.arange(length)) % L.depth, arena]
+        bits = rec[:, 15].view(np.int32)
+        assert np.all(bits[:-1] >> 8 == 0) and bits[-1] >> 8 == 1
+    msgs = []
+    L.check_status(log=msgs.append)
+    assert any("evicted" in m for m in msgs)
+    L.set_counters(status=1)
+    with pytest.raises(_lib.PongmiError):
+        L.check_status(log=msgs.append)
+
+
+def _storable(length, L):
+    return L.T <= length <= L.depth // 2
+
+
+def test_rnn_updates_per_step(golden):
+    """U = 3 DRQN updates per vector step, each on its own batch (Philox counter (step, u)): the fused
+    pm_rnn_selfplay_step_multi equals rollout + update + (sample(u) + update) x 2 bit for bit, and
+    train steps advance by U per enabled step."""
+    U = 3
+    A = _learner(golden, n=1024, n_pool=1, epsilon=0.5, memory_size=2000, min_episodes_for_training_start=1, seed=4,
+                 updates_per_step=U)
+    B = _learner(golden, n=1024, n_pool=1, epsilon=0.5, memory_size=2000, min_episodes_for_training_start=1, seed=4)
+    enabled = 0
+    for _ in range(50):
+        A.step()
+        B.rollout()
+        B.learner.update()
+        obs0 = B.learner.obs.clone()
+        for u in range(1, U):
+            B.sample(u)
+            if B.counters()["train"]:
+                assert not torch.equal(B.learner.obs, obs0)  # a fresh batch per update
+            B.learner.update()
+        enabled += B.counters()["train"]
+    torch.cuda.synchronize()
+    assert torch.equal(A.learner.params, B.learner.params) and torch.equal(A.trans, B.trans)
+    assert A.counters() == B.counters()
+    assert enabled > 10 and A.learner.stats()["steps"] == U * enabled

@@ -10,13 +10,17 @@ push + proportional sample, double-DQN update with target net, Adam), weak-scale
 A step = one vector step: every arena on every rank advances one env step and every rank runs one
 PER update of batch 256. value = total env-steps (all ranks) / max-over-ranks wall time of K steps.
 Rank 0 prints one JSON line. Also reported:
-  roofline      the matrix-core act kernel of the production step, k_act_sp(PM_ACT_B): modelB's QNet
-                forward for every arena + eps-greedy, plus the PER sample blocks (the opponents' act
-                rides in the learner's launch), timed with HIP events on the stream it runs on around
-                every 20th step of the timed region (the others run uninstrumented): FP32 FLOP/s vs
-                the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per launch from the
-                committed counter profile (profiles/r1_pmc.json, same workload), null without it
-  env_roofline  k_env (env tick + replay push + bookkeeping, 282 algorithmic B / env-step) vs 8 TB/s
+  roofline      the production step's first kernel, k_actenv (pm_selfplay_actenv): modelB's QNet
+                forward for every arena on the matrix cores fused with the env tick, replay push and
+                bookkeeping of the same arenas, plus the PER sample + batch-forward blocks (the
+                opponents' act rides in the learner's launch), timed with HIP events on the stream it
+                runs on around every 20th step of the timed region (the others run uninstrumented):
+                FP32 FLOP/s vs the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per
+                launch from the committed counter profile (profiles/r2_pmc.json, same workload), null
+                without it
+  env_roofline  the same k_actenv launch seen as HBM work: 282 algorithmic B / env-step vs 8 TB/s
+  learn_us      the second launch: k_learn (single-workgroup double-DQN update + Adam + sum-tree
+                refresh) with the next step's opponent act on the other CUs; latency-bound
   act_full_roofline  k_act_sp with both players' act (+ the PER sample blocks) in one launch
                 (PM_ACT_ALL), back to back after the timed region (N=1 only)
   env_step_roofline  K1 (pm_env_step, autoreset of done arenas) alone at the same n: 203 B / env-step
@@ -53,7 +57,7 @@ PEAK_HBM_GBS = 8000.0
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` (`name`, or `name@grid` for one of its launch grids) from the
     committed rocprofv3 counter profile, or None."""
-    path = os.path.join(ROOT, "profiles", "r1_pmc.json")
+    path = os.path.join(ROOT, "profiles", "r2_pmc.json")
     try:
         with open(path) as fh:
             return json.load(fh)["kernels"][kernel]["hbm_bytes"]
@@ -318,17 +322,16 @@ def main():
         if ev is None:  # the production path: the overlapped vector step (L.step)
             L.step()
             return
-        # instrumented step: the production step's kernels (pm_selfplay_step_overlap), bracketed for
-        # the per-kernel rooflines: k_act_sp side B (+ PER sample blocks), k_env, then the learner
-        # launch that also acts for the next step's opponents
+        # instrumented step: the production step's launches (pm_selfplay_step_overlap) bracketed one
+        # by one: k_actenv (act B + env + PER sample / batch forward), then the learner launch that
+        # also acts for the next step's opponents
         if not L._aA_ready:
             L.act(_lib.PM_ACT_A)
         ev[0].record()
-        L.act(_lib.PM_ACT_B)
+        L.actenv()
         ev[1].record()
-        L.env_step()
-        ev[2].record()
         L.learn(act_next=True)
+        ev[2].record()
         if dist is not None:
             dist.all_reduce(L.grad)
         L.apply()
@@ -336,7 +339,7 @@ def main():
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
-    # every INSTR-th step of the timed region carries HIP events around k_act_sp and k_env (an event
+    # every INSTR-th step of the timed region carries HIP events around its two launches (an event
     # marker costs GPU time on ROCm; bracketing every step would slow the loop ~15 %)
     inst = set(range(0, args.steps, INSTR))
     evs = {k: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for k in inst}
@@ -354,15 +357,16 @@ def main():
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    act_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
-    env_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)
+    ae_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
+    learn_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)
     c = L.counters()
 
     if rank == 0:
         total = args.arenas * world * args.steps
         value = total / dt
-        achieved = args.arenas * FLOP_PER_ARENA / act_s / 1e12
-        env_gbs = args.arenas * SP_ENV_BYTES / env_s / 1e9
+        achieved = args.arenas * FLOP_PER_ARENA / ae_s / 1e12
+        env_gbs = args.arenas * SP_ENV_BYTES / ae_s / 1e9
+        ae_grid = (args.batch + 63) // 64 + (args.arenas + 255) // 256
         out = {
             "metric": "env-steps/sec (whole node) at 65536 arenas, 1/2/4/8 GPUs; CPU-ref baseline",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -374,16 +378,19 @@ def main():
                        "arenas_per_gpu": args.arenas, "global_arenas": args.arenas * world,
                        "pool": args.pool, "batch": args.batch, "updates_per_vector_step": 1,
                        "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)"},
-            "roofline": {"bound": "mfma", "kernel": "k_act_sp (PM_ACT_B: modelB's act + the PER sample blocks)",
+            "roofline": {"bound": "mfma", "kernel": "k_actenv (modelB's act + env tick + replay push + PER sample "
+                                                    "and batch-forward blocks)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": pmc_traffic(f"k_act_sp@{((args.batch + 3) // 4 + (args.arenas + 255) // 256) * 256}"),
-                         "avg_us": round(act_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
-            "env_roofline": {"bound": "hbm", "kernel": "k_env", "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS,
+                         "traffic": pmc_traffic(f"k_actenv@{ae_grid * 256}"),
+                         "avg_us": round(ae_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
+            "env_roofline": {"bound": "hbm", "kernel": "k_actenv (the same launch as HBM work)",
+                             "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS,
                              "unit": "GB/s", "frac": round(env_gbs / PEAK_HBM_GBS, 4),
-                             "traffic": pmc_traffic("k_env"),
-                             "avg_us": round(env_s * 1e6, 2), "bytes_per_env_step": SP_ENV_BYTES},
+                             "traffic": pmc_traffic(f"k_actenv@{ae_grid * 256}"),
+                             "avg_us": round(ae_s * 1e6, 2), "bytes_per_env_step": SP_ENV_BYTES},
+            "learn_us": round(learn_s * 1e6, 2),
             "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
                         "last_loss": c["last_loss"]},
         }

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 7
+#define PM_ABI_VERSION 8
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -442,8 +442,12 @@ int pm_selfplay_step(const pm_selfplay* sp, void* stream);
  *     epsilon-greedy act (select_action_B, :124-130) only; PM_ACT_A = side A only.
  *   pm_selfplay_learn_act: pm_selfplay_learn, plus side-A actions for the observations the last
  *     pm_selfplay_env wrote (the next vector step's), into sp->aA.
- *   pm_selfplay_step_overlap = act_part(B) + env + learn_act + apply (unsharded).
- * Contract: before act_part(B) / step_overlap, sp->aA must hold side-A actions for the current
+ *   pm_selfplay_actenv: act_part(B) + env fused into one launch (k_actenv): every 256-arena block
+ *     computes modelB's greedy actions for its arenas on the matrix cores and ticks them; the PER
+ *     sampler blocks also compute the batch rows k_env's forward blocks would. Bit-identical to
+ *     act_part(B) + env.
+ *   pm_selfplay_step_overlap = actenv + learn_act + apply (unsharded).
+ * Contract: before act_part(B) / actenv / step_overlap, sp->aA must hold side-A actions for the current
  * observations (pm_selfplay_act_part(A), or learn_act after the last env). Results are
  * bit-identical to pm_selfplay_step. */
 #define PM_ACT_ALL 0
@@ -451,6 +455,7 @@ int pm_selfplay_step(const pm_selfplay* sp, void* stream);
 #define PM_ACT_A 2
 int pm_selfplay_act_part(const pm_selfplay* sp, int32_t part, void* stream);
 int pm_selfplay_learn_act(const pm_selfplay* sp, void* stream);
+int pm_selfplay_actenv(const pm_selfplay* sp, void* stream);
 int pm_selfplay_step_overlap(const pm_selfplay* sp, void* stream);
 
 /* Replay ratio: U >= 1 double-DQN updates per vector step. The reference trains once per env step
@@ -464,7 +469,7 @@ int pm_selfplay_step_overlap(const pm_selfplay* sp, void* stream);
  *     prios.max(), :57 — U * batch >= n scatters can lower the array maximum below the running
  *     maximum the U = 1 step tracks), the sum tree's nodes over the next push range, pos/size/step.
  * PM_UPD_FIRST | PM_UPD_LAST is the U = 1 update (pm_selfplay_learn / pm_selfplay_apply).
- * pm_selfplay_step_multi = act_part(B) + env + learn_ex(FIRST, side-A act) + (U - 1) x [resample +
+ * pm_selfplay_step_multi = actenv + learn_ex(FIRST, side-A act) + (U - 1) x [resample +
  * learn_ex(0)] + commit, unsharded, under step_overlap's contract (sp->aA holds side-A actions for
  * the current observations); U = 1 is pm_selfplay_step_overlap. Sharded callers run the same sequence
  * with an all-reduce of sp->grad and pm_selfplay_apply_ex after every learn_ex. */

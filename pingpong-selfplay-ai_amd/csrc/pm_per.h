@@ -161,131 +161,205 @@ __device__ __forceinline__ double per_chunk_sum(const PerTree& t, int64_t c) {
     return acc;
 }
 
-// One value per lane: the first lane whose running sum exceeds t (searchsorted 'right'); if rounding
-// leaves t at or past the wave's total, the last nonzero lane. `before` = running sum in front of it.
-__device__ inline int lane_find(double v, double t, int lane, double& before, double& val) {
-    const double incl = wave_incl_scan(v, lane);
+// ----------------------------------------------------------------------------- block sampler
+// PrioritizedReplay.sample (scripts/train_iterative.py:64-73): np.random.choice(p) picks the first
+// index whose running sum of p exceeds u (searchsorted 'right'). Here a 256-thread block draws
+// PER_BS = 64 samples at once, descending the tree in three dependent load round trips:
+//   level 2: the block loads every chunk sum once (4 per thread), forms their inclusive prefix in LDS
+//            (one block scan) and each sample binary-searches it for t = u * total;
+//   level 1: 4 lanes per sample read the chosen chunk's 16 sub sums (4 each), a 4-lane scan finds
+//            the sub-block;
+//   level 0: the same 4 lanes read its 64 leaves (16 each, one float4 x4 load) and find the entry.
+// Compared with one wave per sample, the block does the top-level scan once for 64 samples: the
+// wave-wide scans of <= 1024 chunk sums per sample were VALU work that starved beside the act's MFMA
+// streams. Every sum has a fixed order, so a sample is a pure function of (tree, u). When rounding
+// leaves the target at or past a node's running total, the last nonzero child is taken (as before).
+constexpr int PER_BS = 64;       // samples per 256-thread block
+constexpr int PER_ROUND = 1024;  // chunk sums per prefix round (capacities <= 1M: one round)
+
+struct PerSampleSmem {
+    double incl[PER_ROUND];  // inclusive prefix of the round's chunk sums (plus the earlier rounds)
+    double wsum[4];
+};
+
+// The round's inclusive prefix of chunk sums [c0, c0 + 1024) into sm.incl, offset by base; returns
+// the running total after the round. v: this thread's 4 chunk sums (chunks c0 + 4t .. 4t + 3).
+__device__ inline double per_round_prefix(const double (&v)[4], double base, PerSampleSmem& sm) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    double run[4], acc = 0.0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { acc += v[e]; run[e] = acc; }
+    const double incl = wave_incl_scan(acc, lane);
     double excl = __shfl_up(incl, 1);
     if (lane == 0) excl = 0.0;
-    const unsigned long long hit = __ballot(incl > t);
-    int L;
-    if (hit) {
-        L = __ffsll((long long)hit) - 1;
-    } else {
-        const unsigned long long nz = __ballot(v > 0.0);
-        L = nz ? 63 - __clzll((long long)nz) : 0;
-    }
-    before = __shfl(excl, L);
-    val = __shfl(v, L);
-    return L;
-}
-
-// Level-2 search helpers: 16 chunk sums per lane (one load round trip per 1024 chunks).
-__device__ inline int chunk_find(const double (&vals)[16], double part, double incl, double run, double t, int lane,
-                                 double& before) {
-    const unsigned long long hit = __ballot(run + incl > t);
-    if (!hit) return -1;
-    const int L = __ffsll((long long)hit) - 1;
-    double base = run + (incl - part), bef = base, lastbef = base;
-    int found = -1, lastnz = -1;
+    if (lane == 63) sm.wsum[wv] = incl;
+    __syncthreads();
+    double wb = base;
+    for (int w = 0; w < wv; ++w) wb += sm.wsum[w];
+    const double ex = wb + excl;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        if (found < 0 && base + vals[e] > t) { found = e; bef = base; }
-        if (vals[e] > 0.0) { lastnz = e; lastbef = base; }
-        base += vals[e];
-    }
-    if (found < 0) { found = lastnz; bef = lastbef; }  // rounding: lane sum fell short of its scan
-    found = __shfl(found, L);
-    before = __shfl(bef, L);
-    return found < 0 ? -1 : L * 16 + found;
+    for (int e = 0; e < 4; ++e) sm.incl[4 * t + e] = ex + run[e];
+    const double tot = ((base + sm.wsum[0]) + sm.wsum[1]) + sm.wsum[2] + sm.wsum[3];
+    __syncthreads();
+    return tot;
 }
 
-// One wave per sample: idx and the un-normalised IS weight (size * P(i))^-beta for the uniform u.
-// Descends chunk sums (scan of <= 1024 per round trip) -> the chunk's 16 level-1 sums -> the 64
-// leaves of one sub-block: three dependent load round trips for capacities up to 1M.
-// Leaves inside the pending push range read as pr.pval (the push kernel may be writing them).
-__device__ inline void per_sample_one(int64_t size, const PerTree& tr, const PushRange& pr, double beta, double u,
-                                      int64_t& idx_out, float& wraw_out) {
-    const int lane = threadIdx.x & 63;
+// First k in [0, n) with sm.incl[k] > x (n if none).
+__device__ __forceinline__ int per_lds_search(const PerSampleSmem& sm, int n, double x) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sm.incl[mid] > x) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+// 4-lane group search over the group's 4 x NV values (lane q of the group holds values
+// [NV q, NV q + NV) in v, in order): the first value whose running sum exceeds x, else the last
+// nonzero one. Returns its index in [0, 4 NV) (every lane of the group), `before` = running sum in
+// front of it, `val` = the value.
+template <int NV>
+__device__ __forceinline__ int per_group_find(const double (&v)[NV], double x, double& before, double& val) {
+    const int lane = threadIdx.x & 63, q = lane & 3, g0 = lane & ~3;
+    double acc = 0.0;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) acc += v[e];
+    const double s0 = __shfl(acc, g0), s1 = __shfl(acc, g0 + 1), s2 = __shfl(acc, g0 + 2);
+    const double ex = q == 0 ? 0.0 : (q == 1 ? s0 : (q == 2 ? s0 + s1 : (s0 + s1) + s2));
+    int hit = -1, nz = -1;
+    double hb = 0.0, hv = 0.0, nb = 0.0, nv = 0.0, run = ex;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+        if (hit < 0 && run + v[e] > x) { hit = e; hb = run; hv = v[e]; }
+        if (v[e] > 0.0) { nz = e; nb = run; nv = v[e]; }
+        run += v[e];
+    }
+    const unsigned gh = (unsigned)(__ballot(hit >= 0) >> g0) & 15u;
+    const unsigned gn = (unsigned)(__ballot(nz >= 0) >> g0) & 15u;
+    int src, k;
+    if (gh) {
+        src = __ffs(gh) - 1;
+        k = hit;
+    } else {
+        src = gn ? 31 - __clz(gn) : 0;
+        k = nz < 0 ? 0 : nz;
+        hb = nz < 0 ? ex : nb;
+        hv = nz < 0 ? 0.0 : nv;
+    }
+    // every lane computed its candidate; take lane src's (the branch above is group-uniform)
+    const int kk = __shfl(k, g0 + src);
+    before = __shfl(hb, g0 + src);
+    val = __shfl(hv, g0 + src);
+    return src * NV + kk;
+}
+
+// Block-wide (256 threads, block-uniform arguments): samples j0 .. j0 + 63 (those < bs) with uniforms
+// ufn(j), un-normalised IS weights (size * P(i))^-beta. Leaves inside the pending push range read as
+// pr.pval (the push kernel may be writing them). out(j, idx, w) is called once per sample. For
+// capacities <= 1M the chunk sums are loaded before `active` is tested (the caller's control-block
+// read and these loads share one round trip); !active returns with nothing written.
+template <class UFn, class OutFn>
+__device__ inline void per_sample_block(bool active, int64_t size, const PerTree& tr, const PushRange& pr, double beta,
+                                        int j0, int bs, PerSampleSmem& sm, UFn ufn, OutFn out) {
+    const int t = threadIdx.x, q = t & 3;
+    const int j = j0 + (t >> 2);
+    const bool one_round = tr.nchunk <= PER_ROUND;  // kernel-argument uniform
+    double vc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (one_round) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t c = 4 * t + e;
+            vc[e] = c < tr.nchunk ? tr.chunk[c] : 0.0;
+        }
+        asm volatile("" ::"v"(vc[0]), "v"(vc[1]), "v"(vc[2]), "v"(vc[3]));
+    }
+    if (!active) return;  // block-uniform
     const int64_t nb = (size + PER_CHUNK - 1) / PER_CHUNK;
-    // level 2: totals and the chunk
-    double total, before = 0.0, t;
-    int64_t blk = -1;
-    if (nb <= 1024) {  // capacity <= 1M: one round trip, totals and search from the same registers
-        double vals[16];
+    const double u = j < bs ? ufn(j) : 0.0;
+    // level 2
+    double total = 0.0;
+    if (nb > PER_ROUND) {  // capacities > 1M: the total first, one pass over the rounds
+        for (int64_t c0 = 0; c0 < nb; c0 += PER_ROUND) {
+            double v[4];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int64_t c = (int64_t)lane * 16 + e;
-            vals[e] = c < nb ? tr.chunk[c] : 0.0;
-        }
-        double part = 0.0;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) part += vals[e];
-        const double incl = wave_incl_scan(part, lane);
-        total = __shfl(incl, 63);
-        t = u * total;
-        blk = chunk_find(vals, part, incl, 0.0, t, lane, before);
-        PM_BLK(4);
-    } else {
-        total = 0.0;
-        for (int64_t c0 = 0; c0 < nb; c0 += 1024) {
-            double part = 0.0;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int64_t c = c0 + (int64_t)lane * 16 + e;
-                part += c < nb ? tr.chunk[c] : 0.0;
+            for (int e = 0; e < 4; ++e) {
+                const int64_t c = c0 + 4 * t + e;
+                v[e] = c < nb ? tr.chunk[c] : 0.0;
             }
-            total += wave_sum(part);
-        }
-        t = u * total;
-        double run = 0.0;
-        for (int64_t c0 = 0; c0 < nb && blk < 0; c0 += 1024) {
-            double vals[16];
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int64_t c = c0 + (int64_t)lane * 16 + e;
-                vals[e] = c < nb ? tr.chunk[c] : 0.0;
-            }
-            double part = 0.0;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) part += vals[e];
-            const double incl = wave_incl_scan(part, lane);
-            const double tot = __shfl(incl, 63);
-            if (run + tot > t) {
-                double b;
-                const int k = chunk_find(vals, part, incl, run, t, lane, b);
-                if (k >= 0) { blk = c0 + k; before = b; }
-            }
-            run += tot;
+            total = per_round_prefix(v, total, sm);
         }
     }
-    if (blk < 0) {  // u * total rounded up to the total: the last nonzero chunk (rare)
-        for (int64_t c0 = ((nb - 1) / 64) * 64; c0 >= 0 && blk < 0; c0 -= 64) {
-            const int64_t c = c0 + lane;
-            const unsigned long long nz = __ballot(c < nb && tr.chunk[c] > 0.0);
-            if (nz) blk = c0 + 63 - __clzll((long long)nz);
+    int64_t blk = -1, lastnz = 0;
+    double before = 0.0, lastbef = 0.0, x = 0.0, run = 0.0;
+    for (int64_t c0 = 0; c0 < nb; c0 += PER_ROUND) {
+        double v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t c = c0 + 4 * t + e;
+            v[e] = c < nb ? (one_round ? vc[e] : tr.chunk[c]) : 0.0;
         }
-        if (blk < 0) blk = 0;
-        before = 0.0;
-        for (int64_t c = 0; c < blk; ++c) before += tr.chunk[c];
+        const double end = per_round_prefix(v, run, sm);
+        if (nb <= PER_ROUND) total = end;
+        x = u * total;
+        const int n = (int)(nb - c0 < PER_ROUND ? nb - c0 : PER_ROUND);
+        if (blk < 0 && end > run) {
+            const int k = per_lds_search(sm, n, x);
+            if (k < n) {
+                blk = c0 + k;
+                before = k ? sm.incl[k - 1] : run;
+            } else {  // last nonzero chunk of the round: the first to reach the round's end value
+                int lo = 0, hi = n - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sm.incl[mid] >= sm.incl[n - 1]) hi = mid;
+                    else lo = mid + 1;
+                }
+                lastnz = c0 + lo;
+                lastbef = lo ? sm.incl[lo - 1] : run;
+            }
+        }
+        run = end;
+        __syncthreads();  // sm.incl is rewritten by the next round
     }
-    // level 1: the chunk's 16 sub-block sums
+    if (blk < 0) { blk = lastnz; before = lastbef; }
+    PM_BLK(4);
+    // level 1: the chunk's 16 sub sums, 4 per lane of the sample's group
+    double sv[4];
+    const int64_t s0 = blk * PER_FAN + 4 * q;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sv[e] = s0 + e < tr.nsub ? tr.sub[s0 + e] : 0.0;
     double b1, v1;
-    const int64_t s0 = blk * PER_FAN;
-    const double sv = (lane < PER_FAN && s0 + lane < tr.nsub) ? tr.sub[s0 + lane] : 0.0;
-    const int64_t sb = s0 + lane_find(sv, t - before, lane, b1, v1);
+    const int64_t sb = blk * PER_FAN + per_group_find<4>(sv, x - before, b1, v1);
     PM_BLK(5);
-    // level 0: 64 leaves
-    const int64_t e = sb * PER_SUB + lane;
-    const double pv = e < size ? (double)per_leaf(tr.leaf, e, pr) : 0.0;
+    // level 0: the sub-block's 64 leaves, 16 per lane
+    double lv[16];
+    {
+        const int64_t lo = sb * PER_SUB + 16 * q;
+        float f[16];
+        if (lo + 16 <= pr.cap) {
+            const float4* p4 = reinterpret_cast<const float4*>(tr.leaf + lo);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 a = p4[k];
+                f[4 * k] = a.x; f[4 * k + 1] = a.y; f[4 * k + 2] = a.z; f[4 * k + 3] = a.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) f[k] = lo + k < pr.cap ? tr.leaf[lo + k] : 0.f;
+        }
+        const int64_t d0 = pr.dist(lo);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            int64_t d = d0 + k;
+            if (d >= pr.cap) d -= pr.cap;
+            lv[k] = lo + k < size ? (double)(d < pr.n ? pr.pval : f[k]) : 0.0;
+        }
+    }
     double b0, pa;
-    const int k = lane_find(pv, t - before - b1, lane, b0, pa);
+    const int k = per_group_find<16>(lv, x - before - b1, b0, pa);
     PM_BLK(6);
-    idx_out = sb * PER_SUB + k;
-    wraw_out = (float)pow((double)size * (pa / total), -beta);
-#ifdef PM_DIAG
-    asm volatile("" ::"v"(wraw_out));
-#endif
+    if (q == 0 && j < bs) out(j, sb * PER_SUB + k, (float)pow((double)size * (pa / total), -beta));
     PM_BLK(7);
 }
 

@@ -3,7 +3,8 @@
 // Proportional sampling as np.random.choice(p=...) does it (cdf = running sum of p_i = prio_i^alpha,
 // first index whose running sum exceeds u * total: searchsorted 'right'), restructured for HBM: a
 // streaming pass builds the sum tree of pm_per.h (fp32 leaves, 64- and 1024-entry fp64 nodes), then
-// one wave per sample descends it with wave-wide inclusive scans. Every reduction has a fixed order,
+// a 256-thread block per 64 samples descends it (one block-wide prefix of the chunk sums, then 4
+// lanes per sample). Every reduction has a fixed order,
 // so a sample is a pure function of (priorities, u) — no atomics anywhere.
 #include "pm_dev.h"
 #include "pm_host.h"
@@ -41,15 +42,15 @@ __global__ __launch_bounds__(256) void k_per_chunks(PerTree tr) {
 __global__ __launch_bounds__(256) void k_per_sample(int64_t size, double beta, const double* __restrict__ u, uint64_t seed,
                                                     uint64_t counter, PerTree tr, int64_t* __restrict__ idx,
                                                     float* __restrict__ w, int bs) {
-    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= bs) return;  // wave-uniform
-    double uj;
-    if (u) uj = u[j];
-    else { const U4 r = philox64((uint32_t)j, TAG_PER, counter, seed); uj = u53(r.x, r.y); }
-    int64_t i;
-    float wr;
-    per_sample_one(size, tr, PushRange{0, 0, size, 0.f}, beta, uj, i, wr);
-    if ((threadIdx.x & 63) == 0) { idx[j] = i; w[j] = wr; }
+    __shared__ PerSampleSmem sm;
+    per_sample_block(
+        true, size, tr, PushRange{0, 0, size, 0.f}, beta, (int)blockIdx.x * PER_BS, bs, sm,
+        [&](int j) {
+            if (u) return u[j];
+            const U4 r = philox64((uint32_t)j, TAG_PER, counter, seed);
+            return u53(r.x, r.y);
+        },
+        [&](int j, int64_t i, float wr) { idx[j] = i; w[j] = wr; });
 }
 
 __global__ __launch_bounds__(1024) void k_per_normalize(float* __restrict__ w, int bs) {
@@ -111,7 +112,7 @@ extern "C" int pm_per_sample(const float* prios, int64_t size, float alpha, floa
     PM_REQUIRE(((uintptr_t)work & 15) == 0, PM_E_ARG, "pm_per_sample: work must be 16-byte aligned");
     int rc = per_launch_build(prios, size, alpha, nullptr, 0, work, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_per_sample, dim3(pm_blocks(bs, 4)), dim3(256), 0, st, size, (double)beta, u, seed, counter, tr,
+    hipLaunchKernelGGL(k_per_sample, dim3(pm_blocks(bs, PER_BS)), dim3(256), 0, st, size, (double)beta, u, seed, counter, tr,
                        idx, w, bs);
     PM_LAUNCHED("k_per_sample");
     hipLaunchKernelGGL(k_per_normalize, dim3(1), dim3(1024), 0, st, w, bs);

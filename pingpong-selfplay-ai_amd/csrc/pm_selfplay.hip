@@ -2,7 +2,7 @@
 // three kernels, nothing returns to the host:
 //
 //   k_act_sp (MFMA tiles)  both players' QNet forward + eps-greedy / argmax (pm_mfma.h); its first
-//                          ceil(batch/4) blocks draw this step's PER sample (one wave per sample) off
+//                          ceil(batch/64) blocks draw this step's PER sample (64 samples per block) off
 //                          the sum tree, which already accounts for the push k_env is about to make
 //   k_env    (n lanes)     env tick + replay push + episode bookkeeping + serves
 //   k_learn  (1 WG, 1024)  Q_B(s), Q_B(s'), Q_T(s') on the matrix cores into LDS, double-DQN targets,
@@ -71,37 +71,49 @@ __device__ __forceinline__ PushRange push_of(const pm_selfplay& sp, int64_t pos,
 }  // namespace
 
 // ------------------------------------------------------------------------------------ rollout
-// PrioritizedReplay.sample (:64-73) for update sample j: proportional draw + un-normalised IS weight.
-// pending: the step's push has not landed yet (update 0, drawn beside k_env: the tree accounts for it
-// and its leaves read as the pushed value); otherwise (updates 1..U-1) the replay is as k_env left it.
-// The fill is the post-push one either way: pos/size advance only when the step commits.
-__device__ __forceinline__ void sample_wave(const pm_selfplay& sp, int j, bool pending) {
-    if (j >= sp.batch || !learner_active(sp)) return;  // wave-uniform
+// PrioritizedReplay.sample (:64-73) for update samples [64 b, 64 b + 64): proportional draw + un-normalised
+// IS weight, one 256-thread block per 64 samples (pm_per.h: per_sample_block). pending: the step's
+// push has not landed yet (update 0, drawn beside k_env: the tree accounts for it and its leaves read
+// as the pushed value); otherwise (updates 1..U-1) the replay is as k_env left it. The fill is the
+// post-push one either way: pos/size advance only when the step commits.
+__device__ __forceinline__ void sample_block(const pm_selfplay& sp, int b, bool pending, PerSampleSmem& sm,
+                                             int64_t* sidx = nullptr) {
     const pm_ctrl* c = sp.ctrl;
     const int64_t s = c->size + sp.n;
     const int64_t size = s < sp.cap ? s : sp.cap;
     const int64_t frame = c->frame_idx + 1;  // frame_idx += 1 before sampling (:136)
-    const U4 r = philox64((uint32_t)j, TAG_PER, (uint64_t)frame, sp.seed_env);
-    int64_t idx;
-    float wr;
     const PushRange pr = pending ? push_of(sp, c->pos, c->size, c->max_prio) : PushRange{0, 0, sp.cap, 0.f};
-    per_sample_one(size, per_tree(sp.per_work, sp.cap), pr, beta_of(sp, frame), u53(r.x, r.y), idx, wr);
-    if ((threadIdx.x & 63) == 0) { sp.idx[j] = idx; sp.isw[j] = wr; }
+    const uint64_t key = sp.seed_env;
+    per_sample_block(
+        size >= sp.batch, size, per_tree(sp.per_work, sp.cap), pr, beta_of(sp, frame), b * PER_BS, sp.batch, sm,
+        [&](int j) {
+            const U4 r = philox64((uint32_t)j, TAG_PER, (uint64_t)frame, key);
+            return u53(r.x, r.y);
+        },
+        [&](int j, int64_t idx, float w) {
+            sp.idx[j] = idx;
+            sp.isw[j] = w;
+            if (sidx) sidx[j - b * PER_BS] = idx;
+        });
 }
 
 // Both players act (train_iterative.py:240-241) on the matrix cores: ActGrid blocks, modelB tiles
 // with epsilon-greedy, opponent tiles grouped by net (modelA / pool) so weights are tile-uniform.
-// Blocks [0, ceil(batch/4)) sample the update's batch instead (latency-bound, hidden under the act).
+// Blocks [0, ceil(batch/64)) sample the update's batch instead (latency-bound, hidden under the act).
 // part: PM_ACT_ALL (sample + side B + side A), PM_ACT_B (sample + side B), PM_ACT_A (side A only:
 // the opponents' greedy actions depend on nothing the learner writes, so the overlapped step runs
 // them for the next vector step beside k_learn).
+union ActSpShared {
+    ActShared act;
+    PerSampleSmem per;
+};
 __global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp, int part) {
-    __shared__ __attribute__((aligned(16))) ActShared sh;
+    __shared__ __attribute__((aligned(16))) ActSpShared sh;
     PM_BLK(0);
-    const int nsb = part == PM_ACT_A ? 0 : (sp.batch + 3) / 4;
+    const int nsb = part == PM_ACT_A ? 0 : (sp.batch + PER_BS - 1) / PER_BS;
     if ((int)blockIdx.x < nsb) {
         PM_STAMP(64);
-        sample_wave(sp, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), true);
+        sample_block(sp, (int)blockIdx.x, true, sh.per);
         PM_STAMP(65);
         PM_BLK_END();
         return;
@@ -110,7 +122,7 @@ __global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp, i
     const ActGrid g{sp.n, sp.n_pool + 1, sp.chunk_A, sp.chunk_P, part == PM_ACT_A ? 0 : 1};
     const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
     const TileOut outB{sp.aB, nullptr, -1.0, 0, 0};  // greedy here; k_env applies the epsilon draw
-    act_block(sh, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, sp.w_B, sp.obsA, sp.obsB, outA, outB,
+    act_block(sh.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, sp.w_B, sp.obsA, sp.obsB, outA, outB,
               (int)blockIdx.x - nsb, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
     PM_BLK_END();
 }
@@ -131,31 +143,12 @@ __device__ __forceinline__ void batch_row_fwd(const pm_selfplay& sp, const float
     tile_heads(hf1, c2, lane, qt);
 }
 
-// Rows of the batch whose replay row is NOT in this step's push range are stable while k_env runs:
-// k_env's last ceil(2B/128) blocks compute them (one tile per wave) into hfeat [B][80] (features
-// of s | Q_B(s) 0..2, r at 3, Q_B(s') 4..6, action|done bits at 7, Q_T(s') 8..10 at 64..); k_learn
-// computes the rest. Carrying r and the bits here spares k_learn a load that depends on idx.
-// pending = false (updates 1..U-1, k_batch_fwd): no push is in flight, this block computes every row.
-__device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f, bool pending = true) {
-    __shared__ __attribute__((aligned(16))) float lw[kLwFloats];
-    __shared__ __attribute__((aligned(16))) float hf[2][264];
-    if (!learner_active(sp)) return;  // block-uniform
-    stage_frags_lds(sp.w_B, lw, f * 5);
-    for (int k = threadIdx.x; k < 2 * 264; k += blockDim.x) hf[k / 264][k % 264] = sp.learn_heads[k];
-    __syncthreads();
-    const int lane = threadIdx.x & 63, B = sp.batch;
-    const int r0 = f * 128 + (int)(threadIdx.x >> 6) * 32;
-    if (r0 >= 2 * B) return;  // wave-uniform
-    const int r = min(r0 + (lane & 31), 2 * B - 1);
-    const bool nxt = r >= B;
-    const int j = nxt ? r - B : r;
-    const int64_t id = sp.idx[j];
-    const pm_ctrl* c = sp.ctrl;
-    const bool mine = r0 + (lane & 31) < 2 * B && !(pending && push_of(sp, c->pos, c->size, c->max_prio).covers(id));
-    f32x16 c2[2];
-    float qb[3], qt[3];
-    batch_row_fwd(sp, lw, hf[0], hf[1], id, nxt, lane, c2, qb, qt);
-    if (!mine) return;
+// Rows of the batch whose replay row is NOT in this step's push range are stable while the env tick
+// runs: they are computed beside it (one tile per wave) into hfeat [B][80] (features of s | Q_B(s)
+// 0..2, r at 3, Q_B(s') 4..6, action|done bits at 7, Q_T(s') 8..10 at 64..); k_learn computes the
+// rest. Carrying r and the bits here spares k_learn a load that depends on idx.
+__device__ __forceinline__ void store_hfeat(const pm_selfplay& sp, int j, int64_t id, bool nxt, int lane,
+                                            const f32x16 (&c2)[2], const float (&qb)[3], const float (&qt)[3]) {
     float* row = sp.hfeat + (size_t)j * 80;
     const int h = lane >> 5;
     if (!nxt) {
@@ -177,31 +170,102 @@ __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f, bool
     }
 }
 
+// k_env's last ceil(2B/128) blocks (plain step): rows f * 128 .. of the batch (s rows, then s').
+// pending = false (updates 1..U-1, k_batch_fwd): no push is in flight, this block computes every row.
+__device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f, bool pending = true) {
+    __shared__ __attribute__((aligned(16))) float lw[kLwFloats];
+    __shared__ __attribute__((aligned(16))) float hf[2][264];
+    if (!learner_active(sp)) return;  // block-uniform
+    stage_frags_lds(sp.w_B, lw, f * 5);
+    for (int k = threadIdx.x; k < 2 * 264; k += blockDim.x) hf[k / 264][k % 264] = sp.learn_heads[k];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, B = sp.batch;
+    const int r0 = f * 128 + (int)(threadIdx.x >> 6) * 32;
+    if (r0 >= 2 * B) return;  // wave-uniform
+    const int r = min(r0 + (lane & 31), 2 * B - 1);
+    const bool nxt = r >= B;
+    const int j = nxt ? r - B : r;
+    const int64_t id = sp.idx[j];
+    const pm_ctrl* c = sp.ctrl;
+    const bool mine = r0 + (lane & 31) < 2 * B && !(pending && push_of(sp, c->pos, c->size, c->max_prio).covers(id));
+    f32x16 c2[2];
+    float qb[3], qt[3];
+    batch_row_fwd(sp, lw, hf[0], hf[1], id, nxt, lane, c2, qb, qt);
+    if (mine) store_hfeat(sp, j, id, nxt, lane, c2, qb, qt);
+}
+
+// The fused step's sampler blocks: block b draws samples [64 b, 64 b + 64) (per_sample_block) and then
+// computes their stable rows' forward itself, one tile per wave (waves 0-1: s rows of the block's
+// samples, waves 2-3: their s' rows): no other block waits for the sample. The weight image and the
+// update's heads are staged while the sampler descends the tree.
+struct SampleFwdSmem {
+    PerSampleSmem per;
+    float lw[kLwFloats];
+    float hf[pad256(2 * 264)];  // modelB (update noise) [0, 264) | targetB (mu) [264, 528) head fragments
+    int64_t sidx[PER_BS];
+};
+__device__ __forceinline__ void sample_fwd_block(const pm_selfplay& sp, int b, SampleFwdSmem& sm) {
+    stage_frags_lds(sp.w_B, sm.lw, b * 5);
+    copy_lds_f32x4<2 * 264>(sp.learn_heads, sm.hf);
+    sample_block(sp, b, true, sm.per, sm.sidx);
+    if (!learner_active(sp)) return;  // block-uniform (sample_block returned before its first barrier)
+    __syncthreads();  // sidx, staged weights
+    PM_BLK(1);
+    const int lane = threadIdx.x & 63, B = sp.batch;
+    const int r = (int)(threadIdx.x >> 6) * 32 + (lane & 31);  // row of the block's 128: s rows, then s'
+    const bool nxt = r >= PER_BS;
+    const int js = nxt ? r - PER_BS : r;
+    const int j = b * PER_BS + js;
+    const int64_t id = sm.sidx[min(j, B - 1) - b * PER_BS];
+    const pm_ctrl* c = sp.ctrl;
+    const bool mine = j < B && !push_of(sp, c->pos, c->size, c->max_prio).covers(id);
+    f32x16 c2[2];
+    float qb[3], qt[3];
+    batch_row_fwd(sp, sm.lw, sm.hf, sm.hf + 264, id, nxt, lane, c2, qb, qt);
+    if (mine) store_hfeat(sp, j, id, nxt, lane, c2, qb, qt);
+}
+
 __device__ __forceinline__ void write_opp_lists(const pm_selfplay& sp, OppListSmem& sm, int blk, int i, bool valid,
                                                 int net) {
     write_opp_lists(sp.n_pool + 1, sp.opp_list, sp.opp_cnt, sm, blk, i, valid, net);
 }
 
+struct EnvSmem {
+    float lds[2][kBlock][7];
+    long long red[kBlock / 64][6];
+    OppListSmem ol;
+};
+struct ActEnvSmem {
+    EnvSmem e;
+    float lw[kLwFloats];  // modelB's acting fragment image
+};
+
 // env.step (:242) + memory.push (:243) + episode bookkeeping (:245-249) + next opponent (:235-236)
-// and env.reset (:238) for finished arenas; writes next step's observations. HBM-bound.
-__global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
-    // env blocks first, then the learner-forward blocks (measured: dispatching the forward blocks
-    // first lengthens the kernel by ~1 us; last, they finish inside the env blocks' time)
-    const int blk = (int)blockIdx.x;
-    const int nenv = (sp.n + kBlock - 1) / kBlock;
-    if (blk >= nenv) {
-        env_fwd_block(sp, blk - nenv);
-        return;
-    }
-    __shared__ __attribute__((aligned(16))) float lds[2][kBlock][7];
-    __shared__ long long red[kBlock / 64][6];
+// and env.reset (:238) for finished arenas of env block blk; writes next step's observations.
+// ACT (the fused step, k_actenv): modelB's greedy action for the block's 256 arenas is computed here
+// first (select_action_B, :126-130, the argmax side), on the matrix cores: wave w takes the two
+// 32-row tiles of its own 64 arenas, so lane l's action sits in lane l (tile 0 holds rows 0-31 in
+// both lane halves, tile 1 rows 32-63), with no LDS exchange. The env's state loads are issued with
+// the weight staging and land under it. Without ACT (k_env) the argmax comes from k_act_sp via aB.
+template <bool ACT>
+__device__ __forceinline__ void env_block(const pm_selfplay& sp, int blk, EnvSmem& sm, float* lw) {
     const int i0 = blk * kBlock;
     const int i = i0 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const bool valid = i < sp.n;
     const int ii = valid ? i : sp.n - 1;
     const pm_ctrl* c = sp.ctrl;
     if (blk == 0) PM_STAMP_ANY(72);
     PM_ENV_STAMP(0, blk);
+    float xs[2][4];
+    if (ACT) {
+        stage_frags_lds(sp.w_B, lw, blk);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int row = min(i0 + 64 * wv + 32 * k + (lane & 31), sp.n - 1);
+            tile_inputs(sp.obsB + (size_t)row * 7, lane >> 5, xs[k]);
+        }
+    }
     // Every per-arena load is issued here, in one basic block, before any branch (loads placed after
     // a branch were issued only after it, one more HBM round trip). The serve counter goes first:
     // the next episode's opponent and serve are drawn for every lane while the state loads are in
@@ -217,7 +281,7 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
     const float er0 = sp.ep_reward[ii];
     Arena a = load_arena(sp.st, ii);
     const int aA = sp.aA[ii];
-    int aB = sp.aB[ii];
+    int aB = ACT ? 0 : sp.aB[ii];
     __builtin_amdgcn_sched_barrier(0);
     const float maxp = push_prio(size, cmaxp);  // max(prios) if buffer else 1.0 (:57)
     float* leaf = per_tree(sp.per_work, sp.cap).leaf;
@@ -225,8 +289,8 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
 
     // Draws that need only the serve counter and the control block, pinned ahead of everything that
     // waits for the state loads:
-    //   select_action_B (:126-130): random.random() < eps ? randint(0, 2) : argmax (the act kernel
-    //   wrote the argmax; the draw is per-arena VALU work, cheaper here than beside the MFMAs);
+    //   select_action_B (:126-130): random.random() < eps ? randint(0, 2) : argmax (the argmax is
+    //   the act's; the draw is per-arena VALU work, cheaper here than beside the MFMAs);
     //   the next episode's opponent (:235-236) and serve (env.reset(), :238), used if this one ends.
     int onext, eps_a;
     bool eps_hit;
@@ -240,6 +304,19 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
         philox_serve(sp.env, (uint32_t)ii, ns, sp.seed_env, svx, svy, sspn);
         asm volatile("" ::"v"(onext), "v"(svx), "v"(svy), "v"(sspn), "v"(eps_hit), "v"(eps_a));
         __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ACT) {
+        __syncthreads();  // the fragment image is staged (every load of the block has landed)
+        int act[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            f32x16 c2[2];
+            float q[3];
+            tile_hidden(lw, xs[k], lane, c2);
+            tile_heads(lw + F_H, c2, lane, q);
+            act[k] = argmax3(q);
+        }
+        aB = lane < 32 ? act[0] : act[1];
     }
     PM_ENV_STAMP(1, blk);
     if (eps_hit) aB = eps_a;
@@ -256,7 +333,6 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
     const float er = er0 + rB;  // ep_reward += rB (:245)
     const bool fin = valid && d;
     {   // per-block partials, no atomics (:247-249)
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         const bool win = er > 0.f;
         const unsigned long long mf = __ballot(fin), mA = __ballot(fin && o == 0), mwA = __ballot(fin && o == 0 && win);
         const unsigned long long mP = __ballot(fin && o != 0), mwP = __ballot(fin && o != 0 && win);
@@ -264,8 +340,8 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
 #pragma unroll
         for (int s = 32; s > 0; s >>= 1) rs += __shfl_xor(rs, s);
         if (lane == 0) {
-            red[wv][0] = __popcll(mf); red[wv][1] = __popcll(mA); red[wv][2] = __popcll(mwA);
-            red[wv][3] = __popcll(mP); red[wv][4] = __popcll(mwP); red[wv][5] = rs;
+            sm.red[wv][0] = __popcll(mf); sm.red[wv][1] = __popcll(mA); sm.red[wv][2] = __popcll(mwA);
+            sm.red[wv][3] = __popcll(mP); sm.red[wv][4] = __popcll(mwP); sm.red[wv][5] = rs;
         }
     }
     int onew = o;
@@ -295,22 +371,52 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
     }
     PM_ENV_STAMP(3, blk);
 #pragma unroll
-    for (int k = 0; k < 7; ++k) { lds[0][threadIdx.x][k] = nA[k]; lds[1][threadIdx.x][k] = nB[k]; }
+    for (int k = 0; k < 7; ++k) { sm.lds[0][threadIdx.x][k] = nA[k]; sm.lds[1][threadIdx.x][k] = nB[k]; }
     __syncthreads();
     PM_ENV_STAMP(4, blk);
     if (threadIdx.x < 6) {
         long long t = 0;
-        for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
+        for (int w = 0; w < kBlock / 64; ++w) t += sm.red[w][threadIdx.x];
         sp.partials[(size_t)blk * 8 + threadIdx.x] = t;
     }
-    {
-        __shared__ OppListSmem ol;
-        write_opp_lists(sp, ol, blk, i, valid, onew);
-    }
+    write_opp_lists(sp, sm.ol, blk, i, valid, onew);
     PM_ENV_STAMP(5, blk);
-    copy_rows7(sp.obsA, lds[0], i0, sp.n);
-    copy_rows7(sp.obsB, lds[1], i0, sp.n);
+    copy_rows7(sp.obsA, sm.lds[0], i0, sp.n);
+    copy_rows7(sp.obsB, sm.lds[1], i0, sp.n);
     PM_ENV_STAMP_DRAIN(6, blk);
+}
+
+// The plain step's env kernel: env blocks first, then the learner-forward blocks (measured:
+// dispatching the forward blocks first lengthens the kernel by ~1 us; last, they finish inside the
+// env blocks' time).
+__global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
+    const int blk = (int)blockIdx.x;
+    const int nenv = (sp.n + kBlock - 1) / kBlock;
+    if (blk >= nenv) {
+        env_fwd_block(sp, blk - nenv);
+        return;
+    }
+    __shared__ __attribute__((aligned(16))) EnvSmem sm;
+    env_block<false>(sp, blk, sm, nullptr);
+}
+
+// The fused step's first kernel (pm_selfplay_actenv): blocks [0, ceil(B/64)) sample the update's batch
+// and compute its stable rows (sample_fwd_block); every other block acts for modelB and ticks its 256
+// arenas (env_block<true>). Replaces k_act_sp(PM_ACT_B) + k_env of the overlapped step, bit for bit.
+union ActEnvShared {
+    ActEnvSmem ae;
+    SampleFwdSmem sf;
+};
+__global__ __launch_bounds__(kBlock) void k_actenv(const pm_selfplay sp) {
+    __shared__ __attribute__((aligned(16))) ActEnvShared sh;
+    const int nsb = (sp.batch + PER_BS - 1) / PER_BS;
+    if ((int)blockIdx.x < nsb) {
+        PM_BLK(0);
+        sample_fwd_block(sp, (int)blockIdx.x, sh.sf);
+        PM_BLK_END();
+        return;
+    }
+    env_block<true>(sp, (int)blockIdx.x - nsb, sh.ae.e, sh.ae.lw);
 }
 
 // ------------------------------------------------------------------------------------ init
@@ -899,7 +1005,8 @@ __global__ __launch_bounds__(kLearn) void k_prepare(const pm_selfplay sp) {
 // wave per sample), then the batch forward of every row (no pending push: k_env's forward blocks'
 // job, on their own launch).
 __global__ __launch_bounds__(256) void k_resample(const pm_selfplay sp) {
-    sample_wave(sp, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), false);
+    __shared__ PerSampleSmem sm;
+    sample_block(sp, (int)blockIdx.x, false, sm);
 }
 __global__ __launch_bounds__(kBlock) void k_batch_fwd(const pm_selfplay sp) { env_fwd_block(sp, (int)blockIdx.x, false); }
 
@@ -1024,7 +1131,7 @@ extern "C" int pm_selfplay_init(const pm_selfplay* sp, void* stream) {
 namespace {
 int launch_act(const pm_selfplay* sp, int part, hipStream_t st) {
     const ActGrid g{sp->n, sp->n_pool + 1, sp->chunk_A, sp->chunk_P, part == PM_ACT_A ? 0 : 1};
-    const int nsb = part == PM_ACT_A ? 0 : (sp->batch + 3) / 4;
+    const int nsb = part == PM_ACT_A ? 0 : (sp->batch + PER_BS - 1) / PER_BS;
     const int blocks = part == PM_ACT_B ? nsb + g.nb() : nsb + g.blocks();
     hipLaunchKernelGGL(k_act_sp, dim3(blocks), dim3(kActBlock), 0, st, *sp, part);
     PM_LAUNCHED("k_act_sp");
@@ -1063,6 +1170,15 @@ extern "C" int pm_selfplay_env(const pm_selfplay* sp, void* stream) {
     const unsigned nfwd = pm_blocks(2 * sp->batch, 128);  // batch rows not in the push range (env_fwd_block)
     hipLaunchKernelGGL(k_env, dim3(pm_blocks(sp->n, kBlock) + nfwd), dim3(kBlock), 0, pm_stream(stream), *sp);
     PM_LAUNCHED("k_env");
+    return PM_OK;
+}
+
+extern "C" int pm_selfplay_actenv(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    const unsigned nsb = (unsigned)((sp->batch + PER_BS - 1) / PER_BS);
+    hipLaunchKernelGGL(k_actenv, dim3(nsb + pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *sp);
+    PM_LAUNCHED("k_actenv");
     return PM_OK;
 }
 
@@ -1106,7 +1222,7 @@ extern "C" int pm_selfplay_resample(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
     hipStream_t st = pm_stream(stream);
-    hipLaunchKernelGGL(k_resample, dim3((sp->batch + 3) / 4), dim3(256), 0, st, *sp);
+    hipLaunchKernelGGL(k_resample, dim3((sp->batch + PER_BS - 1) / PER_BS), dim3(256), 0, st, *sp);
     PM_LAUNCHED("k_resample");
     hipLaunchKernelGGL(k_batch_fwd, dim3(pm_blocks(2 * sp->batch, 128)), dim3(kBlock), 0, st, *sp);
     PM_LAUNCHED("k_batch_fwd");
@@ -1132,8 +1248,7 @@ extern "C" int pm_selfplay_step_multi(const pm_selfplay* sp, int32_t updates, vo
     PM_REQUIRE(sp->world == 1, PM_E_ARG, "pm_selfplay_step_multi: unsharded only (world=%d)", sp->world);
     if (updates == 1) return pm_selfplay_step_overlap(sp, stream);
     hipStream_t st = pm_stream(stream);
-    if ((rc = launch_act(sp, PM_ACT_B, st))) return rc;
-    if ((rc = pm_selfplay_env(sp, stream))) return rc;
+    if ((rc = pm_selfplay_actenv(sp, stream))) return rc;
     if ((rc = launch_learn(sp, true, st, PM_UPD_FIRST))) return rc;
     if ((rc = pm_selfplay_apply_ex(sp, PM_UPD_FIRST, stream))) return rc;
     for (int u = 1; u < updates; ++u) {
@@ -1151,8 +1266,7 @@ extern "C" int pm_selfplay_step(const pm_selfplay* sp, void* stream) {
 }
 
 extern "C" int pm_selfplay_step_overlap(const pm_selfplay* sp, void* stream) {
-    int rc = pm_selfplay_act_part(sp, PM_ACT_B, stream);
-    if (!rc) rc = pm_selfplay_env(sp, stream);
+    int rc = pm_selfplay_actenv(sp, stream);
     if (!rc) rc = pm_selfplay_learn_act(sp, stream);
     return rc ? rc : pm_selfplay_apply(sp, stream);
 }

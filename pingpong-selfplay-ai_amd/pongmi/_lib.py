@@ -33,7 +33,7 @@ PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class EnvParams(ctypes.Structure):
@@ -142,6 +142,7 @@ _SIGS = {
     "pm_selfplay_step": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_act_part": (c_i32, [c_void_p, c_i32, c_void_p]),
     "pm_selfplay_learn_act": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_actenv": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_step_overlap": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_learn_ex": (c_i32, [c_void_p, c_i32, c_i32, c_void_p]),
     "pm_selfplay_apply_ex": (c_i32, [c_void_p, c_i32, c_void_p]),

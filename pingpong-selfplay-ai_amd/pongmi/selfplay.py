@@ -147,6 +147,11 @@ class SelfPlayLearner:
         if part != _lib.PM_ACT_B:
             self._aA_ready = True
 
+    def actenv(self):
+        """act(PM_ACT_B) + env_step fused into one launch (bit-identical)."""
+        self._aA_ready = False
+        check(self.lib.pm_selfplay_actenv(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_actenv")
+
     def env_step(self):
         self._aA_ready = False
         check(self.lib.pm_selfplay_env(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_env")
@@ -191,8 +196,7 @@ class SelfPlayLearner:
         if self.overlap:
             if not self._aA_ready:
                 self.act(_lib.PM_ACT_A)
-            self.act(_lib.PM_ACT_B)
-            self.env_step()
+            self.actenv()
         else:
             self.rollout()
         for u in range(U):
@@ -227,8 +231,7 @@ class SelfPlayLearner:
             check(self.lib.pm_selfplay_step_overlap(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step_overlap")
             self._aA_ready = True
             return
-        self.act(_lib.PM_ACT_B)
-        self.env_step()
+        self.actenv()
         self.learn(act_next=True)
         self.allreduce(self.grad)
         self.apply()

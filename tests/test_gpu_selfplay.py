@@ -325,12 +325,15 @@ def test_sharded_world2_overlap_equals_plain(golden):
 
     ov = [make(0, True), make(1, True)]
     pl = [make(0, False), make(1, False)]
-    for _ in range(14):
+    for k in range(14):
         for L in ov:
             if not L._aA_ready:
                 L.act(_lib.PM_ACT_A)
-            L.act(_lib.PM_ACT_B)
-            L.env_step()
+            if k % 2:
+                L.act(_lib.PM_ACT_B)
+                L.env_step()
+            else:
+                L.actenv()  # the fused launch: bit-identical to act B + env
             L.learn(act_next=True)
         for L in pl:
             L.rollout()

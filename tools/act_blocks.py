@@ -42,7 +42,7 @@ def main():
         lib.pm_diag_read_blk(buf)
         runs.append(np.array(buf[:], dtype=np.int64).reshape(8, 4096))
     sp = L.sp
-    nsb = (sp.batch + 3) // 4
+    nsb = (sp.batch + 63) // 64  # PER_BS samples per sampler block
     nb = (n + 255) // 256  # kChunkB
     na0 = (n + sp.chunk_A - 1) // sp.chunk_A
     na1 = (n + sp.chunk_P - 1) // sp.chunk_P

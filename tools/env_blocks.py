@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-PHASES = ["begin", "loads issued + speculative draws", "state wait + tick + obs", "bookkeeping + replay/state stores",
+PHASES = ["begin", "loads issued + speculative draws (+ act tiles, fused)", "state wait + tick + obs", "bookkeeping + replay/state stores",
           "LDS staging + barrier", "partials + opponent lists", "obs stores + drain of all stores (end)"]
 
 
@@ -38,13 +38,24 @@ def main():
     torch.cuda.synchronize()
     nb = (n + 255) // 256
     buf = (ctypes.c_uint64 * (8 * 1024))()
-    acc = []
+    blk = (ctypes.c_uint64 * (8 * 4096))()
+    nsb = (256 + 63) // 64  # sampler blocks of the fused kernel (k_actenv, PER_BS = 64)
+    acc, samp = [], []
     for _ in range(20):
-        L.step()
+        if L.overlap:  # the production step's launches, read right after the fused act + env kernel
+            L.actenv()
+        else:
+            L.step()
         torch.cuda.synchronize()
         lib.pm_diag_read_env(buf)
         a = np.array(buf[:], dtype=np.int64).reshape(8, 1024)[:7, :nb]
         acc.append(a)
+        if L.overlap:
+            lib.pm_diag_read_blk(blk)
+            b = np.array(blk[:], dtype=np.int64).reshape(8, 4096)[:, :nsb]
+            samp.append((b - a[0].min()) * 0.01)
+            L.learn(act_next=True)
+            L.apply()
     spans, deltas = [], [[] for _ in PHASES]
     for a in acc:
         t0 = a[0].min()
@@ -57,6 +68,12 @@ def main():
         v = np.array(deltas[k])
         label = "begin offset" if k == 0 else name
         print(f"  {label:44s} p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
+    if samp:
+        s = np.stack(samp)  # [run][slot][block]
+        q = lambda v: " ".join(f"{x:6.2f}" for x in np.percentile(v, [0, 50, 90, 100]))  # noqa: E731
+        print(f"k_actenv sampler+forward blocks ({nsb}), times from the first env block's begin (min p50 p90 max):")
+        print(f"  begin {q(s[:, 0])} | level2 {q(s[:, 4])} | level1 {q(s[:, 5])} | leaves {q(s[:, 6])} | "
+              f"sampled {q(s[:, 1])} | end {q(s[:, 2])}")
 
 
 if __name__ == "__main__":

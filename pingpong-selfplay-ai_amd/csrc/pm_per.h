@@ -118,7 +118,7 @@ __device__ __forceinline__ double per_quarter(const float* __restrict__ leaf, in
     for (int i = 0; i < 16; ++i) {
         int64_t d = d0 + i;
         if (d >= pr.cap) d -= pr.cap;
-        acc += (double)(d < pr.n ? pr.pval : v[i]);
+        acc += lo + i < pr.cap ? (double)(d < pr.n ? pr.pval : v[i]) : 0.0;  // past cap: no leaf
     }
     return acc;
 }

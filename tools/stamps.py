@@ -3,8 +3,9 @@
     make -C pingpong-selfplay-ai_amd/csrc diag && python tools/stamps.py [--steps 20]
 
 Thread 0 of block 0 of each learner kernel records s_memrealtime (100 MHz) at phase boundaries
-(PM_STAMP in pm_selfplay.hip); this prints the mean time of every stamp relative to the start of
-k_act_sp, i.e. the critical path through act (+ PER sample blocks) -> env -> learn.
+(PM_STAMP in pm_selfplay.hip); this prints the median time of every stamp relative to the start of
+the step's first kernel (k_actenv's first env block in the fused step, k_act_sp's first act block in
+the plain one), i.e. the critical path through act + env (+ PER sample blocks) -> learn.
 Diagnostic only (libpongmi_diag.so, never the product library).
 """
 import argparse
@@ -21,7 +22,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 NAMES = {
-    70: "act start (1st act blk)", 64: "sample start", 65: "sample blk0 end", 72: "env start",
+    70: "act start (1st act blk)", 64: "sample start", 65: "sample blk0 end", 72: "env start (1st env blk)",
     0: "learn start", 30: "ph0 issued", 31: "ph0 idx/isw in", 32: "ph0 hfeat in", 33: "ph0 trans in",
     1: "learn loads", 2: "learn fwd (MFMA)", 3: "learn td/loss", 4: "learn scatter+grad",
     8: "ph4 grads out w0", 9: "ph4 grads out w15", 10: "ph4 scatter subs w0", 11: "ph4 scatter subs w15",
@@ -60,7 +61,7 @@ def main():
         v = np.array(buf[:], dtype=np.int64)
         rows.append(v)
     a = np.stack(rows)
-    base = a[:, 70:71]
+    base = a[:, 70:71] if (a[:, 70] != 0).all() else a[:, 72:73]
     rel = (a - base) * 0.01  # 100 MHz ticks -> us
     for slot in sorted(NAMES, key=lambda s: np.median(rel[:, s])):
         if (a[:, slot] == 0).any():

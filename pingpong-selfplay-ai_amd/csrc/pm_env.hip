@@ -48,14 +48,37 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(pm_env_params p, pm_env_st
     if (obsB) store_rows7(obsB, lds, oB, i0, n);
 }
 
+#ifdef PM_DIAG
+// K1 per-wave timeline (diagnostic build only): lane 0 of every wave stamps s_memtime at the phase
+// boundaries of k_env_step; pm_k1_diag_read copies [8][4096] out.
+static __device__ unsigned long long pm_k1_diag[8][4096];
+#define K1_STAMP(k)                                                                             \
+    do {                                                                                        \
+        const unsigned w_ = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);                    \
+        if ((threadIdx.x & 63) == 0 && w_ < 4096) pm_k1_diag[(k)][w_] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define K1_DRAIN() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#else
+#define K1_STAMP(k) \
+    do {            \
+    } while (0)
+#define K1_DRAIN() \
+    do {           \
+    } while (0)
+#endif
+
 // One lane per arena, one wave per SIMD at 65 536 arenas: the kernel is a single load -> tick ->
-// store pass, so its time is the serial latency of that pass. Four things keep it short:
+// store pass, so its time is the serial latency of that pass. What keeps it short:
 //   - the serve counter is loaded first; the next production serve (two Philox draws + sincos) is
 //     drawn for every lane (done lanes use it) in the same scheduling region as the straight-line
-//     tick, so the two independent dependency chains interleave instead of running back to back;
+//     tick, so the two independent dependency chains interleave (drawing it ahead, under the load
+//     latency, measured slower: the draw's own chains then run alone);
 //   - tick() is branch-free, with one shared collide path and reciprocal-multiply division;
+//   - the production reset is branch-free too: every lane forms the served arena and done lanes
+//     select it, so the state stores follow the tick directly, and the term rows of done lanes
+//     leave last, after the block's observation rows;
 //   - every observation row of the block is staged in LDS once, behind one barrier, and leaves as
-//     full float4 stores; term rows of done arenas leave as one dwordx4 + dwordx3 per row;
+//     full float4 stores;
 //   - the autoreset mode and parity-mode injection are template parameters, so no uniform branch
 //     splits the hot block.
 // AR (autoreset): 0 none, 1 reset + full term rows (term row = the step's pre-reset observation),
@@ -69,40 +92,54 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
                                                      const double* __restrict__ inject, int inject_cap,
                                                      uint64_t seed, int32_t* status, int n) {
     __shared__ __attribute__((aligned(16))) float lds[4][kBlock][7];
+    constexpr bool DRAW = AR && !INJ;
     const int i0 = blockIdx.x * kBlock;
     const int t = threadIdx.x;
     const int i = i0 + t;
     const bool full_term = tobsA && AR != 2;  // tobsA and tobsB are both set or both null
-    float oA[7] = {0}, oB[7] = {0};
+    float oA[7] = {0}, oB[7] = {0}, tA[7], tB[7];
+    int tdone = 0;
+    K1_STAMP(0);
     if (i < n) {
         int32_t ns = 0;
         ServeDraw sv{};
         if (AR) ns = __builtin_nontemporal_load(&s.serves[i]);
         Arena a = load_arena(s, i);
         const int xa = aA[i], xb = aB[i];
-        if (AR && !INJ) sv = serve_draw(p, (uint32_t)i, (uint32_t)ns, seed);
+#ifdef PM_DIAG
+        K1_DRAIN();
+        K1_STAMP(1);
+#endif
+        if (DRAW) sv = serve_draw(p, (uint32_t)i, (uint32_t)ns, seed);
         float ra, rb;
         const int d = tick(p, a, xa, xb, ra, rb);
-        // every lane's draw is complete here, ahead of the done branch (the compiler would sink it
-        // into that branch, behind the term-row stores)
-        if (AR && !INJ) asm volatile("" ::"v"(sv.vx), "v"(sv.vy), "v"(sv.spin), "v"(sv.rad));
+        // every lane's draw is complete here, ahead of the reset (the compiler would sink it into
+        // the done lanes' path, behind the term-row stores)
+        if (DRAW) asm volatile("" ::"v"(sv.vx), "v"(sv.vy), "v"(sv.spin), "v"(sv.rad));
+        K1_STAMP(2);
         observe(a, oA, oB);
         if (full_term) {
 #pragma unroll
             for (int k = 0; k < 7; ++k) { lds[2][t][k] = oA[k]; lds[3][t][k] = oB[k]; }
         }
-        if (AR && d) {
+        if constexpr (DRAW) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) { tA[k] = oA[k]; tB[k] = oB[k]; }
+            serve_finish(sv);  // the rare |angle| >= 135 degree redo (a branch no lane normally takes)
+            Arena r = a;
+            serve(r, sv.vx, sv.vy, sv.spin);
+            a.x = d ? r.x : a.x; a.y = d ? r.y : a.y; a.vx = d ? r.vx : a.vx; a.vy = d ? r.vy : a.vy;
+            a.spin = d ? r.spin : a.spin; a.top = d ? r.top : a.top; a.bot = d ? r.bot : a.bot;
+            a.sA = d ? 0 : a.sA; a.sB = d ? 0 : a.sB; a.bounces = d ? 0 : a.bounces;
+            observe(a, oA, oB);
+            s.serves[i] = ns + d;
+        } else if (AR && d) {  // parity mode: the injected serve of done arenas
             if (AR == 2 && tobsA) {
                 store_row7(tobsA + (size_t)i * 7, oA);
                 store_row7(tobsB + (size_t)i * 7, oB);
             }
-            if (INJ) {
-                const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
-                sv.vx = r[0]; sv.vy = r[1]; sv.spin = r[2];
-            } else {
-                serve_finish(sv);
-            }
-            serve(a, sv.vx, sv.vy, sv.spin);
+            const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
+            serve(a, r[0], r[1], r[2]);
             s.serves[i] = ns + 1;
             observe(a, oA, oB);
         }
@@ -110,16 +147,26 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
         rA[i] = ra;
         rB[i] = rb;
         done[i] = (uint8_t)d;
+        tdone = d;
     }
+    K1_STAMP(3);
 #pragma unroll
     for (int k = 0; k < 7; ++k) { lds[0][t][k] = oA[k]; lds[1][t][k] = oB[k]; }
     __syncthreads();
+    K1_STAMP(4);
     copy_rows7(obsA, lds[0], i0, n);
     copy_rows7(obsB, lds[1], i0, n);
     if (full_term) {
         copy_rows7(tobsA, lds[2], i0, n);
         copy_rows7(tobsB, lds[3], i0, n);
     }
+    if (DRAW && AR == 2 && tobsA && tdone) {
+        store_row7(tobsA + (size_t)i * 7, tA);
+        store_row7(tobsB + (size_t)i * 7, tB);
+    }
+    K1_STAMP(5);
+    K1_DRAIN();
+    K1_STAMP(6);
 }
 
 __global__ __launch_bounds__(kBlock) void k_collide(const double* __restrict__ in, const double* __restrict__ inertia,
@@ -174,7 +221,6 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
     PM_REQUIRE(autoreset >= 0 && autoreset <= 2, PM_E_ARG, "pm_env_step: autoreset=%d not in {0,1,2}", autoreset);
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
-    if (n == 0) return PM_OK;
     using K = decltype(&k_env_step<0, false>);
     static const K kernels[3][2] = {{k_env_step<0, false>, k_env_step<0, true>},
                                     {k_env_step<1, false>, k_env_step<1, true>},
@@ -185,6 +231,12 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
     PM_LAUNCHED("k_env_step");
     return PM_OK;
 }
+
+#ifdef PM_DIAG
+extern "C" int pm_k1_diag_read(uint64_t* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_k1_diag), sizeof(pm_k1_diag), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 extern "C" int pm_collide(const double* in, const double* inertia, double* out, int32_t n, void* stream) {
     PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_collide: n=%d", n);

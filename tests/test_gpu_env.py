@@ -126,6 +126,44 @@ def test_autoreset_done_rows_only():
     assert seen > 1000
 
 
+def test_autoreset_serves_match_philox_restatement(orc):
+    """Production autoreset serves of pm_env_step (the branch-free reset): every arena that
+    finishes in a step is served Philox(seed; i, serves[i]) as the oracle restates it (cos/sin within
+    1 ulp of libm), serves[i] counts its resets, and every other arena ticks as the C oracle does."""
+    from pongmi.env import PongEnv2PBatch
+
+    n = 65536
+    kw = dict(ball_speed_range=[0.03, 0.05], spin_range=[-5, 5], max_score=1)
+    p = orc.env_params_from_kwargs(**kw)
+    P = orc.make_params(p)
+    env = PongEnv2PBatch(n, seed=77, autoreset=True, **kw)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    served = 0
+    for t in range(60):
+        before = env.get_state()
+        aA = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=g)
+        aB = torch.randint(0, 3, (n,), device="cuda", dtype=torch.int8, generator=g)
+        _, _, done, _ = env.step(aA, aB)
+        d = done.cpu().numpy().astype(bool)
+        st = env.get_state()
+        arr = orc.arenas_from_soa(before)
+        _, _, _, ed = orc.step_arenas(P, arr, aA.cpu().numpy(), aB.cpu().numpy())
+        assert np.array_equal(d, ed.astype(bool))
+        for k in STATE_ORDER:
+            assert np.array_equal(st[k][~d], arr[k][~d]), (t, k)
+        idx = np.nonzero(d)[0]
+        assert np.array_equal(st["serves"], before["serves"] + d)
+        vx, vy, sp = orc.philox_serve(p, idx, before["serves"][idx], 77)
+        np.testing.assert_allclose(st["vx"][idx], vx, rtol=4e-16, atol=1e-18)
+        np.testing.assert_allclose(st["vy"][idx], vy, rtol=4e-16, atol=1e-18)
+        assert np.array_equal(st["spin"][idx], sp)
+        for k, v in (("x", 0.5), ("y", 0.5), ("top", 0.5), ("bot", 0.5), ("scoreA", 0), ("scoreB", 0), ("bounces", 0)):
+            assert np.all(st[k][idx] == v), (t, k)
+        served += len(idx)
+    assert served > 5000
+
+
 def test_env_empty_and_bad_arguments():
     from pongmi import _lib
     from pongmi.env import PongEnv2PBatch, env_params

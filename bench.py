@@ -189,13 +189,12 @@ def cpu_baseline_rnn(seconds=12.0, n=2048):
                       f"+ env + sequence buffer + DRQN update 64x8 every step), {dt:.1f} s on 1 host core"}
 
 
-def run_rnn(args, dist, rank, world):
+def run_rnn(args, dist, rank, world, allreduce):
     """configs[4]: 32768 arenas/GPU, the train_rnn_iterative loop (QNetRNN both players with (h, c)
     per arena, sequence buffer, DRQN update 64 x 8 with BPTT + clip + Adam every vector step)."""
     from pongmi.rnn_selfplay import RNNSelfPlayLearner
     n = args.arenas or 32768
     pool_n = 4 if args.pool is None else args.pool
-    allreduce = (lambda t: dist.all_reduce(t)) if dist else None
     L = RNNSelfPlayLearner(ENV_KW_RNN, n, synthetic_rnn(1), synthetic_rnn(2),
                            [synthetic_rnn(100 + k) for k in range(pool_n)], epsilon=0.05, seed=7, rank=rank,
                            world=world, allreduce=allreduce)
@@ -213,7 +212,7 @@ def run_rnn(args, dist, rank, world):
             L.learner.update()
         else:
             L.learner.grads()
-            dist.all_reduce(L.learner.grad)
+            allreduce(L.learner.grad)
             L.learner.apply()
         ev[3].record()
 
@@ -258,7 +257,8 @@ def run_rnn(args, dist, rank, world):
                        "arenas_per_gpu": n, "global_arenas": n * world, "pool": pool_n, "batch": 64, "trace_length": 8,
                        "memory_size": L.cap, "ring_depth": L.depth,
                        "updates_in_timed_region": c["train_steps"] - c0["train_steps"],
-                       "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)"},
+                       "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
+                       "all_reduce": args.comm_used if world > 1 else None},
             "roofline": {"bound": "mfma", "kernel": "k_rnn_act (+ k_rnn_fold)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
@@ -293,6 +293,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-overlap", action="store_true", help="dqn: plain step (opponent act in k_act_sp, not in the learner launch)")
+    ap.add_argument("--comm", choices=("native", "torch"), default="native",
+                    help="N > 1: the gradient all-reduce as libpongmi's own RCCL communicator inside one library "
+                         "call per vector step (native), or torch.distributed.all_reduce between launches (torch)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -304,8 +307,19 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    comm = None
+    if dist is not None and args.comm == "native":
+        from pongmi.dist import NativeComm
+        try:
+            comm = NativeComm()
+        except Exception as e:  # every rank sees rank 0's binding failure: all fall back together
+            print(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed.all_reduce",
+                  file=sys.stderr, flush=True)
+    args.comm_used = "native RCCL, in-stream" if comm is not None else "torch.distributed"
+    allreduce = comm if comm is not None else ((lambda t: dist.all_reduce(t)) if dist else None)
+
     if args.workload == "rnn":
-        return run_rnn(args, dist, rank, world)
+        return run_rnn(args, dist, rank, world, allreduce)
     args.arenas = args.arenas or 65536
     args.pool = 8 if args.pool is None else args.pool
     from pongmi import _lib
@@ -313,7 +327,6 @@ def main():
 
     sdB, sdA = synthetic_qnet(1), synthetic_qnet(2)
     pool = [synthetic_qnet(100 + k) for k in range(args.pool)]
-    allreduce = (lambda t: dist.all_reduce(t)) if dist else None
     L = SelfPlayLearner(ENV_KW, args.arenas, sdB, sdA, pool, batch=args.batch, memory_size=args.memory,
                         epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce,
                         overlap=not args.no_overlap)
@@ -333,7 +346,7 @@ def main():
         L.learn(act_next=True)
         ev[2].record()
         if dist is not None:
-            dist.all_reduce(L.grad)
+            allreduce(L.grad)
         L.apply()
 
     for _ in range(args.warmup):
@@ -377,7 +390,8 @@ def main():
                                    "env tick + PER push/sample + double-DQN update + Adam + target sync)",
                        "arenas_per_gpu": args.arenas, "global_arenas": args.arenas * world,
                        "pool": args.pool, "batch": args.batch, "updates_per_vector_step": 1,
-                       "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)"},
+                       "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
+                       "all_reduce": args.comm_used if world > 1 else None},
             "roofline": {"bound": "mfma", "kernel": "k_actenv (modelB's act + env tick + replay push + PER sample "
                                                     "and batch-forward blocks)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",

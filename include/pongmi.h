@@ -29,12 +29,13 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 8
+#define PM_ABI_VERSION 9
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
 #define PM_E_SIZE (-2)    /* size outside the supported range */
 #define PM_E_LAUNCH (-3)  /* launch failed (see pm_last_error) */
+#define PM_E_COMM (-4)    /* RCCL binding / communicator failure (see pm_last_error) */
 
 /* ---------------------------------------------------------------- environment (K1) */
 
@@ -480,6 +481,35 @@ int pm_selfplay_apply_ex(const pm_selfplay* sp, int32_t mode, void* stream);
 int pm_selfplay_resample(const pm_selfplay* sp, void* stream);
 int pm_selfplay_commit(const pm_selfplay* sp, void* stream);
 int pm_selfplay_step_multi(const pm_selfplay* sp, int32_t updates, void* stream);
+
+/* ---------------------------------------------------------------- sharded steps (configs[3]) */
+
+/* The learner's exchange step as a library-owned RCCL communicator. The reference is
+ * single-process (scripts/train_iterative.py:80); the build shards arenas over one process per GPU
+ * and sums the learner's gradient buffer once per update. Through torch.distributed that all-reduce
+ * runs on the process group's own stream (an event hand-off each way) behind a Python call; the
+ * *_step_sharded calls below issue a whole sharded vector step from C, with ncclAllReduce enqueued on
+ * the caller's stream between the kernels (results identical to the Python sequence).
+ *   rccl_path: the RCCL shared library to bind (dlopen at run time; pass the one the process already
+ *     loaded, e.g. torch's bundled librccl.so, so a single RCCL instance serves both).
+ *   pm_comm_unique_id: rank 0 creates the 128-byte id; the caller broadcasts it to every rank.
+ *   pm_comm_init: collective over nranks processes (ncclCommInitRank on the current device).
+ *   pm_comm_allreduce_f32: in-place SUM all-reduce of n floats on `stream`. */
+#define PM_COMM_ID_BYTES 128
+typedef struct pm_comm pm_comm;
+int pm_comm_unique_id(const char* rccl_path, uint8_t* id);
+int pm_comm_init(const char* rccl_path, const uint8_t* id, int32_t nranks, int32_t rank, pm_comm** out);
+int pm_comm_allreduce_f32(pm_comm* comm, float* buf, int64_t n, void* stream);
+int pm_comm_destroy(pm_comm* comm);
+/* One sharded DQN vector step with `updates` updates (sp->world == comm ranks, fuse_apply 0):
+ * actenv; per update u: [resample (u > 0)] + learn_ex (u = 0 with the next step's side-A act) +
+ * all-reduce of sp->grad + apply_ex; commit when updates > 1. Same contract as step_overlap
+ * (sp->aA holds the side-A actions for the current observations). */
+int pm_selfplay_step_sharded(const pm_selfplay* sp, pm_comm* comm, int32_t updates, void* stream);
+/* One sharded QNetRNN vector step: rollout; per update u: [sample(u) (u > 0)] + pm_drqn_grads +
+ * all-reduce of d->grad (gradients + contributing-rank count) + pm_drqn_apply. */
+int pm_rnn_selfplay_step_sharded(const pm_rnn_selfplay* sp, const pm_drqn* d, pm_comm* comm, int32_t updates,
+                                 void* stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* pm_last_error(void);

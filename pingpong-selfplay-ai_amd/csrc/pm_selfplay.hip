@@ -132,12 +132,16 @@ __global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp, i
 // row). This lane's row: trans row `id`, `nxt` selects s'. Returns the pre-ReLU features (MFMA
 // accumulator layout) and Q_B / Q_T of the row (heads from learn_heads, staged in hf0 / hf1).
 // Every output column depends only on its own row, so which tile or kernel computes a row never
-// changes a bit of it.
+// changes a bit of it. rb: the row's reward and action|done bits (trans slots 7 and 15), loaded with
+// the operands (a load placed after the MFMAs costs its consumer one more round trip).
 __device__ __forceinline__ void batch_row_fwd(const pm_selfplay& sp, const float* lw, const float* hf0, const float* hf1,
                                               int64_t id, bool nxt, int lane, f32x16 (&c2)[2], float (&qb)[3],
-                                              float (&qt)[3]) {
+                                              float (&qt)[3], float (&rb)[2]) {
     float xs[4];
-    tile_inputs(sp.trans + id * PM_TRANS_F + (nxt ? 8 : 0), lane >> 5, xs);
+    const float* tr = sp.trans + id * PM_TRANS_F;
+    tile_inputs(tr + (nxt ? 8 : 0), lane >> 5, xs);
+    rb[0] = tr[7];
+    rb[1] = tr[15];
     tile_hidden(lw, xs, lane, c2);
     tile_heads(hf0, c2, lane, qb);
     tile_heads(hf1, c2, lane, qt);
@@ -147,8 +151,8 @@ __device__ __forceinline__ void batch_row_fwd(const pm_selfplay& sp, const float
 // runs: they are computed beside it (one tile per wave) into hfeat [B][80] (features of s | Q_B(s)
 // 0..2, r at 3, Q_B(s') 4..6, action|done bits at 7, Q_T(s') 8..10 at 64..); k_learn computes the
 // rest. Carrying r and the bits here spares k_learn a load that depends on idx.
-__device__ __forceinline__ void store_hfeat(const pm_selfplay& sp, int j, int64_t id, bool nxt, int lane,
-                                            const f32x16 (&c2)[2], const float (&qb)[3], const float (&qt)[3]) {
+__device__ __forceinline__ void store_hfeat(const pm_selfplay& sp, int j, bool nxt, int lane, const f32x16 (&c2)[2],
+                                            const float (&qb)[3], const float (&qt)[3], const float (&rb)[2]) {
     float* row = sp.hfeat + (size_t)j * 80;
     const int h = lane >> 5;
     if (!nxt) {
@@ -159,10 +163,9 @@ __device__ __forceinline__ void store_hfeat(const pm_selfplay& sp, int j, int64_
     }
     if (h == 0) {
         if (!nxt) {
-            const float* tr = sp.trans + id * PM_TRANS_F;
             row[64] = qb[0]; row[65] = qb[1]; row[66] = qb[2];
-            row[67] = tr[7];   // reward
-            row[71] = tr[15];  // action | done << 8 (float bits)
+            row[67] = rb[0];  // reward
+            row[71] = rb[1];  // action | done << 8 (float bits)
         } else {
             row[68] = qb[0]; row[69] = qb[1]; row[70] = qb[2];
             row[72] = qt[0]; row[73] = qt[1]; row[74] = qt[2];
@@ -190,8 +193,9 @@ __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f, bool
     const bool mine = r0 + (lane & 31) < 2 * B && !(pending && push_of(sp, c->pos, c->size, c->max_prio).covers(id));
     f32x16 c2[2];
     float qb[3], qt[3];
-    batch_row_fwd(sp, lw, hf[0], hf[1], id, nxt, lane, c2, qb, qt);
-    if (mine) store_hfeat(sp, j, id, nxt, lane, c2, qb, qt);
+    float rb[2];
+    batch_row_fwd(sp, lw, hf[0], hf[1], id, nxt, lane, c2, qb, qt, rb);
+    if (mine) store_hfeat(sp, j, nxt, lane, c2, qb, qt, rb);
 }
 
 // The fused step's sampler blocks: block b draws samples [64 b, 64 b + 64) (per_sample_block) and then
@@ -221,8 +225,9 @@ __device__ __forceinline__ void sample_fwd_block(const pm_selfplay& sp, int b, S
     const bool mine = j < B && !push_of(sp, c->pos, c->size, c->max_prio).covers(id);
     f32x16 c2[2];
     float qb[3], qt[3];
-    batch_row_fwd(sp, sm.lw, sm.hf, sm.hf + 264, id, nxt, lane, c2, qb, qt);
-    if (mine) store_hfeat(sp, j, id, nxt, lane, c2, qb, qt);
+    float rb[2];
+    batch_row_fwd(sp, sm.lw, sm.hf, sm.hf + 264, id, nxt, lane, c2, qb, qt, rb);
+    if (mine) store_hfeat(sp, j, nxt, lane, c2, qb, qt, rb);
 }
 
 __device__ __forceinline__ void write_opp_lists(const pm_selfplay& sp, OppListSmem& sm, int blk, int i, bool valid,
@@ -761,8 +766,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             const int w = k >= pre[3] ? 3 : k >= pre[2] ? 2 : k >= pre[1] ? 1 : 0;
             const int j = sm.plist[w * 64 + k - pre[w]];
             f32x16 c2[2];
-            float qb[3], qt[3];
-            batch_row_fwd(sp, sm.u.f.lw, sm.u.f.hf, sm.u.f.hf + 264, sm.sidx[j], nxt, lane, c2, qb, qt);
+            float qb[3], qt[3], rb[2];
+            batch_row_fwd(sp, sm.u.f.lw, sm.u.f.hf, sm.u.f.hf + 264, sm.sidx[j], nxt, lane, c2, qb, qt, rb);
             if (wv * 32 + (lane & 31) < 2 * np) {
                 const int h = lane >> 5;
                 if (!nxt) {
@@ -772,10 +777,9 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
                         for (int r = 0; r < 16; ++r) sm.Hs[j][32 * tt + rho(r) + 4 * h] = relu(c2[tt][r]);
                 }
                 if (h == 0) {
-                    if (!nxt) {
-                        const float* tr = sp.trans + sm.sidx[j] * PM_TRANS_F;  // written by this step's k_env
+                    if (!nxt) {  // r and the action|done bits of the row this step's k_actenv wrote
                         sm.qv[j][0] = qb[0]; sm.qv[j][1] = qb[1]; sm.qv[j][2] = qb[2];
-                        sm.qv[j][3] = tr[7]; sm.qv[j][7] = tr[15];
+                        sm.qv[j][3] = rb[0]; sm.qv[j][7] = rb[1];
                     } else {
                         sm.qv[j][4] = qb[0]; sm.qv[j][5] = qb[1]; sm.qv[j][6] = qb[2];
                         sm.qv[j][8] = qt[0]; sm.qv[j][9] = qt[1]; sm.qv[j][10] = qt[2];

@@ -33,7 +33,8 @@ PM_MAX_BATCH = 256
 PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
-ABI_VERSION = 8
+PM_COMM_ID_BYTES = 128
+ABI_VERSION = 9
 
 
 class EnvParams(ctypes.Structure):
@@ -149,6 +150,12 @@ _SIGS = {
     "pm_selfplay_resample": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_commit": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_step_multi": (c_i32, [c_void_p, c_i32, c_void_p]),
+    "pm_comm_unique_id": (c_i32, [ctypes.c_char_p, c_void_p]),
+    "pm_comm_init": (c_i32, [ctypes.c_char_p, c_void_p, c_i32, c_i32, ctypes.POINTER(c_void_p)]),
+    "pm_comm_allreduce_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p]),
+    "pm_comm_destroy": (c_i32, [c_void_p]),
+    "pm_selfplay_step_sharded": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p]),
+    "pm_rnn_selfplay_step_sharded": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_last_error": (ctypes.c_char_p, []),
     "pm_abi_version": (c_i32, []),
     "pm_sizeof": (c_i32, [c_i32]),

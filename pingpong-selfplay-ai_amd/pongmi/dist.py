@@ -66,3 +66,67 @@ def sum_over_ranks(values, device):
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM)
     return [float(v) for v in t.tolist()]
+
+
+def rccl_library_path():
+    """The RCCL shared library the process runs: torch's bundled librccl.so (libtorch_hip loads it at
+    `import torch`), else ROCm's."""
+    for p in (os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"), "/opt/rocm/lib/librccl.so.1"):
+        if os.path.exists(p):
+            return p
+    raise FileNotFoundError("no librccl.so found (torch/lib, /opt/rocm/lib)")
+
+
+class NativeComm:
+    """The learner's gradient all-reduce as a libpongmi-owned RCCL communicator over the ranks of a
+    torch.distributed group (pm_comm_*, include/pongmi.h). Passed as a learner's `allreduce`, it makes
+    every sharded vector step ONE library call (pm_selfplay_step_sharded / pm_rnn_selfplay_step_sharded)
+    with ncclAllReduce on the learner's stream; called on a tensor it is an in-place SUM all-reduce.
+
+    Rank 0 creates the RCCL id and broadcasts it with a status byte over the group, so a failure to
+    bind RCCL raises on every rank (no rank is left waiting in ncclCommInitRank)."""
+
+    def __init__(self, group=None, rccl_path=None):
+        import ctypes
+
+        import torch.distributed as dist
+
+        from . import _lib
+        self._lib = lib = _lib.load()
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        path = (rccl_path or rccl_library_path()).encode()
+        buf = torch.zeros(_lib.PM_COMM_ID_BYTES + 1, dtype=torch.uint8)
+        err = ""
+        if self.rank == 0:
+            rc = lib.pm_comm_unique_id(path, buf.data_ptr())
+            if rc == 0:
+                buf[-1] = 1
+            else:
+                err = lib.pm_last_error().decode(errors="replace")
+        on_dev = dist.get_backend(group) == "nccl"
+        t = buf.cuda() if on_dev else buf
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        buf = t.cpu()
+        if int(buf[-1]) != 1:
+            raise _lib.PongmiError(f"pm_comm_unique_id failed on rank 0: {err or 'see rank 0'}")
+        h = ctypes.c_void_p()
+        _lib.check(lib.pm_comm_init(path, buf.data_ptr(), self.world, self.rank, ctypes.byref(h)), "pm_comm_init")
+        self.handle = h
+
+    @property
+    def pm_comm(self):
+        return self.handle
+
+    def __call__(self, t):
+        from . import _lib
+        _lib.require_device(t, "all-reduce buffer")
+        if t.dtype != torch.float32:
+            raise _lib.PongmiError("NativeComm all-reduces float32 buffers")
+        _lib.check(self._lib.pm_comm_allreduce_f32(self.handle, t.data_ptr(), t.numel(), _lib.stream_ptr()),
+                   "pm_comm_allreduce_f32")
+
+    def close(self):
+        if self.handle:
+            from . import _lib
+            h, self.handle = self.handle, None
+            _lib.check(self._lib.pm_comm_destroy(h), "pm_comm_destroy")

@@ -158,6 +158,11 @@ class RNNSelfPlayLearner:
         """One vector step (n env-steps on this rank) and its `updates_per_step` DRQN updates when
         enabled."""
         U = self.updates_per_step
+        comm = getattr(self.allreduce, "pm_comm", None)
+        if comm is not None:  # pongmi.dist.NativeComm: the sharded step as one call, all-reduce in stream
+            check(self.lib.pm_rnn_selfplay_step_sharded(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), comm,
+                                                        U, stream_ptr()), "pm_rnn_selfplay_step_sharded")
+            return
         if self.world == 1:
             check(self.lib.pm_rnn_selfplay_step_multi(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), U,
                                                       stream_ptr()), "pm_rnn_selfplay_step_multi")

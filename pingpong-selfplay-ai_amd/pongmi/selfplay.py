@@ -20,6 +20,8 @@ Semantics the batching fixes (the reference steps ONE env and updates once per e
     recomputed by pm_selfplay_commit when U > 1.
 Sharded (world > 1): every rank owns n arenas and its own replay; `sp.grad` (520 head grads +
 counters) is summed by one all-reduce per update and every rank applies the identical Adam step.
+`allreduce` is a callable on that buffer (torch.distributed.all_reduce), or a pongmi.dist.NativeComm:
+then a vector step is one library call with the RCCL all-reduce on the learner's stream.
 """
 import ctypes
 
@@ -185,6 +187,15 @@ class SelfPlayLearner:
         """Close a vector step of U > 1 updates: max_prio = max(prios), next-push tree nodes, counters."""
         check(self.lib.pm_selfplay_commit(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_commit")
 
+    def _step_sharded(self, comm):
+        """The sharded step as one library call (pongmi.dist.NativeComm): the all-reduce rides the
+        learner's stream between k_learn and k_adam (same results as the Python sequence)."""
+        if not self._aA_ready:
+            self.act(_lib.PM_ACT_A)
+        check(self.lib.pm_selfplay_step_sharded(ctypes.byref(self.sp), comm, self.updates_per_step, stream_ptr()),
+              "pm_selfplay_step_sharded")
+        self._aA_ready = True
+
     def _step_multi(self):
         U = self.updates_per_step
         if self.world == 1 and self.overlap:
@@ -213,6 +224,10 @@ class SelfPlayLearner:
         """One vector step (n env-steps on this rank) and its `updates_per_step` updates. With
         `overlap` the opponents' act for the next step runs inside the learner's launch
         (bit-identical results)."""
+        comm = getattr(self.allreduce, "pm_comm", None)
+        if comm is not None and self.overlap and not self.sp.fuse_apply:
+            self._step_sharded(comm)
+            return
         if self.updates_per_step > 1:
             self._step_multi()
             return

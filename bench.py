@@ -65,6 +65,20 @@ def pmc_traffic(kernel):
         return None
 
 
+def replicas_identical(dist, params):
+    """N > 1: every rank holds the same learner parameters after the timed region (the replicas apply
+    the identical update to the all-reduced gradients). Compared as the float64 sum of the raw bit
+    patterns and of the values, max == min over ranks."""
+    if dist is None:
+        return None
+    bits = params.view(torch.int32).to(torch.float64)
+    v = torch.stack([bits.sum(), params.to(torch.float64).sum()])
+    hi, lo = v.clone(), -v
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MAX)
+    return bool(torch.equal(hi, -lo))
+
+
 def synthetic_qnet(seed):
     from models.qnet import QNet
     torch.manual_seed(seed)
@@ -237,6 +251,7 @@ def run_rnn(args, dist, rank, world, allreduce):
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    same = replicas_identical(dist, L.learner.params)
     act_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
     env_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)
     upd_s = sum(e[2].elapsed_time(e[3]) for e in evs.values()) * 1e-3 / len(evs)
@@ -258,7 +273,7 @@ def run_rnn(args, dist, rank, world, allreduce):
                        "memory_size": L.cap, "ring_depth": L.depth,
                        "updates_in_timed_region": c["train_steps"] - c0["train_steps"],
                        "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
-                       "all_reduce": args.comm_used if world > 1 else None},
+                       "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same},
             "roofline": {"bound": "mfma", "kernel": "k_rnn_act (+ k_rnn_fold)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
@@ -370,6 +385,7 @@ def main():
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    same = replicas_identical(dist, L.paramsB)
     ae_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
     learn_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)
     c = L.counters()
@@ -391,7 +407,7 @@ def main():
                        "arenas_per_gpu": args.arenas, "global_arenas": args.arenas * world,
                        "pool": args.pool, "batch": args.batch, "updates_per_vector_step": 1,
                        "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
-                       "all_reduce": args.comm_used if world > 1 else None},
+                       "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same},
             "roofline": {"bound": "mfma", "kernel": "k_actenv (modelB's act + env tick + replay push + PER sample "
                                                     "and batch-forward blocks)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",

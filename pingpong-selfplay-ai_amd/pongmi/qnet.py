@@ -63,7 +63,7 @@ def fold(blocks, mode, seed=0, counter=0, counter_dev=None, params_out=None, str
     lib = _lib.load()
     b = blocks.reshape(-1, PM_QNET_NP)
     _lib.require_device(b, "params")
-    w = torch.empty((b.shape[0], PM_QNET_NW), dtype=torch.float32, device=b.device)
+    w = torch.zeros((b.shape[0], PM_QNET_NW), dtype=torch.float32, device=b.device)  # pads stay 0 (deterministic images)
     check(lib.pm_qnet_fold(ptr(b), ptr(params_out), int(mode), int(seed), int(counter), ptr(counter_dev), ptr(w),
                            b.shape[0], stream_ptr(stream)), "pm_qnet_fold")
     return w

@@ -8,6 +8,7 @@ arithmetic with world 2.
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 
@@ -63,7 +64,9 @@ def test_sharded_step_equals_launch_sequence(golden, comm, U):
                 if key == "ctrl":
                     assert sa[key] == sb[key]
                 else:
-                    assert (sa[key] == sb[key]).all(), key
+                    bad = np.argwhere(sa[key] != sb[key])
+                    assert len(bad) == 0, (k, key, len(bad), bad[:4].tolist(), sa[key][tuple(bad[0])],
+                                           sb[key][tuple(bad[0])])
     assert A.counters()["train_steps"] > 0
 
 

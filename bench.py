@@ -213,9 +213,20 @@ def run_rnn(args, dist, rank, world, allreduce):
                            [synthetic_rnn(100 + k) for k in range(pool_n)], epsilon=0.05, seed=7, rank=rank,
                            world=world, allreduce=allreduce)
 
+    from pongmi import _lib
+    overlap = dist is None and L.overlap
+
     def one_step(ev=None):
         if ev is None:
             L.step()
+            return
+        if overlap:  # the production step's two calls: modelB's fold + act, then env + update with the
+            ev[0].record()  # next step's opponent act beside it (the production path's aA is always ready)
+            L.act_part(_lib.PM_ACT_B)
+            ev[1].record()
+            L.finish_overlap()
+            ev[2].record()
+            ev[3].record()
             return
         ev[0].record()
         L.act()
@@ -253,12 +264,13 @@ def run_rnn(args, dist, rank, world, allreduce):
         dt = float(t.item())
     same = replicas_identical(dist, L.learner.params)
     act_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
-    env_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)
+    env_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)  # overlap: env + update
     upd_s = sum(e[2].elapsed_time(e[3]) for e in evs.values()) * 1e-3 / len(evs)
     c = L.counters()
     if rank == 0:
         value = n * world * args.steps / dt
-        achieved = n * RNN_FLOP_PER_ARENA / act_s / 1e12
+        fpa = RNN_FLOP_PER_ARENA // 2 if overlap else RNN_FLOP_PER_ARENA  # overlap: modelB's side only
+        achieved = n * fpa / act_s / 1e12
         env_gbs = n * RNN_ENV_BYTES / env_s / 1e9
         out = {
             "metric": "env-steps/sec (whole node), QNetRNN self-play + DRQN (configs[4])",
@@ -274,19 +286,26 @@ def run_rnn(args, dist, rank, world, allreduce):
                        "updates_in_timed_region": c["train_steps"] - c0["train_steps"],
                        "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
                        "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same},
-            "roofline": {"bound": "mfma", "kernel": "k_rnn_act (+ k_rnn_fold)",
+            "roofline": {"bound": "mfma",
+                         "kernel": "k_rnn_act side B (+ k_rnn_fold): the overlapped step's act" if overlap
+                                   else "k_rnn_act (+ k_rnn_fold)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                         "avg_us": round(act_s * 1e6, 2), "flop_per_arena": RNN_FLOP_PER_ARENA, "n": n},
-            "env_roofline": {"bound": "hbm", "kernel": "k_rsp_env + k_rsp_append + k_rsp_sample",
-                             "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": round(env_gbs / PEAK_HBM_GBS, 4), "avg_us": round(env_s * 1e6, 2),
-                             "bytes_per_env_step": RNN_ENV_BYTES},
-            "drqn_update_us": round(upd_s * 1e6, 2),
+                         "avg_us": round(act_s * 1e6, 2), "flop_per_arena": fpa, "n": n},
+        }
+        if overlap:
+            out["env_update_us"] = round(env_s * 1e6, 2)  # env + sample + DRQN update, the opponents' act beside
+        else:
+            out["env_roofline"] = {"bound": "hbm", "kernel": "k_rsp_env + k_rsp_append + k_rsp_sample",
+                                   "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                   "frac": round(env_gbs / PEAK_HBM_GBS, 4), "avg_us": round(env_s * 1e6, 2),
+                                   "bytes_per_env_step": RNN_ENV_BYTES}
+            out["drqn_update_us"] = round(upd_s * 1e6, 2)
+        out.update({
             "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
                         "seq_size": c["seq_size"], "status": c["status"], **L.learner.stats()},
-        }
+        })
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_rnn(args.cpu_seconds)
         print(json.dumps(out), flush=True)

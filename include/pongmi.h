@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 9
+#define PM_ABI_VERSION 10
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -301,6 +301,9 @@ typedef struct pm_rnn_selfplay {
     int64_t seq_cap, min_episodes;
     double min_epsilon, epsilon_decay, pool_ratio;
     uint64_t seed_env, seed_net;
+    const float *hA_in, *cA_in; /* nullable [n][128]: where the opponents' act reads (h, c) from (it writes
+                                   hA / cA); null = in place. The overlapped step (ABI 10) alternates two
+                                   buffers so a speculative act of the next step can be redone */
 } pm_rnn_selfplay;
 
 /* Ring safety: a stored trajectory is at most depth / 2 steps long (longer ones are dropped, status bit
@@ -324,6 +327,19 @@ int pm_rnn_selfplay_step(const pm_rnn_selfplay *sp, const pm_drqn *d, void *stre
  * x [sample(u) + update]; U = 1 is pm_rnn_selfplay_step. */
 int pm_rnn_selfplay_sample(const pm_rnn_selfplay *sp, const pm_drqn *d, int32_t u, void *stream);
 int pm_rnn_selfplay_step_multi(const pm_rnn_selfplay *sp, const pm_drqn *d, int32_t updates, void *stream);
+/* Overlapped act (ABI 10), as the DQN step's: part PM_ACT_ALL = pm_rnn_selfplay_act, PM_ACT_B = modelB's
+ * fold + act only (select_action_for_model for B, :757-762), PM_ACT_A = the opponents' act only
+ * (:753-755: modelA / pool nets, eval mode). pm_rnn_selfplay_step_overlap = act_part(B) + env + (fork to
+ * side_stream: the NEXT step's act_part(A), on part of the chip) + `updates` DRQN updates + join. The
+ * opponents' act depends on nothing the update writes, so the results are bit-identical to
+ * pm_rnn_selfplay_step_multi. Contract: sp->aA holds the opponents' actions for the current
+ * observations (act_part(A) once, then each overlapped step leaves them for the next). */
+int pm_rnn_selfplay_act_part(const pm_rnn_selfplay *sp, int32_t part, void *stream);
+int pm_rnn_selfplay_step_overlap(const pm_rnn_selfplay *sp, const pm_drqn *d, int32_t updates, void *side_stream,
+                                 void *stream);
+/* step_overlap without its act_part(B) (callers that time modelB's act on its own). */
+int pm_rnn_selfplay_finish_overlap(const pm_rnn_selfplay *sp, const pm_drqn *d, int32_t updates, void *side_stream,
+                                   void *stream);
 
 /* ---------------------------------------------------------------- replay + PER (K4) */
 

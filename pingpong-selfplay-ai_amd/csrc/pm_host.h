@@ -19,6 +19,16 @@ int pm_fail(int code, const char* fmt, ...);
     } while (0)
 
 static inline hipStream_t pm_stream(void* s) { return (hipStream_t)s; }
+
+// K5 act over part of the grid (pm_rnn.hip): part PM_ACT_ALL / PM_ACT_B (modelB's side only) /
+// PM_ACT_A (the opponents' side only); max_blocks > 0 caps the grid (blocks loop over the groups).
+int pm_rnn_act_part(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B, const float* obsA,
+                    const float* obsB, float* hA, float* cA, float* hB, float* cB, const uint8_t* reset, float epsilon,
+                    const double* eps_dev, uint64_t seed, uint64_t counter, const uint64_t* counter_dev, int8_t* aA,
+                    int8_t* aB, float* qA, float* qB, int32_t n, int32_t chunk0, int32_t chunk1,
+                    const int32_t* opp_list, const int32_t* opp_cnt, int32_t part, int32_t max_blocks, void* stream,
+                    const float* hA_in = nullptr, const float* cA_in = nullptr);
+
 static inline unsigned pm_blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
 // ---------------------------------------------------------------- diagnostic stamps (PM_DIAG builds only)

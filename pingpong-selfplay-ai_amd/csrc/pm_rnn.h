@@ -166,17 +166,20 @@ __device__ __forceinline__ void add_bias_lds(const float* b, f32x16& acc) {
 
 // One acting step of QNetRNN for group g of a block's arena list (tiles 4g .. 4g+3, one per wave):
 // q values out through `out`, (h, c) rows updated in HBM. Block-wide (all 4 waves, barriers).
+// (h, c) are read from hin / cin (null: hst / cst, in place) and written to hst / cst.
 template <typename Out>
 __device__ __forceinline__ void rnn_group(const float* __restrict__ w, float* ring, const float* hw,
                                           const float* __restrict__ obs, float* hst, float* cst,
                                           const uint8_t* __restrict__ reset, const int* list, int count, int g,
-                                          const Out& out) {
+                                          const Out& out, const float* hin = nullptr, const float* cin = nullptr) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
     const int row = (4 * g + wave) * 32 + (lane & 31);
     const bool valid = row < count;
     const int arena = list[min(row, count - 1)];
     float* hs = hst + (size_t)arena * 128;
     float* cs = cst + (size_t)arena * 128;
+    const float* hr = (hin ? hin : hst) + (size_t)arena * 128;
+    const float* cr = (cin ? cin : cst) + (size_t)arena * 128;
     const bool zero = reset != nullptr && reset[arena] != 0;
     PM_STG(0);
     PM_STG_CLK(40);
@@ -190,7 +193,7 @@ __device__ __forceinline__ void rnn_group(const float* __restrict__ w, float* ri
 #pragma unroll
         for (int rq = 0; rq < 4; ++rq) {
             const float4 v = zero ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                  : *reinterpret_cast<const float4*>(hs + 32 * t + 8 * rq + 4 * h);
+                                  : *reinterpret_cast<const float4*>(hr + 32 * t + 8 * rq + 4 * h);
             xb[4 + t][4 * rq] = v.x; xb[4 + t][4 * rq + 1] = v.y; xb[4 + t][4 * rq + 2] = v.z; xb[4 + t][4 * rq + 3] = v.w;
         }
     f32x16 c1[2];
@@ -238,7 +241,7 @@ __device__ __forceinline__ void rnn_group(const float* __restrict__ w, float* ri
         float4 cp[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            cp[j] = zero ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(cs + 32 * m + 8 * j + 4 * h);
+            cp[j] = zero ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(cr + 32 * m + 8 * j + 4 * h);
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = f32x16{};
         const int s0 = 2 + 9 * m;

@@ -221,9 +221,9 @@ __device__ __forceinline__ int packed_rows(const int32_t* __restrict__ opp_list,
 // All rows of the block's list, 128 per group (block-uniform loop: every wave takes every barrier).
 __device__ __forceinline__ void rnn_rows(const float* __restrict__ w, RnnShared& sh, const float* __restrict__ obs,
                                          float* hst, float* cst, const uint8_t* __restrict__ reset, int count,
-                                         const RowOut& out) {
+                                         const RowOut& out, const float* hin = nullptr, const float* cin = nullptr) {
     for (int g = 0; g * kRnnRows < count; ++g)
-        rnn_group(w, sh.ring, sh.hw, obs, hst, cst, reset, sh.list, count, g, out);
+        rnn_group(w, sh.ring, sh.hw, obs, hst, cst, reset, sh.list, count, g, out, hin, cin);
 }
 
 __global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_q(const float* __restrict__ w, const float* __restrict__ x,
@@ -244,6 +244,7 @@ struct RnnActArgs {
     const float* w_B;
     const float *obsA, *obsB;
     float *hA, *cA, *hB, *cB;
+    const float *hA_in, *cA_in;  // side A's (h, c) source (null: hA / cA in place)
     const uint8_t* reset;
     int8_t *aA, *aB;
     float *qA, *qB;
@@ -253,10 +254,9 @@ struct RnnActArgs {
     const uint64_t* counter_dev;
 };
 
-// Grid as ActGrid (pm_mfma.h) with kRnnRows-arena chunks on side B; side A grouped by opponent net.
-__global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs A) {
-    __shared__ RnnShared sh;
-    int b = blockIdx.x;
+// Block b of the act grid: ActGrid (pm_mfma.h) with kRnnRows-arena chunks on side B (b < nb); side A
+// grouped by opponent net (b >= nb). Block-wide.
+__device__ __forceinline__ void rnn_act_block(const ActGrid& g, const RnnActArgs& A, int b, RnnShared& sh) {
     const int nb = (g.n + kRnnRows - 1) / kRnnRows;
     const float* w;
     int net = -1, lo, hi;
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs 
         w = A.w_opp + (size_t)k * PM_RNN_NW;
         stage_tables(w, sh.hw);
         __syncthreads();
-        rnn_rows(w, sh, A.obsA, A.hA, A.cA, A.reset, sh.count, RowOut{A.aA, A.qA, -1.0, 0, 0});
+        rnn_rows(w, sh, A.obsA, A.hA, A.cA, A.reset, sh.count, RowOut{A.aA, A.qA, -1.0, 0, 0}, A.hA_in, A.cA_in);
         return;
     }
     if (b < nb) {
@@ -296,7 +296,17 @@ __global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs 
         const double eps = A.eps_dev ? *A.eps_dev : A.eps;
         rnn_rows(w, sh, A.obsB, A.hB, A.cB, A.reset, count, RowOut{A.aB, A.qB, eps, A.seed, ctr});
     } else {
-        rnn_rows(w, sh, A.obsA, A.hA, A.cA, A.reset, count, RowOut{A.aA, A.qA, -1.0, 0, 0});
+        rnn_rows(w, sh, A.obsA, A.hA, A.cA, A.reset, count, RowOut{A.aA, A.qA, -1.0, 0, 0}, A.hA_in, A.cA_in);
+    }
+}
+
+// Blocks [b0, b1) of the act grid, gridDim.x of them at a time (a grid smaller than b1 - b0 loops:
+// the overlapped QNetRNN step runs side A on part of the chip beside the DRQN update).
+__global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs A, int b0, int b1) {
+    __shared__ RnnShared sh;
+    for (int b = b0 + (int)blockIdx.x; b < b1; b += (int)gridDim.x) {
+        __syncthreads();  // the previous block's LDS tables / lists are dead
+        rnn_act_block(g, A, b, sh);
     }
 }
 
@@ -326,18 +336,21 @@ extern "C" int pm_rnn_q(const float* w_eff, const float* x, float* h, float* c, 
     return PM_OK;
 }
 
-extern "C" int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B,
-                          const float* obsA, const float* obsB, float* hA, float* cA, float* hB, float* cB,
-                          const uint8_t* reset, float epsilon, const double* eps_dev, uint64_t seed, uint64_t counter,
-                          const uint64_t* counter_dev, int8_t* aA, int8_t* aB, float* qA, float* qB, int32_t n,
-                          int32_t chunk0, int32_t chunk1, const int32_t* opp_list, const int32_t* opp_cnt,
-                          void* stream) {
+int pm_rnn_act_part(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B, const float* obsA,
+                    const float* obsB, float* hA, float* cA, float* hB, float* cB, const uint8_t* reset, float epsilon,
+                    const double* eps_dev, uint64_t seed, uint64_t counter, const uint64_t* counter_dev, int8_t* aA,
+                    int8_t* aB, float* qA, float* qB, int32_t n, int32_t chunk0, int32_t chunk1,
+                    const int32_t* opp_list, const int32_t* opp_cnt, int32_t part, int32_t max_blocks, void* stream,
+                    const float* hA_in, const float* cA_in) {
     if (n == 0) return PM_OK;
+    PM_REQUIRE(!hA_in == !cA_in && (((uintptr_t)hA_in | (uintptr_t)cA_in) & 15) == 0, PM_E_ARG,
+               "pm_rnn_act: hA_in / cA_in both set (16-B aligned) or both null");
     PM_REQUIRE(w_opp && w_B && obsA && obsB && hA && cA && hB && cB && aA && aB && n > 0 && n_opp >= 1, PM_E_ARG,
                "pm_rnn_act: null buffer or size");
     PM_REQUIRE(((((uintptr_t)w_opp) | ((uintptr_t)w_B) | ((uintptr_t)hA) | ((uintptr_t)cA) | ((uintptr_t)hB) |
                  ((uintptr_t)cB)) & 15) == 0,
                PM_E_ARG, "pm_rnn_act: weights and hidden states must be 16-byte aligned");
+    PM_REQUIRE(part == PM_ACT_ALL || part == PM_ACT_B || part == PM_ACT_A, PM_E_ARG, "pm_rnn_act: part=%d", part);
     if (chunk0 <= 0) chunk0 = 256;
     if (chunk1 <= 0) chunk1 = kRnnList;
     PM_REQUIRE(chunk0 <= kRnnList && chunk1 <= kRnnList, PM_E_SIZE, "pm_rnn_act: chunk > %d", kRnnList);
@@ -347,11 +360,26 @@ extern "C" int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_o
     const ActGrid g{n, opp_id ? n_opp : 1, chunk0, chunk1, 0};
     const int nb = (n + kRnnRows - 1) / kRnnRows;
     const RnnActArgs a{w_opp, opp_id, lists ? opp_list : nullptr, lists ? opp_cnt : nullptr, w_B, obsA, obsB, hA, cA,
-                       hB, cB, reset, aA, aB, qA, qB, (double)epsilon, eps_dev, seed, counter, counter_dev};
+                       hB, cB, hA_in, cA_in, reset, aA, aB, qA, qB, (double)epsilon, eps_dev, seed, counter,
+                       counter_dev};
     const int na = lists ? nb + n_opp : g.blocks();  // packed: sum over nets of ceil(rows / 128) <= nb + nets
-    hipLaunchKernelGGL(k_rnn_act, dim3(nb + na), dim3(kRnnBlock), 0, pm_stream(stream), g, a);
+    const int b0 = part == PM_ACT_A ? nb : 0, b1 = part == PM_ACT_B ? nb : nb + na;
+    int grid = b1 - b0;
+    if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
+    hipLaunchKernelGGL(k_rnn_act, dim3(grid), dim3(kRnnBlock), 0, pm_stream(stream), g, a, b0, b1);
     PM_LAUNCHED("k_rnn_act");
     return PM_OK;
+}
+
+extern "C" int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_opp, const float* w_B,
+                          const float* obsA, const float* obsB, float* hA, float* cA, float* hB, float* cB,
+                          const uint8_t* reset, float epsilon, const double* eps_dev, uint64_t seed, uint64_t counter,
+                          const uint64_t* counter_dev, int8_t* aA, int8_t* aB, float* qA, float* qB, int32_t n,
+                          int32_t chunk0, int32_t chunk1, const int32_t* opp_list, const int32_t* opp_cnt,
+                          void* stream) {
+    return pm_rnn_act_part(w_opp, opp_id, n_opp, w_B, obsA, obsB, hA, cA, hB, cB, reset, epsilon, eps_dev, seed,
+                           counter, counter_dev, aA, aB, qA, qB, n, chunk0, chunk1, opp_list, opp_cnt, PM_ACT_ALL, 0,
+                           stream, nullptr, nullptr);
 }
 
 #ifdef PM_DIAG

@@ -12,6 +12,8 @@
 //                 flag (len(memory) > batch * min_episodes_for_training_start, :768)
 // then pm_drqn_update (K6). Transition rings are [depth][n] records of 64 B written by step
 // (coalesced); an episode is (arena, first step, length), its steps read back from the ring.
+#include <stdlib.h>
+
 #include "pm_host.h"
 #include "pm_mfma.h"
 
@@ -289,17 +291,60 @@ extern "C" int pm_rnn_selfplay_init(const pm_rnn_selfplay* sp, void* stream) {
     return PM_OK;
 }
 
-extern "C" int pm_rnn_selfplay_act(const pm_rnn_selfplay* sp, void* stream) {
-    if (int rc = check(sp)) return rc;
+namespace {
+int act_part(const pm_rnn_selfplay* sp, int part, int max_blocks, void* stream) {
     const uint64_t* ctr = &sp->ctrl->step;
     // modelB.reset_noise() then act (:385-387): one noise draw per vector step for all arenas
-    if (int rc = pm_rnn_fold(sp->paramsB, sp->paramsB, PM_FOLD_TRAIN_FRESH, sp->seed_net, 0, ctr, sp->w_B, 1, stream))
-        return rc;
-    if (int rc = pm_rnn_act(sp->w_opp, sp->opp, 1 + sp->n_pool, sp->w_B, sp->obsA, sp->obsB, sp->hA, sp->cA, sp->hB,
-                            sp->cB, sp->reset, 0.f, &sp->ctrl->epsilon, sp->seed_env, 0, ctr, sp->aA, sp->aB, nullptr,
-                            nullptr, sp->n, sp->chunk_A, sp->chunk_P, sp->opp_list, sp->opp_cnt, stream))
-        return rc;
+    if (part != PM_ACT_A)
+        if (int rc = pm_rnn_fold(sp->paramsB, sp->paramsB, PM_FOLD_TRAIN_FRESH, sp->seed_net, 0, ctr, sp->w_B, 1, stream))
+            return rc;
+    return pm_rnn_act_part(sp->w_opp, sp->opp, 1 + sp->n_pool, sp->w_B, sp->obsA, sp->obsB, sp->hA, sp->cA, sp->hB,
+                           sp->cB, sp->reset, 0.f, &sp->ctrl->epsilon, sp->seed_env, 0, ctr, sp->aA, sp->aB, nullptr,
+                           nullptr, sp->n, sp->chunk_A, sp->chunk_P, sp->opp_list, sp->opp_cnt, part, max_blocks,
+                           stream, sp->hA_in, sp->cA_in);
+}
+
+// Fork / join events of the overlapped step, one pair per device (created on first use).
+int step_events(hipEvent_t& fork, hipEvent_t& join) {
+    static hipEvent_t ev[64][2] = {};
+    int dev = 0;
+    PM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, PM_E_LAUNCH, "hipGetDevice");
+    for (int k = 0; k < 2; ++k)
+        if (!ev[dev][k]) {
+            const hipError_t e = hipEventCreateWithFlags(&ev[dev][k], hipEventDisableTiming);
+            PM_REQUIRE(e == hipSuccess, (int)e, "hipEventCreate: %s", hipGetErrorString(e));
+        }
+    fork = ev[dev][0];
+    join = ev[dev][1];
     return PM_OK;
+}
+
+// CUs left to the DRQN update while the opponents' act runs beside it: the act blocks hold a CU
+// each (one wave per SIMD), so the act grid is capped at the CU count minus this reserve.
+// PONGMI_RNN_RESERVE_CUS overrides the reserve (tuning).
+constexpr int kDrqnReserveCUs = 64;
+int side_a_blocks() {
+    static int cus = 0, reserve = kDrqnReserveCUs;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                     hipSuccess)
+            cus = 256;
+        if (const char* e = getenv("PONGMI_RNN_RESERVE_CUS")) reserve = atoi(e);
+    }
+    return cus > 2 * reserve ? cus - reserve : (cus + 1) / 2;
+}
+}  // namespace
+
+extern "C" int pm_rnn_selfplay_act(const pm_rnn_selfplay* sp, void* stream) {
+    return pm_rnn_selfplay_act_part(sp, PM_ACT_ALL, stream);
+}
+
+extern "C" int pm_rnn_selfplay_act_part(const pm_rnn_selfplay* sp, int32_t part, void* stream) {
+    if (int rc = check(sp)) return rc;
+    PM_REQUIRE(part == PM_ACT_ALL || part == PM_ACT_B || part == PM_ACT_A, PM_E_ARG,
+               "pm_rnn_selfplay_act_part: part=%d", part);
+    return act_part(sp, part, 0, stream);
 }
 
 extern "C" int pm_rnn_selfplay_env(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {
@@ -339,6 +384,48 @@ extern "C" int pm_rnn_selfplay_step(const pm_rnn_selfplay* sp, const pm_drqn* d,
     PM_REQUIRE(d, PM_E_ARG, "pm_rnn_selfplay_step: null learner");
     if (int rc = pm_rnn_selfplay_rollout(sp, d, stream)) return rc;
     return pm_drqn_update(d, stream);
+}
+
+// The overlapped vector step. The opponents' act (modelA / pool nets in eval mode, :753-755) reads
+// only what the env kernel writes (obs A, opponent ids, reset flags) and their own (h, c), never the
+// DRQN update's parameters, so the NEXT step's side A runs on `side_stream` beside this step's update
+// (on part of the chip: the update's kernels are a few dozen blocks each), and this step's act is
+// modelB's side only. Results are bit-identical to pm_rnn_selfplay_step_multi.
+// Contract: sp->aA holds the opponents' actions for the current observations (pm_rnn_selfplay_act_part
+// with PM_ACT_A, or the previous overlapped step); on return `stream` has joined the side stream.
+extern "C" int pm_rnn_selfplay_step_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates,
+                                            void* side_stream, void* stream) {
+    if (int rc = check(sp)) return rc;
+    if (int rc = act_part(sp, PM_ACT_B, 0, stream)) return rc;
+    return pm_rnn_selfplay_finish_overlap(sp, d, updates, side_stream, stream);
+}
+
+// The overlapped step after modelB's act: env + sample, fork (the next step's opponent act on the
+// side stream), the updates, join.
+extern "C" int pm_rnn_selfplay_finish_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates,
+                                              void* side_stream, void* stream) {
+    if (int rc = check(sp)) return rc;
+    PM_REQUIRE(d, PM_E_ARG, "pm_rnn_selfplay_step_overlap: null learner");
+    PM_REQUIRE(updates >= 1, PM_E_ARG, "pm_rnn_selfplay_step_overlap: updates=%d", updates);
+    PM_REQUIRE(side_stream && side_stream != stream, PM_E_ARG, "pm_rnn_selfplay_step_overlap: needs a second stream");
+    hipEvent_t fork, join;
+    if (int rc = step_events(fork, join)) return rc;
+    hipStream_t st = pm_stream(stream), side = pm_stream(side_stream);
+    if (int rc = pm_rnn_selfplay_env(sp, d, stream)) return rc;
+    hipError_t e = hipEventRecord(fork, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+    PM_REQUIRE(e == hipSuccess, (int)e, "step_overlap fork: %s", hipGetErrorString(e));
+    if (int rc = act_part(sp, PM_ACT_A, side_a_blocks(), side_stream)) return rc;
+    e = hipEventRecord(join, side);
+    PM_REQUIRE(e == hipSuccess, (int)e, "step_overlap join record: %s", hipGetErrorString(e));
+    if (int rc = pm_drqn_update(d, stream)) return rc;
+    for (int u = 1; u < updates; ++u) {
+        if (int rc = pm_rnn_selfplay_sample(sp, d, u, stream)) return rc;
+        if (int rc = pm_drqn_update(d, stream)) return rc;
+    }
+    e = hipStreamWaitEvent(st, join, 0);
+    PM_REQUIRE(e == hipSuccess, (int)e, "step_overlap join: %s", hipGetErrorString(e));
+    return PM_OK;
 }
 
 extern "C" int pm_rnn_selfplay_step_multi(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates, void* stream) {

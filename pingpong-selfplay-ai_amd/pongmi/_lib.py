@@ -34,7 +34,7 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class EnvParams(ctypes.Structure):
@@ -95,7 +95,7 @@ class RnnSelfPlay(ctypes.Structure):
         [(n, c_i32) for n in ("n", "n_pool", "depth", "T", "chunk_A", "chunk_P", "max_steps", "_pad")] + \
         [("seq_cap", c_i64), ("min_episodes", c_i64)] + \
         [(n, c_double) for n in ("min_epsilon", "epsilon_decay", "pool_ratio")] + \
-        [("seed_env", c_u64), ("seed_net", c_u64)]
+        [("seed_env", c_u64), ("seed_net", c_u64), ("hA_in", c_void_p), ("cA_in", c_void_p)]
 
 
 CTRL_DTYPE_BYTES = ctypes.sizeof(Ctrl)
@@ -150,6 +150,9 @@ _SIGS = {
     "pm_selfplay_resample": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_commit": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_step_multi": (c_i32, [c_void_p, c_i32, c_void_p]),
+    "pm_rnn_selfplay_act_part": (c_i32, [c_void_p, c_i32, c_void_p]),
+    "pm_rnn_selfplay_step_overlap": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p]),
+    "pm_rnn_selfplay_finish_overlap": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p]),
     "pm_comm_unique_id": (c_i32, [ctypes.c_char_p, c_void_p]),
     "pm_comm_init": (c_i32, [ctypes.c_char_p, c_void_p, c_i32, c_i32, ctypes.POINTER(c_void_p)]),
     "pm_comm_allreduce_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p]),

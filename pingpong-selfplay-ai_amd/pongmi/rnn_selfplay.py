@@ -22,6 +22,9 @@ Semantics the batching fixes (the reference steps ONE env and runs train_step_rn
   * max_episode_steps (:751, default 1000): an episode still running after that many steps ends
     (counters, epsilon decay, new opponent, env.reset, zero (h, c)) while its trajectory goes on
     collecting steps until a done, as push_step's current_episode_trajectory does.
+Overlap (default): the opponents' act of the next vector step (modelA / pool nets in eval mode) reads
+nothing the DRQN update writes, so it runs on a side stream beside the update on part of the chip
+and each step's act is modelB's side only (pm_rnn_selfplay_step_overlap); results are bit-identical.
 Sharded (world > 1): every rank owns n arenas and its own sequence buffer; the gradient (+ the
 contributing-rank count) is summed by one all-reduce per update and every rank applies the
 identical clip + Adam step (pongmi.drqn).
@@ -56,8 +59,14 @@ class RNNSelfPlayLearner:
                  memory_size=200_000, min_episodes_for_training_start=10, depth=None, gamma=0.99, lr=1e-4,
                  epsilon=1.0, min_epsilon=0.05, epsilon_decay=0.999, target_update_interval=2000, pool_ratio=0.4,
                  grad_clip_norm=1.0, episode=0, seed=0, rank=0, world=1, allreduce=None, device=None,
-                 updates_per_step=1, max_episode_steps=1000):
+                 updates_per_step=1, max_episode_steps=1000, overlap=True):
         self.lib = _lib.load()
+        self.overlap = bool(overlap)
+        # The overlapped step acts for the NEXT step's opponents speculatively, reading (h, c) of
+        # buffer _cur and writing the other one; _spec: that act is done for the current observations
+        # (its input state still intact in buffer 1 - _cur), _stale: the opponents changed since, so it
+        # is redone from that state before the next step (bit-identical to the plain step).
+        self._cur, self._spec, self._stale = 0, False, False
         self.updates_per_step = int(updates_per_step)
         if self.updates_per_step < 1:
             raise ValueError("updates_per_step must be >= 1")
@@ -82,7 +91,9 @@ class RNNSelfPlayLearner:
         self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
         self.ep_steps = torch.zeros(n, dtype=torch.int32, device=dev)
         self.reset = torch.ones(n, dtype=torch.uint8, device=dev)
-        self.hA, self.cA, self.hB, self.cB = (torch.zeros((n, 128), **f32) for _ in range(4))
+        self.hB, self.cB = (torch.zeros((n, 128), **f32) for _ in range(2))
+        self._hAb = [torch.zeros((n, 128), **f32) for _ in range(2)]  # opponents' (h, c): two buffers each
+        self._cAb = [torch.zeros((n, 128), **f32) for _ in range(2)]
         self.obsA = torch.zeros((n, 7), **f32)
         self.obsB = torch.zeros((n, 7), **f32)
         self.aA = torch.zeros(n, dtype=torch.int8, device=dev)
@@ -132,20 +143,72 @@ class RNNSelfPlayLearner:
         self.seed = int(seed)
         sp.seed_env, sp.seed_net = shard_seeds(self.seed, self.rank)
         self.sp = sp
+        self.side = torch.cuda.Stream(device=dev)  # the overlapped step's opponent act (beside the update)
         check(self.lib.pm_rnn_selfplay_init(ctypes.byref(sp), stream_ptr()), "pm_rnn_selfplay_init")
 
     # ------------------------------------------------------------------ stepping
+    @property
+    def hA(self):
+        """The opponents' hidden state after the latest act for them, [n, 128]."""
+        return self._hAb[self._cur]
+
+    @property
+    def cA(self):
+        return self._cAb[self._cur]
+
+    def _opp_buffers(self, src, dst):
+        """The opponents' act reads (h, c) from buffer src (None: dst, in place) and writes buffer dst."""
+        sp = self.sp
+        sp.hA, sp.cA = ptr(self._hAb[dst]), ptr(self._cAb[dst])
+        sp.hA_in = None if src is None else ptr(self._hAb[src])
+        sp.cA_in = None if src is None else ptr(self._cAb[src])
+
+    def _prepare_overlap(self):
+        """Before an overlapped step: the opponents' actions for the current observations (the last
+        step's speculative act, redone from its saved input state if the opponents changed since, or a
+        first act in place), then point the act at the other buffer."""
+        if not self._spec or self._stale:
+            self._opp_buffers(1 - self._cur if self._spec else None, self._cur)
+            check(self.lib.pm_rnn_selfplay_act_part(ctypes.byref(self.sp), _lib.PM_ACT_A, stream_ptr()),
+                  "pm_rnn_selfplay_act_part")
+        self._opp_buffers(self._cur, 1 - self._cur)
+
+    def _commit_overlap(self):
+        self._cur = 1 - self._cur
+        self._opp_buffers(None, self._cur)
+        self._spec, self._stale = True, False
+
     def act(self):
-        """modelB fold with fresh noise + both players' act."""
+        """modelB fold with fresh noise + both players' act (in place)."""
+        self._spec = False
         check(self.lib.pm_rnn_selfplay_act(ctypes.byref(self.sp), stream_ptr()), "pm_rnn_selfplay_act")
+
+    def act_part(self, part):
+        """PM_ACT_B: modelB's fold (fresh noise) + act; PM_ACT_A: the opponents' act; PM_ACT_ALL: both
+        (in place)."""
+        if part != _lib.PM_ACT_B:
+            self._spec = False
+        check(self.lib.pm_rnn_selfplay_act_part(ctypes.byref(self.sp), int(part), stream_ptr()),
+              "pm_rnn_selfplay_act_part")
+
+    def finish_overlap(self):
+        """The overlapped step after act_part(PM_ACT_B): env + sample, the next step's opponent act on
+        the side stream beside the updates, join."""
+        self._prepare_overlap()
+        check(self.lib.pm_rnn_selfplay_finish_overlap(ctypes.byref(self.sp), ctypes.byref(self.learner.desc),
+                                                      self.updates_per_step, self.side.cuda_stream, stream_ptr()),
+              "pm_rnn_selfplay_finish_overlap")
+        self._commit_overlap()
 
     def env_step(self):
         """env tick + sequence store + counters + batch sample / enable flag."""
+        self._spec = False
         check(self.lib.pm_rnn_selfplay_env(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),
               "pm_rnn_selfplay_env")
 
     def rollout(self):
         """fold + act + env + sequence store + batch sample (no update)."""
+        self._spec = False
         check(self.lib.pm_rnn_selfplay_rollout(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),
               "pm_rnn_selfplay_rollout")
 
@@ -160,9 +223,18 @@ class RNNSelfPlayLearner:
         U = self.updates_per_step
         comm = getattr(self.allreduce, "pm_comm", None)
         if comm is not None:  # pongmi.dist.NativeComm: the sharded step as one call, all-reduce in stream
+            self._spec = False
             check(self.lib.pm_rnn_selfplay_step_sharded(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), comm,
                                                         U, stream_ptr()), "pm_rnn_selfplay_step_sharded")
             return
+        if self.world == 1 and self.overlap:  # the next step's opponent act beside this step's update
+            self._prepare_overlap()
+            check(self.lib.pm_rnn_selfplay_step_overlap(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), U,
+                                                        self.side.cuda_stream, stream_ptr()),
+                  "pm_rnn_selfplay_step_overlap")
+            self._commit_overlap()
+            return
+        self._spec = False
         if self.world == 1:
             check(self.lib.pm_rnn_selfplay_step_multi(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), U,
                                                       stream_ptr()), "pm_rnn_selfplay_step_multi")
@@ -207,6 +279,7 @@ class RNNSelfPlayLearner:
 
     def set_modelA(self, state):
         """Opponent slot 0: modelA, frozen and in eval mode (train_rnn_iterative.py:343-344)."""
+        self._stale = self._spec
         self.paramsA = pack_state_dict(state, self.device)
         self.w_opp[0] = fold(self.paramsA, _lib.PM_FOLD_EVAL)[0]
 
@@ -232,6 +305,7 @@ class RNNSelfPlayLearner:
 
     def add_pool_model(self, state):
         """pool_models.append(net in eval mode) (:855-859): opponent slot n_pool + 1 for later draws."""
+        self._stale = self._spec
         w = fold(pack_state_dict(state, self.device), _lib.PM_FOLD_EVAL)
         self.w_opp = torch.cat([self.w_opp, w], 0).contiguous()
         self.n_pool += 1

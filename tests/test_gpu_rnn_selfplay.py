@@ -53,8 +53,11 @@ def test_rnn_selfplay_steps_match_oracle(golden, orc, max_steps):
     """max_steps = 24 exercises the max_episode_steps cut (:751): the episode ends (new opponent,
     serve, zero (h, c), counters) but the trajectory goes on until a done."""
     from pongmi import rnn
+    # overlap=False: this test reads the opponents' (h, c) after every step, which the overlapped
+    # step has already advanced for the next one (test_rnn_overlapped_step_is_bitwise_identical)
     L = _learner(golden, n=256, n_pool=2, epsilon=0.0, min_epsilon=0.0, pool_ratio=0.5,
-                 min_episodes_for_training_start=10 ** 6, memory_size=4096, seed=3, max_episode_steps=max_steps)
+                 min_episodes_for_training_start=10 ** 6, memory_size=4096, seed=3, max_episode_steps=max_steps,
+                 overlap=False)
     n, sp = L.n, L.sp
     pv = orc.env_params_from_kwargs(**ENV_KW)
     P = orc.make_params(pv)
@@ -265,3 +268,41 @@ def test_rnn_updates_per_step(golden):
     assert torch.equal(A.learner.params, B.learner.params) and torch.equal(A.trans, B.trans)
     assert A.counters() == B.counters()
     assert enabled > 10 and A.learner.stats()["steps"] == U * enabled
+
+
+@pytest.mark.parametrize("U", [1, 2])
+def test_rnn_overlapped_step_is_bitwise_identical(golden, U):
+    """pm_rnn_selfplay_step_overlap (the next step's opponent act on a side stream beside the DRQN
+    update, modelB's act only in the step) against the plain step: every state, action, ring record,
+    parameter and counter equal, also across a pool model added and a modelA swap mid-run."""
+    from pongmi import _lib
+    kw = dict(n=1024, n_pool=2, epsilon=0.3, memory_size=2000, min_episodes_for_training_start=1, seed=6,
+              updates_per_step=U)
+    A = _learner(golden, overlap=False, **kw)
+    B = _learner(golden, overlap=True, **kw)
+    for k in range(60):
+        if k == 25:
+            for L in (A, B):
+                L.add_pool_model(_rnn_sd(300))
+        if k == 40:
+            for L in (A, B):
+                L.set_modelA(_rnn_sd(301))
+        A.step()
+        B.step()
+        if k % 10 == 9:
+            sa, sb = _snap(A), _snap(B)
+            for key in sa:
+                if key in ("hA", "cA"):  # B's opponent side is already one act ahead (the next step's)
+                    continue
+                if key == "ctrl":
+                    assert sa[key] == sb[key], k
+                elif isinstance(sa[key], torch.Tensor):
+                    assert torch.equal(sa[key], sb[key]), (k, key)
+                else:
+                    assert np.array_equal(sa[key], sb[key]), (k, key)
+    A.act_part(_lib.PM_ACT_A)  # A's opponents act for the current observations, as B's already did
+    torch.cuda.synchronize()
+    assert torch.equal(A.learner.params, B.learner.params)
+    assert torch.equal(A.trans, B.trans) and torch.equal(A.aA, B.aA) and torch.equal(A.aB, B.aB)
+    assert torch.equal(A.hA, B.hA) and torch.equal(A.cA, B.cA)
+    assert A.learner.stats()["steps"] == B.learner.stats()["steps"] > 0

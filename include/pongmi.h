@@ -526,6 +526,9 @@ int pm_selfplay_step_sharded(const pm_selfplay* sp, pm_comm* comm, int32_t updat
  * all-reduce of d->grad (gradients + contributing-rank count) + pm_drqn_apply. */
 int pm_rnn_selfplay_step_sharded(const pm_rnn_selfplay* sp, const pm_drqn* d, pm_comm* comm, int32_t updates,
                                  void* stream);
+/* pm_rnn_selfplay_step_overlap (ABI 10) with every update's gradient all-reduced in stream order. */
+int pm_rnn_selfplay_step_sharded_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, pm_comm* comm, int32_t updates,
+                                         void* side_stream, void* stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* pm_last_error(void);

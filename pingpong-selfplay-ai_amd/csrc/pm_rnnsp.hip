@@ -393,18 +393,19 @@ extern "C" int pm_rnn_selfplay_step(const pm_rnn_selfplay* sp, const pm_drqn* d,
 // modelB's side only. Results are bit-identical to pm_rnn_selfplay_step_multi.
 // Contract: sp->aA holds the opponents' actions for the current observations (pm_rnn_selfplay_act_part
 // with PM_ACT_A, or the previous overlapped step); on return `stream` has joined the side stream.
-extern "C" int pm_rnn_selfplay_step_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates,
-                                            void* side_stream, void* stream) {
-    if (int rc = check(sp)) return rc;
-    if (int rc = act_part(sp, PM_ACT_B, 0, stream)) return rc;
-    return pm_rnn_selfplay_finish_overlap(sp, d, updates, side_stream, stream);
+namespace {
+// One DRQN update; sharded (comm): grads, the in-stream all-reduce of d->grad, apply.
+int drqn_update(const pm_drqn* d, pm_comm* comm, void* stream) {
+    if (!comm) return pm_drqn_update(d, stream);
+    if (int rc = pm_drqn_grads(d, stream)) return rc;
+    if (int rc = pm_comm_allreduce_f32(comm, d->grad, PM_RNN_NPARAM + 4, stream)) return rc;
+    return pm_drqn_apply(d, stream);
 }
 
 // The overlapped step after modelB's act: env + sample, fork (the next step's opponent act on the
 // side stream), the updates, join.
-extern "C" int pm_rnn_selfplay_finish_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates,
-                                              void* side_stream, void* stream) {
-    if (int rc = check(sp)) return rc;
+int finish_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, pm_comm* comm, int32_t updates, void* side_stream,
+                   void* stream) {
     PM_REQUIRE(d, PM_E_ARG, "pm_rnn_selfplay_step_overlap: null learner");
     PM_REQUIRE(updates >= 1, PM_E_ARG, "pm_rnn_selfplay_step_overlap: updates=%d", updates);
     PM_REQUIRE(side_stream && side_stream != stream, PM_E_ARG, "pm_rnn_selfplay_step_overlap: needs a second stream");
@@ -418,14 +419,44 @@ extern "C" int pm_rnn_selfplay_finish_overlap(const pm_rnn_selfplay* sp, const p
     if (int rc = act_part(sp, PM_ACT_A, side_a_blocks(), side_stream)) return rc;
     e = hipEventRecord(join, side);
     PM_REQUIRE(e == hipSuccess, (int)e, "step_overlap join record: %s", hipGetErrorString(e));
-    if (int rc = pm_drqn_update(d, stream)) return rc;
-    for (int u = 1; u < updates; ++u) {
-        if (int rc = pm_rnn_selfplay_sample(sp, d, u, stream)) return rc;
-        if (int rc = pm_drqn_update(d, stream)) return rc;
+    for (int u = 0; u < updates; ++u) {
+        if (u)
+            if (int rc = pm_rnn_selfplay_sample(sp, d, u, stream)) return rc;
+        if (int rc = drqn_update(d, comm, stream)) return rc;
     }
     e = hipStreamWaitEvent(st, join, 0);
     PM_REQUIRE(e == hipSuccess, (int)e, "step_overlap join: %s", hipGetErrorString(e));
     return PM_OK;
+}
+}  // namespace
+
+// The overlapped vector step. The opponents' act (modelA / pool nets in eval mode, :753-755) reads
+// only what the env kernel writes (obs A, opponent ids, reset flags) and their own (h, c), never the
+// DRQN update's parameters, so the NEXT step's side A runs on `side_stream` beside this step's update
+// (on part of the chip: the update's kernels are a few dozen blocks each), and this step's act is
+// modelB's side only. Results are bit-identical to pm_rnn_selfplay_step_multi.
+// Contract: sp->aA holds the opponents' actions for the current observations (pm_rnn_selfplay_act_part
+// with PM_ACT_A, or the previous overlapped step); on return `stream` has joined the side stream.
+extern "C" int pm_rnn_selfplay_step_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates,
+                                            void* side_stream, void* stream) {
+    if (int rc = check(sp)) return rc;
+    if (int rc = act_part(sp, PM_ACT_B, 0, stream)) return rc;
+    return finish_overlap(sp, d, nullptr, updates, side_stream, stream);
+}
+
+extern "C" int pm_rnn_selfplay_finish_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates,
+                                              void* side_stream, void* stream) {
+    if (int rc = check(sp)) return rc;
+    return finish_overlap(sp, d, nullptr, updates, side_stream, stream);
+}
+
+// Sharded and overlapped: the same step with every update's gradient all-reduced in stream order.
+extern "C" int pm_rnn_selfplay_step_sharded_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, pm_comm* comm,
+                                                    int32_t updates, void* side_stream, void* stream) {
+    if (int rc = check(sp)) return rc;
+    PM_REQUIRE(comm, PM_E_ARG, "pm_rnn_selfplay_step_sharded_overlap: null comm");
+    if (int rc = act_part(sp, PM_ACT_B, 0, stream)) return rc;
+    return finish_overlap(sp, d, comm, updates, side_stream, stream);
 }
 
 extern "C" int pm_rnn_selfplay_step_multi(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t updates, void* stream) {

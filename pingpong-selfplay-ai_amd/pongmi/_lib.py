@@ -159,6 +159,7 @@ _SIGS = {
     "pm_comm_destroy": (c_i32, [c_void_p]),
     "pm_selfplay_step_sharded": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_rnn_selfplay_step_sharded": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
+    "pm_rnn_selfplay_step_sharded_overlap": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p, c_void_p]),
     "pm_last_error": (ctypes.c_char_p, []),
     "pm_abi_version": (c_i32, []),
     "pm_sizeof": (c_i32, [c_i32]),

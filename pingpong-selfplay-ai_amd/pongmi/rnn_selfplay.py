@@ -222,6 +222,13 @@ class RNNSelfPlayLearner:
         enabled."""
         U = self.updates_per_step
         comm = getattr(self.allreduce, "pm_comm", None)
+        if comm is not None and self.overlap:  # sharded + overlapped: one call, all-reduce in stream
+            self._prepare_overlap()
+            check(self.lib.pm_rnn_selfplay_step_sharded_overlap(ctypes.byref(self.sp), ctypes.byref(self.learner.desc),
+                                                                comm, U, self.side.cuda_stream, stream_ptr()),
+                  "pm_rnn_selfplay_step_sharded_overlap")
+            self._commit_overlap()
+            return
         if comm is not None:  # pongmi.dist.NativeComm: the sharded step as one call, all-reduce in stream
             self._spec = False
             check(self.lib.pm_rnn_selfplay_step_sharded(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), comm,

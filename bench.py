@@ -130,6 +130,7 @@ def time_act_full(L, launches=50):
     (idempotent: same observations, same sample, same actions), HIP events on its stream: both QNet
     forwards per arena, 19 200 FLOP."""
     from pongmi import _lib
+    featB, L.sp.featB = L.sp.featB, None  # both players' act alone (no features computed ahead)
     for _ in range(5):
         L.act(_lib.PM_ACT_ALL)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -138,6 +139,8 @@ def time_act_full(L, launches=50):
         L.act(_lib.PM_ACT_ALL)
     e1.record()
     e1.synchronize()
+    L.sp.featB = featB
+    L._aA_ready = False
     t = e0.elapsed_time(e1) * 1e-3 / launches
     achieved = L.n * 2 * FLOP_PER_ARENA / t / 1e12
     return {"bound": "mfma", "kernel": "k_act_sp (PM_ACT_ALL: both players + the PER sample blocks)",

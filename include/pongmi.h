@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 10
+#define PM_ABI_VERSION 11
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -417,6 +417,10 @@ typedef struct pm_selfplay {
     int64_t beta_frames, target_update_interval;
     uint64_t seed_env;       /* rank-specific: serves, opponents, epsilon draws */
     uint64_t seed_net;       /* rank-independent: NoisyNet noise, so replicas stay identical */
+    float *featB;            /* nullable [ceil(n/32)][8][64][4]: modelB's hidden features of the current
+                                observations (ABI 11), computed ahead by the side-A act work (the learner
+                                launch's extra blocks, pm_selfplay_act_part A / ALL); pm_selfplay_actenv
+                                then evaluates only the heads. NULL: actenv computes the features */
 } pm_selfplay;
 
 /* Limits: 1 <= batch <= PM_MAX_BATCH (one learner workgroup), batch < n <= cap (every vector step

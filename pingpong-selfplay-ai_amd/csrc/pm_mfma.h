@@ -505,4 +505,55 @@ __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const
     run_tiles(sh.lw, obs, sh.list, sh.count, out, pre);
 }
 
+// modelB's hidden features for the NEXT vector step, computed ahead of the update (the features
+// 7 -> 64 -> 64 are frozen, models/qnet.py:62 with train_iterative.py:97: only the dueling heads
+// train, so they depend on the observations alone). Tiles [t0, t1) of 32 arenas of obs, one per wave
+// at a time: the pre-ReLU layer-2 accumulators c2 of tile_hidden, stored so that the act reads them
+// with coalesced float4 loads: tile T, piece k (0..3: c2[0][4k..4k+3], 4..7: c2[1][4(k-4)..]), lane l
+// at feat4[(T * 8 + k) * 64 + l]. Bit-identical to computing the tile in the act. Block-wide; lw:
+// kLwFloats of LDS for the fragment image of w.
+constexpr int kFeatTileFloats = 8 * 64 * 4;
+// 16-B store with sc1 (write-through: the line leaves this XCD's L2 instead of staying dirty there
+// until the kernel's end-of-launch write-back; the features are read by the next launch only).
+__device__ __forceinline__ void store_f4_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, float4 v) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&v), r, byte_off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ void feat_tiles(float* lw, const float* __restrict__ w, const float* __restrict__ obs, int n,
+                                           int t0, int t1, float* __restrict__ feat) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    stage_frags_lds(w, lw, t0);
+    int tl = t0 + wave;
+    float xs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tl < t1) tile_inputs(obs + (size_t)min(tl * 32 + (lane & 31), n - 1) * 7, lane >> 5, xs);
+    __syncthreads();
+    for (; tl < t1; tl += nw) {  // wave-uniform
+        const int tn = tl + nw;
+        float xn[4] = {xs[0], xs[1], xs[2], xs[3]};
+        if (tn < t1) tile_inputs(obs + (size_t)min(tn * 32 + (lane & 31), n - 1) * 7, lane >> 5, xn);
+        f32x16 c2[2];
+        tile_hidden(lw, xs, lane, c2);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(feat, (short)0, 0x7fffffff, 0x00020000);
+        const int off = (tl * 8 * 64 + lane) * 16;  // bytes; < 2 GB for n < 2^23 arenas
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            store_f4_sc1(rs, off + k * 64 * 16, make_float4(c2[0][4 * k], c2[0][4 * k + 1], c2[0][4 * k + 2], c2[0][4 * k + 3]));
+            store_f4_sc1(rs, off + (4 + k) * 64 * 16,
+                         make_float4(c2[1][4 * k], c2[1][4 * k + 1], c2[1][4 * k + 2], c2[1][4 * k + 3]));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xs[k] = xn[k];
+    }
+}
+// One tile's features as feat_tiles stored them.
+__device__ __forceinline__ void feat_load(const float* __restrict__ feat, int tile, int lane, f32x16 (&c2)[2]) {
+    const float4* src = reinterpret_cast<const float4*>(feat) + (size_t)tile * 8 * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 a = src[k * 64], b = src[(4 + k) * 64];
+        c2[0][4 * k] = a.x; c2[0][4 * k + 1] = a.y; c2[0][4 * k + 2] = a.z; c2[0][4 * k + 3] = a.w;
+        c2[1][4 * k] = b.x; c2[1][4 * k + 1] = b.y; c2[1][4 * k + 2] = b.z; c2[1][4 * k + 3] = b.w;
+    }
+}
+
 }  // namespace pm

@@ -107,10 +107,23 @@ union ActSpShared {
     ActShared act;
     PerSampleSmem per;
 };
+// Feature tiles per feature block: 8 (256-thread blocks, two tiles per wave) / 16 (k_learn's 1024).
+constexpr int kFeatTilesAct = 8, kFeatTilesLearn = 16;
+__host__ __device__ inline int feat_ntiles(int n) { return (n + 31) / 32; }
+
 __global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp, int part) {
     __shared__ __attribute__((aligned(16))) ActSpShared sh;
     PM_BLK(0);
     const int nsb = part == PM_ACT_A ? 0 : (sp.batch + PER_BS - 1) / PER_BS;
+    {   // parts A / ALL with featB: modelB's features for these observations, blocks after the act grid
+        const ActGrid g{sp.n, sp.n_pool + 1, sp.chunk_A, sp.chunk_P, part == PM_ACT_A ? 0 : 1};
+        const int fb = (int)blockIdx.x - nsb - g.blocks();
+        if (fb >= 0) {  // block-uniform
+            const int t0 = fb * kFeatTilesAct;
+            feat_tiles(sh.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + kFeatTilesAct, feat_ntiles(sp.n)), sp.featB);
+            return;
+        }
+    }
     if ((int)blockIdx.x < nsb) {
         PM_STAMP(64);
         sample_block(sp, (int)blockIdx.x, true, sh.per);
@@ -263,7 +276,15 @@ __device__ __forceinline__ void env_block(const pm_selfplay& sp, int blk, EnvSme
     if (blk == 0) PM_STAMP_ANY(72);
     PM_ENV_STAMP(0, blk);
     float xs[2][4];
-    if (ACT) {
+    f32x16 fc2[2][2];  // featB: this wave's two tiles of modelB's features (computed ahead)
+    if (ACT && sp.featB) {
+        // heads only: F_H .. F_BH of the acting image (65 float4) -> LDS; the features from featB
+        if (threadIdx.x < 65)
+            reinterpret_cast<float4*>(lw + F_H)[threadIdx.x] =
+                reinterpret_cast<const float4*>(sp.w_B + PLAIN + F_H)[threadIdx.x];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) feat_load(sp.featB, blk * 8 + 2 * wv + k, lane, fc2[k]);
+    } else if (ACT) {
         stage_frags_lds(sp.w_B, lw, blk);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -312,13 +333,18 @@ __device__ __forceinline__ void env_block(const pm_selfplay& sp, int blk, EnvSme
     }
     if (ACT) {
         __syncthreads();  // the fragment image is staged (every load of the block has landed)
+        PM_ENV_STAMP(7, blk);
         int act[2];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            f32x16 c2[2];
             float q[3];
-            tile_hidden(lw, xs[k], lane, c2);
-            tile_heads(lw + F_H, c2, lane, q);
+            if (sp.featB) {
+                tile_heads(lw + F_H, fc2[k], lane, q);
+            } else {
+                f32x16 c2[2];
+                tile_hidden(lw, xs[k], lane, c2);
+                tile_heads(lw + F_H, c2, lane, q);
+            }
             act[k] = argmax3(q);
         }
         aB = lane < 32 ? act[0] : act[1];
@@ -640,6 +666,12 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         // (the learner is the longer of the two), so they start after its loads are in flight
         __builtin_amdgcn_s_sleep(127);
         const ActGrid g{sp.n, sp.n_pool + 1, chunkA, chunkP, 0};
+        const int fb = (int)blockIdx.x - 1 - g.blocks();
+        if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB)
+            const int t0 = fb * kFeatTilesLearn;
+            feat_tiles(shm.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + kFeatTilesLearn, feat_ntiles(sp.n)), sp.featB);
+            return;
+        }
         const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
         act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,
                   (int)blockIdx.x - 1, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
@@ -1136,7 +1168,8 @@ namespace {
 int launch_act(const pm_selfplay* sp, int part, hipStream_t st) {
     const ActGrid g{sp->n, sp->n_pool + 1, sp->chunk_A, sp->chunk_P, part == PM_ACT_A ? 0 : 1};
     const int nsb = part == PM_ACT_A ? 0 : (sp->batch + PER_BS - 1) / PER_BS;
-    const int blocks = part == PM_ACT_B ? nsb + g.nb() : nsb + g.blocks();
+    int blocks = part == PM_ACT_B ? nsb + g.nb() : nsb + g.blocks();
+    if (part != PM_ACT_B && sp->featB) blocks += (feat_ntiles(sp->n) + kFeatTilesAct - 1) / kFeatTilesAct;
     hipLaunchKernelGGL(k_act_sp, dim3(blocks), dim3(kActBlock), 0, st, *sp, part);
     PM_LAUNCHED("k_act_sp");
     return PM_OK;
@@ -1149,7 +1182,8 @@ ActGrid learn_act_grid(const pm_selfplay* sp) {
 
 int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st, int mode = PM_UPD_FIRST | PM_UPD_LAST) {
     const ActGrid g = learn_act_grid(sp);
-    const unsigned blocks = 1u + (with_act ? (unsigned)g.blocks() : 0u);
+    unsigned blocks = 1u + (with_act ? (unsigned)g.blocks() : 0u);
+    if (with_act && sp->featB) blocks += (unsigned)((feat_ntiles(sp->n) + kFeatTilesLearn - 1) / kFeatTilesLearn);
     hipLaunchKernelGGL(k_learn, dim3(blocks), dim3(kLearn), 0, st, *sp, g.chunk0, g.chunk1, mode);
     PM_LAUNCHED("k_learn");
     return PM_OK;

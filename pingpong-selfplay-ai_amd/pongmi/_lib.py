@@ -34,7 +34,7 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class EnvParams(ctypes.Structure):
@@ -66,7 +66,8 @@ class SelfPlay(ctypes.Structure):
          ("fuse_apply", c_i32), ("_pad0", c_i32), ("cap", c_i64)] + \
         [(n, c_double) for n in ("gamma", "alpha", "lr", "beta1", "beta2", "adam_eps", "min_epsilon", "epsilon_decay",
                                  "pool_ratio", "beta_start")] + \
-        [("beta_frames", c_i64), ("target_update_interval", c_i64), ("seed_env", c_u64), ("seed_net", c_u64)]
+        [("beta_frames", c_i64), ("target_update_interval", c_i64), ("seed_env", c_u64), ("seed_net", c_u64),
+         ("featB", c_void_p)]
 
 
 class DrqnStats(ctypes.Structure):

@@ -52,7 +52,7 @@ class SelfPlayLearner:
                  memory_size=1_000_000, gamma=0.99, lr=2.5e-4, epsilon=0.02, min_epsilon=0.02, epsilon_decay=0.995,
                  target_update_interval=1000, pool_ratio=0.33, alpha=0.6, beta_start=0.4, beta_frames=100000,
                  episode=0, seed=0, rank=0, world=1, allreduce=None, device=None, modelA_noisy=True,
-                 fuse_apply=True, overlap=True, updates_per_step=1):
+                 fuse_apply=True, overlap=True, updates_per_step=1, features_ahead=True):
         self.lib = _lib.load()
         self.updates_per_step = int(updates_per_step)
         if self.updates_per_step < 1:
@@ -105,6 +105,9 @@ class SelfPlayLearner:
         self.obsB = torch.zeros((n, 7), **f32)
         self.aA = torch.zeros(n, dtype=torch.int8, device=dev)
         self.aB = torch.zeros(n, dtype=torch.int8, device=dev)
+        # modelB's hidden features of the next step's observations, computed with the opponents' act
+        # (features are frozen: only the heads train), so the fused act + env kernel evaluates heads only
+        self.featB = torch.zeros(((n + 31) // 32) * 2048, **f32) if features_ahead else None
         # ---- control block
         c = _lib.Ctrl()
         c.epsilon = float(epsilon)
@@ -120,6 +123,7 @@ class SelfPlayLearner:
                      "per_work", "idx", "isw", "grad", "partials", "obsA", "obsB", "aA", "aB", "hfeat", "learn_heads",
                      "ctrl", "opp_list", "opp_cnt"):
             setattr(sp, name, ptr(getattr(self, name)))
+        sp.featB = ptr(self.featB)
         sp.n, sp.n_pool, sp.batch, sp.world, sp.cap = n, self.n_pool, self.batch, self.world, self.cap
         sp.fuse_apply = int(bool(fuse_apply) and self.world == 1)
         p_pool = pool_ratio if self.n_pool else 0.0
@@ -138,8 +142,9 @@ class SelfPlayLearner:
 
     # ------------------------------------------------------------------ stepping
     # `_aA_ready`: sp.aA holds the opponents' actions for the current observations (computed by a
-    # side-A act, or by the extra blocks of the previous step's learner launch). Anything that
-    # changes the observations, opponent ids or opponent weights clears it.
+    # side-A act, or by the extra blocks of the previous step's learner launch), and sp.featB modelB's
+    # features of them (computed by the same launches). Anything that changes the observations,
+    # opponent ids, opponent weights or modelB's feature layers clears it.
     def rollout(self):
         self._aA_ready = False
         check(self.lib.pm_selfplay_rollout(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_rollout")

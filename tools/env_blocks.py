@@ -40,7 +40,7 @@ def main():
     buf = (ctypes.c_uint64 * (8 * 1024))()
     blk = (ctypes.c_uint64 * (8 * 4096))()
     nsb = (256 + 63) // 64  # sampler blocks of the fused kernel (k_actenv, PER_BS = 64)
-    acc, samp = [], []
+    acc, samp, staged = [], [], []
     for _ in range(20):
         if L.overlap:  # the production step's launches, read right after the fused act + env kernel
             L.actenv()
@@ -48,8 +48,11 @@ def main():
             L.step()
         torch.cuda.synchronize()
         lib.pm_diag_read_env(buf)
-        a = np.array(buf[:], dtype=np.int64).reshape(8, 1024)[:7, :nb]
+        full = np.array(buf[:], dtype=np.int64).reshape(8, 1024)
+        a = full[:7, :nb]
         acc.append(a)
+        if L.overlap:
+            staged.append((full[7, :nb] - a[0]) * 0.01)
         if L.overlap:
             lib.pm_diag_read_blk(blk)
             b = np.array(blk[:], dtype=np.int64).reshape(8, 4096)[:, :nsb]
@@ -68,6 +71,10 @@ def main():
         v = np.array(deltas[k])
         label = "begin offset" if k == 0 else name
         print(f"  {label:44s} p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
+    if staged:
+        v = np.concatenate(staged)
+        print(f"  (fused) begin -> loads landed + weights staged  p50 {np.percentile(v, 50):6.2f}  p90 "
+              f"{np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
     if samp:
         s = np.stack(samp)  # [run][slot][block]
         q = lambda v: " ".join(f"{x:6.2f}" for x in np.percentile(v, [0, 50, 90, 100]))  # noqa: E731

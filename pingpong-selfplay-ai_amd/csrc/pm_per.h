@@ -259,9 +259,14 @@ __device__ __forceinline__ int per_group_find(const double (&v)[NV], double x, d
 // pr.pval (the push kernel may be writing them). out(j, idx, w) is called once per sample. For
 // capacities <= 1M the chunk sums are loaded before `active` is tested (the caller's control-block
 // read and these loads share one round trip); !active returns with nothing written.
-template <class UFn, class OutFn>
+struct NoHook {
+    __device__ void operator()() const {}
+};
+// l2done(): called by every thread once the level-2 search is done (before the level-1 loads), where
+// a caller issues work whose loads must not delay the chunk-sum round trip.
+template <class UFn, class OutFn, class Hook = NoHook>
 __device__ inline void per_sample_block(bool active, int64_t size, const PerTree& tr, const PushRange& pr, double beta,
-                                        int j0, int bs, PerSampleSmem& sm, UFn ufn, OutFn out) {
+                                        int j0, int bs, PerSampleSmem& sm, UFn ufn, OutFn out, Hook l2done = Hook()) {
     const int t = threadIdx.x, q = t & 3;
     const int j = j0 + (t >> 2);
     const bool one_round = tr.nchunk <= PER_ROUND;  // kernel-argument uniform
@@ -324,6 +329,7 @@ __device__ inline void per_sample_block(bool active, int64_t size, const PerTree
     }
     if (blk < 0) { blk = lastnz; before = lastbef; }
     PM_BLK(4);
+    l2done();
     // level 1: the chunk's 16 sub sums, 4 per lane of the sample's group
     double sv[4];
     const int64_t s0 = blk * PER_FAN + 4 * q;

@@ -76,8 +76,9 @@ __device__ __forceinline__ PushRange push_of(const pm_selfplay& sp, int64_t pos,
 // push has not landed yet (update 0, drawn beside k_env: the tree accounts for it and its leaves read
 // as the pushed value); otherwise (updates 1..U-1) the replay is as k_env left it. The fill is the
 // post-push one either way: pos/size advance only when the step commits.
+template <class Hook = NoHook>
 __device__ __forceinline__ void sample_block(const pm_selfplay& sp, int b, bool pending, PerSampleSmem& sm,
-                                             int64_t* sidx = nullptr) {
+                                             int64_t* sidx = nullptr, Hook l2done = Hook()) {
     const pm_ctrl* c = sp.ctrl;
     const int64_t s = c->size + sp.n;
     const int64_t size = s < sp.cap ? s : sp.cap;
@@ -94,7 +95,8 @@ __device__ __forceinline__ void sample_block(const pm_selfplay& sp, int b, bool 
             sp.idx[j] = idx;
             sp.isw[j] = w;
             if (sidx) sidx[j - b * PER_BS] = idx;
-        });
+        },
+        l2done);
 }
 
 // Both players act (train_iterative.py:240-241) on the matrix cores: ActGrid blocks, modelB tiles
@@ -222,9 +224,13 @@ struct SampleFwdSmem {
     int64_t sidx[PER_BS];
 };
 __device__ __forceinline__ void sample_fwd_block(const pm_selfplay& sp, int b, SampleFwdSmem& sm) {
-    stage_frags_lds(sp.w_B, sm.lw, b * 5);
-    copy_lds_f32x4<2 * 264>(sp.learn_heads, sm.hf);
-    sample_block(sp, b, true, sm.per, sm.sidx);
+    // the forward's weights are staged once the top level of the descent is done: LDS DMA in flight
+    // makes hipcc wait vmcnt(0) at the next use of a plain load, which would put the 20 KB staging in
+    // front of the chunk-sum round trip
+    sample_block(sp, b, true, sm.per, sm.sidx, [&] {
+        stage_frags_lds(sp.w_B, sm.lw, b * 5);
+        copy_lds_f32x4<2 * 264>(sp.learn_heads, sm.hf);
+    });
     if (!learner_active(sp)) return;  // block-uniform (sample_block returned before its first barrier)
     __syncthreads();  // sidx, staged weights
     PM_BLK(1);

@@ -10,17 +10,20 @@ push + proportional sample, double-DQN update with target net, Adam), weak-scale
 A step = one vector step: every arena on every rank advances one env step and every rank runs one
 PER update of batch 256. value = total env-steps (all ranks) / max-over-ranks wall time of K steps.
 Rank 0 prints one JSON line. Also reported:
-  roofline      the production step's first kernel, k_actenv (pm_selfplay_actenv): modelB's QNet
-                forward for every arena on the matrix cores fused with the env tick, replay push and
-                bookkeeping of the same arenas, plus the PER sample + batch-forward blocks (the
-                opponents' act rides in the learner's launch), timed with HIP events on the stream it
-                runs on around every 20th step of the timed region (the others run uninstrumented):
-                FP32 FLOP/s vs the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per
+  roofline      the step's dominant launch, k_learn + its extra blocks (pm_selfplay_learn_act): the
+                single-workgroup double-DQN update (+ Adam + sum-tree refresh) and, on the other CUs,
+                the next vector step's update-independent QNet work on the matrix cores: the
+                opponents' act (a full forward per arena) and modelB's frozen feature layers (the
+                forward up to the heads). Timed with HIP events on the stream it runs on around every
+                20th step of the timed region (the others run uninstrumented): FP32 FLOP/s of that
+                QNet work vs the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per
                 launch from the committed counter profile (profiles/r2_pmc.json, same workload), null
                 without it
-  env_roofline  the same k_actenv launch seen as HBM work: 282 algorithmic B / env-step vs 8 TB/s
-  learn_us      the second launch: k_learn (single-workgroup double-DQN update + Adam + sum-tree
-                refresh) with the next step's opponent act on the other CUs; latency-bound
+  env_roofline  the first launch, k_actenv (pm_selfplay_actenv): modelB's heads on the features
+                computed ahead, the env tick, replay push and bookkeeping, plus the PER sample +
+                batch-forward blocks, as HBM work: 282 B of env traffic + 256 B of features read per
+                arena vs 8 TB/s
+  learn_us / actenv_us  the two launches' event-timed durations
   act_full_roofline  k_act_sp with both players' act (+ the PER sample blocks) in one launch
                 (PM_ACT_ALL), back to back after the timed region (N=1 only)
   env_step_roofline  K1 (pm_env_step, autoreset of done arenas) alone at the same n: 203 B / env-step
@@ -44,7 +47,9 @@ ENV_KW = dict(paddle_width=0.2, paddle_speed=0.03, max_score=3, enable_spin=True
               restitution=1, friction=0.6, ball_mass=1.0, world_ball_radius=0.03, ball_speed_range=[0.03, 0.05],
               spin_range=[-5, 5], ball_angle_intervals=[[-60, -30], [30, 60]], speed_scale_every=1,
               speed_increment=0.1)  # config.yaml env (render keys dropped)
-FLOP_PER_ARENA = 2 * (7 * 64 + 64 * 64 + 64 * 4)  # one QNet forward (MACs x 2): side B, the production act kernel
+FLOP_PER_ARENA = 2 * (7 * 64 + 64 * 64 + 64 * 4)  # one QNet forward (MACs x 2)
+FEAT_FLOP_PER_ARENA = 2 * (7 * 64 + 64 * 64)  # modelB's feature layers (computed ahead in the learner launch)
+FEAT_BYTES = 64 * 4  # features per arena, written by the learner launch and read by k_actenv
 ENV_BYTES = 203  # K1 algorithmic bytes per env-step
 # k_env (self-play tick): state 7x8 + 3x4 read and written (136), actions 2, opp 4 + ep_reward 4 read and
 # written (16), replay row 64 + priority 4 + PER leaf 4 written, next observations 2x28 written
@@ -415,8 +420,11 @@ def main():
     if rank == 0:
         total = args.arenas * world * args.steps
         value = total / dt
-        achieved = args.arenas * FLOP_PER_ARENA / ae_s / 1e12
-        env_gbs = args.arenas * SP_ENV_BYTES / ae_s / 1e9
+        ahead = L.featB is not None
+        learn_flop = FLOP_PER_ARENA + (FEAT_FLOP_PER_ARENA if ahead else 0)
+        achieved = args.arenas * learn_flop / learn_s / 1e12
+        env_bytes = SP_ENV_BYTES + (FEAT_BYTES if ahead else 0)
+        env_gbs = args.arenas * env_bytes / ae_s / 1e9
         ae_grid = (args.batch + 63) // 64 + (args.arenas + 255) // 256
         out = {
             "metric": "env-steps/sec (whole node) at 65536 arenas, 1/2/4/8 GPUs; CPU-ref baseline",
@@ -430,19 +438,22 @@ def main():
                        "pool": args.pool, "batch": args.batch, "updates_per_vector_step": 1,
                        "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
                        "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same},
-            "roofline": {"bound": "mfma", "kernel": "k_actenv (modelB's act + env tick + replay push + PER sample "
-                                                    "and batch-forward blocks)",
+            "roofline": {"bound": "mfma",
+                         "kernel": "k_learn launch: the double-DQN update (one workgroup) + the next step's "
+                                   "opponents' act and modelB's feature layers on the other CUs",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": pmc_traffic(f"k_actenv@{ae_grid * 256}"),
-                         "avg_us": round(ae_s * 1e6, 2), "flop_per_arena": FLOP_PER_ARENA, "n": args.arenas},
-            "env_roofline": {"bound": "hbm", "kernel": "k_actenv (the same launch as HBM work)",
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": pmc_traffic("k_learn"),
+                         "avg_us": round(learn_s * 1e6, 2), "flop_per_arena": learn_flop, "n": args.arenas},
+            "env_roofline": {"bound": "hbm",
+                             "kernel": "k_actenv (modelB's heads + env tick + replay push + PER sample / batch "
+                                       "forward)" if ahead else "k_actenv (modelB's act + env tick + replay push + "
+                                                                "PER sample / batch forward)",
                              "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS,
                              "unit": "GB/s", "frac": round(env_gbs / PEAK_HBM_GBS, 4),
                              "traffic": pmc_traffic(f"k_actenv@{ae_grid * 256}"),
-                             "avg_us": round(ae_s * 1e6, 2), "bytes_per_env_step": SP_ENV_BYTES},
-            "learn_us": round(learn_s * 1e6, 2),
+                             "avg_us": round(ae_s * 1e6, 2), "bytes_per_env_step": env_bytes},
+            "learn_us": round(learn_s * 1e6, 2), "actenv_us": round(ae_s * 1e6, 2),
             "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
                         "last_loss": c["last_loss"]},
         }

@@ -14,16 +14,18 @@ Rank 0 prints one JSON line. Also reported:
                 single-workgroup double-DQN update (+ Adam + sum-tree refresh) and, on the other CUs,
                 the next vector step's update-independent QNet work on the matrix cores: the
                 opponents' act (a full forward per arena) and modelB's frozen feature layers (the
-                forward up to the heads). Timed with HIP events on the stream it runs on around every
-                20th step of the timed region (the others run uninstrumented): FP32 FLOP/s of that
-                QNet work vs the 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per
+                forward up to the heads). Timed by the launch's own dispatch (pm_timer_arm:
+                hipExtLaunchKernel begin/end events, no marker packets in the stream, the same
+                interval rocprofv3 --kernel-trace reports) on every 20th production step of an
+                instrumented run after the timed region: FP32 FLOP/s of that QNet work vs the
+                157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per
                 launch from the committed counter profile (profiles/r2_pmc.json, same workload), null
                 without it
   env_roofline  the first launch, k_actenv (pm_selfplay_actenv): modelB's heads on the features
                 computed ahead, the env tick, replay push and bookkeeping, plus the PER sample +
                 batch-forward blocks, as HBM work: 282 B of env traffic + 256 B of features read per
                 arena vs 8 TB/s
-  learn_us / actenv_us  the two launches' event-timed durations
+  learn_us / actenv_us  the two launches' own durations (pm_timer_*)
   act_full_roofline  k_act_sp with both players' act (+ the PER sample blocks) in one launch
                 (PM_ACT_ALL), back to back after the timed region (N=1 only)
   env_step_roofline  K1 (pm_env_step, autoreset of done arenas) alone at the same n: 203 B / env-step
@@ -55,7 +57,37 @@ ENV_BYTES = 203  # K1 algorithmic bytes per env-step
 # written (16), replay row 64 + priority 4 + PER leaf 4 written, next observations 2x28 written
 SP_ENV_BYTES = 136 + 2 + 16 + 72 + 56
 PEAK_FP32_TFLOPS = 157.3
-INSTR = 20  # one instrumented (event-bracketed) step per INSTR timed steps (events cost GPU time on ROCm)
+INSTR = 20  # after the timed region: one instrumented (timer-armed) step per INSTR production steps
+
+
+def timed_region(one_step, steps, dist, n_events, after=None):
+    """Time exactly `steps` production steps (barrier + synchronize on both sides, max over ranks),
+    then run steps // INSTR (at least 5) instrumented steps, each after INSTR - 1 production steps,
+    OUTSIDE the timed region (`after()` runs after each, e.g. to read the launch timers): it never
+    counts towards `value`. Returns (seconds, [event tuples])."""
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(n_events)) for _ in range(max(5, steps // INSTR))]
+    for ev in evs:
+        for _ in range(INSTR - 1):
+            one_step()
+        one_step(ev)
+        if after is not None:
+            after()
+    torch.cuda.synchronize()
+    return dt, evs
 PEAK_HBM_GBS = 8000.0
 
 
@@ -228,6 +260,7 @@ def run_rnn(args, dist, rank, world, allreduce):
         if ev is None:
             L.step()
             return
+        _lib.timer_arm(_lib.PM_TIMER_RNN_ACT)  # the step's first k_rnn_act: modelB's side (overlap) or both
         if overlap:  # the production step's two calls: modelB's fold + act, then env + update with the
             ev[0].record()  # next step's opponent act beside it (the production path's aA is always ready)
             L.act_part(_lib.PM_ACT_B)
@@ -254,26 +287,13 @@ def run_rnn(args, dist, rank, world, allreduce):
         one_step()
     torch.cuda.synchronize()
     c0 = L.counters()
-    inst = set(range(0, args.steps, INSTR))
-    evs = {k: tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for k in inst}
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        one_step(evs.get(k))
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    act_t = []
+    dt, evs = timed_region(one_step, args.steps, dist, 4, lambda: act_t.append(_lib.timer_read(_lib.PM_TIMER_RNN_ACT)))
+    c1 = L.counters()
     same = replicas_identical(dist, L.learner.params)
-    act_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
-    env_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)  # overlap: env + update
-    upd_s = sum(e[2].elapsed_time(e[3]) for e in evs.values()) * 1e-3 / len(evs)
+    act_s = sum(act_t) / len(act_t)  # k_rnn_act's own dispatch (pm_timer_*), as rocprofv3 times it
+    env_s = sum(e[1].elapsed_time(e[2]) for e in evs) * 1e-3 / len(evs)  # overlap: env + update
+    upd_s = sum(e[2].elapsed_time(e[3]) for e in evs) * 1e-3 / len(evs)
     c = L.counters()
     if rank == 0:
         value = n * world * args.steps / dt
@@ -291,12 +311,14 @@ def run_rnn(args, dist, rank, world, allreduce):
                                    "clip + Adam every vector step)",
                        "arenas_per_gpu": n, "global_arenas": n * world, "pool": pool_n, "batch": 64, "trace_length": 8,
                        "memory_size": L.cap, "ring_depth": L.depth,
-                       "updates_in_timed_region": c["train_steps"] - c0["train_steps"],
+                       "updates_in_timed_region": c1["train_steps"] - c0["train_steps"],
                        "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
                        "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same},
             "roofline": {"bound": "mfma",
-                         "kernel": "k_rnn_act side B (+ k_rnn_fold): the overlapped step's act" if overlap
-                                   else "k_rnn_act (+ k_rnn_fold)",
+                         "kernel": "k_rnn_act side B: the overlapped step's act for modelB" if overlap
+                                   else "k_rnn_act (both players)",
+                         "timing": "the launch's own begin/end (hipExtLaunchKernel events, pm_timer_arm) "
+                                   "on instrumented production steps after the timed region",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
@@ -374,47 +396,27 @@ def main():
                         overlap=not args.no_overlap)
 
     def one_step(ev=None):
-        if ev is None:  # the production path: the overlapped vector step (L.step)
-            L.step()
-            return
-        # instrumented step: the production step's launches (pm_selfplay_step_overlap) bracketed one
-        # by one: k_actenv (act B + env + PER sample / batch forward), then the learner launch that
-        # also acts for the next step's opponents
-        if not L._aA_ready:
-            L.act(_lib.PM_ACT_A)
-        ev[0].record()
-        L.actenv()
-        ev[1].record()
-        L.learn(act_next=True)
-        ev[2].record()
-        if dist is not None:
-            allreduce(L.grad)
-        L.apply()
+        # the production path: the overlapped vector step (L.step); an instrumented step is the same
+        # call with both of its launches armed (pm_timer_arm: each dispatch records its own begin/end,
+        # no marker packets join the stream)
+        if ev is not None:
+            _lib.timer_arm(_lib.PM_TIMER_ACTENV)
+            _lib.timer_arm(_lib.PM_TIMER_LEARN)
+        L.step()
 
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
-    # every INSTR-th step of the timed region carries HIP events around its two launches (an event
-    # marker costs GPU time on ROCm; bracketing every step would slow the loop ~15 %)
-    inst = set(range(0, args.steps, INSTR))
-    evs = {k: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for k in inst}
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        one_step(evs.get(k))
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    ae_t, learn_t = [], []
+
+    def read_timers():
+        ae_t.append(_lib.timer_read(_lib.PM_TIMER_ACTENV))
+        learn_t.append(_lib.timer_read(_lib.PM_TIMER_LEARN))
+
+    dt, _ = timed_region(one_step, args.steps, dist, 0, read_timers)
     same = replicas_identical(dist, L.paramsB)
-    ae_s = sum(e[0].elapsed_time(e[1]) for e in evs.values()) * 1e-3 / len(evs)
-    learn_s = sum(e[1].elapsed_time(e[2]) for e in evs.values()) * 1e-3 / len(evs)
+    ae_s = sum(ae_t) / len(ae_t)  # the launches' own durations, as rocprofv3 --kernel-trace times them
+    learn_s = sum(learn_t) / len(learn_t)
     c = L.counters()
 
     if rank == 0:

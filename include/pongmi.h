@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 11
+#define PM_ABI_VERSION 12
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -533,6 +533,20 @@ int pm_rnn_selfplay_step_sharded(const pm_rnn_selfplay* sp, const pm_drqn* d, pm
 /* pm_rnn_selfplay_step_overlap (ABI 10) with every update's gradient all-reduced in stream order. */
 int pm_rnn_selfplay_step_sharded_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, pm_comm* comm, int32_t updates,
                                          void* side_stream, void* stream);
+
+/* ---------------------------------------------------------------- launch timing (benchmarks, diagnostics)
+ * pm_timer_arm(kernel) makes the NEXT launch of that kernel, on the calling process's current
+ * device, carry begin/end events in its own dispatch (hipExtLaunchKernel): no marker packet enters
+ * the stream, so the kernel and its neighbours run exactly as unarmed (a hipEventRecord marker
+ * between two launches costs several us of GPU time on ROCm). pm_timer_read waits for that launch
+ * and returns its duration in ms (PM_E_ARG if nothing was timed since the last read). One armed
+ * launch per kernel at a time; never arm while capturing a hipGraph. */
+#define PM_TIMER_ACTENV 0  /* k_actenv: modelB's act (heads) + env tick + replay push + PER sample */
+#define PM_TIMER_LEARN 1   /* k_learn: the double-DQN update + side-A act + modelB's feature layers */
+#define PM_TIMER_RNN_ACT 2 /* k_rnn_act */
+#define PM_TIMER_N 3
+int pm_timer_arm(int32_t kernel);
+int pm_timer_read(int32_t kernel, float* ms);
 
 /* ---------------------------------------------------------------- misc */
 const char* pm_last_error(void);

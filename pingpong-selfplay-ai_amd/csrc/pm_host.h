@@ -1,5 +1,6 @@
 // Host-side helpers shared by the libpongmi translation units.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,6 +31,19 @@ int pm_rnn_act_part(const float* w_opp, const int32_t* opp_id, int32_t n_opp, co
                     const float* hA_in = nullptr, const float* cA_in = nullptr);
 
 static inline unsigned pm_blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+// Launch timing (pm_timer_arm / pm_timer_read, pm_api.cpp): an armed kernel's next launch goes
+// through hipExtLaunchKernel with the timer's events; every other launch is a plain one.
+bool pm_timer_take(int kernel, hipEvent_t* start, hipEvent_t* stop);
+
+template <typename F, typename... Args>
+inline void pm_launch(int timer, F kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
+    hipEvent_t t0, t1;
+    if (pm_timer_take(timer, &t0, &t1))
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, st, t0, t1, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+}
 
 // ---------------------------------------------------------------- diagnostic stamps (PM_DIAG builds only)
 // libpongmi_diag.so is built with -DPM_DIAG: thread 0 of block 0 records s_memrealtime (100 MHz)

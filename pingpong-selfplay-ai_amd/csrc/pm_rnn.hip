@@ -366,7 +366,7 @@ int pm_rnn_act_part(const float* w_opp, const int32_t* opp_id, int32_t n_opp, co
     const int b0 = part == PM_ACT_A ? nb : 0, b1 = part == PM_ACT_B ? nb : nb + na;
     int grid = b1 - b0;
     if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
-    hipLaunchKernelGGL(k_rnn_act, dim3(grid), dim3(kRnnBlock), 0, pm_stream(stream), g, a, b0, b1);
+    pm_launch(PM_TIMER_RNN_ACT, k_rnn_act, dim3(grid), dim3(kRnnBlock), pm_stream(stream), g, a, b0, b1);
     PM_LAUNCHED("k_rnn_act");
     return PM_OK;
 }

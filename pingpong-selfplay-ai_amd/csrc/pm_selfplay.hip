@@ -668,16 +668,16 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     if (blockIdx.x > 0) {
-        // the learner's load phase is latency-bound under these blocks' staging burst; they have slack
-        // (the learner is the longer of the two), so they start after its loads are in flight
-        __builtin_amdgcn_s_sleep(127);
         const ActGrid g{sp.n, sp.n_pool + 1, chunkA, chunkP, 0};
         const int fb = (int)blockIdx.x - 1 - g.blocks();
-        if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB)
+        if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB), started at once
             const int t0 = fb * kFeatTilesLearn;
             feat_tiles(shm.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + kFeatTilesLearn, feat_ntiles(sp.n)), sp.featB);
             return;
         }
+        // the learner's load phase is latency-bound under these blocks' staging burst; they have slack
+        // (the learner is the longer of the two), so they start after its loads are in flight
+        __builtin_amdgcn_s_sleep(127);
         const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
         act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,
                   (int)blockIdx.x - 1, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
@@ -1190,7 +1190,7 @@ int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st, int mode 
     const ActGrid g = learn_act_grid(sp);
     unsigned blocks = 1u + (with_act ? (unsigned)g.blocks() : 0u);
     if (with_act && sp->featB) blocks += (unsigned)((feat_ntiles(sp->n) + kFeatTilesLearn - 1) / kFeatTilesLearn);
-    hipLaunchKernelGGL(k_learn, dim3(blocks), dim3(kLearn), 0, st, *sp, g.chunk0, g.chunk1, mode);
+    pm_launch(PM_TIMER_LEARN, k_learn, dim3(blocks), dim3(kLearn), st, *sp, g.chunk0, g.chunk1, mode);
     PM_LAUNCHED("k_learn");
     return PM_OK;
 }
@@ -1221,7 +1221,7 @@ extern "C" int pm_selfplay_actenv(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
     const unsigned nsb = (unsigned)((sp->batch + PER_BS - 1) / PER_BS);
-    hipLaunchKernelGGL(k_actenv, dim3(nsb + pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, pm_stream(stream), *sp);
+    pm_launch(PM_TIMER_ACTENV, k_actenv, dim3(nsb + pm_blocks(sp->n, kBlock)), dim3(kBlock), pm_stream(stream), *sp);
     PM_LAUNCHED("k_actenv");
     return PM_OK;
 }

@@ -34,7 +34,8 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 11
+ABI_VERSION = 12
+PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT = 0, 1, 2
 
 
 class EnvParams(ctypes.Structure):
@@ -161,6 +162,8 @@ _SIGS = {
     "pm_selfplay_step_sharded": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_rnn_selfplay_step_sharded": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_rnn_selfplay_step_sharded_overlap": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p, c_void_p]),
+    "pm_timer_arm": (c_i32, [c_i32]),
+    "pm_timer_read": (c_i32, [c_i32, ctypes.POINTER(c_float)]),
     "pm_last_error": (ctypes.c_char_p, []),
     "pm_abi_version": (c_i32, []),
     "pm_sizeof": (c_i32, [c_i32]),
@@ -196,6 +199,18 @@ def load():
                               f"vs ctypes {ctypes.sizeof(cls)}")
     _lib = L
     return L
+
+
+def timer_arm(kernel):
+    """The next launch of `kernel` (PM_TIMER_*) records its own begin/end (pm_timer_arm)."""
+    check(load().pm_timer_arm(int(kernel)), "pm_timer_arm")
+
+
+def timer_read(kernel):
+    """Duration in seconds of the launch timed since timer_arm(kernel) (waits for it)."""
+    ms = c_float()
+    check(load().pm_timer_read(int(kernel), ctypes.byref(ms)), "pm_timer_read")
+    return ms.value * 1e-3
 
 
 def check(rc, what=""):

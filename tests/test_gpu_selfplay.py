@@ -258,6 +258,31 @@ def test_deterministic_rerun(golden):
         assert torch.equal(getattr(A, name), getattr(B, name)), name
 
 
+def test_launch_timer_leaves_results_unchanged(golden):
+    """pm_timer_arm: a timed launch (hipExtLaunchKernel with begin/end events) computes exactly what
+    the plain one does, reports a positive duration, and a read without a timed launch is an error."""
+    from pongmi import _lib
+    A = _learner(golden, n=4096, batch=256, cap=16384, seed=11)
+    B = _learner(golden, n=4096, batch=256, cap=16384, seed=11)
+    durations = []
+    for k in range(20):
+        A.step()
+        if k % 3 == 0:
+            _lib.timer_arm(_lib.PM_TIMER_ACTENV)
+            _lib.timer_arm(_lib.PM_TIMER_LEARN)
+        B.step()
+        if k % 3 == 0:
+            durations += [_lib.timer_read(_lib.PM_TIMER_ACTENV), _lib.timer_read(_lib.PM_TIMER_LEARN)]
+    torch.cuda.synchronize()
+    for name in ("paramsB", "prios", "trans", "f64", "opp", "per_work", "idx"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    assert all(0 < d < 0.1 for d in durations), durations
+    with pytest.raises(_lib.PongmiError):
+        _lib.timer_read(_lib.PM_TIMER_LEARN)
+    with pytest.raises(_lib.PongmiError):
+        _lib.timer_arm(3)  # PM_TIMER_N
+
+
 @pytest.mark.parametrize("n,cap", [(1000, 2500), (2048, 8192), (300, 1000), (4096, 4160)])
 def test_sum_tree_incremental_equals_rebuild(golden, n, cap):
     """The PER sum tree is maintained incrementally inside k_learn (scattered sub-blocks + the next

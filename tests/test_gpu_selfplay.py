@@ -337,6 +337,30 @@ def test_overlapped_step_is_bitwise_identical(golden):
     assert A.counters() == B.counters()
 
 
+def test_features_ahead_is_bitwise_identical(golden):
+    """modelB's feature layers computed a launch ahead (the learner launch's feature blocks -> featB,
+    k_actenv evaluates the heads only) equal k_actenv's full forward bit for bit, also across a
+    reset_B (new feature weights: the precomputed features are invalidated and recomputed) and a
+    ragged arena count (the last 32-row feature tile partial)."""
+    for n in (4096, 3000):
+        A = _learner(golden, n=n, batch=256, cap=16384, seed=23, n_pool=3)
+        B = _learner(golden, n=n, batch=256, cap=16384, seed=23, n_pool=3, features_ahead=False)
+        assert A.featB is not None and B.featB is None
+        for k in range(20):
+            if k == 11:
+                sd = _random_qnet_sd(91)
+                A.reset_B(sd, epsilon=0.2)
+                B.reset_B(sd, epsilon=0.2)
+            A.step()
+            B.step()
+        torch.cuda.synchronize()
+        for name in ("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "opp", "w_B",
+                     "learn_heads", "per_work", "idx", "isw", "aA", "aB", "obsA", "obsB", "ep_reward"):
+            assert torch.equal(getattr(A, name), getattr(B, name)), (n, name)
+        assert A.counters() == B.counters()
+        assert A.counters()["train_steps"] > 0
+
+
 def test_sharded_world2_overlap_equals_plain(golden):
     """world = 2 on one device (rank-specific arenas / replay, one summed gradient): the overlapped
     sharded step (act B -> env -> learn with the next side-A act -> all-reduce -> k_adam) equals the

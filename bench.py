@@ -155,10 +155,19 @@ def time_env_step(n, per_graph=50, replays=20):
     e1.synchronize()
     t = e0.elapsed_time(e1) * 1e-3 / (per_graph * replays)
     achieved = n * ENV_BYTES / t / 1e9
+    # the same launch timed from its own dispatch (pm_timer_arm: the interval rocprofv3's kernel trace
+    # reports, without the launch-to-launch gap the graph replay includes), eager launches
+    from pongmi import _lib
+    with torch.cuda.stream(s):
+        for _ in range(per_graph):
+            _lib.timer_arm(_lib.PM_TIMER_ENV_STEP)
+            env.step(aA, aB)
+    td = sum(_lib.timer_read(_lib.PM_TIMER_ENV_STEP) for _ in range(per_graph)) / per_graph
     return {"bound": "hbm", "kernel": "k_env_step", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic("k_env_step"),
             "avg_us": round(t * 1e6, 2), "bytes_per_env_step": ENV_BYTES, "n": n,
-            "timing": f"HIP events over {replays} graph replays x {per_graph} launches, autoreset='done'"}
+            "timing": f"HIP events over {replays} graph replays x {per_graph} launches, autoreset='done'",
+            "dispatch_us": round(td * 1e6, 2), "dispatch_frac": round(n * ENV_BYTES / td / 1e9 / PEAK_HBM_GBS, 4)}
 
 
 def time_act_full(L, launches=50):

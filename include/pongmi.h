@@ -535,16 +535,18 @@ int pm_rnn_selfplay_step_sharded_overlap(const pm_rnn_selfplay* sp, const pm_drq
                                          void* side_stream, void* stream);
 
 /* ---------------------------------------------------------------- launch timing (benchmarks, diagnostics)
- * pm_timer_arm(kernel) makes the NEXT launch of that kernel, on the calling process's current
- * device, carry begin/end events in its own dispatch (hipExtLaunchKernel): no marker packet enters
- * the stream, so the kernel and its neighbours run exactly as unarmed (a hipEventRecord marker
- * between two launches costs several us of GPU time on ROCm). pm_timer_read waits for that launch
- * and returns its duration in ms (PM_E_ARG if nothing was timed since the last read). One armed
- * launch per kernel at a time; never arm while capturing a hipGraph. */
-#define PM_TIMER_ACTENV 0  /* k_actenv: modelB's act (heads) + env tick + replay push + PER sample */
-#define PM_TIMER_LEARN 1   /* k_learn: the double-DQN update + side-A act + modelB's feature layers */
-#define PM_TIMER_RNN_ACT 2 /* k_rnn_act */
-#define PM_TIMER_N 3
+ * pm_timer_arm(kernel) queues one launch of that kernel, on the calling process's current device,
+ * to be timed: the next untimed launch carries begin/end events in its own dispatch
+ * (hipExtLaunchKernel), so no marker packet enters the stream and the kernel and its neighbours run
+ * exactly as unarmed (a hipEventRecord marker between two launches costs several us of GPU time on
+ * ROCm). Up to 64 launches per kernel may be armed or unread at once. pm_timer_read waits for the
+ * oldest timed launch and returns its duration in ms (PM_E_ARG if none is left). Never arm while
+ * capturing a hipGraph. */
+#define PM_TIMER_ACTENV 0   /* k_actenv: modelB's act (heads) + env tick + replay push + PER sample */
+#define PM_TIMER_LEARN 1    /* k_learn: the double-DQN update + side-A act + modelB's feature layers */
+#define PM_TIMER_RNN_ACT 2  /* k_rnn_act */
+#define PM_TIMER_ENV_STEP 3 /* k_env_step (K1, pm_env_step) */
+#define PM_TIMER_N 4
 int pm_timer_arm(int32_t kernel);
 int pm_timer_read(int32_t kernel, float* ms);
 

@@ -19,22 +19,26 @@ int pm_fail(int code, const char* fmt, ...) {
 extern "C" const char* pm_last_error(void) { return g_err; }
 
 // ---------------------------------------------------------------- launch timing
+// Per kernel, a FIFO of kTimerSlots begin/end event pairs: pm_timer_arm queues one more launch to
+// time, the launch takes the next slot, pm_timer_read returns the oldest timed launch's duration.
 namespace {
+constexpr int kTimerSlots = 64;
 struct LaunchTimer {
-    hipEvent_t ev[2] = {nullptr, nullptr};
+    hipEvent_t ev[kTimerSlots][2] = {};
     int device = -1;
-    bool armed = false, pending = false;
+    int armed = 0, pending = 0, head = 0;  // head: the oldest pending slot
 };
 LaunchTimer g_timer[PM_TIMER_N];
 }  // namespace
 
 bool pm_timer_take(int kernel, hipEvent_t* start, hipEvent_t* stop) {
     LaunchTimer& t = g_timer[kernel];
-    if (!t.armed) return false;
-    t.armed = false;
-    t.pending = true;
-    *start = t.ev[0];
-    *stop = t.ev[1];
+    if (t.armed == 0) return false;
+    const int slot = (t.head + t.pending) % kTimerSlots;
+    --t.armed;
+    ++t.pending;
+    *start = t.ev[slot][0];
+    *stop = t.ev[slot][1];
     return true;
 }
 
@@ -45,28 +49,34 @@ extern "C" int pm_timer_arm(int32_t kernel) {
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return pm_fail((int)e, "pm_timer_arm: %s", hipGetErrorString(e));
     if (t.device != dev) {
-        for (hipEvent_t& ev : t.ev) {
-            if (ev) (void)hipEventDestroy(ev);
-            ev = nullptr;
-        }
-        for (hipEvent_t& ev : t.ev)
-            if ((e = hipEventCreate(&ev)) != hipSuccess)
-                return pm_fail((int)e, "pm_timer_arm: hipEventCreate: %s", hipGetErrorString(e));
+        PM_REQUIRE(t.armed == 0 && t.pending == 0, PM_E_ARG, "pm_timer_arm: kernel %d has launches timed on "
+                   "device %d", kernel, t.device);
+        for (auto& pair : t.ev)
+            for (hipEvent_t& ev : pair) {
+                if (ev) (void)hipEventDestroy(ev);
+                ev = nullptr;
+            }
+        for (auto& pair : t.ev)
+            for (hipEvent_t& ev : pair)
+                if ((e = hipEventCreate(&ev)) != hipSuccess)
+                    return pm_fail((int)e, "pm_timer_arm: hipEventCreate: %s", hipGetErrorString(e));
         t.device = dev;
     }
-    t.armed = true;
-    t.pending = false;
+    PM_REQUIRE(t.armed + t.pending < kTimerSlots, PM_E_ARG, "pm_timer_arm: kernel %d has %d launches armed or "
+               "unread (at most %d)", kernel, t.armed + t.pending, kTimerSlots);
+    ++t.armed;
     return 0;
 }
 
 extern "C" int pm_timer_read(int32_t kernel, float* ms) {
     PM_REQUIRE(kernel >= 0 && kernel < PM_TIMER_N && ms, PM_E_ARG, "pm_timer_read: kernel %d", kernel);
     LaunchTimer& t = g_timer[kernel];
-    PM_REQUIRE(t.pending, PM_E_ARG, "pm_timer_read: kernel %d was not launched since pm_timer_arm", kernel);
-    hipError_t e = hipEventSynchronize(t.ev[1]);
-    if (e == hipSuccess) e = hipEventElapsedTime(ms, t.ev[0], t.ev[1]);
+    PM_REQUIRE(t.pending > 0, PM_E_ARG, "pm_timer_read: no timed launch of kernel %d to read", kernel);
+    hipError_t e = hipEventSynchronize(t.ev[t.head][1]);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, t.ev[t.head][0], t.ev[t.head][1]);
     if (e != hipSuccess) return pm_fail((int)e, "pm_timer_read: %s", hipGetErrorString(e));
-    t.pending = false;
+    t.head = (t.head + 1) % kTimerSlots;
+    --t.pending;
     return 0;
 }
 

@@ -3,6 +3,8 @@
 // HBM-bound: per env-step 203 algorithmic bytes (fp64 state 7x8 read + write, int32 scores /
 // bounces 12 read + write, actions 2, obs 56, rewards 8, done 1). Observations leave the kernel
 // through an LDS transpose so every store is a full 16-byte-per-lane coalesced write.
+#include <stdlib.h>
+
 #include "pm_dev.h"
 #include "pm_host.h"
 
@@ -83,7 +85,8 @@ static __device__ unsigned long long pm_k1_diag[8][4096];
 //     splits the hot block.
 // AR (autoreset): 0 none, 1 reset + full term rows (term row = the step's pre-reset observation),
 // 2 reset + term rows written for done arenas only (the other rows are left as they were).
-template <int AR, bool INJ>
+// WT: write-through outputs (pm_dev.h st_out), chosen by the arena count at launch.
+template <int AR, bool INJ, bool WT>
 __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
                                                      const int8_t* __restrict__ aB, float* __restrict__ obsA,
                                                      float* __restrict__ obsB, float* __restrict__ rA,
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
             a.spin = d ? r.spin : a.spin; a.top = d ? r.top : a.top; a.bot = d ? r.bot : a.bot;
             a.sA = d ? 0 : a.sA; a.sB = d ? 0 : a.sB; a.bounces = d ? 0 : a.bounces;
             observe(a, oA, oB);
-            s.serves[i] = ns + d;
+            st_out<WT>(&s.serves[i], ns + d);
         } else if (AR && d) {  // parity mode: the injected serve of done arenas
             if (AR == 2 && tobsA) {
                 store_row7(tobsA + (size_t)i * 7, oA);
@@ -143,9 +146,9 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
             s.serves[i] = ns + 1;
             observe(a, oA, oB);
         }
-        store_arena(s, i, a);
-        rA[i] = ra;
-        rB[i] = rb;
+        store_arena<WT>(s, i, a);
+        st_out<WT>(&rA[i], ra);
+        st_out<WT>(&rB[i], rb);
         done[i] = (uint8_t)d;
         tdone = d;
     }
@@ -154,11 +157,11 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
     for (int k = 0; k < 7; ++k) { lds[0][t][k] = oA[k]; lds[1][t][k] = oB[k]; }
     __syncthreads();
     K1_STAMP(4);
-    copy_rows7(obsA, lds[0], i0, n);
-    copy_rows7(obsB, lds[1], i0, n);
+    copy_rows7<WT>(obsA, lds[0], i0, n);
+    copy_rows7<WT>(obsB, lds[1], i0, n);
     if (full_term) {
-        copy_rows7(tobsA, lds[2], i0, n);
-        copy_rows7(tobsB, lds[3], i0, n);
+        copy_rows7<WT>(tobsA, lds[2], i0, n);
+        copy_rows7<WT>(tobsB, lds[3], i0, n);
     }
     if (DRAW && AR == 2 && tobsA && tdone) {
         store_row7(tobsA + (size_t)i * 7, tA);
@@ -185,6 +188,17 @@ __global__ __launch_bounds__(kBlock) void k_collide(const double* __restrict__ i
     out[(size_t)i * 3 + 0] = vn2;
     out[(size_t)i * 3 + 1] = vt2;
     out[(size_t)i * 3 + 2] = om2;
+}
+
+// Write-through K1 outputs up to kK1WtMax arenas (latency-bound sizes); PONGMI_K1_WT=0/1 forces
+// the choice (experiments).
+constexpr int32_t kK1WtMax = 131072;
+int k1_write_through(int32_t n) {
+    static const int forced = [] {
+        const char* e = getenv("PONGMI_K1_WT");
+        return e && *e ? atoi(e) : -1;
+    }();
+    return forced >= 0 ? (forced != 0) : (n <= kK1WtMax);
 }
 
 bool state_ok(const pm_env_state* s) {
@@ -221,13 +235,17 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
     PM_REQUIRE(autoreset >= 0 && autoreset <= 2, PM_E_ARG, "pm_env_step: autoreset=%d not in {0,1,2}", autoreset);
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
-    using K = decltype(&k_env_step<0, false>);
-    static const K kernels[3][2] = {{k_env_step<0, false>, k_env_step<0, true>},
-                                    {k_env_step<1, false>, k_env_step<1, true>},
-                                    {k_env_step<2, false>, k_env_step<2, true>}};
-    hipLaunchKernelGGL(kernels[autoreset][inject != nullptr], dim3(pm_blocks(n, kBlock)), dim3(kBlock), 0,
-                       pm_stream(stream), *p, *s, aA, aB, obsA, obsB, rA, rB, done, term_obsA, term_obsB, inject,
-                       inject_cap, seed, status, n);
+    using K = decltype(&k_env_step<0, false, false>);
+    static const K kernels[2][3][2] = {
+        {{k_env_step<0, false, false>, k_env_step<0, true, false>},
+         {k_env_step<1, false, false>, k_env_step<1, true, false>},
+         {k_env_step<2, false, false>, k_env_step<2, true, false>}},
+        {{k_env_step<0, false, true>, k_env_step<0, true, true>},
+         {k_env_step<1, false, true>, k_env_step<1, true, true>},
+         {k_env_step<2, false, true>, k_env_step<2, true, true>}}};
+    pm_launch(PM_TIMER_ENV_STEP, kernels[k1_write_through(n)][autoreset][inject != nullptr], dim3(pm_blocks(n, kBlock)),
+              dim3(kBlock), pm_stream(stream), *p, *s, aA, aB, obsA, obsB, rA, rB, done, term_obsA, term_obsB, inject,
+              inject_cap, seed, status, n);
     PM_LAUNCHED("k_env_step");
     return PM_OK;
 }

@@ -111,6 +111,12 @@ union ActSpShared {
 };
 // Feature tiles per feature block: 8 (256-thread blocks, two tiles per wave) / 16 (k_learn's 1024).
 constexpr int kFeatTilesAct = 8, kFeatTilesLearn = 16;
+// The env blocks' replay rows, state and observation rows go out write-through (pm_dev.h st_out):
+// none of it is re-read from this L2 before the kernel boundary. PM_ENV_WT=0 builds plain stores.
+#ifndef PM_ENV_WT
+#define PM_ENV_WT 0
+#endif
+constexpr bool kEnvWTRows = (PM_ENV_WT & 1) != 0, kEnvWTState = (PM_ENV_WT & 2) != 0, kEnvWTObs = (PM_ENV_WT & 4) != 0;
 __host__ __device__ inline int feat_ntiles(int n) { return (n + 31) / 32; }
 
 __global__ __launch_bounds__(kActBlock, 4) void k_act_sp(const pm_selfplay sp, int part) {
@@ -386,11 +392,13 @@ __device__ __forceinline__ void env_block(const pm_selfplay& sp, int blk, EnvSme
         // memory.push((oB, aB, rB, nB, done)) (:243, :56-63)
         int64_t slot = pos + i;  // pos < cap and i < n <= cap: one conditional subtract is the modulo
         if (slot >= sp.cap) slot -= sp.cap;  // (a per-lane 64-bit % is a ~100-instruction expansion)
+        // write-through (pm_dev.h st_out): the ring is re-read only by later samples, and the state and
+        // observation rows only by later launches, so none of it stays dirty in L2 for the boundary
         float4* row = reinterpret_cast<float4*>(sp.trans + slot * PM_TRANS_F);
-        row[0] = make_float4(oB[0], oB[1], oB[2], oB[3]);
-        row[1] = make_float4(oB[4], oB[5], oB[6], rB);
-        row[2] = make_float4(nB[0], nB[1], nB[2], nB[3]);
-        row[3] = make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
+        st_f4<kEnvWTRows>(row + 0, make_float4(oB[0], oB[1], oB[2], oB[3]));
+        st_f4<kEnvWTRows>(row + 1, make_float4(oB[4], oB[5], oB[6], rB));
+        st_f4<kEnvWTRows>(row + 2, make_float4(nB[0], nB[1], nB[2], nB[3]));
+        st_f4<kEnvWTRows>(row + 3, make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8))));
         sp.prios[slot] = maxp;
         leaf[slot] = pval;
         float ernew = er;
@@ -401,7 +409,7 @@ __device__ __forceinline__ void env_block(const pm_selfplay& sp, int blk, EnvSme
             ernew = 0.f;
             observe(a, nA, nB);
         }
-        store_arena(sp.st, i, a);
+        store_arena<kEnvWTState>(sp.st, i, a);
         sp.opp[i] = onew;
         sp.aB[i] = (int8_t)aB;  // the action taken
         sp.ep_reward[i] = ernew;
@@ -418,8 +426,8 @@ __device__ __forceinline__ void env_block(const pm_selfplay& sp, int blk, EnvSme
     }
     write_opp_lists(sp, sm.ol, blk, i, valid, onew);
     PM_ENV_STAMP(5, blk);
-    copy_rows7(sp.obsA, sm.lds[0], i0, sp.n);
-    copy_rows7(sp.obsB, sm.lds[1], i0, sp.n);
+    copy_rows7<kEnvWTObs>(sp.obsA, sm.lds[0], i0, sp.n);
+    copy_rows7<kEnvWTObs>(sp.obsB, sm.lds[1], i0, sp.n);
     PM_ENV_STAMP_DRAIN(6, blk);
 }
 

@@ -35,7 +35,7 @@ PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
 ABI_VERSION = 12
-PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT = 0, 1, 2
+PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_N = 0, 1, 2, 3, 4
 
 
 class EnvParams(ctypes.Structure):
@@ -202,12 +202,12 @@ def load():
 
 
 def timer_arm(kernel):
-    """The next launch of `kernel` (PM_TIMER_*) records its own begin/end (pm_timer_arm)."""
+    """Queue one launch of `kernel` (PM_TIMER_*) to record its own begin/end (pm_timer_arm)."""
     check(load().pm_timer_arm(int(kernel)), "pm_timer_arm")
 
 
 def timer_read(kernel):
-    """Duration in seconds of the launch timed since timer_arm(kernel) (waits for it)."""
+    """Duration in seconds of the oldest unread timed launch of `kernel` (waits for it)."""
     ms = c_float()
     check(load().pm_timer_read(int(kernel), ctypes.byref(ms)), "pm_timer_read")
     return ms.value * 1e-3

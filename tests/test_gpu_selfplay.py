@@ -280,7 +280,7 @@ def test_launch_timer_leaves_results_unchanged(golden):
     with pytest.raises(_lib.PongmiError):
         _lib.timer_read(_lib.PM_TIMER_LEARN)
     with pytest.raises(_lib.PongmiError):
-        _lib.timer_arm(3)  # PM_TIMER_N
+        _lib.timer_arm(_lib.PM_TIMER_N)
 
 
 @pytest.mark.parametrize("n,cap", [(1000, 2500), (2048, 8192), (300, 1000), (4096, 4160)])

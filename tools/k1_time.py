@@ -13,4 +13,5 @@ import bench  # noqa: E402
 for n in [int(a) for a in sys.argv[1:]] or [65536, 262144]:
     for rep in range(2):
         r = bench.time_env_step(n)
-        print(json.dumps({"n": n, "rep": rep, "avg_us": r["avg_us"], "frac": r["frac"]}), flush=True)
+        print(json.dumps({"n": n, "rep": rep, "avg_us": r["avg_us"], "frac": r["frac"], "dispatch_us": r["dispatch_us"],
+                          "dispatch_frac": r["dispatch_frac"]}), flush=True)

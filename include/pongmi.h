@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 12
+#define PM_ABI_VERSION 13
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -375,7 +375,8 @@ typedef struct pm_ctrl {
     int64_t ep_step;         /* episodes finished during the current vector step          */
     int64_t win_A, ep_A, win_P, ep_P; /* wins / episodes of B vs modelA and vs pool (:247-248) */
     double reward_B;         /* sum of rB over finished episodes                          */
-    int32_t status;          /* error bits                                               */
+    int32_t status;          /* bit 0: the push-row hand-off inside k_learn timed out; the learner
+                                computes those rows itself from then on (results unchanged)      */
     int32_t max_bits;        /* pm_selfplay_commit scratch: float bits of max(prios); 0 between steps */
 } pm_ctrl;
 
@@ -399,7 +400,9 @@ typedef struct pm_selfplay {
     int64_t *partials;       /* [ceil(n/256)][8] per-block episode counters of the rollout          */
     float *obsA, *obsB;      /* [n][7] observations of the current step (written by the env kernel) */
     int8_t *aA, *aB;         /* [n] actions of the current step (written by the act kernel)        */
-    float *hfeat;            /* [batch][80] batch forward scratch: features of s, Q values at 64.. */
+    float *hfeat;            /* [2 * batch + 1][80] batch forward scratch: rows [0, batch) features of s,
+                                Q values at 64.. (stable rows); rows [batch, 2 batch) the push rows
+                                k_learn's block 1 hands to the learner; row 2 batch word 0 its flag */
     float *learn_heads;      /* [3][264] next update's modelB heads (fresh noise) and targetB heads in
                                 MFMA fragment order, and that noise (epsilon-buffer layout)        */
     pm_ctrl *ctrl;

@@ -114,7 +114,7 @@ constexpr int kFeatTilesAct = 8, kFeatTilesLearn = 16;
 // The env blocks' replay rows, state and observation rows go out write-through (pm_dev.h st_out):
 // none of it is re-read from this L2 before the kernel boundary. PM_ENV_WT=0 builds plain stores.
 #ifndef PM_ENV_WT
-#define PM_ENV_WT 0
+#define PM_ENV_WT 6
 #endif
 constexpr bool kEnvWTRows = (PM_ENV_WT & 1) != 0, kEnvWTState = (PM_ENV_WT & 2) != 0, kEnvWTObs = (PM_ENV_WT & 4) != 0;
 __host__ __device__ inline int feat_ntiles(int n) { return (n + 31) / 32; }
@@ -172,24 +172,25 @@ __device__ __forceinline__ void batch_row_fwd(const pm_selfplay& sp, const float
 // runs: they are computed beside it (one tile per wave) into hfeat [B][80] (features of s | Q_B(s)
 // 0..2, r at 3, Q_B(s') 4..6, action|done bits at 7, Q_T(s') 8..10 at 64..); k_learn computes the
 // rest. Carrying r and the bits here spares k_learn a load that depends on idx.
-__device__ __forceinline__ void store_hfeat(const pm_selfplay& sp, int j, bool nxt, int lane, const f32x16 (&c2)[2],
+template <bool WT = false>
+__device__ __forceinline__ void store_hfeat(float* hfeat, int j, bool nxt, int lane, const f32x16 (&c2)[2],
                                             const float (&qb)[3], const float (&qt)[3], const float (&rb)[2]) {
-    float* row = sp.hfeat + (size_t)j * 80;
+    float* row = hfeat + (size_t)j * 80;
     const int h = lane >> 5;
     if (!nxt) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) row[32 * t + rho(q) + 4 * h] = relu(c2[t][q]);
+            for (int q = 0; q < 16; ++q) st_out<WT>(&row[32 * t + rho(q) + 4 * h], relu(c2[t][q]));
     }
     if (h == 0) {
         if (!nxt) {
-            row[64] = qb[0]; row[65] = qb[1]; row[66] = qb[2];
-            row[67] = rb[0];  // reward
-            row[71] = rb[1];  // action | done << 8 (float bits)
+            st_out<WT>(&row[64], qb[0]); st_out<WT>(&row[65], qb[1]); st_out<WT>(&row[66], qb[2]);
+            st_out<WT>(&row[67], rb[0]);  // reward
+            st_out<WT>(&row[71], rb[1]);  // action | done << 8 (float bits)
         } else {
-            row[68] = qb[0]; row[69] = qb[1]; row[70] = qb[2];
-            row[72] = qt[0]; row[73] = qt[1]; row[74] = qt[2];
+            st_out<WT>(&row[68], qb[0]); st_out<WT>(&row[69], qb[1]); st_out<WT>(&row[70], qb[2]);
+            st_out<WT>(&row[72], qt[0]); st_out<WT>(&row[73], qt[1]); st_out<WT>(&row[74], qt[2]);
         }
     }
 }
@@ -216,7 +217,7 @@ __device__ __forceinline__ void env_fwd_block(const pm_selfplay& sp, int f, bool
     float qb[3], qt[3];
     float rb[2];
     batch_row_fwd(sp, lw, hf[0], hf[1], id, nxt, lane, c2, qb, qt, rb);
-    if (mine) store_hfeat(sp, j, nxt, lane, c2, qb, qt, rb);
+    if (mine) store_hfeat(sp.hfeat, j, nxt, lane, c2, qb, qt, rb);
 }
 
 // The fused step's sampler blocks: block b draws samples [64 b, 64 b + 64) (per_sample_block) and then
@@ -252,7 +253,7 @@ __device__ __forceinline__ void sample_fwd_block(const pm_selfplay& sp, int b, S
     float qb[3], qt[3];
     float rb[2];
     batch_row_fwd(sp, sm.lw, sm.hf, sm.hf + 264, id, nxt, lane, c2, qb, qt, rb);
-    if (mine) store_hfeat(sp, j, nxt, lane, c2, qb, qt, rb);
+    if (mine) store_hfeat(sp.hfeat, j, nxt, lane, c2, qb, qt, rb);
 }
 
 __device__ __forceinline__ void write_opp_lists(const pm_selfplay& sp, OppListSmem& sm, int blk, int i, bool valid,
@@ -634,12 +635,84 @@ __device__ __forceinline__ void apply_finish(const pm_selfplay& sp, ApplySmem& s
 }
 
 // ------------------------------------------------------------------------------------ learner
+// ---- the push-range rows of an update's batch: the samples whose replay row this step's k_actenv
+// wrote (its sampler blocks cannot read them), s rows then s' rows, one 32-row tile per wave, in
+// plist order (pcnt: per-wave counts of the ballot that built plist; B <= 256: waves 0..3).
+// emit(j, nxt, lane, c2, qb, qt, rb) runs for the lanes that hold a row.
+template <typename Emit>
+__device__ __forceinline__ void push_rows_fwd(const pm_selfplay& sp, const float* lw, const float* hf,
+                                              const int64_t* sidx, const int* plist, const int* pcnt, int wv, int lane,
+                                              Emit emit) {
+    int pre[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) pre[w + 1] = pre[w] + pcnt[w];
+    const int np = pre[4];
+    if (wv * 32 >= 2 * np) return;  // wave-uniform
+    const int rr = min(wv * 32 + (lane & 31), 2 * np - 1);
+    const bool nxt = rr >= np;
+    const int k = nxt ? rr - np : rr;
+    const int w = k >= pre[3] ? 3 : k >= pre[2] ? 2 : k >= pre[1] ? 1 : 0;
+    const int j = plist[w * 64 + k - pre[w]];
+    f32x16 c2[2];
+    float qb[3], qt[3], rb[2];
+    batch_row_fwd(sp, lw, hf, hf + 264, sidx[j], nxt, lane, c2, qb, qt, rb);
+    if (wv * 32 + (lane & 31) < 2 * np) emit(j, nxt, lane, c2, qb, qt, rb);
+}
+
+// The push-row hand-off inside k_learn: block 1 computes the push rows beside the learner's load
+// phase and publishes them in hfeat rows [B, 2B) (hfeat row layout), then the flag word at hfeat row
+// 2B = ctrl.step + 1. Publication follows the cross-CU rules for write-through hand-offs: every
+// payload store and the flag store sc1, every storing wave waits vmcnt(0), a workgroup barrier,
+// then one lane stores the flag; the learner polls the flag with sc1 loads from one lane, joins a
+// barrier, and reads the payload with sc1 loads only. The learner increments ctrl.step only after
+// this point, so the token names this update. Block 1 waits for nothing, so it always completes;
+// the poll is bounded anyway (kPushPollMax, ~20 ms): a flag that never came sets ctrl.status bit 0,
+// which the host reports as an error (pongmi.selfplay.SelfPlayLearner.check_status).
+constexpr int kPushPollMax = 20000;
+constexpr int PM_CTRL_PUSH_TIMEOUT = 1;
+__device__ __forceinline__ bool push_handoff(int mode, bool train) { return (mode & PM_UPD_FIRST) && train; }
+__device__ __forceinline__ int* push_flag(const pm_selfplay& sp) {
+    return reinterpret_cast<int*>(sp.hfeat + (size_t)2 * sp.batch * 80);
+}
+__device__ __forceinline__ int push_token(const pm_ctrl& cs) { return (int)((uint32_t)cs.step + 1u); }
+
+struct PushFwdSmem {
+    float lw[kLwFloats];
+    float hf[pad256(2 * 264)];
+    int64_t sidx[PM_MAX_BATCH];
+    int plist[PM_MAX_BATCH];
+    int pcnt[16];
+};
+__device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, PushFwdSmem& sm) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
+    PM_STAMP_ANY(50);
+    stage_frags_lds(sp.w_B, sm.lw, 0);
+    copy_lds_f32x4<2 * 264>(sp.learn_heads, sm.hf);
+    const int64_t id = t < B ? sp.idx[t] : 0;
+    __builtin_amdgcn_sched_barrier(0);
+    const pm_ctrl cs = *sp.ctrl;
+    const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
+    if (!push_handoff(mode, s_after >= B)) return;  // block-uniform: the learner does not wait
+    const bool ip = t < B && push_of(sp, cs.pos, cs.size, cs.max_prio).covers(id);
+    const unsigned long long m = __ballot(ip);
+    if (ip) sm.plist[wv * 64 + __popcll(m & ((1ull << lane) - 1ull))] = t;
+    if (lane == 0) sm.pcnt[wv] = __popcll(m);
+    if (t < B) sm.sidx[t] = id;
+    __syncthreads();
+    PM_STAMP_ANY(51);
+    float* pay = sp.hfeat + (size_t)B * 80;
+    push_rows_fwd(sp, sm.lw, sm.hf, sm.sidx, sm.plist, sm.pcnt, wv, lane,
+                  [&](int j, bool nxt, int ln, const f32x16 (&c2)[2], const float (&qb)[3], const float (&qt)[3],
+                      const float (&rb)[2]) { store_hfeat<true>(pay, j, nxt, ln, c2, qb, qt, rb); });
+    PM_STAMP_ANY(52);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are complete
+    __syncthreads();
+    PM_STAMP_ANY(53);
+    if (t == 0) st_out<true>(push_flag(sp), push_token(cs));
+}
+
 struct LearnSmem {
     union {
-        struct {  // forward phase
-            float lw[kLwFloats];  // modelB.features fragments (== targetB.features: frozen)
-            float hf[pad256(2 * 264)];  // modelB (update noise) [0, 264) / targetB (mu) [264, 528) head fragments
-        } f;
         float gpart[16][256];  // gradient phase: per-wave partial sums
     } u;
     float Hs[PM_MAX_BATCH][65];  // ReLU(features(s)) of the batch
@@ -662,6 +735,7 @@ struct LearnSmem {
 union LearnShared {
     LearnSmem learn;
     ActShared act;
+    PushFwdSmem pf;
 };
 static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 
@@ -673,11 +747,17 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // mode (PM_UPD_*): FIRST = the update that follows this step's k_env (its batch may hold rows of the
 // push k_env just made, which this kernel computes; it sums the rollout's episode counters); LAST =
 // the step's last update (refreshes the sum tree for the next push, commits the step). U = 1: both.
+// Block 1 is push_fwd_block; the side-A act blocks (launches with side blocks) follow it.
 __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     if (blockIdx.x > 0) {
+        if (blockIdx.x == 1) {
+            push_fwd_block(sp, mode, shm.pf);
+            return;
+        }
+        const int sb = (int)blockIdx.x - 2;  // side block index
         const ActGrid g{sp.n, sp.n_pool + 1, chunkA, chunkP, 0};
-        const int fb = (int)blockIdx.x - 1 - g.blocks();
+        const int fb = sb - g.blocks();
         if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB), started at once
             const int t0 = fb * kFeatTilesLearn;
             feat_tiles(shm.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + kFeatTilesLearn, feat_ntiles(sp.n)), sp.featB);
@@ -688,7 +768,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         __builtin_amdgcn_s_sleep(127);
         const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
         act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,
-                  (int)blockIdx.x - 1, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
+                  sb, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
         return;
     }
     LearnSmem& sm = shm.learn;
@@ -697,18 +777,13 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     pm_ctrl* c = sp.ctrl;
     PM_STAMP(0);
     const pm_ctrl cs = *c;  // loop counters as the step found them (only this kernel / k_adam commit)
-    const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
-    const bool train = s_after >= B;
     const PerTree tree = per_tree(sp.per_work, sp.cap);
     const bool first = mode & PM_UPD_FIRST, last = mode & PM_UPD_LAST;
 
     // ---- phase 0: every independent load, issued before any use. LDS-bound arrays go global ->
     // LDS directly (global_load_lds); register loads are issued unconditionally (gating them on the
     // control block, or storing each to LDS right away, costs one round trip per load).
-    const bool act = train && t < B;
     const int nbr = (sp.n + kBlock - 1) / kBlock;
-    stage_frags_lds(sp.w_B, sm.u.f.lw, 0);
-    copy_lds_f32x4<2 * 264>(sp.learn_heads, sm.u.f.hf);
     copy_lds_f32x4<260>(sp.learn_heads + 528, sm.eps_tr);
     if (sp.fuse_apply) load_apply_inputs(sp, sm.ap, false);
     long long part[6] = {0, 0, 0, 0, 0, 0};
@@ -733,6 +808,9 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     for (int b = t + kLearn; first && b < nbr; b += kLearn)  // n > 256 * 1024 arenas only
 #pragma unroll
         for (int k = 0; k < 6; ++k) part[k] += sp.partials[(size_t)b * 8 + k];
+    const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
+    const bool train = s_after >= B;
+    const bool act = train && t < B;
     // fused: the optimizer's scalar prologue on waves with slack in this load phase (they are not
     // on the dependent idx -> replay-row path of waves 0-3): the Adam bias corrections (two fp64
     // pow) on the last thread, both NoisyNet draws of the apply on the upper half of the block
@@ -800,37 +878,34 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][0];
         sm.ap.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)(float)s);
     }
-    if (train) {  // rows in the push range: one 32-row tile per wave (s rows then s' rows)
+    if (train) {  // rows in the push range (s rows then s' rows)
         int pre[5] = {0, 0, 0, 0, 0};
 #pragma unroll
         for (int w = 0; w < 4; ++w) pre[w + 1] = pre[w] + sm.pcnt[w];  // B <= 256: waves 0..3
         const int np = pre[4];
-        if (wv * 32 < 2 * np) {  // wave-uniform
-            const int rr = min(wv * 32 + (lane & 31), 2 * np - 1);
-            const bool nxt = rr >= np;
-            const int k = nxt ? rr - np : rr;
-            const int w = k >= pre[3] ? 3 : k >= pre[2] ? 2 : k >= pre[1] ? 1 : 0;
-            const int j = sm.plist[w * 64 + k - pre[w]];
-            f32x16 c2[2];
-            float qb[3], qt[3], rb[2];
-            batch_row_fwd(sp, sm.u.f.lw, sm.u.f.hf, sm.u.f.hf + 264, sm.sidx[j], nxt, lane, c2, qb, qt, rb);
-            if (wv * 32 + (lane & 31) < 2 * np) {
-                const int h = lane >> 5;
-                if (!nxt) {
-#pragma unroll
-                    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) sm.Hs[j][32 * tt + rho(r) + 4 * h] = relu(c2[tt][r]);
-                }
-                if (h == 0) {
-                    if (!nxt) {  // r and the action|done bits of the row this step's k_actenv wrote
-                        sm.qv[j][0] = qb[0]; sm.qv[j][1] = qb[1]; sm.qv[j][2] = qb[2];
-                        sm.qv[j][3] = rb[0]; sm.qv[j][7] = rb[1];
-                    } else {
-                        sm.qv[j][4] = qb[0]; sm.qv[j][5] = qb[1]; sm.qv[j][6] = qb[2];
-                        sm.qv[j][8] = qt[0]; sm.qv[j][9] = qt[1]; sm.qv[j][10] = qt[2];
+        if (np > 0 && push_handoff(mode, train)) {  // block-uniform: block 1 computes them
+            if (t == 0) {
+                const int* flag = push_flag(sp);
+                const int tok = push_token(cs);
+                int it = 0;
+                while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tok) {
+                    if (++it == kPushPollMax) {
+                        c->status = cs.status | PM_CTRL_PUSH_TIMEOUT;
+                        break;
                     }
+                    __builtin_amdgcn_s_sleep(2);
                 }
+            }
+            __syncthreads();
+            PM_STAMP(54);
+            const float* pay = sp.hfeat + (size_t)B * 80;
+            for (int k = t; k < np * 76; k += kLearn) {
+                const int q = k / 76, f = k - q * 76;
+                const int w = q >= pre[3] ? 3 : q >= pre[2] ? 2 : q >= pre[1] ? 1 : 0;
+                const int j = sm.plist[w * 64 + q - pre[w]];
+                const float v = __hip_atomic_load(pay + (size_t)j * 80 + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (f < 64) sm.Hs[j][f] = v;
+                else sm.qv[j][f - 64] = v;
             }
         }
     }
@@ -1196,7 +1271,7 @@ ActGrid learn_act_grid(const pm_selfplay* sp) {
 
 int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st, int mode = PM_UPD_FIRST | PM_UPD_LAST) {
     const ActGrid g = learn_act_grid(sp);
-    unsigned blocks = 1u + (with_act ? (unsigned)g.blocks() : 0u);
+    unsigned blocks = 2u + (with_act ? (unsigned)g.blocks() : 0u);  // learner, push-row block, side blocks
     if (with_act && sp->featB) blocks += (unsigned)((feat_ntiles(sp->n) + kFeatTilesLearn - 1) / kFeatTilesLearn);
     pm_launch(PM_TIMER_LEARN, k_learn, dim3(blocks), dim3(kLearn), st, *sp, g.chunk0, g.chunk1, mode);
     PM_LAUNCHED("k_learn");

@@ -160,6 +160,7 @@ class QNetGenerations:
                                self.check_every)
                 wA, wP = self.evaluate(rng)
                 c = L.counters()
+                L.check_status(c)
                 log(f"[Gen {g}] vs A:{wA:.2f}, vs Pool:{wP:.2f}, eps={c['epsilon']:.3f}")
                 if wA >= t["curr_win_threshold"] and wP >= t["pool_win_threshold"]:
                     log(f"升級! generation {g} done.")

@@ -99,7 +99,7 @@ class SelfPlayLearner:
         self.isw = torch.zeros(self.batch, **f32)
         self.grad = torch.zeros(PM_QNET_NHEAD + 8, **f32)
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
-        self.hfeat = torch.zeros((self.batch, 80), **f32)
+        self.hfeat = torch.zeros((2 * self.batch + 1, 80), **f32)  # + the push-row hand-off rows and flag
         self.learn_heads = torch.zeros(3 * 264, **f32)
         self.obsA = torch.zeros((n, 7), **f32)
         self.obsB = torch.zeros((n, 7), **f32)
@@ -260,6 +260,13 @@ class SelfPlayLearner:
     def counters(self):
         c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))
         return {k: getattr(c, k) for k, _ in _lib.Ctrl._fields_ if not k.startswith("_")}
+
+    def check_status(self, c=None):
+        """Device error bits (pm_ctrl.status): bit 0 = an update's push-row hand-off inside k_learn
+        timed out (its push rows were not computed: that update is void). Raises on any bit."""
+        st = int((c or self.counters())["status"])
+        if st:
+            raise _lib.PongmiError(f"self-play learner: device status {st} (bit 0: push-row hand-off timed out)")
 
     def set_epsilon(self, eps):
         c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))

@@ -359,6 +359,7 @@ def test_features_ahead_is_bitwise_identical(golden):
             assert torch.equal(getattr(A, name), getattr(B, name)), (n, name)
         assert A.counters() == B.counters()
         assert A.counters()["train_steps"] > 0
+        A.check_status()  # no push-row hand-off timed out
 
 
 def test_sharded_world2_overlap_equals_plain(golden):

@@ -29,6 +29,8 @@ NAMES = {
     12: "ph4 push subs w0", 13: "ph4 push subs w15", 14: "ph4 edges w0", 15: "ph4 edges w15",
     35: "ph0 before prologue", 34: "ph0 after prologue", 40: "ph0 w0 loads landed",
     41: "ph0 w4 loads landed", 42: "ph0 w8 loads landed", 43: "ph0 w15 loads landed",
+    50: "push blk start", 51: "push blk loads", 52: "push blk fwd done", 53: "push blk stores drained",
+    54: "learn push flag seen",
     5: "learn tree level1", 6: "learn tree level2", 20: "apply adam", 21: "apply derive", 7: "learn end",
 }
 

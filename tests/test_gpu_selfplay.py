@@ -196,6 +196,49 @@ def test_learn_and_apply_match_oracle(orc, golden):
         assert after["size"] == size
 
 
+def test_production_size_step_matches_oracle(orc, golden):
+    """configs[2] at its full size (the bench's workload: 65 536 arenas, replay cap 1e6, batch 256,
+    pool 8): the rollout of every arena and the update's PER draw, loss, head gradients and priority
+    scatter against the oracle, over vector steps with the replay still filling."""
+    L = _learner(golden, n=65536, batch=256, cap=1_000_000, n_pool=8, epsilon=0.3, fuse_apply=False)
+    sp = L.sp
+    for step in range(3):
+        pre = _snap(L)
+        L.rollout()
+        post = _snap(L)
+        _check_rollout(orc, L, pre, post)
+        L.learn()
+        torch.cuda.synchronize()
+        c = pre["ctrl"]
+        size = min(c["size"] + L.n, L.cap)
+        frame = c["frame_idx"] + 1
+        beta = min(1.0, 0.4 + frame * 0.6 / 100000)
+        r = orc.philox64(np.arange(L.batch), orc.TAG_PER, np.full(L.batch, frame, np.uint64), sp.seed_env)
+        ref_idx, ref_w = orc.per_sample(post["prios"], size, L.batch, beta, orc.u53(r[0], r[1]))
+        idx = L.idx.cpu().numpy()
+        assert np.mean(idx == ref_idx) > 0.99
+        rows = post["trans"][idx]
+        bits = rows[:, 15].view(np.int32)
+        a, dn = bits & 0xFF, ((bits >> 8) & 1).astype(bool)
+        isw = L.isw.cpu().numpy()
+        w = isw / isw.max()
+        same = idx == ref_idx
+        np.testing.assert_allclose(w[same], ref_w[same], rtol=3e-5)
+        from pongmi.qnet import unpack_state_dict
+        sdB = {k: v.numpy() for k, v in unpack_state_dict(L.paramsB).items()}
+        heads = orc.pack_heads(sdB)
+        theads = orc.pack_heads({k: v.numpy() for k, v in unpack_state_dict(L.paramsT).items()})
+        res = orc.dqn_loss_grads(sdB, heads, theads, sdB, rows[:, 0:7], a, rows[:, 7], rows[:, 8:15], dn, w, 0.99)
+        grad = L.grad.cpu().numpy()
+        np.testing.assert_allclose(grad[:520], res["grads"], rtol=2e-4, atol=2e-6)
+        np.testing.assert_allclose(L.counters()["last_loss"], res["loss"], rtol=1e-4)
+        exp_pr = post["prios"].copy()
+        orc.per_update(exp_pr, idx, res["errors"])
+        np.testing.assert_allclose(L.prios.cpu().numpy(), exp_pr, rtol=2e-5, atol=3e-5)
+        L.apply()
+    assert L.counters()["train_steps"] == 3 and L.counters()["size"] == 3 * 65536
+
+
 def test_no_update_before_batch_is_full(golden):
     """train_step returns while len(memory) < batch_size (:134): no Adam, counters still advance."""
     L = _learner(golden, n=300, batch=256, cap=1000)
@@ -283,7 +326,8 @@ def test_launch_timer_leaves_results_unchanged(golden):
         _lib.timer_arm(_lib.PM_TIMER_N)
 
 
-@pytest.mark.parametrize("n,cap", [(1000, 2500), (2048, 8192), (300, 1000), (4096, 4160)])
+@pytest.mark.parametrize("n,cap", [(1000, 2500), (2048, 8192), (300, 1000), (4096, 4160),
+                                   (65536, 1_000_000)])  # the last: the bench's configs[2] sizes
 def test_sum_tree_incremental_equals_rebuild(golden, n, cap):
     """The PER sum tree is maintained incrementally inside k_learn (scattered sub-blocks + the next
     push range, with the pending push substituted). After many steps — ring wrap-arounds at
@@ -335,6 +379,26 @@ def test_overlapped_step_is_bitwise_identical(golden):
                  "learn_heads", "per_work", "idx", "isw", "aA", "aB", "obsA", "obsB", "ep_reward"):
         assert torch.equal(getattr(A, name), getattr(B, name)), name
     assert A.counters() == B.counters()
+
+
+def test_production_step_equals_plain_at_full_size(golden):
+    """The bench's production step (overlapped, features ahead, fused apply) at configs[2]'s full
+    size equals the plain three-kernel step bit for bit, across the replay ring's first wrap
+    (1e6 / 65 536 = 15.3 vector steps) and a target sync."""
+    kw = dict(n=65536, batch=256, cap=1_000_000, seed=23, n_pool=8, target_update_interval=10)
+    A = _learner(golden, **kw)
+    B = _learner(golden, overlap=False, features_ahead=False, fuse_apply=False, **kw)
+    for _ in range(20):
+        A.step()
+        B.rollout()
+        B.learn()
+        B.apply()
+    torch.cuda.synchronize()
+    for name in ("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "opp", "w_B",
+                 "learn_heads", "per_work", "idx", "isw", "aB", "obsA", "obsB", "ep_reward"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    ca, cb = A.counters(), B.counters()
+    assert ca == cb and ca["train_steps"] == 20 and ca["size"] == 1_000_000
 
 
 def test_features_ahead_is_bitwise_identical(golden):

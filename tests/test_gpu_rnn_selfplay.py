@@ -48,14 +48,15 @@ def _snap(L):
                 ctrl=L.counters())
 
 
-@pytest.mark.parametrize("max_steps", [1000, 24])
-def test_rnn_selfplay_steps_match_oracle(golden, orc, max_steps):
+@pytest.mark.parametrize("n,max_steps,nsteps", [(256, 1000, 60), (256, 24, 60), (32768, 1000, 90)])
+def test_rnn_selfplay_steps_match_oracle(golden, orc, n, max_steps, nsteps):
     """max_steps = 24 exercises the max_episode_steps cut (:751): the episode ends (new opponent,
-    serve, zero (h, c), counters) but the trajectory goes on until a done."""
+    serve, zero (h, c), counters) but the trajectory goes on until a done. n = 32 768 is configs[4]'s
+    full arena count."""
     from pongmi import rnn
     # overlap=False: this test reads the opponents' (h, c) after every step, which the overlapped
     # step has already advanced for the next one (test_rnn_overlapped_step_is_bitwise_identical)
-    L = _learner(golden, n=256, n_pool=2, epsilon=0.0, min_epsilon=0.0, pool_ratio=0.5,
+    L = _learner(golden, n=n, n_pool=2, epsilon=0.0, min_epsilon=0.0, pool_ratio=0.5,
                  min_episodes_for_training_start=10 ** 6, memory_size=4096, seed=3, max_episode_steps=max_steps,
                  overlap=False)
     n, sp = L.n, L.sp
@@ -63,7 +64,7 @@ def test_rnn_selfplay_steps_match_oracle(golden, orc, max_steps):
     P = orc.make_params(pv)
     names = ("x", "y", "vx", "vy", "spin", "top", "bot")
     finished = cut = long_traj = 0
-    for k in range(60):
+    for k in range(nsteps):
         pre = _snap(L)
         L.step()
         post = _snap(L)
@@ -305,4 +306,24 @@ def test_rnn_overlapped_step_is_bitwise_identical(golden, U):
     assert torch.equal(A.learner.params, B.learner.params)
     assert torch.equal(A.trans, B.trans) and torch.equal(A.aA, B.aA) and torch.equal(A.aB, B.aB)
     assert torch.equal(A.hA, B.hA) and torch.equal(A.cA, B.cA)
+    assert A.learner.stats()["steps"] == B.learner.stats()["steps"] > 0
+
+
+def test_rnn_production_step_equals_plain_at_full_size(golden):
+    """configs[4] at its full size (the bench's workload: 32 768 arenas, pool 4, sequence buffer
+    200 000, DRQN 64 x 8 every step once the buffer holds enough episodes): the overlapped production
+    step equals the plain step bit for bit through the start of training."""
+    from pongmi import _lib
+    kw = dict(n=32768, n_pool=4, epsilon=0.05, seed=7)
+    A = _learner(golden, overlap=False, **kw)
+    B = _learner(golden, overlap=True, **kw)
+    for _ in range(40):
+        A.step()
+        B.step()
+    A.act_part(_lib.PM_ACT_A)  # A's opponents act for the current observations, as B's already did
+    torch.cuda.synchronize()
+    assert torch.equal(A.learner.params, B.learner.params)
+    assert torch.equal(A.trans, B.trans) and torch.equal(A.aA, B.aA) and torch.equal(A.aB, B.aB)
+    assert torch.equal(A.hA, B.hA) and torch.equal(A.cA, B.cA) and torch.equal(A.hB, B.hB)
+    assert A.counters() == B.counters()
     assert A.learner.stats()["steps"] == B.learner.stats()["steps"] > 0

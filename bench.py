@@ -91,10 +91,11 @@ def timed_region(one_step, steps, dist, n_events, after=None):
 PEAK_HBM_GBS = 8000.0
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, profile="r2_pmc.json"):
     """HBM bytes per launch of `kernel` (`name`, or `name@grid` for one of its launch grids) from the
-    committed rocprofv3 counter profile, or None."""
-    path = os.path.join(ROOT, "profiles", "r2_pmc.json")
+    committed rocprofv3 counter profile (profiles/r2_pmc.json: the default workload;
+    profiles/r2_rnn_pmc.json: --workload rnn), or None."""
+    path = os.path.join(ROOT, "profiles", profile)
     try:
         with open(path) as fh:
             return json.load(fh)["kernels"][kernel]["hbm_bytes"]
@@ -330,7 +331,10 @@ def run_rnn(args, dist, rank, world, allreduce):
                                    "on instrumented production steps after the timed region",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         # modelB's side: 256 blocks x 256 lanes (the overlapped step's only k_rnn_act of
+                         # that grid); the plain step's both-players launch has no committed pass
+                         "traffic": pmc_traffic(f"k_rnn_act@{256 * 256}", "r2_rnn_pmc.json") if overlap and n == 32768 else None,
                          "avg_us": round(act_s * 1e6, 2), "flop_per_arena": fpa, "n": n},
         }
         if overlap:

@@ -23,8 +23,11 @@ grids = defaultdict(set)
 for f in sorted(glob.glob(os.path.join(root, f"pmc_{tag}_*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        short = name.split("::")[-1].split("(")[0] if "::" in name else name.split("(")[0]
-        short = short.split("<")[0].strip()  # template arguments (k_env_step<2, false>)
+        # drop namespaces before cutting at the argument list: argument types carry "::" too
+        # (k_rnn_act(pm::ActGrid, ...)), and so do template arguments (k_env_step<2, false>)
+        short = name.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+        short = short.split("::")[-1].strip()
+        short = short[5:] if short.startswith("void ") else short
         grid = r.get("Grid_Size") or r.get("Grid_Size_X") or "0"
         acc[f"{short}@{grid}"][r["Counter_Name"]].append(float(r["Counter_Value"]))
         grids[short].add(int(grid))

@@ -69,6 +69,8 @@ def lib():
         L.or_step_batch.argtypes = [P, P, P, P, P, P, P, P, I32]
         L.or_rollout_random.argtypes = [P, U64, ctypes.c_int64, P]
         L.or_rollout_random.restype = ctypes.c_int64
+        L.or_qnet_f32.argtypes = [P, P, I32, P, P]
+        L.or_argmax3.argtypes = [P, I32, P]
         for f in ("or_mt_sizeof", "or_params_sizeof", "or_arena_sizeof"):
             getattr(L, f).restype = I32
         assert L.or_mt_sizeof() == ctypes.sizeof(OrMT)
@@ -257,6 +259,37 @@ def qnet_forward(eff, x):
     return qnet_heads(eff, qnet_features(eff, x))
 
 
+def qnet_forward_f32(w, x, want_feat=False):
+    """QNet.forward in float32 in the one fixed order libpongmi's matrix-core tile uses (k-ordered
+    fmaf chains; oracle/pong_oracle.c or_qnet_f32 states the order). w: an effective-weight block
+    (include/pongmi.h PM_QNET_NW floats, plain part first), x [n,7] f32. Returns q [n,3] f32 (and the
+    pre-ReLU layer-2 features [n,64] with want_feat). Exact: the device's Q must equal it bitwise."""
+    w = np.ascontiguousarray(np.asarray(w, np.float32).ravel()[:4932])
+    x = np.ascontiguousarray(x, np.float32).reshape(-1, 7)
+    n = x.shape[0]
+    q = np.zeros((n, 3), np.float32)
+    feat = np.zeros((n, 64), np.float32) if want_feat else None
+    lib().or_qnet_f32(w.ctypes.data, x.ctypes.data, n, q.ctypes.data, feat.ctypes.data if want_feat else None)
+    return (q, feat) if want_feat else q
+
+
+def fold_heads_f32(sd, mode):
+    """NoisyLinear.forward's effective heads (models/qnet.py:43-50) in torch's float32 arithmetic:
+    eval W = mu, train W = mu + (sigma * eps) (product rounded, then the sum). Returns the 4932-float
+    plain effective-weight block (W1 | b1 | W2 | b2 | Wh[V, A0..2] | bh)."""
+    f = lambda k: np.asarray(sd[k], np.float32)  # noqa: E731
+    parts = [f("features.0.weight").ravel(), f("features.0.bias"), f("features.2.weight").ravel(), f("features.2.bias")]
+    wh, bh = [], []
+    for h in ("fc_V", "fc_A"):
+        W, b = f(f"{h}.weight_mu"), f(f"{h}.bias_mu")
+        if mode == "train":
+            W = W + f(f"{h}.weight_sigma") * f(f"{h}.weight_epsilon")
+            b = b + f(f"{h}.bias_sigma") * f(f"{h}.bias_epsilon")
+        wh.append(W.reshape(-1, 64))
+        bh.append(b.ravel())
+    return np.concatenate(parts + [np.concatenate(wh).ravel(), np.concatenate(bh)]).astype(np.float32)
+
+
 def argmax_first(q):
     """torch argmax: first index of the maximum."""
     return np.argmax(q, axis=1)
@@ -437,6 +470,151 @@ def per_sample(prios, size, bs, beta, uniforms, alpha=0.6):
     w = (np.float32(size) * probs[idxs]) ** np.float32(-beta)
     w = w / w.max()
     return idxs.astype(np.int64), w.astype(np.float32)
+
+
+# PrioritizedReplay.sample's proportional draw as libpongmi's sum tree evaluates it. np.random.choice
+# (:66) normalises p in float32 and searches a float64 cumsum; the device descends fp64 node sums.
+# Both pick "the first entry whose running sum of p exceeds u" — the same distribution — but their
+# roundings differ near a CDF boundary, so an exact comparison needs the device's own summation
+# order. These two functions restate it (csrc/pm_per.h: per_quarter / per_combine / per_chunk_sum
+# for the nodes, per_round_prefix / per_lds_search / per_group_find for the descent), from the
+# priorities alone; tests/test_gpu_selfplay.py asserts equality for every draw, and
+# per_boundary_band() below ties the draw back to np.random.choice's own algorithm.
+PER_SUB, PER_FAN, PER_CHUNK = 64, 16, 1024
+
+
+def _seq_sum(cols):
+    """Sequential left-to-right float64 sum over axis 1 (cols [m, k])."""
+    acc = np.zeros(cols.shape[0])
+    for k in range(cols.shape[1]):
+        acc = acc + cols[:, k]
+    return acc
+
+
+def per_tree(prios, cap, alpha=0.6):
+    """Leaves powf(prio, alpha) (f32), level-1 nodes ((q0+q1)+q2)+q3 of sequential 16-leaf fp64 sums,
+    level-2 nodes sequential sums of 16 level-1 nodes. Returns (chunk, sub, leaf)."""
+    leaf = np.asarray(prios[:cap], np.float32) ** np.float32(alpha)
+    nsub = (cap + PER_SUB - 1) // PER_SUB
+    nch = (cap + PER_CHUNK - 1) // PER_CHUNK
+    lf = np.zeros(nsub * PER_SUB)
+    lf[:cap] = leaf.astype(np.float64)
+    q = [_seq_sum(lf.reshape(nsub, 4, 16)[:, k, :]) for k in range(4)]
+    sub = ((q[0] + q[1]) + q[2]) + q[3]
+    sp = np.zeros(nch * PER_FAN)
+    sp[:nsub] = sub
+    chunk = _seq_sum(sp.reshape(nch, PER_FAN))
+    return chunk, sub, leaf
+
+
+def _wave_incl_scan(v):
+    """Hillis-Steele inclusive scan of 64 lanes (v += shfl_up(v, o) for o = 1, 2, .., 32)."""
+    v = v.copy()
+    for o in (1, 2, 4, 8, 16, 32):
+        u = np.concatenate([np.zeros(o), v[:-o]])
+        v = np.where(np.arange(64) >= o, v + u, v)
+    return v
+
+
+def _round_prefix(vals):
+    """per_round_prefix for one round from base 0: vals [1024] chunk sums -> (incl [1024], total)."""
+    v = vals.reshape(256, 4)
+    run = np.cumsum(v, axis=1)  # sequential per thread (4 terms: cumsum is left to right)
+    acc = run[:, 3]
+    incl = np.zeros(1024)
+    wsum = []
+    for wv in range(4):
+        sc = _wave_incl_scan(acc[64 * wv:64 * wv + 64])
+        wsum.append(sc[63])
+        excl = np.concatenate([[0.0], sc[:-1]])
+        wb = 0.0
+        for k in range(wv):
+            wb = wb + wsum[k]
+        ex = wb + excl
+        incl[256 * wv:256 * wv + 256] = (ex[:, None] + run[64 * wv:64 * wv + 64]).ravel()
+    total = (((0.0 + wsum[0]) + wsum[1]) + wsum[2]) + wsum[3]
+    return incl, total
+
+
+def _group_find(v, x):
+    """per_group_find: 4 lanes x NV values in order; first value whose running sum exceeds x, else the
+    last nonzero one. Returns (index, sum before it, value)."""
+    nv = len(v) // 4
+    lanes = v.reshape(4, nv)
+    s = [0.0] * 4
+    for q in range(4):
+        a = 0.0
+        for e in range(nv):
+            a = a + lanes[q, e]
+        s[q] = a
+    exs = [0.0, s[0], s[0] + s[1], (s[0] + s[1]) + s[2]]
+    hit, nz = None, None
+    for q in range(4):
+        run = exs[q]
+        h = z = None
+        for e in range(nv):
+            val = lanes[q, e]
+            if h is None and run + val > x:
+                h = (e, run, val)
+            if val > 0.0:
+                z = (e, run, val)
+            run = run + val
+        if h is not None and hit is None:
+            hit = (q, h)
+        if z is not None:
+            nz = (q, z)
+    if hit is not None:
+        q, (e, b, val) = hit
+    elif nz is not None:
+        q, (e, b, val) = nz
+    else:
+        q, (e, b, val) = 0, (0, exs[0], 0.0)
+    return q * nv + e, b, val
+
+
+def per_sample_tree(prios, size, cap, beta, uniforms, alpha=0.6, tree=None):
+    """The device's draw (csrc/pm_per.h per_sample_block) for capacities <= 1M (one prefix round):
+    indices and un-normalised IS weights (size * P(i))^-beta, exactly as libpongmi computes them.
+    prios: the priorities the sample sees (pushes applied). Returns (idx int64, w f32)."""
+    chunk, sub, leaf = tree if tree is not None else per_tree(prios, cap, alpha)
+    nch = chunk.shape[0]
+    assert nch <= 1024, "one prefix round"
+    nb = (size + PER_CHUNK - 1) // PER_CHUNK
+    vals = np.zeros(1024)
+    vals[:nb] = chunk[:nb]
+    incl, total = _round_prefix(vals)
+    idx = np.zeros(len(uniforms), np.int64)
+    w = np.zeros(len(uniforms), np.float32)
+    lf = np.asarray(leaf, np.float32)
+    for j, u in enumerate(np.asarray(uniforms, np.float64)):
+        x = u * total
+        k = int(np.searchsorted(incl[:nb] > x, True)) if np.any(incl[:nb] > x) else nb
+        if k < nb:
+            blk, before = k, (incl[k - 1] if k else 0.0)
+        else:
+            lo = int(np.argmax(incl[:nb] >= incl[nb - 1]))
+            blk, before = lo, (incl[lo - 1] if lo else 0.0)
+        sv = np.array([sub[blk * 16 + e] if blk * 16 + e < sub.shape[0] else 0.0 for e in range(16)])
+        f1, b1, _ = _group_find(sv, x - before)
+        sb = blk * 16 + f1
+        e0 = sb * PER_SUB
+        lv = np.array([float(lf[e0 + e]) if e0 + e < size else 0.0 for e in range(64)])
+        f0, _, pa = _group_find(lv, (x - before) - b1)
+        idx[j] = e0 + f0
+        w[j] = np.float32(((float(size) * (pa / total)) ** (-beta)))
+    return idx, w
+
+
+def per_boundary_band(prios, size, uniforms, alpha=0.6, tol=5e-7):
+    """Which draws lie within `tol` of a CDF boundary of P(i) = prio_i^alpha / sum, where
+    np.random.choice's float32-normalised CDF (per_sample) and any exact-order sum may disagree:
+    the float32 normalisation moves each CDF value by <= 2^-23 relative, and a 1-ulp difference in a
+    float32 prio^alpha moves it by as much again, so 5e-7 bounds the disagreement. Returns a bool mask;
+    outside it every correct sampler must pick np.random.choice's index."""
+    p = np.asarray(prios[:size], np.float32).astype(np.float64) ** alpha
+    cdf = np.cumsum(p) / p.sum()
+    u = np.asarray(uniforms, np.float64)
+    return np.searchsorted(cdf, u - tol, side="right") != np.searchsorted(cdf, u + tol, side="right")
 
 
 def per_update(prios, idxs, errors):

@@ -125,3 +125,28 @@ def test_drop_in_modules_import_with_reference_names():
     x = torch.rand(5, 7)
     y = net(x)  # CPU tensors: the module keeps the reference's tensor semantics
     assert y.shape == (5, 3)
+
+
+def test_integration_stub_runs(monkeypatch):
+    """INTEGRATION.md section 1's ctypes stub (the binding a reference maintainer would add) runs
+    as written against the built library: its ABI assertion holds, its pm_env_step argtypes have as
+    many entries as the header's prototype, and a bad call surfaces pm_last_error as RuntimeError."""
+    from pongmi import _lib
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = text[text.index("## 1."):text.index("## 2.")]
+    code = re.search(r"```python\n(.*?)```", sec, re.S).group(1)
+    hdr = open(os.path.join(ROOT, "include", "pongmi.h")).read()
+    abi = re.search(r"#define PM_ABI_VERSION (\d+)", hdr).group(1)
+    assert f"== {abi}" in code
+    os.environ["PONGMI_LIB"] = _lib.LIB_PATH
+    ns = {}
+    exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    proto = re.search(r"int pm_env_step\((.*?)\);", hdr, re.S).group(1)
+    assert len(ns["_lib"].pm_env_step.argtypes) == len(proto.split(","))
+    # n = 4 with a state of null device pointers: the library rejects the call before any HIP work
+    # and the stub raises its message
+    from pongmi.env import env_params
+    T = torch.zeros(4, dtype=torch.int8)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda: type("S", (), {"cuda_stream": 0})())  # no GPU here
+    with pytest.raises(RuntimeError, match="pm_env_step"):
+        ns["env_step"](env_params(), _lib.EnvState(), T, T, T, T, T, T, T)

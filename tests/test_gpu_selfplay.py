@@ -36,7 +36,8 @@ def _learner(golden, n=2048, batch=256, cap=8192, n_pool=2, **kw):
 def _snap(L):
     torch.cuda.synchronize()
     return dict(f64=L.f64.cpu().numpy().copy(), i32=L.i32.cpu().numpy().copy(), opp=L.opp.cpu().numpy().copy(),
-                er=L.ep_reward.cpu().numpy().copy(), ctrl=L.counters(), trans=L.trans.cpu().numpy().copy(),
+                er=L.ep_reward.cpu().numpy().copy(), ctrl=L.counters(), aA=L.aA.cpu().numpy().copy(),
+                aB=L.aB.cpu().numpy().copy(), trans=L.trans.cpu().numpy().copy(),
                 prios=L.prios.cpu().numpy().copy(), paramsB=L.paramsB.cpu().numpy().copy(),
                 paramsT=L.paramsT.cpu().numpy().copy(), w_B=L.w_B.cpu().numpy().copy(),
                 w_opp=L.w_opp.cpu().numpy().copy(), m=L.adam_m.cpu().numpy().copy(), v=L.adam_v.cpu().numpy().copy())
@@ -65,27 +66,28 @@ def _check_rollout(orc, L, pre, post):
     oA, oB = orc.obs_of_arenas(arr)
     c = pre["ctrl"]
     step = c["step"]
-    qa = np.zeros((n, 3))
+    # both players' Q in the float32 restatement of the device's evaluation order (bitwise equal to
+    # the matrix-core tile), so every arena's greedy action is checked, near-ties included
+    qa = np.zeros((n, 3), np.float32)
     for k in range(L.n_pool + 1):
         sel = pre["opp"] == k
-        qa[sel] = orc.qnet_forward(_eff_from_w(pre["w_opp"][k]), oA[sel])
-    qb = orc.qnet_forward(_eff_from_w(pre["w_B"]), oB)
+        qa[sel] = orc.qnet_forward_f32(pre["w_opp"][k], oA[sel])
+    qb = orc.qnet_forward_f32(pre["w_B"], oB)
     r = orc.philox64(np.arange(n), orc.TAG_ACT, np.full(n, step, np.uint64), sp.seed_env)
     explore = orc.u53(r[0], r[1]) < c["epsilon"]
     aA = np.argmax(qa, 1)
     aB = np.where(explore, orc.below(r[2], 3), np.argmax(qb, 1))
-    sa, sb = np.sort(qa, 1), np.sort(qb, 1)
-    ok = (sa[:, 2] - sa[:, 1] > 1e-4) & ((sb[:, 2] - sb[:, 1] > 1e-4) | explore)
     nA, nB, rew, done = orc.step_arenas(P, arr, aA.astype(np.int8), aB.astype(np.int8))
     d = done.astype(bool)
     # replay rows pushed at (pos + i) % cap
     slots = (c["pos"] + np.arange(n)) % L.cap
     rows = post["trans"][slots]
-    assert np.array_equal(rows[ok, 0:7], oB[ok])
-    assert np.array_equal(rows[ok, 7], rew[ok, 1])
-    assert np.array_equal(rows[ok, 8:15], nB[ok])
+    assert np.array_equal(post["aA"], aA) and np.array_equal(post["aB"], aB)  # every arena
+    assert np.array_equal(rows[:, 0:7], oB)
+    assert np.array_equal(rows[:, 7], rew[:, 1])
+    assert np.array_equal(rows[:, 8:15], nB)
     bits = rows[:, 15].view(np.int32)
-    assert np.array_equal(bits[ok] & 0xFF, aB[ok]) and np.array_equal((bits[ok] >> 8) & 1, done[ok])
+    assert np.array_equal(bits & 0xFF, aB) and np.array_equal((bits >> 8) & 1, done)
     maxp = 1.0 if c["size"] == 0 else c["max_prio"]
     assert np.all(post["prios"][slots] == np.float32(maxp))
     # bookkeeping and serves
@@ -95,23 +97,42 @@ def _check_rollout(orc, L, pre, post):
     use_pool = (L.n_pool > 0) & (orc.u53(q[0], q[1]) < sp.pool_ratio)
     newopp = np.where(use_pool, 1 + orc.below(q[2], max(L.n_pool, 1)), 0)
     vx, vy, spn = orc.philox_serve(pv, np.arange(n), ns, sp.seed_env)
-    m = ok & d
-    assert np.array_equal(post["opp"][m], newopp[m]) and np.array_equal(post["opp"][ok & ~d], pre["opp"][ok & ~d])
-    assert np.all(post["er"][m] == 0) and np.array_equal(post["er"][ok & ~d], er[ok & ~d])
+    m = d
+    assert np.array_equal(post["opp"][m], newopp[m]) and np.array_equal(post["opp"][~d], pre["opp"][~d])
+    assert np.all(post["er"][m] == 0) and np.array_equal(post["er"][~d], er[~d])
     assert np.all(post["i32"][3][m] == ns[m] + 1)
     np.testing.assert_allclose(post["f64"][2][m], vx[m], rtol=4e-16, atol=1e-18)
     np.testing.assert_allclose(post["f64"][3][m], vy[m], rtol=4e-16, atol=1e-18)
     assert np.array_equal(post["f64"][4][m], spn[m]) and np.all(post["f64"][0][m] == 0.5)
-    keep = ok & ~d
+    keep = ~d
     for j, k in enumerate(names):
         assert np.array_equal(post["f64"][j][keep], arr[k][keep]), k
     for j, k in enumerate(("scoreA", "scoreB", "bounces")):
         assert np.array_equal(post["i32"][j][keep], arr[k][keep]), k
-    assert ok.mean() > 0.95
     win = er > 0
     return dict(fin=int(d.sum()), finA=int((d & (pre["opp"] == 0)).sum()), winA=int((d & (pre["opp"] == 0) & win).sum()),
                 finP=int((d & (pre["opp"] != 0)).sum()), winP=int((d & (pre["opp"] != 0) & win).sum()),
                 rsum=int(er[d].sum()))
+
+
+def _check_per(orc, prios, size, cap, beta, u, idx, isw):
+    """The update's PER draw, every one of its `batch` samples: indices and IS weights equal the
+    restatement of the device's sum-tree descent (oracle.per_sample_tree, its own fp64 summation
+    order) exactly; against np.random.choice's float32-normalised CDF (oracle.per_sample, the
+    reference's algorithm) the indices are equal on every draw outside the CDF-boundary rounding band
+    (oracle.per_boundary_band), and the band's count is printed (expected 0 or a few at 1e5+
+    entries). Returns the normalised weights."""
+    tidx, tw = orc.per_sample_tree(prios, size, cap, beta, u)
+    assert np.array_equal(idx, tidx), f"{(idx != tidx).sum()} PER indices differ from the tree restatement"
+    np.testing.assert_allclose(isw, tw, rtol=1.2e-7)  # one float32 ulp: the fp64 pow's last bit
+    ref_idx, ref_w = orc.per_sample(prios, size, len(u), beta, u)
+    band = orc.per_boundary_band(prios, size, u)
+    assert np.array_equal(idx[~band], ref_idx[~band])
+    print(f"PER: size {size}, {int(band.sum())} of {len(u)} draws in the CDF rounding band, "
+          f"{int((idx != ref_idx).sum())} differ from np.random.choice's there")
+    w = isw / isw.max()
+    np.testing.assert_allclose(w, ref_w, rtol=3e-5)  # every draw
+    return w
 
 
 def test_rollout_matches_oracle(orc, golden):
@@ -151,18 +172,13 @@ def test_learn_and_apply_match_oracle(orc, golden):
         beta = min(1.0, 0.4 + frame * 0.6 / 100000)
         r = orc.philox64(np.arange(L.batch), orc.TAG_PER, np.full(L.batch, frame, np.uint64), sp.seed_env)
         u = orc.u53(r[0], r[1])
-        ref_idx, ref_w = orc.per_sample(pre["prios"], size, L.batch, beta, u)
         idx = L.idx.cpu().numpy()
-        assert np.mean(idx == ref_idx) > 0.99
+        w = _check_per(orc, pre["prios"], size, L.cap, beta, u, idx, L.isw.cpu().numpy())
         rows = pre["trans"][idx]
         s, ns = rows[:, 0:7], rows[:, 8:15]
         rwd = rows[:, 7]
         bits = rows[:, 15].view(np.int32)
         a, dn = bits & 0xFF, ((bits >> 8) & 1).astype(bool)
-        isw = L.isw.cpu().numpy()
-        w = isw / isw.max()
-        same = idx == ref_idx
-        np.testing.assert_allclose(w[same], ref_w[same], rtol=3e-5)
         from pongmi.qnet import unpack_state_dict
         sdB = {k: v.numpy() for k, v in unpack_state_dict(L.paramsB).items()}  # eps = the update's noise
         fVi, fVo, fAi, fAo = orc.philox_noise(sp.seed_net, orc.TAG_NOISE_TRAIN, c["train_steps"] + 1)
@@ -214,16 +230,11 @@ def test_production_size_step_matches_oracle(orc, golden):
         frame = c["frame_idx"] + 1
         beta = min(1.0, 0.4 + frame * 0.6 / 100000)
         r = orc.philox64(np.arange(L.batch), orc.TAG_PER, np.full(L.batch, frame, np.uint64), sp.seed_env)
-        ref_idx, ref_w = orc.per_sample(post["prios"], size, L.batch, beta, orc.u53(r[0], r[1]))
         idx = L.idx.cpu().numpy()
-        assert np.mean(idx == ref_idx) > 0.99
+        w = _check_per(orc, post["prios"], size, L.cap, beta, orc.u53(r[0], r[1]), idx, L.isw.cpu().numpy())
         rows = post["trans"][idx]
         bits = rows[:, 15].view(np.int32)
         a, dn = bits & 0xFF, ((bits >> 8) & 1).astype(bool)
-        isw = L.isw.cpu().numpy()
-        w = isw / isw.max()
-        same = idx == ref_idx
-        np.testing.assert_allclose(w[same], ref_w[same], rtol=3e-5)
         from pongmi.qnet import unpack_state_dict
         sdB = {k: v.numpy() for k, v in unpack_state_dict(L.paramsB).items()}
         heads = orc.pack_heads(sdB)
@@ -517,13 +528,10 @@ def test_multi_update_step_matches_oracle(orc, golden):
             r = orc.philox64(np.arange(L.batch), orc.TAG_PER, np.full(L.batch, frame, np.uint64), sp.seed_env)
             # update 0's batch was drawn beside k_env with the push pending: the pushed priorities
             # are in pre["prios"] already, so every update samples from its snapshot
-            ref_idx, ref_w = orc.per_sample(pre["prios"], size, L.batch, beta, orc.u53(r[0], r[1]))
             idx = L.idx.cpu().numpy()
-            assert np.mean(idx == ref_idx) > 0.99, (step, u)
+            w = _check_per(orc, pre["prios"], size, L.cap, beta, orc.u53(r[0], r[1]), idx, L.isw.cpu().numpy())
             rows = pre["trans"][idx]
             bits = rows[:, 15].view(np.int32)
-            isw = L.isw.cpu().numpy()
-            w = isw / isw.max()
             sdB = {k: v.numpy() for k, v in unpack_state_dict(L.paramsB).items()}
             fVi, fVo, fAi, fAo = orc.philox_noise(sp.seed_net, orc.TAG_NOISE_TRAIN, c["train_steps"] + 1)
             np.testing.assert_allclose(sdB["fc_A.weight_epsilon"], np.outer(fAo, fAi), rtol=2e-6, atol=1e-7)

@@ -171,3 +171,53 @@ def test_drqn_update_matches_reference(golden, orc):
         np.testing.assert_allclose(info["norm"], gd[f"u{k}_norm"], rtol=1e-4)
     for k in orc.RNN_PARAM_KEYS:
         np.testing.assert_allclose(np.ravel(sd[k])[::8], gd["final_sub." + k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_qnet_f32_order_restatement_matches_reference(orc, golden):
+    """The float32 restatement of the device's evaluation order (what the GPU tests compare every
+    action against) is itself a faithful QNet.forward: within float32 rounding of the reference's
+    Q values, and equal argmax wherever the reference's top two Q differ by more than that rounding."""
+    g = golden("qnet")
+    for who in ("modelB", "modelA"):
+        sd = {k[len(who) + 1:]: v for k, v in g.items() if k.startswith(who + ".") and "q_" not in k}
+        for mode in ("eval", "train"):
+            q = orc.qnet_forward_f32(orc.fold_heads_f32(sd, mode), g["obs"])
+            ref = g[f"{who}.q_{mode}"]
+            np.testing.assert_allclose(q, ref, rtol=0, atol=2e-5)
+            gap = np.sort(ref, 1)
+            clear = (gap[:, -1] - gap[:, -2]) > 4e-5
+            assert np.array_equal(np.argmax(q, 1)[clear], np.argmax(ref, 1)[clear])
+
+
+def test_per_tree_restatement_matches_reference(orc, golden):
+    """The restatement of the device's sum-tree descent picks the reference's np.random.choice index
+    on every draw of the golden PER fixture (the 2 draws that sit in the CDF rounding band included),
+    and its IS weights equal the reference's."""
+    g = golden("per")
+    draws = 0
+    for ph in range(int(g["n_phases"])):
+        u = 0
+        while f"p{ph}.u{u}.idxs" in g:
+            k = f"p{ph}.u{u}."
+            size = int(g[k + "size"])
+            idx, w = orc.per_sample_tree(g[k + "prios_before"], size, size, float(g[k + "beta"]), g[k + "uniforms"])
+            assert np.array_equal(idx, g[k + "idxs"])
+            np.testing.assert_allclose(w / w.max(), g[k + "weights"], rtol=2e-6)
+            draws += len(idx)
+            u += 1
+    assert draws >= 256
+
+
+@pytest.mark.parametrize("size", [1, 1023, 1025, 4096, 200_000, 1_000_000])
+def test_per_tree_restatement_vs_choice_outside_band(orc, size):
+    """At every buffer size: the tree order and np.random.choice's float32-normalised CDF pick the same
+    index for every uniform outside the CDF-boundary rounding band (per_boundary_band)."""
+    rng = np.random.RandomState(size)
+    pr = rng.uniform(0, 3, size).astype(np.float32)
+    pr[rng.rand(size) < 0.1] = 0.0
+    pr[0] = 0.5
+    u = rng.random_sample(512)
+    idx, _ = orc.per_sample_tree(pr, size, size, 0.5, u)
+    ref, _ = orc.per_sample(pr, size, 512, 0.5, u)
+    band = orc.per_boundary_band(pr, size, u)
+    assert np.array_equal(idx[~band], ref[~band]) and np.all(pr[idx] > 0)

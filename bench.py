@@ -117,6 +117,29 @@ def replicas_identical(dist, params):
     return bool(torch.equal(hi, -lo))
 
 
+def shard_proof(dist, rank, world, n, steps_done, status, comm, grad=None):
+    """N > 1: what every rank saw, gathered to rank 0 so the line can only be produced by N live
+    ranks: RCCL's own view of the communicator (pm_comm_info: ncclCommCount / ncclCommUserRank /
+    device), the arenas and vector steps this rank ran, its device status word, and — for the DQN
+    learner — the packed buffer's updated-flag after the last SUM all-reduce (= the number of ranks
+    whose update entered it). Returns (per-rank list, ok)."""
+    if dist is None:
+        return None, True
+    nr, rr, dev = comm.info() if comm is not None else (dist.get_world_size(), dist.get_rank(), torch.cuda.current_device())
+    upd = float(grad[521].item()) if grad is not None else -1.0
+    row = torch.zeros((world, 8), dtype=torch.float64, device="cuda")
+    row[rank] = torch.tensor([rank, nr, rr, dev, n, steps_done, status, upd], dtype=torch.float64)
+    dist.all_reduce(row)
+    rows = [dict(rank=int(r[0]), rccl_nranks=int(r[1]), rccl_rank=int(r[2]), device=int(r[3]), arenas=int(r[4]),
+                 vector_steps=int(r[5]), status=int(r[6]), **({"allreduce_updated_sum": r[7]} if grad is not None else {}))
+            for r in row.cpu().tolist()]
+    ok = all(r["rccl_nranks"] == world and r["rccl_rank"] == r["rank"] and r["status"] == 0 for r in rows)
+    ok = ok and len({r["vector_steps"] for r in rows}) == 1
+    if grad is not None:
+        ok = ok and all(r["allreduce_updated_sum"] == world for r in rows)
+    return rows, ok
+
+
 def synthetic_qnet(seed):
     from models.qnet import QNet
     torch.manual_seed(seed)
@@ -218,6 +241,41 @@ def cpu_baseline(n, seconds=12.0):
                       f"batch 256), {dt:.1f} s on 1 host core"}
 
 
+def _config0_worker(seconds, seed, q):
+    from oracle import oracle as orc
+    P = orc.make_params(orc.env_params_from_kwargs(**ENV_KW))
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.rollout_random(P, seed + steps, 200_000)
+        steps += 200_000
+    q.put((steps, time.perf_counter() - t0))
+
+
+def cpu_config0(seconds=3.0, procs=None):
+    """BASELINE configs[0]: ONE PongEnv2P arena, random vs random, the scalar CPU step loop
+    (random.seed, randint actions for A then B, reset on done), as the oracle's C
+    restatement (oracle/pong_oracle.c or_rollout_random, pinned to the reference's own loop output by
+    tests/test_oracle_golden.py::test_rollout_random_matches_reference_loop) on 1 host core and on
+    `procs` independent processes (one arena each, like the reference run once per core)."""
+    import multiprocessing as mpr
+    procs = procs or max(1, min(16, len(os.sched_getaffinity(0))))
+    out = {}
+    for k in (1, procs):
+        ctx = mpr.get_context("fork")
+        q = ctx.Queue()
+        ps = [ctx.Process(target=_config0_worker, args=(seconds, 1000 * r, q)) for r in range(k)]
+        for p in ps:
+            p.start()
+        res = [q.get() for _ in ps]
+        for p in ps:
+            p.join()
+        out[f"cores_{k}"] = round(sum(st / dt for st, dt in res), 1)
+    return {"workload": "configs[0]: 1 arena per process, random vs random, scalar step loop with reset on done",
+            "unit": "env-steps/s", "value_1core": out["cores_1"], "value_all": out[f"cores_{procs}"], "cores": procs,
+            "kind": "port", "sample": f"oracle/pong_oracle.c or_rollout_random, {seconds:.0f} s per process",
+            "reference_python_measured": "94 k env-steps/s per core, 442 k on 8 processes (SURVEY 6, survey container)"}
+
+
 ENV_KW_RNN = dict(ENV_KW, restitution=1.0, speed_scale_every=5, speed_increment=0.2)  # config_rnn.yaml:6-28
 # QNetRNN multiply-adds per row: 7(+bias)x64 + 64x128 + 256x512 (LSTM gates) + 128x128 + 128x4 heads
 RNN_MAC = 8 * 64 + 64 * 128 + 256 * 512 + 128 * 128 + 128 * 4
@@ -305,6 +363,8 @@ def run_rnn(args, dist, rank, world, allreduce):
     env_s = sum(e[1].elapsed_time(e[2]) for e in evs) * 1e-3 / len(evs)  # overlap: env + update
     upd_s = sum(e[2].elapsed_time(e[3]) for e in evs) * 1e-3 / len(evs)
     c = L.counters()
+    shards, shards_ok = shard_proof(dist, rank, world, n, c["step"], c["status"] & 1, args.comm)
+    failed = (c["status"] & 1) != 0 or not shards_ok or (dist is not None and not same)
     if rank == 0:
         value = n * world * args.steps / dt
         fpa = RNN_FLOP_PER_ARENA // 2 if overlap else RNN_FLOP_PER_ARENA  # overlap: modelB's side only
@@ -323,7 +383,8 @@ def run_rnn(args, dist, rank, world, allreduce):
                        "memory_size": L.cap, "ring_depth": L.depth,
                        "updates_in_timed_region": c1["train_steps"] - c0["train_steps"],
                        "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
-                       "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same},
+                       "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same,
+                       "shards": shards},
             "roofline": {"bound": "mfma",
                          "kernel": "k_rnn_act side B: the overlapped step's act for modelB" if overlap
                                    else "k_rnn_act (both players)",
@@ -351,9 +412,13 @@ def run_rnn(args, dist, rank, world, allreduce):
         })
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_rnn(args.cpu_seconds)
+        if failed:
+            out["error"] = "device status bit 0 (overwritten ring read) / shard proof failed"
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if failed:
+        sys.exit(3)
 
 
 def main():
@@ -369,6 +434,12 @@ def main():
     ap.add_argument("--memory", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--updates-per-step", type=int, default=1,
+                    help="dqn: PER updates of `batch` per vector step (U; SURVEY 8d: 1 default, 64 the stress "
+                         "variant; the reference's own ratio is one update per env step, i.e. U = arenas)")
+    ap.add_argument("--weights", choices=("reference", "random"), default="reference",
+                    help="reference: model5-5_fault.pth's QNet weights (tests/golden/qnet.npz) for modelB and modelA "
+                         "(SURVEY 8d); random: random-init nets of the reference architecture")
     ap.add_argument("--no-overlap", action="store_true", help="dqn: plain step (opponent act in k_act_sp, not in the learner launch)")
     ap.add_argument("--comm", choices=("native", "torch"), default="native",
                     help="N > 1: the gradient all-reduce as libpongmi's own RCCL communicator inside one library "
@@ -378,6 +449,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # configs[0]'s scalar CPU loop runs in forked worker processes: before this process touches the GPU
+    args.cpu_config0 = cpu_config0() if world == 1 and args.workload == "dqn" and not args.no_cpu_baseline else None
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -387,12 +460,9 @@ def main():
     comm = None
     if dist is not None and args.comm == "native":
         from pongmi.dist import NativeComm
-        try:
-            comm = NativeComm()
-        except Exception as e:  # every rank sees rank 0's binding failure: all fall back together
-            print(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed.all_reduce",
-                  file=sys.stderr, flush=True)
+        comm = NativeComm()  # raises on every rank if RCCL cannot be bound: no silent fallback
     args.comm_used = "native RCCL, in-stream" if comm is not None else "torch.distributed"
+    args.comm = comm
     allreduce = comm if comm is not None else ((lambda t: dist.all_reduce(t)) if dist else None)
 
     if args.workload == "rnn":
@@ -402,11 +472,11 @@ def main():
     from pongmi import _lib
     from pongmi.selfplay import SelfPlayLearner
 
-    sdB, sdA = synthetic_qnet(1), synthetic_qnet(2)
-    pool = [synthetic_qnet(100 + k) for k in range(args.pool)]
+    U = max(1, int(args.updates_per_step))
+    sdB, sdA, pool, wdesc = bench_nets(args.weights, args.pool)
     L = SelfPlayLearner(ENV_KW, args.arenas, sdB, sdA, pool, batch=args.batch, memory_size=args.memory,
                         epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce,
-                        overlap=not args.no_overlap)
+                        overlap=not args.no_overlap, updates_per_step=U)
 
     def one_step(ev=None):
         # the production path: the overlapped vector step (L.step); an instrumented step is the same
@@ -420,6 +490,7 @@ def main():
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
+    c0 = L.counters()
     ae_t, learn_t = [], []
 
     def read_timers():
@@ -431,6 +502,8 @@ def main():
     ae_s = sum(ae_t) / len(ae_t)  # the launches' own durations, as rocprofv3 --kernel-trace times them
     learn_s = sum(learn_t) / len(learn_t)
     c = L.counters()
+    shards, shards_ok = shard_proof(dist, rank, world, args.arenas, c["step"], c["status"], args.comm, L.grad)
+    failed = c["status"] != 0 or not shards_ok or (dist is not None and not same)
 
     if rank == 0:
         total = args.arenas * world * args.steps
@@ -446,19 +519,21 @@ def main():
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64 env state / f32 QNet",
-            "data": "synthetic (random-init QNet weights of the reference architecture, Philox serves)",
+            "data": f"synthetic observations from the env itself (Philox serves); {wdesc}",
             "config": {"workload": "configs[2]: 65536 arenas/GPU, full DQN train_iterative loop (act both players + "
                                    "env tick + PER push/sample + double-DQN update + Adam + target sync)",
                        "arenas_per_gpu": args.arenas, "global_arenas": args.arenas * world,
-                       "pool": args.pool, "batch": args.batch, "updates_per_vector_step": 1,
+                       "pool": args.pool, "batch": args.batch, "updates_per_vector_step": U,
+                       "updates_in_timed_region": c["train_steps"] - c0["train_steps"],
                        "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
-                       "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same},
+                       "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same,
+                       "shards": shards},
             "roofline": {"bound": "mfma",
                          "kernel": "k_learn launch: the double-DQN update (one workgroup) + the next step's "
                                    "opponents' act and modelB's feature layers on the other CUs",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": pmc_traffic("k_learn"),
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": pmc_traffic("k_learn") if U == 1 else None,
                          "avg_us": round(learn_s * 1e6, 2), "flop_per_arena": learn_flop, "n": args.arenas},
             "env_roofline": {"bound": "hbm",
                              "kernel": "k_actenv (modelB's heads + env tick + replay push + PER sample / batch "
@@ -466,20 +541,43 @@ def main():
                                                                 "PER sample / batch forward)",
                              "achieved": round(env_gbs, 1), "peak": PEAK_HBM_GBS,
                              "unit": "GB/s", "frac": round(env_gbs / PEAK_HBM_GBS, 4),
-                             "traffic": pmc_traffic(f"k_actenv@{ae_grid * 256}"),
+                             "traffic": pmc_traffic(f"k_actenv@{ae_grid * 256}") if U == 1 else None,
                              "avg_us": round(ae_s * 1e6, 2), "bytes_per_env_step": env_bytes},
             "learn_us": round(learn_s * 1e6, 2), "actenv_us": round(ae_s * 1e6, 2),
             "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
-                        "last_loss": c["last_loss"]},
+                        "last_loss": c["last_loss"], "status": c["status"]},
         }
+        if U > 1:
+            out["us_per_update"] = round(dt / args.steps / U * 1e6, 3)
         if world == 1:
             out["act_full_roofline"] = time_act_full(L)
             out["env_step_roofline"] = time_env_step(args.arenas)
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline(args.arenas, args.cpu_seconds)
+                out["cpu_config0"] = args.cpu_config0
+        if failed:
+            out["error"] = "device status / shard proof failed: see learner.status and config.shards"
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if failed:
+        sys.exit(3)
+
+
+def bench_nets(which, n_pool):
+    """(modelB, modelA, pool, description). reference: SURVEY 8d's acting nets, model5-5_fault.pth's
+    QNet (tests/golden/qnet.npz holds its modelB / modelA state_dicts, written by make_golden.py from
+    the reference checkpoint) for modelB and for modelA; the pool is its modelA plus random-init nets
+    (the reference's pool loads its legacy fc.* files with strict=False, i.e. as random nets)."""
+    if which == "random":
+        return (synthetic_qnet(1), synthetic_qnet(2), [synthetic_qnet(100 + k) for k in range(n_pool)],
+                "random-init QNet weights of the reference architecture")
+    g = np.load(os.path.join(ROOT, "tests", "golden", "qnet.npz"))
+    sd = {who: {k[len(who) + 1:]: torch.from_numpy(g[k].copy()) for k in g.files
+                if k.startswith(who + ".") and "q_" not in k} for who in ("modelB", "modelA")}
+    pool = ([sd["modelA"]] if n_pool else []) + [synthetic_qnet(100 + k) for k in range(max(0, n_pool - 1))]
+    return (sd["modelB"], sd["modelB"], pool,
+            "model5-5_fault.pth QNet weights (modelB for both players; pool = its modelA + random-init nets)")
 
 
 if __name__ == "__main__":

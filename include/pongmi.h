@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 13
+#define PM_ABI_VERSION 15
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -85,11 +85,15 @@ int pm_env_reset(const pm_env_params* p, const pm_env_state* s, const uint8_t* m
  *   autoreset 1: every term row is written (the step's pre-reset observation of every arena);
  *   autoreset 2: only the rows of arenas with done[i] != 0 are written, the others keep their
  *                contents (next state for replay = done ? term_obs : obs; SURVEY.md §8d's 203 B
- *                per env-step). With autoreset 0 the term rows, if given, equal obs. */
+ *                per env-step). With autoreset 0 the term rows, if given, equal obs.
+ * Serves of done arenas (ABI 15): with `inject` as pm_env_reset (serves[i] indexes the table and is
+ * incremented); in production (inject NULL) from Philox(seed) keyed by (i, counter) — `counter` is
+ * the caller's env-step count (PongEnv2PBatch passes its own) — so the draw needs nothing from
+ * memory and overlaps the state loads; serves[i] is then neither read nor written. */
 int pm_env_step(const pm_env_params* p, const pm_env_state* s, const int8_t* aA, const int8_t* aB, float* obsA,
                 float* obsB, float* rA, float* rB, uint8_t* done, float* term_obsA, float* term_obsB,
-                int32_t autoreset, const double* inject, int32_t inject_cap, uint64_t seed, int32_t* status,
-                int32_t n, void* stream);
+                int32_t autoreset, const double* inject, int32_t inject_cap, uint64_t seed, uint64_t counter,
+                int32_t* status, int32_t n, void* stream);
 
 /* collide_sphere_with_moving_plane (envs/physics.py:3-23) over n rows: in [n][8] =
  * (vn, vt, u, omega, e, mu, m, R) fp64, with I = (2/5)*m*R**2 supplied per row in inertia[n]
@@ -113,6 +117,14 @@ int pm_collide(const double* in, const double* inertia, double* out, int32_t n, 
 #define PM_QNET_HEAD_OFF 4672
 #define PM_QNET_EPS_OFF 5192
 #define PM_QNET_NW 9944
+/* The learner's packed exchange buffer sp->grad (float32, PM_GRAD_LEN), the one thing a sharded
+ * update all-reduces (SUM): the 520 head gradients of this shard's batch, then the episodes this
+ * shard finished in the vector step (update 0 only) and the "an update ran" flag (1 per shard, so
+ * the sum counts the ranks that trained). Every rank then applies Adam to grads / world and decays
+ * epsilon by the summed episode count. */
+#define PM_GRAD_EPISODES 520
+#define PM_GRAD_UPDATED 521
+#define PM_GRAD_LEN 528
 
 #define PM_FOLD_EVAL 0        /* NoisyLinear eval mode: W = mu                          (qnet.py:47-49) */
 #define PM_FOLD_TRAIN 1       /* train mode with the block's epsilon buffers: mu+sigma*eps (qnet.py:44-46) */
@@ -517,13 +529,16 @@ int pm_selfplay_step_multi(const pm_selfplay* sp, int32_t updates, void* stream)
  *     loaded, e.g. torch's bundled librccl.so, so a single RCCL instance serves both).
  *   pm_comm_unique_id: rank 0 creates the 128-byte id; the caller broadcasts it to every rank.
  *   pm_comm_init: collective over nranks processes (ncclCommInitRank on the current device).
- *   pm_comm_allreduce_f32: in-place SUM all-reduce of n floats on `stream`. */
+ *   pm_comm_allreduce_f32: in-place SUM all-reduce of n floats on `stream`.
+ *   pm_comm_info: the communicator's own view of the group, from RCCL itself (ncclCommCount,
+ *     ncclCommUserRank, ncclCommCuDevice): a caller proves a sharded run really spans N ranks. */
 #define PM_COMM_ID_BYTES 128
 typedef struct pm_comm pm_comm;
 int pm_comm_unique_id(const char* rccl_path, uint8_t* id);
 int pm_comm_init(const char* rccl_path, const uint8_t* id, int32_t nranks, int32_t rank, pm_comm** out);
 int pm_comm_allreduce_f32(pm_comm* comm, float* buf, int64_t n, void* stream);
 int pm_comm_destroy(pm_comm* comm);
+int pm_comm_info(const pm_comm* comm, int32_t* nranks, int32_t* rank, int32_t* device);
 /* One sharded DQN vector step with `updates` updates (sp->world == comm ranks, fuse_apply 0):
  * actenv; per update u: [resample (u > 0)] + learn_ex (u = 0 with the next step's side-A act) +
  * all-reduce of sp->grad + apply_ex; commit when updates > 1. Same contract as step_overlap

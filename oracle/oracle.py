@@ -706,6 +706,7 @@ def adam_step(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
 # Restatement of the counter-based generator libpongmi draws from (Philox4x32-10, Salmon et al.
 # SC'11), so tests can replay the device's serves / epsilon draws / PER uniforms / noise.
 TAG_SERVE, TAG_ACT, TAG_OPP, TAG_NOISE_ACT, TAG_PER, TAG_NOISE_TRAIN = 1, 2, 3, 4, 5, 6
+TAG_SERVE_STEP = 9
 _M0, _M1, _W0, _W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
 
 
@@ -747,11 +748,18 @@ def normal_f32(a, b):
     return (r * np.cos(np.float32(6.28318530717958647692) * u2)).astype(np.float32)
 
 
-def philox_serve(params_dict, i, nserve, seed):
-    """The device's production serve (pm_dev.h philox_serve) restated: arrays i, nserve."""
+def philox_serve(params_dict, i, nserve, seed, step=None):
+    """The device's production serve (pm_dev.h serve_draw) restated: arrays i, nserve. With `step`
+    (K1's step-keyed stream, ABI 15: pm_env_step's counter) the key is (i, TAG_SERVE_STEP, step lo,
+    step hi) and nserve is ignored."""
     p = params_dict
-    r0 = philox(i, TAG_SERVE, nserve, 0, seed)
-    r1 = philox(i, TAG_SERVE | 0x100, nserve, 0, seed)
+    if step is None:
+        r0 = philox(i, TAG_SERVE, nserve, 0, seed)
+        r1 = philox(i, TAG_SERVE | 0x100, nserve, 0, seed)
+    else:
+        lo, hi = int(step) & 0xFFFFFFFF, int(step) >> 32
+        r0 = philox(i, TAG_SERVE_STEP, lo, hi, seed)
+        r1 = philox(i, TAG_SERVE_STEP | 0x100, lo, hi, seed)
     speed = p["speed_lo"] + (p["speed_hi"] - p["speed_lo"]) * u53(r0[0], r0[1])
     coin = u53(r0[2], r0[3]) < 0.5
     u = u53(r1[0], r1[1])

@@ -35,6 +35,9 @@ struct Rccl {
     ncclResult_t (*all_reduce)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
+    ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
+    ncclResult_t (*comm_user_rank)(const ncclComm_t, int*) = nullptr;
+    ncclResult_t (*comm_device)(const ncclComm_t, int*) = nullptr;
 };
 
 int bind(const char* path, Rccl& r) {
@@ -48,6 +51,9 @@ int bind(const char* path, Rccl& r) {
     r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
     r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    r.comm_count = (decltype(r.comm_count))dlsym(h, "ncclCommCount");
+    r.comm_user_rank = (decltype(r.comm_user_rank))dlsym(h, "ncclCommUserRank");
+    r.comm_device = (decltype(r.comm_device))dlsym(h, "ncclCommCuDevice");
     PM_REQUIRE(r.get_unique_id && r.comm_init_rank && r.all_reduce && r.comm_destroy && r.error_string, PM_E_COMM,
                "pm_comm: %s lacks the ncclGetUniqueId / ncclCommInitRank / ncclAllReduce / ncclCommDestroy / "
                "ncclGetErrorString symbols",
@@ -108,6 +114,22 @@ extern "C" int pm_comm_destroy(pm_comm* c) {
     return PM_OK;
 }
 
+// The group as RCCL itself reports it (not the numbers the caller passed to pm_comm_init).
+extern "C" int pm_comm_info(const pm_comm* c, int32_t* nranks, int32_t* rank, int32_t* device) {
+    PM_REQUIRE(c && c->comm, PM_E_ARG, "pm_comm_info: null communicator");
+    PM_REQUIRE(c->rccl.comm_count && c->rccl.comm_user_rank && c->rccl.comm_device, PM_E_COMM,
+               "pm_comm_info: RCCL lacks ncclCommCount / ncclCommUserRank / ncclCommCuDevice");
+    int n = 0, r = 0, d = 0;
+    ncclResult_t e = c->rccl.comm_count(c->comm, &n);
+    if (!e) e = c->rccl.comm_user_rank(c->comm, &r);
+    if (!e) e = c->rccl.comm_device(c->comm, &d);
+    PM_REQUIRE(e == 0, PM_E_COMM, "ncclCommCount / UserRank / CuDevice: %s", c->rccl.error_string(e));
+    if (nranks) *nranks = n;
+    if (rank) *rank = r;
+    if (device) *device = d;
+    return PM_OK;
+}
+
 extern "C" int pm_comm_allreduce_f32(pm_comm* c, float* buf, int64_t n, void* stream) {
     PM_REQUIRE(c && c->comm && buf && n >= 0, PM_E_ARG, "pm_comm_allreduce_f32: null comm / buffer");
     if (n == 0) return PM_OK;
@@ -125,7 +147,7 @@ extern "C" int pm_selfplay_step_sharded(const pm_selfplay* sp, pm_comm* c, int32
     PM_REQUIRE(!sp->fuse_apply, PM_E_ARG, "pm_selfplay_step_sharded: the learner fuses its apply (world 1)");
     PM_REQUIRE(sp->world == c->nranks, PM_E_ARG, "pm_selfplay_step_sharded: learner world %d vs communicator %d",
                sp->world, c->nranks);
-    const int32_t n_grad = PM_QNET_NHEAD + 8;  // sp->grad: head gradients, finished episodes, updated flag, pad
+    const int32_t n_grad = PM_GRAD_LEN;  // sp->grad: head gradients, finished episodes, updated flag, pad
     int rc = pm_selfplay_actenv(sp, stream);
     for (int u = 0; !rc && u < updates; ++u) {
         const int32_t mode = updates == 1 ? (PM_UPD_FIRST | PM_UPD_LAST) : (u == 0 ? PM_UPD_FIRST : 0);

@@ -64,7 +64,8 @@ static __device__ unsigned long long pm_diag_blk[8][4096];
 namespace pm {
 
 // ----------------------------------------------------------------------------- RNG
-enum : uint32_t { TAG_SERVE = 1, TAG_ACT = 2, TAG_OPP = 3, TAG_NOISE_ACT = 4, TAG_PER = 5, TAG_NOISE_TRAIN = 6, TAG_NOISE_RNN = 7, TAG_SEQ = 8 };
+enum : uint32_t { TAG_SERVE = 1, TAG_ACT = 2, TAG_OPP = 3, TAG_NOISE_ACT = 4, TAG_PER = 5, TAG_NOISE_TRAIN = 6, TAG_NOISE_RNN = 7, TAG_SEQ = 8,
+                  TAG_SERVE_STEP = 9 };
 
 struct U4 {
     uint32_t x, y, z, w;
@@ -254,9 +255,12 @@ __device__ __forceinline__ void sincos_serve(double x, double& s, double& c) {
 struct ServeDraw {
     double speed, rad, vx, vy, spin;
 };
-__device__ __forceinline__ ServeDraw serve_draw(const pm_env_params& p, uint32_t i, uint32_t nserve, uint64_t seed) {
-    const U4 r0 = philox(i, TAG_SERVE, nserve, 0u, seed);
-    const U4 r1 = philox(i, TAG_SERVE | 0x100u, nserve, 0u, seed);
+// Counter (i, tag, c2, c3): (i, TAG_SERVE, serve number, 0) for the serve-count stream, (i,
+// TAG_SERVE_STEP, step lo, step hi) for K1's step-keyed production stream.
+__device__ __forceinline__ ServeDraw serve_draw(const pm_env_params& p, uint32_t i, uint32_t nserve, uint64_t seed,
+                                                uint32_t tag = TAG_SERVE, uint32_t c3 = 0u) {
+    const U4 r0 = philox(i, tag, nserve, c3, seed);
+    const U4 r1 = philox(i, tag | 0x100u, nserve, c3, seed);
     ServeDraw d;
     d.speed = p.speed_lo + (p.speed_hi - p.speed_lo) * u53(r0.x, r0.y);
     const bool first = u53(r0.z, r0.w) < 0.5;

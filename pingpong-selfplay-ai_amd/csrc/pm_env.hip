@@ -71,10 +71,11 @@ static __device__ unsigned long long pm_k1_diag[8][4096];
 
 // One lane per arena, one wave per SIMD at 65 536 arenas: the kernel is a single load -> tick ->
 // store pass, so its time is the serial latency of that pass. What keeps it short:
-//   - the serve counter is loaded first; the next production serve (two Philox draws + sincos) is
-//     drawn for every lane (done lanes use it) in the same scheduling region as the straight-line
-//     tick, so the two independent dependency chains interleave (drawing it ahead, under the load
-//     latency, measured slower: the draw's own chains then run alone);
+//   - the production serve (two Philox draws + sincos) is keyed by (arena, env-step counter), a
+//     kernel argument (ABI 15), so every lane draws it while its state loads are in flight: the
+//     draw no longer waits for a loaded per-arena serve counter, and that counter's 8 bytes per
+//     arena are neither read nor written (round 2 keyed it by the serve count and drew it beside the
+//     tick);
 //   - tick() is branch-free, with one shared collide path and reciprocal-multiply division;
 //   - the production reset is branch-free too: every lane forms the served arena and done lanes
 //     select it, so the state stores follow the tick directly, and the term rows of done lanes
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
                                                      float* __restrict__ rB, uint8_t* __restrict__ done,
                                                      float* __restrict__ tobsA, float* __restrict__ tobsB,
                                                      const double* __restrict__ inject, int inject_cap,
-                                                     uint64_t seed, int32_t* status, int n) {
+                                                     uint64_t seed, uint64_t ctr, int32_t* status, int n) {
     __shared__ __attribute__((aligned(16))) float lds[4][kBlock][7];
     constexpr bool DRAW = AR && !INJ;
     const int i0 = blockIdx.x * kBlock;
@@ -106,19 +107,21 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
     if (i < n) {
         int32_t ns = 0;
         ServeDraw sv{};
-        if (AR) ns = __builtin_nontemporal_load(&s.serves[i]);
+        if (INJ) ns = __builtin_nontemporal_load(&s.serves[i]);
         Arena a = load_arena(s, i);
         const int xa = aA[i], xb = aB[i];
+        // the step-keyed draw depends on no load: it runs while the state is in flight, and is
+        // pinned complete ahead of the tick (the compiler would sink it into the done lanes' path)
+        if (DRAW) {
+            sv = serve_draw(p, (uint32_t)i, (uint32_t)ctr, seed, TAG_SERVE_STEP, (uint32_t)(ctr >> 32));
+            asm volatile("" ::"v"(sv.vx), "v"(sv.vy), "v"(sv.spin), "v"(sv.rad));
+        }
 #ifdef PM_DIAG
         K1_DRAIN();
         K1_STAMP(1);
 #endif
-        if (DRAW) sv = serve_draw(p, (uint32_t)i, (uint32_t)ns, seed);
         float ra, rb;
         const int d = tick(p, a, xa, xb, ra, rb);
-        // every lane's draw is complete here, ahead of the reset (the compiler would sink it into
-        // the done lanes' path, behind the term-row stores)
-        if (DRAW) asm volatile("" ::"v"(sv.vx), "v"(sv.vy), "v"(sv.spin), "v"(sv.rad));
         K1_STAMP(2);
         observe(a, oA, oB);
         if (full_term) {
@@ -135,7 +138,6 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
             a.spin = d ? r.spin : a.spin; a.top = d ? r.top : a.top; a.bot = d ? r.bot : a.bot;
             a.sA = d ? 0 : a.sA; a.sB = d ? 0 : a.sB; a.bounces = d ? 0 : a.bounces;
             observe(a, oA, oB);
-            st_out<WT>(&s.serves[i], ns + d);
         } else if (AR && d) {  // parity mode: the injected serve of done arenas
             if (AR == 2 && tobsA) {
                 store_row7(tobsA + (size_t)i * 7, oA);
@@ -226,7 +228,7 @@ extern "C" int pm_env_reset(const pm_env_params* p, const pm_env_state* s, const
 extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const int8_t* aA, const int8_t* aB,
                            float* obsA, float* obsB, float* rA, float* rB, uint8_t* done, float* term_obsA,
                            float* term_obsB, int32_t autoreset, const double* inject, int32_t inject_cap,
-                           uint64_t seed, int32_t* status, int32_t n, void* stream) {
+                           uint64_t seed, uint64_t counter, int32_t* status, int32_t n, void* stream) {
     PM_REQUIRE(n >= 0, PM_E_SIZE, "pm_env_step: n=%d", n);
     if (n == 0) return PM_OK;
     PM_REQUIRE(p && state_ok(s), PM_E_ARG, "pm_env_step: null params/state");
@@ -245,7 +247,7 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
          {k_env_step<2, false, true>, k_env_step<2, true, true>}}};
     pm_launch(PM_TIMER_ENV_STEP, kernels[k1_write_through(n)][autoreset][inject != nullptr], dim3(pm_blocks(n, kBlock)),
               dim3(kBlock), pm_stream(stream), *p, *s, aA, aB, obsA, obsB, rA, rB, done, term_obsA, term_obsB, inject,
-              inject_cap, seed, status, n);
+              inject_cap, seed, counter, status, n);
     PM_LAUNCHED("k_env_step");
     return PM_OK;
 }

@@ -50,7 +50,8 @@ namespace {
 constexpr int kBlock = 256;
 static_assert(kBlock == kRowBlock, "row staging assumes kRowBlock-thread blocks");
 constexpr int kLearn = 1024;              // k_learn / k_adam / k_prepare block
-constexpr int kGradN = PM_QNET_NHEAD;     // grad[520] = finished episodes, grad[521] = updated flag
+constexpr int kGradN = PM_GRAD_EPISODES;  // grad[kGradN] = finished episodes, grad[kGradN + 1] = updated flag
+static_assert(PM_GRAD_EPISODES == PM_QNET_NHEAD && PM_GRAD_UPDATED == kGradN + 1 && PM_GRAD_LEN >= kGradN + 2, "grad layout");
 constexpr uint32_t kHashEmpty = 0xFFFFFFFFu;
 
 __device__ __forceinline__ bool learner_active(const pm_selfplay& sp) {

@@ -24,6 +24,7 @@ PM_QNET_NHEAD = 520
 PM_QNET_HEAD_OFF = 4672
 PM_QNET_EPS_OFF = 5192
 PM_QNET_NW = 9944
+PM_GRAD_EPISODES, PM_GRAD_UPDATED, PM_GRAD_LEN = 520, 521, 528
 PM_QNET_PLAIN = 4936
 PM_RNN_NP = 192012
 PM_RNN_NPARAM = 174984
@@ -34,7 +35,7 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 13
+ABI_VERSION = 15
 PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_N = 0, 1, 2, 3, 4
 
 
@@ -107,7 +108,7 @@ _SIGS = {
     "pm_env_reset": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_u64, c_void_p, c_void_p, c_void_p, c_i32,
                              c_void_p]),
     "pm_env_step": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_u64, c_void_p, c_i32, c_void_p]),
+                            c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_u64, c_u64, c_void_p, c_i32, c_void_p]),
     "pm_collide": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_qnet_fold": (c_i32, [c_void_p, c_void_p, c_i32, c_u64, c_u64, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_qnet_q": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
@@ -159,6 +160,7 @@ _SIGS = {
     "pm_comm_init": (c_i32, [ctypes.c_char_p, c_void_p, c_i32, c_i32, ctypes.POINTER(c_void_p)]),
     "pm_comm_allreduce_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p]),
     "pm_comm_destroy": (c_i32, [c_void_p]),
+    "pm_comm_info": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "pm_selfplay_step_sharded": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_rnn_selfplay_step_sharded": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_rnn_selfplay_step_sharded_overlap": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p, c_void_p]),

@@ -113,6 +113,16 @@ class NativeComm:
         _lib.check(lib.pm_comm_init(path, buf.data_ptr(), self.world, self.rank, ctypes.byref(h)), "pm_comm_init")
         self.handle = h
 
+    def info(self):
+        """(nranks, rank, device) as RCCL reports them for this communicator (pm_comm_info)."""
+        import ctypes
+
+        from . import _lib
+        n, r, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self._lib.pm_comm_info(self.handle, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d)),
+                   "pm_comm_info")
+        return n.value, r.value, d.value
+
     @property
     def pm_comm(self):
         return self.handle

@@ -102,7 +102,10 @@ class PongEnv2PBatch:
     same kernel; obs then holds the post-reset observation and info['term_obsA'/'term_obsB'] the
     observation the step returned before the reset (what the reference pushes to replay as next
     state). autoreset="done" writes the term rows of finished arenas only (the others keep old
-    contents: next state = where(done, term_obs, obs)), which saves 56 B of stores per env-step."""
+    contents: next state = where(done, term_obs, obs)), which saves 56 B of stores per env-step.
+    Production (Philox) serves of autoreset arenas are keyed by (arena, self.counter), the number
+    of step() calls so far (ABI 15); a parity-mode serve table is indexed by the per-arena serve
+    count instead, as pm_env_reset does."""
 
     def __init__(self, n, device="cuda", seed=0, serve_table=None, autoreset=False, **env_kw):
         self.lib = _lib.load()
@@ -113,6 +116,7 @@ class PongEnv2PBatch:
         self.cfg = env_config(**env_kw)
         self.params = env_params(**env_kw)
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.counter = 0  # env steps taken: the Philox key of each step's autoreset serves
         if autoreset not in (False, True, 0, 1, "done"):
             raise ValueError(f"autoreset must be False, True or 'done', got {autoreset!r}")
         self.autoreset = 2 if autoreset == "done" else int(bool(autoreset))
@@ -156,7 +160,8 @@ class PongEnv2PBatch:
         check(self.lib.pm_env_step(ctypes_ref(self.params), ctypes_ref(self.state), ptr(aA), ptr(aB), ptr(self.obsA),
                                    ptr(self.obsB), ptr(self.rA), ptr(self.rB), ptr(self.done), ptr(self.term_obsA),
                                    ptr(self.term_obsB), self.autoreset, ptr(self.inject), self.inject_cap,
-                                   self.seed, None, self.n, stream_ptr()), "pm_env_step")
+                                   self.seed, self.counter, None, self.n, stream_ptr()), "pm_env_step")
+        self.counter += 1
         info = {}
         if self.autoreset:
             info = {"term_obsA": self.term_obsA, "term_obsB": self.term_obsB}

@@ -29,7 +29,8 @@ import numpy as np
 import torch
 
 from . import _lib, checkpoint
-from ._lib import PM_QNET_NHEAD, PM_QNET_NP, PM_QNET_NW, PM_TRANS_F, check, ptr, stream_ptr
+from ._lib import (PM_GRAD_EPISODES, PM_GRAD_LEN, PM_GRAD_UPDATED, PM_QNET_NHEAD, PM_QNET_NP, PM_QNET_NW,  # noqa: F401
+                   PM_TRANS_F, check, ptr, stream_ptr)
 from .dist import shard_seeds, splitmix64  # noqa: F401
 from .env import env_config, env_params
 from .qnet import HEAD_KEYS, fold, pack_state_dict, unpack_state_dict
@@ -45,6 +46,39 @@ def act_chunk(p, rows=96, cap=4096, lo=256):
     while c < cap and c * p < rows:
         c *= 2
     return c
+
+
+def sharded_vector_step(L, allreduce, updates):
+    """One vector step of a (sharded) learner as its launch sequence: the Python twin of
+    pm_selfplay_step_sharded (csrc/pm_comm.cpp), for an `allreduce` callable on the packed buffer
+    (torch.distributed, gloo in the CPU tests) instead of the library's RCCL communicator.
+
+      overlap: [act(A) if the opponents' actions are stale] + actenv, else rollout;
+      per update u: [resample (u > 0)] + learn_ex(u = 0: FIRST (| LAST when U = 1), with the next
+        step's side-A act when overlapped) + allreduce(L.grad) + apply_ex(same mode);
+      U > 1: commit.
+
+    L.grad is the packed exchange buffer (include/pongmi.h PM_GRAD_*): [0, 520) the shard's head
+    gradients, [PM_GRAD_EPISODES] its finished episodes (update 0), [PM_GRAD_UPDATED] 1 if it trained;
+    after the SUM every rank's apply uses grads / world and decays epsilon by the summed episodes.
+    `allreduce` None: a single learner (world 1, unfused apply). `L` needs only the learner's launch
+    methods, so the CPU tests drive this same sequence with oracle-backed shards."""
+    if L.overlap:
+        if not L._aA_ready:
+            L.act(_lib.PM_ACT_A)
+        L.actenv()
+    else:
+        L.rollout()
+    for u in range(updates):
+        mode = (_lib.PM_UPD_FIRST | (_lib.PM_UPD_LAST if updates == 1 else 0)) if u == 0 else 0
+        if u:
+            L.resample()
+        L.learn_ex(mode, act_next=L.overlap and u == 0)
+        if allreduce is not None:
+            allreduce(L.grad)
+        L.apply_ex(mode)
+    if updates > 1:
+        L.commit()
 
 
 class SelfPlayLearner:
@@ -97,7 +131,7 @@ class SelfPlayLearner:
         self.per_work = torch.zeros(max(self.lib.pm_per_work_bytes(self.cap), 256), dtype=torch.uint8, device=dev)
         self.idx = torch.zeros(self.batch, dtype=torch.int64, device=dev)
         self.isw = torch.zeros(self.batch, **f32)
-        self.grad = torch.zeros(PM_QNET_NHEAD + 8, **f32)
+        self.grad = torch.zeros(PM_GRAD_LEN, **f32)  # the packed exchange buffer (include/pongmi.h PM_GRAD_*)
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
         self.hfeat = torch.zeros((2 * self.batch + 1, 80), **f32)  # + the push-row hand-off rows and flag
         self.learn_heads = torch.zeros(3 * 264, **f32)
@@ -209,21 +243,7 @@ class SelfPlayLearner:
             check(self.lib.pm_selfplay_step_multi(ctypes.byref(self.sp), U, stream_ptr()), "pm_selfplay_step_multi")
             self._aA_ready = True
             return
-        if self.overlap:
-            if not self._aA_ready:
-                self.act(_lib.PM_ACT_A)
-            self.actenv()
-        else:
-            self.rollout()
-        for u in range(U):
-            mode = _lib.PM_UPD_FIRST if u == 0 else 0
-            if u:
-                self.resample()
-            self.learn_ex(mode, act_next=self.overlap and u == 0)
-            if self.world > 1:
-                self.allreduce(self.grad)
-            self.apply_ex(mode)
-        self.commit()
+        sharded_vector_step(self, self.allreduce if self.world > 1 else None, U)
 
     def step(self):
         """One vector step (n env-steps on this rank) and its `updates_per_step` updates. With
@@ -236,25 +256,16 @@ class SelfPlayLearner:
         if self.updates_per_step > 1:
             self._step_multi()
             return
+        if self.world > 1:
+            sharded_vector_step(self, self.allreduce, 1)
+            return
         if not self.overlap:
-            if self.world == 1:
-                check(self.lib.pm_selfplay_step(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step")
-                return
-            self.rollout()
-            self.learn()
-            self.allreduce(self.grad)  # one RCCL all-reduce per update: 520 grads + counters
-            self.apply()
+            check(self.lib.pm_selfplay_step(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step")
             return
         if not self._aA_ready:
             self.act(_lib.PM_ACT_A)
-        if self.world == 1:
-            check(self.lib.pm_selfplay_step_overlap(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step_overlap")
-            self._aA_ready = True
-            return
-        self.actenv()
-        self.learn(act_next=True)
-        self.allreduce(self.grad)
-        self.apply()
+        check(self.lib.pm_selfplay_step_overlap(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step_overlap")
+        self._aA_ready = True
 
     # ------------------------------------------------------------------ state readout (syncs)
     def counters(self):
@@ -318,4 +329,5 @@ class SelfPlayLearner:
 
 
 HEAD_NAMES = HEAD_KEYS
-__all__ = ["SelfPlayLearner", "splitmix64", "HEAD_NAMES", "PM_QNET_NP"]
+__all__ = ["SelfPlayLearner", "sharded_vector_step", "splitmix64", "HEAD_NAMES", "PM_QNET_NP", "PM_GRAD_EPISODES",
+           "PM_GRAD_UPDATED", "PM_GRAD_LEN"]

@@ -38,7 +38,7 @@ def test_struct_layouts_and_constants_match_header():
         assert L.pm_sizeof(which) == __import__("ctypes").sizeof(cls)
     hdr = open(os.path.join(ROOT, "include", "pongmi.h")).read()
     for k in ("PM_QNET_NP", "PM_QNET_NHEAD", "PM_QNET_HEAD_OFF", "PM_QNET_EPS_OFF", "PM_QNET_NW", "PM_TRANS_F",
-              "PM_MAX_BATCH"):
+              "PM_MAX_BATCH", "PM_GRAD_EPISODES", "PM_GRAD_UPDATED", "PM_GRAD_LEN"):
         v = int(re.search(rf"#define {k} (\d+)", hdr).group(1))
         assert getattr(_lib, k) == v, k
 
@@ -46,7 +46,7 @@ def test_struct_layouts_and_constants_match_header():
 def test_entry_points_reject_bad_arguments_without_a_gpu():
     from pongmi import _lib
     L = _lib.load()
-    assert L.pm_env_step(None, None, None, None, None, None, None, None, None, None, None, 0, None, 0, 0, None, 4,
+    assert L.pm_env_step(None, None, None, None, None, None, None, None, None, None, None, 0, None, 0, 0, 0, None, 4,
                          None) == -1
     assert L.pm_qnet_fold(None, None, 7, 0, 0, None, None, 1, None) == -1
     assert b"mode" in L.pm_last_error()

@@ -128,8 +128,9 @@ def test_autoreset_done_rows_only():
 
 def test_autoreset_serves_match_philox_restatement(orc):
     """Production autoreset serves of pm_env_step (the branch-free reset): every arena that
-    finishes in a step is served Philox(seed; i, serves[i]) as the oracle restates it (cos/sin within
-    1 ulp of libm), serves[i] counts its resets, and every other arena ticks as the C oracle does."""
+    finishes in step t is served Philox(seed; i, TAG_SERVE_STEP, t) as the oracle restates it
+    (cos/sin within 1 ulp of libm), serves[] is left alone (ABI 15: the step-keyed draw reads no
+    counter), and every other arena ticks as the C oracle does."""
     from pongmi.env import PongEnv2PBatch
 
     n = 65536
@@ -153,8 +154,9 @@ def test_autoreset_serves_match_philox_restatement(orc):
         for k in STATE_ORDER:
             assert np.array_equal(st[k][~d], arr[k][~d]), (t, k)
         idx = np.nonzero(d)[0]
-        assert np.array_equal(st["serves"], before["serves"] + d)
-        vx, vy, sp = orc.philox_serve(p, idx, before["serves"][idx], 77)
+        assert np.array_equal(st["serves"], before["serves"])
+        assert env.counter == t + 1
+        vx, vy, sp = orc.philox_serve(p, idx, None, 77, step=t)
         np.testing.assert_allclose(st["vx"][idx], vx, rtol=4e-16, atol=1e-18)
         np.testing.assert_allclose(st["vy"][idx], vy, rtol=4e-16, atol=1e-18)
         assert np.array_equal(st["spin"][idx], sp)
@@ -181,10 +183,10 @@ def test_env_empty_and_bad_arguments():
         PongEnv2PBatch(4, autoreset="sometimes")
     with pytest.raises(_lib.PongmiError):
         _lib.check(_lib.load().pm_env_step(None, None, None, None, None, None, None, None, None, None, None, 0, None,
-                                           0, 0, None, 4, None))
+                                           0, 0, 0, None, 4, None))
     with pytest.raises(_lib.PongmiError):
         _lib.check(_lib.load().pm_env_step(None, None, None, None, None, None, None, None, None, None, None, 0, None,
-                                           0, 0, None, -1, None))
+                                           0, 0, 0, None, -1, None))
 
 
 def test_production_serves_match_philox_restatement(orc):

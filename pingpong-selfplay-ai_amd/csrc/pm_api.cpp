@@ -31,15 +31,30 @@ struct LaunchTimer {
 LaunchTimer g_timer[PM_TIMER_N];
 }  // namespace
 
+// The next armed slot of `kernel` for a launch on the current device. A launch on another device than
+// the one the timer was armed on stays untimed (its events belong to that device), and the slot
+// stays armed for the next launch there.
 bool pm_timer_take(int kernel, hipEvent_t* start, hipEvent_t* stop) {
     LaunchTimer& t = g_timer[kernel];
     if (t.armed == 0) return false;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != t.device) return false;
     const int slot = (t.head + t.pending) % kTimerSlots;
     --t.armed;
     ++t.pending;
     *start = t.ev[slot][0];
     *stop = t.ev[slot][1];
     return true;
+}
+
+// A timed launch that failed to enqueue: its slot goes back to armed (its events were never
+// recorded, so a pm_timer_read of it would fail and shift every later read by one).
+void pm_timer_release(int kernel) {
+    LaunchTimer& t = g_timer[kernel];
+    if (t.pending > 0) {
+        --t.pending;
+        ++t.armed;
+    }
 }
 
 extern "C" int pm_timer_arm(int32_t kernel) {

@@ -35,14 +35,17 @@ static inline unsigned pm_blocks(int64_t n, int per) { return (unsigned)((n + pe
 // Launch timing (pm_timer_arm / pm_timer_read, pm_api.cpp): an armed kernel's next launch goes
 // through hipExtLaunchKernel with the timer's events; every other launch is a plain one.
 bool pm_timer_take(int kernel, hipEvent_t* start, hipEvent_t* stop);
+void pm_timer_release(int kernel);
 
 template <typename F, typename... Args>
 inline void pm_launch(int timer, F kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
     hipEvent_t t0, t1;
-    if (pm_timer_take(timer, &t0, &t1))
+    if (pm_timer_take(timer, &t0, &t1)) {
         hipExtLaunchKernelGGL(kernel, grid, block, 0, st, t0, t1, 0, args...);
-    else
+        if (hipPeekAtLastError() != hipSuccess) pm_timer_release(timer);  // never enqueued: not pending
+    } else {
         hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+    }
 }
 
 // ---------------------------------------------------------------- diagnostic stamps (PM_DIAG builds only)

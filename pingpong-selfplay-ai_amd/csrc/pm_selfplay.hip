@@ -665,10 +665,16 @@ __device__ __forceinline__ void push_rows_fwd(const pm_selfplay& sp, const float
 // 2B = ctrl.step + 1. Publication follows the cross-CU rules for write-through hand-offs: every
 // payload store and the flag store sc1, every storing wave waits vmcnt(0), a workgroup barrier,
 // then one lane stores the flag; the learner polls the flag with sc1 loads from one lane, joins a
-// barrier, and reads the payload with sc1 loads only. The learner increments ctrl.step only after
-// this point, so the token names this update. Block 1 waits for nothing, so it always completes;
-// the poll is bounded anyway (kPushPollMax, ~20 ms): a flag that never came sets ctrl.status bit 0,
-// which the host reports as an error (pongmi.selfplay.SelfPlayLearner.check_status).
+// barrier, and reads the payload with sc1 loads only. Block 1 reads the control block unsynchronised,
+// so in a FIRST update it ALWAYS publishes its token (at once, with no rows, when the update does not
+// train) and a learner that commits the control block in this launch (fused apply) waits for that
+// token before the commit even when it needed no rows: block 1 can then never see the next step's
+// control block and publish the token the NEXT launch's learner polls for with rows built from this
+// step's push range. Block 1 waits for nothing, so it always completes; the poll is
+// bounded anyway (kPushPollMax, ~20 ms): a flag that never came sets ctrl.status bit 0, which the
+// host reports as an error (pongmi.selfplay.SelfPlayLearner.check_status), and an update whose push
+// rows never came is void: it trains nothing (no scatter, gradients, Adam or train-step count), as
+// an update before the replay holds a batch.
 constexpr int kPushPollMax = 20000;
 constexpr int PM_CTRL_PUSH_TIMEOUT = 1;
 __device__ __forceinline__ bool push_handoff(int mode, bool train) { return (mode & PM_UPD_FIRST) && train; }
@@ -676,6 +682,20 @@ __device__ __forceinline__ int* push_flag(const pm_selfplay& sp) {
     return reinterpret_cast<int*>(sp.hfeat + (size_t)2 * sp.batch * 80);
 }
 __device__ __forceinline__ int push_token(const pm_ctrl& cs) { return (int)((uint32_t)cs.step + 1u); }
+
+// One lane polls for block 1's token of this update (bounded). false: it never came (status bit 0 set).
+__device__ __forceinline__ bool push_wait(const pm_selfplay& sp, const pm_ctrl& cs) {
+    const int* flag = push_flag(sp);
+    const int tok = push_token(cs);
+    for (int it = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tok; ++it) {
+        if (it == kPushPollMax) {
+            sp.ctrl->status = cs.status | PM_CTRL_PUSH_TIMEOUT;
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
 
 struct PushFwdSmem {
     float lw[kLwFloats];
@@ -693,7 +713,10 @@ __device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, 
     __builtin_amdgcn_sched_barrier(0);
     const pm_ctrl cs = *sp.ctrl;
     const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
-    if (!push_handoff(mode, s_after >= B)) return;  // block-uniform: the learner does not wait
+    if (!push_handoff(mode, s_after >= B)) {  // block-uniform: no rows to compute
+        if ((mode & PM_UPD_FIRST) && t == 0) st_out<true>(push_flag(sp), push_token(cs));
+        return;
+    }
     const bool ip = t < B && push_of(sp, cs.pos, cs.size, cs.max_prio).covers(id);
     const unsigned long long m = __ballot(ip);
     if (ip) sm.plist[wv * 64 + __popcll(m & ((1ull << lane) - 1ull))] = t;
@@ -728,6 +751,7 @@ struct LearnSmem {
     long long ctot[6];           // their sums (phase 1)
     int plist[PM_MAX_BATCH];     // samples whose row is in this step's push range, per wave slot
     int pcnt[16];
+    int void_upd;                // the push-row hand-off timed out: this update trains nothing
     ApplySmem ap;
 };
 
@@ -810,8 +834,9 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
 #pragma unroll
         for (int k = 0; k < 6; ++k) part[k] += sp.partials[(size_t)b * 8 + k];
     const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
-    const bool train = s_after >= B;
-    const bool act = train && t < B;
+    bool train = s_after >= B;  // cleared (block-uniformly) if the push rows never arrive: a void update
+    bool act = train && t < B;
+    if (t == 0) sm.void_upd = 0;
     // fused: the optimizer's scalar prologue on waves with slack in this load phase (they are not
     // on the dependent idx -> replay-row path of waves 0-3): the Adam bias corrections (two fp64
     // pow) on the last thread, both NoisyNet draws of the apply on the upper half of the block
@@ -869,6 +894,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
 
     // ---- phase 1: counters; the batch forward on the matrix cores (one 32-row tile per wave)
     long long ep_fin = 0;
+    bool waited = false;  // block-uniform: the push-row token was seen
     if (t < 6) {
         long long s = 0;
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][t];
@@ -885,18 +911,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         for (int w = 0; w < 4; ++w) pre[w + 1] = pre[w] + sm.pcnt[w];  // B <= 256: waves 0..3
         const int np = pre[4];
         if (np > 0 && push_handoff(mode, train)) {  // block-uniform: block 1 computes them
-            if (t == 0) {
-                const int* flag = push_flag(sp);
-                const int tok = push_token(cs);
-                int it = 0;
-                while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tok) {
-                    if (++it == kPushPollMax) {
-                        c->status = cs.status | PM_CTRL_PUSH_TIMEOUT;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
+            waited = true;
+            if (t == 0 && !push_wait(sp, cs)) sm.void_upd = 1;
             __syncthreads();
             PM_STAMP(54);
             const float* pay = sp.hfeat + (size_t)B * 80;
@@ -914,6 +930,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     for (int w = 1; w < 16; ++w) wmax = fmaxf(wmax, sm.red[w][0]);
     __syncthreads();
     PM_STAMP(2);
+    if (sm.void_upd) train = act = false;  // block-uniform: the hand-off timed out
     ep_fin = sm.ctot[0];
     if (first && t == 0) {  // rollout bookkeeping (:245-249)
         c->ep_step = ep_fin;
@@ -1093,6 +1110,10 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         }
     }
     PM_STAMP(6);
+    if (sp.fuse_apply && first && !waited) {  // block 1 read the control block before this launch commits it
+        if (t == 0) push_wait(sp, cs);
+        __syncthreads();
+    }
     if (sp.fuse_apply) apply_finish(sp, sm.ap, cs, mode);  // unsharded: Adam ran with the gradients (phase 4)
     PM_STAMP(7);
 }

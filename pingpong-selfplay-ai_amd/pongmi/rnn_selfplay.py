@@ -207,7 +207,20 @@ class RNNSelfPlayLearner:
               "pm_rnn_selfplay_env")
 
     def rollout(self):
-        """fold + act + env + sequence store + batch sample (no update)."""
+        """fold + act + env + sequence store + batch sample (no update). After an overlapped step the
+        opponents already acted for the current observations (speculatively, into buffer _cur): acting
+        for them again would advance their LSTM state twice on one observation, so the rollout then
+        acts for modelB only (the speculative act redone first if the opponents changed since)."""
+        if self._spec:
+            if self._stale:
+                self._opp_buffers(1 - self._cur, self._cur)
+                check(self.lib.pm_rnn_selfplay_act_part(ctypes.byref(self.sp), _lib.PM_ACT_A, stream_ptr()),
+                      "pm_rnn_selfplay_act_part")
+                self._opp_buffers(None, self._cur)
+                self._stale = False
+            self.act_part(_lib.PM_ACT_B)
+            self.env_step()
+            return
         self._spec = False
         check(self.lib.pm_rnn_selfplay_rollout(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), stream_ptr()),
               "pm_rnn_selfplay_rollout")

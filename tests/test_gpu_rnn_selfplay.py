@@ -309,6 +309,43 @@ def test_rnn_overlapped_step_is_bitwise_identical(golden, U):
     assert A.learner.stats()["steps"] == B.learner.stats()["steps"] > 0
 
 
+@pytest.mark.parametrize("change", [None, "modelA"])
+def test_rnn_split_step_after_overlapped_steps(golden, change):
+    """The generation controller's save-boundary step (rollout + updates, pongmi.generations
+    RNNGenerations._step) between overlapped steps, optionally after a modelA swap: the opponents'
+    (h, c) and actions, modelB's state and every counter equal an uninterrupted plain run (the
+    opponents' LSTM must advance exactly once per observation: ADVICE r2)."""
+    kw = dict(n=1024, n_pool=2, epsilon=0.3, memory_size=2000, min_episodes_for_training_start=1, seed=9)
+    A = _learner(golden, overlap=True, **kw)
+    B = _learner(golden, overlap=False, **kw)
+    for k in range(30):
+        if change and k == 17:
+            for L in (A, B):
+                L.set_modelA(_rnn_sd(305))
+        B.step()
+        if k in (12, 17, 18):  # the controller's split step (save boundary)
+            A.rollout()
+            A.learner.update()
+        else:
+            A.step()
+    sa, sb = _snap(A), _snap(B)
+    for key in sa:
+        if key in ("hA", "cA"):
+            continue  # A's opponents are one (speculative) act ahead after an overlapped step
+        if key == "ctrl":
+            assert sa[key] == sb[key]
+        elif isinstance(sa[key], torch.Tensor):
+            assert torch.equal(sa[key], sb[key]), key
+        else:
+            assert np.array_equal(sa[key], sb[key]), key
+    from pongmi import _lib
+    B.act_part(_lib.PM_ACT_A)  # B's opponents act for the current observations, as A's speculative act did
+    torch.cuda.synchronize()
+    assert torch.equal(A.hA, B.hA) and torch.equal(A.cA, B.cA) and torch.equal(A.aA, B.aA)
+    assert torch.equal(A.learner.params, B.learner.params) and torch.equal(A.trans, B.trans)
+    assert A.learner.stats()["steps"] == B.learner.stats()["steps"] > 0
+
+
 def test_rnn_production_step_equals_plain_at_full_size(golden):
     """configs[4] at its full size (the bench's workload: 32 768 arenas, pool 4, sequence buffer
     200 000, DRQN 64 x 8 every step once the buffer holds enough episodes): the overlapped production

@@ -437,6 +437,9 @@ def main():
     ap.add_argument("--updates-per-step", type=int, default=1,
                     help="dqn: PER updates of `batch` per vector step (U; SURVEY 8d: 1 default, 64 the stress "
                          "variant; the reference's own ratio is one update per env step, i.e. U = arenas)")
+    ap.add_argument("--no-learn-multi", action="store_true",
+                    help="dqn, U > 1: updates 1..U-1 as three launches each (resample, batch forward, learn) "
+                         "instead of one single-workgroup launch for all of them (k_learn_multi)")
     ap.add_argument("--weights", choices=("reference", "random"), default="reference",
                     help="reference: model5-5_fault.pth's QNet weights (tests/golden/qnet.npz) for modelB and modelA "
                          "(SURVEY 8d); random: random-init nets of the reference architecture")
@@ -476,7 +479,7 @@ def main():
     sdB, sdA, pool, wdesc = bench_nets(args.weights, args.pool)
     L = SelfPlayLearner(ENV_KW, args.arenas, sdB, sdA, pool, batch=args.batch, memory_size=args.memory,
                         epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce,
-                        overlap=not args.no_overlap, updates_per_step=U)
+                        overlap=not args.no_overlap, updates_per_step=U, learn_multi=not args.no_learn_multi)
 
     def one_step(ev=None):
         # the production path: the overlapped vector step (L.step); an instrumented step is the same
@@ -549,6 +552,7 @@ def main():
         }
         if U > 1:
             out["us_per_update"] = round(dt / args.steps / U * 1e6, 3)
+            out["learn_multi"] = L.frow is not None
         if world == 1:
             out["act_full_roofline"] = time_act_full(L)
             out["env_step_roofline"] = time_env_step(args.arenas)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 15
+#define PM_ABI_VERSION 16
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -436,6 +436,14 @@ typedef struct pm_selfplay {
                                 observations (ABI 11), computed ahead by the side-A act work (the learner
                                 launch's extra blocks, pm_selfplay_act_part A / ALL); pm_selfplay_actenv
                                 then evaluates only the heads. NULL: actenv computes the features */
+    float *frow;             /* nullable [cap][64] (ABI 16): ReLU(modelB's hidden features) of every replay
+                                row's s, written at push time by pm_selfplay_actenv from featB (the features
+                                are frozen: train_iterative.py:97). Needs featB. */
+    int32_t frow_ready;      /* nonzero: every replay row with a nonzero priority was pushed through actenv
+                                since modelB's feature layers last changed, so frow is current; then
+                                pm_selfplay_step_multi runs updates 1..U-1 as ONE single-workgroup launch
+                                (k_learn_multi) instead of 3 launches per update */
+    int32_t _pad1;
 } pm_selfplay;
 
 /* Limits: 1 <= batch <= PM_MAX_BATCH (one learner workgroup), batch < n <= cap (every vector step

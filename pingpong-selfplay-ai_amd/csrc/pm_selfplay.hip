@@ -360,6 +360,21 @@ __device__ __forceinline__ void env_block(const pm_selfplay& sp, int blk, EnvSme
                 tile_heads(lw + F_H, c2, lane, q);
             }
             act[k] = argmax3(q);
+            if (sp.featB && sp.frow) {  // k_learn_multi's features of s: ReLU(layer 2) of this push's rows
+                const int ar = i0 + 64 * wv + 32 * k + (lane & 31);
+                if (ar < sp.n) {
+                    int64_t slot = pos + ar;
+                    if (slot >= sp.cap) slot -= sp.cap;
+                    float4* fr = reinterpret_cast<float4*>(sp.frow + slot * 64) + (lane >> 5);
+#pragma unroll
+                    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+                        for (int q4 = 0; q4 < 4; ++q4)  // units 32 jt + 8 q4 + 4 h + 0..3
+                            st_f4<kEnvWTRows>(fr + 8 * jt + 2 * q4,
+                                              make_float4(relu(fc2[k][jt][4 * q4]), relu(fc2[k][jt][4 * q4 + 1]),
+                                                          relu(fc2[k][jt][4 * q4 + 2]), relu(fc2[k][jt][4 * q4 + 3])));
+                }
+            }
         }
         aB = lane < 32 ? act[0] : act[1];
     }
@@ -595,6 +610,8 @@ __device__ __forceinline__ void adam_one(const pm_selfplay& sp, ApplySmem& sm, i
     sp.adam_m[k] = m;
     sp.adam_v[k] = v;
     sm.hp[k] = p;
+    sm.m[k] = m;  // k_learn_multi runs the next update from LDS
+    sm.v[k] = v;
 }
 __device__ __forceinline__ void apply_adam(const pm_selfplay& sp, ApplySmem& sm) {
     const int t = threadIdx.x, nt = blockDim.x;
@@ -1228,6 +1245,579 @@ __global__ __launch_bounds__(kLearn) void k_commit(const pm_selfplay sp) {
     }
 }
 
+// ------------------------------------------------------------------------------------ U > 1 in one launch
+// k_learn_multi: updates 1..U-1 of a vector step (after update 0's k_learn, before pm_selfplay_commit)
+// as ONE single-workgroup launch, instead of k_resample + k_batch_fwd + k_learn per update (three
+// launches, two of them on other CUs, ~30 us per update). Bit-identical to that sequence: the same
+// PER descent (the chunk-level prefix in per_round_prefix's order, per_group_find for levels 1 and
+// 0), the same head chains as tile_heads, and k_learn's phases 2-5 and fused apply in the same
+// arithmetic order. What makes one workgroup enough:
+//   - the features are frozen (train_iterative.py:97), so the batch forward needs only the heads:
+//     ReLU(features(s)) of every replay row is stored at push time (sp.frow, written by k_actenv from
+//     featB), features(s') of row i is frow[(i + n) % cap] (the same arena's next push) or, for this
+//     step's own push, featB; a done row's s' never enters the target (nq * (1 - done)), so the
+//     post-reset features stand in for the terminal ones there;
+//   - the sum tree's top level (<= 1024 chunk sums) lives in LDS for all the updates; tree reads go
+//     around L1 (nontemporal loads), so the workgroup's own scatters and refreshes are always seen;
+//   - head parameters, Adam moments, the update's noisy heads and the next noise stay in LDS; the
+//     global copies are written as the sequence of launches would leave them.
+constexpr int kMultiChunks = PER_ROUND;  // level-2 nodes kept in LDS (capacity <= 1 M entries)
+
+struct MultiSmem {
+    float Hs[PM_MAX_BATCH][65];   // ReLU(features(s)) of the batch (k_learn's Hs)
+    float qv[PM_MAX_BATCH][12];   // Q_B(s) 0..2 | r 3 | Q_B(s') 4..6 | action|done bits 7 | Q_T(s') 8..10
+    float coef[PM_MAX_BATCH][4];
+    float gpart[16][256];
+    float hf[2][264];             // the update's modelB heads (fresh noise) | targetB heads, fragment order
+    float eps_tr[pad256(260)];    // the update's noise (eps section layout)
+    double chunk[kMultiChunks];   // level-2 nodes
+    double incl[kMultiChunks];    // their inclusive prefix (per_round_prefix)
+    double wsum[16];
+    int64_t sidx[PM_MAX_BATCH];
+    float sw[PM_MAX_BATCH];       // un-normalised IS weights
+    uint32_t hkey[512];
+    int hwin[512];
+    float red[16][8];
+    double total;
+    double pa[PM_MAX_BATCH];      // the drawn leaf's value per sample (its IS weight's pow in a pass of its own)
+    int64_t ts, frame;            // train_steps, frame_idx as the updates advance them
+    float maxp, loss;
+    ApplySmem ap;
+};
+static_assert(sizeof(MultiSmem) <= 160 * 1024, "k_learn_multi LDS");
+
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T* p) { return __builtin_nontemporal_load(p); }
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+// 16 consecutive floats [lo, lo + 16) around L1 (4 x 16-byte loads; scalar loads past cap read 0).
+// 16-scalar-load sweeps of a 4-lane group per sample cost 15 us per level here (one request per lane
+// and load), the 16-byte ones a tenth of that.
+__device__ __forceinline__ void ld_nt16(const float* p, int64_t lo, int64_t cap, float (&v)[16]) {
+    if (lo + 16 <= cap) {
+        const f32x4v* p4 = reinterpret_cast<const f32x4v*>(p + lo);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4v x = __builtin_nontemporal_load(p4 + q);
+            v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = lo + i < cap ? ld_nt(p + lo + i) : 0.f;
+    }
+}
+
+// per_quarter / per_sub_sum4 (no pending push) with loads around L1.
+__device__ __forceinline__ double multi_quarter(const float* leaf, int64_t sb, int k, int64_t cap) {
+    const int64_t lo = sb * PER_SUB + 16 * k;
+    float v[16];
+    ld_nt16(leaf, lo, cap, v);
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc += lo + i < cap ? (double)v[i] : 0.0;
+    return acc;
+}
+__device__ __forceinline__ double multi_sub_sum4(const float* leaf, int64_t sb, int64_t cap) {
+    const int lane = threadIdx.x & 63, base = lane & ~3;
+    const double q = multi_quarter(leaf, sb, lane & 3, cap);
+    return per_combine(__shfl(q, base), __shfl(q, base + 1), __shfl(q, base + 2), __shfl(q, base + 3));
+}
+__device__ __forceinline__ double multi_chunk_sum(const PerTree& t, int64_t c) {
+    typedef double f64x2v __attribute__((ext_vector_type(2)));
+    double v[PER_FAN];
+    if (c * PER_FAN + PER_FAN <= t.nsub) {  // sub is 256-byte aligned: 16-byte loads of the node's 16
+        const f64x2v* p = reinterpret_cast<const f64x2v*>(t.sub + c * PER_FAN);
+#pragma unroll
+        for (int k = 0; k < PER_FAN / 2; ++k) {
+            const f64x2v x = __builtin_nontemporal_load(p + k);
+            v[2 * k] = x.x;
+            v[2 * k + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < PER_FAN; ++k) v[k] = c * PER_FAN + k < t.nsub ? ld_nt(t.sub + c * PER_FAN + k) : 0.0;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER_FAN; ++k) acc += v[k];
+    return acc;
+}
+
+// One lane half's share of tile_heads: the fmaf chains over this half's 32 units (32 tt + 8 q4 + 4 h
+// + e, in tile_heads' (t, r) order with r = 4 q4 + e), x[16 tt + 4 q4 + e] = ReLU'd feature. The
+// cross-half add and the rest follow in half_heads_finish (lanes t and t ^ 1 hold the two halves).
+__device__ __forceinline__ void half_chains(const float* hf, int h, const float (&x)[32], float (&s)[4]) {
+    float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    const float4* hw = reinterpret_cast<const float4*>(hf + h * 128);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const float4 w = hw[k];  // (t, r) = (k >> 4, k & 15): unit 32 t + rho(r) + 4 h
+        v = fmaf(w.x, x[k], v);
+        a0 = fmaf(w.y, x[k], a0);
+        a1 = fmaf(w.z, x[k], a1);
+        a2 = fmaf(w.w, x[k], a2);
+    }
+    s[0] = v; s[1] = a0; s[2] = a1; s[3] = a2;
+}
+// The same chains for two rows with one sweep of the weights (the sweep's LDS reads bound this phase).
+__device__ __forceinline__ void half_chains2(const float* hf, int h, const float (&xa)[32], const float (&xb)[32],
+                                             float (&sa)[4], float (&sb)[4]) {
+    float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, u = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
+    const float4* hw = reinterpret_cast<const float4*>(hf + h * 128);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const float4 w = hw[k];
+        v = fmaf(w.x, xa[k], v);
+        a0 = fmaf(w.y, xa[k], a0);
+        a1 = fmaf(w.z, xa[k], a1);
+        a2 = fmaf(w.w, xa[k], a2);
+        u = fmaf(w.x, xb[k], u);
+        b0 = fmaf(w.y, xb[k], b0);
+        b1 = fmaf(w.z, xb[k], b1);
+        b2 = fmaf(w.w, xb[k], b2);
+    }
+    sa[0] = v; sa[1] = a0; sa[2] = a1; sa[3] = a2;
+    sb[0] = u; sb[1] = b0; sb[2] = b1; sb[3] = b2;
+}
+__device__ __forceinline__ void half_heads_finish(const float* hf, const float (&s)[4], float (&q)[3]) {
+    float v = s[0] + __shfl_xor(s[0], 1), a0 = s[1] + __shfl_xor(s[1], 1);  // v_h0 + v_h1 in either lane
+    float a1 = s[2] + __shfl_xor(s[2], 1), a2 = s[3] + __shfl_xor(s[3], 1);
+    v += hf[256];
+    a0 += hf[257];
+    a1 += hf[258];
+    a2 += hf[259];
+    const float mean = ((a0 + a1) + a2) / 3.0f;
+    q[0] = v + (a0 - mean);
+    q[1] = v + (a1 - mean);
+    q[2] = v + (a2 - mean);
+}
+
+// Half h's 32 ReLU'd features of a replay row from frow (8 float4: units 32 tt + 8 q4 + 4 h + 0..3) ...
+__device__ __forceinline__ void load_frow_half(const float* frow, int64_t slot, int h, float (&x)[32]) {
+    const float4* p = reinterpret_cast<const float4*>(frow + slot * 64) + h;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float4 v = p[2 * k];
+        x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+    }
+}
+// ... or of one arena from featB (feat_tiles' layout: tile a / 32, piece 4 tt + q4, lane half h,
+// component e; pre-ReLU there).
+__device__ __forceinline__ void load_featB_half(const float* featB, int a, int h, float (&x)[32]) {
+    const float4* p = reinterpret_cast<const float4*>(featB) + (size_t)(a >> 5) * 8 * 64 + 32 * h + (a & 31);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float4 v = p[k * 64];
+        x[4 * k] = relu(v.x); x[4 * k + 1] = relu(v.y); x[4 * k + 2] = relu(v.z); x[4 * k + 3] = relu(v.w);
+    }
+}
+
+// per_group_find<16> over lv[k] = lo + k < size ? (double)f[k] : 0 with the leaves kept as floats.
+__device__ __forceinline__ int group_find16f(const float (&f)[16], int64_t lo, int64_t size, double x, double& before,
+                                             double& val) {
+    const int lane = threadIdx.x & 63, q = lane & 3, g0 = lane & ~3;
+    auto lv = [&](int e) { return lo + e < size ? (double)f[e] : 0.0; };
+    double acc = 0.0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc += lv(e);
+    const double s0 = __shfl(acc, g0), s1 = __shfl(acc, g0 + 1), s2 = __shfl(acc, g0 + 2);
+    const double ex = q == 0 ? 0.0 : (q == 1 ? s0 : (q == 2 ? s0 + s1 : (s0 + s1) + s2));
+    int hit = -1, nz = -1;
+    double hb = 0.0, hv = 0.0, nb = 0.0, nv = 0.0, run = ex;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const double v = lv(e);
+        if (hit < 0 && run + v > x) { hit = e; hb = run; hv = v; }
+        if (v > 0.0) { nz = e; nb = run; nv = v; }
+        run += v;
+    }
+    const unsigned gh = (unsigned)(__ballot(hit >= 0) >> g0) & 15u;
+    const unsigned gn = (unsigned)(__ballot(nz >= 0) >> g0) & 15u;
+    int src, k;
+    if (gh) {
+        src = __ffs(gh) - 1;
+        k = hit;
+    } else {
+        src = gn ? 31 - __clz(gn) : 0;
+        k = nz < 0 ? 0 : nz;
+        hb = nz < 0 ? ex : nb;
+        hv = nz < 0 ? 0.0 : nv;
+    }
+    const int kk = __shfl(k, g0 + src);
+    before = __shfl(hb, g0 + src);
+    val = __shfl(hv, g0 + src);
+    return src * 16 + kk;
+}
+
+// The update's noise in eps-section layout from the FRESH fold's draws (what fold_heads_from writes
+// to its eps_out), threads [0, 260).
+__device__ __forceinline__ void noise_to_eps(const float* noise, float* eps) {
+    const int k = threadIdx.x;
+    if (k >= 260) return;
+    const int row = k < 256 ? k >> 6 : k - 256, col = k & 63;
+    const bool w = k < 256;
+    float ep;
+    int eo;
+    if (row == 0) {
+        ep = w ? noise[64] * noise[col] : noise[64];
+        eo = w ? E_VWEP + col : E_VBEP;
+    } else {
+        const int a = row - 1;
+        ep = w ? noise[129 + a] * noise[65 + col] : noise[129 + a];
+        eo = w ? E_AWEP + a * 64 + col : E_ABEP + a;
+    }
+    eps[eo] = ep;
+}
+
+// One update of k_learn_multi. A function of its own (not inlined): inside the kernel's loop the
+// compiler hoisted every loop-invariant address and kernel-argument load out of it and spilled them
+// (~700 B of scratch per lane at the 128-VGPR cap of a 1024-thread workgroup).
+__device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, int64_t size, int64_t nb, int64_t c_pos,
+                                          uint64_t c_step) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
+    const PerTree tree = per_tree(sp.per_work, sp.cap);
+    PM_STAMP(100);
+    const int64_t ts = sm.ts, frame = sm.frame + 1;  // frame_idx += 1 before sampling (:136)
+    for (int k = t; k < 512; k += kLearn) { sm.hkey[k] = kHashEmpty; sm.hwin[k] = -1; }
+    // ---- PER sample (per_sample_block, no pending push): level 2 over the LDS chunk sums
+    {
+        double run[4] = {0.0, 0.0, 0.0, 0.0}, acc = 0.0, incl = 0.0;
+        if (t < 256) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t ch = 4 * t + e;
+                acc += ch < nb ? sm.chunk[ch] : 0.0;
+                run[e] = acc;
+            }
+        }
+        incl = wave_incl_scan(acc, lane);
+        double excl = __shfl_up(incl, 1);
+        if (lane == 0) excl = 0.0;
+        if (lane == 63) sm.wsum[wv] = incl;
+        __syncthreads();
+        if (t < 256) {
+            double wb = 0.0;
+            for (int w = 0; w < wv; ++w) wb += sm.wsum[w];
+            const double ex = wb + excl;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sm.incl[4 * t + e] = ex + run[e];
+        }
+        if (t == 0) sm.total = ((0.0 + sm.wsum[0]) + sm.wsum[1]) + sm.wsum[2] + sm.wsum[3];
+        __syncthreads();
+    }
+    PM_STAMP(101);
+    const double total = sm.total;
+    {
+        const int j = t >> 2, q = t & 3;
+        const int n = (int)nb;
+        double x = 0.0, before = 0.0;
+        int64_t blk = 0;
+        {
+            const U4 r = philox64((uint32_t)j, TAG_PER, (uint64_t)frame, sp.seed_env);
+            const double uu = j < B ? u53(r.x, r.y) : 0.0;
+            x = uu * total;
+            if (total > 0.0) {
+                int lo = 0, hi = n;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sm.incl[mid] > x) hi = mid;
+                    else lo = mid + 1;
+                }
+                if (lo < n) {
+                    blk = lo;
+                    before = lo ? sm.incl[lo - 1] : 0.0;
+                } else {  // the last nonzero chunk: the first to reach the end value
+                    int l2 = 0, h2 = n - 1;
+                    while (l2 < h2) {
+                        const int mid = (l2 + h2) >> 1;
+                        if (sm.incl[mid] >= sm.incl[n - 1]) h2 = mid;
+                        else l2 = mid + 1;
+                    }
+                    blk = l2;
+                    before = l2 ? sm.incl[l2 - 1] : 0.0;
+                }
+            }
+        }
+        PM_STAMP(111);
+        double sv[4];
+        const int64_t s0 = blk * PER_FAN + 4 * q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sv[e] = s0 + e < tree.nsub ? ld_nt(tree.sub + s0 + e) : 0.0;
+        double b1, v1;
+        const int64_t sb = blk * PER_FAN + per_group_find<4>(sv, x - before, b1, v1);
+        PM_STAMP(112);
+        float lf[16];
+        const int64_t lo = sb * PER_SUB + 16 * q;
+        ld_nt16(tree.leaf, lo, sp.cap, lf);
+        double b0, pa;
+        const int k = group_find16f(lf, lo, size, x - before - b1, b0, pa);
+        PM_STAMP(113);
+        // ---- the sample's three head evaluations on the same 4 lanes, each lane one sweep of one head
+        // set's weights (those LDS reads bound this phase): lanes 0-1 (lane halves h) run Q_B(s) and
+        // Q_B(s') on modelB's heads, lanes 2-3 Q_T(s') on targetB's. The row loads are issued as soon as
+        // the descent has the index; lanes 0-1 keep the features of s for Hs, lane 1 loads the reward
+        // and action|done bits, lane 0 forms the IS weight while the loads are in flight.
+        const int64_t id = sb * PER_SUB + k;
+        const int h = q & 1, set = q >> 1;
+        float xs[32], xn[32];
+        float rb[2] = {0.f, 0.f};
+        {
+            int64_t a = id - c_pos;
+            if (a < 0) a += sp.cap;
+            if (a < sp.n) {  // this step's push: s' = the observations featB holds
+                load_featB_half(sp.featB, (int)a, h, xn);
+            } else {
+                int64_t nx = id + sp.n;
+                if (nx >= sp.cap) nx -= sp.cap;
+                load_frow_half(sp.frow, nx, h, xn);
+            }
+        }
+        if (set == 0) {
+            load_frow_half(sp.frow, id, h, xs);
+            if (h) {
+                const float* tr = sp.trans + id * PM_TRANS_F;
+                rb[0] = tr[7];
+                rb[1] = tr[15];
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 32; ++e) xs[e] = xn[e];
+        }
+#ifdef PM_DIAG
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PM_STAMP(117);
+#endif
+        const float* hfs = sm.hf[set];
+        float s1[4], s2[4], q1[3], q2[3];
+        half_chains2(hfs, h, xs, xn, s1, s2);  // set 0: Q_B(s), Q_B(s'); set 1: Q_T(s') (twice)
+        half_heads_finish(hfs, s1, q1);
+        half_heads_finish(hfs, s2, q2);
+        PM_STAMP(118);
+        if (j < B) {
+            if (set == 0) {
+#pragma unroll
+                for (int e = 0; e < 32; ++e) sm.Hs[j][32 * (e >> 4) + 8 * ((e >> 2) & 3) + 4 * h + (e & 3)] = xs[e];
+                if (h == 0) {
+                    sm.qv[j][0] = q1[0]; sm.qv[j][1] = q1[1]; sm.qv[j][2] = q1[2];
+                    sm.qv[j][4] = q2[0]; sm.qv[j][5] = q2[1]; sm.qv[j][6] = q2[2];
+                    sm.sidx[j] = id;
+                    sm.pa[j] = pa;
+                    sp.idx[j] = id;
+                } else {
+                    sm.qv[j][3] = rb[0];
+                    sm.qv[j][7] = rb[1];
+                }
+            } else if (h == 0) {
+                sm.qv[j][8] = q1[0]; sm.qv[j][9] = q1[1]; sm.qv[j][10] = q1[2];
+            }
+        }
+    }
+    __syncthreads();
+    PM_STAMP(102);
+    // this update's noise is left in modelB's epsilon buffers by its phase 0 (reset_noise); the
+    // target sync below copies it from there
+    const bool act = t < B;
+    // the IS weights (size * P(i))^-beta, one fp64 pow per lane on the batch's waves only (every
+    // wave running it for its 16 samples cost ~3 us of VALU issue)
+    const float wraw = act ? (float)pow((double)size * (sm.pa[t] / total), -beta_of(sp, frame)) : 0.f;
+    if (act) sp.isw[t] = wraw;
+    const int64_t id = act ? sm.sidx[t] : 0;
+    {
+        float m = wraw;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        if (lane == 0) sm.red[wv][0] = m;
+    }
+    __syncthreads();
+    PM_STAMP(103);
+    float wmax = sm.red[0][0];
+    for (int w = 1; w < 16; ++w) wmax = fmaxf(wmax, sm.red[w][0]);
+    __syncthreads();
+    PM_STAMP(104);
+    // ---- k_learn phase 2: double-DQN targets, loss, priorities, bias grads
+    float lossp = 0.f, prio = 0.f;
+    float cf[4] = {0.f, 0.f, 0.f, 0.f};
+    int slot = 0;
+    if (act) {
+        const float rwd = sm.qv[t][3];
+        const int bits = __float_as_int(sm.qv[t][7]);
+        const int a = bits & 0xff, dn = (bits >> 8) & 1;
+        const float qs[3] = {sm.qv[t][0], sm.qv[t][1], sm.qv[t][2]};
+        const float qn[3] = {sm.qv[t][4], sm.qv[t][5], sm.qv[t][6]};
+        const float qt[3] = {sm.qv[t][8], sm.qv[t][9], sm.qv[t][10]};
+        const float q = qs[a];
+        const float nq = qt[argmax3(qn)];
+        const float tgt = rwd + (float)sp.gamma * nq * (dn ? 0.f : 1.f);
+        const float diff = q - tgt;
+        const float w = wraw / wmax;
+        lossp = w * (diff * diff);
+        const float g = 2.f * w * diff / (float)B;
+        cf[0] = g;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cf[1 + k] = g * ((k == a ? 1.f : 0.f) - 1.f / 3.f);
+        *reinterpret_cast<float4*>(sm.coef[t]) = make_float4(cf[0], cf[1], cf[2], cf[3]);
+        prio = fabsf(diff) + 1e-6f;
+        const uint32_t key = (uint32_t)id;
+        slot = (int)((key * 2654435761u) >> 23);
+        for (;;) {
+            const uint32_t old = atomicCAS(&sm.hkey[slot], kHashEmpty, key);
+            if (old == kHashEmpty || old == key) break;
+            slot = (slot + 1) & 511;
+        }
+        atomicMax(&sm.hwin[slot], t);
+    } else if (t >= kLearn / 2) {  // the apply's scalar prologue on waves the TD phase leaves idle:
+        if (t >= kLearn - 2) adam_const_lane(sp, ts + 1, sm.ap, t - (kLearn - 2));  // Adam's corrections
+        gen_both_noises_on(sp, sm.ap, c_step + 1, (uint64_t)(ts + 1) + 1, kLearn / 2);  // both noises
+    }
+    {
+        float s = lossp, mp = prio;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o);
+            mp = fmaxf(mp, __shfl_xor(mp, o));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cf[k] += __shfl_xor(cf[k], o);
+        }
+        if (lane == 0) {
+            sm.red[wv][1] = s; sm.red[wv][2] = mp;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sm.red[wv][3 + k] = cf[k];
+        }
+    }
+    __syncthreads();
+    PM_STAMP(105);
+    // ---- phase 3: priority scatter; head gradient partials (16 waves x 16 samples)
+    if (act && sm.hwin[slot] == t) {
+        sp.prios[id] = prio;
+        tree.leaf[id] = prio_pow(prio, (float)sp.alpha);
+    }
+    {
+        float mpx = sm.red[0][2];
+        for (int w = 1; w < 16; ++w) mpx = fmaxf(mpx, sm.red[w][2]);
+        float l = 0.f;
+        for (int w = 0; w < 16; ++w) l += sm.red[w][1];
+        if (t == 0) {
+            sm.loss = l / (float)B;
+            sm.maxp = fmaxf(sm.maxp, mpx);
+        }
+        const int col = t & 63;
+        float g[4] = {0.f, 0.f, 0.f, 0.f};
+        const int j0 = wv * 16, j1 = min(j0 + 16, B);
+        for (int j = j0; j < j1; ++j) {
+            const float4 k4 = *reinterpret_cast<const float4*>(sm.coef[j]);
+            const float h = sm.Hs[j][col];
+            g[0] = fmaf(k4.x, h, g[0]);
+            g[1] = fmaf(k4.y, h, g[1]);
+            g[2] = fmaf(k4.z, h, g[2]);
+            g[3] = fmaf(k4.w, h, g[3]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm.gpart[wv][r * 64 + col] = g[r];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the scatter's stores are in L2 before the
+    __syncthreads();                                   // refresh's L1-bypassing loads
+    PM_STAMP(106);
+    // ---- phase 4: gradients + Adam on the thread that forms each; level-1 nodes of the scatter
+    if (t < 256) {
+        float g = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) g += sm.gpart[w][t];
+        const int row = t >> 6, col = t & 63;
+        float* gs = sm.ap.g;
+        const int a = row - 1;
+        const int kmu = row == 0 ? col : 130 + a * 64 + col, ksg = row == 0 ? 65 + col : 325 + a * 64 + col;
+        const float gsg = g * sm.eps_tr[row == 0 ? P_VWEP - PM_QNET_EPS_OFF + col
+                                                 : P_AWEP - PM_QNET_EPS_OFF + a * 64 + col];
+        gs[kmu] = g;
+        gs[ksg] = gsg;
+        adam_one(sp, sm.ap, kmu, g);
+        adam_one(sp, sm.ap, ksg, gsg);
+    } else if (t < 260) {
+        const int k = t - 256;
+        float g = 0.f;
+        for (int w = 0; w < 16; ++w) g += sm.red[w][3 + k];
+        float* gs = sm.ap.g;
+        const int kmu = k == 0 ? 64 : 322 + k - 1, ksg = k == 0 ? 129 : 517 + k - 1;
+        const float gsg = g * sm.eps_tr[k == 0 ? P_VBEP - PM_QNET_EPS_OFF : P_ABEP - PM_QNET_EPS_OFF + k - 1];
+        gs[kmu] = g;
+        gs[ksg] = gsg;
+        adam_one(sp, sm.ap, kmu, g);
+        adam_one(sp, sm.ap, ksg, gsg);
+    }
+    PM_STAMP(115);
+    {
+        const int j = min(t >> 2, B - 1);
+        const int64_t sb = sm.sidx[j] / PER_SUB;
+        const double v = multi_sub_sum4(tree.leaf, sb, sp.cap);
+        PM_STAMP(116);
+        if ((t & 3) == 0) tree.sub[sb] = v;
+    }
+    if (t == 0) { sm.ap.g[kGradN] = 0.f; sm.ap.g[kGradN + 1] = 1.f; }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // level-1 stores land before level 2 reads them
+    __syncthreads();
+    PM_STAMP(107);
+    for (int k = t; k < kGradN + 2; k += kLearn) sp.grad[k] = sm.ap.g[k];
+    // ---- phase 5: level-2 nodes of the scatter (global and the LDS copy)
+    if (act && sm.hwin[slot] == t) {
+        const int64_t ch = id / PER_CHUNK;
+        const double v = multi_chunk_sum(tree, ch);
+        tree.chunk[ch] = v;
+        sm.chunk[ch] = v;
+    }
+    // ---- apply_finish (mode 0): target sync, next weights; counters at the end of the launch
+    if (t == 0) { sm.ts = ts + 1; sm.frame = frame; }
+    if ((ts + 1) % sp.target_update_interval == 0) {  // targetB.load_state_dict(modelB) (:166-168)
+        for (int k = t; k < PM_QNET_NHEAD; k += kLearn) sm.ap.tmu[k] = sm.ap.hp[k];
+        for (int k = t; k < PM_QNET_NP; k += kLearn) {
+            const int h = k - PM_QNET_HEAD_OFF, e = k - PM_QNET_EPS_OFF;
+            sp.paramsT[k] = (h >= 0 && h < PM_QNET_NHEAD) ? sm.ap.hp[h]
+                            : (e >= 0 ? sm.eps_tr[e] : sp.paramsB[k]);  // eps: this update's noise
+        }
+        __syncthreads();
+    }
+    PM_STAMP(108);
+    derive_weights(sp, sm.ap);  // w_B, learn_heads (global), modelB's eps buffers <- the acting noise
+    __syncthreads();
+    PM_STAMP(109);
+    heads_to_frags(sm.ap.heads[1], sm.hf[0]);
+    heads_to_frags(sm.ap.heads[2], sm.hf[1]);
+    noise_to_eps(sm.ap.ntrain, sm.eps_tr);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tree's stores land before the next descent
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kLearn, 1) void k_learn_multi(const pm_selfplay sp, int updates) {
+    __shared__ __attribute__((aligned(16))) MultiSmem sm;
+    const int t = threadIdx.x, B = sp.batch;
+    const PerTree tree = per_tree(sp.per_work, sp.cap);
+    pm_ctrl* c = sp.ctrl;
+    const int64_t c_pos = c->pos, c_size = c->size;
+    const uint64_t c_step = c->step;
+    const int64_t s_all = c_size + sp.n;
+    const int64_t size = s_all < sp.cap ? s_all : sp.cap;  // the replay as this step's push left it
+    if (size < B) return;  // block-uniform: no update trains (each would only re-derive the same weights)
+    const int64_t nb = (size + PER_CHUNK - 1) / PER_CHUNK;
+    // ---- state into LDS
+    for (int k = t; k < kMultiChunks; k += kLearn) sm.chunk[k] = k < tree.nchunk ? ld_nt(tree.chunk + k) : 0.0;
+    for (int k = t; k < 2 * 264; k += kLearn) sm.hf[k / 264][k % 264] = sp.learn_heads[k];
+    for (int k = t; k < 260; k += kLearn) sm.eps_tr[k] = sp.learn_heads[528 + k];
+    load_apply_inputs(sp, sm.ap, false);
+    if (t == 0) {  // loop-carried counters live in LDS (registers are the scarce resource here)
+        sm.ts = c->train_steps;
+        sm.frame = c->frame_idx;
+        sm.maxp = c->max_prio;
+        sm.loss = c->last_loss;
+    }
+    __syncthreads();
+
+    for (int u = 1; u < updates; ++u) multi_update(sp, sm, size, nb, c_pos, c_step);
+    if (t == 0) {
+        c->train_steps = sm.ts;
+        c->frame_idx = sm.frame;
+        c->last_loss = sm.loss;
+        c->max_prio = sm.maxp;
+    }
+}
+
 namespace {
 int check(const pm_selfplay* sp) {
     PM_REQUIRE(sp && sp->ctrl && sp->trans && sp->prios && sp->per_work && sp->idx && sp->isw && sp->grad &&
@@ -1287,6 +1877,14 @@ int launch_act(const pm_selfplay* sp, int part, hipStream_t st) {
 }
 
 // The side-A act grid of k_learn's extra blocks (1024 threads: four act blocks' worth each).
+// k_learn_multi's preconditions: features of every live replay row stored (frow_ready), the current
+// observations' features in featB (the update-0 launch computes them), the fused apply, a sum tree
+// whose top level fits LDS.
+bool multi_ok(const pm_selfplay* sp) {
+    return sp->frow && sp->frow_ready && sp->featB && sp->fuse_apply && sp->world == 1 &&
+           (sp->cap + PER_CHUNK - 1) / PER_CHUNK <= kMultiChunks && ((uintptr_t)sp->frow & 15) == 0;
+}
+
 ActGrid learn_act_grid(const pm_selfplay* sp) {
     return ActGrid{sp->n, sp->n_pool + 1, std::min(4 * sp->chunk_A, kListMax), std::min(4 * sp->chunk_P, kListMax), 0};
 }
@@ -1400,6 +1998,11 @@ extern "C" int pm_selfplay_step_multi(const pm_selfplay* sp, int32_t updates, vo
     if ((rc = pm_selfplay_actenv(sp, stream))) return rc;
     if ((rc = launch_learn(sp, true, st, PM_UPD_FIRST))) return rc;
     if ((rc = pm_selfplay_apply_ex(sp, PM_UPD_FIRST, stream))) return rc;
+    if (multi_ok(sp)) {  // updates 1..U-1 in one single-workgroup launch
+        hipLaunchKernelGGL(k_learn_multi, dim3(1), dim3(kLearn), 0, st, *sp, (int)updates);
+        PM_LAUNCHED("k_learn_multi");
+        return pm_selfplay_commit(sp, stream);
+    }
     for (int u = 1; u < updates; ++u) {
         if ((rc = pm_selfplay_resample(sp, stream))) return rc;
         if ((rc = launch_learn(sp, false, st, 0))) return rc;

@@ -35,7 +35,7 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 15
+ABI_VERSION = 16
 PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_N = 0, 1, 2, 3, 4
 
 
@@ -69,7 +69,7 @@ class SelfPlay(ctypes.Structure):
         [(n, c_double) for n in ("gamma", "alpha", "lr", "beta1", "beta2", "adam_eps", "min_epsilon", "epsilon_decay",
                                  "pool_ratio", "beta_start")] + \
         [("beta_frames", c_i64), ("target_update_interval", c_i64), ("seed_env", c_u64), ("seed_net", c_u64),
-         ("featB", c_void_p)]
+         ("featB", c_void_p), ("frow", c_void_p), ("frow_ready", c_i32), ("_pad1", c_i32)]
 
 
 class DrqnStats(ctypes.Structure):

@@ -86,7 +86,7 @@ class SelfPlayLearner:
                  memory_size=1_000_000, gamma=0.99, lr=2.5e-4, epsilon=0.02, min_epsilon=0.02, epsilon_decay=0.995,
                  target_update_interval=1000, pool_ratio=0.33, alpha=0.6, beta_start=0.4, beta_frames=100000,
                  episode=0, seed=0, rank=0, world=1, allreduce=None, device=None, modelA_noisy=True,
-                 fuse_apply=True, overlap=True, updates_per_step=1, features_ahead=True):
+                 fuse_apply=True, overlap=True, updates_per_step=1, features_ahead=True, learn_multi=True):
         self.lib = _lib.load()
         self.updates_per_step = int(updates_per_step)
         if self.updates_per_step < 1:
@@ -142,6 +142,11 @@ class SelfPlayLearner:
         # modelB's hidden features of the next step's observations, computed with the opponents' act
         # (features are frozen: only the heads train), so the fused act + env kernel evaluates heads only
         self.featB = torch.zeros(((n + 31) // 32) * 2048, **f32) if features_ahead else None
+        # U > 1: ReLU(modelB's features) of every replay row's s, stored at push time, so updates 1..U-1
+        # of a vector step run as one single-workgroup launch (k_learn_multi; 256 B per replay row)
+        use_frow = learn_multi and self.updates_per_step > 1 and features_ahead and self.overlap and world == 1
+        self.frow = torch.zeros((self.cap, 64), **f32) if use_frow else None
+        self._frow_wait = 0  # vector steps pushed through actenv still needed before frow is current
         # ---- control block
         c = _lib.Ctrl()
         c.epsilon = float(epsilon)
@@ -158,6 +163,8 @@ class SelfPlayLearner:
                      "ctrl", "opp_list", "opp_cnt"):
             setattr(sp, name, ptr(getattr(self, name)))
         sp.featB = ptr(self.featB)
+        sp.frow = ptr(self.frow)
+        sp.frow_ready = int(self.frow is not None)
         sp.n, sp.n_pool, sp.batch, sp.world, sp.cap = n, self.n_pool, self.batch, self.world, self.cap
         sp.fuse_apply = int(bool(fuse_apply) and self.world == 1)
         p_pool = pool_ratio if self.n_pool else 0.0
@@ -179,8 +186,20 @@ class SelfPlayLearner:
     # side-A act, or by the extra blocks of the previous step's learner launch), and sp.featB modelB's
     # features of them (computed by the same launches). Anything that changes the observations,
     # opponent ids, opponent weights or modelB's feature layers clears it.
+    def _frow_pushed(self, through_actenv):
+        """Bookkeeping of sp.frow_ready: a push through k_env (rollout / env_step) stores no features, so
+        k_learn_multi waits until those rows have left the ring (cap / n pushes through actenv)."""
+        if self.frow is None:
+            return
+        if through_actenv:
+            self._frow_wait = max(0, self._frow_wait - 1)
+        else:
+            self._frow_wait = -(-self.cap // self.n) + 1
+        self.sp.frow_ready = int(self._frow_wait == 0)
+
     def rollout(self):
         self._aA_ready = False
+        self._frow_pushed(False)
         check(self.lib.pm_selfplay_rollout(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_rollout")
 
     def act(self, part=_lib.PM_ACT_ALL):
@@ -191,10 +210,12 @@ class SelfPlayLearner:
     def actenv(self):
         """act(PM_ACT_B) + env_step fused into one launch (bit-identical)."""
         self._aA_ready = False
+        self._frow_pushed(True)
         check(self.lib.pm_selfplay_actenv(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_actenv")
 
     def env_step(self):
         self._aA_ready = False
+        self._frow_pushed(False)
         check(self.lib.pm_selfplay_env(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_env")
 
     def learn(self, act_next=False):
@@ -229,6 +250,7 @@ class SelfPlayLearner:
     def _step_sharded(self, comm):
         """The sharded step as one library call (pongmi.dist.NativeComm): the all-reduce rides the
         learner's stream between k_learn and k_adam (same results as the Python sequence)."""
+        self._frow_pushed(True)
         if not self._aA_ready:
             self.act(_lib.PM_ACT_A)
         check(self.lib.pm_selfplay_step_sharded(ctypes.byref(self.sp), comm, self.updates_per_step, stream_ptr()),
@@ -240,6 +262,7 @@ class SelfPlayLearner:
         if self.world == 1 and self.overlap:
             if not self._aA_ready:
                 self.act(_lib.PM_ACT_A)
+            self._frow_pushed(True)
             check(self.lib.pm_selfplay_step_multi(ctypes.byref(self.sp), U, stream_ptr()), "pm_selfplay_step_multi")
             self._aA_ready = True
             return
@@ -260,10 +283,12 @@ class SelfPlayLearner:
             sharded_vector_step(self, self.allreduce, 1)
             return
         if not self.overlap:
+            self._frow_pushed(False)
             check(self.lib.pm_selfplay_step(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step")
             return
         if not self._aA_ready:
             self.act(_lib.PM_ACT_A)
+        self._frow_pushed(True)
         check(self.lib.pm_selfplay_step_overlap(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_step_overlap")
         self._aA_ready = True
 
@@ -321,10 +346,15 @@ class SelfPlayLearner:
         c.epsilon = float(epsilon)
         self.ctrl.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
         self.prepare()
+        if self.frow is not None:  # the replay is empty: every row k_learn_multi can reach is pushed from now
+            self._frow_wait = 0
+            self.sp.frow_ready = 1
 
     def prepare(self):
-        """Re-derive acting weights / next-update heads after the host replaced parameters."""
+        """Re-derive acting weights / next-update heads after the host replaced parameters. modelB's
+        feature layers may have changed, so the stored row features (frow) wait for a turn of the ring."""
         self._aA_ready = False
+        self._frow_pushed(False)
         check(self.lib.pm_selfplay_prepare(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_prepare")
 
 

@@ -615,3 +615,69 @@ def test_multi_update_sharded_replicas(golden):
     assert c0["train_steps"] == c1["train_steps"] == 5 * U and c0["epsilon"] == c1["epsilon"]
     for L in Ls:
         assert L.counters()["max_prio"] == L.prios.cpu().numpy().max()
+
+
+def _assert_same(A, B, names=("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "opp", "w_B",
+                              "learn_heads", "per_work", "idx", "isw", "aB", "ep_reward", "grad")):
+    torch.cuda.synchronize()
+    for name in names:
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    assert A.counters() == B.counters()
+
+
+@pytest.mark.parametrize("n,cap,U,steps,sync", [(1024, 4096, 5, 12, 7), (65536, 1_000_000, 6, 18, 13)])
+def test_learn_multi_equals_split(golden, n, cap, U, steps, sync):
+    """Updates 1..U-1 of a vector step as ONE single-workgroup launch (k_learn_multi: features of s
+    stored at push time, the tree's top level in LDS) equal the launch-per-update split path (resample +
+    batch forward + learn_ex + apply_ex per update) bit for bit: parameters, Adam state, priorities,
+    the whole sum tree, the acting / next-update weights, the last batch and its gradients, every
+    counter; across the replay ring's wrap and target syncs inside a launch. configs[2]'s full size
+    is the second case."""
+    kw = dict(n=n, batch=256, cap=cap, seed=31, n_pool=3, updates_per_step=U, target_update_interval=sync)
+    A = _learner(golden, **kw)
+    B = _learner(golden, fuse_apply=False, overlap=False, **kw)
+    assert A.frow is not None and B.frow is None and A.sp.frow_ready == 1
+    for k in range(steps):
+        A.step()
+        _drive_split(B, U)
+        if k % 5 == 4:
+            _assert_same(A, B)
+    _assert_same(A, B)
+    assert A.counters()["train_steps"] == steps * U
+
+
+def test_learn_multi_waits_for_stored_features(golden):
+    """A push through k_env (rollout / env_step) stores no row features: the fused multi-update path
+    stands down until those rows have left the ring (cap / n pushes), and a reset_B (empty replay)
+    re-arms it at once; the results equal the split path throughout."""
+    U, n, cap = 3, 1024, 4096
+    kw = dict(n=n, batch=256, cap=cap, seed=37, n_pool=2, updates_per_step=U, target_update_interval=5)
+    A = _learner(golden, **kw)
+    B = _learner(golden, fuse_apply=False, overlap=False, **kw)
+    ready = []
+    for k in range(16):
+        if k == 3:  # a plain push on A (the k_env path), the same step on B
+            from pongmi import _lib
+            A.act()
+            A.env_step()
+            for u in range(U):
+                mode = _lib.PM_UPD_FIRST if u == 0 else 0
+                if u:
+                    A.resample()
+                A.learn_ex(mode)
+                A.apply_ex(mode)
+            A.commit()
+            _drive_split(B, U)
+        elif k == 10:
+            sd = _random_qnet_sd(93)
+            A.reset_B(sd, epsilon=0.4)
+            B.reset_B(sd, epsilon=0.4)
+            ready.append(A.sp.frow_ready)
+            A.step()
+            _drive_split(B, U)
+        else:
+            A.step()
+            _drive_split(B, U)
+        ready.append(A.sp.frow_ready)
+    _assert_same(A, B)
+    assert ready[3] == 0 and ready[4] == 0 and 1 in ready[5:10] and ready[10] == 1

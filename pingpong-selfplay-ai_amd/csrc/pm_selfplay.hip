@@ -1264,7 +1264,7 @@ __global__ __launch_bounds__(kLearn) void k_commit(const pm_selfplay sp) {
 constexpr int kMultiChunks = PER_ROUND;  // level-2 nodes kept in LDS (capacity <= 1 M entries)
 
 struct MultiSmem {
-    float Hs[PM_MAX_BATCH][65];   // ReLU(features(s)) of the batch (k_learn's Hs)
+    float Hs[PM_MAX_BATCH][68];   // ReLU(features(s)) of the batch (k_learn's Hs); 16-byte rows
     float qv[PM_MAX_BATCH][12];   // Q_B(s) 0..2 | r 3 | Q_B(s') 4..6 | action|done bits 7 | Q_T(s') 8..10
     float coef[PM_MAX_BATCH][4];
     float gpart[16][256];
@@ -1595,7 +1595,9 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
         if (j < B) {
             if (set == 0) {
 #pragma unroll
-                for (int e = 0; e < 32; ++e) sm.Hs[j][32 * (e >> 4) + 8 * ((e >> 2) & 3) + 4 * h + (e & 3)] = xs[e];
+                for (int e = 0; e < 32; e += 4)  // units 32 tt + 8 q4 + 4 h + 0..3: one 16-byte store each
+                    *reinterpret_cast<float4*>(&sm.Hs[j][32 * (e >> 4) + 8 * ((e >> 2) & 3) + 4 * h]) =
+                        make_float4(xs[e], xs[e + 1], xs[e + 2], xs[e + 3]);
                 if (h == 0) {
                     sm.qv[j][0] = q1[0]; sm.qv[j][1] = q1[1]; sm.qv[j][2] = q1[2];
                     sm.qv[j][4] = q2[0]; sm.qv[j][5] = q2[1]; sm.qv[j][6] = q2[2];

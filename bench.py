@@ -311,6 +311,45 @@ def cpu_baseline_rnn(seconds=12.0, n=2048):
                       f"+ env + sequence buffer + DRQN update 64x8 every step), {dt:.1f} s on 1 host core"}
 
 
+def drqn_flop(B, T):
+    """FLOPs of one DRQN update (2 x MACs): three forward streams through F1, F2, the LSTM input and
+    recurrent projections (T*B columns each) and the shared head + heads on h_T (B columns); BPTT of
+    the obs stream: dWih, dWhh, dF2 = Wih^T dZ, dh = Whh^T dz, dW2, dF1, dW1, and the head's dW_S,
+    dh_T."""
+    C0 = T * B
+    fwd = 3 * C0 * (7 * 64 + 64 * 128 + 2 * 128 * 512) + 3 * B * (128 * 128 + 128 * 4)
+    bwd = C0 * (4 * 128 * 512 + 2 * 64 * 128 + 7 * 64) + B * 2 * 128 * 128
+    return 2 * (fwd + bwd)
+
+
+def time_drqn_update(D, launches=50):
+    """The DRQN update alone (pm_drqn_update, 5 launches) back to back on its last batch after the
+    timed region (HIP events on the stream), and the persistent recurrence k_dq_recur by its own
+    dispatch (pm_timer_arm). Restores nothing: it runs after the measured steps."""
+    from pongmi import _lib
+    for _ in range(5):
+        D.update()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(launches):
+        D.update()
+    e1.record()
+    e1.synchronize()
+    t = e0.elapsed_time(e1) * 1e-3 / launches
+    for _ in range(10):
+        _lib.timer_arm(_lib.PM_TIMER_DRQN)
+        D.update()
+    rec = sum(_lib.timer_read(_lib.PM_TIMER_DRQN) for _ in range(10)) / 10
+    flop = drqn_flop(D.batch, D.T)
+    achieved = flop / t / 1e12
+    return {"bound": "mfma", "kernel": "pm_drqn_update (k_dq_embed + k_dq_recur + k_dq_wgrad + k_drqn_norm + "
+                                       "k_drqn_adam), the whole update",
+            "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "update_us": round(t * 1e6, 2),
+            "recur_us": round(rec * 1e6, 2), "launches_per_update": 5, "flop_per_update": flop,
+            "batch": D.batch, "T": D.T, "timing": f"HIP events over {launches} back-to-back updates"}
+
+
 def run_rnn(args, dist, rank, world, allreduce):
     """configs[4]: 32768 arenas/GPU, the train_rnn_iterative loop (QNetRNN both players with (h, c)
     per arena, sequence buffer, DRQN update 64 x 8 with BPTT + clip + Adam every vector step)."""
@@ -364,7 +403,9 @@ def run_rnn(args, dist, rank, world, allreduce):
     upd_s = sum(e[2].elapsed_time(e[3]) for e in evs) * 1e-3 / len(evs)
     c = L.counters()
     shards, shards_ok = shard_proof(dist, rank, world, n, c["step"], c["status"] & 1, args.comm)
-    failed = (c["status"] & 1) != 0 or not shards_ok or (dist is not None and not same)
+    dst = L.learner.stats()
+    failed = (c["status"] & 1) != 0 or dst["status"] != 0 or not shards_ok or (dist is not None and not same)
+    drqn = time_drqn_update(L.learner) if world == 1 else None
     if rank == 0:
         value = n * world * args.steps / dt
         fpa = RNN_FLOP_PER_ARENA // 2 if overlap else RNN_FLOP_PER_ARENA  # overlap: modelB's side only
@@ -408,7 +449,8 @@ def run_rnn(args, dist, rank, world, allreduce):
             out["drqn_update_us"] = round(upd_s * 1e6, 2)
         out.update({
             "learner": {"train_steps": c["train_steps"], "episodes": c["episodes"], "epsilon": c["epsilon"],
-                        "seq_size": c["seq_size"], "status": c["status"], **L.learner.stats()},
+                        "seq_size": c["seq_size"], **dst, "status": c["status"], "drqn_status": dst["status"]},
+            "drqn_roofline": drqn,
         })
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_rnn(args.cpu_seconds)
@@ -421,13 +463,128 @@ def run_rnn(args, dist, rank, world, allreduce):
         sys.exit(3)
 
 
+def cpu_baseline_infer(seconds=12.0, n=4096):
+    from threadpoolctl import threadpool_limits
+    from oracle.cpu_selfplay import CpuRollout
+    sdB, _, _, _ = bench_nets("reference", 0)
+    np_sd = lambda s: {k: v.numpy() for k, v in s.items()}  # noqa: E731
+    with threadpool_limits(1):
+        cpu = CpuRollout(ENV_KW, n, np_sd(sdB), np_sd(sdB), epsilon=0.02)
+        cpu.step()
+        t0 = time.perf_counter()
+        steps = 0
+        while time.perf_counter() - t0 < seconds:
+            cpu.step()
+            steps += 1
+        dt = time.perf_counter() - t0
+    return {"value": round(n * steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/cpu_selfplay.py CpuRollout: {steps} vector steps x {n} arenas (both players' QNet "
+                      f"f32 + fresh noise per step + eps-greedy + C oracle tick + reset on done), {dt:.1f} s on 1 host core",
+            "reference_python_measured": "4 600 env-steps/s, batch-1 QNet rollout, 1 thread (SURVEY 6)"}
+
+
+def run_infer(args, dist, rank, world):
+    """configs[1]: 4096 arenas/GPU, QNet inference-only self-play (both players act, modelB with fresh
+    NoisyNet noise per vector step and eps = 0.02, autoreset), as the K9 megakernel (pm_rollout):
+    `--infer-chunk` vector steps per launch, the arenas in registers in between. Shards are independent
+    (per-rank env seed), no collective."""
+    from pongmi import _lib
+    from pongmi.env import PongEnv2PBatch
+    from pongmi.qnet import fold, pack_state_dict
+    from pongmi.rollout import STATS, SelfPlayRollout
+    n = args.arenas or 4096
+    steps = args.steps
+    chunk = max(1, min(args.infer_chunk, steps))
+    sdB, sdA, _, wdesc = bench_nets(args.weights, 0)
+    pB = pack_state_dict(sdB).reshape(-1)
+    wA = fold(pack_state_dict(sdA), _lib.PM_FOLD_TRAIN).reshape(-1)  # modelA: mu + sigma * (its frozen eps)
+    env = PongEnv2PBatch(n, seed=0x5EED + rank, autoreset=True, **ENV_KW)
+    env.reset()
+    R = SelfPlayRollout(env, wA, pB, epsilon=0.02, seed_net=0x5EED + 1000 * rank)
+    R.run(args.warmup)
+    torch.cuda.synchronize()
+    tot = torch.zeros(len(STATS), dtype=torch.int64, device="cuda")
+
+    def run(k):
+        done = 0
+        while done < k:
+            c = min(chunk, k - done)
+            tot.add_(R.run(c, sync=False))
+            done += c
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        dist.all_reduce(tot)
+    # after the timed region: the megakernel's own dispatch (pm_timer_arm, as rocprofv3 times it) on
+    # `reps` launches of `chunk` steps, and the same launches bracketed by HIP events on the stream
+    reps = 3
+    ks = []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        _lib.timer_arm(_lib.PM_TIMER_ROLLOUT)
+        R.run(chunk, sync=False)
+    e1.record()
+    e1.synchronize()
+    ks = [_lib.timer_read(_lib.PM_TIMER_ROLLOUT) for _ in range(reps)]
+    k_s = sum(ks) / reps
+    ev_s = e0.elapsed_time(e1) * 1e-3 / reps
+    st = dict(zip(STATS, tot.cpu().tolist()))
+    if rank == 0:
+        value = n * world * steps / dt
+        flop = n * chunk * 2 * FLOP_PER_ARENA
+        achieved = flop / k_s / 1e12
+        out = {
+            "metric": "env-steps/sec (whole node), QNet inference-only self-play rollout (configs[1])",
+            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64 env state / f32 QNet",
+            "data": f"synthetic: the env's own Philox serves; {wdesc}",
+            "config": {"workload": "configs[1]: 4096 arenas/GPU, QNet inference-only self-play rollout (modelA "
+                                   "greedy on mu + sigma*eps, modelB fresh noise every vector step + eps-greedy "
+                                   "0.02, autoreset)",
+                       "arenas_per_gpu": n, "global_arenas": n * world, "steps_per_launch": chunk,
+                       "launches_in_timed_region": -(-steps // chunk), "parallelism": f"dp{world} (independent "
+                       "arena shards, no collective)"},
+            "roofline": {"bound": "mfma", "kernel": "k_rollout (K9: both players' QNet forward + env tick, "
+                                                    f"{chunk} vector steps per launch)",
+                         "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
+                         "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "avg_us": round(k_s * 1e6, 1), "avg_us_per_step": round(k_s / chunk * 1e6, 4),
+                         "flop_per_env_step": 2 * FLOP_PER_ARENA, "n": n,
+                         "waves": 2 * (-(-n // 32)), "wave_slots": 256 * 4,
+                         "timing": f"pm_timer_arm dispatch of {reps} launches after the timed region; "
+                                   f"HIP events incl. the heads fold: {ev_s * 1e6:.1f} us per launch"},
+            "rollout": st,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_infer(args.cpu_seconds, n)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--workload", choices=("dqn", "rnn"), default="dqn",
-                    help="dqn: configs[2] (the headline); rnn: configs[4], the QNetRNN / DRQN loop")
+    ap.add_argument("--steps", type=int, default=None, help="vector steps timed (200; infer: 10000)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed vector steps first (30; infer: 100)")
+    ap.add_argument("--workload", choices=("dqn", "rnn", "infer"), default="dqn",
+                    help="dqn: configs[2] (the headline); rnn: configs[4], the QNetRNN / DRQN loop; infer: "
+                         "configs[1], the inference-only rollout megakernel")
+    ap.add_argument("--infer-chunk", type=int, default=10000, help="infer: vector steps per pm_rollout launch")
     ap.add_argument("--arenas", type=int, default=None, help="arenas per GPU (65536 dqn, 32768 rnn)")
     ap.add_argument("--pool", type=int, default=None, help="opponent pool size (synthetic nets; 8 dqn, 4 rnn)")
     ap.add_argument("--batch", type=int, default=256)
@@ -448,6 +605,9 @@ def main():
                     help="N > 1: the gradient all-reduce as libpongmi's own RCCL communicator inside one library "
                          "call per vector step (native), or torch.distributed.all_reduce between launches (torch)")
     args = ap.parse_args()
+    infer = args.workload == "infer"
+    args.steps = args.steps if args.steps is not None else (10000 if infer else 200)
+    args.warmup = args.warmup if args.warmup is not None else (100 if infer else 30)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -461,7 +621,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     comm = None
-    if dist is not None and args.comm == "native":
+    if dist is not None and args.comm == "native" and not infer:
         from pongmi.dist import NativeComm
         comm = NativeComm()  # raises on every rank if RCCL cannot be bound: no silent fallback
     args.comm_used = "native RCCL, in-stream" if comm is not None else "torch.distributed"
@@ -470,6 +630,8 @@ def main():
 
     if args.workload == "rnn":
         return run_rnn(args, dist, rank, world, allreduce)
+    if infer:
+        return run_infer(args, dist, rank, world)
     args.arenas = args.arenas or 65536
     args.pool = 8 if args.pool is None else args.pool
     from pongmi import _lib

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 16
+#define PM_ABI_VERSION 17
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -171,6 +171,24 @@ int pm_play(const pm_env_params* p, const float* w_nets, int32_t n_nets, const i
             const int32_t* blk_range, int32_t n_blocks, const int32_t* order, const double* serves, int32_t n,
             int32_t max_steps, int32_t* scoreA, int32_t* scoreB, int32_t* length, int8_t* last, int32_t* status,
             void* stream);
+
+/* K9 — inference-only self-play rollout, `steps` vector steps in one launch (BASELINE configs[1];
+ * csrc/pm_rollout.hip). Replaces the act/step loop of scripts/train_iterative.py:239-242 with the
+ * learner switched off: per vector step c = counter0 + s, modelB's heads are refolded with fresh
+ * noise (reset_noise, :125; Philox(seed_net, c) as pm_qnet_fold PM_FOLD_TRAIN_FRESH), player A acts
+ * greedily on wA, player B epsilon-greedily on wB's features + the fresh heads (Philox(seed_env, c)
+ * as pm_qnet_act), and every arena ticks with autoreset (the step-keyed serve of pm_env_step,
+ * Philox(seed_env, c)). Bit-identical to that fold -> act -> env_step sequence. wA / wB: effective
+ * weights (PM_QNET_NW, 16-B aligned; wB any fold of paramsB: only its feature layers are read);
+ * paramsB: modelB's parameter block (PM_QNET_NP; its eps section is not written); heads_ws: device
+ * workspace of steps * PM_ROLL_HEADS floats, 16-B aligned. On return the state holds the arenas after
+ * the last step and obsA / obsB [n][7] their observations. stats (nullable, device, accumulated):
+ * [0] episodes finished, [1] of them won by B, [2] points won by A, [3] points won by B. The serve
+ * counters (s->serves) are neither read nor written. */
+#define PM_ROLL_HEADS 264
+int pm_rollout(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB, const float* paramsB,
+               float epsilon, uint64_t seed_env, uint64_t seed_net, uint64_t counter0, int32_t steps, float* heads_ws,
+               float* obsA, float* obsB, int64_t* stats, int32_t n, void* stream);
 
 /* ---------------------------------------------------------------- QNetRNN (K5) */
 
@@ -572,7 +590,9 @@ int pm_rnn_selfplay_step_sharded_overlap(const pm_rnn_selfplay* sp, const pm_drq
 #define PM_TIMER_LEARN 1    /* k_learn: the double-DQN update + side-A act + modelB's feature layers */
 #define PM_TIMER_RNN_ACT 2  /* k_rnn_act */
 #define PM_TIMER_ENV_STEP 3 /* k_env_step (K1, pm_env_step) */
-#define PM_TIMER_N 4
+#define PM_TIMER_ROLLOUT 4  /* k_rollout (K9, pm_rollout) */
+#define PM_TIMER_DRQN 5     /* k_dq_recur (K6: the DRQN update's persistent recurrence, pm_drqn_grads) */
+#define PM_TIMER_N 6
 int pm_timer_arm(int32_t kernel);
 int pm_timer_read(int32_t kernel, float* ms);
 

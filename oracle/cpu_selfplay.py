@@ -106,3 +106,46 @@ class CpuSelfPlay:
             if self.t % 1000 == 0:
                 self.target = self.heads.copy()
         return n
+
+
+class CpuRollout:
+    """BASELINE configs[1] on the CPU: the inference-only rollout (scripts/train_iterative.py:239-242
+    with the learner off) for n arenas — modelA greedy on folded weights, modelB epsilon-greedy with
+    fresh NoisyNet noise per vector step (select_action_B, :125-130), the C oracle's tick, reset on
+    done. bench.py --workload infer's `cpu_baseline` ("kind": "port"), on one core."""
+
+    def __init__(self, env_kw, n, sdB, sdA, epsilon=0.02, seed=0):
+        self.rng = np.random.RandomState(seed)
+        self.pv = orc.env_params_from_kwargs(**env_kw)
+        self.P = orc.make_params(self.pv)
+        self.n, self.eps = n, epsilon
+        self.sdB = {k: np.asarray(v, np.float32) for k, v in sdB.items()}
+        self.effA = _eff32({k: np.asarray(v) for k, v in sdA.items()}, True)
+        self.arr = np.zeros(n, orc.ARENA_DTYPE)
+        self._serve(np.ones(n, bool))
+
+    def _serve(self, mask):
+        k = int(mask.sum())
+        if k == 0:
+            return
+        p = self.pv
+        speed = self.rng.uniform(p["speed_lo"], p["speed_hi"], k)
+        coin = self.rng.rand(k) < 0.5
+        ang = np.where(coin, self.rng.uniform(p["ang0_lo"], p["ang0_hi"], k), self.rng.uniform(p["ang1_lo"], p["ang1_hi"], k))
+        rad = np.radians(ang)
+        orc.serve_arenas(self.arr, mask, speed * np.cos(rad), speed * np.sin(rad),
+                         self.rng.uniform(p["spin_lo"], p["spin_hi"], k))
+
+    def step(self):
+        n = self.n
+        oA, oB = orc.obs_of_arenas(self.arr)
+        wn = orc.noise_from_raw(self.rng.randn(64).astype(np.float32), self.rng.randn(1).astype(np.float32))
+        an = orc.noise_from_raw(self.rng.randn(64).astype(np.float32), self.rng.randn(3).astype(np.float32))
+        eps_act = {"fc_V.weight_epsilon": wn[0], "fc_V.bias_epsilon": wn[1], "fc_A.weight_epsilon": an[0],
+                   "fc_A.bias_epsilon": an[1]}
+        qb = _q32(_eff32(self.sdB, True, eps_act), oB)
+        aA = np.argmax(_q32(self.effA, oA), 1).astype(np.int8)
+        aB = np.where(self.rng.rand(n) < self.eps, self.rng.randint(0, 3, n), np.argmax(qb, 1)).astype(np.int8)
+        _, _, _, done = orc.step_arenas(self.P, self.arr, aA, aB)
+        self._serve(done > 0)
+        return n

@@ -1,359 +1,784 @@
 // K6 — the DRQN update (train_step_rnn, scripts/train_rnn_iterative.py:400-531) on the device.
 //
-// One update is a fixed chain of launches on one stream, every GEMM on the exact-f32 MFMA:
-//   prep        plain effective heads (modelB train: mu + sigma*eps; targetB eval: mu), the batch
-//               gathered feature-major X[7][2*T*B] (column t*B + b; obs then next), last-step a/r/done
-//   embed x3    F1 = ReLU(W1 X + b1), F2 = ReLU(W2 F1 + b2), Zx = Wih F2 + bih + bhh — modelB on
-//               obs and next, targetB on next (three streams of T*B columns)
-//   fwd   xT    one LSTM step for all three streams (gate pre-activations Zx_t + Whh h_{t-1}; the
-//               four gates of a 32-unit block land in one workgroup, cell update in its epilogue);
-//               the obs stream keeps h, c and the gate activations for BPTT
-//   heads x3    S = ReLU(W_S h_T + b_S) (GEMM); Q, double-DQN target, smooth-L1, dQ -> V/A grads,
-//               dS (one workgroup); dW_S, db_S, dh_T = W_S^T dS (GEMM)
-//   bwd   xT    one BPTT step: dz_t from (dh_t, dc_t, the cached gates) into LDS, dh_{t-1} = Whh^T dz_t
-//   wgrad x3    dWih = dZ F2^T, dWhh = dZ H_{t-1}^T, db = rowsum dZ, dF2 = Wih^T dZ (masked by the
-//               ReLU) -> dW2, db2, dF1 -> dW1, db1
-//   (apply)     NoisyLinear sigma grads = mu grads * epsilon, formed in the norm pass
-// then (pm_drqn_apply) the global-norm clip (fp64 partials, fixed order) and torch's Adam.
-// Nothing uses atomics: the update is bit-reproducible run to run.
-#include "pm_gemm.h"
+// Five launches per update, every matrix product on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32):
+//
+//   k_dq_embed  (grads 1/3) the batch through the feature layers and the LSTM input projection for
+//               all three streams (modelB on obs, modelB on next, targetB on next): per (stream,
+//               32-column tile, time step) F1 = ReLU(W1 x + b1), F2 = ReLU(W2 F1 + b2) and
+//               Zx = Wih F2 + bih + bhh, Zx written in the accumulator layout the recurrence starts
+//               from; the obs stream's F1 / F2 kept for the weight gradients.
+//   k_dq_recur  (grads 2/3) the whole recurrence, persistent: every (stream, column tile) is a group
+//               of 16 workgroups, workgroup m owning LSTM units 8m..8m+7 (all four gates: one 32-row
+//               MFMA tile, its Whh rows in registers, K split over the 4 waves). Per time step the
+//               group exchanges h through write-through (sc1) stores + a per-workgroup step flag
+//               (MI355X_MICROARCH.md hand-off table, row 1), the cell state never leaves registers.
+//               Then the heads: each workgroup computes its 8 rows of the shared head and their
+//               partial V / A; the obs stream's group gathers all three streams' partial Q, forms the
+//               double-DQN target, smooth-L1 and dQ, the head gradients of its rows, and starts BPTT
+//               from dh_T = W_S^T dS; per BPTT step dz in registers (gates and c saved by the
+//               forward), dh_{t-1} = Whh^T dz as per-workgroup partials exchanged the same way.
+//   k_dq_wgrad  (grads 3/3) the weight gradients: dWih = dZ F2^T, dWhh = dZ H^T and the biases over
+//               all T*B columns (one workgroup per 32x32 output tile, K split over 16 waves); per
+//               32-column tile dF2 = Wih^T dZ -> ReLU mask -> dW2 / db2 partials -> dF1 = W2^T dP2
+//               -> dW1 / db1 partials, summed in a fixed order by the last tile to finish (arrival
+//               ticket); the head gradient partials of the column tiles summed likewise.
+//   k_drqn_norm, k_drqn_adam  (pm_drqn_apply) the NoisyLinear sigma gradients (mu gradient x epsilon),
+//               the global-norm clip (fp64 partials, fixed order) and torch's Adam, target sync.
+//
+// Every reduction runs in a fixed order and nothing sums through atomics, so an update is
+// bit-reproducible run to run (the arrival ticket only picks which workgroup does the final sum).
 #include "pm_host.h"
 #include "pm_rnn.h"
 
 namespace pm {
 namespace {
 
-constexpr int kNormBlocks = 64;
-// plain effective head block (floats)
-enum : int { E_S = 0, E_SB = 16384, E_V = 16512, E_VB = 16640, E_A = 16644, E_AB = 17028, E_N = 17040 };
+constexpr int kG = 16;           // workgroups per recurrence group (8 LSTM units each)
+constexpr int kNormBlocks = 256;  // k_drqn_norm blocks (fp64 partials, summed in order by k_drqn_adam)
+constexpr int kWgA = 128;        // k_dq_wgrad: dWih / dWhh output tiles
+constexpr int kWgC = 4;          // k_dq_wgrad: head-partial reduce workgroups
+constexpr int kLowN = 8832;      // grad [0, kLowN): W1, b1, W2, b2 (the column-tile partials)
+// per-column-tile head gradient partials (floats)
+enum : int { HP_WS = 0, HP_BS = 16384, HP_V = 16512, HP_VB = 16640, HP_A = 16641, HP_AB = 17025, HP_N = 17028 };
+constexpr int kHpStride = 17088;  // HP_N rounded up to 64
 
-struct DrqnArgs {
-    int B, T, C0, ldh;  // C0 = T*B columns per stream; ldh = (T+1)*B (h / c histories)
+struct DqArgs {
+    int B, T, nct, C0;
     const float *params, *target;
-    float *grad;
-    float *X, *F1B, *F1T, *F2B, *F2T, *ZxB, *ZxT;
-    float *Hp0, *Hp1, *Hp2, *Cs0, *Cs1, *Cs2;
-    float *G0, *S0, *S1, *S2, *dS, *dH0, *dH1, *dC0, *dC1, *dZ, *dP2, *dP1;
-    float *effB, *effT;
-    int32_t *a_last;
-    float *r_last, *d_last, *one;
-    double *part;
-    int64_t *tstep;
+    float* grad;
     const float *obs, *next;
-    const int32_t *act;
-    const float *rew;
-    const uint8_t *done;
-    pm_drqn_stats *stats;
+    const int32_t* act;
+    const float* rew;
+    const uint8_t* done;
+    pm_drqn_stats* stats;
     const int32_t* enable;
     float gamma;
+    float *ZX;   // [3][nct][T][16][1024]     Zx in the recurrence's accumulator layout
+    float *HS;   // [3][nct][T+1][32][128]    h_t per column (the hand-off slots; slot 0 unused)
+    float *F1T;  // [64][C0]                  obs stream F1 (column c = t*B + b)
+    float *F2T;  // [128][C0]                 obs stream F2
+    float *H;    // [128][C0]                 obs stream h_t, the input hidden of step t
+    float *GS;   // [nct][T][16][64][16]      obs stream activated gates, wave-0 lane layout
+    float *CS;   // [nct][T][16][64][4]       obs stream c_{t+1}
+    float *dZ;   // [512][C0]
+    float *QP;   // [3][nct][16][32][4]       partial (V, A0, A1, A2) of each workgroup's 8 head rows
+    float *DHP;  // [nct][T][16][32][128]     slot t: per-workgroup partials of dh_{t+1}
+    float *HP;   // [nct][kHpStride]          head gradient partials per column tile
+    float *LP;   // [nct][4]                  loss / q sums per column tile
+    float *W2P;  // [C0 / 32][kLowN]          W1 / b1 / W2 / b2 gradient partials per column tile
+    double* part;
+    int64_t* tstep;
+    int32_t* flags;  // [3][nct][16] forward | [3][nct][16] Q | [nct][16] backward | ticket
 };
 
-// workspace carve-up (floats unless noted), 64-float aligned pieces
-struct DrqnLayout {
-    int64_t off[40];
-    int n = 0;
+// workspace carve-up, 64-float aligned pieces
+struct DqLayout {
     int64_t total = 0;
     int64_t add(int64_t floats) {
-        off[n++] = total;
+        const int64_t o = total;
         total += (floats + 63) / 64 * 64;
-        return off[n - 1];
+        return o;
     }
 };
 
-inline int64_t drqn_layout(int B, int T, DrqnArgs* a, void* work) {
-    const int64_t C0 = (int64_t)T * B, ldh = (int64_t)(T + 1) * B;
-    DrqnLayout L;
-    const int64_t oX = L.add(7 * 2 * C0), oF1B = L.add(64 * 2 * C0), oF1T = L.add(64 * C0), oF2B = L.add(128 * 2 * C0),
-                  oF2T = L.add(128 * C0), oZxB = L.add(512 * 2 * C0), oZxT = L.add(512 * C0);
-    int64_t oHp[3], oCs[3];
-    for (int s = 0; s < 3; ++s) { oHp[s] = L.add(128 * ldh); oCs[s] = L.add(128 * ldh); }
-    const int64_t oG0 = L.add(512 * C0), oS0 = L.add(128 * B), oS1 = L.add(128 * B), oS2 = L.add(128 * B),
-                  odS = L.add(128 * B), odH0 = L.add(128 * B), odH1 = L.add(128 * B), odC0 = L.add(128 * B),
-                  odC1 = L.add(128 * B), odZ = L.add(512 * C0), odP2 = L.add(128 * C0), odP1 = L.add(64 * C0),
-                  oEB = L.add(E_N), oET = L.add(E_N), oA = L.add(B), oR = L.add(B), oD = L.add(B), oOne = L.add(4),
-                  oPart = L.add(2 * kNormBlocks), oTs = L.add(4);
-    const int64_t bytes = L.total * 4;
+inline int64_t dq_layout(int B, int T, DqArgs* a, void* work) {
+    const int64_t nct = B / 32, C0 = (int64_t)T * B;
+    DqLayout L;
+    const int64_t oZX = L.add(3 * nct * T * 16 * 1024), oHS = L.add(3 * nct * (T + 1) * 4096), oF1 = L.add(64 * C0),
+                  oF2 = L.add(128 * C0), oH = L.add(128 * C0), oGS = L.add(nct * T * 16 * 1024),
+                  oCS = L.add(nct * T * 16 * 256), odZ = L.add(512 * C0), oQP = L.add(3 * nct * 16 * 128),
+                  oDHP = L.add(nct * T * 16 * 4096), oHP = L.add(nct * kHpStride), oLP = L.add(nct * 4),
+                  oW2P = L.add(C0 / 32 * kLowN), oPart = L.add(2 * kNormBlocks), oTs = L.add(4),
+                  oFl = L.add(7 * nct * 16 + 4);
     if (a && work) {
         float* w = static_cast<float*>(work);
-        a->B = B; a->T = T; a->C0 = (int)C0; a->ldh = (int)ldh;
-        a->X = w + oX; a->F1B = w + oF1B; a->F1T = w + oF1T; a->F2B = w + oF2B; a->F2T = w + oF2T;
-        a->ZxB = w + oZxB; a->ZxT = w + oZxT;
-        a->Hp0 = w + oHp[0]; a->Hp1 = w + oHp[1]; a->Hp2 = w + oHp[2];
-        a->Cs0 = w + oCs[0]; a->Cs1 = w + oCs[1]; a->Cs2 = w + oCs[2];
-        a->G0 = w + oG0; a->S0 = w + oS0; a->S1 = w + oS1; a->S2 = w + oS2; a->dS = w + odS;
-        a->dH0 = w + odH0; a->dH1 = w + odH1; a->dC0 = w + odC0; a->dC1 = w + odC1;
-        a->dZ = w + odZ; a->dP2 = w + odP2; a->dP1 = w + odP1; a->effB = w + oEB; a->effT = w + oET;
-        a->a_last = reinterpret_cast<int32_t*>(w + oA); a->r_last = w + oR; a->d_last = w + oD; a->one = w + oOne;
-        a->part = reinterpret_cast<double*>(w + oPart); a->tstep = reinterpret_cast<int64_t*>(w + oTs);
+        a->B = B; a->T = T; a->nct = (int)nct; a->C0 = (int)C0;
+        a->ZX = w + oZX; a->HS = w + oHS; a->F1T = w + oF1; a->F2T = w + oF2; a->H = w + oH; a->GS = w + oGS;
+        a->CS = w + oCS; a->dZ = w + odZ; a->QP = w + oQP; a->DHP = w + oDHP; a->HP = w + oHP; a->LP = w + oLP;
+        a->W2P = w + oW2P; a->part = reinterpret_cast<double*>(w + oPart);
+        a->tstep = reinterpret_cast<int64_t*>(w + oTs); a->flags = reinterpret_cast<int32_t*>(w + oFl);
     }
-    return bytes;
+    return L.total * 4;
 }
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ bool skipped(const DqArgs& a) { return a.enable && *a.enable == 0; }
 
-// ---------------------------------------------------------------- prep
-__device__ __forceinline__ bool skipped(const DrqnArgs& a) { return a.enable && *a.enable == 0; }
+// ---------------------------------------------------------------- hand-off primitives
+// Write-through (sc1) 16-byte stores and loads through a buffer resource (MI355X_MICROARCH.md,
+// hand-off table row 1: every byte of a hand-off stored and loaded sc1, the flag an sc1 store by one
+// lane after the storing wave's vmcnt(0), the consumer's poll an sc1 load).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    typedef __attribute__((ext_vector_type(4))) float f4v;
+    const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, float4 v) { store_f4_sc1(r, byte_off, v); }
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void flag_set(int32_t* f, int v) {
+    __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Lanes [0, n) of the calling wave poll flags f[lane] (sc1 loads) until every one is >= need.
+// Bounded: a wait that never completes sets status bit 1 and returns (the update is then void).
+__device__ __forceinline__ void wait_flags(const int32_t* f, int n, int need, int lane, pm_drqn_stats* st) {
+    bool ok = lane >= n;
+    for (int it = 0; it < (1 << 21); ++it) {
+        if (!ok) ok = __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+        if (__all(ok)) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) atomicOr(&st->status, 2);
+}
 
-__global__ __launch_bounds__(256) void k_drqn_prep(DrqnArgs a) {
-    const int tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+// ---------------------------------------------------------------- 1: embedding + input projection
+// grid: 3 streams x nct column tiles x T steps x 4 row quarters; wave w computes the Zx tile of
+// recurrence workgroup m = 4 * quarter + w. Tile rows: row r' of workgroup m is gate r' >> 3 of LSTM
+// unit 8m + (r' & 7), i.e. Wih / Whh row 128 (r' >> 3) + 8m + (r' & 7).
+__global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
+    const int nct = a.nct, T = a.T, B = a.B;
+    int bid = blockIdx.x;
+    const int rq = bid & 3;
+    bid >>= 2;
+    const int t = bid % T;
+    bid /= T;
+    const int ct = bid % nct, s = bid / nct;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
+    if (blockIdx.x == 0)
+        for (int i = tid; i < 7 * nct * 16 + 4; i += 256) a.flags[i] = 0;
     if (skipped(a)) {  // this replica contributes nothing to the all-reduce
-        for (int i = tid; i < PM_RNN_NPARAM + 4; i += nt) a.grad[i] = 0.f;
+        for (int i = blockIdx.x * 256 + tid; i < PM_RNN_NPARAM + 4; i += gridDim.x * 256) a.grad[i] = 0.f;
         return;
     }
-    if (tid == 0) a.grad[PM_RNN_NPARAM] = 1.0f;
-    // effective heads: modelB train (mu + sigma * eps, NoisyLinear.forward :44-46), targetB eval (mu)
-    for (int i = tid; i < 2 * E_N; i += nt) {
-        const bool T = i >= E_N;
-        const int k = T ? i - E_N : i;
-        const float* p = T ? a.target : a.params;
-        int mu = -1, sg = 0, ep = 0;
-        if (k < E_SB) { mu = R_P_SWMU + k; sg = R_P_SWSG + k; ep = R_P_SWEP + k; }
-        else if (k < E_V) { mu = R_P_SBMU + k - E_SB; sg = R_P_SBSG + k - E_SB; ep = R_P_SBEP + k - E_SB; }
-        else if (k < E_VB) { mu = R_P_VWMU + k - E_V; sg = R_P_VWSG + k - E_V; ep = R_P_VWEP + k - E_V; }
-        else if (k == E_VB) { mu = R_P_VBMU; sg = R_P_VBSG; ep = R_P_VBEP; }
-        else if (k >= E_A && k < E_AB) { mu = R_P_AWMU + k - E_A; sg = R_P_AWSG + k - E_A; ep = R_P_AWEP + k - E_A; }
-        else if (k >= E_AB && k < E_AB + 3) { mu = R_P_ABMU + k - E_AB; sg = R_P_ABSG + k - E_AB; ep = R_P_ABEP + k - E_AB; }
-        float v = 0.f;
-        if (mu >= 0) v = T ? p[mu] : p[mu] + p[sg] * p[ep];
-        (T ? a.effT : a.effB)[k] = v;
-    }
-    // the batch, feature-major: X[i][t*B + b] = obs[b][t][i], X[i][C0 + t*B + b] = next[b][t][i]
-    const int B = a.B, Tn = a.T, C0 = a.C0;
-    for (int e = tid; e < 2 * C0 * 7; e += nt) {
-        const int i = e / (2 * C0), col = e % (2 * C0);
-        const int nx = col >= C0, cc = col - nx * C0, t = cc / B, b = cc % B;
-        a.X[e] = (nx ? a.next : a.obs)[((int64_t)b * Tn + t) * 7 + i];
-    }
-    for (int b = tid; b < B; b += nt) {
-        const int64_t j = (int64_t)b * Tn + Tn - 1;
-        a.a_last[b] = a.act[j];
-        a.r_last[b] = a.rew[j];
-        a.d_last[b] = a.done[j] ? 1.f : 0.f;
-    }
-    if (tid == 0) a.one[0] = 1.0f;
-}
-
-// ---------------------------------------------------------------- forward LSTM step
-// grid: 3 streams x (B/32) column tiles x 4 hidden blocks; wave q = gate q (torch order i, f, g, o)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_drqn_fwd(DrqnArgs a, int t) {
-    if (skipped(a)) return;
-    __shared__ float gate[4][32][33];
-    const int B = a.B, C0 = a.C0, ldh = a.ldh, nct = B / 32;
-    const int mb = blockIdx.x & 3, ct = (blockIdx.x >> 2) % nct, s = blockIdx.x / (4 * nct);
+    if (blockIdx.x == 0 && tid == 0) a.grad[PM_RNN_NPARAM] = 1.0f;
+    __shared__ __attribute__((aligned(16))) float F2s[32][132];
     const float* P = s == 2 ? a.target : a.params;
-    const float* Zx = s == 2 ? a.ZxT : a.ZxB;
-    const int64_t ldz = s == 2 ? C0 : 2 * C0;
-    const int zc = (s == 1 ? C0 : 0) + t * B + ct * 32;
-    float* Hp = s == 0 ? a.Hp0 : (s == 1 ? a.Hp1 : a.Hp2);
-    float* Cs = s == 0 ? a.Cs0 : (s == 1 ? a.Cs1 : a.Cs2);
-    const int q = threadIdx.x >> 6, lane = threadIdx.x & 63, r32 = lane & 31, h = lane >> 5;
-    const int g0 = q * 128 + 32 * mb;
-    gemm_f32x16 acc;
+    const int b = ct * 32 + col;
+    const int64_t c = (int64_t)t * B + b;
+    float xs[4];
+    tile_inputs((s == 0 ? a.obs : a.next) + ((int64_t)b * T + t) * 7, h, xs);
+    // F1 (both 32-row tiles, every wave): input k' = 2 s4 + h, k' = 0 the constant 1 (weight: b1)
+    f32x16 c1[2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = Zx[(int64_t)(g0 + (r & 3) + 8 * (r >> 2) + 4 * h) * ldz + zc + r32];
-    if (t > 0) {  // + Whh h_{t-1}: all 16 + 64 operand loads of the wave issued before the 64 MFMAs
-        const float* __restrict__ Wr = P + R_P_WHH + (int64_t)(g0 + r32) * 128;
-        const float* __restrict__ Hc = Hp + t * B + ct * 32 + r32;
-        float4 w4[16];
-        float hb[64];
+    for (int jt = 0; jt < 2; ++jt) {
+        const int row = 32 * jt + col;
+        c1[jt] = f32x16{};
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int k0 = 8 * j + 4 * h;
-            w4[j] = *reinterpret_cast<const float4*>(Wr + k0);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) hb[4 * j + e] = Hc[(int64_t)(k0 + e) * ldh];
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const int kk = 2 * s4 + h;
+            const float wv = kk == 0 ? P[R_P_F1B + row] : P[R_P_F1W + row * 7 + kk - 1];
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv, xs[s4], c1[jt], 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);  // keep every load ahead of the MFMA chain
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w4[j].x, hb[4 * j], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w4[j].y, hb[4 * j + 1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w4[j].z, hb[4 * j + 2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w4[j].w, hb[4 * j + 3], acc, 0, 0, 0);
-        }
+        for (int r = 0; r < 16; ++r) c1[jt][r] = relu(c1[jt][r]);
     }
+    // F2 tile w: rows 32w + rho(r) + 4h; K = 64 over the two F1 tiles (k = 32 t2 + rho(r) + 4h)
+    f32x16 f2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) f2[r] = P[R_P_F2B + 32 * w + rho(r) + 4 * h];
+    {
+        const float* w2 = P + R_P_F2W + (32 * w + col) * 64 + 4 * h;
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float4 v = *reinterpret_cast<const float4*>(w2 + 32 * t2 + 8 * i);
+                f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, c1[t2][4 * i + 0], f2, 0, 0, 0);
+                f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, c1[t2][4 * i + 1], f2, 0, 0, 0);
+                f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, c1[t2][4 * i + 2], f2, 0, 0, 0);
+                f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, c1[t2][4 * i + 3], f2, 0, 0, 0);
+            }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) f2[r] = relu(f2[r]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<float4*>(&F2s[col][32 * w + 8 * i + 4 * h]) =
+            make_float4(f2[4 * i], f2[4 * i + 1], f2[4 * i + 2], f2[4 * i + 3]);
+    if (s == 0 && rq == 0) {  // the obs stream's features for the weight gradients, [unit][column]
+        const int64_t C0 = a.C0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a.F2T[(int64_t)(32 * w + rho(r) + 4 * h) * C0 + c] = f2[r];
+        if (w < 2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a.F1T[(int64_t)(32 * w + rho(r) + 4 * h) * C0 + c] = c1[w][r];
+    }
+    __syncthreads();
+    // Zx tile of recurrence workgroup m: K = 128 with k = 8j + 4h + e for k-step (j, e)
+    const int m = 4 * rq + w;
+    f32x16 z;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const float v = acc[r];
-        gate[q][(r & 3) + 8 * (r >> 2) + 4 * h][r32] = q == 2 ? tanhf(v) : sigm(v);
+        const int rr = rho(r) + 4 * h;
+        const int g = 128 * (rr >> 3) + 8 * m + (rr & 7);
+        z[r] = P[R_P_BIH + g] + P[R_P_BHH + g];
     }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 1024; e += 256) {
-        const int u = e >> 5, c = e & 31, U = 32 * mb + u, col = ct * 32 + c;
-        const float gi = gate[0][u][c], gf = gate[1][u][c], gg = gate[2][u][c], go = gate[3][u][c];
-        const float cp = t > 0 ? Cs[(int64_t)U * ldh + t * B + col] : 0.f;
-        const float c2 = gf * cp + gi * gg;  // cy = forgetgate * cx + ingate * cellgate
-        const float h2 = go * tanhf(c2);
-        Cs[(int64_t)U * ldh + (t + 1) * B + col] = c2;
-        Hp[(int64_t)U * ldh + (t + 1) * B + col] = h2;
-        if (t == 0) { Cs[(int64_t)U * ldh + col] = 0.f; Hp[(int64_t)U * ldh + col] = 0.f; }
-        if (s == 0) {
-            const int64_t gc = (int64_t)t * B + col;
-            a.G0[(int64_t)U * C0 + gc] = gi;
-            a.G0[(int64_t)(128 + U) * C0 + gc] = gf;
-            a.G0[(int64_t)(256 + U) * C0 + gc] = gg;
-            a.G0[(int64_t)(384 + U) * C0 + gc] = go;
-        }
-    }
-}
-
-// ---------------------------------------------------------------- heads: Q, TD target, loss, dQ
-__global__ __launch_bounds__(256) void k_drqn_q(DrqnArgs a) {
-    if (skipped(a)) return;
-    __shared__ float Q[3][256][3];
-    __shared__ float dV[256], dA[256][3], lv[256], qv[256];
-    const int B = a.B, tid = threadIdx.x;
-    for (int e = tid; e < 3 * B; e += 256) {
-        const int s = e / B, b = e % B;
-        const float* eff = s == 2 ? a.effT : a.effB;
-        const float* S = s == 0 ? a.S0 : (s == 1 ? a.S1 : a.S2);
-        float v = 0.f, x0 = 0.f, x1 = 0.f, x2 = 0.f;
-#pragma unroll 16
-        for (int u = 0; u < 128; ++u) {
-            const float su = S[u * B + b];
-            v += eff[E_V + u] * su;
-            x0 += eff[E_A + u] * su;
-            x1 += eff[E_A + 128 + u] * su;
-            x2 += eff[E_A + 256 + u] * su;
-        }
-        v += eff[E_VB];
-        x0 += eff[E_AB]; x1 += eff[E_AB + 1]; x2 += eff[E_AB + 2];
-        const float mean = ((x0 + x1) + x2) / 3.0f;  // A.mean(dim=1)
-        Q[s][b][0] = v + (x0 - mean);
-        Q[s][b][1] = v + (x1 - mean);
-        Q[s][b][2] = v + (x2 - mean);
-    }
-    __syncthreads();
-    if (tid < B) {
-        const int b = tid, ac = a.a_last[b];
-        const float q = Q[0][b][ac];
-        const int as = argmax3(Q[1][b]);  // argmax Q_B(next) (first max)
-        const float y = a.r_last[b] + a.gamma * Q[2][b][as] * (1.0f - a.d_last[b]);
-        const float d = q - y, ad = fabsf(d);
-        lv[b] = ad < 1.0f ? 0.5f * d * d : ad - 0.5f;  // smooth_l1, beta 1
-        qv[b] = q;
-        const float gq = fminf(fmaxf(d, -1.0f), 1.0f) / (float)B;
-        dV[b] = gq;
+    const float* wr = P + R_P_WIH + (int64_t)(128 * (col >> 3) + 8 * m + (col & 7)) * 128 + 4 * h;
+    float4 av[16];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) dA[b][k] = (k == ac ? gq : 0.f) - gq / 3.0f;
-    }
-    __syncthreads();
-    float* g = a.grad;
-    if (tid == 0) {
-        float ls = 0.f, qs = 0.f;
-        for (int b = 0; b < B; ++b) { ls += lv[b]; qs += qv[b]; }
-        a.stats->loss = ls / (float)B;
-        a.stats->q_mean = qs / (float)B;
-    }
-    if (tid < 128) {
-        const int u = tid;
-        float gv = 0.f, g0 = 0.f, g1 = 0.f, g2 = 0.f;
-#pragma unroll 16
-        for (int b = 0; b < B; ++b) {
-            const float su = a.S0[u * B + b];
-            gv += dV[b] * su; g0 += dA[b][0] * su; g1 += dA[b][1] * su; g2 += dA[b][2] * su;
-        }
-        g[R_P_VWMU + u] = gv;
-        g[R_P_AWMU + u] = g0; g[R_P_AWMU + 128 + u] = g1; g[R_P_AWMU + 256 + u] = g2;
-    } else if (tid < 132) {
-        const int k = tid - 128;
-        float sacc = 0.f;
-        for (int b = 0; b < B; ++b) sacc += k == 0 ? dV[b] : dA[b][k - 1];
-        g[k == 0 ? R_P_VBMU : R_P_ABMU + k - 1] = sacc;
-    }
-    const float* eff = a.effB;
-    for (int e = tid; e < 128 * B; e += 256) {
-        const int u = e / B, b = e % B;
-        const float ds = eff[E_V + u] * dV[b] + eff[E_A + u] * dA[b][0] + eff[E_A + 128 + u] * dA[b][1] +
-                         eff[E_A + 256 + u] * dA[b][2];
-        a.dS[e] = a.S0[e] > 0.f ? ds : 0.f;
-    }
-}
-
-// ---------------------------------------------------------------- one BPTT step
-// grid: 4 unit tiles x (B/32) column tiles. dz_t for all 512 gate rows of the block's columns in
-// LDS; the block writes dz_t / dc_{t-1} for its own 32 units and dh_{t-1} = Whh^T dz_t for them.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_drqn_bwd(DrqnArgs a, int t) {
-    if (skipped(a)) return;
-    __shared__ float dz[512][33];
-    __shared__ float red[4][16][64];
-    const int B = a.B, C0 = a.C0, ldh = a.ldh, Tn = a.T;
-    const int mu = blockIdx.x & 3, ct = blockIdx.x >> 2;
-    const float* dHin = ((Tn - 1 - t) & 1) ? a.dH1 : a.dH0;
-    float* dHout = ((Tn - t) & 1) ? a.dH1 : a.dH0;
-    const float* dCin = ((Tn - 1 - t) & 1) ? a.dC1 : a.dC0;
-    float* dCout = ((Tn - t) & 1) ? a.dC1 : a.dC0;
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    const float* __restrict__ Wc = a.params + R_P_WHH + 32 * mu + (ln & 31);  // A(m = u_out, k = g) = Whh[g][u_out]
-    float wa[64];  // this wave's K quarter of the Whh column, loaded before the elementwise pass
-    if (t > 0) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) wa[4 * j + e] = Wc[(int64_t)(128 * wv + 8 * j + 4 * (ln >> 5) + e) * 128];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // 16 (unit, column) pairs per thread in two halves: the 8 operand loads of 8 pairs are issued
-    // before any of their stores (the workspace pointers may alias, so the compiler would not)
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        float v[8][8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int e = threadIdx.x + 256 * (8 * half + q);
-            const int u = e >> 5, col = ct * 32 + (e & 31);
-            const int64_t gc = (int64_t)t * B + col;
-            v[q][0] = dHin[u * B + col];
-            v[q][1] = t == Tn - 1 ? 0.f : dCin[u * B + col];
-            v[q][2] = a.G0[(int64_t)u * C0 + gc];
-            v[q][3] = a.G0[(int64_t)(128 + u) * C0 + gc];
-            v[q][4] = a.G0[(int64_t)(256 + u) * C0 + gc];
-            v[q][5] = a.G0[(int64_t)(384 + u) * C0 + gc];
-            v[q][6] = a.Cs0[(int64_t)u * ldh + (t + 1) * B + col];
-            v[q][7] = a.Cs0[(int64_t)u * ldh + t * B + col];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int e = threadIdx.x + 256 * (8 * half + q);
-            const int u = e >> 5, c = e & 31, col = ct * 32 + c;
-            const int64_t gc = (int64_t)t * B + col;
-            const float dh = v[q][0], dcc = v[q][1], gi = v[q][2], gf = v[q][3], gg = v[q][4], go = v[q][5];
-            const float cT = v[q][6], cp = v[q][7];
-            const float tc = tanhf(cT);
-            const float dc = dcc + dh * go * (1.0f - tc * tc);
-            const float dzi = dc * gg * (gi * (1.0f - gi));
-            const float dzf = dc * cp * (gf * (1.0f - gf));
-            const float dzg = dc * gi * (1.0f - gg * gg);
-            const float dzo = dh * tc * (go * (1.0f - go));
-            dz[u][c] = dzi; dz[128 + u][c] = dzf; dz[256 + u][c] = dzg; dz[384 + u][c] = dzo;
-            if ((u >> 5) == mu) {
-                a.dZ[(int64_t)u * C0 + gc] = dzi;
-                a.dZ[(int64_t)(128 + u) * C0 + gc] = dzf;
-                a.dZ[(int64_t)(256 + u) * C0 + gc] = dzg;
-                a.dZ[(int64_t)(384 + u) * C0 + gc] = dzo;
-                dCout[u * B + col] = dc * gf;
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
-    if (t == 0) return;  // dh_{-1} is not needed
-    const int w = wv, lane = ln, r32 = lane & 31, h = lane >> 5;
-    gemm_f32x16 acc = {};
+    for (int j = 0; j < 16; ++j) av[j] = *reinterpret_cast<const float4*>(wr + 8 * j);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        const int k0 = 128 * w + 8 * j + 4 * h;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + e], dz[k0 + e][r32], acc, 0, 0, 0);
+        const float4 bv = *reinterpret_cast<const float4*>(&F2s[col][8 * j + 4 * h]);
+        z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, bv.x, z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, bv.y, z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, bv.z, z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, bv.w, z, 0, 0, 0);
     }
+    float4* zx = reinterpret_cast<float4*>(a.ZX + ((((int64_t)s * nct + ct) * T + t) * 16 + m) * 1024) + lane;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[w][r][lane] = acc[r];
+    for (int i = 0; i < 4; ++i) zx[64 * i] = make_float4(z[4 * i], z[4 * i + 1], z[4 * i + 2], z[4 * i + 3]);
+}
+
+// ---------------------------------------------------------------- 2: the recurrence (persistent)
+struct RecurSmem {
+    float red[3][16][64];                            // partial accumulators of waves 1..3
+    __attribute__((aligned(16))) float dzs[4][64][4];  // BPTT: wave 0's dz fragments for the other waves
+    __attribute__((aligned(16))) float hT[32][132];  // h_T of this column tile [column][unit]
+    float dS[8][32];                                 // dS of this workgroup's 8 shared-head rows
+    float ws[8][128];                                // those rows of the effective W_S
+};
+
+__device__ __forceinline__ float eff_w(const float* P, int mu, int sg, int ep, bool noisy) {
+    return noisy ? P[mu] + P[sg] * P[ep] : P[mu];  // NoisyLinear: mu + sigma * epsilon (train), mu (eval)
+}
+
+__global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
+    if (skipped(a)) return;
+    __shared__ RecurSmem sm;
+    const int nct = a.nct, T = a.T, B = a.B;
+    int bid = blockIdx.x;
+    const int m = bid & 15;
+    bid >>= 4;
+    const int ct = bid % nct, so = bid / nct;
+    const int s = so == 2 ? 0 : so + 1;  // streams 1 and 2 first: the obs stream's group waits for them
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
+    const bool noisy = s != 2;  // modelB in train mode, targetB in eval mode
+    const float* P = s == 2 ? a.target : a.params;
+    const int64_t C0 = a.C0;
+    const int bcol = ct * 32 + col;
+    const int grp = s * nct + ct;
+    float* HSg = a.HS + (int64_t)grp * (T + 1) * 4096;
+    const __amdgpu_buffer_rsrc_t rHS = rsrc(HSg);
+    int32_t* fl = a.flags + grp * 16;
+    // this wave's Whh fragments: row 128 q + 8m + j of lane row col (q = col >> 3, j = col & 7), K quarter w
+    float wa[16];
+    {
+        const float* wr = P + R_P_WHH + (int64_t)(128 * (col >> 3) + 8 * m + (col & 7)) * 128 + 32 * w + 4 * h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 v = *reinterpret_cast<const float4*>(wr + 8 * j);
+            wa[4 * j] = v.x; wa[4 * j + 1] = v.y; wa[4 * j + 2] = v.z; wa[4 * j + 3] = v.w;
+        }
+    }
+    const float4* zx = reinterpret_cast<const float4*>(a.ZX + ((int64_t)grp * T * 16 + m) * 1024) + lane;
+    float cst[4] = {0.f, 0.f, 0.f, 0.f};  // wave 0: c of units 8m + 4h + e, column col
+    float4 zn[4];
+    if (w == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zn[i] = zx[64 * i];
+    // ---------------- forward
+    for (int t = 0; t < T; ++t) {
+        f32x16 acc = {};
+        if (w == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { acc[4 * i] = zn[i].x; acc[4 * i + 1] = zn[i].y; acc[4 * i + 2] = zn[i].z; acc[4 * i + 3] = zn[i].w; }
+            if (t + 1 < T)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) zn[i] = zx[(int64_t)(t + 1) * 16 * 256 + 64 * i];
+        }
+        if (t > 0) {
+            if (w == 0) wait_flags(fl, 16, t, lane, a.stats);
+            __syncthreads();  // h_t published by the whole group
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 hv = ld_sc1(rHS, ((t * 32 + col) * 128 + 32 * w + 8 * j + 4 * h) * 4);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + 0], hv.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + 1], hv.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + 2], hv.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + 3], hv.w, acc, 0, 0, 0);
+            }
+            if (w > 0)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sm.red[w - 1][r][lane] = acc[r];
+            __syncthreads();
+        }
+        if (w != 0) continue;
+        // wave 0: the cell of units 8m + 4h + e (gate q in register 4q + e), column col
+        float hn[4], gt[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float z = acc[r];
+            if (t > 0) z = ((z + sm.red[0][r][lane]) + sm.red[1][r][lane]) + sm.red[2][r][lane];
+            gt[r] = (r >> 2) == 2 ? tanhf(z) : sigm(z);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            cst[e] = gt[4 + e] * cst[e] + gt[e] * gt[8 + e];  // cy = forgetgate * cx + ingate * cellgate
+            hn[e] = gt[12 + e] * tanhf(cst[e]);
+        }
+        st_sc1(rHS, (((t + 1) * 32 + col) * 128 + 8 * m + 4 * h) * 4, make_float4(hn[0], hn[1], hn[2], hn[3]));
+        if (s == 0) {  // what BPTT and the weight gradients need of the obs stream
+            float4* g4 = reinterpret_cast<float4*>(a.GS + (((int64_t)ct * T + t) * 16 + m) * 1024) + lane;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) g4[64 * i] = make_float4(gt[4 * i], gt[4 * i + 1], gt[4 * i + 2], gt[4 * i + 3]);
+            reinterpret_cast<float4*>(a.CS + (((int64_t)ct * T + t) * 16 + m) * 256)[lane] =
+                make_float4(cst[0], cst[1], cst[2], cst[3]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float* hr = a.H + (int64_t)(8 * m + 4 * h + e) * C0 + bcol;
+                if (t + 1 < T) hr[(int64_t)(t + 1) * B] = hn[e];
+                if (t == 0) hr[0] = 0.f;
+            }
+        }
+        drain();
+        if (lane == 0) flag_set(fl + m, t + 1);
+    }
+    // ---------------- heads: rows 8m .. 8m+7 of the shared head (A rows duplicated x4 in the tile)
+    if (w == 0) wait_flags(fl, 16, T, lane, a.stats);
+    __syncthreads();  // h_T published
+    f32x16 sacc = {};
+    {
+        const int u = 8 * m + (col & 7);  // S row of lane row col
+        const int kb = 32 * w + 4 * h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 hv = ld_sc1(rHS, ((T * 32 + col) * 128 + kb + 8 * j) * 4);
+            *reinterpret_cast<float4*>(&sm.hT[col][kb + 8 * j]) = hv;
+            const int k0 = u * 128 + kb + 8 * j;
+            float wv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) wv[e] = eff_w(P, R_P_SWMU + k0 + e, R_P_SWSG + k0 + e, R_P_SWEP + k0 + e, noisy);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[0], hv.x, sacc, 0, 0, 0);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[1], hv.y, sacc, 0, 0, 0);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[2], hv.z, sacc, 0, 0, 0);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[3], hv.w, sacc, 0, 0, 0);
+        }
+    }
+    if (w > 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm.red[w - 1][r][lane] = sacc[r];
     __syncthreads();
-    for (int e = threadIdx.x; e < 1024; e += 256) {
-        const int r = e >> 6, ln = e & 63;
-        const int m = (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5), n = ln & 31;
-        dHout[(32 * mu + m) * B + ct * 32 + n] = ((red[0][r][ln] + red[1][r][ln]) + red[2][r][ln]) + red[3][r][ln];
+    // wave 0: S rows u_e = 8m + 4h + e (registers r = e), their V / A partials
+    float sv[4], sr[4];
+    float* QPs = a.QP + (int64_t)grp * 16 * 128;
+    if (w == 0) {
+        float pv = 0.f, pa0 = 0.f, pa1 = 0.f, pa2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int u = 8 * m + 4 * h + e;
+            const float z = ((sacc[e] + sm.red[0][e][lane]) + sm.red[1][e][lane]) + sm.red[2][e][lane];
+            sv[e] = z + eff_w(P, R_P_SBMU + u, R_P_SBSG + u, R_P_SBEP + u, noisy);
+            sr[e] = relu(sv[e]);
+            pv = fmaf(eff_w(P, R_P_VWMU + u, R_P_VWSG + u, R_P_VWEP + u, noisy), sr[e], pv);
+            pa0 = fmaf(eff_w(P, R_P_AWMU + u, R_P_AWSG + u, R_P_AWEP + u, noisy), sr[e], pa0);
+            pa1 = fmaf(eff_w(P, R_P_AWMU + 128 + u, R_P_AWSG + 128 + u, R_P_AWEP + 128 + u, noisy), sr[e], pa1);
+            pa2 = fmaf(eff_w(P, R_P_AWMU + 256 + u, R_P_AWSG + 256 + u, R_P_AWEP + 256 + u, noisy), sr[e], pa2);
+        }
+        pv += __shfl_xor(pv, 32);
+        pa0 += __shfl_xor(pa0, 32);
+        pa1 += __shfl_xor(pa1, 32);
+        pa2 += __shfl_xor(pa2, 32);
+        if (h == 0) st_sc1(rsrc(QPs), (m * 32 + col) * 16, make_float4(pv, pa0, pa1, pa2));
+        drain();
+        if (lane == 0) flag_set(a.flags + 3 * nct * 16 + grp * 16 + m, 1);
+    }
+    if (s != 0) return;  // block-uniform: the next-state streams are done
+    // ---------------- the loss and the head gradients (obs stream), on wave 0
+    float dV = 0.f, dA[3] = {0.f, 0.f, 0.f};
+    if (w == 0) {
+        const int32_t* fq = a.flags + 3 * nct * 16;
+        // lanes [0, 48): stream (lane >> 4), workgroup (lane & 15) of this column tile
+        {
+            const int sl = lane >> 4;
+            bool ok = lane >= 48;
+            for (int it = 0; it < (1 << 21); ++it) {
+                if (!ok) ok = __hip_atomic_load(fq + (sl * nct + ct) * 16 + (lane & 15), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) >= 1;
+                if (__all(ok)) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (it == (1 << 21) - 1 && lane == 0) atomicOr(&a.stats->status, 2);
+            }
+        }
+        float q[3][3];
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+            const float* QPst = a.QP + (int64_t)(st * nct + ct) * 16 * 128;
+            const __amdgpu_buffer_rsrc_t rq = rsrc(QPst);
+            float v = 0.f, x0 = 0.f, x1 = 0.f, x2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {  // this lane half's 8 workgroups, in order
+                const float4 p = ld_sc1(rq, ((8 * h + k) * 32 + col) * 16);
+                v += p.x; x0 += p.y; x1 += p.z; x2 += p.w;
+            }
+            v += __shfl_xor(v, 32);  // + the other half (commutative: both halves agree bit for bit)
+            x0 += __shfl_xor(x0, 32);
+            x1 += __shfl_xor(x1, 32);
+            x2 += __shfl_xor(x2, 32);
+            const float* Pst = st == 2 ? a.target : a.params;
+            const bool nz = st != 2;
+            v += eff_w(Pst, R_P_VBMU, R_P_VBSG, R_P_VBEP, nz);
+            x0 += eff_w(Pst, R_P_ABMU + 0, R_P_ABSG + 0, R_P_ABEP + 0, nz);
+            x1 += eff_w(Pst, R_P_ABMU + 1, R_P_ABSG + 1, R_P_ABEP + 1, nz);
+            x2 += eff_w(Pst, R_P_ABMU + 2, R_P_ABSG + 2, R_P_ABEP + 2, nz);
+            const float mean = ((x0 + x1) + x2) / 3.0f;  // A.mean(dim=1)
+            q[st][0] = v + (x0 - mean);
+            q[st][1] = v + (x1 - mean);
+            q[st][2] = v + (x2 - mean);
+        }
+        const int64_t jl = (int64_t)bcol * T + T - 1;  // the sequence's last step
+        const int ac = a.act[jl];
+        const float rl = a.rew[jl], dl = a.done[jl] ? 1.f : 0.f;
+        const float qa = ac == 0 ? q[0][0] : (ac == 1 ? q[0][1] : q[0][2]);
+        const int as = argmax3(q[1]);  // argmax Q_B(next) (first max)
+        const float y = rl + a.gamma * q[2][as] * (1.0f - dl);
+        const float d = qa - y, ad = fabsf(d);
+        float lv = ad < 1.0f ? 0.5f * d * d : ad - 0.5f;  // smooth_l1, beta 1
+        const float gq = fminf(fmaxf(d, -1.0f), 1.0f) / (float)B;
+        dV = gq;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dA[k] = (k == ac ? gq : 0.f) - gq / 3.0f;
+        if (m == 0) {  // loss / q sums of this column tile (lanes of half 0)
+            float qs = qa;
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) { lv += __shfl_xor(lv, o); qs += __shfl_xor(qs, o); }
+            if (lane == 0) { a.LP[ct * 4 + 0] = lv; a.LP[ct * 4 + 1] = qs; }
+        }
+        // dS of rows u_e (modelB's effective V / A weights), the head gradients of those rows
+        float* HPc = a.HP + (int64_t)ct * kHpStride;
+        float gv[4], ga[3][4], gb[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int u = 8 * m + 4 * h + e;
+            const float* Q = a.params;
+            const float ds = eff_w(Q, R_P_VWMU + u, R_P_VWSG + u, R_P_VWEP + u, true) * dV +
+                             eff_w(Q, R_P_AWMU + u, R_P_AWSG + u, R_P_AWEP + u, true) * dA[0] +
+                             eff_w(Q, R_P_AWMU + 128 + u, R_P_AWSG + 128 + u, R_P_AWEP + 128 + u, true) * dA[1] +
+                             eff_w(Q, R_P_AWMU + 256 + u, R_P_AWSG + 256 + u, R_P_AWEP + 256 + u, true) * dA[2];
+            const float dsm = sv[e] > 0.f ? ds : 0.f;
+            sm.dS[4 * h + e][col] = dsm;
+            gv[e] = dV * sr[e];
+            ga[0][e] = dA[0] * sr[e];
+            ga[1][e] = dA[1] * sr[e];
+            ga[2][e] = dA[2] * sr[e];
+            gb[e] = dsm;
+        }
+        // sums over the 32 columns of the half (fixed butterfly)
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                gv[e] += __shfl_xor(gv[e], o);
+                ga[0][e] += __shfl_xor(ga[0][e], o);
+                ga[1][e] += __shfl_xor(ga[1][e], o);
+                ga[2][e] += __shfl_xor(ga[2][e], o);
+                gb[e] += __shfl_xor(gb[e], o);
+            }
+        if (col == 0)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int u = 8 * m + 4 * h + e;
+                HPc[HP_V + u] = gv[e];
+                HPc[HP_A + u] = ga[0][e];
+                HPc[HP_A + 128 + u] = ga[1][e];
+                HPc[HP_A + 256 + u] = ga[2][e];
+                HPc[HP_BS + u] = gb[e];
+            }
+        if (m == 0) {
+            float sb = dV, sa0 = dA[0], sa1 = dA[1], sa2 = dA[2];
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) {
+                sb += __shfl_xor(sb, o); sa0 += __shfl_xor(sa0, o); sa1 += __shfl_xor(sa1, o); sa2 += __shfl_xor(sa2, o);
+            }
+            if (lane == 0) { HPc[HP_VB] = sb; HPc[HP_AB] = sa0; HPc[HP_AB + 1] = sa1; HPc[HP_AB + 2] = sa2; }
+        }
+    }
+    // this workgroup's rows of modelB's effective W_S (for dh_T)
+    for (int k = tid; k < 8 * 128; k += 256) {
+        const int u = 8 * m + (k >> 7), kk = k & 127, o = u * 128 + kk;
+        sm.ws[k >> 7][kk] = eff_w(a.params, R_P_SWMU + o, R_P_SWSG + o, R_P_SWEP + o, true);
+    }
+    __syncthreads();  // dS, h_T, ws
+    {   // dW_S rows (partial over this column tile): thread (k', row half)
+        const int kk = tid & 127, hr = tid >> 7;
+        float g4[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int c2 = 0; c2 < 32; ++c2) {
+            const float hv = sm.hT[c2][kk];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) g4[e] = fmaf(sm.dS[4 * hr + e][c2], hv, g4[e]);
+        }
+        float* HPc = a.HP + (int64_t)ct * kHpStride;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) HPc[HP_WS + (8 * m + 4 * hr + e) * 128 + kk] = g4[e];
+    }
+    const __amdgpu_buffer_rsrc_t rDH = rsrc(a.DHP + (int64_t)ct * T * 16 * 4096);
+    {   // dh_T partial over this workgroup's 8 rows: thread (column, 16 units)
+        const int c2 = tid >> 3, u0 = (tid & 7) * 16;
+        float o16[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o16[k] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float ds = sm.dS[r][c2];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) o16[k] = fmaf(sm.ws[r][u0 + k], ds, o16[k]);
+        }
+        const int base = (((T - 1) * 16 + m) * 32 + c2) * 128 + u0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st_sc1(rDH, (base + 4 * i) * 4, make_float4(o16[4 * i], o16[4 * i + 1], o16[4 * i + 2], o16[4 * i + 3]));
+    }
+    drain();
+    __syncthreads();
+    int32_t* fb = a.flags + 6 * nct * 16 + ct * 16;
+    if (tid == 0) flag_set(fb + m, 1);
+    // ---------------- BPTT
+    // Whh^T fragments of this wave's output tile (units u' = 32w + col): k-step r covers gate rows
+    // rho(r) + 4h of this workgroup's tile, i.e. Whh row 128 (r >> 2) + 8m + (r & 3) + 4h
+    float wt[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        wt[r] = a.params[R_P_WHH + (int64_t)(128 * (r >> 2) + 8 * m + (r & 3) + 4 * h) * 128 + 32 * w + col];
+    float dc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int t = T - 1; t >= 0; --t) {
+        float dz[16];
+        if (w == 0) {
+            const float4* g4 = reinterpret_cast<const float4*>(a.GS + (((int64_t)ct * T + t) * 16 + m) * 1024) + lane;
+            float gt[16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float4 v = g4[64 * i];
+                gt[4 * i] = v.x; gt[4 * i + 1] = v.y; gt[4 * i + 2] = v.z; gt[4 * i + 3] = v.w;
+            }
+            const float4 cn = reinterpret_cast<const float4*>(a.CS + (((int64_t)ct * T + t) * 16 + m) * 256)[lane];
+            const float4 cp = t > 0 ? reinterpret_cast<const float4*>(a.CS + (((int64_t)ct * T + t - 1) * 16 + m) * 256)[lane]
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float cT[4] = {cn.x, cn.y, cn.z, cn.w}, cP[4] = {cp.x, cp.y, cp.z, cp.w};
+            wait_flags(fb, 16, T - t, lane, a.stats);
+            float dh[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {  // the 16 workgroups' partials of dh_{t+1}, in order
+                const float4 p = ld_sc1(rDH, (((t * 16 + k) * 32 + col) * 128 + 8 * m + 4 * h) * 4);
+                dh[0] += p.x; dh[1] += p.y; dh[2] += p.z; dh[3] += p.w;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float gi = gt[e], gf = gt[4 + e], gg = gt[8 + e], go = gt[12 + e];
+                const float tc = tanhf(cT[e]);
+                const float dcc = dc[e] + dh[e] * go * (1.0f - tc * tc);
+                dz[e] = dcc * gg * (gi * (1.0f - gi));
+                dz[4 + e] = dcc * cP[e] * (gf * (1.0f - gf));
+                dz[8 + e] = dcc * gi * (1.0f - gg * gg);
+                dz[12 + e] = dh[e] * tc * (go * (1.0f - go));
+                dc[e] = dcc * gf;
+            }
+            const int64_t cc = (int64_t)t * B + bcol;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a.dZ[(int64_t)(128 * (r >> 2) + 8 * m + 4 * h + (r & 3)) * C0 + cc] = dz[r];
+            if (t > 0)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    *reinterpret_cast<float4*>(&sm.dzs[i][lane][0]) = make_float4(dz[4 * i], dz[4 * i + 1], dz[4 * i + 2], dz[4 * i + 3]);
+        }
+        if (t == 0) break;  // dh_0 (the zero initial state) is not needed
+        __syncthreads();  // dz fragments
+        if (w != 0)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float4 v = *reinterpret_cast<const float4*>(&sm.dzs[i][lane][0]);
+                dz[4 * i] = v.x; dz[4 * i + 1] = v.y; dz[4 * i + 2] = v.z; dz[4 * i + 3] = v.w;
+            }
+        f32x16 acc = {};
+        // r-th k-step: this workgroup's gate rows rho(r) + 4h (the accumulator layout of dz)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wt[r], dz[r], acc, 0, 0, 0);
+        const int base = (((t - 1) * 16 + m) * 32 + col) * 128 + 32 * w + 4 * h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            st_sc1(rDH, (base + 8 * i) * 4, make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]));
+        drain();
+        __syncthreads();
+        if (tid == 0) flag_set(fb + m, T - t + 1);
+    }
+}
+
+// ---------------------------------------------------------------- 3: weight gradients
+struct WgSmem {
+    union {
+        float red[16][16][64];          // type A: per-wave partial tiles
+        struct {
+            float red2[4][128][33];     // type B: dF2 K-quarter partials, later dF1 partials
+            float dP2[128][33];
+            float dP1[64][33];
+            float F1s[64][33];
+        } b;
+    };
+    float rs[16][64];
+    int last;
+};
+
+__global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
+    if (skipped(a)) return;
+    __shared__ WgSmem sm;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
+    const int64_t C0 = a.C0;
+    const int B = a.B, T = a.T, nct = a.nct;
+    const int nB = a.C0 / 32;
+    int bid = blockIdx.x;
+    if (bid < kWgA) {
+        // ---- dWih (mat 0) / dWhh (mat 1) tile: rows g in [32 gt, +32), columns k' in [32 kt, +32)
+        const int mat = bid >> 6, gt = (bid >> 2) & 15, kt = bid & 3;
+        const float* Ar = a.dZ + (int64_t)(32 * gt + col) * C0 + 4 * h;
+        const float* Br = (mat == 0 ? a.F2T : a.H) + (int64_t)(32 * kt + col) * C0 + 4 * h;
+        f32x16 acc = {};
+        float rsum = 0.f;
+        for (int kc = w; kc * 8 < C0; kc += 16) {  // 8-column chunks, round robin over the waves
+            const float4 av = *reinterpret_cast<const float4*>(Ar + 8 * kc);
+            const float4 bv = *reinterpret_cast<const float4*>(Br + 8 * kc);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
+            rsum += ((av.x + av.y) + av.z) + av.w;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sm.red[w][r][lane] = acc[r];
+        sm.rs[w][lane] = rsum;
+        __syncthreads();
+        if (w == 0) {
+            float* G = a.grad + (mat == 0 ? R_P_WIH : R_P_WHH);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float v = sm.red[0][r][lane];
+                for (int k = 1; k < 16; ++k) v += sm.red[k][r][lane];
+                G[(int64_t)(32 * gt + rho(r) + 4 * h) * 128 + 32 * kt + col] = v;
+            }
+            if (mat == 0 && kt == 0) {  // db_ih = db_hh = row sums of dZ
+                float v = sm.rs[0][lane];
+                for (int k = 1; k < 16; ++k) v += sm.rs[k][lane];
+                v += __shfl_xor(v, 32);
+                if (h == 0) { a.grad[R_P_BIH + 32 * gt + col] = v; a.grad[R_P_BHH + 32 * gt + col] = v; }
+            }
+        }
+        return;
+    }
+    bid -= kWgA;
+    if (bid < nB) {
+        // ---- column tile: columns [c0, c0 + 32) (one time step t, batch rows b0 .. b0 + 31)
+        const int64_t c0 = (int64_t)bid * 32;
+        const int t = (int)(c0 / B), b0 = (int)(c0 % B);
+        // dF2 = Wih^T dZ: wave (out tile ot = w & 3, K quarter kq = w >> 2), k = g = 128 kq + 2p + h
+        {
+            const int ot = w & 3, kq = w >> 2;
+            f32x16 acc = {};
+            const float* Wc = a.params + R_P_WIH + 32 * ot + col;
+            const float* Zc = a.dZ + c0 + col;
+#pragma unroll 8
+            for (int p = 0; p < 64; ++p) {
+                const int g = 128 * kq + 2 * p + h;
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Wc[(int64_t)g * 128], Zc[(int64_t)g * C0], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sm.b.red2[kq][32 * ot + rho(r) + 4 * h][col] = acc[r];
+        }
+        for (int k = tid; k < 64 * 32; k += 1024) sm.b.F1s[k >> 5][k & 31] = a.F1T[(int64_t)(k >> 5) * C0 + c0 + (k & 31)];
+        __syncthreads();
+        for (int k = tid; k < 128 * 32; k += 1024) {
+            const int u = k >> 5, c2 = k & 31;
+            const float v = ((sm.b.red2[0][u][c2] + sm.b.red2[1][u][c2]) + sm.b.red2[2][u][c2]) + sm.b.red2[3][u][c2];
+            sm.b.dP2[u][c2] = a.F2T[(int64_t)u * C0 + c0 + c2] > 0.f ? v : 0.f;  // through the ReLU
+        }
+        __syncthreads();
+        float* Wp = a.W2P + (int64_t)bid * kLowN;
+        {   // dW2 partial [k'][j] = sum_c dP2[k'][c] F1[j][c]; db2 partial
+            const int u = tid >> 3, j0 = (tid & 7) * 8;
+            float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int c2 = 0; c2 < 32; ++c2) {
+                const float d = sm.b.dP2[u][c2];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) o8[k] = fmaf(d, sm.b.F1s[j0 + k][c2], o8[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) Wp[R_P_F2W + u * 64 + j0 + k] = o8[k];
+            if ((tid & 7) == 0) {
+                float sb = 0.f;
+                for (int c2 = 0; c2 < 32; ++c2) sb += sm.b.dP2[u][c2];
+                Wp[R_P_F2B + u] = sb;
+            }
+        }
+        {   // dF1 = W2^T dP2: wave (out tile jt = w & 1, K eighth ke = w >> 1), k = k' = 16 ke + 2p + h
+            const int jt = w & 1, ke = w >> 1;
+            f32x16 acc = {};
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int k = 16 * ke + 2 * p + h;
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.params[R_P_F2W + k * 64 + 32 * jt + col], sm.b.dP2[k][col], acc, 0, 0, 0);
+            }
+            __syncthreads();  // red2 is free again (the dP2 pass is done)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sm.b.red2[ke >> 1][(ke & 1) * 64 + 32 * jt + rho(r) + 4 * h][col] = acc[r];
+        }
+        __syncthreads();
+        for (int k = tid; k < 64 * 32; k += 1024) {
+            const int j = k >> 5, c2 = k & 31;
+            float v = 0.f;
+#pragma unroll
+            for (int ke = 0; ke < 8; ++ke) v += sm.b.red2[ke >> 1][(ke & 1) * 64 + j][c2];
+            sm.b.dP1[j][c2] = sm.b.F1s[j][c2] > 0.f ? v : 0.f;
+        }
+        __syncthreads();
+        if (tid < 448) {  // dW1 partial [j][i] = sum_c dP1[j][c] x_i[c]
+            const int j = tid / 7, i = tid % 7;
+            float v = 0.f;
+            for (int c2 = 0; c2 < 32; ++c2) v = fmaf(sm.b.dP1[j][c2], a.obs[((int64_t)(b0 + c2) * T + t) * 7 + i], v);
+            Wp[R_P_F1W + j * 7 + i] = v;
+        } else if (tid < 512) {
+            const int j = tid - 448;
+            float v = 0.f;
+            for (int c2 = 0; c2 < 32; ++c2) v += sm.b.dP1[j][c2];
+            Wp[R_P_F1B + j] = v;
+        }
+        // arrival ticket: the last column tile sums every tile's partials in tile order
+        drain();
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            drain();
+            const int k = atomicAdd(a.flags + 7 * nct * 16, 1);
+            sm.last = k == nB - 1;
+            if (sm.last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            drain();
+        }
+        __syncthreads();
+        if (!sm.last) return;
+        for (int i = tid; i < kLowN; i += 1024) {
+            float v = 0.f;
+            for (int k = 0; k < nB; ++k) v += a.W2P[(int64_t)k * kLowN + i];
+            a.grad[i] = v;
+        }
+        return;
+    }
+    bid -= nB;
+    // ---- head partials: sum over column tiles in order
+    const int per = (HP_N + kWgC - 1) / kWgC, lo = bid * per, hi = min(HP_N, lo + per);
+    for (int i = lo + tid; i < hi; i += 1024) {
+        float v = 0.f;
+        for (int k = 0; k < nct; ++k) v += a.HP[(int64_t)k * kHpStride + i];
+        int dst;
+        if (i < HP_BS) dst = R_P_SWMU + i;
+        else if (i < HP_V) dst = R_P_SBMU + i - HP_BS;
+        else if (i < HP_VB) dst = R_P_VWMU + i - HP_V;
+        else if (i == HP_VB) dst = R_P_VBMU;
+        else if (i < HP_AB) dst = R_P_AWMU + i - HP_A;
+        else dst = R_P_ABMU + i - HP_AB;
+        a.grad[dst] = v;
+    }
+    if (bid == 0 && tid == 0) {
+        float ls = 0.f, qs = 0.f;
+        for (int k = 0; k < nct; ++k) { ls += a.LP[k * 4]; qs += a.LP[k * 4 + 1]; }
+        a.stats->loss = ls / (float)B;
+        a.stats->q_mean = qs / (float)B;
     }
 }
 
@@ -370,7 +795,7 @@ __device__ __forceinline__ int sigma_source(int i, int& ep) {
 }
 
 // ---------------------------------------------------------------- clip + Adam
-__global__ __launch_bounds__(256) void k_drqn_norm(DrqnArgs a) {
+__global__ __launch_bounds__(256) void k_drqn_norm(DqArgs a) {
     __shared__ double red[256];
     const float ranks = a.grad[PM_RNN_NPARAM];  // replicas that contributed (summed by the all-reduce)
     if (!(ranks > 0.f)) return;
@@ -411,7 +836,7 @@ struct AdamK {
     int64_t interval;
 };
 
-__global__ __launch_bounds__(256) void k_drqn_adam(DrqnArgs a, AdamK k, float* params, float* target, float* m_,
+__global__ __launch_bounds__(256) void k_drqn_adam(DqArgs a, AdamK k, float* params, float* target, float* m_,
                                                    float* v_) {
     __shared__ float cf[3];
     __shared__ int64_t ts_s;
@@ -474,80 +899,33 @@ int check(const pm_drqn* d) {
 using namespace pm;
 
 extern "C" int64_t pm_drqn_work_bytes(int32_t batch, int32_t T) {
-    if (batch < 1 || T < 1) return -1;
-    return drqn_layout(batch, T, nullptr, nullptr);
+    if (batch < 32 || batch % 32 || T < 1) return -1;
+    return dq_layout(batch, T, nullptr, nullptr);
 }
 
 extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     if (int rc = check(d)) return rc;
     PM_REQUIRE(d->obs && d->next && d->act && d->rew && d->done, PM_E_ARG, "pm_drqn_grads: null batch");
     hipStream_t st = pm_stream(stream);
-    DrqnArgs a{};
-    drqn_layout(d->batch, d->T, &a, d->work);
+    DqArgs a{};
+    dq_layout(d->batch, d->T, &a, d->work);
     a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats; a.enable = d->enable;
     a.obs = d->obs; a.next = d->next; a.act = d->act; a.rew = d->rew; a.done = d->done;
     a.gamma = (float)d->gamma;
-    const int B = a.B, C0 = a.C0, ldh = a.ldh, T = a.T, nct = B / 32;
-    const float *PB = d->params, *PT = d->target;
-    float* g = d->grad;
-    hipLaunchKernelGGL(k_drqn_prep, dim3(64), dim3(256), 0, st, a);
-    PM_LAUNCHED("k_drqn_prep");
-    // embedding: modelB on [obs | next] (2*C0 columns), targetB on next (C0 columns)
-    GemmProb p[kGemmMax];
-    p[0] = gemm_prob(PB + R_P_F1W, 7, 1, a.X, 2 * C0, 1, a.F1B, 2 * C0, 1, 64, 2 * C0, 7, GF_RELU, PB + R_P_F1B);
-    p[1] = gemm_prob(PT + R_P_F1W, 7, 1, a.X + C0, 2 * C0, 1, a.F1T, C0, 1, 64, C0, 7, GF_RELU, PT + R_P_F1B);
-    PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (F1)");
-    p[0] = gemm_prob(PB + R_P_F2W, 64, 1, a.F1B, 2 * C0, 1, a.F2B, 2 * C0, 1, 128, 2 * C0, 64, GF_RELU, PB + R_P_F2B);
-    p[1] = gemm_prob(PT + R_P_F2W, 64, 1, a.F1T, C0, 1, a.F2T, C0, 1, 128, C0, 64, GF_RELU, PT + R_P_F2B);
-    PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (F2)");
-    p[0] = gemm_prob(PB + R_P_WIH, 128, 1, a.F2B, 2 * C0, 1, a.ZxB, 2 * C0, 1, 512, 2 * C0, 128, 0, PB + R_P_BIH,
-                     PB + R_P_BHH);
-    p[1] = gemm_prob(PT + R_P_WIH, 128, 1, a.F2T, C0, 1, a.ZxT, C0, 1, 512, C0, 128, 0, PT + R_P_BIH, PT + R_P_BHH);
-    PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (Zx)");
-    for (int t = 0; t < T; ++t) {
-        hipLaunchKernelGGL(k_drqn_fwd, dim3(3 * nct * 4), dim3(256), 0, st, a, t);
-        PM_LAUNCHED("k_drqn_fwd");
-    }
-    // shared head on h_T (column T*B of the histories)
-    const int64_t hT = (int64_t)T * B;
-    p[0] = gemm_prob(a.effB + E_S, 128, 1, a.Hp0 + hT, ldh, 1, a.S0, B, 1, 128, B, 128, GF_RELU, a.effB + E_SB);
-    p[1] = gemm_prob(a.effB + E_S, 128, 1, a.Hp1 + hT, ldh, 1, a.S1, B, 1, 128, B, 128, GF_RELU, a.effB + E_SB);
-    p[2] = gemm_prob(a.effT + E_S, 128, 1, a.Hp2 + hT, ldh, 1, a.S2, B, 1, 128, B, 128, GF_RELU, a.effT + E_SB);
-    PM_REQUIRE(gemm_launch(p, 3, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (S)");
-    hipLaunchKernelGGL(k_drqn_q, dim3(1), dim3(256), 0, st, a);
-    PM_LAUNCHED("k_drqn_q");
-    p[0] = gemm_prob(a.dS, B, 1, a.Hp0 + hT, 1, ldh, g + R_P_SWMU, 128, 1, 128, 128, B);  // dW_S = dS h_T^T
-    p[1] = gemm_prob(a.dS, B, 1, a.one, 0, 0, g + R_P_SBMU, 1, 0, 128, 1, B);             // db_S
-    p[2] = gemm_prob(a.effB + E_S, 1, 128, a.dS, B, 1, a.dH0, B, 1, 128, B, 128);          // dh_T = W_S^T dS
-    PM_REQUIRE(gemm_launch(p, 3, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dS)");
-    for (int t = T - 1; t >= 0; --t) {
-        hipLaunchKernelGGL(k_drqn_bwd, dim3(4 * nct), dim3(256), 0, st, a, t);
-        PM_LAUNCHED("k_drqn_bwd");
-    }
-    // weight gradients over all T*B columns of the obs stream
-    p[0] = gemm_prob(a.dZ, C0, 1, a.F2B, 1, 2 * C0, g + R_P_WIH, 128, 1, 512, 128, C0);  // dWih = dZ F2^T
-    p[1] = gemm_prob(a.dZ, C0, 1, a.Hp0, 1, ldh, g + R_P_WHH, 128, 1, 512, 128, C0);     // dWhh = dZ H_{t-1}^T
-    p[2] = gemm_prob(a.dZ, C0, 1, a.one, 0, 0, g + R_P_BIH, 1, 0, 512, 1, C0);           // db_ih
-    p[3] = gemm_prob(a.dZ, C0, 1, a.one, 0, 0, g + R_P_BHH, 1, 0, 512, 1, C0);           // db_hh
-    p[4] = gemm_prob(PB + R_P_WIH, 1, 128, a.dZ, C0, 1, a.dP2, C0, 1, 128, C0, 512, 0, nullptr, nullptr, a.F2B,
-                     2 * C0, 1);  // dF2 = Wih^T dZ, through the ReLU
-    PM_REQUIRE(gemm_launch(p, 5, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dZ)");
-    p[0] = gemm_prob(a.dP2, C0, 1, a.F1B, 1, 2 * C0, g + R_P_F2W, 64, 1, 128, 64, C0);  // dW2
-    p[1] = gemm_prob(a.dP2, C0, 1, a.one, 0, 0, g + R_P_F2B, 1, 0, 128, 1, C0);         // db2
-    p[2] = gemm_prob(PB + R_P_F2W, 1, 64, a.dP2, C0, 1, a.dP1, C0, 1, 64, C0, 128, 0, nullptr, nullptr, a.F1B, 2 * C0,
-                     1);  // dF1 = W2^T dF2, through the ReLU
-    PM_REQUIRE(gemm_launch(p, 3, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dP2)");
-    p[0] = gemm_prob(a.dP1, C0, 1, a.X, 1, 2 * C0, g + R_P_F1W, 7, 1, 64, 7, C0);  // dW1
-    p[1] = gemm_prob(a.dP1, C0, 1, a.one, 0, 0, g + R_P_F1B, 1, 0, 64, 1, C0);     // db1
-    PM_REQUIRE(gemm_launch(p, 2, st, d->enable) == hipSuccess, PM_E_LAUNCH, "k_gemm (dP1)");
+    hipLaunchKernelGGL(k_dq_embed, dim3(3 * a.nct * a.T * 4), dim3(256), 0, st, a);
+    PM_LAUNCHED("k_dq_embed");
+    pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(3 * a.nct * kG), dim3(256), st, a);
+    PM_LAUNCHED("k_dq_recur");
+    hipLaunchKernelGGL(k_dq_wgrad, dim3(kWgA + a.C0 / 32 + kWgC), dim3(1024), 0, st, a);
+    PM_LAUNCHED("k_dq_wgrad");
     return PM_OK;
 }
 
 extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) {
     if (int rc = check(d)) return rc;
     hipStream_t st = pm_stream(stream);
-    DrqnArgs a{};
-    drqn_layout(d->batch, d->T, &a, d->work);
+    DqArgs a{};
+    dq_layout(d->batch, d->T, &a, d->work);
     a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats;
     hipLaunchKernelGGL(k_drqn_norm, dim3(kNormBlocks), dim3(256), 0, st, a);
     PM_LAUNCHED("k_drqn_norm");

@@ -1,0 +1,160 @@
+// K9 — inference-only self-play rollout, K vector steps per launch (BASELINE configs[1]).
+//
+// The rollout of scripts/train_iterative.py:239-242 without learning, for n arenas in lockstep: per
+// vector step both players act — modelA greedy on its folded weights (:240; modelA keeps NoisyNet's
+// frozen epsilon buffers), modelB NoisyNet with fresh noise per vector step shared by all arenas
+// (reset_noise in select_action_B, :125) and epsilon-greedy (:126-130) — then PongEnv2P.step ticks
+// every arena and finished ones are served again (the step-keyed Philox serve of pm_env_step's
+// production autoreset). Stepped as launches, one vector step is three kernels (fold, act, env) that
+// move the fp64 state and the observations through HBM; here every arena stays in registers for all
+// K steps and only its final state leaves the CU.
+//
+// Two kernels per launch:
+//   k_rollout_heads — one block per step folds modelB's heads with that step's noise (gen_noise +
+//     fold_heads_from, exactly pm_qnet_fold FRESH) into the F_H/F_BH fragment order: 264 floats per
+//     step in a caller workspace (PM_ROLL_HEADS);
+//   k_rollout — a block of 2 waves owns one tile of 32 arenas: wave 0 plays A, wave 1 plays B (two
+//     SIMDs, so the two 72-MFMA forwards of a step run side by side). Both waves keep the same fp64
+//     arena in both lane halves (the MFMA tile layout gives column lane & 31 to both), exchange the
+//     step's actions through LDS behind one barrier and tick identically. Wave B streams the next
+//     step's heads global -> LDS (global_load_lds, 1 KB, double-buffered) while it computes the
+//     current step, so the heads never cost a round trip on the step's critical path.
+//
+// Bit-identical to `steps` repetitions of pm_qnet_fold(paramsB, FRESH, seed_net, c) ->
+// pm_qnet_act({wA}, NULL, w_B, obsA, obsB, epsilon, seed_env, c) -> pm_env_step(autoreset, seed_env,
+// c) with c = counter0 + s (tests/test_gpu_rollout.py).
+#include "pm_host.h"
+#include "pm_mfma.h"
+
+using namespace pm;
+
+namespace {
+
+constexpr int kRollBlock = 128;  // wave 0: player A, wave 1: player B, one tile of 32 arenas
+constexpr int kHeadsBlock = 256;
+static_assert(PM_ROLL_HEADS == 264, "heads workspace stride: 256 fragment floats + 4 biases + 4 pad");
+
+__global__ __launch_bounds__(kHeadsBlock) void k_rollout_heads(const float* __restrict__ paramsB, uint64_t seed_net,
+                                                               uint64_t counter0, float* __restrict__ ws) {
+    __shared__ float noise[132];
+    __shared__ float heads[260];
+    gen_noise(seed_net, TAG_NOISE_ACT, counter0 + blockIdx.x, noise, threadIdx.x, blockDim.x);
+    __syncthreads();
+    fold_heads_from(paramsB + PM_QNET_HEAD_OFF, nullptr, noise, PM_FOLD_TRAIN_FRESH, heads, nullptr, threadIdx.x,
+                    blockDim.x);
+    __syncthreads();
+    float* hf = ws + (size_t)blockIdx.x * PM_ROLL_HEADS;
+    heads_to_frags(heads, hf);
+    if (threadIdx.x < 4) hf[260 + threadIdx.x] = 0.f;
+}
+
+struct RollShared {
+    float lw[kLwFloats];   // modelA's fragment image
+    float lwB[kLwFloats];  // modelB's feature fragments (its heads come from hf)
+    float hf[2][320];      // modelB's heads of the step (fragment order, 256 + biases), double-buffered
+    int act[2][2][32];     // [step & 1][player][column]
+    long long red[2][4];
+};
+
+// Stream step t's heads (PM_ROLL_HEADS floats at ws + t * PM_ROLL_HEADS) into dst: one 16-byte and one
+// 4-byte global_load_lds (the latter's tail lanes re-read the biases' pad). Wave-wide; completes at
+// the issuing wave's next vmcnt(0).
+__device__ __forceinline__ void fetch_heads(const float* __restrict__ ws, int t, float* dst, int lane) {
+    const float* src = ws + (size_t)t * PM_ROLL_HEADS;
+    __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(src) + lane), (lds_void*)dst, 16,
+                                     0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 256 + (lane & 7)), (lds_void*)(dst + 256), 4, 0, 0);
+}
+
+__global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, const pm_env_state s,
+                                                        const float* __restrict__ wA, const float* __restrict__ wB,
+                                                        const float* __restrict__ ws, double eps, uint64_t seed_env,
+                                                        uint64_t counter0, int steps, float* __restrict__ obsA,
+                                                        float* __restrict__ obsB, long long* __restrict__ stats,
+                                                        int n) {
+    __shared__ __attribute__((aligned(16))) RollShared sm;
+    const int lane = threadIdx.x & 63, player = threadIdx.x >> 6, col = lane & 31;
+    const int i = blockIdx.x * 32 + col;
+    const bool valid = i < n;
+    stage_frags_lds(wA, sm.lw, blockIdx.x);  // block-wide: chunks spread over both waves
+    stage_frags_lds(wB, sm.lwB, blockIdx.x + kLwChunks / 2);
+    if (player) fetch_heads(ws, 0, sm.hf[0], lane);
+    Arena a = load_arena(s, valid ? i : n - 1);
+    const float* lw = player ? sm.lwB : sm.lw;
+    long long fin = 0, winB = 0, ptA = 0, ptB = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // both images and step 0's heads in LDS
+    for (int st = 0; st < steps; ++st) {
+        const uint64_t ctr = counter0 + (uint64_t)st;
+        if (player && st + 1 < steps) fetch_heads(ws, st + 1, sm.hf[(st + 1) & 1], lane);  // lands during the MFMAs
+        float oA[7], oB[7];
+        observe(a, oA, oB);
+        float xs[4];
+        tile_inputs(player ? oB : oA, lane >> 5, xs);
+        f32x16 c2[2];
+        tile_hidden(lw, xs, lane, c2);
+        float q[3];
+        tile_heads(player ? sm.hf[st & 1] : sm.lw + F_H, c2, lane, q);
+        int act = argmax3(q);
+        if (player) {  // random.random() < eps ? randint(0, 2) : argmax (train_iterative.py:126-130)
+            const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed_env);
+            if (u53(rr.x, rr.y) < eps) act = (int)below(rr.z, 3u);
+        }
+        if (lane < 32) sm.act[st & 1][player][col] = act;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave B: the next step's heads have landed
+        __syncthreads();  // both players' actions
+        const int aA = sm.act[st & 1][0][col], aB = sm.act[st & 1][1][col];
+        float rA, rB;
+        const int d = tick(p, a, aA, aB, rA, rB);
+        ptA += rA > 0.f ? 1 : 0;
+        ptB += rB > 0.f ? 1 : 0;
+        if (d) {  // env.reset() with K1's step-keyed production serve
+            fin += 1;
+            winB += rB > 0.f ? 1 : 0;
+            ServeDraw sv = serve_draw(p, (uint32_t)i, (uint32_t)ctr, seed_env, TAG_SERVE_STEP, (uint32_t)(ctr >> 32));
+            serve_finish(sv);
+            serve(a, sv.vx, sv.vy, sv.spin);
+        }
+    }
+    if (player == 0 && lane < 32 && valid) {  // wave A writes the arenas and their observations
+        store_arena(s, i, a);
+        float oA[7], oB[7];
+        observe(a, oA, oB);
+        store_row7(obsA + (size_t)i * 7, oA);
+        store_row7(obsB + (size_t)i * 7, oB);
+    }
+    if (!stats) return;  // block-uniform
+    const bool mine = player == 0 && lane < 32 && valid;  // one lane per arena
+    long long v[4] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    }
+    if (player == 0 && lane < 4) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane),
+                                           (unsigned long long)(lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3]));
+}
+
+}  // namespace
+
+extern "C" int pm_rollout(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB,
+                          const float* paramsB, float epsilon, uint64_t seed_env, uint64_t seed_net, uint64_t counter0,
+                          int32_t steps, float* heads_ws, float* obsA, float* obsB, int64_t* stats, int32_t n,
+                          void* stream) {
+    PM_REQUIRE(n >= 0 && steps >= 0, PM_E_SIZE, "pm_rollout: n=%d steps=%d", n, steps);
+    if (n == 0 || steps == 0) return PM_OK;
+    PM_REQUIRE(p && s && s->x && s->y && s->vx && s->vy && s->spin && s->top && s->bot && s->scoreA && s->scoreB &&
+                   s->bounces && wA && wB && paramsB && heads_ws && obsA && obsB,
+               PM_E_ARG, "pm_rollout: null buffer");
+    PM_REQUIRE((((uintptr_t)wA) | ((uintptr_t)wB) | ((uintptr_t)heads_ws)) % 16 == 0, PM_E_ARG,
+               "pm_rollout: wA, wB and heads_ws must be 16-byte aligned");
+    PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_rollout: speed_scale_every must be > 0");
+    hipStream_t st = pm_stream(stream);
+    hipLaunchKernelGGL(k_rollout_heads, dim3(steps), dim3(kHeadsBlock), 0, st, paramsB, seed_net, counter0, heads_ws);
+    PM_LAUNCHED("k_rollout_heads");
+    pm_launch(PM_TIMER_ROLLOUT, k_rollout, dim3(pm_blocks(n, 32)), dim3(kRollBlock), st, *p, *s, wA, wB,
+              (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
+              reinterpret_cast<long long*>(stats), n);
+    PM_LAUNCHED("k_rollout");
+    return PM_OK;
+}

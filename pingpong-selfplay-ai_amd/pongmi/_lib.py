@@ -35,8 +35,10 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 16
-PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_N = 0, 1, 2, 3, 4
+ABI_VERSION = 17
+PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_ROLLOUT, PM_TIMER_DRQN, PM_TIMER_N = \
+    0, 1, 2, 3, 4, 5, 6
+PM_ROLL_HEADS = 264
 
 
 class EnvParams(ctypes.Structure):
@@ -121,6 +123,8 @@ _SIGS = {
                            c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
     "pm_play": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_i32,
                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pm_rollout": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_u64, c_u64, c_u64, c_i32,
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_drqn_work_bytes": (c_i64, [c_i32, c_i32]),
     "pm_drqn_grads": (c_i32, [c_void_p, c_void_p]),
     "pm_drqn_apply": (c_i32, [c_void_p, c_void_p]),

@@ -93,9 +93,10 @@ class DRQNLearner:
         self._call(self.lib.pm_drqn_apply, stream)
 
     def stats(self):
-        """(steps, loss, pre-clip grad norm, mean q) of the last update (host sync)."""
+        """(steps, loss, pre-clip grad norm, mean q, status) of the last update (host sync). status bit 1:
+        a hand-off inside the persistent recurrence timed out (that update is void)."""
         s = _lib.DrqnStats.from_buffer_copy(bytes(self.stats_buf.cpu().numpy()))
-        return dict(steps=s.steps, adam_t=s.adam_t, loss=s.loss, norm=s.norm, q_mean=s.q_mean)
+        return dict(steps=s.steps, adam_t=s.adam_t, loss=s.loss, norm=s.norm, q_mean=s.q_mean, status=s.status)
 
     def state_dict(self):
         """modelB's state_dict (reference key names)."""

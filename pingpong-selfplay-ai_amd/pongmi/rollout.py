@@ -1,0 +1,82 @@
+"""Host side of K9 (pm_rollout, csrc/pm_rollout.hip): inference-only self-play, K vector steps per launch.
+
+BASELINE configs[1]: the rollout of scripts/train_iterative.py:239-242 with the learner switched off
+— modelA greedy on its folded weights, modelB epsilon-greedy with fresh NoisyNet noise every vector
+step (select_action_B's reset_noise, :125), PongEnv2P autoreset — for n arenas in lockstep. One
+launch runs `steps` vector steps with every arena held in registers; the result is bit-identical to
+`steps` repetitions of
+
+    w_B = qnet.fold(paramsB, PM_FOLD_TRAIN_FRESH, seed=seed_net, counter=c)
+    aA, aB = qnet.act(wA, None, w_B, env.obsA, env.obsB, epsilon, seed=env.seed, counter=c)
+    env.step(aA, aB)                       # autoreset, step-keyed serves: env.counter == c
+
+with c = env.counter (tests/test_gpu_rollout.py). The rollout advances env.counter by `steps`, and
+leaves env.obsA / env.obsB holding the observations after the last step; rewards / done / term_obs
+of the last step are not produced (no learner consumes them).
+"""
+import torch
+
+from . import _lib
+from ._lib import PM_QNET_NP, PM_QNET_NW, PM_ROLL_HEADS, check, ptr, require_device, stream_ptr
+from .env import ctypes_ref
+
+STATS = ("episodes", "wins_B", "points_A", "points_B")
+
+
+class SelfPlayRollout:
+    """configs[1]'s workload on a PongEnv2PBatch: modelA (effective weights wA, PM_QNET_NW) against
+    modelB (packed parameters paramsB, PM_QNET_NP; NoisyNet heads refolded per vector step).
+
+    run(steps) -> dict of STATS accumulated over the call (host ints; reading them synchronises),
+    or the device tensor with sync=False."""
+
+    def __init__(self, env, wA, paramsB, epsilon=0.02, seed_net=0):
+        self.lib = _lib.load()
+        if env.inject is not None:
+            raise _lib.PongmiError("SelfPlayRollout uses production (Philox) serves: the env has a serve table")
+        if not env.autoreset:
+            raise _lib.PongmiError("SelfPlayRollout needs an autoreset env (the rollout never stops an arena)")
+        self.env = env
+        self.wA = _weights(wA, PM_QNET_NW, "wA", env.device)
+        self.paramsB = _weights(paramsB, PM_QNET_NP, "paramsB", env.device)
+        self.epsilon = float(epsilon)
+        self.seed_net = int(seed_net) & 0xFFFFFFFFFFFFFFFF
+        from .qnet import fold
+        # modelB's feature layers (its heads are refolded inside the launch every vector step)
+        self.wB = fold(self.paramsB, _lib.PM_FOLD_EVAL).reshape(-1)
+        self.heads = torch.empty(0, dtype=torch.float32, device=env.device)
+        self.stats = torch.zeros(len(STATS), dtype=torch.int64, device=env.device)
+
+    def set_paramsB(self, paramsB):
+        """New modelB parameters (e.g. after a generation's training)."""
+        from .qnet import fold
+        self.paramsB = _weights(paramsB, PM_QNET_NP, "paramsB", self.env.device)
+        self.wB = fold(self.paramsB, _lib.PM_FOLD_EVAL).reshape(-1)
+
+    def run(self, steps, sync=True):
+        steps = int(steps)
+        if steps < 0:
+            raise ValueError("steps must be >= 0")
+        if self.heads.numel() < steps * PM_ROLL_HEADS:
+            self.heads = torch.empty(steps * PM_ROLL_HEADS, dtype=torch.float32, device=self.env.device)
+        self.stats.zero_()
+        env = self.env
+        check(self.lib.pm_rollout(ctypes_ref(env.params), ctypes_ref(env.state), ptr(self.wA), ptr(self.wB),
+                                  ptr(self.paramsB), self.epsilon, env.seed, self.seed_net, env.counter, steps,
+                                  ptr(self.heads), ptr(env.obsA), ptr(env.obsB), ptr(self.stats), env.n, stream_ptr()),
+              "pm_rollout")
+        env.counter += steps
+        if not sync:
+            return self.stats
+        return dict(zip(STATS, (int(v) for v in self.stats.cpu().tolist())))
+
+
+def _weights(t, size, name, device):
+    require_device(t, name)
+    t = t.reshape(-1)
+    if t.numel() != size or t.dtype != torch.float32:
+        raise ValueError(f"{name} must hold {size} float32 values, got {t.numel()} {t.dtype}")
+    t = t.to(device).contiguous()  # the env's device (a no-op when already there)
+    if t.data_ptr() % 16:
+        t = t.clone()
+    return t

@@ -501,6 +501,7 @@ def run_infer(args, dist, rank, world):
     env = PongEnv2PBatch(n, seed=0x5EED + rank, autoreset=True, **ENV_KW)
     env.reset()
     R = SelfPlayRollout(env, wA, pB, epsilon=0.02, seed_net=0x5EED + 1000 * rank)
+    R.reserve(max(chunk, args.warmup))  # the heads workspace is allocated before the timed region
     R.run(args.warmup)
     torch.cuda.synchronize()
     tot = torch.zeros(len(STATS), dtype=torch.int64, device="cuda")

@@ -54,21 +54,21 @@ struct DqArgs {
     const int32_t* enable;
     float gamma;
     float *ZX;   // [3][nct][T][16][1024]     Zx in the recurrence's accumulator layout
-    float *HS;   // [3][nct][T+1][32][128]    h_t per column (the hand-off slots; slot 0 unused)
+    float *HS;   // [3][nct][T+1][32][128] x2 h_t granules {value, tag} (the hand-off slots; slot 0 unused)
     float *F1T;  // [64][C0]                  obs stream F1 (column c = t*B + b)
     float *F2T;  // [128][C0]                 obs stream F2
     float *H;    // [128][C0]                 obs stream h_t, the input hidden of step t
     float *GS;   // [nct][T][16][64][16]      obs stream activated gates, wave-0 lane layout
     float *CS;   // [nct][T][16][64][4]       obs stream c_{t+1}
     float *dZ;   // [512][C0]
-    float *QP;   // [3][nct][16][32][4]       partial (V, A0, A1, A2) of each workgroup's 8 head rows
-    float *DHP;  // [nct][T][16][32][128]     slot t: per-workgroup partials of dh_{t+1}
+    float *QP;   // [3][nct][16][32][4] x2    partial (V, A0, A1, A2) granules of each workgroup's 8 head rows
+    float *DHP;  // [nct][T][16][32][128] x2  slot t: per-workgroup partial granules of dh_{t+1}
     float *HP;   // [nct][kHpStride]          head gradient partials per column tile
     float *LP;   // [nct][4]                  loss / q sums per column tile
     float *W2P;  // [C0 / 32][kLowN]          W1 / b1 / W2 / b2 gradient partials per column tile
     double* part;
     int64_t* tstep;
-    int32_t* flags;  // [3][nct][16] forward | [3][nct][16] Q | [nct][16] backward | ticket
+    int32_t* flags;  // [0] update epoch (the granule tag base), [1] k_dq_wgrad's arrival ticket
 };
 
 // workspace carve-up, 64-float aligned pieces
@@ -84,12 +84,12 @@ struct DqLayout {
 inline int64_t dq_layout(int B, int T, DqArgs* a, void* work) {
     const int64_t nct = B / 32, C0 = (int64_t)T * B;
     DqLayout L;
-    const int64_t oZX = L.add(3 * nct * T * 16 * 1024), oHS = L.add(3 * nct * (T + 1) * 4096), oF1 = L.add(64 * C0),
+    const int64_t oZX = L.add(3 * nct * T * 16 * 1024), oHS = L.add(3 * nct * (T + 1) * 8192), oF1 = L.add(64 * C0),
                   oF2 = L.add(128 * C0), oH = L.add(128 * C0), oGS = L.add(nct * T * 16 * 1024),
-                  oCS = L.add(nct * T * 16 * 256), odZ = L.add(512 * C0), oQP = L.add(3 * nct * 16 * 128),
-                  oDHP = L.add(nct * T * 16 * 4096), oHP = L.add(nct * kHpStride), oLP = L.add(nct * 4),
+                  oCS = L.add(nct * T * 16 * 256), odZ = L.add(512 * C0), oQP = L.add(3 * nct * 16 * 256),
+                  oDHP = L.add(nct * T * 16 * 8192), oHP = L.add(nct * kHpStride), oLP = L.add(nct * 4),
                   oW2P = L.add(C0 / 32 * kLowN), oPart = L.add(2 * kNormBlocks), oTs = L.add(4),
-                  oFl = L.add(7 * nct * 16 + 4);
+                  oFl = L.add(4);
     if (a && work) {
         float* w = static_cast<float*>(work);
         a->B = B; a->T = T; a->nct = (int)nct; a->C0 = (int)C0;
@@ -101,36 +101,88 @@ inline int64_t dq_layout(int B, int T, DqArgs* a, void* work) {
     return L.total * 4;
 }
 
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// diagnostic builds: thread 0 of a chosen block stamps s_memrealtime (100 MHz) at phase boundaries
+#ifdef PM_DIAG
+#define DQ_STAMP(slot, cond)                                                                    \
+    do {                                                                                        \
+        if (threadIdx.x == 0 && (cond)) pm_diag_buf[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define DQ_STAMP(slot, cond) \
+    do {                     \
+    } while (0)
+#endif
 __device__ __forceinline__ bool skipped(const DqArgs& a) { return a.enable && *a.enable == 0; }
 
 // ---------------------------------------------------------------- hand-off primitives
-// Write-through (sc1) 16-byte stores and loads through a buffer resource (MI355X_MICROARCH.md,
-// hand-off table row 1: every byte of a hand-off stored and loaded sc1, the flag an sc1 store by one
-// lane after the storing wave's vmcnt(0), the consumer's poll an sc1 load).
+// In-launch hand-offs move data-tagged granules (MI355X_MICROARCH.md, R2 / handoff-1to1): each
+// 8-byte granule is {value, tag} and the data IS the signal — the producer writes it with a
+// write-through (sc1) 16-byte store (two granules), the consumer polls the granules themselves with
+// sc1 loads until every tag matches, so no flag, no drain and no barrier sits between them. Tags
+// carry the update's epoch (k_dq_embed bumps it), so a slot left by an earlier update never matches.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ float4 ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
-    typedef __attribute__((ext_vector_type(4))) float f4v;
-    const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */));
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, float4 v) { store_f4_sc1(r, byte_off, v); }
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void flag_set(int32_t* f, int v) {
-    __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// 4-byte write-through store / L2-coherent load (sc1), for the column-tile partials handed to the
+// workgroups that sum them within the same launch (hand-off table row 1: sc1 on both sides)
+__device__ __forceinline__ void st_wt(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_wt(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+// two granules {v0, tag}, {v1, tag} with one 16-byte write-through store
+__device__ __forceinline__ void st_g2(__amdgpu_buffer_rsrc_t r, int byte_off, float v0, float v1, uint32_t tag) {
+    const u32x4 q = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(q, r, byte_off, 0, 16 /* sc1 */);
 }
-// Lanes [0, n) of the calling wave poll flags f[lane] (sc1 loads) until every one is >= need.
-// Bounded: a wait that never completes sets status bit 1 and returns (the update is then void).
-__device__ __forceinline__ void wait_flags(const int32_t* f, int n, int need, int lane, pm_drqn_stats* st) {
-    bool ok = lane >= n;
-    for (int it = 0; it < (1 << 21); ++it) {
-        if (!ok) ok = __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+// Poll the granule pairs at byte offsets off[i] (16-B aligned, from base) until every tag equals
+// `tag`; v[2i], v[2i+1] get the values. The polls are 8-byte agent-scope atomic loads (sc1): a
+// plain or volatile-flagged buffer load is loop-invariant to the compiler and gets hoisted out of
+// the poll. Wave-wide; bounded (status bit 1 and garbage values on a timeout: the update is void).
+template <int N, bool SLEEP = false>
+__device__ __forceinline__ void gather(const void* base, const int (&off)[N], uint32_t tag, float (&v)[2 * N],
+                                       pm_drqn_stats* st) {
+    const char* b = static_cast<const char*>(base);
+    for (int it = 0;; ++it) {
+        uint64_t q[2 * N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(b + off[i]);
+            q[2 * i] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            q[2 * i + 1] = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 2 * N; ++i) {
+            ok = ok && (uint32_t)(q[i] >> 32) == tag;
+            v[i] = __uint_as_float((uint32_t)q[i]);
+        }
+        if (__all(ok)) return;
+        if (it == (1 << 20)) {
+            if ((threadIdx.x & 63) == 0) atomicOr(&st->status, 2);
+            return;
+        }
+        // (a sleep here with N > 8 makes the compiler keep the callers' arrays live across the loop:
+        // thousands of spilled registers; the re-issued loads' round trip paces those polls instead)
+        if constexpr (SLEEP) __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+
+// Lanes [0, n) of one wave poll one granule each (byte offset soff) until its tag equals `tag`: the
+// wait for n producers costs one 8-byte load per producer per poll instead of a whole slot sweep by
+// every wave (sweeping pollers congested the fabric: ~5 us per hop). Bounded like gather.
+__device__ __forceinline__ void poll_tags(const void* base, int soff, int n, uint32_t tag, pm_drqn_stats* st) {
+    const char* b = static_cast<const char*>(base);
+    bool ok = (int)(threadIdx.x & 63) >= n;
+    for (int it = 0; it < (1 << 20); ++it) {
+        if (!ok)
+            ok = (uint32_t)(__hip_atomic_load(reinterpret_cast<const uint64_t*>(b + soff), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
         if (__all(ok)) return;
         __builtin_amdgcn_s_sleep(1);
     }
-    if (lane == 0) atomicOr(&st->status, 2);
+    if ((threadIdx.x & 63) == 0) atomicOr(&st->status, 2);
 }
 
 // ---------------------------------------------------------------- 1: embedding + input projection
@@ -146,19 +198,35 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
     bid /= T;
     const int ct = bid % nct, s = bid / nct;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
-    if (blockIdx.x == 0)
-        for (int i = tid; i < 7 * nct * 16 + 4; i += 256) a.flags[i] = 0;
+    if (blockIdx.x == 0 && tid == 0) {  // a new tag epoch for k_dq_recur's hand-offs; the wgrad ticket
+        a.flags[0] = a.flags[0] + 1;
+        a.flags[1] = 0;
+    }
     if (skipped(a)) {  // this replica contributes nothing to the all-reduce
         for (int i = blockIdx.x * 256 + tid; i < PM_RNN_NPARAM + 4; i += gridDim.x * 256) a.grad[i] = 0.f;
         return;
     }
     if (blockIdx.x == 0 && tid == 0) a.grad[PM_RNN_NPARAM] = 1.0f;
     __shared__ __attribute__((aligned(16))) float F2s[32][132];
+    DQ_STAMP(220, blockIdx.x == 0);
     const float* P = s == 2 ? a.target : a.params;
     const int b = ct * 32 + col;
     const int64_t c = (int64_t)t * B + b;
     float xs[4];
     tile_inputs((s == 0 ? a.obs : a.next) + ((int64_t)b * T + t) * 7, h, xs);
+    // every weight operand of the wave is loaded up front: the Zx A fragments (64 registers) land
+    // while F1 / F2 compute instead of after the F2 barrier
+    const int m = 4 * rq + w;
+    const float* wr = P + R_P_WIH + (int64_t)(128 * (col >> 3) + 8 * m + (col & 7)) * 128 + 4 * h;
+    float4 av[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) av[j] = *reinterpret_cast<const float4*>(wr + 8 * j);
+    float4 w2v[8];
+    {
+        const float* w2 = P + R_P_F2W + (32 * w + col) * 64 + 4 * h;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w2v[i] = *reinterpret_cast<const float4*>(w2 + 32 * (i >> 2) + 8 * (i & 3));
+    }
     // F1 (both 32-row tiles, every wave): input k' = 2 s4 + h, k' = 0 the constant 1 (weight: b1)
     f32x16 c1[2];
 #pragma unroll
@@ -179,12 +247,11 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) f2[r] = P[R_P_F2B + 32 * w + rho(r) + 4 * h];
     {
-        const float* w2 = P + R_P_F2W + (32 * w + col) * 64 + 4 * h;
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float4 v = *reinterpret_cast<const float4*>(w2 + 32 * t2 + 8 * i);
+                const float4 v = w2v[4 * t2 + i];
                 f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, c1[t2][4 * i + 0], f2, 0, 0, 0);
                 f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, c1[t2][4 * i + 1], f2, 0, 0, 0);
                 f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, c1[t2][4 * i + 2], f2, 0, 0, 0);
@@ -207,7 +274,6 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
     }
     __syncthreads();
     // Zx tile of recurrence workgroup m: K = 128 with k = 8j + 4h + e for k-step (j, e)
-    const int m = 4 * rq + w;
     f32x16 z;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -215,10 +281,6 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
         const int g = 128 * (rr >> 3) + 8 * m + (rr & 7);
         z[r] = P[R_P_BIH + g] + P[R_P_BHH + g];
     }
-    const float* wr = P + R_P_WIH + (int64_t)(128 * (col >> 3) + 8 * m + (col & 7)) * 128 + 4 * h;
-    float4 av[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) av[j] = *reinterpret_cast<const float4*>(wr + 8 * j);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const float4 bv = *reinterpret_cast<const float4*>(&F2s[col][8 * j + 4 * h]);
@@ -230,21 +292,29 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
     float4* zx = reinterpret_cast<float4*>(a.ZX + ((((int64_t)s * nct + ct) * T + t) * 16 + m) * 1024) + lane;
 #pragma unroll
     for (int i = 0; i < 4; ++i) zx[64 * i] = make_float4(z[4 * i], z[4 * i + 1], z[4 * i + 2], z[4 * i + 3]);
+    DQ_STAMP(222, blockIdx.x == 0);
 }
 
 // ---------------------------------------------------------------- 2: the recurrence (persistent)
 struct RecurSmem {
-    float red[3][16][64];                            // partial accumulators of waves 1..3
+    float red[2][4][16][64];  // the waves' partial accumulators, by step parity: a wave gathers its next
+                              // h from other workgroups and may write a step ahead of a slower wave's read
     __attribute__((aligned(16))) float dzs[4][64][4];  // BPTT: wave 0's dz fragments for the other waves
     __attribute__((aligned(16))) float hT[32][132];  // h_T of this column tile [column][unit]
     float dS[8][32];                                 // dS of this workgroup's 8 shared-head rows
     float ws[8][128];                                // those rows of the effective W_S
+    __attribute__((aligned(16))) float qs[3][32][4]; // the three streams' summed V / A per column
+    __attribute__((aligned(16))) float dhs[4][64][4];  // BPTT: each wave's sum of 4 producers' dh partials
 };
 
 __device__ __forceinline__ float eff_w(const float* P, int mu, int sg, int ep, bool noisy) {
     return noisy ? P[mu] + P[sg] * P[ep] : P[mu];  // NoisyLinear: mu + sigma * epsilon (train), mu (eval)
 }
 
+// Slot layouts (granules, 8 B each):
+//   HS  [grp][T+1][32 col][128 unit]   h_t of a (stream, column tile) group, tag E + t
+//   QP  [grp][16 m][32 col][4]         the V / A partials of workgroup m's 8 shared-head rows, tag E + 1
+//   DHP [ct][T][16 m][32 col][128]     workgroup m's partial of dh_{t+1} (slot t), tag E + t + 1
 __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
     if (skipped(a)) return;
     __shared__ RecurSmem sm;
@@ -253,16 +323,18 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
     const int m = bid & 15;
     bid >>= 4;
     const int ct = bid % nct, so = bid / nct;
-    const int s = so == 2 ? 0 : so + 1;  // streams 1 and 2 first: the obs stream's group waits for them
+    const int s = so == 2 ? 0 : so + 1;  // the next-state streams first: the obs stream's group waits for them
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
     const bool noisy = s != 2;  // modelB in train mode, targetB in eval mode
     const float* P = s == 2 ? a.target : a.params;
     const int64_t C0 = a.C0;
     const int bcol = ct * 32 + col;
     const int grp = s * nct + ct;
-    float* HSg = a.HS + (int64_t)grp * (T + 1) * 4096;
-    const __amdgpu_buffer_rsrc_t rHS = rsrc(HSg);
-    int32_t* fl = a.flags + grp * 16;
+    const uint32_t E = (uint32_t)a.flags[0] << 7;  // this update's tag base (T + 1 < 128)
+    [[maybe_unused]] const bool so0 = s == 0 && ct == 0 && m == 0, s10 = blockIdx.x == 0;  // stamping blocks (diag)
+    DQ_STAMP(1, so0);
+    DQ_STAMP(111, s10);
+    float* HSg = a.HS + (int64_t)grp * (T + 1) * 8192;
     // this wave's Whh fragments: row 128 q + 8m + j of lane row col (q = col >> 3, j = col & 7), K quarter w
     float wa[16];
     {
@@ -273,150 +345,176 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
             wa[4 * j] = v.x; wa[4 * j + 1] = v.y; wa[4 * j + 2] = v.z; wa[4 * j + 3] = v.w;
         }
     }
-    const float4* zx = reinterpret_cast<const float4*>(a.ZX + ((int64_t)grp * T * 16 + m) * 1024) + lane;
-    float cst[4] = {0.f, 0.f, 0.f, 0.f};  // wave 0: c of units 8m + 4h + e, column col
-    float4 zn[4];
-    if (w == 0)
+    if (s == 0)  // the obs stream's rows of modelB's effective W_S (for dh_T), published by a later barrier
+        for (int k = tid; k < 8 * 128; k += 256) {
+            const int u = 8 * m + (k >> 7), kk = k & 127, o = u * 128 + kk;
+            sm.ws[k >> 7][kk] = eff_w(a.params, R_P_SWMU + o, R_P_SWSG + o, R_P_SWEP + o, true);
+        }
+    // the K-quarter slot offsets of this lane: units 32w + 8j + 4h + {0..3} of column col
+    int hoff[8];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) zn[i] = zx[64 * i];
+    for (int j = 0; j < 4; ++j) {
+        hoff[2 * j] = (col * 128 + 32 * w + 8 * j + 4 * h) * 8;
+        hoff[2 * j + 1] = hoff[2 * j] + 16;
+    }
+    // Zx of this wave's unit e = w (registers 4q + w of the tile, one float of each float4 chunk q)
+    const float* zx = a.ZX + ((int64_t)grp * T * 16 + m) * 1024 + lane * 4 + w;
+    float c1 = 0.f;  // c of unit 8m + 4h + w, column col (each wave owns one unit per lane half)
+    float zn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zn[q] = zx[q * 256];
     // ---------------- forward
     for (int t = 0; t < T; ++t) {
-        f32x16 acc = {};
-        if (w == 0) {
+        float z[4] = {zn[0], zn[1], zn[2], zn[3]};
+        if (t + 1 < T)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { acc[4 * i] = zn[i].x; acc[4 * i + 1] = zn[i].y; acc[4 * i + 2] = zn[i].z; acc[4 * i + 3] = zn[i].w; }
-            if (t + 1 < T)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) zn[i] = zx[(int64_t)(t + 1) * 16 * 256 + 64 * i];
-        }
+            for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)(t + 1) * 16 * 1024 + q * 256];
         if (t > 0) {
-            if (w == 0) wait_flags(fl, 16, t, lane, a.stats);
-            __syncthreads();  // h_t published by the whole group
+            float hv[16];
+            int off[8];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4 hv = ld_sc1(rHS, ((t * 32 + col) * 128 + 32 * w + 8 * j + 4 * h) * 4);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + 0], hv.x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + 1], hv.y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + 2], hv.z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * j + 3], hv.w, acc, 0, 0, 0);
-            }
-            if (w > 0)
+            for (int i = 0; i < 8; ++i) off[i] = hoff[i] + t * 32 * 128 * 8;
+            // lanes 0..3 wait for the last granule of this wave's 4 producers, then the K quarter is read once
+            poll_tags(HSg, ((t * 32 + 31) * 128 + 8 * (4 * w + (lane & 3)) + 7) * 8, 4, E + t, a.stats);
+            gather<8, false>(HSg, off, E + t, hv, a.stats);  // h_t of the group, this wave's K quarter
+            DQ_STAMP(160 + t, so0 && t < 10);
+            f32x16 acc = {};
 #pragma unroll
-                for (int r = 0; r < 16; ++r) sm.red[w - 1][r][lane] = acc[r];
+            for (int k = 0; k < 16; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[k], hv[k], acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sm.red[t & 1][w][r][lane] = acc[r];
             __syncthreads();
-        }
-        if (w != 0) continue;
-        // wave 0: the cell of units 8m + 4h + e (gate q in register 4q + e), column col
-        float hn[4], gt[16];
+            DQ_STAMP(170 + t, so0 && t < 10);
+            // unit e = w: gate q is register 4q + w of every wave's partial
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float z = acc[r];
-            if (t > 0) z = ((z + sm.red[0][r][lane]) + sm.red[1][r][lane]) + sm.red[2][r][lane];
-            gt[r] = (r >> 2) == 2 ? tanhf(z) : sigm(z);
+            for (int q = 0; q < 4; ++q)
+                z[q] = (((z[q] + sm.red[t & 1][0][4 * q + w][lane]) + sm.red[t & 1][1][4 * q + w][lane]) +
+                        sm.red[t & 1][2][4 * q + w][lane]) + sm.red[t & 1][3][4 * q + w][lane];
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            cst[e] = gt[4 + e] * cst[e] + gt[e] * gt[8 + e];  // cy = forgetgate * cx + ingate * cellgate
-            hn[e] = gt[12 + e] * tanhf(cst[e]);
+        // the cell of unit 8m + 4h + w (v_exp_f32 / v_rcp_f32 activations, a few ulp)
+        const float gi = sig_hw(z[0]), gf = sig_hw(z[1]), gg = tanh_hw(z[2]), go = sig_hw(z[3]);
+        c1 = gf * c1 + gi * gg;  // cy = forgetgate * cx + ingate * cellgate
+        const float hn = go * tanh_hw(c1);
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(HSg) + ((t + 1) * 32 + col) * 128 + 8 * m + 4 * h + w,
+                           ((uint64_t)(E + t + 1) << 32) | __float_as_uint(hn), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        DQ_STAMP(10 + t, so0 && t < 30);
+        DQ_STAMP(120 + t, s10 && t < 30);
+        if (s == 0) {  // what BPTT and the weight gradients need of the obs stream (plain stores)
+            float* g = a.GS + (((int64_t)ct * T + t) * 16 + m) * 1024 + lane * 4 + w;
+            g[0] = gi; g[256] = gf; g[512] = gg; g[768] = go;
+            a.CS[(((int64_t)ct * T + t) * 16 + m) * 256 + lane * 4 + w] = c1;
+            float* hr = a.H + (int64_t)(8 * m + 4 * h + w) * C0 + bcol;
+            if (t + 1 < T) hr[(int64_t)(t + 1) * B] = hn;
+            if (t == 0) hr[0] = 0.f;
         }
-        st_sc1(rHS, (((t + 1) * 32 + col) * 128 + 8 * m + 4 * h) * 4, make_float4(hn[0], hn[1], hn[2], hn[3]));
-        if (s == 0) {  // what BPTT and the weight gradients need of the obs stream
-            float4* g4 = reinterpret_cast<float4*>(a.GS + (((int64_t)ct * T + t) * 16 + m) * 1024) + lane;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) g4[64 * i] = make_float4(gt[4 * i], gt[4 * i + 1], gt[4 * i + 2], gt[4 * i + 3]);
-            reinterpret_cast<float4*>(a.CS + (((int64_t)ct * T + t) * 16 + m) * 256)[lane] =
-                make_float4(cst[0], cst[1], cst[2], cst[3]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float* hr = a.H + (int64_t)(8 * m + 4 * h + e) * C0 + bcol;
-                if (t + 1 < T) hr[(int64_t)(t + 1) * B] = hn[e];
-                if (t == 0) hr[0] = 0.f;
-            }
-        }
-        drain();
-        if (lane == 0) flag_set(fl + m, t + 1);
     }
     // ---------------- heads: rows 8m .. 8m+7 of the shared head (A rows duplicated x4 in the tile)
-    if (w == 0) wait_flags(fl, 16, T, lane, a.stats);
-    __syncthreads();  // h_T published
+    // the shared head's A fragments (row 8m + (col & 7), duplicated x4; K quarter w), loaded while h_T is polled
+    float wsf[16];
+    {
+        const int o = (8 * m + (col & 7)) * 128 + 32 * w + 4 * h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = o + 8 * j + e;
+                wsf[4 * j + e] = eff_w(P, R_P_SWMU + k, R_P_SWSG + k, R_P_SWEP + k, noisy);
+            }
+    }
+    // wave 0's head weights of S rows 8m + 4h + e: bias, V, A0..2 (effective), loaded while h_T is polled
+    float hw5[4][5];
+    if (w == 0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int u = 8 * m + 4 * h + e;
+            hw5[e][0] = eff_w(P, R_P_SBMU + u, R_P_SBSG + u, R_P_SBEP + u, noisy);
+            hw5[e][1] = eff_w(P, R_P_VWMU + u, R_P_VWSG + u, R_P_VWEP + u, noisy);
+            hw5[e][2] = eff_w(P, R_P_AWMU + u, R_P_AWSG + u, R_P_AWEP + u, noisy);
+            hw5[e][3] = eff_w(P, R_P_AWMU + 128 + u, R_P_AWSG + 128 + u, R_P_AWEP + 128 + u, noisy);
+            hw5[e][4] = eff_w(P, R_P_AWMU + 256 + u, R_P_AWSG + 256 + u, R_P_AWEP + 256 + u, noisy);
+        }
     f32x16 sacc = {};
     {
-        const int u = 8 * m + (col & 7);  // S row of lane row col
-        const int kb = 32 * w + 4 * h;
+        float hv[16];
+        int off[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float4 hv = ld_sc1(rHS, ((T * 32 + col) * 128 + kb + 8 * j) * 4);
-            *reinterpret_cast<float4*>(&sm.hT[col][kb + 8 * j]) = hv;
-            const int k0 = u * 128 + kb + 8 * j;
-            float wv[4];
+        for (int i = 0; i < 8; ++i) off[i] = hoff[i] + T * 32 * 128 * 8;
+        poll_tags(HSg, ((T * 32 + 31) * 128 + 8 * (4 * w + (lane & 3)) + 7) * 8, 4, E + T, a.stats);
+        gather<8, false>(HSg, off, E + T, hv, a.stats);  // h_T
 #pragma unroll
-            for (int e = 0; e < 4; ++e) wv[e] = eff_w(P, R_P_SWMU + k0 + e, R_P_SWSG + k0 + e, R_P_SWEP + k0 + e, noisy);
-            sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[0], hv.x, sacc, 0, 0, 0);
-            sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[1], hv.y, sacc, 0, 0, 0);
-            sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[2], hv.z, sacc, 0, 0, 0);
-            sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[3], hv.w, sacc, 0, 0, 0);
-        }
+        for (int j = 0; j < 4; ++j)
+            *reinterpret_cast<float4*>(&sm.hT[col][32 * w + 8 * j + 4 * h]) =
+                make_float4(hv[4 * j], hv[4 * j + 1], hv[4 * j + 2], hv[4 * j + 3]);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wsf[k], hv[k], sacc, 0, 0, 0);
     }
     if (w > 0)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sm.red[w - 1][r][lane] = sacc[r];
+        for (int r = 0; r < 4; ++r) sm.red[T & 1][w][r][lane] = sacc[r];
     __syncthreads();
     // wave 0: S rows u_e = 8m + 4h + e (registers r = e), their V / A partials
     float sv[4], sr[4];
-    float* QPs = a.QP + (int64_t)grp * 16 * 128;
     if (w == 0) {
         float pv = 0.f, pa0 = 0.f, pa1 = 0.f, pa2 = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int u = 8 * m + 4 * h + e;
-            const float z = ((sacc[e] + sm.red[0][e][lane]) + sm.red[1][e][lane]) + sm.red[2][e][lane];
-            sv[e] = z + eff_w(P, R_P_SBMU + u, R_P_SBSG + u, R_P_SBEP + u, noisy);
+            const float z = ((sacc[e] + sm.red[T & 1][1][e][lane]) + sm.red[T & 1][2][e][lane]) + sm.red[T & 1][3][e][lane];
+            sv[e] = z + hw5[e][0];
             sr[e] = relu(sv[e]);
-            pv = fmaf(eff_w(P, R_P_VWMU + u, R_P_VWSG + u, R_P_VWEP + u, noisy), sr[e], pv);
-            pa0 = fmaf(eff_w(P, R_P_AWMU + u, R_P_AWSG + u, R_P_AWEP + u, noisy), sr[e], pa0);
-            pa1 = fmaf(eff_w(P, R_P_AWMU + 128 + u, R_P_AWSG + 128 + u, R_P_AWEP + 128 + u, noisy), sr[e], pa1);
-            pa2 = fmaf(eff_w(P, R_P_AWMU + 256 + u, R_P_AWSG + 256 + u, R_P_AWEP + 256 + u, noisy), sr[e], pa2);
+            pv = fmaf(hw5[e][1], sr[e], pv);
+            pa0 = fmaf(hw5[e][2], sr[e], pa0);
+            pa1 = fmaf(hw5[e][3], sr[e], pa1);
+            pa2 = fmaf(hw5[e][4], sr[e], pa2);
         }
         pv += __shfl_xor(pv, 32);
         pa0 += __shfl_xor(pa0, 32);
         pa1 += __shfl_xor(pa1, 32);
         pa2 += __shfl_xor(pa2, 32);
-        if (h == 0) st_sc1(rsrc(QPs), (m * 32 + col) * 16, make_float4(pv, pa0, pa1, pa2));
-        drain();
-        if (lane == 0) flag_set(a.flags + 3 * nct * 16 + grp * 16 + m, 1);
+        if (h == 0) {
+            const __amdgpu_buffer_rsrc_t rq = rsrc(a.QP + (int64_t)grp * 16 * 256);
+            st_g2(rq, (m * 32 + col) * 32, pv, pa0, E + 1);
+            st_g2(rq, (m * 32 + col) * 32 + 16, pa1, pa2, E + 1);
+        }
     }
+    DQ_STAMP(50, so0);
+    DQ_STAMP(150, s10);
     if (s != 0) return;  // block-uniform: the next-state streams are done
-    // ---------------- the loss and the head gradients (obs stream), on wave 0
+    // ---------------- the loss and the head gradients (obs stream)
+    if (w < 3) {  // wave st gathers stream st's 16 partials of this column tile (8 per lane half)
+        const int st = w;
+        const float* QPs = a.QP + (int64_t)(st * nct + ct) * 16 * 256;
+        float p[32];
+#pragma unroll
+        for (int k0 = 0; k0 < 8; k0 += 4) {
+            int off[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                off[2 * k] = ((8 * h + k0 + k) * 32 + col) * 32;
+                off[2 * k + 1] = off[2 * k] + 16;
+            }
+            float pp[16];
+            gather<8, true>(QPs, off, E + 1, pp, a.stats);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) p[4 * k0 + k] = pp[k];
+        }
+        float v = 0.f, x0 = 0.f, x1 = 0.f, x2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { v += p[4 * k]; x0 += p[4 * k + 1]; x1 += p[4 * k + 2]; x2 += p[4 * k + 3]; }
+        v += __shfl_xor(v, 32);  // + the other half (commutative: both halves agree bit for bit)
+        x0 += __shfl_xor(x0, 32);
+        x1 += __shfl_xor(x1, 32);
+        x2 += __shfl_xor(x2, 32);
+        if (h == 0) *reinterpret_cast<float4*>(&sm.qs[st][col][0]) = make_float4(v, x0, x1, x2);
+    }
+    __syncthreads();
     float dV = 0.f, dA[3] = {0.f, 0.f, 0.f};
     if (w == 0) {
-        const int32_t* fq = a.flags + 3 * nct * 16;
-        // lanes [0, 48): stream (lane >> 4), workgroup (lane & 15) of this column tile
-        {
-            const int sl = lane >> 4;
-            bool ok = lane >= 48;
-            for (int it = 0; it < (1 << 21); ++it) {
-                if (!ok) ok = __hip_atomic_load(fq + (sl * nct + ct) * 16 + (lane & 15), __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT) >= 1;
-                if (__all(ok)) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (it == (1 << 21) - 1 && lane == 0) atomicOr(&a.stats->status, 2);
-            }
-        }
         float q[3][3];
 #pragma unroll
         for (int st = 0; st < 3; ++st) {
-            const float* QPst = a.QP + (int64_t)(st * nct + ct) * 16 * 128;
-            const __amdgpu_buffer_rsrc_t rq = rsrc(QPst);
-            float v = 0.f, x0 = 0.f, x1 = 0.f, x2 = 0.f;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {  // this lane half's 8 workgroups, in order
-                const float4 p = ld_sc1(rq, ((8 * h + k) * 32 + col) * 16);
-                v += p.x; x0 += p.y; x1 += p.z; x2 += p.w;
-            }
-            v += __shfl_xor(v, 32);  // + the other half (commutative: both halves agree bit for bit)
-            x0 += __shfl_xor(x0, 32);
-            x1 += __shfl_xor(x1, 32);
-            x2 += __shfl_xor(x2, 32);
+            const float4 qv = *reinterpret_cast<const float4*>(&sm.qs[st][col][0]);
+            float v = qv.x, x0 = qv.y, x1 = qv.z, x2 = qv.w;
             const float* Pst = st == 2 ? a.target : a.params;
             const bool nz = st != 2;
             v += eff_w(Pst, R_P_VBMU, R_P_VBSG, R_P_VBEP, nz);
@@ -428,6 +526,7 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
             q[st][1] = v + (x1 - mean);
             q[st][2] = v + (x2 - mean);
         }
+        DQ_STAMP(51, so0);
         const int64_t jl = (int64_t)bcol * T + T - 1;  // the sequence's last step
         const int ac = a.act[jl];
         const float rl = a.rew[jl], dl = a.done[jl] ? 1.f : 0.f;
@@ -451,12 +550,7 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
         float gv[4], ga[3][4], gb[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int u = 8 * m + 4 * h + e;
-            const float* Q = a.params;
-            const float ds = eff_w(Q, R_P_VWMU + u, R_P_VWSG + u, R_P_VWEP + u, true) * dV +
-                             eff_w(Q, R_P_AWMU + u, R_P_AWSG + u, R_P_AWEP + u, true) * dA[0] +
-                             eff_w(Q, R_P_AWMU + 128 + u, R_P_AWSG + 128 + u, R_P_AWEP + 128 + u, true) * dA[1] +
-                             eff_w(Q, R_P_AWMU + 256 + u, R_P_AWSG + 256 + u, R_P_AWEP + 256 + u, true) * dA[2];
+            const float ds = hw5[e][1] * dV + hw5[e][2] * dA[0] + hw5[e][3] * dA[1] + hw5[e][4] * dA[2];
             const float dsm = sv[e] > 0.f ? ds : 0.f;
             sm.dS[4 * h + e][col] = dsm;
             gv[e] = dV * sr[e];
@@ -495,12 +589,24 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
             if (lane == 0) { HPc[HP_VB] = sb; HPc[HP_AB] = sa0; HPc[HP_AB + 1] = sa1; HPc[HP_AB + 2] = sa2; }
         }
     }
-    // this workgroup's rows of modelB's effective W_S (for dh_T)
-    for (int k = tid; k < 8 * 128; k += 256) {
-        const int u = 8 * m + (k >> 7), kk = k & 127, o = u * 128 + kk;
-        sm.ws[k >> 7][kk] = eff_w(a.params, R_P_SWMU + o, R_P_SWSG + o, R_P_SWEP + o, true);
+    __syncthreads();  // dS (h_T and ws: earlier barriers)
+    const float* DHc = a.DHP + (int64_t)ct * T * 16 * 8192;
+    const __amdgpu_buffer_rsrc_t rDH = rsrc(DHc);
+    {   // dh_T partial over this workgroup's 8 rows: thread (column, 16 units) -> slot T - 1
+        const int c2 = tid >> 3, u0 = (tid & 7) * 16;
+        float o16[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o16[k] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float ds = sm.dS[r][c2];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) o16[k] = fmaf(sm.ws[r][u0 + k], ds, o16[k]);
+        }
+        const int base = ((((T - 1) * 16 + m) * 32 + c2) * 128 + u0) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st_g2(rDH, base + 16 * i, o16[2 * i], o16[2 * i + 1], E + T);
     }
-    __syncthreads();  // dS, h_T, ws
     {   // dW_S rows (partial over this column tile): thread (k', row half)
         const int kk = tid & 127, hr = tid >> 7;
         float g4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -513,26 +619,7 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) HPc[HP_WS + (8 * m + 4 * hr + e) * 128 + kk] = g4[e];
     }
-    const __amdgpu_buffer_rsrc_t rDH = rsrc(a.DHP + (int64_t)ct * T * 16 * 4096);
-    {   // dh_T partial over this workgroup's 8 rows: thread (column, 16 units)
-        const int c2 = tid >> 3, u0 = (tid & 7) * 16;
-        float o16[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) o16[k] = 0.f;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const float ds = sm.dS[r][c2];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) o16[k] = fmaf(sm.ws[r][u0 + k], ds, o16[k]);
-        }
-        const int base = (((T - 1) * 16 + m) * 32 + c2) * 128 + u0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st_sc1(rDH, (base + 4 * i) * 4, make_float4(o16[4 * i], o16[4 * i + 1], o16[4 * i + 2], o16[4 * i + 3]));
-    }
-    drain();
-    __syncthreads();
-    int32_t* fb = a.flags + 6 * nct * 16 + ct * 16;
-    if (tid == 0) flag_set(fb + m, 1);
+    DQ_STAMP(52, so0);
     // ---------------- BPTT
     // Whh^T fragments of this wave's output tile (units u' = 32w + col): k-step r covers gate rows
     // rho(r) + 4h of this workgroup's tile, i.e. Whh row 128 (r >> 2) + 8m + (r & 3) + 4h
@@ -543,9 +630,9 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
     float dc[4] = {0.f, 0.f, 0.f, 0.f};
     for (int t = T - 1; t >= 0; --t) {
         float dz[16];
+        float gt[16], cT[4], cP[4];  // wave 0: this step's gates and cells, loaded ahead of the dh wait
         if (w == 0) {
             const float4* g4 = reinterpret_cast<const float4*>(a.GS + (((int64_t)ct * T + t) * 16 + m) * 1024) + lane;
-            float gt[16];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float4 v = g4[64 * i];
@@ -554,18 +641,40 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
             const float4 cn = reinterpret_cast<const float4*>(a.CS + (((int64_t)ct * T + t) * 16 + m) * 256)[lane];
             const float4 cp = t > 0 ? reinterpret_cast<const float4*>(a.CS + (((int64_t)ct * T + t - 1) * 16 + m) * 256)[lane]
                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float cT[4] = {cn.x, cn.y, cn.z, cn.w}, cP[4] = {cp.x, cp.y, cp.z, cp.w};
-            wait_flags(fb, 16, T - t, lane, a.stats);
+            cT[0] = cn.x; cT[1] = cn.y; cT[2] = cn.z; cT[3] = cn.w;
+            cP[0] = cp.x; cP[1] = cp.y; cP[2] = cp.z; cP[3] = cp.w;
+        }
+        {   // every wave gathers 4 producers' partials of dh_{t+1} for this workgroup's units
+            int off[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                off[2 * k] = ((((t * 16 + 4 * w + k) * 32) + col) * 128 + 8 * m + 4 * h) * 8;
+                off[2 * k + 1] = off[2 * k] + 16;
+            }
+            float p[16];
+            poll_tags(DHc, (((t * 16 + 4 * w + (lane & 3)) * 32 + 31) * 128 + 32 * (m >> 2) + 31) * 8, 4, E + t + 1,
+                      a.stats);
+            gather<8, false>(DHc, off, E + t + 1, p, a.stats);
+            float d4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                d4[0] += p[4 * k]; d4[1] += p[4 * k + 1]; d4[2] += p[4 * k + 2]; d4[3] += p[4 * k + 3];
+            }
+            *reinterpret_cast<float4*>(&sm.dhs[w][lane][0]) = make_float4(d4[0], d4[1], d4[2], d4[3]);
+        }
+        DQ_STAMP(60 + t, so0 && t < 30);
+        __syncthreads();  // the four waves' dh sums (dhs is rewritten only after every wave published)
+        if (w == 0) {
             float dh[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {  // the 16 workgroups' partials of dh_{t+1}, in order
-                const float4 p = ld_sc1(rDH, (((t * 16 + k) * 32 + col) * 128 + 8 * m + 4 * h) * 4);
-                dh[0] += p.x; dh[1] += p.y; dh[2] += p.z; dh[3] += p.w;
+            for (int k = 0; k < 4; ++k) {  // the 16 producers' partials, in producer order
+                const float4 v = *reinterpret_cast<const float4*>(&sm.dhs[k][lane][0]);
+                dh[0] += v.x; dh[1] += v.y; dh[2] += v.z; dh[3] += v.w;
             }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const float gi = gt[e], gf = gt[4 + e], gg = gt[8 + e], go = gt[12 + e];
-                const float tc = tanhf(cT[e]);
+                const float tc = tanh_hw(cT[e]);
                 const float dcc = dc[e] + dh[e] * go * (1.0f - tc * tc);
                 dz[e] = dcc * gg * (gi * (1.0f - gi));
                 dz[4 + e] = dcc * cP[e] * (gf * (1.0f - gf));
@@ -573,16 +682,16 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
                 dz[12 + e] = dh[e] * tc * (go * (1.0f - go));
                 dc[e] = dcc * gf;
             }
-            const int64_t cc = (int64_t)t * B + bcol;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a.dZ[(int64_t)(128 * (r >> 2) + 8 * m + 4 * h + (r & 3)) * C0 + cc] = dz[r];
             if (t > 0)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     *reinterpret_cast<float4*>(&sm.dzs[i][lane][0]) = make_float4(dz[4 * i], dz[4 * i + 1], dz[4 * i + 2], dz[4 * i + 3]);
+            const int64_t cc = (int64_t)t * B + bcol;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a.dZ[(int64_t)(128 * (r >> 2) + 8 * m + 4 * h + (r & 3)) * C0 + cc] = dz[r];
         }
         if (t == 0) break;  // dh_0 (the zero initial state) is not needed
-        __syncthreads();  // dz fragments
+        __syncthreads();  // dz fragments (reused at the next step only after every wave has published)
         if (w != 0)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -593,14 +702,15 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
         // r-th k-step: this workgroup's gate rows rho(r) + 4h (the accumulator layout of dz)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wt[r], dz[r], acc, 0, 0, 0);
-        const int base = (((t - 1) * 16 + m) * 32 + col) * 128 + 32 * w + 4 * h;
+        const int base = ((((t - 1) * 16 + m) * 32 + col) * 128 + 32 * w + 4 * h) * 8;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            st_sc1(rDH, (base + 8 * i) * 4, make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]));
-        drain();
-        __syncthreads();
-        if (tid == 0) flag_set(fb + m, T - t + 1);
+        for (int i = 0; i < 4; ++i) {
+            st_g2(rDH, base + 64 * i, acc[4 * i], acc[4 * i + 1], E + t);
+            st_g2(rDH, base + 64 * i + 16, acc[4 * i + 2], acc[4 * i + 3], E + t);
+        }
+        DQ_STAMP(90 + t, so0 && t < 30);
     }
+    DQ_STAMP(2, so0);
 }
 
 // ---------------------------------------------------------------- 3: weight gradients
@@ -615,6 +725,7 @@ struct WgSmem {
         } b;
     };
     float rs[16][64];
+    float Xs[7][32];
     int last;
 };
 
@@ -626,6 +737,8 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
     const int B = a.B, T = a.T, nct = a.nct;
     const int nB = a.C0 / 32;
     int bid = blockIdx.x;
+    DQ_STAMP(210, bid == 0);
+    DQ_STAMP(200, bid == kWgA);
     if (bid < kWgA) {
         // ---- dWih (mat 0) / dWhh (mat 1) tile: rows g in [32 gt, +32), columns k' in [32 kt, +32)
         const int mat = bid >> 6, gt = (bid >> 2) & 15, kt = bid & 3;
@@ -633,14 +746,24 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
         const float* Br = (mat == 0 ? a.F2T : a.H) + (int64_t)(32 * kt + col) * C0 + 4 * h;
         f32x16 acc = {};
         float rsum = 0.f;
-        for (int kc = w; kc * 8 < C0; kc += 16) {  // 8-column chunks, round robin over the waves
-            const float4 av = *reinterpret_cast<const float4*>(Ar + 8 * kc);
-            const float4 bv = *reinterpret_cast<const float4*>(Br + 8 * kc);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
-            rsum += ((av.x + av.y) + av.z) + av.w;
+        const int nch = (int)(C0 / 8);  // 8-column chunks, round robin over the waves, 4 in flight
+        for (int kc0 = w; kc0 < nch; kc0 += 64) {
+            float4 av[4], bv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kc = min(kc0 + 16 * j, nch - 1);
+                av[j] = *reinterpret_cast<const float4*>(Ar + 8 * kc);
+                bv[j] = *reinterpret_cast<const float4*>(Br + 8 * kc);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (kc0 + 16 * j >= nch) break;  // wave-uniform
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, bv[j].x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, bv[j].y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, bv[j].z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, bv[j].w, acc, 0, 0, 0);
+                rsum += ((av[j].x + av[j].y) + av[j].z) + av[j].w;
+            }
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) sm.red[w][r][lane] = acc[r];
@@ -654,6 +777,7 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
                 for (int k = 1; k < 16; ++k) v += sm.red[k][r][lane];
                 G[(int64_t)(32 * gt + rho(r) + 4 * h) * 128 + 32 * kt + col] = v;
             }
+            DQ_STAMP(211, bid == 0);
             if (mat == 0 && kt == 0) {  // db_ih = db_hh = row sums of dZ
                 float v = sm.rs[0][lane];
                 for (int k = 1; k < 16; ++k) v += sm.rs[k][lane];
@@ -674,16 +798,24 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
             f32x16 acc = {};
             const float* Wc = a.params + R_P_WIH + 32 * ot + col;
             const float* Zc = a.dZ + c0 + col;
-#pragma unroll 8
-            for (int p = 0; p < 64; ++p) {
-                const int g = 128 * kq + 2 * p + h;
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Wc[(int64_t)g * 128], Zc[(int64_t)g * C0], acc, 0, 0, 0);
+            for (int p0 = 0; p0 < 64; p0 += 16) {  // 32 operand loads in flight per batch (64 queue worse)
+                float wa16[16], za16[16];
+#pragma unroll
+                for (int p = 0; p < 16; ++p) {
+                    const int g = 128 * kq + 2 * (p0 + p) + h;
+                    wa16[p] = Wc[(int64_t)g * 128];
+                    za16[p] = Zc[(int64_t)g * C0];
+                }
+#pragma unroll
+                for (int p = 0; p < 16; ++p) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa16[p], za16[p], acc, 0, 0, 0);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) sm.b.red2[kq][32 * ot + rho(r) + 4 * h][col] = acc[r];
         }
         for (int k = tid; k < 64 * 32; k += 1024) sm.b.F1s[k >> 5][k & 31] = a.F1T[(int64_t)(k >> 5) * C0 + c0 + (k & 31)];
+        if (tid < 224) sm.Xs[tid % 7][tid / 7] = a.obs[((int64_t)(b0 + tid / 7) * T + t) * 7 + tid % 7];  // x of the 32 columns
         __syncthreads();
+        DQ_STAMP(201, bid == 0);
         for (int k = tid; k < 128 * 32; k += 1024) {
             const int u = k >> 5, c2 = k & 31;
             const float v = ((sm.b.red2[0][u][c2] + sm.b.red2[1][u][c2]) + sm.b.red2[2][u][c2]) + sm.b.red2[3][u][c2];
@@ -691,21 +823,20 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
         }
         __syncthreads();
         float* Wp = a.W2P + (int64_t)bid * kLowN;
-        {   // dW2 partial [k'][j] = sum_c dP2[k'][c] F1[j][c]; db2 partial
-            const int u = tid >> 3, j0 = (tid & 7) * 8;
-            float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            for (int c2 = 0; c2 < 32; ++c2) {
-                const float d = sm.b.dP2[u][c2];
+        if (w < 8) {  // dW2 partial [k'][j] = sum_c dP2[k'][c] F1[j][c]: wave -> tile (k' tile w & 3, j tile w >> 2)
+            const int rt = w & 3, jt = w >> 2;
+            f32x16 acc = {};
 #pragma unroll
-                for (int k = 0; k < 8; ++k) o8[k] = fmaf(d, sm.b.F1s[j0 + k][c2], o8[k]);
-            }
+            for (int p = 0; p < 16; ++p)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sm.b.dP2[32 * rt + col][2 * p + h], sm.b.F1s[32 * jt + col][2 * p + h],
+                                                          acc, 0, 0, 0);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) Wp[R_P_F2W + u * 64 + j0 + k] = o8[k];
-            if ((tid & 7) == 0) {
-                float sb = 0.f;
-                for (int c2 = 0; c2 < 32; ++c2) sb += sm.b.dP2[u][c2];
-                Wp[R_P_F2B + u] = sb;
-            }
+            for (int r = 0; r < 16; ++r) st_wt(&Wp[R_P_F2W + (32 * rt + rho(r) + 4 * h) * 64 + 32 * jt + col], acc[r]);
+        } else if (tid < 512 + 128) {  // db2 partial
+            const int u = tid - 512;
+            float sb = 0.f;
+            for (int c2 = 0; c2 < 32; ++c2) sb += sm.b.dP2[u][c2];
+            st_wt(&Wp[R_P_F2B + u], sb);
         }
         {   // dF1 = W2^T dP2: wave (out tile jt = w & 1, K eighth ke = w >> 1), k = k' = 16 ke + 2p + h
             const int jt = w & 1, ke = w >> 1;
@@ -728,35 +859,66 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
             sm.b.dP1[j][c2] = sm.b.F1s[j][c2] > 0.f ? v : 0.f;
         }
         __syncthreads();
+        DQ_STAMP(204, bid == 0);
         if (tid < 448) {  // dW1 partial [j][i] = sum_c dP1[j][c] x_i[c]
             const int j = tid / 7, i = tid % 7;
             float v = 0.f;
-            for (int c2 = 0; c2 < 32; ++c2) v = fmaf(sm.b.dP1[j][c2], a.obs[((int64_t)(b0 + c2) * T + t) * 7 + i], v);
-            Wp[R_P_F1W + j * 7 + i] = v;
+            for (int c2 = 0; c2 < 32; ++c2) v = fmaf(sm.b.dP1[j][c2], sm.Xs[i][c2], v);
+            st_wt(&Wp[R_P_F1W + j * 7 + i], v);
         } else if (tid < 512) {
             const int j = tid - 448;
             float v = 0.f;
             for (int c2 = 0; c2 < 32; ++c2) v += sm.b.dP1[j][c2];
-            Wp[R_P_F1B + j] = v;
+            st_wt(&Wp[R_P_F1B + j], v);
         }
-        // arrival ticket: the last column tile sums every tile's partials in tile order
+        // arrival ticket: the last R column tiles to finish wait for the rest, then each sums a
+        // quarter of the partials in tile order (the earlier arrivers are done, so the wait is short)
+        const int R = min(4, nB);
         drain();
         __syncthreads();
         if (tid == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             drain();
-            const int k = atomicAdd(a.flags + 7 * nct * 16, 1);
-            sm.last = k == nB - 1;
-            if (sm.last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            drain();
+            const int k = atomicAdd(a.flags + 1, 1);
+            int slot = k - (nB - R);
+            if (slot >= 0) {
+                for (int it = 0; it < (1 << 22); ++it) {
+                    if (__hip_atomic_load(a.flags + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nB) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (it == (1 << 22) - 1) { atomicOr(&a.stats->status, 2); slot = -1; }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                drain();
+            }
+            sm.last = slot;
         }
         __syncthreads();
-        if (!sm.last) return;
-        for (int i = tid; i < kLowN; i += 1024) {
-            float v = 0.f;
-            for (int k = 0; k < nB; ++k) v += a.W2P[(int64_t)k * kLowN + i];
-            a.grad[i] = v;
+        DQ_STAMP(206, bid == 0);
+        DQ_STAMP(207, sm.last == 0);
+        if (sm.last < 0) return;
+        const int per = (kLowN / R + 3) & ~3, lo = sm.last * per, hi = min(kLowN, lo + per);
+        for (int i0 = lo + tid; i0 < hi; i0 += 4 * 1024) {  // 4 elements x 8 tiles = 32 loads in flight
+            float v[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < nB; k += 8) {
+                float x[4][8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int i = min(i0 + e * 1024, hi - 1);
+                        x[e][j] = k + j < nB ? ld_wt(&a.W2P[(int64_t)(k + j) * kLowN + i]) : 0.f;
+                    }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (k + j < nB) v[e] += x[e][j];  // in tile order
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (i0 + e * 1024 < hi) a.grad[i0 + e * 1024] = v[e];
         }
+        DQ_STAMP(208, true);
         return;
     }
     bid -= nB;
@@ -897,6 +1059,16 @@ int check(const pm_drqn* d) {
 }  // namespace pm
 
 using namespace pm;
+
+#ifdef PM_DIAG
+extern "C" int pm_diag_read_drqn(uint64_t* out) {  // [256] stamps of the DRQN kernels
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_buf), sizeof(uint64_t) * 256);
+}
+extern "C" int pm_diag_clear_drqn(void) {
+    static const unsigned long long z[256] = {0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(pm_diag_buf), z, sizeof(z));
+}
+#endif
 
 extern "C" int64_t pm_drqn_work_bytes(int32_t batch, int32_t T) {
     if (batch < 32 || batch % 32 || T < 1) return -1;

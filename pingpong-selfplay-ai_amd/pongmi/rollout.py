@@ -53,12 +53,16 @@ class SelfPlayRollout:
         self.paramsB = _weights(paramsB, PM_QNET_NP, "paramsB", self.env.device)
         self.wB = fold(self.paramsB, _lib.PM_FOLD_EVAL).reshape(-1)
 
+    def reserve(self, steps):
+        """Allocate the heads workspace for launches of up to `steps` vector steps ahead of time."""
+        if self.heads.numel() < int(steps) * PM_ROLL_HEADS:
+            self.heads = torch.empty(int(steps) * PM_ROLL_HEADS, dtype=torch.float32, device=self.env.device)
+
     def run(self, steps, sync=True):
         steps = int(steps)
         if steps < 0:
             raise ValueError("steps must be >= 0")
-        if self.heads.numel() < steps * PM_ROLL_HEADS:
-            self.heads = torch.empty(steps * PM_ROLL_HEADS, dtype=torch.float32, device=self.env.device)
+        self.reserve(steps)
         self.stats.zero_()
         env = self.env
         check(self.lib.pm_rollout(ctypes_ref(env.params), ctypes_ref(env.state), ptr(self.wA), ptr(self.wB),

@@ -30,7 +30,7 @@ using namespace pm;
 
 namespace {
 
-constexpr int kRollBlock = 128;  // wave 0: player A, wave 1: player B, one tile of 32 arenas
+constexpr int kRollBlock = 256;  // waves 2p + j: player p (0 = A, 1 = B), layer-2 tile j; one tile of 32 arenas
 constexpr int kHeadsBlock = 256;
 static_assert(PM_ROLL_HEADS == 264, "heads workspace stride: 256 fragment floats + 4 biases + 4 pad");
 
@@ -52,8 +52,8 @@ struct RollShared {
     float lw[kLwFloats];   // modelA's fragment image
     float lwB[kLwFloats];  // modelB's feature fragments (its heads come from hf)
     float hf[2][320];      // modelB's heads of the step (fragment order, 256 + biases), double-buffered
+    __attribute__((aligned(16))) float part[2][2][64][4];  // [step & 1][player] head chains after c2[0]
     int act[2][2][32];     // [step & 1][player][column]
-    long long red[2][4];
 };
 
 // Stream step t's heads (PM_ROLL_HEADS floats at ws + t * PM_ROLL_HEADS) into dst: one 16-byte and one
@@ -66,6 +66,96 @@ __device__ __forceinline__ void fetch_heads(const float* __restrict__ ws, int t,
     __builtin_amdgcn_global_load_lds((const void*)(src + 256 + (lane & 7)), (lds_void*)(dst + 256), 4, 0, 0);
 }
 
+// Layer 1 (both 32-row tiles) and layer-2 tile jt of tile_hidden (pm_mfma.h), MFMA for MFMA in the same
+// order: the two layer-2 tiles are independent accumulator chains, so a wave computing one of them
+// produces exactly the registers tile_hidden gives for it.
+template <typename F>
+__device__ __forceinline__ void hidden_half(const float* lw, const float (&xs)[4], int lane, int jt, f32x16& c2,
+                                            F&& valu) {
+    const int h = lane >> 5;
+    f32x16 c1[2];
+    const f32x16 zero = {};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const float4 w = reinterpret_cast<const float4*>(lw + F_W1)[t * 64 + lane];
+        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, xs[0], zero, 0, 0, 0);
+        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, xs[1], c1[t], 0, 0, 0);
+        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, xs[2], c1[t], 0, 0, 0);
+        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, xs[3], c1[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) c1[t][r] = relu(c1[t][r]);
+    {
+        const float4* b = reinterpret_cast<const float4*>(lw + F_B2 + (jt * 2 + h) * 16);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 v = b[q4];
+            c2[4 * q4 + 0] = v.x; c2[4 * q4 + 1] = v.y; c2[4 * q4 + 2] = v.z; c2[4 * q4 + 3] = v.w;
+        }
+    }
+    const float4* w2 = reinterpret_cast<const float4*>(lw + F_W2) + lane + jt * 8 * 64;
+    float4 wcur = w2[0];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {  // g = t * 4 + rq (tile_hidden's g8 for this jt)
+        const int t = g >> 2, rq = g & 3;
+        const float4 wnext = w2[((g + 1) & 7) * 64];
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.x, c1[t][4 * rq + 0], c2, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.y, c1[t][4 * rq + 1], c2, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.z, c1[t][4 * rq + 2], c2, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.w, c1[t][4 * rq + 3], c2, 0, 0, 0);
+        valu(g);  // independent VALU work, scheduled between this group's dependent MFMAs
+        wcur = wnext;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// serve_draw (pm_dev.h) for the step-keyed stream, split into four stages so that its integer and fp64
+// work fills the gaps of the dependent MFMA chain: the same expressions in the same order, so the
+// draw is bit-identical. Every lane draws, done or not (the select happens after the tick).
+struct StagedServe {
+    U4 r0, r1;
+    ServeDraw d;
+    __device__ __forceinline__ void stage(int g, const pm_env_params& p, uint32_t i, uint64_t ctr, uint64_t seed) {
+        if (g == 0) r0 = philox(i, TAG_SERVE_STEP, (uint32_t)ctr, (uint32_t)(ctr >> 32), seed);
+        if (g == 1) r1 = philox(i, TAG_SERVE_STEP | 0x100u, (uint32_t)ctr, (uint32_t)(ctr >> 32), seed);
+        if (g == 2) {
+            d.speed = p.speed_lo + (p.speed_hi - p.speed_lo) * u53(r0.x, r0.y);
+            const bool first = u53(r0.z, r0.w) < 0.5;
+            const double lo = first ? p.ang0_lo : p.ang1_lo, hi = first ? p.ang0_hi : p.ang1_hi;
+            const double ang = lo + (hi - lo) * u53(r1.x, r1.y);
+            d.rad = ang * (3.141592653589793 / 180.0);
+            d.spin = p.spin_lo + (p.spin_hi - p.spin_lo) * u53(r1.z, r1.w);
+        }
+        if (g == 3) {
+            double sn, cs;
+            sincos_serve(d.rad, sn, cs);
+            d.vx = d.speed * cs;
+            d.vy = d.speed * sn;
+        }
+    }
+};
+
+// tile_heads' fmaf chains over the rows of one layer-2 tile (t = the tile), continuing from acc.
+__device__ __forceinline__ void heads_half(const float* hf, const f32x16& c2, int lane, int t, float (&acc)[4]) {
+    const float4* hw = reinterpret_cast<const float4*>(hf + (lane >> 5) * 128) + t * 16;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float x = relu(c2[r]);
+        const float4 w = hw[r];
+        acc[0] = fmaf(w.x, x, acc[0]);
+        acc[1] = fmaf(w.y, x, acc[1]);
+        acc[2] = fmaf(w.z, x, acc[2]);
+        acc[3] = fmaf(w.w, x, acc[3]);
+    }
+}
+
+// A block of 4 waves owns one tile of 32 arenas: wave 2 p + j computes layer-2 tile j of player p's
+// forward (p = 0: A on modelA's image, p = 1: B on modelB's features + the step's heads), so each
+// forward is 40 MFMAs deep instead of 72. Wave j = 0 runs the head chains over its tile's rows and
+// hands the four partial sums per lane to wave j = 1 through LDS, which continues them over its rows:
+// the same fmaf sequence as tile_heads, so every Q value and action is bit-identical to pm_qnet_act.
 __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, const pm_env_state s,
                                                         const float* __restrict__ wA, const float* __restrict__ wB,
                                                         const float* __restrict__ ws, double eps, uint64_t seed_env,
@@ -73,12 +163,13 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
                                                         float* __restrict__ obsB, long long* __restrict__ stats,
                                                         int n) {
     __shared__ __attribute__((aligned(16))) RollShared sm;
-    const int lane = threadIdx.x & 63, player = threadIdx.x >> 6, col = lane & 31;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane & 31;
+    const int player = wv >> 1, half = wv & 1;
     const int i = blockIdx.x * 32 + col;
     const bool valid = i < n;
-    stage_frags_lds(wA, sm.lw, blockIdx.x);  // block-wide: chunks spread over both waves
+    stage_frags_lds(wA, sm.lw, blockIdx.x);  // block-wide: chunks spread over the waves
     stage_frags_lds(wB, sm.lwB, blockIdx.x + kLwChunks / 2);
-    if (player) fetch_heads(ws, 0, sm.hf[0], lane);
+    if (wv == 3) fetch_heads(ws, 0, sm.hf[0], lane);
     Arena a = load_arena(s, valid ? i : n - 1);
     const float* lw = player ? sm.lwB : sm.lw;
     long long fin = 0, winB = 0, ptA = 0, ptB = 0;
@@ -86,22 +177,46 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
     __syncthreads();  // both images and step 0's heads in LDS
     for (int st = 0; st < steps; ++st) {
         const uint64_t ctr = counter0 + (uint64_t)st;
-        if (player && st + 1 < steps) fetch_heads(ws, st + 1, sm.hf[(st + 1) & 1], lane);  // lands during the MFMAs
-        float oA[7], oB[7];
+        if (wv == 3 && st + 1 < steps) fetch_heads(ws, st + 1, sm.hf[(st + 1) & 1], lane);  // lands during the MFMAs
+        float oA[7], oB[7], o[7];
         observe(a, oA, oB);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) o[k] = player ? oB[k] : oA[k];  // selects, not a pointer (no scratch)
         float xs[4];
-        tile_inputs(player ? oB : oA, lane >> 5, xs);
-        f32x16 c2[2];
-        tile_hidden(lw, xs, lane, c2);
-        float q[3];
-        tile_heads(player ? sm.hf[st & 1] : sm.lw + F_H, c2, lane, q);
-        int act = argmax3(q);
-        if (player) {  // random.random() < eps ? randint(0, 2) : argmax (train_iterative.py:126-130)
-            const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed_env);
-            if (u53(rr.x, rr.y) < eps) act = (int)below(rr.z, 3u);
+        tile_inputs(o, lane >> 5, xs);
+        f32x16 c2;
+        StagedServe sv;
+        hidden_half(lw, xs, lane, half, c2, [&](int g) { sv.stage(g, p, (uint32_t)i, ctr, seed_env); });
+        const float* hf = player ? sm.hf[st & 1] : sm.lw + F_H;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        if (half == 0) {
+            heads_half(hf, c2, lane, 0, acc);
+            *reinterpret_cast<float4*>(&sm.part[st & 1][player][lane][0]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
         }
-        if (lane < 32) sm.act[st & 1][player][col] = act;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave B: the next step's heads have landed
+        __syncthreads();  // the chains over layer-2 tile 0
+        if (half == 1) {
+            const float4 pa = *reinterpret_cast<const float4*>(&sm.part[st & 1][player][lane][0]);
+            acc[0] = pa.x; acc[1] = pa.y; acc[2] = pa.z; acc[3] = pa.w;
+            heads_half(hf, c2, lane, 1, acc);
+            float v = acc[0], a0 = acc[1], a1 = acc[2], a2 = acc[3];
+            v += __shfl_xor(v, 32);
+            a0 += __shfl_xor(a0, 32);
+            a1 += __shfl_xor(a1, 32);
+            a2 += __shfl_xor(a2, 32);
+            v += hf[256];
+            a0 += hf[257];
+            a1 += hf[258];
+            a2 += hf[259];
+            const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
+            const float q[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
+            int act = argmax3(q);
+            if (player) {  // random.random() < eps ? randint(0, 2) : argmax (train_iterative.py:126-130)
+                const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed_env);
+                if (u53(rr.x, rr.y) < eps) act = (int)below(rr.z, 3u);
+            }
+            if (lane < 32) sm.act[st & 1][player][col] = act;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 3: the next step's heads have landed
         __syncthreads();  // both players' actions
         const int aA = sm.act[st & 1][0][col], aB = sm.act[st & 1][1][col];
         float rA, rB;
@@ -111,12 +226,11 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
         if (d) {  // env.reset() with K1's step-keyed production serve
             fin += 1;
             winB += rB > 0.f ? 1 : 0;
-            ServeDraw sv = serve_draw(p, (uint32_t)i, (uint32_t)ctr, seed_env, TAG_SERVE_STEP, (uint32_t)(ctr >> 32));
-            serve_finish(sv);
-            serve(a, sv.vx, sv.vy, sv.spin);
+            serve_finish(sv.d);  // the rare |angle| >= 135 degree redo
+            serve(a, sv.d.vx, sv.d.vy, sv.d.spin);
         }
     }
-    if (player == 0 && lane < 32 && valid) {  // wave A writes the arenas and their observations
+    if (wv == 0 && lane < 32 && valid) {  // wave 0 writes the arenas and their observations
         store_arena(s, i, a);
         float oA[7], oB[7];
         observe(a, oA, oB);
@@ -124,15 +238,15 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
         store_row7(obsB + (size_t)i * 7, oB);
     }
     if (!stats) return;  // block-uniform
-    const bool mine = player == 0 && lane < 32 && valid;  // one lane per arena
+    const bool mine = wv == 0 && lane < 32 && valid;  // one lane per arena
     long long v[4] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
     }
-    if (player == 0 && lane < 4) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane),
-                                           (unsigned long long)(lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3]));
+    if (wv == 0 && lane < 4) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane),
+                                       (unsigned long long)(lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3]));
 }
 
 }  // namespace

@@ -19,7 +19,7 @@ Rank 0 prints one JSON line. Also reported:
                 interval rocprofv3 --kernel-trace reports) on every 20th production step of an
                 instrumented run after the timed region: FP32 FLOP/s of that QNet work vs the
                 157.3 TF dense FP32 matrix peak; `traffic` = its HBM bytes per
-                launch from the committed counter profile (profiles/r2_pmc.json, same workload), null
+                launch from the committed counter profile (profiles/r3_pmc.json, same workload), null
                 without it
   env_roofline  the first launch, k_actenv (pm_selfplay_actenv): modelB's heads on the features
                 computed ahead, the env tick, replay push and bookkeeping, plus the PER sample +
@@ -91,10 +91,11 @@ def timed_region(one_step, steps, dist, n_events, after=None):
 PEAK_HBM_GBS = 8000.0
 
 
-def pmc_traffic(kernel, profile="r2_pmc.json"):
+def pmc_traffic(kernel, profile="r3_pmc.json"):
     """HBM bytes per launch of `kernel` (`name`, or `name@grid` for one of its launch grids) from the
-    committed rocprofv3 counter profile (profiles/r2_pmc.json: the default workload;
-    profiles/r2_rnn_pmc.json: --workload rnn), or None."""
+    committed rocprofv3 counter profile (profiles/r3_pmc.json: the default workload;
+    profiles/r3_rnn_pmc.json: --workload rnn; profiles/r3_infer_pmc.json: --workload infer, 2 000-step
+    launches), or None."""
     path = os.path.join(ROOT, "profiles", profile)
     try:
         with open(path) as fh:
@@ -342,10 +343,13 @@ def time_drqn_update(D, launches=50):
     rec = sum(_lib.timer_read(_lib.PM_TIMER_DRQN) for _ in range(10)) / 10
     flop = drqn_flop(D.batch, D.T)
     achieved = flop / t / 1e12
+    ks = ("k_dq_embed", "k_dq_recur", "k_dq_wgrad", "k_drqn_norm", "k_drqn_adam")
+    tr = [pmc_traffic(k, "r3_rnn_pmc.json") for k in ks]
+    traffic = round(sum(tr), 1) if all(x is not None for x in tr) and (D.batch, D.T) == (64, 8) else None
     return {"bound": "mfma", "kernel": "pm_drqn_update (k_dq_embed + k_dq_recur + k_dq_wgrad + k_drqn_norm + "
                                        "k_drqn_adam), the whole update",
             "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "update_us": round(t * 1e6, 2),
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "update_us": round(t * 1e6, 2),
             "recur_us": round(rec * 1e6, 2), "launches_per_update": 5, "flop_per_update": flop,
             "batch": D.batch, "T": D.T, "timing": f"HIP events over {launches} back-to-back updates"}
 
@@ -436,7 +440,7 @@ def run_rnn(args, dist, rank, world, allreduce):
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          # modelB's side: 256 blocks x 256 lanes (the overlapped step's only k_rnn_act of
                          # that grid); the plain step's both-players launch has no committed pass
-                         "traffic": pmc_traffic(f"k_rnn_act@{256 * 256}", "r2_rnn_pmc.json") if overlap and n == 32768 else None,
+                         "traffic": pmc_traffic(f"k_rnn_act@{256 * 256}", "r3_rnn_pmc.json") if overlap and n == 32768 else None,
                          "avg_us": round(act_s * 1e6, 2), "flop_per_arena": fpa, "n": n},
         }
         if overlap:
@@ -481,6 +485,13 @@ def cpu_baseline_infer(seconds=12.0, n=4096):
             "sample": f"oracle/cpu_selfplay.py CpuRollout: {steps} vector steps x {n} arenas (both players' QNet "
                       f"f32 + fresh noise per step + eps-greedy + C oracle tick + reset on done), {dt:.1f} s on 1 host core",
             "reference_python_measured": "4 600 env-steps/s, batch-1 QNet rollout, 1 thread (SURVEY 6)"}
+
+
+def infer_traffic(n, chunk, pmc_steps=2000):
+    """k_rollout's HBM bytes for a launch of `chunk` steps, scaled from the committed counter pass
+    (profiles/r3_infer_pmc.json: launches of 2 000 steps at 4 096 arenas); None at other sizes."""
+    b = pmc_traffic("k_rollout", "r3_infer_pmc.json")
+    return None if b is None or n != 4096 else round(b * chunk / pmc_steps, 1)
 
 
 def run_infer(args, dist, rank, world):
@@ -567,7 +578,7 @@ def run_infer(args, dist, rank, world):
                                                     f"{chunk} vector steps per launch)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": infer_traffic(n, chunk),
                          "avg_us": round(k_s * 1e6, 1), "avg_us_per_step": round(k_s / chunk * 1e6, 4),
                          "flop_per_env_step": 2 * FLOP_PER_ARENA, "n": n,
                          "waves": 2 * (-(-n // 32)), "wave_slots": 256 * 4,

@@ -324,7 +324,7 @@ def drqn_flop(B, T):
 
 
 def time_drqn_update(D, launches=50):
-    """The DRQN update alone (pm_drqn_update, 5 launches) back to back on its last batch after the
+    """The DRQN update alone (pm_drqn_update, 4 launches) back to back on its last batch after the
     timed region (HIP events on the stream), and the persistent recurrence k_dq_recur by its own
     dispatch (pm_timer_arm). Restores nothing: it runs after the measured steps."""
     from pongmi import _lib
@@ -343,14 +343,14 @@ def time_drqn_update(D, launches=50):
     rec = sum(_lib.timer_read(_lib.PM_TIMER_DRQN) for _ in range(10)) / 10
     flop = drqn_flop(D.batch, D.T)
     achieved = flop / t / 1e12
-    ks = ("k_dq_embed", "k_dq_recur", "k_dq_wgrad", "k_drqn_norm", "k_drqn_adam")
+    ks = ("k_dq_embed", "k_dq_recur", "k_dq_wgrad", "k_drqn_apply")
     tr = [pmc_traffic(k, "r3_rnn_pmc.json") for k in ks]
     traffic = round(sum(tr), 1) if all(x is not None for x in tr) and (D.batch, D.T) == (64, 8) else None
-    return {"bound": "mfma", "kernel": "pm_drqn_update (k_dq_embed + k_dq_recur + k_dq_wgrad + k_drqn_norm + "
-                                       "k_drqn_adam), the whole update",
+    return {"bound": "mfma", "kernel": "pm_drqn_update (k_dq_embed + k_dq_recur + k_dq_wgrad + k_drqn_apply), "
+                                       "the whole update",
             "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "update_us": round(t * 1e6, 2),
-            "recur_us": round(rec * 1e6, 2), "launches_per_update": 5, "flop_per_update": flop,
+            "recur_us": round(rec * 1e6, 2), "launches_per_update": 4, "flop_per_update": flop,
             "batch": D.batch, "T": D.T, "timing": f"HIP events over {launches} back-to-back updates"}
 
 

@@ -1,6 +1,6 @@
 // K6 — the DRQN update (train_step_rnn, scripts/train_rnn_iterative.py:400-531) on the device.
 //
-// Five launches per update, every matrix product on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32):
+// Four launches per update, every matrix product on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32):
 //
 //   k_dq_embed  (grads 1/3) the batch through the feature layers and the LSTM input projection for
 //               all three streams (modelB on obs, modelB on next, targetB on next): per (stream,
@@ -22,8 +22,9 @@
 //               32-column tile dF2 = Wih^T dZ -> ReLU mask -> dW2 / db2 partials -> dF1 = W2^T dP2
 //               -> dW1 / db1 partials, summed in a fixed order by the last tile to finish (arrival
 //               ticket); the head gradient partials of the column tiles summed likewise.
-//   k_drqn_norm, k_drqn_adam  (pm_drqn_apply) the NoisyLinear sigma gradients (mu gradient x epsilon),
-//               the global-norm clip (fp64 partials, fixed order) and torch's Adam, target sync.
+//   k_drqn_apply (pm_drqn_apply) the NoisyLinear sigma gradients (mu gradient x epsilon), the global-
+//               norm clip (fp64 partials met on an arrival ticket, summed in block order) and torch's
+//               Adam, target sync: four launches per update in all.
 //
 // Every reduction runs in a fixed order and nothing sums through atomics, so an update is
 // bit-reproducible run to run (the arrival ticket only picks which workgroup does the final sum).
@@ -34,7 +35,7 @@ namespace pm {
 namespace {
 
 constexpr int kG = 16;           // workgroups per recurrence group (8 LSTM units each)
-constexpr int kNormBlocks = 256;  // k_drqn_norm blocks (fp64 partials, summed in order by k_drqn_adam)
+constexpr int kNormBlocks = 256;  // k_drqn_apply blocks (fp64 norm partials, summed in block order)
 constexpr int kWgA = 128;        // k_dq_wgrad: dWih / dWhh output tiles
 constexpr int kWgC = 4;          // k_dq_wgrad: head-partial reduce workgroups
 constexpr int kLowN = 8832;      // grad [0, kLowN): W1, b1, W2, b2 (the column-tile partials)
@@ -68,7 +69,7 @@ struct DqArgs {
     float *W2P;  // [C0 / 32][kLowN]          W1 / b1 / W2 / b2 gradient partials per column tile
     double* part;
     int64_t* tstep;
-    int32_t* flags;  // [0] update epoch (the granule tag base), [1] k_dq_wgrad's arrival ticket
+    int32_t* flags;  // [0] update epoch (the granule tag base), [1] k_dq_wgrad's ticket, [2] k_drqn_apply's
 };
 
 // workspace carve-up, 64-float aligned pieces
@@ -201,6 +202,7 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
     if (blockIdx.x == 0 && tid == 0) {  // a new tag epoch for k_dq_recur's hand-offs; the wgrad ticket
         a.flags[0] = a.flags[0] + 1;
         a.flags[1] = 0;
+        a.flags[2] = 0;  // k_drqn_apply's arrival counter (monotonic within an apply, generation-based)
     }
     if (skipped(a)) {  // this replica contributes nothing to the all-reduce
         for (int i = blockIdx.x * 256 + tid; i < PM_RNN_NPARAM + 4; i += gridDim.x * 256) a.grad[i] = 0.f;
@@ -686,11 +688,14 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     *reinterpret_cast<float4*>(&sm.dzs[i][lane][0]) = make_float4(dz[4 * i], dz[4 * i + 1], dz[4 * i + 2], dz[4 * i + 3]);
-            const int64_t cc = (int64_t)t * B + bcol;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a.dZ[(int64_t)(128 * (r >> 2) + 8 * m + 4 * h + (r & 3)) * C0 + cc] = dz[r];
         }
-        if (t == 0) break;  // dh_0 (the zero initial state) is not needed
+        const int64_t cc = (int64_t)t * B + bcol;
+        if (t == 0) {  // dh_0 (the zero initial state) is not needed
+            if (w == 0)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) a.dZ[(int64_t)(128 * (r >> 2) + 8 * m + 4 * h + (r & 3)) * C0 + cc] = dz[r];
+            break;
+        }
         __syncthreads();  // dz fragments (reused at the next step only after every wave has published)
         if (w != 0)
 #pragma unroll
@@ -708,6 +713,9 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
             st_g2(rDH, base + 64 * i, acc[4 * i], acc[4 * i + 1], E + t);
             st_g2(rDH, base + 64 * i + 16, acc[4 * i + 2], acc[4 * i + 3], E + t);
         }
+        if (w == 0)  // for the weight gradients, behind the hand-off stores in this wave's queue
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a.dZ[(int64_t)(128 * (r >> 2) + 8 * m + 4 * h + (r & 3)) * C0 + cc] = dz[r];
         DQ_STAMP(90 + t, so0 && t < 30);
     }
     DQ_STAMP(2, so0);
@@ -718,7 +726,10 @@ struct WgSmem {
     union {
         float red[16][16][64];          // type A: per-wave partial tiles
         struct {
-            float red2[4][128][33];     // type B: dF2 K-quarter partials, later dF1 partials
+            union {
+                float dZs[512][32];     // type B: this column tile's dZ block (the dF2 B operands)
+                float red2[4][128][33]; // type B: dF2 K-quarter partials, later dF1 partials
+            };
             float dP2[128][33];
             float dP1[64][33];
             float F1s[64][33];
@@ -792,23 +803,26 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
         // ---- column tile: columns [c0, c0 + 32) (one time step t, batch rows b0 .. b0 + 31)
         const int64_t c0 = (int64_t)bid * 32;
         const int t = (int)(c0 / B), b0 = (int)(c0 % B);
+        // the dZ block of the tile (512 rows x 128 B) global -> LDS, 8 rows per wave instruction
+        for (int k = w; k < 64; k += 16) {
+            const int row = 8 * k + (lane >> 3);
+            __builtin_amdgcn_global_load_lds((const void*)(a.dZ + (int64_t)row * C0 + c0 + 4 * (lane & 7)),
+                                             (lds_void*)&sm.b.dZs[8 * k][0], 16, 0, 0);
+        }
         // dF2 = Wih^T dZ: wave (out tile ot = w & 3, K quarter kq = w >> 2), k = g = 128 kq + 2p + h
         {
             const int ot = w & 3, kq = w >> 2;
             f32x16 acc = {};
             const float* Wc = a.params + R_P_WIH + 32 * ot + col;
-            const float* Zc = a.dZ + c0 + col;
-            for (int p0 = 0; p0 < 64; p0 += 16) {  // 32 operand loads in flight per batch (64 queue worse)
-                float wa16[16], za16[16];
+            float wa64[64];  // this wave's Wih^T operands, all in flight while the dZ block lands
 #pragma unroll
-                for (int p = 0; p < 16; ++p) {
-                    const int g = 128 * kq + 2 * (p0 + p) + h;
-                    wa16[p] = Wc[(int64_t)g * 128];
-                    za16[p] = Zc[(int64_t)g * C0];
-                }
+            for (int p = 0; p < 64; ++p) wa64[p] = Wc[(int64_t)(128 * kq + 2 * p + h) * 128];
+            drain();
+            __syncthreads();  // the dZ block (global_load_lds) from every wave
 #pragma unroll
-                for (int p = 0; p < 16; ++p) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa16[p], za16[p], acc, 0, 0, 0);
-            }
+            for (int p = 0; p < 64; ++p)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa64[p], sm.b.dZs[128 * kq + 2 * p + h][col], acc, 0, 0, 0);
+            __syncthreads();  // dZs is overlaid by red2
 #pragma unroll
             for (int r = 0; r < 16; ++r) sm.b.red2[kq][32 * ot + rho(r) + 4 * h][col] = acc[r];
         }
@@ -957,79 +971,98 @@ __device__ __forceinline__ int sigma_source(int i, int& ep) {
 }
 
 // ---------------------------------------------------------------- clip + Adam
-__global__ __launch_bounds__(256) void k_drqn_norm(DqArgs a) {
-    __shared__ double red[256];
-    const float ranks = a.grad[PM_RNN_NPARAM];  // replicas that contributed (summed by the all-reduce)
-    if (!(ranks > 0.f)) return;
-    const float inv_world = 1.0f / ranks;
-    const int n = PM_RNN_NPARAM, per = (n + kNormBlocks - 1) / kNormBlocks;
-    const int lo = blockIdx.x * per, hi = min(n, lo + per);
-    double s = 0.0;
-#pragma unroll 4
-    for (int i = lo + threadIdx.x; i < hi; i += 256) {
-        int ep;
-        const int src = i >= R_P_SWSG ? sigma_source(i, ep) : -1;
-        float graw = a.grad[i];
-        if (src >= 0) {
-            graw = a.grad[src] * a.params[ep];
-            a.grad[i] = graw;
-        }
-        const float g = graw * inv_world;
-        s += (double)g * (double)g;
-    }
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) a.part[blockIdx.x] = red[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // tstep[0]: train step (target sync), tstep[1]: Adam t
-        const int64_t ts = a.stats->steps + 1, at = a.stats->adam_t + 1;
-        a.tstep[0] = ts;
-        a.tstep[1] = at;
-        a.stats->steps = ts;
-        a.stats->adam_t = at;
-    }
-}
-
 struct AdamK {
     double lr, beta1, beta2, eps, max_norm;
     int64_t interval;
 };
 
-__global__ __launch_bounds__(256) void k_drqn_adam(DqArgs a, AdamK k, float* params, float* target, float* m_,
-                                                   float* v_) {
+// One launch for the apply (round 3): every block forms its slice's sigma gradients and fp64 sum of
+// squares, arrives on a monotonic ticket and waits for the other blocks (kNormBlocks = 256, one per
+// CU: all resident), sums the 256 partials in block order — the same order in every block, so every
+// block derives the identical clip coefficient — and runs Adam on its slice of the parameters.
+__global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* params, float* target, float* m_,
+                                                    float* v_) {
+    constexpr int kPer = (PM_RNN_NP + kNormBlocks - 1) / kNormBlocks, kEl = (kPer + 255) / 256;
+    __shared__ double red[256];
     __shared__ float cf[3];
     __shared__ int64_t ts_s;
-    const float ranks = a.grad[PM_RNN_NPARAM];
-    if (!(ranks > 0.f)) return;
+    const float ranks = a.grad[PM_RNN_NPARAM];  // replicas that contributed (summed by the all-reduce)
+    if (!(ranks > 0.f)) return;                 // grid-uniform
     const float inv_world = 1.0f / ranks;
-    __shared__ double ps[kNormBlocks];
-    if (threadIdx.x < kNormBlocks) ps[threadIdx.x] = a.part[threadIdx.x];
+    const int64_t ts = a.stats->steps + 1, at = a.stats->adam_t + 1;  // read before any block's arrival
+    // one slice per block for both phases, every operand loaded up front (kEl elements per thread):
+    // the sigma gradients a block forms are the ones its Adam reads
+    const int plo = blockIdx.x * kPer, phi = min(PM_RNN_NP, plo + kPer);
+    float g[kEl], mm[kEl], vv[kEl], pr[kEl];
+    double sq = 0.0;
+#pragma unroll
+    for (int e = 0; e < kEl; ++e) {
+        const int i = plo + threadIdx.x + 256 * e;
+        g[e] = 0.f; mm[e] = 0.f; vv[e] = 0.f; pr[e] = 0.f;
+        if (i < phi) pr[e] = params[i];
+        if (i < min(phi, PM_RNN_NPARAM)) {
+            int ep;
+            const int src = i >= R_P_SWSG ? sigma_source(i, ep) : -1;
+            float graw = src >= 0 ? a.grad[src] * a.params[ep] : a.grad[i];
+            mm[e] = m_[i];
+            vv[e] = v_[i];
+            if (src >= 0) a.grad[i] = graw;
+            g[e] = graw * inv_world;
+            sq += (double)g[e] * (double)g[e];
+        }
+    }
+    red[threadIdx.x] = sq;
     __syncthreads();
+    for (int kk = 128; kk > 0; kk >>= 1) {
+        if (threadIdx.x < kk) red[threadIdx.x] += red[threadIdx.x + kk];
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
-        double ss = 0.0;
-        for (int j = 0; j < kNormBlocks; ++j) ss += ps[j];
+        __hip_atomic_store(a.part + blockIdx.x, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        drain();
+        const uint32_t tk = atomicAdd(reinterpret_cast<unsigned*>(a.flags + 2), 1u);
+        const uint32_t goal = (tk / kNormBlocks + 1) * kNormBlocks;  // this update's generation complete
+        for (int it = 0; it < (1 << 22); ++it) {
+            if ((uint32_t)__hip_atomic_load(a.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - goal < 0x80000000u)
+                break;
+            __builtin_amdgcn_s_sleep(1);
+            if (it == (1 << 22) - 1) atomicOr(&a.stats->status, 4);
+        }
+    }
+    __syncthreads();
+    red[threadIdx.x] = __hip_atomic_load(a.part + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    for (int kk = 128; kk > 0; kk >>= 1) {  // the same fixed tree in every block
+        if (threadIdx.x < kk) red[threadIdx.x] += red[threadIdx.x + kk];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double ss = red[0];
         const float norm = (float)sqrt(ss);
         const float coef = (float)(k.max_norm / ((double)norm + 1e-6));  // clip_coef
-        const int64_t ts = a.tstep[0], at = a.tstep[1];
         const double bc1 = 1.0 - pow(k.beta1, (double)at), bc2 = 1.0 - pow(k.beta2, (double)at);
         cf[0] = coef < 1.0f ? coef : 1.0f;  // clamp(clip_coef, max=1)
         cf[1] = (float)(k.lr / bc1);
         cf[2] = (float)sqrt(bc2);
         ts_s = ts;
-        if (blockIdx.x == 0) a.stats->norm = norm;
+        if (blockIdx.x == 0) {
+            a.stats->norm = norm;
+            a.stats->steps = ts;
+            a.stats->adam_t = at;
+        }
     }
     __syncthreads();
     const float coef = cf[0], step_size = cf[1], bc2s = cf[2];
     const bool sync = ts_s % k.interval == 0;  // targetB.load_state_dict(modelB.state_dict()) (:529-530)
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < PM_RNN_NP; i += gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int e = 0; e < kEl; ++e) {
+        const int i = plo + threadIdx.x + 256 * e;
+        if (i >= phi) continue;
         if (i < PM_RNN_NPARAM) {
-            const float g = (a.grad[i] * inv_world) * coef;
-            float m = m_[i], v = v_[i], p = params[i];
-            m = m + (float)(1.0 - k.beta1) * (g - m);                 // exp_avg.lerp_(grad, 1-beta1)
-            v = v * (float)k.beta2 + (float)(1.0 - k.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
+            const float gc = g[e] * coef;
+            float m = mm[e], v = vv[e], p = pr[e];
+            m = m + (float)(1.0 - k.beta1) * (gc - m);                  // exp_avg.lerp_(grad, 1-beta1)
+            v = v * (float)k.beta2 + (float)(1.0 - k.beta2) * gc * gc;  // mul_(beta2).addcmul_(g, g, 1-beta2)
             const float denom = sqrtf(v) / bc2s + (float)k.eps;
             p = p - step_size * (m / denom);
             params[i] = p;
@@ -1037,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_drqn_adam(DqArgs a, AdamK k, float* par
             v_[i] = v;
             if (sync) target[i] = p;
         } else if (sync) {
-            target[i] = params[i];  // the epsilon buffers
+            target[i] = pr[e];  // the epsilon buffers
         }
     }
 }
@@ -1099,12 +1132,10 @@ extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) {
     DqArgs a{};
     dq_layout(d->batch, d->T, &a, d->work);
     a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats;
-    hipLaunchKernelGGL(k_drqn_norm, dim3(kNormBlocks), dim3(256), 0, st, a);
-    PM_LAUNCHED("k_drqn_norm");
     AdamK k{d->lr, d->beta1, d->beta2, d->adam_eps, d->max_norm, d->target_update_interval};
-    hipLaunchKernelGGL(k_drqn_adam, dim3(pm_blocks(PM_RNN_NP, 256)), dim3(256), 0, st, a, k, d->params, d->target,
-                       d->adam_m, d->adam_v);
-    PM_LAUNCHED("k_drqn_adam");
+    hipLaunchKernelGGL(k_drqn_apply, dim3(kNormBlocks), dim3(256), 0, st, a, k, d->params, d->target, d->adam_m,
+                       d->adam_v);
+    PM_LAUNCHED("k_drqn_apply");
     return PM_OK;
 }
 

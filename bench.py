@@ -494,6 +494,44 @@ def infer_traffic(n, chunk, pmc_steps=2000):
     return None if b is None or n != 4096 else round(b * chunk / pmc_steps, 1)
 
 
+def time_infer_stepped(wA, pB, n=4096, per_graph=100, replays=5):
+    """The composition K9 replaces, for comparison: per vector step pm_qnet_fold (modelB, fresh noise)
+    -> pm_qnet_act (both players) -> pm_env_step (autoreset), `per_graph` steps captured in one HIP
+    graph (SURVEY 8d's configs[1] recipe), HIP events over `replays` replays."""
+    from pongmi import _lib
+    from pongmi.env import PongEnv2PBatch
+    from pongmi.qnet import act, fold
+    env = PongEnv2PBatch(n, seed=0x5EED, autoreset=True, **ENV_KW)
+    env.reset()
+    wA2 = wA.reshape(1, -1)
+
+    def steps():
+        for _ in range(per_graph):
+            c = env.counter
+            wB = fold(pB, _lib.PM_FOLD_TRAIN_FRESH, seed=0x5EED, counter=c)
+            aA, aB = act(wA2, None, wB, env.obsA, env.obsB, 0.02, seed=env.seed, counter=c)
+            env.step(aA, aB)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        steps()  # warm-up (allocations, lazy loads)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            steps()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(replays):
+            g.replay()
+        e1.record(s)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) * 1e-3 / (per_graph * replays)
+    return {"value": round(n / t, 1), "us_per_step": round(t * 1e6, 3), "launches_per_step": 3,
+            "timing": f"{per_graph} vector steps per HIP graph, events over {replays} replays"}
+
+
 def run_infer(args, dist, rank, world):
     """configs[1]: 4096 arenas/GPU, QNet inference-only self-play (both players act, modelB with fresh
     NoisyNet noise per vector step and eps = 0.02, autoreset), as the K9 megakernel (pm_rollout):
@@ -585,6 +623,7 @@ def run_infer(args, dist, rank, world):
                          "timing": f"pm_timer_arm dispatch of {reps} launches after the timed region; "
                                    f"HIP events incl. the heads fold: {ev_s * 1e6:.1f} us per launch"},
             "rollout": st,
+            "stepped": time_infer_stepped(wA, pB, n) if world == 1 else None,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_infer(args.cpu_seconds, n)

@@ -532,18 +532,33 @@ def time_infer_stepped(wA, pB, n=4096, per_graph=100, replays=5):
             "timing": f"{per_graph} vector steps per HIP graph, events over {replays} replays"}
 
 
+REPLAY_BYTES = 16 * 4 + 4 + 4  # per pushed transition: the 64-B row, its priority and its PER leaf
+
+
 def run_infer(args, dist, rank, world):
     """configs[1]: 4096 arenas/GPU, QNet inference-only self-play (both players act, modelB with fresh
     NoisyNet noise per vector step and eps = 0.02, autoreset), as the K9 megakernel (pm_rollout):
     `--infer-chunk` vector steps per launch, the arenas in registers in between. Shards are independent
-    (per-rank env seed), no collective."""
+    (per-rank env seed), no collective.
+
+    --workload collect: the same launches at configs[2]'s 65 536 arenas with every
+    transition pushed into a 1e6-row PER replay ring (pm_rollout_push; the sum tree's nodes rebuilt
+    after each launch): as many vector steps per launch as the ring holds without a slot being
+    written twice (15)."""
     from pongmi import _lib
     from pongmi.env import PongEnv2PBatch
     from pongmi.qnet import fold, pack_state_dict
-    from pongmi.rollout import STATS, SelfPlayRollout
-    n = args.arenas or 4096
+    from pongmi.replay import DeviceReplay
+    from pongmi.rollout import STATS, STATS_PUSH, SelfPlayRollout
+    collect = args.workload == "collect"
+    n = args.arenas or (65536 if collect else 4096)
     steps = args.steps
     chunk = max(1, min(args.infer_chunk, steps))
+    replay = None
+    if collect:
+        replay = DeviceReplay(args.memory, "cuda")
+        chunk = max(1, min(chunk, args.memory // n))
+        STATS = STATS_PUSH  # noqa: N806
     sdB, sdA, _, wdesc = bench_nets(args.weights, 0)
     pB = pack_state_dict(sdB).reshape(-1)
     wA = fold(pack_state_dict(sdA), _lib.PM_FOLD_TRAIN).reshape(-1)  # modelA: mu + sigma * (its frozen eps)
@@ -552,15 +567,15 @@ def run_infer(args, dist, rank, world):
     R = SelfPlayRollout(env, wA, pB, epsilon=0.02, seed_net=0x5EED + 1000 * rank)
     # the warm-up runs long enough (>= 5000 vector steps, ~15 ms) for the clocks to settle: a 100-step
     # warm-up left the first ~30 ms of the timed launch at ramp-up clocks (timed region 2x the launch)
-    warm = max(args.warmup, 5000)
-    R.reserve(max(chunk, warm))  # the heads workspace is allocated before the timed region
+    warm = max(args.warmup, 5000 if not collect else 600)
+    R.reserve(chunk if collect else max(chunk, warm))  # the heads workspace is allocated before the timed region
     tot = torch.zeros(len(STATS), dtype=torch.int64, device="cuda")
 
     def run(k):
         done = 0
         while done < k:
             c = min(chunk, k - done)
-            tot.add_(R.run(c, sync=False))
+            tot.add_(R.run(c, sync=False, replay=replay)[:len(STATS)])
             done += c
 
     run(warm)  # the same calls as the timed region (torch loads its add kernel lazily on first use)
@@ -589,7 +604,7 @@ def run_infer(args, dist, rank, world):
     e0.record()
     for _ in range(reps):
         _lib.timer_arm(_lib.PM_TIMER_ROLLOUT)
-        R.run(chunk, sync=False)
+        R.run(chunk, sync=False, replay=replay)
     e1.record()
     e1.synchronize()
     ks = [_lib.timer_read(_lib.PM_TIMER_ROLLOUT) for _ in range(reps)]
@@ -627,6 +642,25 @@ def run_infer(args, dist, rank, world):
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_infer(args.cpu_seconds, n)
+        if collect:
+            rb = n * chunk * REPLAY_BYTES / k_s / 1e9
+            out["metric"] = ("env-steps/sec (whole node), collecting self-play rollout: every transition pushed "
+                             "into the PER replay ring (SURVEY 8f3)")
+            out["config"]["workload"] = (f"8f3 at configs[2]'s arena count: {n} arenas/GPU, the configs[1] rollout "
+                                         f"(eps 0.02 held, learner off) + memory.push of every transition into a "
+                                         f"{args.memory}-row PER ring, {chunk} vector steps per launch")
+            out["config"]["replay_cap"] = args.memory
+            out["roofline"]["kernel"] = (f"k_rollout<push> (both players' QNet forward + env tick + replay push, "
+                                         f"{chunk} vector steps per launch)")
+            out["roofline"]["traffic"] = None
+            out["replay_roofline"] = {"bound": "hbm", "achieved": round(rb, 2), "peak": PEAK_HBM_GBS,
+                                      "unit": "GB/s", "frac": round(rb / PEAK_HBM_GBS, 4),
+                                      "bytes_per_transition": REPLAY_BYTES,
+                                      "note": "replay-write bytes (row 64 + priority 4 + PER leaf 4) per launch / "
+                                              "k_rollout<push> dispatch time; the launch is MFMA-latency bound"}
+            out["stepped"] = None
+            out.pop("cpu_baseline", None)
+            out["replay"] = {"pos": replay.pos, "size": replay.size}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -637,9 +671,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="vector steps timed (200; infer: 10000)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed vector steps first (30; infer: 100)")
-    ap.add_argument("--workload", choices=("dqn", "rnn", "infer"), default="dqn",
+    ap.add_argument("--workload", choices=("dqn", "rnn", "infer", "collect"), default="dqn",
                     help="dqn: configs[2] (the headline); rnn: configs[4], the QNetRNN / DRQN loop; infer: "
-                         "configs[1], the inference-only rollout megakernel")
+                         "configs[1], the inference-only rollout megakernel; collect: 8f3, that megakernel "
+                         "pushing every transition into the PER replay ring at 65 536 arenas")
     ap.add_argument("--infer-chunk", type=int, default=10000, help="infer: vector steps per pm_rollout launch")
     ap.add_argument("--arenas", type=int, default=None, help="arenas per GPU (65536 dqn, 32768 rnn)")
     ap.add_argument("--pool", type=int, default=None, help="opponent pool size (synthetic nets; 8 dqn, 4 rnn)")
@@ -661,8 +696,9 @@ def main():
                     help="N > 1: the gradient all-reduce as libpongmi's own RCCL communicator inside one library "
                          "call per vector step (native), or torch.distributed.all_reduce between launches (torch)")
     args = ap.parse_args()
-    infer = args.workload == "infer"
-    args.steps = args.steps if args.steps is not None else (10000 if infer else 200)
+    infer = args.workload in ("infer", "collect")
+    collect = args.workload == "collect"
+    args.steps = args.steps if args.steps is not None else (3000 if collect else 10000 if infer else 200)
     args.warmup = args.warmup if args.warmup is not None else (100 if infer else 30)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

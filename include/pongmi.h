@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 17
+#define PM_ABI_VERSION 18
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -189,6 +189,32 @@ int pm_play(const pm_env_params* p, const float* w_nets, int32_t n_nets, const i
 int pm_rollout(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB, const float* paramsB,
                float epsilon, uint64_t seed_env, uint64_t seed_net, uint64_t counter0, int32_t steps, float* heads_ws,
                float* obsA, float* obsB, int64_t* stats, int32_t n, void* stream);
+
+/* §8f3 — the collecting rollout (ABI 18): pm_rollout's launch that also pushes every vector step's
+ * transitions into a replay ring from registers, as the training loop's memory.push((oB, aB, rB, nB,
+ * done)) (scripts/train_iterative.py:242-243, PrioritizedReplay.push :56-63) with the learner switched
+ * off (no train_step between pushes, epsilon held for the launch). Step s's arena i lands in slot
+ * (pos + s * n + i) mod cap: row (s = obsB before the step, r = rB, s' = the step's terminal obsB,
+ * bits(aB | done << 8)), prios[slot] = prio, and, with per_work, the PER leaf powf(prio, alpha) —
+ * after the launch the sum tree's nodes are rebuilt over the whole ring (per_work then is the
+ * pm_per_work_bytes(cap) tree of pm_per_sample). ep_reward [n] is carried (ep_reward += rB, zeroed
+ * on done). steps * n <= cap (no slot is written twice in one launch). stats (nullable, device,
+ * accumulated) holds 6 entries: pm_rollout's four, then [4] episodes with ep_reward > 0 (the loop's
+ * win, :247-248), [5] the sum of ep_reward over finished episodes. Bit-identical to `steps`
+ * repetitions of pm_rollout's stepped composition with pm_env_step's terminal observations pushed
+ * in arena order (tests/test_gpu_rollout.py). */
+typedef struct pm_roll_replay {
+    float *trans;      /* [cap][PM_TRANS_F], 16-byte aligned */
+    float *prios;      /* [cap] */
+    void *per_work;    /* nullable: PER sum tree (pm_per_work_bytes(cap), 16-byte aligned) */
+    float *ep_reward;  /* [n] */
+    int64_t pos, cap;  /* 0 <= pos < cap */
+    float prio, alpha; /* the pushed priority (max(prios), or 1.0 into an empty buffer) and PER alpha */
+} pm_roll_replay;
+int pm_rollout_push(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB,
+                    const float* paramsB, float epsilon, uint64_t seed_env, uint64_t seed_net, uint64_t counter0,
+                    int32_t steps, float* heads_ws, float* obsA, float* obsB, const pm_roll_replay* rp, int64_t* stats,
+                    int32_t n, void* stream);
 
 /* ---------------------------------------------------------------- QNetRNN (K5) */
 
@@ -388,6 +414,10 @@ int pm_per_sample(const float* prios, int64_t size, float alpha, float beta, con
 /* update_priorities (train_iterative.py:74-76): prios[idx[j]] = |err[j]| + 1e-6, sequential order
  * (the last duplicate index wins). */
 int pm_per_update(float* prios, const int64_t* idx, const float* err, int32_t bs, void* stream);
+/* Full rebuild of a PER sum tree over prios[0, cap) (leaves prio^alpha, then both node levels) into
+ * `work` (pm_per_work_bytes(cap)): the tree pm_rollout_push maintains, after the host changed
+ * priorities by other means (ABI 18). */
+int pm_per_build(const float* prios, int64_t cap, float alpha, void* work, void* stream);
 
 /* ---------------------------------------------------------------- self-play learner (K1+K2+K3+K4) */
 
@@ -600,7 +630,8 @@ int pm_timer_read(int32_t kernel, float* ms);
 const char* pm_last_error(void);
 int pm_abi_version(void);
 int32_t pm_sizeof(int32_t which); /* 0: pm_env_params 1: pm_env_state 2: pm_ctrl 3: pm_selfplay 4: pm_drqn
-                                     5: pm_drqn_stats 6: pm_rnn_ctrl 7: pm_rnn_selfplay */
+                                     5: pm_drqn_stats 6: pm_rnn_ctrl 7: pm_rnn_selfplay
+                                     8: pm_roll_replay */
 
 #ifdef __cplusplus
 }

@@ -107,6 +107,7 @@ extern "C" int32_t pm_sizeof(int32_t which) {
         case 5: return (int32_t)sizeof(pm_drqn_stats);
         case 6: return (int32_t)sizeof(pm_rnn_ctrl);
         case 7: return (int32_t)sizeof(pm_rnn_selfplay);
+        case 8: return (int32_t)sizeof(pm_roll_replay);
         default: return -1;
     }
 }

@@ -374,5 +374,7 @@ __device__ inline void per_sample_block(bool active, int64_t size, const PerTree
 int per_launch_build(const float* prios, int64_t cap, float alpha, const pm_ctrl* ctrl, int64_t n_push, void* work,
                      hipStream_t st);
 int per_launch_update(float* prios, const int64_t* idx, const float* err, int bs, hipStream_t st);
+// Level-1 and level-2 nodes over leaves already written (no pending push range).
+int per_launch_nodes(void* work, int64_t cap, hipStream_t st);
 
 }  // namespace pm

@@ -96,6 +96,16 @@ int per_launch_build(const float* prios, int64_t cap, float alpha, const pm_ctrl
     PM_LAUNCHED("k_per_chunks");
     return PM_OK;
 }
+int per_launch_nodes(void* work, int64_t cap, hipStream_t st) {
+    const PerTree tr = per_tree(work, cap);
+    const auto grid = [](int64_t n) { return (unsigned)(n > 0 ? (n + 255) / 256 : 1); };
+    hipLaunchKernelGGL(k_per_subs, dim3(grid(tr.nsub)), dim3(256), 0, st, cap, 0.f, (const pm_ctrl*)nullptr,
+                       (int64_t)0, tr);
+    PM_LAUNCHED("k_per_subs");
+    hipLaunchKernelGGL(k_per_chunks, dim3(grid(tr.nchunk)), dim3(256), 0, st, tr);
+    PM_LAUNCHED("k_per_chunks");
+    return PM_OK;
+}
 int per_launch_update(float* prios, const int64_t* idx, const float* err, int bs, hipStream_t st) {
     hipLaunchKernelGGL(k_per_update, dim3(pm_blocks(bs, 256)), dim3(256), 0, st, prios, idx, err, bs);
     PM_LAUNCHED("k_per_update");
@@ -118,6 +128,13 @@ extern "C" int pm_per_sample(const float* prios, int64_t size, float alpha, floa
     hipLaunchKernelGGL(k_per_normalize, dim3(1), dim3(1024), 0, st, w, bs);
     PM_LAUNCHED("k_per_normalize");
     return PM_OK;
+}
+
+extern "C" int pm_per_build(const float* prios, int64_t cap, float alpha, void* work, void* stream) {
+    PM_REQUIRE(prios && work, PM_E_ARG, "pm_per_build: null buffer");
+    PM_REQUIRE(cap > 0, PM_E_SIZE, "pm_per_build: cap=%lld", (long long)cap);
+    PM_REQUIRE(((uintptr_t)work & 15) == 0, PM_E_ARG, "pm_per_build: work must be 16-byte aligned");
+    return per_launch_build(prios, cap, alpha, nullptr, 0, work, pm_stream(stream));
 }
 
 extern "C" int pm_per_update(float* prios, const int64_t* idx, const float* err, int32_t bs, void* stream) {

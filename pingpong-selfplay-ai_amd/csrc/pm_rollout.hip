@@ -23,8 +23,17 @@
 // Bit-identical to `steps` repetitions of pm_qnet_fold(paramsB, FRESH, seed_net, c) ->
 // pm_qnet_act({wA}, NULL, w_B, obsA, obsB, epsilon, seed_env, c) -> pm_env_step(autoreset, seed_env,
 // c) with c = counter0 + s (tests/test_gpu_rollout.py).
+//
+// pm_rollout_push (§8f3, the collecting rollout) runs the same launch and also writes every vector
+// step's transitions straight from registers into the replay ring, as memory.push((oB, aB, rB, nB,
+// done)) does in the training loop (train_iterative.py:242-243, :56-63): one 64-byte row (s[7], r,
+// s'[7], bits(aB | done << 8)), its priority and its PER leaf, with ep_reward carried per arena
+// (:238, :245) and the episodes' win / reward counts (:247-249). Wave 3 issues the step's three
+// stores right after the tick; the vmcnt(0) it already waits on for the next step's heads retires
+// them a full step later, so no store latency reaches the step's critical path.
 #include "pm_host.h"
 #include "pm_mfma.h"
+#include "pm_per.h"
 
 using namespace pm;
 
@@ -64,6 +73,27 @@ __device__ __forceinline__ void fetch_heads(const float* __restrict__ ws, int t,
     __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(src) + lane), (lds_void*)dst, 16,
                                      0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(src + 256 + (lane & 7)), (lds_void*)(dst + 256), 4, 0, 0);
+}
+
+// fetch_heads for the loop: the same two LDS-DMA loads issued from inline asm. With the builtin the
+// compiler cannot tell the DMA's LDS target from the weight image the next ds_reads hit and puts a
+// vmcnt(0) right behind the fetch (measured in the ISA: the prefetch then overlapped nothing, and a
+// collecting launch's replay stores were waited there too). Issued here, the only wait is the
+// explicit vmcnt(0) wave 3 executes before the step's second barrier.
+__device__ __forceinline__ void fetch_heads_async(const float* __restrict__ ws, int t, float* dst, int lane) {
+    const float* src = ws + (size_t)t * PM_ROLL_HEADS;
+    const uint32_t m0a = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+    const float4* g4 = reinterpret_cast<const float4*>(src) + lane;
+    const float* g1 = src + 256 + (lane & 7);
+    asm volatile(
+        "s_mov_b32 m0, %0\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, off\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %3, off" ::"s"(m0a),
+        "s"(m0a + 1024u), "v"(g4), "v"(g1)
+        : "memory", "m0");
 }
 
 // Layer 1 (both 32-row tiles) and layer-2 tile jt of tile_hidden (pm_mfma.h), MFMA for MFMA in the same
@@ -151,17 +181,28 @@ __device__ __forceinline__ void heads_half(const float* hf, const f32x16& c2, in
     }
 }
 
+// The collecting rollout's replay target (pm_roll_replay, device side).
+struct RollPush {
+    float* trans;
+    float* prios;
+    float* leaf;       // nullable: the PER leaves (prio^alpha) of pm_per_work_bytes(cap) work
+    float* ep_reward;  // [n], carried
+    int64_t pos, cap;  // ring slot of step 0's arena 0; steps * n <= cap, so no slot is written twice
+    float prio, alpha;
+};
+
 // A block of 4 waves owns one tile of 32 arenas: wave 2 p + j computes layer-2 tile j of player p's
 // forward (p = 0: A on modelA's image, p = 1: B on modelB's features + the step's heads), so each
 // forward is 40 MFMAs deep instead of 72. Wave j = 0 runs the head chains over its tile's rows and
 // hands the four partial sums per lane to wave j = 1 through LDS, which continues them over its rows:
 // the same fmaf sequence as tile_heads, so every Q value and action is bit-identical to pm_qnet_act.
+template <bool PUSH>
 __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, const pm_env_state s,
                                                         const float* __restrict__ wA, const float* __restrict__ wB,
                                                         const float* __restrict__ ws, double eps, uint64_t seed_env,
                                                         uint64_t counter0, int steps, float* __restrict__ obsA,
                                                         float* __restrict__ obsB, long long* __restrict__ stats,
-                                                        int n) {
+                                                        int n, const RollPush rp) {
     __shared__ __attribute__((aligned(16))) RollShared sm;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane & 31;
     const int player = wv >> 1, half = wv & 1;
@@ -172,12 +213,17 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
     if (wv == 3) fetch_heads(ws, 0, sm.hf[0], lane);
     Arena a = load_arena(s, valid ? i : n - 1);
     const float* lw = player ? sm.lwB : sm.lw;
-    long long fin = 0, winB = 0, ptA = 0, ptB = 0;
+    long long fin = 0, winB = 0, ptA = 0, ptB = 0, winE = 0, rsum = 0;
+    float er = 0.f, leafv = 0.f;
+    if constexpr (PUSH) {
+        er = rp.ep_reward[valid ? i : n - 1];
+        leafv = prio_pow(rp.prio, rp.alpha);  // memory.push's priority as a PER leaf
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // both images and step 0's heads in LDS
     for (int st = 0; st < steps; ++st) {
         const uint64_t ctr = counter0 + (uint64_t)st;
-        if (wv == 3 && st + 1 < steps) fetch_heads(ws, st + 1, sm.hf[(st + 1) & 1], lane);  // lands during the MFMAs
+        if (wv == 3 && st + 1 < steps) fetch_heads_async(ws, st + 1, sm.hf[(st + 1) & 1], lane);  // lands during the MFMAs
         float oA[7], oB[7], o[7];
         observe(a, oA, oB);
 #pragma unroll
@@ -216,13 +262,35 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
             }
             if (lane < 32) sm.act[st & 1][player][col] = act;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 3: the next step's heads have landed
+        // wave 3: the next step's heads have landed (and, collecting, the previous step's replay stores)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // both players' actions
         const int aA = sm.act[st & 1][0][col], aB = sm.act[st & 1][1][col];
         float rA, rB;
         const int d = tick(p, a, aA, aB, rA, rB);
         ptA += rA > 0.f ? 1 : 0;
         ptB += rB > 0.f ? 1 : 0;
+        if constexpr (PUSH) {
+            er += rB;  // ep_reward += rB (:245)
+            if (d) {
+                winE += er > 0.f ? 1 : 0;
+                rsum += (long long)er;
+            }
+            if (wv == 3 && valid) {  // memory.push((oB, aB, rB, nB, done)): lanes < 32 s, lanes >= 32 s'
+                float nA[7], nB[7];
+                observe(a, nA, nB);  // the terminal observation, before the serve
+                int64_t slot = rp.pos + (int64_t)st * n + i;
+                if (slot >= rp.cap) slot -= rp.cap;
+                float4* row = reinterpret_cast<float4*>(rp.trans + slot * PM_TRANS_F) + (lane >> 5) * 2;
+                const bool hi = lane >= 32;
+                st_f4<false>(row, hi ? make_float4(nB[0], nB[1], nB[2], nB[3]) : make_float4(oB[0], oB[1], oB[2], oB[3]));
+                st_f4<false>(row + 1, hi ? make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)))
+                                         : make_float4(oB[4], oB[5], oB[6], rB));
+                if (!hi) rp.prios[slot] = rp.prio;
+                else if (rp.leaf) rp.leaf[slot] = leafv;
+            }
+            if (d) er = 0.f;
+        }
         if (d) {  // env.reset() with K1's step-keyed production serve
             fin += 1;
             winB += rB > 0.f ? 1 : 0;
@@ -236,39 +304,80 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
         observe(a, oA, oB);
         store_row7(obsA + (size_t)i * 7, oA);
         store_row7(obsB + (size_t)i * 7, oB);
+        if constexpr (PUSH) rp.ep_reward[i] = er;
     }
     if (!stats) return;  // block-uniform
+    constexpr int NS = PUSH ? 6 : 4;
     const bool mine = wv == 0 && lane < 32 && valid;  // one lane per arena
-    long long v[4] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0};
+    long long v[6] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0, mine ? winE : 0,
+                      mine ? rsum : 0};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NS; ++k) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
     }
-    if (wv == 0 && lane < 4) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane),
-                                       (unsigned long long)(lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3]));
+    long long mv = v[0];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) mv = lane == k ? v[k] : mv;
+    if (wv == 0 && lane < NS) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane), (unsigned long long)mv);
 }
 
 }  // namespace
+
+static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB,
+                          const float* paramsB, float epsilon, uint64_t seed_env, uint64_t seed_net, uint64_t counter0,
+                          int32_t steps, float* heads_ws, float* obsA, float* obsB, const RollPush* rp, void* per_work,
+                          int64_t* stats, int32_t n, void* stream) {
+    const char* name = rp ? "pm_rollout_push" : "pm_rollout";
+    PM_REQUIRE(n >= 0 && steps >= 0, PM_E_SIZE, "%s: n=%d steps=%d", name, n, steps);
+    if (n == 0 || steps == 0) return PM_OK;
+    PM_REQUIRE(p && s && s->x && s->y && s->vx && s->vy && s->spin && s->top && s->bot && s->scoreA && s->scoreB &&
+                   s->bounces && wA && wB && paramsB && heads_ws && obsA && obsB,
+               PM_E_ARG, "%s: null buffer", name);
+    PM_REQUIRE((((uintptr_t)wA) | ((uintptr_t)wB) | ((uintptr_t)heads_ws)) % 16 == 0, PM_E_ARG,
+               "%s: wA, wB and heads_ws must be 16-byte aligned", name);
+    PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "%s: speed_scale_every must be > 0", name);
+    hipStream_t st = pm_stream(stream);
+    hipLaunchKernelGGL(k_rollout_heads, dim3(steps), dim3(kHeadsBlock), 0, st, paramsB, seed_net, counter0, heads_ws);
+    PM_LAUNCHED("k_rollout_heads");
+    const dim3 grid(pm_blocks(n, 32)), block(kRollBlock);
+    if (rp) {
+        pm_launch(PM_TIMER_ROLLOUT, k_rollout<true>, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
+                  (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n,
+                  *rp);
+        PM_LAUNCHED("k_rollout<push>");
+        if (per_work) return per_launch_nodes(per_work, rp->cap, st);
+        return PM_OK;
+    }
+    pm_launch(PM_TIMER_ROLLOUT, k_rollout<false>, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
+              (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n,
+              RollPush{});
+    PM_LAUNCHED("k_rollout");
+    return PM_OK;
+}
 
 extern "C" int pm_rollout(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB,
                           const float* paramsB, float epsilon, uint64_t seed_env, uint64_t seed_net, uint64_t counter0,
                           int32_t steps, float* heads_ws, float* obsA, float* obsB, int64_t* stats, int32_t n,
                           void* stream) {
-    PM_REQUIRE(n >= 0 && steps >= 0, PM_E_SIZE, "pm_rollout: n=%d steps=%d", n, steps);
-    if (n == 0 || steps == 0) return PM_OK;
-    PM_REQUIRE(p && s && s->x && s->y && s->vx && s->vy && s->spin && s->top && s->bot && s->scoreA && s->scoreB &&
-                   s->bounces && wA && wB && paramsB && heads_ws && obsA && obsB,
-               PM_E_ARG, "pm_rollout: null buffer");
-    PM_REQUIRE((((uintptr_t)wA) | ((uintptr_t)wB) | ((uintptr_t)heads_ws)) % 16 == 0, PM_E_ARG,
-               "pm_rollout: wA, wB and heads_ws must be 16-byte aligned");
-    PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_rollout: speed_scale_every must be > 0");
-    hipStream_t st = pm_stream(stream);
-    hipLaunchKernelGGL(k_rollout_heads, dim3(steps), dim3(kHeadsBlock), 0, st, paramsB, seed_net, counter0, heads_ws);
-    PM_LAUNCHED("k_rollout_heads");
-    pm_launch(PM_TIMER_ROLLOUT, k_rollout, dim3(pm_blocks(n, 32)), dim3(kRollBlock), st, *p, *s, wA, wB,
-              (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
-              reinterpret_cast<long long*>(stats), n);
-    PM_LAUNCHED("k_rollout");
-    return PM_OK;
+    return rollout_launch(p, s, wA, wB, paramsB, epsilon, seed_env, seed_net, counter0, steps, heads_ws, obsA, obsB,
+                          nullptr, nullptr, stats, n, stream);
+}
+
+extern "C" int pm_rollout_push(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB,
+                               const float* paramsB, float epsilon, uint64_t seed_env, uint64_t seed_net,
+                               uint64_t counter0, int32_t steps, float* heads_ws, float* obsA, float* obsB,
+                               const pm_roll_replay* rp, int64_t* stats, int32_t n, void* stream) {
+    PM_REQUIRE(rp && rp->trans && rp->prios && rp->ep_reward, PM_E_ARG, "pm_rollout_push: null replay buffer");
+    PM_REQUIRE(rp->cap > 0 && rp->pos >= 0 && rp->pos < rp->cap, PM_E_SIZE, "pm_rollout_push: pos=%lld cap=%lld",
+               (long long)rp->pos, (long long)rp->cap);
+    PM_REQUIRE(n >= 0 && steps >= 0 && (int64_t)steps * n <= rp->cap, PM_E_SIZE,
+               "pm_rollout_push: steps * n = %lld exceeds cap %lld (a slot would be written twice in one launch)",
+               (long long)steps * n, (long long)rp->cap);
+    PM_REQUIRE(((uintptr_t)rp->trans) % 16 == 0 && ((uintptr_t)rp->per_work) % 16 == 0, PM_E_ARG,
+               "pm_rollout_push: trans and per_work must be 16-byte aligned");
+    const RollPush d{rp->trans, rp->prios, rp->per_work ? per_tree(rp->per_work, rp->cap).leaf : nullptr,
+                     rp->ep_reward, rp->pos, rp->cap, rp->prio, rp->alpha};
+    return rollout_launch(p, s, wA, wB, paramsB, epsilon, seed_env, seed_net, counter0, steps, heads_ws, obsA, obsB,
+                          &d, rp->per_work, stats, n, stream);
 }

@@ -35,7 +35,7 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 17
+ABI_VERSION = 18
 PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_ROLLOUT, PM_TIMER_DRQN, PM_TIMER_N = \
     0, 1, 2, 3, 4, 5, 6
 PM_ROLL_HEADS = 264
@@ -72,6 +72,11 @@ class SelfPlay(ctypes.Structure):
                                  "pool_ratio", "beta_start")] + \
         [("beta_frames", c_i64), ("target_update_interval", c_i64), ("seed_env", c_u64), ("seed_net", c_u64),
          ("featB", c_void_p), ("frow", c_void_p), ("frow_ready", c_i32), ("_pad1", c_i32)]
+
+
+class RollReplay(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("trans", "prios", "per_work", "ep_reward")] + \
+        [("pos", c_i64), ("cap", c_i64), ("prio", c_float), ("alpha", c_float)]
 
 
 class DrqnStats(ctypes.Structure):
@@ -125,6 +130,9 @@ _SIGS = {
                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pm_rollout": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_u64, c_u64, c_u64, c_i32,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
+    "pm_per_build": (c_i32, [c_void_p, c_i64, c_float, c_void_p, c_void_p]),
+    "pm_rollout_push": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_u64, c_u64, c_u64,
+                                c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_drqn_work_bytes": (c_i64, [c_i32, c_i32]),
     "pm_drqn_grads": (c_i32, [c_void_p, c_void_p]),
     "pm_drqn_apply": (c_i32, [c_void_p, c_void_p]),

@@ -13,6 +13,12 @@ launch runs `steps` vector steps with every arena held in registers; the result 
 with c = env.counter (tests/test_gpu_rollout.py). The rollout advances env.counter by `steps`, and
 leaves env.obsA / env.obsB holding the observations after the last step; rewards / done / term_obs
 of the last step are not produced (no learner consumes them).
+
+With `replay=` (a pongmi.replay.DeviceReplay) the same launch is §8f3's collecting rollout
+(pm_rollout_push): every vector step also pushes its n transitions into the ring as the training
+loop's memory.push((oB, aB, rB, nB, done)) (:242-243) — the rows go from registers to the ring, and
+the launch leaves the PER sum tree current — with ep_reward carried per arena (:245) and the stats
+gaining the loop's episode wins (ep_reward > 0, :247) and reward sum.
 """
 import torch
 
@@ -21,6 +27,7 @@ from ._lib import PM_QNET_NP, PM_QNET_NW, PM_ROLL_HEADS, check, ptr, require_dev
 from .env import ctypes_ref
 
 STATS = ("episodes", "wins_B", "points_A", "points_B")
+STATS_PUSH = STATS + ("wins_B_episode", "reward_B")
 
 
 class SelfPlayRollout:
@@ -45,7 +52,8 @@ class SelfPlayRollout:
         # modelB's feature layers (its heads are refolded inside the launch every vector step)
         self.wB = fold(self.paramsB, _lib.PM_FOLD_EVAL).reshape(-1)
         self.heads = torch.empty(0, dtype=torch.float32, device=env.device)
-        self.stats = torch.zeros(len(STATS), dtype=torch.int64, device=env.device)
+        self.stats = torch.zeros(len(STATS_PUSH), dtype=torch.int64, device=env.device)
+        self.ep_reward = torch.zeros(env.n, dtype=torch.float32, device=env.device)  # collecting: per arena
 
     def set_paramsB(self, paramsB):
         """New modelB parameters (e.g. after a generation's training)."""
@@ -58,21 +66,38 @@ class SelfPlayRollout:
         if self.heads.numel() < int(steps) * PM_ROLL_HEADS:
             self.heads = torch.empty(int(steps) * PM_ROLL_HEADS, dtype=torch.float32, device=self.env.device)
 
-    def run(self, steps, sync=True):
+    def run(self, steps, sync=True, replay=None):
+        """replay: None (inference only, pm_rollout) or a DeviceReplay the launch pushes every step's
+        transitions into (pm_rollout_push; steps * n <= replay.cap)."""
         steps = int(steps)
         if steps < 0:
             raise ValueError("steps must be >= 0")
         self.reserve(steps)
         self.stats.zero_()
         env = self.env
-        check(self.lib.pm_rollout(ctypes_ref(env.params), ctypes_ref(env.state), ptr(self.wA), ptr(self.wB),
-                                  ptr(self.paramsB), self.epsilon, env.seed, self.seed_net, env.counter, steps,
-                                  ptr(self.heads), ptr(env.obsA), ptr(env.obsB), ptr(self.stats), env.n, stream_ptr()),
-              "pm_rollout")
+        names = STATS
+        if replay is None:
+            check(self.lib.pm_rollout(ctypes_ref(env.params), ctypes_ref(env.state), ptr(self.wA), ptr(self.wB),
+                                      ptr(self.paramsB), self.epsilon, env.seed, self.seed_net, env.counter, steps,
+                                      ptr(self.heads), ptr(env.obsA), ptr(env.obsB), ptr(self.stats), env.n,
+                                      stream_ptr()), "pm_rollout")
+        else:
+            names = STATS_PUSH
+            rp = _lib.RollReplay(trans=ptr(replay.trans), prios=ptr(replay.prios), per_work=ptr(replay.work),
+                                 ep_reward=ptr(self.ep_reward), pos=replay.pos, cap=replay.cap,
+                                 prio=replay.push_prio(), alpha=replay.alpha)
+            check(self.lib.pm_rollout_push(ctypes_ref(env.params), ctypes_ref(env.state), ptr(self.wA), ptr(self.wB),
+                                           ptr(self.paramsB), self.epsilon, env.seed, self.seed_net, env.counter,
+                                           steps, ptr(self.heads), ptr(env.obsA), ptr(env.obsB), ctypes_ref(rp),
+                                           ptr(self.stats), env.n, stream_ptr()), "pm_rollout_push")
+            if steps and env.n:
+                if replay.size == 0:
+                    replay.max_prio = 1.0
+                replay.advance(steps * env.n)
         env.counter += steps
         if not sync:
             return self.stats
-        return dict(zip(STATS, (int(v) for v in self.stats.cpu().tolist())))
+        return dict(zip(names, (int(v) for v in self.stats[:len(names)].cpu().tolist())))
 
 
 def _weights(t, size, name, device):

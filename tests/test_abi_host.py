@@ -34,7 +34,8 @@ def test_struct_layouts_and_constants_match_header():
     from pongmi import _lib
     L = _lib.load()
     assert L.pm_abi_version() == _lib.ABI_VERSION
-    for which, cls in ((0, _lib.EnvParams), (1, _lib.EnvState), (2, _lib.Ctrl), (3, _lib.SelfPlay)):
+    for which, cls in ((0, _lib.EnvParams), (1, _lib.EnvState), (2, _lib.Ctrl), (3, _lib.SelfPlay),
+                       (8, _lib.RollReplay)):
         assert L.pm_sizeof(which) == __import__("ctypes").sizeof(cls)
     hdr = open(os.path.join(ROOT, "include", "pongmi.h")).read()
     for k in ("PM_QNET_NP", "PM_QNET_NHEAD", "PM_QNET_HEAD_OFF", "PM_QNET_EPS_OFF", "PM_QNET_NW", "PM_TRANS_F",

@@ -105,3 +105,126 @@ def test_rollout_failure_paths():
     assert all(np.array_equal(before[k], after[k]) for k in before)
     with pytest.raises(ValueError):
         r.run(-1)
+
+
+# ---------------------------------------------------------------------------------------------------
+# §8f3: the collecting rollout (pm_rollout_push) — the same launch with every transition pushed into
+# the replay ring from registers. Checked bit for bit against the stepped composition above with the
+# training loop's memory.push((oB, aB, rB, nB, done)) (scripts/train_iterative.py:242-243) applied
+# on the host in arena order, ep_reward / win bookkeeping (:245-248), and the PER sum tree against a
+# full rebuild from the priorities (pm_per_sample's build).
+
+
+def _stepped_push(env, wA, paramsB, eps, seed_net, steps, ring, ep, prio, alpha):
+    """`steps` stepped vector steps; pushes into the host ring dict (trans, prios, pos, cap)."""
+    from pongmi import _lib
+    from pongmi.qnet import act, fold
+    n, cap = env.n, ring["cap"]
+    tot = np.zeros(6, np.int64)
+    for _ in range(steps):
+        c = env.counter
+        wB = fold(paramsB, _lib.PM_FOLD_TRAIN_FRESH, seed=seed_net, counter=c)
+        aA, aB = act(wA.reshape(1, -1), None, wB, env.obsA, env.obsB, eps, seed=env.seed, counter=c)[:2]
+        s = env.obsB.cpu().numpy().copy()
+        _, (rA, rB), done, info = env.step(aA, aB)
+        nB = info["term_obsB"].cpu().numpy()
+        r = rB.cpu().numpy()
+        d = done.cpu().numpy().astype(bool)
+        a = aB.cpu().numpy().astype(np.int32)
+        slot = (ring["pos"] + np.arange(n)) % cap
+        ring["trans"][slot, 0:7] = s
+        ring["trans"][slot, 7] = r
+        ring["trans"][slot, 8:15] = nB
+        ring["trans"][slot, 15] = (a | (d.astype(np.int32) << 8)).view(np.float32)
+        ring["prios"][slot] = prio
+        ring["pos"] = (ring["pos"] + n) % cap
+        ep += r
+        tot += np.array([d.sum(), (d & (r > 0)).sum(), (rA.cpu().numpy() > 0).sum(), (r > 0).sum(),
+                         (d & (ep > 0)).sum(), int(ep[d].sum())])
+        ep[d] = 0
+    return tot
+
+
+def _tree_equals_rebuild(replay):
+    """The launch-maintained sum tree equals pm_per_sample's full rebuild from prios (size == cap)."""
+    from pongmi import replay as rp
+    assert replay.size == replay.cap
+    rp.per_sample(replay.prios, replay.size, 8, 0.4, alpha=replay.alpha, seed=1)
+    ref = rp._workspace(replay.cap, replay.prios.device).cpu()
+    got = replay.work.cpu()
+    nchunk, nsub = -(-replay.cap // 1024), -(-replay.cap // 64)
+    o1 = rp._pad(nchunk)
+    o2 = o1 + rp._pad(nsub)
+    for lo, nbytes in ((0, 8 * nchunk), (o1, 8 * nsub), (o2, 4 * replay.cap)):  # chunk / sub sums, leaves
+        assert torch.equal(got[lo:lo + nbytes], ref[lo:lo + nbytes]), lo
+
+
+@pytest.mark.parametrize("n,cap,launches,eps", [(1000, 1000 * 50, (30, 40), 0.02), (333, 333 * 60, (35, 45), 1.0),
+                                                (4096, 4096 * 24, (10, 14), 0.02)])
+def test_collect_equals_stepped_push(n, cap, launches, eps):
+    from pongmi.replay import DeviceReplay
+    from pongmi.rollout import STATS_PUSH, SelfPlayRollout
+    wA, paramsB = _models(n + 1)
+    seed_env, seed_net = 0xC011 + n, 5 + n
+    fused, ref = _env(n, seed_env), _env(n, seed_env)
+    replay = DeviceReplay(cap, fused.device)
+    roll = SelfPlayRollout(fused, wA, paramsB, epsilon=eps, seed_net=seed_net)
+    ring = {"trans": np.zeros((cap, 16), np.float32), "prios": np.zeros(cap, np.float32), "pos": 0, "cap": cap}
+    ep = np.zeros(n, np.float32)
+    tot = np.zeros(6, np.int64)
+    got = np.zeros(6, np.int64)
+    for k, steps in enumerate(launches):
+        if k == 1:  # priorities changed by a learner between launches: the next push stores their max
+            g = torch.Generator().manual_seed(n)
+            new = torch.rand(replay.size, generator=g) * 3 + 0.01
+            replay.prios[:replay.size] = new.to(replay.prios.device)
+            ring["prios"][:replay.size] = new.numpy()
+            replay.refresh()
+        prio = replay.push_prio()
+        st = roll.run(steps, replay=replay)
+        got += np.array([st[k2] for k2 in STATS_PUSH])
+        tot += _stepped_push(ref, wA, paramsB, eps, seed_net, steps, ring, ep, np.float32(prio), replay.alpha)
+    _same_env(fused, ref)
+    assert got.tolist() == tot.tolist()
+    assert replay.pos == ring["pos"] and replay.size == min(cap, sum(launches) * n)
+    assert np.array_equal(replay.trans.cpu().numpy().view(np.int32), ring["trans"].view(np.int32))
+    assert np.array_equal(replay.prios.cpu().numpy(), ring["prios"])
+    assert np.array_equal(roll.ep_reward.cpu().numpy(), ep)
+    assert got[0] > 0
+    _tree_equals_rebuild(replay)
+
+
+def test_collect_full_size_ring():
+    """configs[2]'s arena count: 65 536 arenas, 15 vector steps in one launch fill a 983 040-row ring
+    exactly; rows, tree and state against the stepped composition."""
+    from pongmi.replay import DeviceReplay
+    from pongmi.rollout import STATS_PUSH, SelfPlayRollout
+    n, steps = 65536, 15
+    cap = n * steps
+    wA, paramsB = _models(11)
+    fused, ref = _env(n, 0x5EED), _env(n, 0x5EED)
+    replay = DeviceReplay(cap, fused.device)
+    roll = SelfPlayRollout(fused, wA, paramsB, epsilon=0.02, seed_net=9)
+    st = roll.run(steps, replay=replay)
+    ring = {"trans": np.zeros((cap, 16), np.float32), "prios": np.zeros(cap, np.float32), "pos": 0, "cap": cap}
+    ep = np.zeros(n, np.float32)
+    tot = _stepped_push(ref, wA, paramsB, 0.02, 9, steps, ring, ep, np.float32(1.0), replay.alpha)
+    _same_env(fused, ref)
+    assert [st[k] for k in STATS_PUSH] == tot.tolist()
+    assert np.array_equal(replay.trans.cpu().numpy().view(np.int32), ring["trans"].view(np.int32))
+    assert np.array_equal(replay.prios.cpu().numpy(), ring["prios"])
+    _tree_equals_rebuild(replay)
+
+
+def test_collect_failure_paths():
+    from pongmi import _lib
+    from pongmi.replay import DeviceReplay
+    from pongmi.rollout import SelfPlayRollout
+    wA, paramsB = _models(2)
+    env = _env(100, 3)
+    roll = SelfPlayRollout(env, wA, paramsB)
+    with pytest.raises(_lib.PongmiError):
+        roll.run(3, replay=DeviceReplay(250, env.device))  # 300 pushes > cap: a slot written twice
+    assert env.counter == 0
+    r = DeviceReplay(300, env.device)
+    assert roll.run(0, replay=r)["episodes"] == 0 and r.size == 0

@@ -467,13 +467,13 @@ def run_rnn(args, dist, rank, world, allreduce):
         sys.exit(3)
 
 
-def cpu_baseline_infer(seconds=12.0, n=4096):
+def cpu_baseline_infer(seconds=12.0, n=4096, replay_cap=0):
     from threadpoolctl import threadpool_limits
     from oracle.cpu_selfplay import CpuRollout
     sdB, _, _, _ = bench_nets("reference", 0)
     np_sd = lambda s: {k: v.numpy() for k, v in s.items()}  # noqa: E731
     with threadpool_limits(1):
-        cpu = CpuRollout(ENV_KW, n, np_sd(sdB), np_sd(sdB), epsilon=0.02)
+        cpu = CpuRollout(ENV_KW, n, np_sd(sdB), np_sd(sdB), epsilon=0.02, replay_cap=replay_cap)
         cpu.step()
         t0 = time.perf_counter()
         steps = 0
@@ -483,7 +483,8 @@ def cpu_baseline_infer(seconds=12.0, n=4096):
         dt = time.perf_counter() - t0
     return {"value": round(n * steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/cpu_selfplay.py CpuRollout: {steps} vector steps x {n} arenas (both players' QNet "
-                      f"f32 + fresh noise per step + eps-greedy + C oracle tick + reset on done), {dt:.1f} s on 1 host core",
+                      f"f32 + fresh noise per step + eps-greedy + C oracle tick + reset on done"
+                      f"{f' + memory.push into a {replay_cap}-row ring' if replay_cap else ''}), {dt:.1f} s on 1 host core",
             "reference_python_measured": "4 600 env-steps/s, batch-1 QNet rollout, 1 thread (SURVEY 6)"}
 
 
@@ -641,7 +642,10 @@ def run_infer(args, dist, rank, world):
             "stepped": time_infer_stepped(wA, pB, n) if world == 1 else None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_infer(args.cpu_seconds, n)
+            # collect: the port at 4 096 arenas with the push (the 65 536-arena vector step would take
+            # most of the bounded sample per step)
+            out["cpu_baseline"] = cpu_baseline_infer(args.cpu_seconds, 4096 if collect else n,
+                                                     replay_cap=args.memory if collect else 0)
         if collect:
             rb = n * chunk * REPLAY_BYTES / k_s / 1e9
             out["metric"] = ("env-steps/sec (whole node), collecting self-play rollout: every transition pushed "
@@ -659,7 +663,6 @@ def run_infer(args, dist, rank, world):
                                       "note": "replay-write bytes (row 64 + priority 4 + PER leaf 4) per launch / "
                                               "k_rollout<push> dispatch time; the launch is MFMA-latency bound"}
             out["stepped"] = None
-            out.pop("cpu_baseline", None)
             out["replay"] = {"pos": replay.pos, "size": replay.size}
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -114,8 +114,18 @@ class CpuRollout:
     fresh NoisyNet noise per vector step (select_action_B, :125-130), the C oracle's tick, reset on
     done. bench.py --workload infer's `cpu_baseline` ("kind": "port"), on one core."""
 
-    def __init__(self, env_kw, n, sdB, sdA, epsilon=0.02, seed=0):
+    def __init__(self, env_kw, n, sdB, sdA, epsilon=0.02, seed=0, replay_cap=0):
         self.rng = np.random.RandomState(seed)
+        # replay_cap > 0: bench --workload collect's baseline — every transition is also pushed, as
+        # memory.push((oB, aB, rB, nB, done)) (:242-243, :56-63), into a [cap][16] f32 ring with its
+        # priority (max priority, 1.0 here: no learner) and PER leaf prio ** 0.6
+        self.cap = int(replay_cap)
+        if self.cap:
+            self.trans = np.zeros((self.cap, 16), np.float32)
+            self.prios = np.zeros(self.cap, np.float32)
+            self.leaves = np.zeros(self.cap, np.float32)
+            self.ep_reward = np.zeros(n, np.float32)
+            self.pos = 0
         self.pv = orc.env_params_from_kwargs(**env_kw)
         self.P = orc.make_params(self.pv)
         self.n, self.eps = n, epsilon
@@ -146,6 +156,19 @@ class CpuRollout:
         qb = _q32(_eff32(self.sdB, True, eps_act), oB)
         aA = np.argmax(_q32(self.effA, oA), 1).astype(np.int8)
         aB = np.where(self.rng.rand(n) < self.eps, self.rng.randint(0, 3, n), np.argmax(qb, 1)).astype(np.int8)
-        _, _, _, done = orc.step_arenas(self.P, self.arr, aA, aB)
+        _, nB, rew, done = orc.step_arenas(self.P, self.arr, aA, aB)
+        if self.cap:
+            slot = (self.pos + np.arange(n)) % self.cap
+            row = self.trans[slot]
+            row[:, 0:7] = oB
+            row[:, 7] = rew[:, 1]
+            row[:, 8:15] = nB
+            row[:, 15] = (aB.astype(np.int32) | (done.astype(np.int32) << 8)).view(np.float32)
+            self.trans[slot] = row
+            self.prios[slot] = 1.0
+            self.leaves[slot] = np.float32(1.0) ** np.float32(0.6)
+            self.pos = (self.pos + n) % self.cap
+            self.ep_reward += rew[:, 1]
+            self.ep_reward[done > 0] = 0.0
         self._serve(done > 0)
         return n

@@ -196,15 +196,26 @@ struct RollPush {
 // forward is 40 MFMAs deep instead of 72. Wave j = 0 runs the head chains over its tile's rows and
 // hands the four partial sums per lane to wave j = 1 through LDS, which continues them over its rows:
 // the same fmaf sequence as tile_heads, so every Q value and action is bit-identical to pm_qnet_act.
+// Waves per SIMD the register budget is sized for (PM_ROLL_WAVES, default 2: 224 registers incl. the
+// 48 accumulator AGPRs; 3 caps the kernel at 168).
+#ifndef PM_ROLL_WAVES
+#define PM_ROLL_WAVES 0
+#endif
+#if PM_ROLL_WAVES > 0
+#define PM_ROLL_ATTR __attribute__((amdgpu_waves_per_eu(PM_ROLL_WAVES, PM_ROLL_WAVES)))
+#else
+#define PM_ROLL_ATTR
+#endif
 template <bool PUSH>
-__global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, const pm_env_state s,
+__global__ __launch_bounds__(kRollBlock) PM_ROLL_ATTR void k_rollout(const pm_env_params p, const pm_env_state s,
                                                         const float* __restrict__ wA, const float* __restrict__ wB,
                                                         const float* __restrict__ ws, double eps, uint64_t seed_env,
                                                         uint64_t counter0, int steps, float* __restrict__ obsA,
                                                         float* __restrict__ obsB, long long* __restrict__ stats,
                                                         int n, const RollPush rp) {
     __shared__ __attribute__((aligned(16))) RollShared sm;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane & 31;
+    const int lane = threadIdx.x & 63, col = lane & 31;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPRs, not VGPRs
     const int player = wv >> 1, half = wv & 1;
     const int i = blockIdx.x * 32 + col;
     const bool valid = i < n;
@@ -213,11 +224,12 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
     if (wv == 3) fetch_heads(ws, 0, sm.hf[0], lane);
     Arena a = load_arena(s, valid ? i : n - 1);
     const float* lw = player ? sm.lwB : sm.lw;
-    long long fin = 0, winB = 0, ptA = 0, ptB = 0, winE = 0, rsum = 0;
+    int fin = 0, winB = 0, ptA = 0, ptB = 0, winE = 0, rsum = 0;  // per arena: |count| <= steps < 2^31
     float er = 0.f, leafv = 0.f;
     if constexpr (PUSH) {
         er = rp.ep_reward[valid ? i : n - 1];
-        leafv = prio_pow(rp.prio, rp.alpha);  // memory.push's priority as a PER leaf
+        // memory.push's priority as a PER leaf (wave-uniform: kept in an SGPR)
+        leafv = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(prio_pow(rp.prio, rp.alpha))));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // both images and step 0's heads in LDS
@@ -260,7 +272,9 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
                 const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed_env);
                 if (u53(rr.x, rr.y) < eps) act = (int)below(rr.z, 3u);
             }
-            if (lane < 32) sm.act[st & 1][player][col] = act;
+            if (lane < 32) {
+                sm.act[st & 1][player][col] = act;
+            }
         }
         // wave 3: the next step's heads have landed (and, collecting, the previous step's replay stores)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -274,7 +288,7 @@ __global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, c
             er += rB;  // ep_reward += rB (:245)
             if (d) {
                 winE += er > 0.f ? 1 : 0;
-                rsum += (long long)er;
+                rsum += (int)er;
             }
             if (wv == 3 && valid) {  // memory.push((oB, aB, rB, nB, done)): lanes < 32 s, lanes >= 32 s'
                 float nA[7], nB[7];

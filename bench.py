@@ -654,14 +654,14 @@ def run_infer(args, dist, rank, world):
                                          f"(eps 0.02 held, learner off) + memory.push of every transition into a "
                                          f"{args.memory}-row PER ring, {chunk} vector steps per launch")
             out["config"]["replay_cap"] = args.memory
-            out["roofline"]["kernel"] = (f"k_rollout<push> (both players' QNet forward + env tick + replay push, "
+            out["roofline"]["kernel"] = (f"k_rollout_push (both players' QNet forward + env tick + replay push, "
                                          f"{chunk} vector steps per launch)")
             out["roofline"]["traffic"] = None
             out["replay_roofline"] = {"bound": "hbm", "achieved": round(rb, 2), "peak": PEAK_HBM_GBS,
                                       "unit": "GB/s", "frac": round(rb / PEAK_HBM_GBS, 4),
                                       "bytes_per_transition": REPLAY_BYTES,
                                       "note": "replay-write bytes (row 64 + priority 4 + PER leaf 4) per launch / "
-                                              "k_rollout<push> dispatch time; the launch is MFMA-latency bound"}
+                                              "k_rollout_push dispatch time; the launch is MFMA-latency bound"}
             out["stepped"] = None
             out["replay"] = {"pos": replay.pos, "size": replay.size}
         print(json.dumps(out), flush=True)

@@ -196,23 +196,12 @@ struct RollPush {
 // forward is 40 MFMAs deep instead of 72. Wave j = 0 runs the head chains over its tile's rows and
 // hands the four partial sums per lane to wave j = 1 through LDS, which continues them over its rows:
 // the same fmaf sequence as tile_heads, so every Q value and action is bit-identical to pm_qnet_act.
-// Waves per SIMD the register budget is sized for (PM_ROLL_WAVES, default 2: 224 registers incl. the
-// 48 accumulator AGPRs; 3 caps the kernel at 168).
-#ifndef PM_ROLL_WAVES
-#define PM_ROLL_WAVES 0
-#endif
-#if PM_ROLL_WAVES > 0
-#define PM_ROLL_ATTR __attribute__((amdgpu_waves_per_eu(PM_ROLL_WAVES, PM_ROLL_WAVES)))
-#else
-#define PM_ROLL_ATTR
-#endif
 template <bool PUSH>
-__global__ __launch_bounds__(kRollBlock) PM_ROLL_ATTR void k_rollout(const pm_env_params p, const pm_env_state s,
-                                                        const float* __restrict__ wA, const float* __restrict__ wB,
-                                                        const float* __restrict__ ws, double eps, uint64_t seed_env,
-                                                        uint64_t counter0, int steps, float* __restrict__ obsA,
-                                                        float* __restrict__ obsB, long long* __restrict__ stats,
-                                                        int n, const RollPush rp) {
+__device__ __forceinline__ void rollout_body(const pm_env_params& p, const pm_env_state& s, const float* __restrict__ wA,
+                                             const float* __restrict__ wB, const float* __restrict__ ws, double eps,
+                                             uint64_t seed_env, uint64_t counter0, int steps, float* __restrict__ obsA,
+                                             float* __restrict__ obsB, long long* __restrict__ stats, int n,
+                                             const RollPush& rp) {
     __shared__ __attribute__((aligned(16))) RollShared sm;
     const int lane = threadIdx.x & 63, col = lane & 31;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPRs, not VGPRs
@@ -336,6 +325,27 @@ __global__ __launch_bounds__(kRollBlock) PM_ROLL_ATTR void k_rollout(const pm_en
     if (wv == 0 && lane < NS) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane), (unsigned long long)mv);
 }
 
+// The inference launch keeps the compiler's own register budget (2 waves per SIMD with the MFMA
+// accumulators in AGPRs: 3.14 us per vector step at 4 096 arenas). The collecting launch runs 65 536
+// arenas, 16 blocks per CU queued: capped at 168 registers it fits 3 waves per SIMD, 19.9 against
+// 21.0 us per vector step (same-box A/B, profiles/r3_roll_ab.txt); the same cap on the inference
+// launch costs 15 % (3.61 us: no AGPR accumulators).
+__global__ __launch_bounds__(kRollBlock) void k_rollout(const pm_env_params p, const pm_env_state s,
+                                                        const float* __restrict__ wA, const float* __restrict__ wB,
+                                                        const float* __restrict__ ws, double eps, uint64_t seed_env,
+                                                        uint64_t counter0, int steps, float* __restrict__ obsA,
+                                                        float* __restrict__ obsB, long long* __restrict__ stats,
+                                                        int n) {
+    rollout_body<false>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
+}
+
+__global__ __launch_bounds__(kRollBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_rollout_push(
+    const pm_env_params p, const pm_env_state s, const float* __restrict__ wA, const float* __restrict__ wB,
+    const float* __restrict__ ws, double eps, uint64_t seed_env, uint64_t counter0, int steps,
+    float* __restrict__ obsA, float* __restrict__ obsB, long long* __restrict__ stats, int n, const RollPush rp) {
+    rollout_body<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
+}
+
 }  // namespace
 
 static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB,
@@ -356,16 +366,15 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
     PM_LAUNCHED("k_rollout_heads");
     const dim3 grid(pm_blocks(n, 32)), block(kRollBlock);
     if (rp) {
-        pm_launch(PM_TIMER_ROLLOUT, k_rollout<true>, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
+        pm_launch(PM_TIMER_ROLLOUT, k_rollout_push, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
                   (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n,
                   *rp);
-        PM_LAUNCHED("k_rollout<push>");
+        PM_LAUNCHED("k_rollout_push");
         if (per_work) return per_launch_nodes(per_work, rp->cap, st);
         return PM_OK;
     }
-    pm_launch(PM_TIMER_ROLLOUT, k_rollout<false>, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
-              (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n,
-              RollPush{});
+    pm_launch(PM_TIMER_ROLLOUT, k_rollout, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
+              (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n);
     PM_LAUNCHED("k_rollout");
     return PM_OK;
 }

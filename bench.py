@@ -656,7 +656,11 @@ def run_infer(args, dist, rank, world):
             out["config"]["replay_cap"] = args.memory
             out["roofline"]["kernel"] = (f"k_rollout_push (both players' QNet forward + env tick + replay push, "
                                          f"{chunk} vector steps per launch)")
-            out["roofline"]["traffic"] = None
+            # HBM bytes per launch from the committed counter passes (profiles/r3_collect_pmc.json,
+            # tools/gpu_r3_collect_pmc.sh: 65 536 arenas, 15-step launches); None at other shapes
+            tb = pmc_traffic("k_rollout_push", "r3_collect_pmc.json")
+            out["roofline"]["traffic"] = tb if (n, chunk) == (65536, 15) else None
+            out["roofline"]["algorithmic_bytes"] = n * chunk * REPLAY_BYTES + n * (136 + 56)
             out["replay_roofline"] = {"bound": "hbm", "achieved": round(rb, 2), "peak": PEAK_HBM_GBS,
                                       "unit": "GB/s", "frac": round(rb / PEAK_HBM_GBS, 4),
                                       "bytes_per_transition": REPLAY_BYTES,

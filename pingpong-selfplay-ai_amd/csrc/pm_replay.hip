@@ -27,11 +27,17 @@ __global__ __launch_bounds__(256) void k_per_leaves(const float* __restrict__ pr
         leaf[e] = prio_pow(prios[e], alpha);
 }
 
+// Four lanes per level-1 node (per_sub_sum4: lane & 3 sums one 16-leaf quarter, the same combine as
+// per_sub_sum), so a wave reads 16 nodes' 4 KB of leaves contiguously instead of 64 scattered 256-B
+// rows. The loop bound is block-uniform: every lane of a group of four reaches the shuffles.
 __global__ __launch_bounds__(256) void k_per_subs(int64_t cap, float alpha, const pm_ctrl* ctrl, int64_t n_push,
                                                   PerTree tr) {
     const PushRange pr = push_range(ctrl, n_push, cap, alpha);
-    for (int64_t s = blockIdx.x * 256 + threadIdx.x; s < tr.nsub; s += (int64_t)gridDim.x * 256)
-        tr.sub[s] = per_sub_sum(tr.leaf, s, pr);
+    for (int64_t t0 = (int64_t)blockIdx.x * 256; t0 < tr.nsub * 4; t0 += (int64_t)gridDim.x * 256) {
+        const int64_t t = t0 + threadIdx.x, sb = t >> 2;
+        const double v = per_sub_sum4(tr.leaf, sb < tr.nsub ? sb : tr.nsub - 1, pr);
+        if ((t & 3) == 0 && sb < tr.nsub) tr.sub[sb] = v;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_per_chunks(PerTree tr) {
@@ -90,7 +96,7 @@ int per_launch_build(const float* prios, int64_t cap, float alpha, const pm_ctrl
     };
     hipLaunchKernelGGL(k_per_leaves, dim3(grid(cap)), dim3(256), 0, st, prios, cap, alpha, tr.leaf);
     PM_LAUNCHED("k_per_leaves");
-    hipLaunchKernelGGL(k_per_subs, dim3(grid(tr.nsub)), dim3(256), 0, st, cap, alpha, ctrl, n_push, tr);
+    hipLaunchKernelGGL(k_per_subs, dim3(grid(tr.nsub * 4)), dim3(256), 0, st, cap, alpha, ctrl, n_push, tr);
     PM_LAUNCHED("k_per_subs");
     hipLaunchKernelGGL(k_per_chunks, dim3(grid(tr.nchunk)), dim3(256), 0, st, tr);
     PM_LAUNCHED("k_per_chunks");
@@ -99,7 +105,7 @@ int per_launch_build(const float* prios, int64_t cap, float alpha, const pm_ctrl
 int per_launch_nodes(void* work, int64_t cap, hipStream_t st) {
     const PerTree tr = per_tree(work, cap);
     const auto grid = [](int64_t n) { return (unsigned)(n > 0 ? (n + 255) / 256 : 1); };
-    hipLaunchKernelGGL(k_per_subs, dim3(grid(tr.nsub)), dim3(256), 0, st, cap, 0.f, (const pm_ctrl*)nullptr,
+    hipLaunchKernelGGL(k_per_subs, dim3(grid(tr.nsub * 4)), dim3(256), 0, st, cap, 0.f, (const pm_ctrl*)nullptr,
                        (int64_t)0, tr);
     PM_LAUNCHED("k_per_subs");
     hipLaunchKernelGGL(k_per_chunks, dim3(grid(tr.nchunk)), dim3(256), 0, st, tr);

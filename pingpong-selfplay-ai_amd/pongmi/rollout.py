@@ -53,7 +53,8 @@ class SelfPlayRollout:
         self.wB = fold(self.paramsB, _lib.PM_FOLD_EVAL).reshape(-1)
         self.heads = torch.empty(0, dtype=torch.float32, device=env.device)
         self.stats = torch.zeros(len(STATS_PUSH), dtype=torch.int64, device=env.device)
-        self.ep_reward = torch.zeros(env.n, dtype=torch.float32, device=env.device)  # collecting: per arena
+        # collecting: ep_reward of each arena's running episode (zero it if the env is reset elsewhere)
+        self.ep_reward = torch.zeros(env.n, dtype=torch.float32, device=env.device)
 
     def set_paramsB(self, paramsB):
         """New modelB parameters (e.g. after a generation's training)."""

@@ -228,3 +228,36 @@ def test_collect_failure_paths():
     assert env.counter == 0
     r = DeviceReplay(300, env.device)
     assert roll.run(0, replay=r)["episodes"] == 0 and r.size == 0
+
+
+def test_collect_without_tree_matches():
+    """per_work = NULL (no PER leaves, no node rebuild): the same rows, priorities and state as with the
+    tree; the host side's DeviceReplay always passes one, so this drives the C-ABI directly."""
+    import ctypes
+    from pongmi import _lib
+    from pongmi._lib import ptr, stream_ptr
+    from pongmi.env import ctypes_ref
+    from pongmi.replay import DeviceReplay
+    from pongmi.rollout import SelfPlayRollout
+    n, steps = 500, 60
+    wA, paramsB = _models(21)
+    a, b = _env(n, 77), _env(n, 77)
+    ra, rb = SelfPlayRollout(a, wA, paramsB, seed_net=4), SelfPlayRollout(b, wA, paramsB, seed_net=4)
+    with_tree = DeviceReplay(n * steps, a.device)
+    ra.run(steps, replay=with_tree)
+    trans = torch.zeros((n * steps, 16), dtype=torch.float32, device=b.device)
+    prios = torch.zeros(n * steps, dtype=torch.float32, device=b.device)
+    rb.reserve(steps)
+    stats = torch.zeros(6, dtype=torch.int64, device=b.device)
+    rp = _lib.RollReplay(trans=ptr(trans), prios=ptr(prios), per_work=None, ep_reward=ptr(rb.ep_reward), pos=0,
+                         cap=n * steps, prio=1.0, alpha=0.6)
+    L = _lib.load()
+    _lib.check(L.pm_rollout_push(ctypes_ref(b.params), ctypes_ref(b.state), ptr(rb.wA), ptr(rb.wB), ptr(rb.paramsB),
+                                 rb.epsilon, b.seed, rb.seed_net, b.counter, steps, ptr(rb.heads), ptr(b.obsA),
+                                 ptr(b.obsB), ctypes.byref(rp), ptr(stats), n, stream_ptr()), "pm_rollout_push")
+    b.counter += steps
+    _same_env(a, b)
+    assert torch.equal(trans.view(torch.int32).cpu(), with_tree.trans.view(torch.int32).cpu())
+    assert torch.equal(prios.cpu(), with_tree.prios.cpu())
+    assert torch.equal(ra.ep_reward.cpu(), rb.ep_reward.cpu())
+    assert int(stats[0]) > 0

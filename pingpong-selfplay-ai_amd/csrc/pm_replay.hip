@@ -40,6 +40,29 @@ __global__ __launch_bounds__(256) void k_per_subs(int64_t cap, float alpha, cons
     }
 }
 
+// Both node levels in one launch: a block computes 64 level-1 nodes (four lanes each, as k_per_subs)
+// into HBM and LDS, then four of its threads sum their 16-node groups into the level-2 nodes in
+// per_chunk_sum's order (same values: the 16 loads per_chunk_sum would issue come from LDS).
+__global__ __launch_bounds__(256) void k_per_nodes(int64_t cap, float alpha, const pm_ctrl* ctrl, int64_t n_push,
+                                                   PerTree tr) {
+    __shared__ double subl[64];
+    const PushRange pr = push_range(ctrl, n_push, cap, alpha);
+    const int64_t sb = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+    const double v = per_sub_sum4(tr.leaf, sb < tr.nsub ? sb : tr.nsub - 1, pr);
+    if ((threadIdx.x & 3) == 0) {
+        subl[threadIdx.x >> 2] = sb < tr.nsub ? v : 0.0;
+        if (sb < tr.nsub) tr.sub[sb] = v;
+    }
+    __syncthreads();
+    const int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x;
+    if (threadIdx.x < 4 && c < tr.nchunk) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < PER_FAN; ++k) acc += subl[threadIdx.x * PER_FAN + k];
+        tr.chunk[c] = acc;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_per_chunks(PerTree tr) {
     for (int64_t c = blockIdx.x * 256 + threadIdx.x; c < tr.nchunk; c += (int64_t)gridDim.x * 256)
         tr.chunk[c] = per_chunk_sum(tr, c);
@@ -105,11 +128,9 @@ int per_launch_build(const float* prios, int64_t cap, float alpha, const pm_ctrl
 int per_launch_nodes(void* work, int64_t cap, hipStream_t st) {
     const PerTree tr = per_tree(work, cap);
     const auto grid = [](int64_t n) { return (unsigned)(n > 0 ? (n + 255) / 256 : 1); };
-    hipLaunchKernelGGL(k_per_subs, dim3(grid(tr.nsub * 4)), dim3(256), 0, st, cap, 0.f, (const pm_ctrl*)nullptr,
-                       (int64_t)0, tr);
-    PM_LAUNCHED("k_per_subs");
-    hipLaunchKernelGGL(k_per_chunks, dim3(grid(tr.nchunk)), dim3(256), 0, st, tr);
-    PM_LAUNCHED("k_per_chunks");
+    hipLaunchKernelGGL(k_per_nodes, dim3((unsigned)((tr.nsub + 63) / 64)), dim3(256), 0, st, cap, 0.f,
+                       (const pm_ctrl*)nullptr, (int64_t)0, tr);
+    PM_LAUNCHED("k_per_nodes");
     return PM_OK;
 }
 int per_launch_update(float* prios, const int64_t* idx, const float* err, int bs, hipStream_t st) {

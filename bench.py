@@ -147,7 +147,7 @@ def synthetic_qnet(seed):
     return {k: v.clone() for k, v in QNet(7, 3).state_dict().items()}
 
 
-def time_env_step(n, per_graph=50, replays=20):
+def time_env_step(n, per_graph=50, replays=40, warm_replays=100):
     """K1 alone: pm_env_step with autoreset of done arenas (term rows for done arenas only: the
     203 B / env-step of SURVEY.md 8d). `per_graph` back-to-back launches are captured in one HIP
     graph so the host launch rate (ctypes, ~8 us per call) does not pace the queue; HIP events on
@@ -171,8 +171,8 @@ def time_env_step(n, per_graph=50, replays=20):
             for _ in range(per_graph):
                 env.step(aA, aB)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for _ in range(3):
-            g.replay()
+        for _ in range(warm_replays):  # ~20 ms of back-to-back K1 first: the clocks settle (a 3-replay
+            g.replay()                 # warm-up read 4.64 us on one box where others gave 4.07-4.17)
         e0.record(s)
         for _ in range(replays):
             g.replay()

@@ -60,11 +60,13 @@ PEAK_FP32_TFLOPS = 157.3
 INSTR = 20  # after the timed region: one instrumented (timer-armed) step per INSTR production steps
 
 
-def timed_region(one_step, steps, dist, n_events, after=None):
+def timed_region(one_step, steps, dist, n_events, after=None, at_end=None):
     """Time exactly `steps` production steps (barrier + synchronize on both sides, max over ranks),
     then run steps // INSTR (at least 5) instrumented steps, each after INSTR - 1 production steps,
     OUTSIDE the timed region (`after()` runs after each, e.g. to read the launch timers): it never
-    counts towards `value`. Returns (seconds, [event tuples])."""
+    counts towards `value`. `at_end()` runs right after the timed region, before any instrumented
+    step (e.g. to read the counters the timed steps left). Returns (seconds, [event tuples], at_end's
+    result)."""
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -79,6 +81,7 @@ def timed_region(one_step, steps, dist, n_events, after=None):
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    end = at_end() if at_end is not None else None
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(n_events)) for _ in range(max(5, steps // INSTR))]
     for ev in evs:
         for _ in range(INSTR - 1):
@@ -87,7 +90,9 @@ def timed_region(one_step, steps, dist, n_events, after=None):
         if after is not None:
             after()
     torch.cuda.synchronize()
-    return dt, evs
+    return dt, evs, end
+
+
 PEAK_HBM_GBS = 8000.0
 
 
@@ -221,14 +226,17 @@ def time_act_full(L, launches=50):
             "timing": f"HIP events over {launches} back-to-back launches"}
 
 
-def cpu_baseline(n, seconds=12.0):
+def cpu_baseline(n, nets, seconds=12.0, epsilon=0.08):
+    """The oracle's CPU port of the same vector step, acting with the GPU leg's nets (`nets` =
+    bench_nets(...): modelB, modelA, pool, description) and its epsilon, so both legs play the same
+    policies (episode lengths, hence reset and bookkeeping load, match)."""
     from threadpoolctl import threadpool_limits
     from oracle.cpu_selfplay import CpuSelfPlay
-    sdB, sdA = synthetic_qnet(1), synthetic_qnet(2)
-    pool = [synthetic_qnet(100 + k) for k in range(4)]
+    sdB, sdA, pool, wdesc = nets
+    np_sd = lambda s: {k: v.numpy() for k, v in s.items()}  # noqa: E731
     with threadpool_limits(1):
-        cpu = CpuSelfPlay(ENV_KW, n, {k: v.numpy() for k, v in sdB.items()}, {k: v.numpy() for k, v in sdA.items()},
-                          [{k: v.numpy() for k, v in s.items()} for s in pool], batch=256, cap=1_000_000)
+        cpu = CpuSelfPlay(ENV_KW, n, np_sd(sdB), np_sd(sdA), [np_sd(s) for s in pool], batch=256, cap=1_000_000,
+                          epsilon=epsilon)
         for _ in range(2):
             cpu.step()
         t0 = time.perf_counter()
@@ -239,7 +247,8 @@ def cpu_baseline(n, seconds=12.0):
         dt = time.perf_counter() - t0
     return {"value": round(n * steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/cpu_selfplay.py: {steps} vector steps x {n} arenas (full DQN loop, PER cap 1e6, "
-                      f"batch 256), {dt:.1f} s on 1 host core"}
+                      f"batch 256, eps {epsilon}, pool {len(pool)}), {dt:.1f} s on 1 host core",
+            "weights": wdesc}
 
 
 def _config0_worker(seconds, seed, q):
@@ -399,8 +408,8 @@ def run_rnn(args, dist, rank, world, allreduce):
     torch.cuda.synchronize()
     c0 = L.counters()
     act_t = []
-    dt, evs = timed_region(one_step, args.steps, dist, 4, lambda: act_t.append(_lib.timer_read(_lib.PM_TIMER_RNN_ACT)))
-    c1 = L.counters()
+    dt, evs, c1 = timed_region(one_step, args.steps, dist, 4, lambda: act_t.append(_lib.timer_read(_lib.PM_TIMER_RNN_ACT)),
+                               L.counters)
     same = replicas_identical(dist, L.learner.params)
     act_s = sum(act_t) / len(act_t)  # k_rnn_act's own dispatch (pm_timer_*), as rocprofv3 times it
     env_s = sum(e[1].elapsed_time(e[2]) for e in evs) * 1e-3 / len(evs)  # overlap: env + update
@@ -737,7 +746,8 @@ def main():
     from pongmi.selfplay import SelfPlayLearner
 
     U = max(1, int(args.updates_per_step))
-    sdB, sdA, pool, wdesc = bench_nets(args.weights, args.pool)
+    nets = bench_nets(args.weights, args.pool)
+    sdB, sdA, pool, wdesc = nets
     L = SelfPlayLearner(ENV_KW, args.arenas, sdB, sdA, pool, batch=args.batch, memory_size=args.memory,
                         epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce,
                         overlap=not args.no_overlap, updates_per_step=U, learn_multi=not args.no_learn_multi)
@@ -761,7 +771,7 @@ def main():
         ae_t.append(_lib.timer_read(_lib.PM_TIMER_ACTENV))
         learn_t.append(_lib.timer_read(_lib.PM_TIMER_LEARN))
 
-    dt, _ = timed_region(one_step, args.steps, dist, 0, read_timers)
+    dt, _, c1 = timed_region(one_step, args.steps, dist, 0, read_timers, L.counters)
     same = replicas_identical(dist, L.paramsB)
     ae_s = sum(ae_t) / len(ae_t)  # the launches' own durations, as rocprofv3 --kernel-trace times them
     learn_s = sum(learn_t) / len(learn_t)
@@ -788,7 +798,7 @@ def main():
                                    "env tick + PER push/sample + double-DQN update + Adam + target sync)",
                        "arenas_per_gpu": args.arenas, "global_arenas": args.arenas * world,
                        "pool": args.pool, "batch": args.batch, "updates_per_vector_step": U,
-                       "updates_in_timed_region": c["train_steps"] - c0["train_steps"],
+                       "updates_in_timed_region": c1["train_steps"] - c0["train_steps"],
                        "memory_size": args.memory, "parallelism": f"dp{world} (arena shards, 1 all-reduce/update)",
                        "all_reduce": args.comm_used if world > 1 else None, "replicas_identical": same,
                        "shards": shards},
@@ -818,7 +828,7 @@ def main():
             out["act_full_roofline"] = time_act_full(L)
             out["env_step_roofline"] = time_env_step(args.arenas)
             if not args.no_cpu_baseline:
-                out["cpu_baseline"] = cpu_baseline(args.arenas, args.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(args.arenas, nets, args.cpu_seconds)
                 out["cpu_config0"] = args.cpu_config0
         if failed:
             out["error"] = "device status / shard proof failed: see learner.status and config.shards"

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 18
+#define PM_ABI_VERSION 19
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -266,7 +266,9 @@ typedef struct pm_drqn_stats {
     float loss;     /* smooth_l1 loss of the last update */
     float norm;     /* pre-clip total gradient norm of the last update (of the rank mean) */
     float q_mean;   /* mean q of the last batch */
-    int32_t status;
+    int32_t status; /* latched error bits: 2 = a hand-off inside pm_drqn_grads timed out on this replica;
+                     * 4 = pm_drqn_apply's norm arrival timed out (that block's slice not stepped);
+                     * 8 = an update was voided (a timeout on any rank: no Adam step, no target sync) */
 } pm_drqn_stats;
 
 typedef struct pm_drqn {
@@ -275,7 +277,9 @@ typedef struct pm_drqn {
     float *adam_m, *adam_v; /* [PM_RNN_NPARAM] */
     float *grad;            /* [PM_RNN_NPARAM + 4] gradients in packed parameter order, then at
                              * [PM_RNN_NPARAM] the number of ranks that contributed (1 per enabled
-                             * replica) — both summed by the all-reduce; apply divides by it */
+                             * replica) and at [PM_RNN_NPARAM + 1] the number of ranks whose update
+                             * timed out — all summed by the all-reduce; apply divides by the first
+                             * and does nothing when the second is non-zero */
     void *work;             /* pm_drqn_work_bytes(batch, T) bytes, 16-byte aligned */
     pm_drqn_stats *stats;
     const float *obs, *next; /* [batch][T][7] */
@@ -287,6 +291,9 @@ typedef struct pm_drqn {
     int32_t T;               /* 1 .. 64 */
     int64_t target_update_interval;
     double gamma, lr, beta1, beta2, adam_eps, max_norm;
+    int32_t poll_limit;     /* polls per in-launch hand-off before it times out: 0 = default (2^20);
+                             * < 0 = none (every hand-off times out: a test hook for the void path) */
+    int32_t reserved;
 } pm_drqn;
 
 int64_t pm_drqn_work_bytes(int32_t batch, int32_t T);

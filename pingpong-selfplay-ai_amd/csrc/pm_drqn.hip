@@ -70,7 +70,9 @@ struct DqArgs {
     double* part;
     int64_t* tstep;
     int32_t* flags;  // [0] update epoch (the granule tag base), [1] k_dq_wgrad's ticket, [2] k_drqn_apply's
+    int poll_limit;  // polls per hand-off wait (pm_drqn.poll_limit: 0 = 2^20; < 0 = none, a test hook)
 };
+__device__ __forceinline__ int hand_limit(int pl) { return pl == 0 ? (1 << 20) : (pl < 0 ? 0 : pl); }
 
 // workspace carve-up, 64-float aligned pieces
 struct DqLayout {
@@ -125,6 +127,11 @@ __device__ __forceinline__ bool skipped(const DqArgs& a) { return a.enable && *a
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
+struct HandoffCtl {
+    pm_drqn_stats* st;
+    float* vflag;  // grad + PM_RNN_NPARAM + 1
+    int limit;     // polls per hand-off before it counts as timed out
+};
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // 4-byte write-through store / L2-coherent load (sc1), for the column-tile partials handed to the
 // workgroups that sum them within the same launch (hand-off table row 1: sc1 on both sides)
@@ -139,10 +146,17 @@ __device__ __forceinline__ void st_g2(__amdgpu_buffer_rsrc_t r, int byte_off, fl
 // Poll the granule pairs at byte offsets off[i] (16-B aligned, from base) until every tag equals
 // `tag`; v[2i], v[2i+1] get the values. The polls are 8-byte agent-scope atomic loads (sc1): a
 // plain or volatile-flagged buffer load is loop-invariant to the compiler and gets hoisted out of
-// the poll. Wave-wide; bounded (status bit 1 and garbage values on a timeout: the update is void).
+// the poll. Wave-wide; bounded by hc.limit polls. On a timeout the values are garbage, so the update
+// is voided (void_update): status bit 1 latched, and grad[PM_RNN_NPARAM + 1] (the void count) set.
+// That slot rides the gradient all-reduce, so every rank's k_drqn_apply sees it and skips the Adam
+// step and the target sync of that update: the parameters stay untouched and the replicas identical.
+__device__ __forceinline__ void void_update(const HandoffCtl& hc) {
+    atomicOr(&hc.st->status, 2);
+    __hip_atomic_store(hc.vflag, 1.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <int N, bool SLEEP = false>
 __device__ __forceinline__ void gather(const void* base, const int (&off)[N], uint32_t tag, float (&v)[2 * N],
-                                       pm_drqn_stats* st) {
+                                       const HandoffCtl& hc) {
     const char* b = static_cast<const char*>(base);
     for (int it = 0;; ++it) {
         uint64_t q[2 * N];
@@ -159,8 +173,8 @@ __device__ __forceinline__ void gather(const void* base, const int (&off)[N], ui
             v[i] = __uint_as_float((uint32_t)q[i]);
         }
         if (__all(ok)) return;
-        if (it == (1 << 20)) {
-            if ((threadIdx.x & 63) == 0) atomicOr(&st->status, 2);
+        if (it >= hc.limit) {
+            if ((threadIdx.x & 63) == 0) void_update(hc);
             return;
         }
         // (a sleep here with N > 8 makes the compiler keep the callers' arrays live across the loop:
@@ -173,17 +187,17 @@ __device__ __forceinline__ void gather(const void* base, const int (&off)[N], ui
 // Lanes [0, n) of one wave poll one granule each (byte offset soff) until its tag equals `tag`: the
 // wait for n producers costs one 8-byte load per producer per poll instead of a whole slot sweep by
 // every wave (sweeping pollers congested the fabric: ~5 us per hop). Bounded like gather.
-__device__ __forceinline__ void poll_tags(const void* base, int soff, int n, uint32_t tag, pm_drqn_stats* st) {
+__device__ __forceinline__ void poll_tags(const void* base, int soff, int n, uint32_t tag, const HandoffCtl& hc) {
     const char* b = static_cast<const char*>(base);
     bool ok = (int)(threadIdx.x & 63) >= n;
-    for (int it = 0; it < (1 << 20); ++it) {
+    for (int it = 0; it < hc.limit; ++it) {
         if (!ok)
             ok = (uint32_t)(__hip_atomic_load(reinterpret_cast<const uint64_t*>(b + soff), __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
         if (__all(ok)) return;
         __builtin_amdgcn_s_sleep(1);
     }
-    if ((threadIdx.x & 63) == 0) atomicOr(&st->status, 2);
+    if ((threadIdx.x & 63) == 0) void_update(hc);
 }
 
 // ---------------------------------------------------------------- 1: embedding + input projection
@@ -208,7 +222,10 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
         for (int i = blockIdx.x * 256 + tid; i < PM_RNN_NPARAM + 4; i += gridDim.x * 256) a.grad[i] = 0.f;
         return;
     }
-    if (blockIdx.x == 0 && tid == 0) a.grad[PM_RNN_NPARAM] = 1.0f;
+    if (blockIdx.x == 0 && tid == 0) {
+        a.grad[PM_RNN_NPARAM] = 1.0f;      // this replica contributes
+        a.grad[PM_RNN_NPARAM + 1] = 0.0f;  // no hand-off has timed out (yet) in this update
+    }
     __shared__ __attribute__((aligned(16))) float F2s[32][132];
     DQ_STAMP(220, blockIdx.x == 0);
     const float* P = s == 2 ? a.target : a.params;
@@ -333,6 +350,7 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
     const int bcol = ct * 32 + col;
     const int grp = s * nct + ct;
     const uint32_t E = (uint32_t)a.flags[0] << 7;  // this update's tag base (T + 1 < 128)
+    const HandoffCtl hc{a.stats, a.grad + PM_RNN_NPARAM + 1, hand_limit(a.poll_limit)};
     [[maybe_unused]] const bool so0 = s == 0 && ct == 0 && m == 0, s10 = blockIdx.x == 0;  // stamping blocks (diag)
     DQ_STAMP(1, so0);
     DQ_STAMP(111, s10);
@@ -377,8 +395,8 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) off[i] = hoff[i] + t * 32 * 128 * 8;
             // lanes 0..3 wait for the last granule of this wave's 4 producers, then the K quarter is read once
-            poll_tags(HSg, ((t * 32 + 31) * 128 + 8 * (4 * w + (lane & 3)) + 7) * 8, 4, E + t, a.stats);
-            gather<8, false>(HSg, off, E + t, hv, a.stats);  // h_t of the group, this wave's K quarter
+            poll_tags(HSg, ((t * 32 + 31) * 128 + 8 * (4 * w + (lane & 3)) + 7) * 8, 4, E + t, hc);
+            gather<8, false>(HSg, off, E + t, hv, hc);  // h_t of the group, this wave's K quarter
             DQ_STAMP(160 + t, so0 && t < 10);
             f32x16 acc = {};
 #pragma unroll
@@ -442,8 +460,8 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
         int off[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) off[i] = hoff[i] + T * 32 * 128 * 8;
-        poll_tags(HSg, ((T * 32 + 31) * 128 + 8 * (4 * w + (lane & 3)) + 7) * 8, 4, E + T, a.stats);
-        gather<8, false>(HSg, off, E + T, hv, a.stats);  // h_T
+        poll_tags(HSg, ((T * 32 + 31) * 128 + 8 * (4 * w + (lane & 3)) + 7) * 8, 4, E + T, hc);
+        gather<8, false>(HSg, off, E + T, hv, hc);  // h_T
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             *reinterpret_cast<float4*>(&sm.hT[col][32 * w + 8 * j + 4 * h]) =
@@ -496,7 +514,7 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
                 off[2 * k + 1] = off[2 * k] + 16;
             }
             float pp[16];
-            gather<8, true>(QPs, off, E + 1, pp, a.stats);
+            gather<8, true>(QPs, off, E + 1, pp, hc);
 #pragma unroll
             for (int k = 0; k < 16; ++k) p[4 * k0 + k] = pp[k];
         }
@@ -655,8 +673,8 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
             }
             float p[16];
             poll_tags(DHc, (((t * 16 + 4 * w + (lane & 3)) * 32 + 31) * 128 + 32 * (m >> 2) + 31) * 8, 4, E + t + 1,
-                      a.stats);
-            gather<8, false>(DHc, off, E + t + 1, p, a.stats);
+                      hc);
+            gather<8, false>(DHc, off, E + t + 1, p, hc);
             float d4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -896,10 +914,11 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
             const int k = atomicAdd(a.flags + 1, 1);
             int slot = k - (nB - R);
             if (slot >= 0) {
-                for (int it = 0; it < (1 << 22); ++it) {
+                const HandoffCtl hc{a.stats, a.grad + PM_RNN_NPARAM + 1, 4 * hand_limit(a.poll_limit)};
+                for (int it = 0;; ++it) {
                     if (__hip_atomic_load(a.flags + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nB) break;
+                    if (it >= hc.limit) { void_update(hc); slot = -1; break; }
                     __builtin_amdgcn_s_sleep(2);
-                    if (it == (1 << 22) - 1) { atomicOr(&a.stats->status, 2); slot = -1; }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 drain();
@@ -986,8 +1005,13 @@ __global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* pa
     __shared__ double red[256];
     __shared__ float cf[3];
     __shared__ int64_t ts_s;
+    __shared__ int late;
     const float ranks = a.grad[PM_RNN_NPARAM];  // replicas that contributed (summed by the all-reduce)
     if (!(ranks > 0.f)) return;                 // grid-uniform
+    if (a.grad[PM_RNN_NPARAM + 1] != 0.f) {     // a hand-off timed out on some rank: the update is void
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&a.stats->status, 8);
+        return;                                 // grid-uniform: no Adam, no target sync, no step count
+    }
     const float inv_world = 1.0f / ranks;
     const int64_t ts = a.stats->steps + 1, at = a.stats->adam_t + 1;  // read before any block's arrival
     // one slice per block for both phases, every operand loaded up front (kEl elements per thread):
@@ -1022,14 +1046,20 @@ __global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* pa
         drain();
         const uint32_t tk = atomicAdd(reinterpret_cast<unsigned*>(a.flags + 2), 1u);
         const uint32_t goal = (tk / kNormBlocks + 1) * kNormBlocks;  // this update's generation complete
-        for (int it = 0; it < (1 << 22); ++it) {
+        late = 0;
+        for (int it = 0;; ++it) {
             if ((uint32_t)__hip_atomic_load(a.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - goal < 0x80000000u)
                 break;
+            if (it >= (1 << 22)) {  // the norm would be partial: this block leaves its slice untouched
+                atomicOr(&a.stats->status, 4);
+                late = 1;
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
-            if (it == (1 << 22) - 1) atomicOr(&a.stats->status, 4);
         }
     }
     __syncthreads();
+    if (late) return;  // block-uniform
     red[threadIdx.x] = __hip_atomic_load(a.part + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     for (int kk = 128; kk > 0; kk >>= 1) {  // the same fixed tree in every block
@@ -1117,6 +1147,7 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats; a.enable = d->enable;
     a.obs = d->obs; a.next = d->next; a.act = d->act; a.rew = d->rew; a.done = d->done;
     a.gamma = (float)d->gamma;
+    a.poll_limit = d->poll_limit;
     hipLaunchKernelGGL(k_dq_embed, dim3(3 * a.nct * a.T * 4), dim3(256), 0, st, a);
     PM_LAUNCHED("k_dq_embed");
     pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(3 * a.nct * kG), dim3(256), st, a);

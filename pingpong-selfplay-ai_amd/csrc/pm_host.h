@@ -41,6 +41,9 @@ template <typename F, typename... Args>
 inline void pm_launch(int timer, F kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
     hipEvent_t t0, t1;
     if (pm_timer_take(timer, &t0, &t1)) {
+        // the error state is sticky per thread: clear whatever an earlier, unrelated call left, so the
+        // peek below sees this launch's own result (the caller's PM_LAUNCHED still consumes it)
+        (void)hipGetLastError();
         hipExtLaunchKernelGGL(kernel, grid, block, 0, st, t0, t1, 0, args...);
         if (hipPeekAtLastError() != hipSuccess) pm_timer_release(timer);  // never enqueued: not pending
     } else {

@@ -13,12 +13,15 @@
 //   k_rollout_heads — one block per step folds modelB's heads with that step's noise (gen_noise +
 //     fold_heads_from, exactly pm_qnet_fold FRESH) into the F_H/F_BH fragment order: 264 floats per
 //     step in a caller workspace (PM_ROLL_HEADS);
-//   k_rollout — a block of 2 waves owns one tile of 32 arenas: wave 0 plays A, wave 1 plays B (two
-//     SIMDs, so the two 72-MFMA forwards of a step run side by side). Both waves keep the same fp64
-//     arena in both lane halves (the MFMA tile layout gives column lane & 31 to both), exchange the
-//     step's actions through LDS behind one barrier and tick identically. Wave B streams the next
-//     step's heads global -> LDS (global_load_lds, 1 KB, double-buffered) while it computes the
-//     current step, so the heads never cost a round trip on the step's critical path.
+//   k_rollout — a block of 4 waves (kRollBlock = 256) owns one tile of 32 arenas. Wave 2p + j works
+//     for player p (0 = A, 1 = B) and computes layer-2 tile j of that player's forward (layer 1 in
+//     both), so a forward is 40 dependent MFMAs on two SIMDs instead of 72 on one. The j = 0 wave runs
+//     the head chains over its rows and hands the partial sums to the j = 1 wave through LDS (part[]),
+//     which continues them in tile_heads' fmaf order and forms the action. Every wave keeps the same
+//     fp64 arena in both lane halves (the MFMA tile layout gives column lane & 31 to both), the
+//     actions meet in LDS behind the step's barriers and all four waves tick identically. Wave 3
+//     streams the next step's heads global -> LDS (global_load_lds, 1 KB, double-buffered) while it
+//     computes the current step, so the heads never cost a round trip on the step's critical path.
 //
 // Bit-identical to `steps` repetitions of pm_qnet_fold(paramsB, FRESH, seed_net, c) ->
 // pm_qnet_act({wA}, NULL, w_B, obsA, obsB, epsilon, seed_env, c) -> pm_env_step(autoreset, seed_env,

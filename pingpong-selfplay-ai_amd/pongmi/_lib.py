@@ -35,7 +35,7 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 18
+ABI_VERSION = 19
 PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_ROLLOUT, PM_TIMER_DRQN, PM_TIMER_N = \
     0, 1, 2, 3, 4, 5, 6
 PM_ROLL_HEADS = 264
@@ -88,7 +88,8 @@ class Drqn(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("params", "target", "adam_m", "adam_v", "grad", "work", "stats", "obs", "next",
                                         "act", "rew", "done", "enable")] + \
         [("batch", c_i32), ("T", c_i32), ("target_update_interval", c_i64)] + \
-        [(n, c_double) for n in ("gamma", "lr", "beta1", "beta2", "adam_eps", "max_norm")]
+        [(n, c_double) for n in ("gamma", "lr", "beta1", "beta2", "adam_eps", "max_norm")] + \
+        [("poll_limit", c_i32), ("reserved", c_i32)]
 
 
 class RnnCtrl(ctypes.Structure):

@@ -26,7 +26,7 @@ PARAM_SHAPES = [s for k, s in PARAM_LAYOUT if k in PARAM_KEYS]  # modelB.paramet
 
 class DRQNLearner:
     def __init__(self, modelB, target=None, *, batch=64, T=8, gamma=0.99, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
-                 max_norm=1.0, target_update_interval=2000, enable=None, device="cuda"):
+                 max_norm=1.0, target_update_interval=2000, enable=None, device="cuda", poll_limit=0):
         """modelB / target: a QNetRNN module, its state_dict, or a packed [PM_RNN_NP] tensor;
         target None = a copy of modelB (targetB.load_state_dict(modelB.state_dict()), :336-338)."""
         self.lib = _lib.load()
@@ -40,7 +40,9 @@ class DRQNLearner:
         nbytes = self.lib.pm_drqn_work_bytes(self.batch, self.T)
         if nbytes < 0:
             raise ValueError("invalid batch / T")
-        self.work = torch.empty((nbytes + 15) // 16 * 4, dtype=torch.float32, device=self.device)
+        # zeroed once: the hand-off slots' tags and the tag epoch (flags[0]) must not start as whatever
+        # the allocator hands back (a stale granule whose tag matched would be read before its producer)
+        self.work = torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=self.device)
         self.stats_buf = torch.zeros(ctypes.sizeof(_lib.DrqnStats), dtype=torch.uint8, device=self.device)
         self.obs = torch.zeros((self.batch, self.T, 7), dtype=torch.float32, device=self.device)
         self.next = torch.zeros_like(self.obs)
@@ -57,6 +59,7 @@ class DRQNLearner:
         d.target_update_interval = int(target_update_interval)
         d.gamma, d.lr, d.beta1, d.beta2, d.adam_eps, d.max_norm = float(gamma), float(lr), float(betas[0]), \
             float(betas[1]), float(eps), float(max_norm)
+        d.poll_limit = int(poll_limit)  # 0: the library default; < 0 is the tests' forced-timeout hook
         self.desc = d
 
     def _block(self, m):
@@ -93,10 +96,20 @@ class DRQNLearner:
         self._call(self.lib.pm_drqn_apply, stream)
 
     def stats(self):
-        """(steps, loss, pre-clip grad norm, mean q, status) of the last update (host sync). status bit 1:
-        a hand-off inside the persistent recurrence timed out (that update is void)."""
+        """(steps, loss, pre-clip grad norm, mean q, status) of the last update (host sync). status
+        (latched) 2: a hand-off inside pm_drqn_grads timed out on this replica; 4: the apply's norm
+        arrival timed out; 8: an update was voided (a timeout on any rank: parameters, Adam state, step
+        count and target left as they were)."""
         s = _lib.DrqnStats.from_buffer_copy(bytes(self.stats_buf.cpu().numpy()))
         return dict(steps=s.steps, adam_t=s.adam_t, loss=s.loss, norm=s.norm, q_mean=s.q_mean, status=s.status)
+
+    def check_status(self):
+        """Raise when any update was voided or partly applied (status bits above; host sync)."""
+        st = self.stats()["status"]
+        if st & 14:
+            raise _lib.PongmiError(f"DRQN update: device status {st} (2: hand-off timed out, 4: apply arrival "
+                                   f"timed out, 8: update voided)")
+        return st
 
     def state_dict(self):
         """modelB's state_dict (reference key names)."""

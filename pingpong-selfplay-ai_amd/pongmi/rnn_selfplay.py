@@ -270,11 +270,14 @@ class RNNSelfPlayLearner:
     def check_status(self, c=None, log=print):
         """Device error bits (pm_rnn_ctrl.status): bit 0 (a sample read an overwritten ring step) means
         corrupted training data and raises; bits 1 / 2 (episodes evicted by age / a trajectory longer
-        than depth / 2 dropped: `depth` is too small for the episode lengths seen) warn once each."""
+        than depth / 2 dropped: `depth` is too small for the episode lengths seen) warn once each. The
+        DRQN learner's pm_drqn_stats.status is checked too: a timed-out hand-off (a voided update)
+        raises."""
         st = int((c or self.counters())["status"])
         if st & 1:
             raise _lib.PongmiError(f"RNN sequence buffer: a sampled step had been overwritten (status {st}); "
                                    f"depth {self.depth} is too small")
+        self.learner.check_status()  # the DRQN update's own word (pm_drqn_stats.status): a void update raises
         new = st & 6 & ~self._warned
         if new & 2:
             log(f"[WARNING] sequence buffer: episodes older than depth/2 = {self.depth // 2} steps were evicted "

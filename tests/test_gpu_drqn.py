@@ -133,3 +133,71 @@ def test_drqn_disabled_replica_contributes_nothing(golden):
     L.update()
     assert L.grad[-4].item() == 1.0 and L.stats()["steps"] == 1 and not torch.equal(L.params, p0)
     np.testing.assert_allclose(L.stats()["loss"], gd["u0_loss"], rtol=1e-4)
+
+
+def _adam_f32(p, m, v, g, norm, at, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8, max_norm=1.0):
+    """torch's clip_grad_norm_ + Adam step restated in float32 in the kernel's operation order (the
+    clip coefficient from the device's own pre-clip norm, which is an fp64 sum in a fixed tree)."""
+    f = np.float32
+    coef = f(max_norm / (np.float64(f(norm)) + 1e-6))
+    coef = min(coef, f(1.0))
+    bc1, bc2 = 1.0 - b1 ** at, 1.0 - b2 ** at
+    step_size, bc2s = f(lr / bc1), f(np.sqrt(bc2))
+    gc = g.astype(f) * coef
+    m = m + f(1.0 - b1) * (gc - m)
+    v = v * f(b2) + f(1.0 - b2) * gc * gc
+    denom = np.sqrt(v) / bc2s + f(eps)
+    return p - step_size * (m / denom), m, v
+
+
+def test_drqn_clip_adam_exact(golden):
+    """The clip + Adam half of train_step_rnn is exact: given the update's own gradient (read back
+    after apply, sigma slots formed) and its pre-clip norm, every parameter and both Adam moments
+    equal a float32 restatement bit for bit, over three updates; the norm equals the fp64 norm of
+    that gradient. With the gradients checked against autograd / the oracle above, this pins the
+    parameters without the Adam sign-of-rounding escape (_assert_params)."""
+    from pongmi._lib import PM_RNN_NPARAM
+    from pongmi.drqn import DRQNLearner
+    gr, gd = golden("rnn"), golden("drqn")
+    L = DRQNLearner(_sd(gr), batch=64, T=8)
+    for k in range(3):
+        p0 = L.params.cpu().numpy()[:PM_RNN_NPARAM].copy()
+        m0, v0 = L.adam_m.cpu().numpy().copy(), L.adam_v.cpu().numpy().copy()
+        L.update(*(torch.from_numpy(x) for x in _batch(gd, k)))
+        st = L.stats()
+        g = L.grad.cpu().numpy()[:PM_RNN_NPARAM]
+        np.testing.assert_allclose(st["norm"], np.sqrt(np.sum(g.astype(np.float64) ** 2)), rtol=1e-6)
+        p, m, v = _adam_f32(p0, m0, v0, g, st["norm"], k + 1)
+        np.testing.assert_array_equal(L.adam_m.cpu().numpy(), m, err_msg=f"exp_avg, update {k}")
+        np.testing.assert_array_equal(L.adam_v.cpu().numpy(), v, err_msg=f"exp_avg_sq, update {k}")
+        np.testing.assert_array_equal(L.params.cpu().numpy()[:PM_RNN_NPARAM], p, err_msg=f"params, update {k}")
+
+
+def test_drqn_timeout_voids_update(golden):
+    """A hand-off timeout inside pm_drqn_grads voids the update: forced with the poll_limit test hook
+    (< 0: every in-launch wait times out at once), the update leaves parameters, target, Adam moments
+    and the step counters untouched, latches status bits 2 (timed out) and 8 (voided), and
+    check_status raises (RNNSelfPlayLearner.check_status calls it). Restoring the limit, the
+    next update runs normally and equals a fresh learner's first update bit for bit."""
+    from pongmi import _lib
+    from pongmi.drqn import DRQNLearner
+    gr, gd = golden("rnn"), golden("drqn")
+    b = tuple(torch.from_numpy(x) for x in _batch(gd, 0))
+    L = DRQNLearner(_sd(gr), batch=64, T=8, poll_limit=-1, target_update_interval=1)
+    p0, t0 = L.params.clone(), L.target.clone()
+    L.update(*b)
+    st = L.stats()
+    assert st["status"] & 2 and st["status"] & 8, st
+    assert st["steps"] == 0 and st["adam_t"] == 0
+    assert torch.equal(L.params, p0) and torch.equal(L.target, t0)  # interval 1: a sync would have copied
+    assert torch.count_nonzero(L.adam_m) == 0 and torch.count_nonzero(L.adam_v) == 0
+    assert L.grad[-3].item() > 0  # the void count that rides the all-reduce
+    with pytest.raises(_lib.PongmiError):
+        L.check_status()
+    L.desc.poll_limit = 0
+    L._set_stats(status=0)
+    L.update(*b)
+    assert L.stats()["status"] == 0 and L.stats()["steps"] == 1 and L.grad[-3].item() == 0
+    R = DRQNLearner(_sd(gr), batch=64, T=8, target_update_interval=1)
+    R.update(*b)
+    assert torch.equal(L.params, R.params) and torch.equal(L.adam_v, R.adam_v) and torch.equal(L.target, R.target)

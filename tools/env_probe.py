@@ -47,7 +47,8 @@ def probe(n, reps):
             check(lib.pm_env_step(ctypes_ref(env.params), ctypes_ref(env.state), ptr(aA), ptr(aB), ptr(env.obsA),
                                   ptr(env.obsB), ptr(env.rA), ptr(env.rB), ptr(env.done),
                                   ptr(env.term_obsA) if term else None, ptr(env.term_obsB) if term else None,
-                                  int(autoreset), None, 0, env.seed, None, n, stream_ptr()), "pm_env_step")
+                                  int(autoreset), None, 0, env.seed, env.counter, None, n, stream_ptr()),
+                  "pm_env_step")
         return f
 
     out = {"n": n}

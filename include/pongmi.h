@@ -367,6 +367,8 @@ typedef struct pm_rnn_selfplay {
     const float *hA_in, *cA_in; /* nullable [n][128]: where the opponents' act reads (h, c) from (it writes
                                    hA / cA); null = in place. The overlapped step (ABI 10) alternates two
                                    buffers so a speculative act of the next step can be redone */
+    float *qA, *qB;        /* nullable [n][3]: the Q values each player's act chose from (ABI 19; parity
+                              tests read them beside the actions of the same launch) */
 } pm_rnn_selfplay;
 
 /* Ring safety: a stored trajectory is at most depth / 2 steps long (longer ones are dropped, status bit

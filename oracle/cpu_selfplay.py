@@ -172,3 +172,79 @@ class CpuRollout:
             self.ep_reward[done > 0] = 0.0
         self._serve(done > 0)
         return n
+
+
+class PhiloxRollout:
+    """TEST ORACLE for K9 (pm_rollout) and the collecting rollout (pm_rollout_push): the
+    rollout of scripts/train_iterative.py:239-245 with the learner off, restated on the device's own
+    random streams and float32 order so a launch can be compared with it bit for bit, independently of
+    every other device path. Per vector step with counter c:
+      - modelB.reset_noise() (select_action_B, :125): the Philox noise of (seed_net, TAG_NOISE_ACT, c)
+        (oracle.philox_noise, bit-exact with the device's normal()), folded mu + sigma * eps in torch's
+        float32 order (fold_heads_f32);
+      - both forwards in the matrix-core tile's fmaf order (qnet_forward_f32); modelA greedy on its own
+        frozen epsilon buffers (:240), modelB eps-greedy with the Philox draw of (arena, TAG_ACT, c)
+        (:126-130);
+      - env.step on the C oracle (envs/my_pong_env_2p.py:116-225), finished arenas served again from
+        the step-keyed Philox serve (oracle.philox_serve(step=c));
+      - with a replay ring: memory.push((oB, aB, rB, nB, done)) (:242-243, PrioritizedReplay.push
+        :56-63) into slot (pos + s n + i) % cap with the given push priority; ep_reward += rB, and the
+        episode wins ep_reward > 0 (:245-249).
+    The start state is the device env's (get_state()), so the launch's input is shared and nothing
+    else is."""
+
+    def __init__(self, env_kw, state, sdA, sdB, epsilon, seed_env, seed_net, counter, replay=None):
+        self.pv = orc.env_params_from_kwargs(**env_kw)
+        self.P = orc.make_params(self.pv)
+        self.arr = np.zeros(len(state["x"]), orc.ARENA_DTYPE)
+        for k in ("x", "y", "vx", "vy", "spin", "top", "bot", "scoreA", "scoreB", "bounces"):
+            self.arr[k] = state[k]
+        self.n = len(self.arr)
+        f = lambda sd: {k: np.asarray(v, np.float32) for k, v in sd.items()}  # noqa: E731
+        self.sdB = f(sdB)
+        self.wA = orc.fold_heads_f32(f(sdA), "train")
+        self.eps, self.seed_env, self.seed_net, self.counter = float(epsilon), int(seed_env), int(seed_net), int(counter)
+        self.replay = replay  # dict(trans [cap,16] f32, prios [cap] f32, pos, cap, prio) or None
+        self.ep_reward = np.zeros(self.n, np.float32)
+        self.stats = np.zeros(6, np.int64)  # episodes, done & rB > 0, points A, points B, episode wins, reward sum
+
+    def heads_B(self, c):
+        fVi, fVo, fAi, fAo = orc.philox_noise(self.seed_net, orc.TAG_NOISE_ACT, c)
+        eps = {"fc_V.weight_epsilon": np.outer(fVo, fVi).astype(np.float32), "fc_V.bias_epsilon": fVo,
+               "fc_A.weight_epsilon": np.outer(fAo, fAi).astype(np.float32), "fc_A.bias_epsilon": fAo}
+        return orc.fold_heads_f32({**self.sdB, **eps}, "train")
+
+    def step(self, s=0):
+        n, c = self.n, self.counter
+        arenas = np.arange(n)
+        oA, oB = orc.obs_of_arenas(self.arr)
+        aA = orc.argmax_first(orc.qnet_forward_f32(self.wA, oA))
+        aB, _ = orc.eps_greedy(orc.qnet_forward_f32(self.heads_B(c), oB), self.eps, self.seed_env, c, arenas)
+        _, nB, rew, done = orc.step_arenas(self.P, self.arr, aA.astype(np.int8), aB.astype(np.int8))
+        d = done.astype(bool)
+        rA, rB = rew[:, 0], rew[:, 1]
+        if self.replay is not None:
+            R = self.replay
+            slot = (R["pos"] + s * n + arenas) % R["cap"]
+            R["trans"][slot, 0:7] = oB
+            R["trans"][slot, 7] = rB
+            R["trans"][slot, 8:15] = nB
+            R["trans"][slot, 15] = (aB.astype(np.int32) | (d.astype(np.int32) << 8)).view(np.float32)
+            R["prios"][slot] = R["prio"]
+        self.ep_reward += rB
+        self.stats += np.array([d.sum(), (d & (rB > 0)).sum(), (rA > 0).sum(), (rB > 0).sum(),
+                                (d & (self.ep_reward > 0)).sum(), int(self.ep_reward[d].sum())])
+        self.ep_reward[d] = 0.0
+        if d.any():
+            i = np.nonzero(d)[0]
+            vx, vy, spin = orc.philox_serve(self.pv, i, None, self.seed_env, step=c)
+            orc.serve_arenas(self.arr, d, vx, vy, spin)
+        self.counter += 1
+        return aA, aB
+
+    def run(self, steps):
+        for s in range(steps):
+            self.step(s)
+        if self.replay is not None:
+            self.replay["pos"] = (self.replay["pos"] + steps * self.n) % self.replay["cap"]
+        return self.stats

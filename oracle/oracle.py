@@ -211,9 +211,11 @@ def rollout_random(params, seed, steps):
 
 # ----------------------------------------------------------------------------- QNet (numpy)
 def scale_noise(raw):
-    """models/qnet.py:35-36: x.sign() * sqrt(|x|)."""
+    """models/qnet.py:35-36: x.sign() * sqrt(|x|) (the root correctly rounded, as the device's
+    pm_dev.h scale_noise: float(sqrt(double(|x|))))."""
     raw = np.asarray(raw, np.float32)
-    return (np.sign(raw) * np.sqrt(np.abs(raw))).astype(np.float32)
+    sgn = np.where(raw > 0, np.float32(1), np.where(raw < 0, np.float32(-1), np.float32(0))).astype(np.float32)
+    return (sgn * np.sqrt(np.abs(raw).astype(np.float64)).astype(np.float32)).astype(np.float32)
 
 
 def noise_from_raw(raw_in, raw_out):
@@ -740,12 +742,84 @@ def below(r, n):
     return ((np.asarray(r, np.uint64) * np.uint64(n)) >> np.uint64(32)).astype(np.int64)
 
 
+# pm_dev.h normal(): Box-Muller's cos branch in double with +, -, *, /, sqrt only, in the device's
+# exact evaluation order (numpy float64 elementwise operations are the same correctly rounded IEEE
+# operations and never fuse), rounded once to float: bit-identical to every device draw.
+_LN_C = (0.66666666666666663, 0.40000000000000002, 0.28571428571428570, 0.22222222222222221, 0.18181818181818182,
+         0.15384615384615385)
+_COS_C = (-0.5, 0.041666666666666664, -0.0013888888888888889, 2.4801587301587302e-05, -2.755731922398589e-07,
+          2.0876756987868100e-09, -1.1470745597729725e-11)
+_SIN_C = (-0.16666666666666666, 0.0083333333333333332, -0.00019841269841269841, 2.7557319223985893e-06,
+          -2.5052108385441720e-08, 1.6059043836821613e-10, -7.6471637318198164e-13)
+
+
+def _horner(z, coefs):
+    """c0 + z * (c1 + z * (... + z * c_last)), evaluated innermost first."""
+    acc = np.full(np.shape(z), coefs[-1], np.float64)
+    for c in coefs[-2::-1]:
+        acc = c + z * acc
+    return acc
+
+
+def det_ln_u1(k):
+    """pm_dev.h det_ln_u1: ln(k 2^-24) for integer k in [1, 2^24]."""
+    mant, ex = np.frexp(np.asarray(k, np.float64))  # k = mant 2^ex, mant in [0.5, 1): m = 2 mant in [1, 2)
+    m, e = mant * 2.0, ex.astype(np.int64) - 1
+    big = m > 1.4142135623730951
+    m, e = np.where(big, m * 0.5, m), np.where(big, e + 1, e)
+    s = (m - 1.0) / (m + 1.0)
+    s2 = s * s
+    p = s2 * _horner(s2, _LN_C)
+    return (e - 24).astype(np.float64) * 0.69314718055994531 + (2.0 * s + s * p)
+
+
+def det_cos_turn(t):
+    """pm_dev.h det_cos_turn: cos(2 pi t) for t on the 24-bit grid of [0, 1)."""
+    t = np.asarray(t, np.float64)
+    q = np.floor(4.0 * t + 0.5)
+    th = 6.2831853071795862 * (t - 0.25 * q)
+    z = th * th
+    c = 1.0 + z * _horner(z, _COS_C)
+    sn = th * (1.0 + z * _horner(z, _SIN_C))
+    qi = q.astype(np.int64) & 3
+    return np.where(qi == 0, c, np.where(qi == 1, -sn, np.where(qi == 2, -c, sn)))
+
+
 def normal_f32(a, b):
-    """Box-Muller cos branch in float32, as the device's normal()."""
-    u1 = ((np.asarray(a, np.uint32) >> 8).astype(np.float32) + np.float32(1.0)) * np.float32(2.0 ** -24)
-    u2 = (np.asarray(b, np.uint32) >> 8).astype(np.float32) * np.float32(2.0 ** -24)
-    r = np.sqrt(np.float32(-2.0) * np.log(u1))
-    return (r * np.cos(np.float32(6.28318530717958647692) * u2)).astype(np.float32)
+    """The device's N(0, 1) draw (pm_dev.h normal) from two u32 arrays, bit for bit."""
+    k = (np.asarray(a, np.uint32) >> 8).astype(np.int64) + 1
+    r = np.sqrt(-2.0 * det_ln_u1(k))
+    u2 = (np.asarray(b, np.uint32) >> 8).astype(np.float64) * 2.0 ** -24
+    return (r * det_cos_turn(u2)).astype(np.float32)
+
+
+def sincos_serve(x):
+    """pm_dev.h sincos_serve restated (numpy float64, same operation order): sin and cos of x for
+    |x| < 3 pi / 4 by one Cody-Waite step and fdlibm's __kernel_sin / __kernel_cos, bit for bit."""
+    x = np.asarray(x, np.float64)
+    pio4, pio2_1, pio2_1t = 7.85398163397448278999e-01, 1.57079632673412561417e+00, 6.07710050650619224932e-11
+    n = np.where(x > pio4, 1, np.where(x < -pio4, -1, 0))
+    z0 = np.where(n > 0, x - pio2_1, x + pio2_1)
+    t = np.where(n > 0, pio2_1t, -pio2_1t)
+    y0 = z0 - t
+    y1 = (z0 - y0) - t
+    y0 = np.where(n == 0, x, y0)
+    y1 = np.where(n == 0, 0.0, y1)
+    S1, S2, S3 = -1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04
+    S4, S5, S6 = 2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10
+    z = y0 * y0
+    v = z * y0
+    rs = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)))
+    ks = y0 - ((z * (0.5 * y1 - v * rs) - y1) - v * S1)
+    C1, C2, C3 = 4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05
+    C4, C5, C6 = -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11
+    rc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))))
+    hz = 0.5 * z
+    w = 1.0 - hz
+    kc = w + (((1.0 - w) - hz) + (z * rc - y0 * y1))
+    s = np.where(n == 0, ks, np.where(n > 0, kc, -kc))
+    c = np.where(n == 0, kc, np.where(n > 0, -ks, ks))
+    return s, c
 
 
 def philox_serve(params_dict, i, nserve, seed, step=None):
@@ -766,7 +840,10 @@ def philox_serve(params_dict, i, nserve, seed, step=None):
     ang = np.where(coin, p["ang0_lo"] + (p["ang0_hi"] - p["ang0_lo"]) * u, p["ang1_lo"] + (p["ang1_hi"] - p["ang1_lo"]) * u)
     rad = ang * (3.141592653589793 / 180.0)
     spin = p["spin_lo"] + (p["spin_hi"] - p["spin_lo"]) * u53(r1[2], r1[3])
-    return speed * np.cos(rad), speed * np.sin(rad), spin
+    sn, cs = sincos_serve(rad)
+    far = ~(np.abs(rad) < 2.35619449019234483700)  # the device redoes these with OCML's sincos (< 1 ulp)
+    sn, cs = np.where(far, np.sin(rad), sn), np.where(far, np.cos(rad), cs)
+    return speed * cs, speed * sn, spin
 
 
 def philox_noise(seed, tag, ctr):
@@ -779,3 +856,39 @@ def philox_noise(seed, tag, ctr):
             r = philox64(e, tag | (layer << 8) | (which << 12), np.full(n, ctr, np.uint64), seed)
             out.append(scale_noise(normal_f32(r[0], r[1])))
     return out
+
+
+TAG_NOISE_RNN = 7
+
+
+def rnn_philox_noise(seed, ctr):
+    """QNetRNN's reset_noise (models/qnet_rnn.py:33-41, the three NoisyLinear layers fc_shared_head.0,
+    fc_V, fc_A) as the device draws it (pm_rnn.hip rnn_noise: Philox(e, TAG_NOISE_RNN | layer << 8 |
+    which << 12, ctr), Box-Muller, _scale_noise), returned as the epsilon buffers reset_noise leaves:
+    {key.weight_epsilon: eps_out.ger(eps_in), key.bias_epsilon: eps_out}."""
+    out = {}
+    for layer, (key, n_in, n_out) in enumerate((("fc_shared_head.0", 128, 128), ("fc_V", 128, 1), ("fc_A", 128, 3))):
+        f = []
+        for which, n in ((0, n_in), (1, n_out)):
+            e = np.arange(n)
+            r = philox64(e, TAG_NOISE_RNN | (layer << 8) | (which << 12), np.full(n, ctr, np.uint64), seed)
+            f.append(scale_noise(normal_f32(r[0], r[1])))
+        out[f"{key}.weight_epsilon"] = np.outer(f[1], f[0]).astype(np.float32)
+        out[f"{key}.bias_epsilon"] = f[1]
+    return out
+
+
+def rnn_act_decision(q, eps, seed, ctr, arenas):
+    """select_action_for_model's choice (scripts/train_rnn_iterative.py:371-389) — and
+    select_action_B's (scripts/train_iterative.py:124-130), the same rule — with the device's Philox
+    streams: random.random() < eps ? randint(0, 2) : argmax Q (first max). Returns (action, explore
+    mask); eps <= 0 never explores (the opponents' greedy act)."""
+    greedy = argmax_first(q)
+    if eps <= 0.0:
+        return greedy, np.zeros(len(greedy), bool)
+    r = philox64(arenas, TAG_ACT, np.full(len(arenas), ctr, np.uint64), seed)
+    explore = u53(r[0], r[1]) < eps
+    return np.where(explore, below(r[2], 3), greedy), explore
+
+
+eps_greedy = rnn_act_decision

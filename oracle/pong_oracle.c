@@ -19,7 +19,10 @@
  * All arithmetic is IEEE binary64 in exactly the reference's evaluation order (Python evaluates
  * `a*b*c` as `(a*b)*c`); build with -ffp-contract=off so no FMA is formed.
  */
+#define _GNU_SOURCE
 #include <math.h>
+#include <pthread.h>
+#include <unistd.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -320,8 +323,8 @@ static float relu_f32(float x) {
     return x;
 }
 
-void or_qnet_f32(const float* w, const float* obs, int32_t n, float* q, float* feat) {
-    for (int32_t i = 0; i < n; i++) {
+static void qnet_rows(const float* w, const float* obs, int32_t i0, int32_t i1, float* q, float* feat) {
+    for (int32_t i = i0; i < i1; i++) {
         const float* x = obs + 7 * (int64_t)i;
         float h1[64], h2[64], hs[4];
         for (int j = 0; j < 64; j++) {
@@ -357,6 +360,42 @@ void or_qnet_f32(const float* w, const float* obs, int32_t n, float* q, float* f
         const float mean = ((hs[1] + hs[2]) + hs[3]) / 3.0f;
         for (int c = 0; c < 3; c++) q[3 * (int64_t)i + c] = hs[0] + (hs[1 + c] - mean);
     }
+}
+
+typedef struct {
+    const float *w, *obs;
+    int32_t i0, i1;
+    float *q, *feat;
+} qnet_job;
+
+static void* qnet_job_run(void* p) {
+    const qnet_job* j = (const qnet_job*)p;
+    qnet_rows(j->w, j->obs, j->i0, j->i1, j->q, j->feat);
+    return NULL;
+}
+
+/* Rows are independent: large batches are split over up to 16 threads (each row's arithmetic, and so
+ * every output bit, is the same whichever thread computes it). */
+void or_qnet_f32(const float* w, const float* obs, int32_t n, float* q, float* feat) {
+    long nt = sysconf(_SC_NPROCESSORS_ONLN);
+    if (nt > 16) nt = 16;
+    if (n < 4096 || nt < 2) {
+        qnet_rows(w, obs, 0, n, q, feat);
+        return;
+    }
+    pthread_t th[16];
+    qnet_job jobs[16];
+    const int32_t per = (int32_t)((n + nt - 1) / nt);
+    int started = 0;
+    for (long t = 0; t < nt; t++) {
+        const int32_t i0 = (int32_t)(t * per), i1 = i0 + per < n ? i0 + per : n;
+        jobs[t] = (qnet_job){w, obs, i0, i1 > i0 ? i1 : i0, q, feat};
+        if (t > 0 && pthread_create(&th[t], NULL, qnet_job_run, &jobs[t]) == 0) started |= 1 << t;
+        else if (t > 0) qnet_job_run(&jobs[t]);
+    }
+    qnet_job_run(&jobs[0]);
+    for (long t = 1; t < nt; t++)
+        if (started & (1 << t)) pthread_join(th[t], NULL);
 }
 
 /* torch argmax over [n][3] (first maximal index), as an int8 action row. */

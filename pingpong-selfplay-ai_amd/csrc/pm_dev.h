@@ -100,18 +100,43 @@ __device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
 __device__ __forceinline__ int32_t below(uint32_t r, uint32_t n) {
     return (int32_t)(((uint64_t)r * n) >> 32);
 }
-// one N(0,1) float by Box-Muller from two u32 (torch.randn stand-in, distribution parity)
-__device__ __forceinline__ float normal(uint32_t a, uint32_t b, bool second) {
-    const float u1 = ((float)(a >> 8) + 1.0f) * 0x1.0p-24f;  // (0, 1]
-    const float u2 = (float)(b >> 8) * 0x1.0p-24f;           // [0, 1)
-    const float r = sqrtf(-2.0f * logf(u1));
-    const float th = 6.28318530717958647692f * u2;
-    return second ? r * sinf(th) : r * cosf(th);
+// One N(0,1) float by Box-Muller (cos branch) from two u32: the torch.randn stand-in (distribution
+// parity with the reference). Evaluated in double with +, -, *, /, sqrt only — a fixed polynomial
+// log (atanh series on m in [sqrt(1/2), sqrt(2))) and cos (Taylor on the octant-reduced angle) —
+// then rounded once to float. Every step is a correctly rounded IEEE operation (this file builds with
+// -ffp-contract=off), so the oracle's numpy restatement (oracle.normal_f32) reproduces every draw bit
+// for bit: the noise, and with it every NoisyNet forward, is pinned exactly, not to an ulp band.
+// Accuracy: |log error| < 1e-15, |cos error| < 1e-15, far below the float the result is rounded to.
+__device__ __forceinline__ double det_ln_u1(uint32_t k) {  // ln(k * 2^-24), k in [1, 2^24]
+    int e = 31 - __builtin_clz(k);                        // k = m 2^e, m in [1, 2)
+    double m = (double)k / (double)(1u << e);             // exact
+    if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;  // ln m = 2 atanh(s)
+    const double p = s2 * (0.66666666666666663 + s2 * (0.40000000000000002 + s2 * (0.28571428571428570 +
+                     s2 * (0.22222222222222221 + s2 * (0.18181818181818182 + s2 * 0.15384615384615385)))));
+    return (double)(e - 24) * 0.69314718055994531 + (2.0 * s + s * p);
 }
-// NoisyLinear._scale_noise (models/qnet.py:35-36): sign(x) * sqrt(|x|)
+__device__ __forceinline__ double det_cos_turn(double t) {  // cos(2 pi t), t in [0, 1) (24-bit grid)
+    const double q = floor(4.0 * t + 0.5);                 // octant-centred quadrant 0..4
+    const double th = 6.2831853071795862 * (t - 0.25 * q);  // [-pi/4, pi/4]
+    const double z = th * th;
+    const double c = 1.0 + z * (-0.5 + z * (0.041666666666666664 + z * (-0.0013888888888888889 +
+                     z * (2.4801587301587302e-05 + z * (-2.755731922398589e-07 + z * (2.0876756987868100e-09 +
+                     z * -1.1470745597729725e-11))))));
+    const double s = th * (1.0 + z * (-0.16666666666666666 + z * (0.0083333333333333332 + z * (-0.00019841269841269841 +
+                     z * (2.7557319223985893e-06 + z * (-2.5052108385441720e-08 + z * (1.6059043836821613e-10 +
+                     z * -7.6471637318198164e-13)))))));
+    const int qi = (int)q & 3;
+    return qi == 0 ? c : (qi == 1 ? -s : (qi == 2 ? -c : s));
+}
+__device__ __forceinline__ float normal(uint32_t a, uint32_t b) {
+    const double r = sqrt(-2.0 * det_ln_u1((a >> 8) + 1u));  // u1 = ((a >> 8) + 1) 2^-24 in (0, 1]
+    return (float)(r * det_cos_turn((double)(b >> 8) * 0x1.0p-24));  // u2 in [0, 1)
+}
+// NoisyLinear._scale_noise (models/qnet.py:35-36): sign(x) * sqrt(|x|), the root correctly rounded
 __device__ __forceinline__ float scale_noise(float x) {
     const float s = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
-    return s * sqrtf(fabsf(x));
+    return s * (float)sqrt((double)fabsf(x));
 }
 
 // ----------------------------------------------------------------------------- environment
@@ -407,7 +432,7 @@ __device__ __forceinline__ void gen_noise(uint64_t seed, uint32_t tag, uint64_t 
         const uint32_t which = kk < 64 ? 0u : 1u;
         const uint32_t e = which ? kk - 64 : kk;
         const U4 r = philox64(e, tag | (layer << 8) | (which << 12), ctr, seed);
-        noise[k] = scale_noise(normal(r.x, r.y, false));
+        noise[k] = scale_noise(normal(r.x, r.y));
     }
 }
 

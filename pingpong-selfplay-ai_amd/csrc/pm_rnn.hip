@@ -21,7 +21,7 @@ __device__ __forceinline__ void rnn_noise(uint64_t seed, uint64_t ctr, float* no
         else if (k < 385) { layer = 1; which = k >= 384; e = which ? 0u : (uint32_t)(k - 256); }
         else { layer = 2; which = k >= 513; e = which ? (uint32_t)(k - 513) : (uint32_t)(k - 385); }
         const U4 r = philox64(e, TAG_NOISE_RNN | (layer << 8) | (which << 12), ctr, seed);
-        noise[k] = scale_noise(normal(r.x, r.y, false));
+        noise[k] = scale_noise(normal(r.x, r.y));
     }
 }
 

@@ -299,8 +299,8 @@ int act_part(const pm_rnn_selfplay* sp, int part, int max_blocks, void* stream) 
         if (int rc = pm_rnn_fold(sp->paramsB, sp->paramsB, PM_FOLD_TRAIN_FRESH, sp->seed_net, 0, ctr, sp->w_B, 1, stream))
             return rc;
     return pm_rnn_act_part(sp->w_opp, sp->opp, 1 + sp->n_pool, sp->w_B, sp->obsA, sp->obsB, sp->hA, sp->cA, sp->hB,
-                           sp->cB, sp->reset, 0.f, &sp->ctrl->epsilon, sp->seed_env, 0, ctr, sp->aA, sp->aB, nullptr,
-                           nullptr, sp->n, sp->chunk_A, sp->chunk_P, sp->opp_list, sp->opp_cnt, part, max_blocks,
+                           sp->cB, sp->reset, 0.f, &sp->ctrl->epsilon, sp->seed_env, 0, ctr, sp->aA, sp->aB, sp->qA,
+                           sp->qB, sp->n, sp->chunk_A, sp->chunk_P, sp->opp_list, sp->opp_cnt, part, max_blocks,
                            stream, sp->hA_in, sp->cA_in);
 }
 

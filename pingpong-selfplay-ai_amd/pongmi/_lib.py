@@ -106,7 +106,8 @@ class RnnSelfPlay(ctypes.Structure):
         [(n, c_i32) for n in ("n", "n_pool", "depth", "T", "chunk_A", "chunk_P", "max_steps", "_pad")] + \
         [("seq_cap", c_i64), ("min_episodes", c_i64)] + \
         [(n, c_double) for n in ("min_epsilon", "epsilon_decay", "pool_ratio")] + \
-        [("seed_env", c_u64), ("seed_net", c_u64), ("hA_in", c_void_p), ("cA_in", c_void_p)]
+        [("seed_env", c_u64), ("seed_net", c_u64), ("hA_in", c_void_p), ("cA_in", c_void_p), ("qA", c_void_p),
+         ("qB", c_void_p)]
 
 
 CTRL_DTYPE_BYTES = ctypes.sizeof(Ctrl)

@@ -59,7 +59,7 @@ class RNNSelfPlayLearner:
                  memory_size=200_000, min_episodes_for_training_start=10, depth=None, gamma=0.99, lr=1e-4,
                  epsilon=1.0, min_epsilon=0.05, epsilon_decay=0.999, target_update_interval=2000, pool_ratio=0.4,
                  grad_clip_norm=1.0, episode=0, seed=0, rank=0, world=1, allreduce=None, device=None,
-                 updates_per_step=1, max_episode_steps=1000, overlap=True):
+                 updates_per_step=1, max_episode_steps=1000, overlap=True, record_q=False):
         self.lib = _lib.load()
         self.overlap = bool(overlap)
         # The overlapped step acts for the NEXT step's opponents speculatively, reading (h, c) of
@@ -132,6 +132,11 @@ class RNNSelfPlayLearner:
                      "enable", "ctrl"):
             setattr(sp, name, ptr(getattr(self, name)))
         sp.paramsB = ptr(self.learner.params)
+        # record_q: the act also writes the Q values each player chose from ([n, 3] each, qA / qB), for
+        # parity checks of the acting decision beside the actions of the same launch
+        self.qA = torch.zeros((n, 3), **f32) if record_q else None
+        self.qB = torch.zeros((n, 3), **f32) if record_q else None
+        sp.qA, sp.qB = (ptr(self.qA), ptr(self.qB)) if record_q else (None, None)
         sp.n, sp.n_pool, sp.depth, sp.T = n, self.n_pool, self.depth, self.T
         sp.max_steps = int(max_episode_steps or 0)
         p_pool = pool_ratio if self.n_pool else 0.0

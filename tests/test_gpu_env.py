@@ -157,8 +157,8 @@ def test_autoreset_serves_match_philox_restatement(orc):
         assert np.array_equal(st["serves"], before["serves"])
         assert env.counter == t + 1
         vx, vy, sp = orc.philox_serve(p, idx, None, 77, step=t)
-        np.testing.assert_allclose(st["vx"][idx], vx, rtol=4e-16, atol=1e-18)
-        np.testing.assert_allclose(st["vy"][idx], vy, rtol=4e-16, atol=1e-18)
+        assert np.array_equal(st["vx"][idx], vx)
+        assert np.array_equal(st["vy"][idx], vy)
         assert np.array_equal(st["spin"][idx], sp)
         for k, v in (("x", 0.5), ("y", 0.5), ("top", 0.5), ("bot", 0.5), ("scoreA", 0), ("scoreB", 0), ("bounces", 0)):
             assert np.all(st[k][idx] == v), (t, k)
@@ -201,8 +201,8 @@ def test_production_serves_match_philox_restatement(orc):
     st = env.get_state()
     p = orc.env_params_from_kwargs(**kw)
     vx, vy, sp = orc.philox_serve(p, np.arange(n), np.zeros(n, np.int64), 1234)
-    np.testing.assert_allclose(st["vx"], vx, rtol=4e-16, atol=1e-18)
-    np.testing.assert_allclose(st["vy"], vy, rtol=4e-16, atol=1e-18)
+    assert np.array_equal(st["vx"], vx)
+    assert np.array_equal(st["vy"], vy)
     assert np.array_equal(st["spin"], sp)
     speed = np.hypot(st["vx"], st["vy"])
     ang = np.degrees(np.arctan2(st["vy"], st["vx"]))

@@ -261,3 +261,105 @@ def test_collect_without_tree_matches():
     assert torch.equal(prios.cpu(), with_tree.prios.cpu())
     assert torch.equal(ra.ep_reward.cpu(), rb.ep_reward.cpu())
     assert int(stats[0]) > 0
+
+
+# ---------------------------------------------------------------------------------------------------
+# Both launches against the oracle directly (oracle.cpu_selfplay.PhiloxRollout: the rollout restated
+# on the device's Philox streams — noise, epsilon draws, serves — with the QNet in the tile's float32
+# order and the C oracle's tick), not only against the stepped HIP composition: rows (as int32),
+# priorities, PER leaves and tree, the env state, observations, ep_reward and counters, bit for bit.
+CFG = dict(paddle_width=0.2, paddle_speed=0.03, max_score=3, enable_spin=True, magnus_factor=0.025, restitution=1,
+           friction=0.6, ball_mass=1.0, world_ball_radius=0.03, ball_speed_range=[0.03, 0.05], spin_range=[-5, 5],
+           ball_angle_intervals=[[-60, -30], [30, 60]], speed_scale_every=1, speed_increment=0.1)  # config.yaml
+
+
+def _nets(seed):
+    from models.qnet import QNet
+    from pongmi import _lib
+    from pongmi.qnet import fold, pack_state_dict
+    torch.manual_seed(seed)
+    mA, mB = QNet(7, 3), QNet(7, 3)
+    sdA = {k: v.numpy() for k, v in mA.state_dict().items()}
+    sdB = {k: v.numpy() for k, v in mB.state_dict().items()}
+    return sdA, sdB, fold(pack_state_dict(mA.state_dict()), _lib.PM_FOLD_TRAIN).reshape(-1), \
+        pack_state_dict(mB.state_dict()).reshape(-1)
+
+
+def _env_matches_oracle(env, o, orc):
+    st = env.get_state()
+    for k in ("x", "y", "vx", "vy", "spin", "top", "bot", "scoreA", "scoreB", "bounces"):
+        assert np.array_equal(st[k], o.arr[k]), k
+    oA, oB = orc.obs_of_arenas(o.arr)
+    assert np.array_equal(env.obsA.cpu().numpy(), oA) and np.array_equal(env.obsB.cpu().numpy(), oB)
+    assert env.counter == o.counter
+
+
+@pytest.mark.parametrize("n,steps,eps", [(4096, 120, 0.02), (333, 80, 1.0), (1000, 100, 0.0)])
+def test_rollout_matches_oracle(orc, n, steps, eps):
+    """K9 (pm_rollout, configs[1]) against the oracle rollout: state, observations, counters."""
+    from oracle.cpu_selfplay import PhiloxRollout
+    from pongmi.env import PongEnv2PBatch
+    from pongmi.rollout import STATS, SelfPlayRollout
+    sdA, sdB, wA, paramsB = _nets(100 + n)
+    seed_env, seed_net = 0x5EED + n, 31 + n
+    env = PongEnv2PBatch(n, seed=seed_env, autoreset=True, **CFG)
+    env.reset()
+    o = PhiloxRollout(CFG, env.get_state(), sdA, sdB, eps, seed_env, seed_net, env.counter)
+    assert np.array_equal(o.wA, wA.cpu().numpy()[:4932])  # modelA's fold (its frozen eps) restated
+    st = SelfPlayRollout(env, wA, paramsB, epsilon=eps, seed_net=seed_net).run(steps)
+    tot = o.run(steps)
+    _env_matches_oracle(env, o, orc)
+    assert [st[k] for k in STATS] == tot[:4].tolist()
+    assert tot[0] > 0
+
+
+@pytest.mark.parametrize("n,steps_per_launch,launches", [(4096, 12, 2), (65536, 15, 1)])
+def test_collect_matches_oracle(orc, n, steps_per_launch, launches):
+    """The collecting rollout (pm_rollout_push) against the oracle with memory.push: at 4 096 arenas
+    over two launches, the ring wrapping inside the second and the priorities changed in between (the
+    push then stores their max); at configs[2]'s 65 536 arenas, one 15-step launch filling a
+    983 040-row ring exactly."""
+    from oracle.cpu_selfplay import PhiloxRollout
+    from pongmi.env import PongEnv2PBatch
+    from pongmi.replay import DeviceReplay
+    from pongmi.rollout import STATS_PUSH, SelfPlayRollout
+    sdA, sdB, wA, paramsB = _nets(7 + n)
+    seed_env, seed_net, eps = 0xC0DE + n, 11 + n, 0.02
+    cap = n * steps_per_launch * launches - (n // 2 if launches > 1 else 0)  # wraps inside the last launch
+    cap = max(cap, n * steps_per_launch)
+    env = PongEnv2PBatch(n, seed=seed_env, autoreset=True, **CFG)
+    env.reset()
+    replay = DeviceReplay(cap, env.device)
+    roll = SelfPlayRollout(env, wA, paramsB, epsilon=eps, seed_net=seed_net)
+    ring = {"trans": np.zeros((cap, 16), np.float32), "prios": np.zeros(cap, np.float32), "pos": 0, "cap": cap}
+    o = PhiloxRollout(CFG, env.get_state(), sdA, sdB, eps, seed_env, seed_net, env.counter, replay=ring)
+    got = np.zeros(6, np.int64)
+    for k in range(launches):
+        if k == 1:  # a learner changed the priorities between the launches
+            g = torch.Generator().manual_seed(n)
+            new = torch.rand(replay.size, generator=g) * 3 + 0.01
+            replay.prios[:replay.size] = new.to(replay.prios.device)
+            ring["prios"][:replay.size] = new.numpy()
+            replay.refresh()
+        ring["prio"] = np.float32(ring["prios"].max() if k else 1.0)  # PrioritizedReplay.push's max (:57)
+        assert np.float32(replay.push_prio()) == ring["prio"]
+        st = roll.run(steps_per_launch, replay=replay)
+        got += np.array([st[k2] for k2 in STATS_PUSH])
+        o.run(steps_per_launch)
+    _env_matches_oracle(env, o, orc)
+    assert got.tolist() == o.stats.tolist()
+    assert replay.pos == ring["pos"]
+    assert np.array_equal(replay.trans.cpu().numpy().view(np.int32), ring["trans"].view(np.int32))
+    assert np.array_equal(replay.prios.cpu().numpy(), ring["prios"])
+    assert np.array_equal(roll.ep_reward.cpu().numpy(), o.ep_reward)
+    # the PER leaves prio ** alpha and both node levels, restated (oracle.per_tree) from the oracle's prios
+    from pongmi import replay as rp
+    chunk, sub, leaf = orc.per_tree(ring["prios"], cap, replay.alpha)
+    work = replay.work.cpu()
+    nchunk, nsub = -(-cap // 1024), -(-cap // 64)
+    o1 = rp._pad(nchunk)
+    o2 = o1 + rp._pad(nsub)
+    assert np.array_equal(work[:8 * nchunk].numpy().view(np.float64), chunk)
+    assert np.array_equal(work[o1:o1 + 8 * nsub].numpy().view(np.float64), sub)
+    assert np.array_equal(work[o2:o2 + 4 * cap].numpy().view(np.float32), leaf)
+    assert got[0] > 0

@@ -708,6 +708,10 @@ def main():
                     help="reference: model5-5_fault.pth's QNet weights (tests/golden/qnet.npz) for modelB and modelA "
                          "(SURVEY 8d); random: random-init nets of the reference architecture")
     ap.add_argument("--no-overlap", action="store_true", help="dqn: plain step (opponent act in k_act_sp, not in the learner launch)")
+    ap.add_argument("--no-features-ahead", action="store_true",
+                    help="dqn: k_actenv's env blocks run modelB's whole forward (features + heads) themselves instead "
+                         "of reading the features the previous learner launch computed ahead (featB): the A/B of the "
+                         "featB round trip")
     ap.add_argument("--comm", choices=("native", "torch"), default="native",
                     help="N > 1: the gradient all-reduce as libpongmi's own RCCL communicator inside one library "
                          "call per vector step (native), or torch.distributed.all_reduce between launches (torch)")
@@ -750,7 +754,8 @@ def main():
     sdB, sdA, pool, wdesc = nets
     L = SelfPlayLearner(ENV_KW, args.arenas, sdB, sdA, pool, batch=args.batch, memory_size=args.memory,
                         epsilon=0.08, seed=7, rank=rank, world=world, allreduce=allreduce,
-                        overlap=not args.no_overlap, updates_per_step=U, learn_multi=not args.no_learn_multi)
+                        overlap=not args.no_overlap, updates_per_step=U, learn_multi=not args.no_learn_multi,
+                        features_ahead=not args.no_features_ahead)
 
     def one_step(ev=None):
         # the production path: the overlapped vector step (L.step); an instrumented step is the same

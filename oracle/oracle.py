@@ -493,10 +493,35 @@ def _seq_sum(cols):
     return acc
 
 
+_EXP_C = (1.0, 1.0, 0.5, 0.16666666666666666, 0.041666666666666664, 0.008333333333333333, 0.001388888888888889,
+          0.0001984126984126984, 2.48015873015873e-05, 2.7557319223985893e-06, 2.755731922398589e-07,
+          2.505210838544172e-08, 2.08767569878681e-09, 1.6059043836821613e-10)
+
+
+def det_pow_f32(p, alpha):
+    """csrc/pm_per.h prio_pow restated: the PER leaf prio ** alpha in double from correctly rounded
+    operations (atanh-series log, Cody-Waite + Taylor exp), rounded once to float — bit for bit the
+    device's leaf, and within an ulp of numpy's float32 power (the reference's, :67)."""
+    p = np.asarray(p, np.float32)
+    a = np.float64(np.float32(alpha))
+    mant, ex = np.frexp(np.where(p > 0, p, np.float32(1)).astype(np.float64))
+    m, e = mant * 2.0, ex.astype(np.int64) - 1
+    big = m > 1.4142135623730951
+    m, e = np.where(big, m * 0.5, m), np.where(big, e + 1, e)
+    s = (m - 1.0) / (m + 1.0)
+    s2 = s * s
+    q = s2 * _horner(s2, _LN_C)
+    y = a * (e.astype(np.float64) * 0.69314718055994531 + (2.0 * s + s * q))
+    k = np.floor(y * 1.4426950408889634 + 0.5)
+    r = (y - k * 6.93147180369123816490e-01) - k * 1.90821492927058770002e-10
+    out = np.ldexp(_horner(r, _EXP_C), k.astype(np.int64)).astype(np.float32)
+    return np.where(p > 0, out, np.float32(0)).astype(np.float32)
+
+
 def per_tree(prios, cap, alpha=0.6):
-    """Leaves powf(prio, alpha) (f32), level-1 nodes ((q0+q1)+q2)+q3 of sequential 16-leaf fp64 sums,
-    level-2 nodes sequential sums of 16 level-1 nodes. Returns (chunk, sub, leaf)."""
-    leaf = np.asarray(prios[:cap], np.float32) ** np.float32(alpha)
+    """Leaves prio_pow(prio, alpha) (f32, det_pow_f32), level-1 nodes ((q0+q1)+q2)+q3 of sequential
+    16-leaf fp64 sums, level-2 nodes sequential sums of 16 level-1 nodes. Returns (chunk, sub, leaf)."""
+    leaf = det_pow_f32(prios[:cap], alpha)
     nsub = (cap + PER_SUB - 1) // PER_SUB
     nch = (cap + PER_CHUNK - 1) // PER_CHUNK
     lf = np.zeros(nsub * PER_SUB)
@@ -746,7 +771,7 @@ def below(r, n):
 # exact evaluation order (numpy float64 elementwise operations are the same correctly rounded IEEE
 # operations and never fuse), rounded once to float: bit-identical to every device draw.
 _LN_C = (0.66666666666666663, 0.40000000000000002, 0.28571428571428570, 0.22222222222222221, 0.18181818181818182,
-         0.15384615384615385)
+         0.15384615384615385, 0.13333333333333333, 0.11764705882352941, 0.10526315789473684, 0.09523809523809523)
 _COS_C = (-0.5, 0.041666666666666664, -0.0013888888888888889, 2.4801587301587302e-05, -2.755731922398589e-07,
           2.0876756987868100e-09, -1.1470745597729725e-11)
 _SIN_C = (-0.16666666666666666, 0.0083333333333333332, -0.00019841269841269841, 2.7557319223985893e-06,

@@ -106,14 +106,16 @@ __device__ __forceinline__ int32_t below(uint32_t r, uint32_t n) {
 // then rounded once to float. Every step is a correctly rounded IEEE operation (this file builds with
 // -ffp-contract=off), so the oracle's numpy restatement (oracle.normal_f32) reproduces every draw bit
 // for bit: the noise, and with it every NoisyNet forward, is pinned exactly, not to an ulp band.
-// Accuracy: |log error| < 1e-15, |cos error| < 1e-15, far below the float the result is rounded to.
+// Accuracy: log and cos within ~1e-16 relative, far below the float the result is rounded to.
 __device__ __forceinline__ double det_ln_u1(uint32_t k) {  // ln(k * 2^-24), k in [1, 2^24]
     int e = 31 - __builtin_clz(k);                        // k = m 2^e, m in [1, 2)
     double m = (double)k / (double)(1u << e);             // exact
     if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
     const double s = (m - 1.0) / (m + 1.0), s2 = s * s;  // ln m = 2 atanh(s)
     const double p = s2 * (0.66666666666666663 + s2 * (0.40000000000000002 + s2 * (0.28571428571428570 +
-                     s2 * (0.22222222222222221 + s2 * (0.18181818181818182 + s2 * 0.15384615384615385)))));
+                     s2 * (0.22222222222222221 + s2 * (0.18181818181818182 + s2 * (0.15384615384615385 +
+                     s2 * (0.13333333333333333 + s2 * (0.11764705882352941 + s2 * (0.10526315789473684 +
+                     s2 * 0.09523809523809523)))))))));
     return (double)(e - 24) * 0.69314718055994531 + (2.0 * s + s * p);
 }
 __device__ __forceinline__ double det_cos_turn(double t) {  // cos(2 pi t), t in [0, 1) (24-bit grid)

@@ -90,7 +90,31 @@ __device__ __forceinline__ RingNodes ring_nodes(const PushRange& pr, int64_t g) 
     return r;
 }
 
-__device__ __forceinline__ float prio_pow(float p, float alpha) { return powf(p, alpha); }
+// prio ** alpha, PrioritizedReplay's leaf (train_iterative.py:67: prios ** alpha in float32). Formed
+// in double from +, -, *, / and exact scalings only — ln p by the atanh series on m in
+// [sqrt(1/2), sqrt(2)), exp by a Cody-Waite split and its Taylor series — then rounded once to float:
+// within an ulp of numpy's powf (the reference's arithmetic), and a fixed sequence of correctly
+// rounded operations, so the oracle (oracle.det_pow_f32) restates every leaf bit for bit.
+__device__ __forceinline__ float prio_pow(float p, float alpha) {
+    if (!(p > 0.f)) return 0.f;
+    int e;
+    double m = 2.0 * frexp((double)p, &e);  // p = m 2^(e - 1), m in [1, 2): exact
+    e = e - 1;
+    if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    const double q = s2 * (0.66666666666666663 + s2 * (0.40000000000000002 + s2 * (0.28571428571428570 +
+                     s2 * (0.22222222222222221 + s2 * (0.18181818181818182 + s2 * (0.15384615384615385 +
+                     s2 * (0.13333333333333333 + s2 * (0.11764705882352941 + s2 * (0.10526315789473684 +
+                     s2 * 0.09523809523809523)))))))));
+    const double y = (double)alpha * ((double)e * 0.69314718055994531 + (2.0 * s + s * q));
+    const double k = floor(y * 1.4426950408889634 + 0.5);
+    const double r = (y - k * 6.93147180369123816490e-01) - k * 1.90821492927058770002e-10;  // |r| <= ln2 / 2
+    const double ex = 1.0 + r * (1.0 + r * (0.5 + r * (0.16666666666666666 + r * (0.041666666666666664 +
+                      r * (0.008333333333333333 + r * (0.001388888888888889 + r * (0.0001984126984126984 +
+                      r * (2.48015873015873e-05 + r * (2.7557319223985893e-06 + r * (2.755731922398589e-07 +
+                      r * (2.505210838544172e-08 + r * (2.08767569878681e-09 + r * 1.6059043836821613e-10))))))))))));
+    return (float)ldexp(ex, (int)k);
+}
 
 // Leaf e as the tree sees it: pushed value inside the pending push range, 0 past cap.
 __device__ __forceinline__ float per_leaf(const float* __restrict__ leaf, int64_t e, const PushRange& pr) {

@@ -339,11 +339,11 @@ def test_launch_timer_leaves_results_unchanged(golden):
 
 @pytest.mark.parametrize("n,cap", [(1000, 2500), (2048, 8192), (300, 1000), (4096, 4160),
                                    (65536, 1_000_000)])  # the last: the bench's configs[2] sizes
-def test_sum_tree_incremental_equals_rebuild(golden, n, cap):
+def test_sum_tree_incremental_equals_rebuild(golden, orc, n, cap):
     """The PER sum tree is maintained incrementally inside k_learn (scattered sub-blocks + the next
     push range, with the pending push substituted). After many steps — ring wrap-arounds at
     capacities that are not multiples of the 64/1024-entry nodes — it must equal a full rebuild
-    (pm_selfplay_prepare) bit for bit, and the leaves must match the oracle's prio^alpha sums."""
+    (pm_selfplay_prepare) bit for bit, and the chunk sums must equal the oracle's (oracle.per_tree) exactly."""
     L = _learner(golden, n=n, batch=256, cap=cap, seed=4, epsilon=0.5)
     for k in range(3 * cap // n + 7):
         L.step()
@@ -359,9 +359,8 @@ def test_sum_tree_incremental_equals_rebuild(golden, n, cap):
     pos = c["pos"]
     slots = (pos + np.arange(n)) % cap  # the push the tree already accounts for
     pr[slots] = np.float32(c["max_prio"])
-    ref = np.array([np.sum((pr[k * 1024:(k + 1) * 1024] ** np.float32(0.6)).astype(np.float64))
-                    for k in range(nch)])
-    np.testing.assert_allclose(chunks, ref, rtol=1e-6)  # device powf vs numpy float32 pow
+    ref, _, _ = orc.per_tree(pr, cap)  # the leaves prio ** 0.6 and the fp64 node sums in the device's order
+    assert np.array_equal(chunks, ref)
 
 
 def test_overlapped_step_is_bitwise_identical(golden):

@@ -14,7 +14,10 @@ import os
 import sys
 from collections import defaultdict
 
-args = [a for a in sys.argv[1:] if not a.startswith("--")]
+argv = sys.argv[1:]
+if "--json" in argv:  # the option's value is not a positional argument
+    del argv[argv.index("--json") + 1]
+args = [a for a in argv if not a.startswith("--")]
 tag = args[0] if args else "r1"
 root = args[1] if len(args) > 1 else "gpurun_out"
 out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None

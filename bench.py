@@ -621,6 +621,8 @@ def run_infer(args, dist, rank, world):
     k_s = sum(ks) / reps
     ev_s = e0.elapsed_time(e1) * 1e-3 / reps
     st = dict(zip(STATS, tot.cpu().tolist()))
+    r16 = int(os.environ.get("PONGMI_ROLL16", "1") or "1")  # the library's tile choice (pm_rollout.hip roll16)
+    tile16 = bool(r16 & (2 if collect else 1))
     if rank == 0:
         value = n * world * steps / dt
         flop = n * chunk * 2 * FLOP_PER_ARENA
@@ -637,14 +639,15 @@ def run_infer(args, dist, rank, world):
                        "arenas_per_gpu": n, "global_arenas": n * world, "steps_per_launch": chunk,
                        "launches_in_timed_region": -(-steps // chunk), "parallelism": f"dp{world} (independent "
                        "arena shards, no collective)"},
-            "roofline": {"bound": "mfma", "kernel": "k_rollout (K9: both players' QNet forward + env tick, "
-                                                    f"{chunk} vector steps per launch)",
+            "roofline": {"bound": "mfma", "kernel": (f"k_rollout16 (K9 on 16-arena tiles, v_mfma_f32_16x16x4_f32" if tile16
+                                                     else "k_rollout (K9 on 32-arena tiles") +
+                                                    f": both players' QNet forward + env tick, {chunk} vector steps per launch)",
                          "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": infer_traffic(n, chunk),
                          "avg_us": round(k_s * 1e6, 1), "avg_us_per_step": round(k_s / chunk * 1e6, 4),
                          "flop_per_env_step": 2 * FLOP_PER_ARENA, "n": n,
-                         "waves": 2 * (-(-n // 32)), "wave_slots": 256 * 4,
+                         "waves": 8 * (-(-n // 16)) if tile16 else 4 * (-(-n // 32)), "wave_slots": 256 * 4,
                          "timing": f"pm_timer_arm dispatch of {reps} launches after the timed region; "
                                    f"HIP events incl. the heads fold: {ev_s * 1e6:.1f} us per launch"},
             "rollout": st,
@@ -663,8 +666,8 @@ def run_infer(args, dist, rank, world):
                                          f"(eps 0.02 held, learner off) + memory.push of every transition into a "
                                          f"{args.memory}-row PER ring, {chunk} vector steps per launch")
             out["config"]["replay_cap"] = args.memory
-            out["roofline"]["kernel"] = (f"k_rollout_push (both players' QNet forward + env tick + replay push, "
-                                         f"{chunk} vector steps per launch)")
+            out["roofline"]["kernel"] = (f"{'k_rollout16_push' if tile16 else 'k_rollout_push'} (both players' QNet "
+                                         f"forward + env tick + replay push, {chunk} vector steps per launch)")
             # HBM bytes per launch from the committed counter passes (profiles/r3_collect_pmc.json,
             # tools/gpu_r3_collect_pmc.sh: 65 536 arenas, 15-step launches); None at other shapes
             tb = pmc_traffic("k_rollout_push", "r3_collect_pmc.json")

@@ -34,6 +34,8 @@
 // (:238, :245) and the episodes' win / reward counts (:247-249). Wave 3 issues the step's three
 // stores right after the tick; the vmcnt(0) it already waits on for the next step's heads retires
 // them a full step later, so no store latency reaches the step's critical path.
+#include <stdlib.h>
+
 #include "pm_host.h"
 #include "pm_mfma.h"
 #include "pm_per.h"
@@ -349,6 +351,279 @@ __global__ __launch_bounds__(kRollBlock) __attribute__((amdgpu_waves_per_eu(3, 3
     rollout_body<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// K9 on 16-arena tiles (the inference launch): v_mfma_f32_16x16x4_f32 is, like the 32x32x2 form, a
+// k-ordered fmaf chain bit for bit (tools/mfma_order_probe.hip: 0 of 102 400 outputs differ), so a
+// QNet forward computed in 16-row / 16-column tiles over the SAME k sequences as tile_hidden /
+// tile_heads gives the same bits. Half the tile width doubles the tiles: 4 096 arenas are 256 blocks,
+// one per CU, instead of 128 blocks on half the chip, and each block's MFMA chain is half as long.
+//
+// Block = 8 waves, wave 4p + rt: player p, row tile rt (16 of the 64 units) of both layers.
+//   layer 1 (K 8: bias + 7 inputs; all four row tiles in every wave, 8 MFMAs) -> ReLU -> the wave's own
+//   LDS slab in layer 2's k order (tile_hidden's pair sequence (t, r) -> units 32t + rho(r) + {0, 4}) ->
+//   layer 2 (K 64, 16 MFMAs from the bias) -> ReLU -> LDS in the head chains' order -> wave 0: both
+//   players' head chains (lanes 32p + 16h + col: half h of column col, tile_heads' per-half fmaf
+//   chains and cross-half add), the actions, then the fp64 tick of the 16 arenas (kept in wave 0's
+//   registers, replicated over its four lane groups) and the next observations into LDS. Two barriers
+//   per vector step. Every LDS array a lane group reads as float4 runs keeps its 16 columns side by
+//   side (conflict-free ds_read_b128; the first layout, [col][64], ran 3.67 us per step).
+constexpr int kR16Block = 512;
+
+// layer 2's k order: sequence position of unit u, and the unit at position q
+__device__ __forceinline__ int l2_pos(int u) {
+    const int t = u >> 5, v = u & 31, b = (v >> 2) & 1, r = (v & 3) + 4 * (v >> 3);
+    return 2 * (16 * t + r) + b;
+}
+__device__ __forceinline__ int l2_unit(int q) {
+    const int i = q >> 1, b = q & 1;
+    return 32 * (i >> 4) + rho(i & 15) + 4 * b;
+}
+// the head chains' order: unit u is element 16t + r of half (u >> 2) & 1's chain
+__device__ __forceinline__ int head_pos(int u) {
+    const int t = u >> 5, v = u & 31;
+    return 16 * t + (v & 3) + 4 * (v >> 3);
+}
+
+typedef float f32x4v16 __attribute__((ext_vector_type(4)));
+
+struct Roll16Shared {
+    __attribute__((aligned(16))) float img2[2][4][4][64][4];  // [p][rt][s4][lane][e]: layer-2 A, instruction 4 s4 + e
+    __attribute__((aligned(16))) float img1[2][4][64][2];     // [p][rt][lane][s]: layer-1 A
+    __attribute__((aligned(16))) float b2v[2][4][4][4];       // [p][rt][g][r]: b2[16 rt + 4 g + r]
+    __attribute__((aligned(16))) float hfA[264];              // modelA's heads (F_H / F_BH order)
+    __attribute__((aligned(16))) float hfB[2][320];           // modelB's heads of the step, double-buffered
+    // the two staging arrays are read as float4 runs whose 16 lanes per lane group sit side by side
+    // (lane col at [..][col][4]): one ds_read_b128 pass per lane group, no bank conflict
+    __attribute__((aligned(16))) float h1s[8][4][4][16][4];   // per wave [g][s >> 2][col][s & 3]: layer-2 B of instruction s
+    __attribute__((aligned(16))) float c2s[2][2][8][16][4];   // [p][h][q >> 2][col][q & 3]: ReLU(layer 2), chain order
+    float ob[2][16][8];                                       // [p][col]: the observations of the step
+};
+
+template <bool PUSH>
+__device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_env_state& s, const float* __restrict__ wA,
+                                               const float* __restrict__ wB, const float* __restrict__ ws, double eps,
+                                               uint64_t seed_env, uint64_t counter0, int steps, float* __restrict__ obsA,
+                                               float* __restrict__ obsB, long long* __restrict__ stats, int n,
+                                               const RollPush& rp) {
+    __shared__ Roll16Shared sm;
+    const int t = threadIdx.x, lane = t & 63, col = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int player = wv >> 2, rt = wv & 3;
+    const int i = blockIdx.x * 16 + col;
+    const bool valid = i < n;
+    // ---- operand images from the plain effective weights (once per launch; global reads hit L2)
+    for (int k = t; k < 2 * 4 * 4 * 64 * 4; k += kR16Block) {
+        const int pp = k >> 12, r2 = (k >> 10) & 3, s4 = (k >> 8) & 3, ln = (k >> 2) & 63, e = k & 3;
+        const float* w = pp ? wB : wA;
+        (&sm.img2[0][0][0][0][0])[k] = w[W2 + (16 * r2 + (ln & 15)) * 64 + l2_unit(4 * (4 * s4 + e) + (ln >> 4))];
+    }
+    for (int k = t; k < 2 * 4 * 64 * 2; k += kR16Block) {
+        const int pp = k >> 9, r2 = (k >> 7) & 3, ln = (k >> 1) & 63, sx = k & 1;
+        const float* w = pp ? wB : wA;
+        const int row = 16 * r2 + (ln & 15), kk = 4 * sx + (ln >> 4);  // input k' = 0 is the constant 1 (b1)
+        (&sm.img1[0][0][0][0])[k] = kk == 0 ? w[B1 + row] : w[W1 + row * 7 + kk - 1];
+    }
+    if (t < 128) {
+        const int pp = t >> 6, r2 = (t >> 4) & 3, gg = (t >> 2) & 3, r = t & 3;
+        (&sm.b2v[0][0][0][0])[t] = (pp ? wB : wA)[B2 + 16 * r2 + 4 * gg + r];
+    }
+    if (t < 260) sm.hfA[t] = t < 256 ? wA[PLAIN + F_H + t] : wA[PLAIN + F_BH + t - 256];
+    if (wv == 7) fetch_heads(ws, 0, sm.hfB[0], lane);
+    // ---- wave 0 keeps the 16 arenas (every lane group a copy) and ticks them
+    Arena a{};
+    int fin = 0, winB = 0, ptA = 0, ptB = 0, winE = 0, rsum = 0;
+    float er = 0.f, leafv = 0.f;
+    if (wv == 0) {
+        a = load_arena(s, valid ? i : n - 1);
+        float oA[7], oB[7];
+        observe(a, oA, oB);
+        if (g < 2)
+#pragma unroll
+            for (int k = 0; k < 7; ++k) sm.ob[g][col][k] = g ? oB[k] : oA[k];
+        if constexpr (PUSH) {
+            er = rp.ep_reward[valid ? i : n - 1];
+            leafv = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(prio_pow(rp.prio, rp.alpha))));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const float4* im2 = reinterpret_cast<const float4*>(sm.img2[player][rt][0][lane]);
+    for (int st = 0; st < steps; ++st) {
+        const uint64_t ctr = counter0 + (uint64_t)st;
+        if (wv == 7 && st + 1 < steps) fetch_heads_async(ws, st + 1, sm.hfB[(st + 1) & 1], lane);  // lands during the step
+        // layer 1, all four row tiles (every wave of the player: no barrier), input k' = 4 s + g
+        const float* o = sm.ob[player][col];
+        const float x0 = g == 0 ? 1.0f : o[g - 1], x1 = o[3 + g];
+        const f32x4v16 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r1 = 0; r1 < 4; ++r1) {
+            const float2 w1 = *reinterpret_cast<const float2*>(sm.img1[player][r1][lane]);
+            f32x4v16 c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, x0, zero, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.y, x1, c1, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // unit 16 r1 + 4 g + r -> its slot in layer 2's k order
+                const int q = l2_pos(16 * r1 + 4 * g + r), sq = q >> 2;
+                sm.h1s[wv][q & 3][sq >> 2][col][sq & 3] = relu(c1[r]);
+            }
+        }
+        // the wave reads back what its own lanes wrote: LDS serves one wave's instructions in order
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float bs[16];
+        {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 v = *reinterpret_cast<const float4*>(sm.h1s[wv][g][k][col]);
+                bs[4 * k] = v.x; bs[4 * k + 1] = v.y; bs[4 * k + 2] = v.z; bs[4 * k + 3] = v.w;
+            }
+        }
+        const float4 bi = *reinterpret_cast<const float4*>(sm.b2v[player][rt][g]);
+        f32x4v16 c2 = {bi.x, bi.y, bi.z, bi.w};
+        StagedServe sv;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const float4 w = im2[s4 * 64];
+            c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, bs[4 * s4 + 0], c2, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, bs[4 * s4 + 1], c2, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, bs[4 * s4 + 2], c2, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, bs[4 * s4 + 3], c2, 0, 0, 0);
+            if (wv == 0) sv.stage(s4, p, (uint32_t)i, ctr, seed_env);  // the serve draw in the chain's gaps
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int u = 16 * rt + 4 * g + r, q = head_pos(u);
+            sm.c2s[player][(u >> 2) & 1][q >> 2][col][q & 3] = relu(c2[r]);
+        }
+        if (wv == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next step's heads landed
+        __syncthreads();  // (B) both players' layer 2
+        if (wv == 0) {
+            // heads: lane 32 hp + 16 hh + col runs half hh's four chains of player hp, column col
+            const int hp = lane >> 5, hh = (lane >> 4) & 1;
+            const float* hf = hp ? sm.hfB[st & 1] : sm.hfA;
+            const float4* hw = reinterpret_cast<const float4*>(hf) + hh * 32;
+            float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float4 x = *reinterpret_cast<const float4*>(sm.c2s[hp][hh][k][col]);
+                const float xx[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float4 w = hw[4 * k + e];
+                    v = fmaf(w.x, xx[e], v);
+                    a0 = fmaf(w.y, xx[e], a0);
+                    a1 = fmaf(w.z, xx[e], a1);
+                    a2 = fmaf(w.w, xx[e], a2);
+                }
+            }
+            v += __shfl_xor(v, 16);  // + the other half (both lanes get the same bits)
+            a0 += __shfl_xor(a0, 16);
+            a1 += __shfl_xor(a1, 16);
+            a2 += __shfl_xor(a2, 16);
+            v += hf[256];
+            a0 += hf[257];
+            a1 += hf[258];
+            a2 += hf[259];
+            const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
+            const float q[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
+            int act = argmax3(q);
+            if (hp) {  // random.random() < eps ? randint(0, 2) : argmax (train_iterative.py:126-130)
+                const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed_env);
+                if (u53(rr.x, rr.y) < eps) act = (int)below(rr.z, 3u);
+            }
+            const int aA = __shfl(act, col), aB = __shfl(act, 32 + col);
+            float sB[7];  // the step's observation of B (memory.push's s)
+#pragma unroll
+            for (int k = 0; k < 7; ++k) sB[k] = sm.ob[1][col][k];
+            float rA, rB;
+            const int d = tick(p, a, aA, aB, rA, rB);
+            ptA += rA > 0.f ? 1 : 0;
+            ptB += rB > 0.f ? 1 : 0;
+            if constexpr (PUSH) {
+                er += rB;  // ep_reward += rB (:245)
+                if (d) {
+                    winE += er > 0.f ? 1 : 0;
+                    rsum += (int)er;
+                }
+                if (valid) {  // memory.push((oB, aB, rB, nB, done)): lane group g stores the row's float4 g
+                    float nA[7], nB[7];
+                    observe(a, nA, nB);  // the terminal observation, before the serve
+                    int64_t slot = rp.pos + (int64_t)st * n + i;
+                    if (slot >= rp.cap) slot -= rp.cap;
+                    const float4 v = g == 0 ? make_float4(sB[0], sB[1], sB[2], sB[3])
+                                   : g == 1 ? make_float4(sB[4], sB[5], sB[6], rB)
+                                   : g == 2 ? make_float4(nB[0], nB[1], nB[2], nB[3])
+                                            : make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)));
+                    st_f4<false>(reinterpret_cast<float4*>(rp.trans + slot * PM_TRANS_F) + g, v);
+                    if (g == 0) rp.prios[slot] = rp.prio;
+                    else if (g == 1 && rp.leaf) rp.leaf[slot] = leafv;
+                }
+                if (d) er = 0.f;
+            }
+            if (d) {  // env.reset() with K1's step-keyed production serve
+                fin += 1;
+                winB += rB > 0.f ? 1 : 0;
+                serve_finish(sv.d);
+                serve(a, sv.d.vx, sv.d.vy, sv.d.spin);
+            }
+            float oA[7], oB[7];
+            observe(a, oA, oB);
+            if (g < 2)
+#pragma unroll
+                for (int k = 0; k < 7; ++k) sm.ob[g][col][k] = g ? oB[k] : oA[k];
+        }
+        __syncthreads();  // (C) the next observations
+    }
+    if (wv == 0 && g == 0 && valid) {
+        store_arena(s, i, a);
+        float oA[7], oB[7];
+        observe(a, oA, oB);
+        store_row7(obsA + (size_t)i * 7, oA);
+        store_row7(obsB + (size_t)i * 7, oB);
+        if constexpr (PUSH) rp.ep_reward[i] = er;
+    }
+    if (!stats || wv != 0) return;
+    constexpr int NS = PUSH ? 6 : 4;
+    const bool mine = g == 0 && valid;  // one lane per arena
+    long long v[6] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0, mine ? winE : 0,
+                      mine ? rsum : 0};
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    long long mv = v[0];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) mv = lane == k ? v[k] : mv;
+    if (lane < NS) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane), (unsigned long long)mv);
+}
+
+__global__ __launch_bounds__(kR16Block) void k_rollout16(const pm_env_params p, const pm_env_state s,
+                                                         const float* __restrict__ wA, const float* __restrict__ wB,
+                                                         const float* __restrict__ ws, double eps, uint64_t seed_env,
+                                                         uint64_t counter0, int steps, float* __restrict__ obsA,
+                                                         float* __restrict__ obsB, long long* __restrict__ stats,
+                                                         int n) {
+    rollout16_body<false>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
+}
+// the collecting launch runs 65 536 arenas (4 096 blocks): two blocks per CU (4 waves per SIMD) need
+// <= 128 registers
+__global__ __launch_bounds__(kR16Block) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_rollout16_push(
+    const pm_env_params p, const pm_env_state s, const float* __restrict__ wA, const float* __restrict__ wB,
+    const float* __restrict__ ws, double eps, uint64_t seed_env, uint64_t counter0, int steps,
+    float* __restrict__ obsA, float* __restrict__ obsB, long long* __restrict__ stats, int n, const RollPush rp) {
+    rollout16_body<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
+}
+
+// 16-arena tiles: PONGMI_ROLL16 bit 0 = the inference launch, bit 1 = the collecting launch (A/B only)
+int roll16() {
+    static const int v = [] {
+        const char* e = getenv("PONGMI_ROLL16");
+        return e && *e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 }  // namespace
 
 static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB,
@@ -368,12 +643,27 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
     hipLaunchKernelGGL(k_rollout_heads, dim3(steps), dim3(kHeadsBlock), 0, st, paramsB, seed_net, counter0, heads_ws);
     PM_LAUNCHED("k_rollout_heads");
     const dim3 grid(pm_blocks(n, 32)), block(kRollBlock);
+    if (rp && (roll16() & 2)) {
+        pm_launch(PM_TIMER_ROLLOUT, k_rollout16_push, dim3(pm_blocks(n, 16)), dim3(kR16Block), st, *p, *s, wA, wB,
+                  (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
+                  reinterpret_cast<long long*>(stats), n, *rp);
+        PM_LAUNCHED("k_rollout16_push");
+        if (per_work) return per_launch_nodes(per_work, rp->cap, st);
+        return PM_OK;
+    }
     if (rp) {
         pm_launch(PM_TIMER_ROLLOUT, k_rollout_push, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
                   (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n,
                   *rp);
         PM_LAUNCHED("k_rollout_push");
         if (per_work) return per_launch_nodes(per_work, rp->cap, st);
+        return PM_OK;
+    }
+    if (roll16() & 1) {
+        pm_launch(PM_TIMER_ROLLOUT, k_rollout16, dim3(pm_blocks(n, 16)), dim3(kR16Block), st, *p, *s, wA, wB,
+                  (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
+                  reinterpret_cast<long long*>(stats), n);
+        PM_LAUNCHED("k_rollout16");
         return PM_OK;
     }
     pm_launch(PM_TIMER_ROLLOUT, k_rollout, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,

@@ -43,8 +43,12 @@ def _assert_params(got, ref, what, steps):
 
 
 def _assert_grads(got, ref, what):
+    worst = 0.0
     for k, r in ref.items():
-        np.testing.assert_allclose(got[k], r, rtol=1e-3, atol=1e-5 * np.abs(r).max() + 1e-9, err_msg=f"{what}: {k}")
+        tol = 1e-5 * np.abs(r).max() + 1e-9
+        np.testing.assert_allclose(got[k], r, rtol=1e-3, atol=tol, err_msg=f"{what}: {k}")
+        worst = max(worst, float(np.max(np.abs(got[k] - r) / (tol + 1e-3 * np.abs(r)))))
+    print(f"\n{what}: gradient error / tolerance (rtol 1e-3, atol 1e-5 max|g|) max {worst:.4f}")
 
 
 def test_drqn_update_matches_reference(golden):

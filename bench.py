@@ -100,13 +100,16 @@ def pmc_traffic(kernel, profile="r3_pmc.json"):
     """HBM bytes per launch of `kernel` (`name`, or `name@grid` for one of its launch grids) from the
     committed rocprofv3 counter profile (profiles/r3_pmc.json: the default workload;
     profiles/r3_rnn_pmc.json: --workload rnn; profiles/r3_infer_pmc.json: --workload infer, 2 000-step
-    launches), or None."""
-    path = os.path.join(ROOT, "profiles", profile)
-    try:
-        with open(path) as fh:
-            return json.load(fh)["kernels"][kernel]["hbm_bytes"]
-    except (OSError, KeyError, ValueError):
-        return None
+    launches), or None. A newer round's profile of the same name (r4_pmc.json, …) wins when it
+    holds the kernel."""
+    stem = profile[3:] if profile.startswith("r3_") else profile
+    for name in (f"r4_{stem}", profile):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as fh:
+                return json.load(fh)["kernels"][kernel]["hbm_bytes"]
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def replicas_identical(dist, params):
@@ -497,10 +500,11 @@ def cpu_baseline_infer(seconds=12.0, n=4096, replay_cap=0):
             "reference_python_measured": "4 600 env-steps/s, batch-1 QNet rollout, 1 thread (SURVEY 6)"}
 
 
-def infer_traffic(n, chunk, pmc_steps=2000):
-    """k_rollout's HBM bytes for a launch of `chunk` steps, scaled from the committed counter pass
-    (profiles/r3_infer_pmc.json: launches of 2 000 steps at 4 096 arenas); None at other sizes."""
-    b = pmc_traffic("k_rollout", "r3_infer_pmc.json")
+def infer_traffic(n, chunk, pmc_steps=2000, kernel="k_rollout"):
+    """`kernel`'s (k_rollout / k_rollout16) HBM bytes for a launch of `chunk` steps, scaled from the
+    committed counter pass (profiles/r4_infer_pmc.json or r3_infer_pmc.json: launches of 2 000 steps
+    at 4 096 arenas); None at other sizes."""
+    b = pmc_traffic(kernel, "r3_infer_pmc.json")
     return None if b is None or n != 4096 else round(b * chunk / pmc_steps, 1)
 
 
@@ -642,9 +646,10 @@ def run_infer(args, dist, rank, world):
             "roofline": {"bound": "mfma", "kernel": (f"k_rollout16 (K9 on 16-arena tiles, v_mfma_f32_16x16x4_f32" if tile16
                                                      else "k_rollout (K9 on 32-arena tiles") +
                                                     f": both players' QNet forward + env tick, {chunk} vector steps per launch)",
-                         "compute": "v_mfma_f32_32x32x2_f32 (exact fp32; dense FP32 matrix peak 157.3 TF)",
+                         "compute": f"{'v_mfma_f32_16x16x4_f32' if tile16 else 'v_mfma_f32_32x32x2_f32'} (exact fp32; "
+                                    "dense FP32 matrix peak 157.3 TF)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": infer_traffic(n, chunk),
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": infer_traffic(n, chunk, kernel="k_rollout16" if tile16 else "k_rollout"),
                          "avg_us": round(k_s * 1e6, 1), "avg_us_per_step": round(k_s / chunk * 1e6, 4),
                          "flop_per_env_step": 2 * FLOP_PER_ARENA, "n": n,
                          "waves": 8 * (-(-n // 16)) if tile16 else 4 * (-(-n // 32)), "wave_slots": 256 * 4,

@@ -359,14 +359,15 @@ __global__ __launch_bounds__(kRollBlock) __attribute__((amdgpu_waves_per_eu(3, 3
 // one per CU, instead of 128 blocks on half the chip, and each block's MFMA chain is half as long.
 //
 // Block = 8 waves, wave 4p + rt: player p, row tile rt (16 of the 64 units) of both layers.
-//   layer 1 (K 8: bias + 7 inputs; all four row tiles in every wave, 8 MFMAs) -> ReLU -> the wave's own
-//   LDS slab in layer 2's k order (tile_hidden's pair sequence (t, r) -> units 32t + rho(r) + {0, 4}) ->
-//   layer 2 (K 64, 16 MFMAs from the bias) -> ReLU -> LDS in the head chains' order -> wave 0: both
-//   players' head chains (lanes 32p + 16h + col: half h of column col, tile_heads' per-half fmaf
-//   chains and cross-half add), the actions, then the fp64 tick of the 16 arenas (kept in wave 0's
-//   registers, replicated over its four lane groups) and the next observations into LDS. Two barriers
-//   per vector step. Every LDS array a lane group reads as float4 runs keeps its 16 columns side by
-//   side (conflict-free ds_read_b128; the first layout, [col][64], ran 3.67 us per step).
+//   layer 1 (K 8: bias + 7 inputs, 2 MFMAs) -> ReLU -> LDS in layer 2's k order (tile_hidden's pair
+//   sequence (t, r) -> units 32t + rho(r) + {0, 4}) -> layer 2 (K 64, 16 MFMAs from the bias) -> ReLU
+//   -> LDS in the head chains' order -> wave 0: both players' head chains (lanes 32p + 16h + col: half
+//   h of column col, tile_heads' per-half fmaf chains and cross-half add), the actions, then the fp64
+//   tick of the 16 arenas (kept in wave 0's registers, replicated over its four lane groups) and the
+//   next observations into LDS. Three barriers per vector step (every wave computing all four layer-1
+//   tiles into a slab of its own, to drop the first, ran 4.13 us per step against 2.69:
+//   profiles/r4_roll16_ab.txt). Every LDS array a lane group reads as float4 runs keeps its 16 columns
+//   side by side (conflict-free ds_read_b128; the first layout, [col][64], ran 3.67 us per step).
 constexpr int kR16Block = 512;
 
 // layer 2's k order: sequence position of unit u, and the unit at position q
@@ -394,7 +395,7 @@ struct Roll16Shared {
     __attribute__((aligned(16))) float hfB[2][320];           // modelB's heads of the step, double-buffered
     // the two staging arrays are read as float4 runs whose 16 lanes per lane group sit side by side
     // (lane col at [..][col][4]): one ds_read_b128 pass per lane group, no bank conflict
-    __attribute__((aligned(16))) float h1s[8][4][4][16][4];   // per wave [g][s >> 2][col][s & 3]: layer-2 B of instruction s
+    __attribute__((aligned(16))) float h1s[2][4][4][16][4];   // [p][g][s >> 2][col][s & 3]: layer-2 B of instruction s
     __attribute__((aligned(16))) float c2s[2][2][8][16][4];   // [p][h][q >> 2][col][q & 3]: ReLU(layer 2), chain order
     float ob[2][16][8];                                       // [p][col]: the observations of the step
 };
@@ -451,30 +452,26 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     for (int st = 0; st < steps; ++st) {
         const uint64_t ctr = counter0 + (uint64_t)st;
         if (wv == 7 && st + 1 < steps) fetch_heads_async(ws, st + 1, sm.hfB[(st + 1) & 1], lane);  // lands during the step
-        // layer 1, all four row tiles (every wave of the player: no barrier), input k' = 4 s + g
-        const float* o = sm.ob[player][col];
-        const float x0 = g == 0 ? 1.0f : o[g - 1], x1 = o[3 + g];
-        const f32x4v16 zero = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r1 = 0; r1 < 4; ++r1) {
-            const float2 w1 = *reinterpret_cast<const float2*>(sm.img1[player][r1][lane]);
+        // layer 1, the wave's row tile (K 8: bias + 7 inputs, input k' = 4 s + g) -> ReLU -> LDS
+        {
+            const float* o = sm.ob[player][col];
+            const float x0 = g == 0 ? 1.0f : o[g - 1], x1 = o[3 + g];
+            const float2 w1 = *reinterpret_cast<const float2*>(sm.img1[player][rt][lane]);
+            const f32x4v16 zero = {0.f, 0.f, 0.f, 0.f};
             f32x4v16 c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, x0, zero, 0, 0, 0);
             c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.y, x1, c1, 0, 0, 0);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {  // unit 16 r1 + 4 g + r -> its slot in layer 2's k order
-                const int q = l2_pos(16 * r1 + 4 * g + r), sq = q >> 2;
-                sm.h1s[wv][q & 3][sq >> 2][col][sq & 3] = relu(c1[r]);
+            for (int r = 0; r < 4; ++r) {  // unit 16 rt + 4 g + r -> its slot in layer 2's k order
+                const int q = l2_pos(16 * rt + 4 * g + r), sq = q >> 2;
+                sm.h1s[player][q & 3][sq >> 2][col][sq & 3] = relu(c1[r]);
             }
         }
-        // the wave reads back what its own lanes wrote: LDS serves one wave's instructions in order
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();  // (A) the player's layer 1
         float bs[16];
         {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float4 v = *reinterpret_cast<const float4*>(sm.h1s[wv][g][k][col]);
+                const float4 v = *reinterpret_cast<const float4*>(sm.h1s[player][g][k][col]);
                 bs[4 * k] = v.x; bs[4 * k + 1] = v.y; bs[4 * k + 2] = v.z; bs[4 * k + 3] = v.w;
             }
         }

@@ -3,10 +3,13 @@ torch autograd (tests/golden/drqn.npz) and against the float64 oracle (oracle.dr
 
 Tolerances (fp32 on the device; exact-f32 MFMA sums in a different order than torch's CPU GEMMs):
 loss / pre-clip norm rtol 1e-4; gradients rtol 1e-3 with atol 1e-5 x the tensor's largest
-magnitude (the same bar the oracle meets against the reference); parameters after three clipped
-Adam steps: Adam normalises every element's step to ~lr = 1e-4, so an element whose gradient is
-at fp32 rounding level moves by +-lr in a direction the rounding decides — every element within
-3 steps x lr, and all but < 0.5 % within rtol 1e-5 / atol 1e-6.
+magnitude (the same bar the oracle meets against the reference). Parameters after clipped Adam
+steps, as a band check: Adam normalises every element's step to ~lr = 1e-4 x sign(m), so an element
+whose float64 gradient at some step is within the gradient tolerance of zero (|g| <= 2e-5 x the
+tensor's largest |g|: the sign is a rounding decision) may move by up to 2 lr per step the other
+way — the band, counted and printed; every other element must be within 1e-6 + 1e-5 |ref|, with no
+fraction allowed to escape. The apply itself (clip + Adam given the device's gradient and norm) is
+pinned bit for bit by test_drqn_clip_adam_exact.
 """
 import numpy as np
 import pytest
@@ -35,11 +38,31 @@ def _grads(L):
     return out
 
 
-def _assert_params(got, ref, what, steps):
-    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
-    np.testing.assert_allclose(got, ref, rtol=0, atol=steps * 1e-4 * 1.01, err_msg=what)
-    off = np.abs(got - ref) > 1e-6 + 1e-5 * np.abs(ref)
-    assert off.mean() < 0.005, f"{what}: {off.sum()} of {off.size} elements beyond 1e-6"
+BAND_REL = 2e-5  # twice the gradient check's atol (1e-5 x the tensor's largest |g|)
+
+
+def _band(grads_per_step, k):
+    """Elements of parameter k whose float64 gradient at any step is within BAND_REL x the tensor's
+    largest |g| of zero: their Adam direction is a rounding decision."""
+    band = None
+    for g in grads_per_step:
+        g = np.asarray(g[k], np.float64)
+        b = np.abs(g) <= BAND_REL * np.abs(g).max()
+        band = b if band is None else band | b
+    return band
+
+
+def _assert_params(got, ref, what, steps, band, tally=None):
+    got, ref = np.asarray(got, np.float64).reshape(-1), np.asarray(ref, np.float64).reshape(-1)
+    band = np.asarray(band).reshape(-1)
+    np.testing.assert_allclose(got[band], ref[band], rtol=0, atol=steps * 2e-4 * 1.01, err_msg=f"{what} (band)")
+    np.testing.assert_allclose(got[~band], ref[~band], rtol=1e-5, atol=1e-6, err_msg=what)
+    if tally is not None:
+        tally[0] += int(band.sum())
+        tally[1] += band.size
+        err = np.abs(got - ref) / (1e-6 + 1e-5 * np.abs(ref))
+        tally[2] = max(tally[2], float(np.max(err[~band], initial=0.0)))
+        tally[3] += int((err[band] > 1.0).sum())  # band elements that did use the band
 
 
 def _assert_grads(got, ref, what):
@@ -51,7 +74,7 @@ def _assert_grads(got, ref, what):
     print(f"\n{what}: gradient error / tolerance (rtol 1e-3, atol 1e-5 max|g|) max {worst:.4f}")
 
 
-def test_drqn_update_matches_reference(golden):
+def test_drqn_update_matches_reference(golden, orc):
     from pongmi.drqn import DRQNLearner
     gr, gd = golden("rnn"), golden("drqn")
     L = DRQNLearner(_sd(gr), batch=64, T=8)
@@ -64,9 +87,20 @@ def test_drqn_update_matches_reference(golden):
         if k == 0:
             _assert_grads(_grads(L), {k2[len("u0_grad."):]: v for k2, v in gd.items() if k2.startswith("u0_grad.")},
                           "update 0")
+    # the band: the float64 oracle's gradients of the same three updates
+    p64 = {k: v.numpy().astype(np.float64) for k, v in _sd(gr).items()}
+    adam, gsteps = {}, []
+    for k in range(3):
+        p64, info = orc.drqn_update(p64, {k2: v.numpy().astype(np.float64) for k2, v in _sd(gr).items()}, adam, k + 1,
+                                    _batch(gd, k))
+        gsteps.append(info["grads"])
     sd = L.state_dict()
+    tally = [0, 0, 0.0, 0]
     for k in (n[len("final_sub."):] for n in gd if n.startswith("final_sub.")):
-        _assert_params(sd[k].numpy().reshape(-1)[::8], gd["final_sub." + k], k, 3)
+        _assert_params(sd[k].numpy().reshape(-1)[::8], gd["final_sub." + k], k, 3, _band(gsteps, k).reshape(-1)[::8],
+                       tally)
+    print(f"\nparameters after 3 updates: {tally[0]} of {tally[1]} elements in the sign band, {tally[3]} of them "
+          f"beyond 1e-6 + 1e-5 |ref|; worst off-band error / (1e-6 + 1e-5 |ref|) {tally[2]:.4f}")
     # targetB untouched (interval 2000), epsilon buffers unchanged
     assert torch.equal(L.target_state_dict()["lstm.weight_hh_l0"], _sd(gr)["lstm.weight_hh_l0"])
     assert torch.equal(sd["fc_A.weight_epsilon"], _sd(gr)["fc_A.weight_epsilon"])
@@ -97,8 +131,11 @@ def test_drqn_against_oracle_ragged(golden, orc, B, T):
     new, _ = orc.drqn_update({k: v.astype(np.float64) for k, v in sd.items()},
                              {k: v.astype(np.float64) for k, v in tsd.items()}, {}, 1, (obs, act, rew, nxt, done))
     got = L.state_dict()
+    tally = [0, 0, 0.0, 0]
     for k in orc.RNN_PARAM_KEYS:
-        _assert_params(got[k].numpy(), new[k], k, 1)
+        _assert_params(got[k].numpy(), new[k], k, 1, _band([info["grads"]], k), tally)
+    print(f"B={B} T={T}: {tally[0]} of {tally[1]} parameters in the sign band, {tally[3]} of them beyond "
+          f"1e-6 + 1e-5 |ref|; worst off-band error / (1e-6 + 1e-5 |ref|) {tally[2]:.4f}")
 
 
 def test_drqn_deterministic_world_and_target_sync(golden):

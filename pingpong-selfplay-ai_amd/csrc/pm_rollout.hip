@@ -370,6 +370,24 @@ __global__ __launch_bounds__(kRollBlock) __attribute__((amdgpu_waves_per_eu(3, 3
 //   side by side (conflict-free ds_read_b128; the first layout, [col][64], ran 3.67 us per step).
 constexpr int kR16Block = 512;
 
+#ifdef PM_DIAG
+// k_rollout16's per-step phases (diagnostic build only): waves 0 (heads + tick) and 1 (a layer wave)
+// of block 0 add the s_memtime cycles between phase points over every step of the launch.
+static __device__ unsigned long long pm_diag_roll[2][8];
+#define ROLL_T(k)                                                                 \
+    do {                                                                          \
+        if (diag) {                                                               \
+            const unsigned long long now_ = __builtin_amdgcn_s_memtime();         \
+            dacc[(k)] += now_ - dprev;                                            \
+            dprev = now_;                                                         \
+        }                                                                         \
+    } while (0)
+#else
+#define ROLL_T(k) \
+    do {          \
+    } while (0)
+#endif
+
 // layer 2's k order: sequence position of unit u, and the unit at position q
 __device__ __forceinline__ int l2_pos(int u) {
     const int t = u >> 5, v = u & 31, b = (v >> 2) & 1, r = (v & 3) + 4 * (v >> 3);
@@ -449,6 +467,10 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const float4* im2 = reinterpret_cast<const float4*>(sm.img2[player][rt][0][lane]);
+#ifdef PM_DIAG
+    const bool diag = blockIdx.x == 0 && wv < 2;
+    unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dprev = __builtin_amdgcn_s_memtime();
+#endif
     for (int st = 0; st < steps; ++st) {
         const uint64_t ctr = counter0 + (uint64_t)st;
         if (wv == 7 && st + 1 < steps) fetch_heads_async(ws, st + 1, sm.hfB[(st + 1) & 1], lane);  // lands during the step
@@ -466,7 +488,9 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
                 sm.h1s[player][q & 3][sq >> 2][col][sq & 3] = relu(c1[r]);
             }
         }
+        ROLL_T(0);        // step start (barrier C) -> layer 1 issued
         __syncthreads();  // (A) the player's layer 1
+        ROLL_T(1);
         float bs[16];
         {
 #pragma unroll
@@ -494,7 +518,9 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             sm.c2s[player][(u >> 2) & 1][q >> 2][col][q & 3] = relu(c2[r]);
         }
         if (wv == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next step's heads landed
+        ROLL_T(2);        // layer 2 + staging
         __syncthreads();  // (B) both players' layer 2
+        ROLL_T(3);
         if (wv == 0) {
             // heads: lane 32 hp + 16 hh + col runs half hh's four chains of player hp, column col
             const int hp = lane >> 5, hh = (lane >> 4) & 1;
@@ -530,6 +556,7 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
                 if (u53(rr.x, rr.y) < eps) act = (int)below(rr.z, 3u);
             }
             const int aA = __shfl(act, col), aB = __shfl(act, 32 + col);
+            ROLL_T(4);    // heads + actions
             float sB[7];  // the step's observation of B (memory.push's s)
 #pragma unroll
             for (int k = 0; k < 7; ++k) sB[k] = sm.ob[1][col][k];
@@ -569,9 +596,16 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             if (g < 2)
 #pragma unroll
                 for (int k = 0; k < 7; ++k) sm.ob[g][col][k] = g ? oB[k] : oA[k];
+            ROLL_T(5);    // tick (+ push) + next observations
         }
         __syncthreads();  // (C) the next observations
+        ROLL_T(6);
     }
+#ifdef PM_DIAG
+    if (diag && lane == 0)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pm_diag_roll[wv][k] = k < 7 ? dacc[k] : (unsigned long long)steps;
+#endif
     if (wv == 0 && g == 0 && valid) {
         store_arena(s, i, a);
         float oA[7], oB[7];
@@ -668,6 +702,12 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
     PM_LAUNCHED("k_rollout");
     return PM_OK;
 }
+
+#ifdef PM_DIAG
+extern "C" int pm_diag_read_roll(uint64_t* out) {  // [2][8]: waves 0 / 1 of block 0, cycles per phase, [7] steps
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_roll), sizeof(pm_diag_roll));
+}
+#endif
 
 extern "C" int pm_rollout(const pm_env_params* p, const pm_env_state* s, const float* wA, const float* wB,
                           const float* paramsB, float epsilon, uint64_t seed_env, uint64_t seed_net, uint64_t counter0,

@@ -11,6 +11,7 @@ timeout -k 10 300 python3 bench.py --workload infer --no-cpu-baseline > gpurun_o
 python3 -c "
 import json; d=json.load(open('gpurun_out/r4m_infer.json')); print('infer', d['value'], d['roofline']['avg_us_per_step'], d['roofline']['frac'])" &&
 timeout -k 10 120 python3 tools/stamps.py > gpurun_out/r4m_stamps.txt 2>&1 && echo STAMPS_OK &&
-timeout -k 10 120 python3 tools/multi_stamps.py > gpurun_out/r4m_multi_stamps.txt 2>&1 && echo MULTI_OK || exit 1
+timeout -k 10 120 python3 tools/multi_stamps.py > gpurun_out/r4m_multi_stamps.txt 2>&1 && echo MULTI_OK &&
+timeout -k 10 120 python3 tools/roll_stamps.py > gpurun_out/r4m_roll_stamps.txt 2>&1 && echo ROLL_OK && cat gpurun_out/r4m_roll_stamps.txt || exit 1
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_drqn.py -q -x -s --timeout 200 --timeout-method thread \
     > gpurun_out/r4m_drqn.log 2>&1; rc=$?; tail -n 2 gpurun_out/r4m_drqn.log; grep -E "band|gradient error" gpurun_out/r4m_drqn.log; exit $rc

@@ -1,27 +1,25 @@
 // K6 — the DRQN update (train_step_rnn, scripts/train_rnn_iterative.py:400-531) on the device.
 //
-// Four launches per update, every matrix product on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32):
+// Four launches per update; the batched products on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32), the
+// per-sequence recurrence on the f32 VALU (same 32 fmaf / cycle / SIMD as the f32 MFMA on gfx950):
 //
 //   k_dq_embed  (grads 1/3) the batch through the feature layers and the LSTM input projection for
 //               all three streams (modelB on obs, modelB on next, targetB on next): per (stream,
 //               32-column tile, time step) F1 = ReLU(W1 x + b1), F2 = ReLU(W2 F1 + b2) and
-//               Zx = Wih F2 + bih + bhh, Zx written in the accumulator layout the recurrence starts
-//               from; the obs stream's F1 / F2 kept for the weight gradients.
-//   k_dq_recur  (grads 2/3) the whole recurrence, persistent: every (stream, column tile) is a group
-//               of 16 workgroups, workgroup m owning LSTM units 8m..8m+7 (all four gates: one 32-row
-//               MFMA tile, its Whh rows in registers, K split over the 4 waves). Per time step the
-//               group exchanges h through write-through (sc1) stores + a per-workgroup step flag
-//               (MI355X_MICROARCH.md hand-off table, row 1), the cell state never leaves registers.
-//               Then the heads: each workgroup computes its 8 rows of the shared head and their
-//               partial V / A; the obs stream's group gathers all three streams' partial Q, forms the
-//               double-DQN target, smooth-L1 and dQ, the head gradients of its rows, and starts BPTT
-//               from dh_T = W_S^T dS; per BPTT step dz in registers (gates and c saved by the
-//               forward), dh_{t-1} = Whh^T dz as per-workgroup partials exchanged the same way.
+//               Zx = Wih F2 + bih + bhh, Zx written [stream][t][gate row][sequence]; the obs stream's
+//               F1 / F2 kept for the weight gradients; the effective head weights of modelB (train
+//               mode) and targetB (eval mode) for the recurrence's heads.
+//   k_dq_recur  (grads 2/3) the recurrence, one 1024-thread workgroup per sequence (modelB: obs and
+//               next as two columns; targetB: two sequences' next), Whh in registers, no per-step
+//               hand-off between CUs: forward, heads, the double-DQN target (targetB's Q(s_T) is the
+//               one granule hand-off), smooth-L1 and dQ, dS, dh_T = W_S^T dS and BPTT with
+//               dh_{t-1} = Whh^T dz summed in a fixed order through LDS.
 //   k_dq_wgrad  (grads 3/3) the weight gradients: dWih = dZ F2^T, dWhh = dZ H^T and the biases over
-//               all T*B columns (one workgroup per 32x32 output tile, K split over 16 waves); per
-//               32-column tile dF2 = Wih^T dZ -> ReLU mask -> dW2 / db2 partials -> dF1 = W2^T dP2
-//               -> dW1 / db1 partials, summed in a fixed order by the last tile to finish (arrival
-//               ticket); the head gradient partials of the column tiles summed likewise.
+//               all T*B columns, dW_S = dS h_T^T and db_S over the B sequences (one workgroup per
+//               32x32 output tile, K split over 16 waves); per 32-column tile dF2 = Wih^T dZ -> ReLU
+//               mask -> dW2 / db2 partials -> dF1 = W2^T dP2 -> dW1 / db1 partials, summed in a fixed
+//               order by the last tile to finish (arrival ticket); the V / A head gradients summed
+//               over the sequences in order.
 //   k_drqn_apply (pm_drqn_apply) the NoisyLinear sigma gradients (mu gradient x epsilon), the global-
 //               norm clip (fp64 partials met on an arrival ticket, summed in block order) and torch's
 //               Adam, target sync: four launches per update in all.
@@ -34,14 +32,12 @@
 namespace pm {
 namespace {
 
-constexpr int kG = 16;           // workgroups per recurrence group (8 LSTM units each)
+constexpr int kRecThreads = 1024;  // k_dq_recur workgroup: thread 8u + kg = (LSTM unit u, K eighth kg)
 constexpr int kNormBlocks = 256;  // k_drqn_apply blocks (fp64 norm partials, summed in block order)
-constexpr int kWgA = 128;        // k_dq_wgrad: dWih / dWhh output tiles
-constexpr int kWgC = 4;          // k_dq_wgrad: head-partial reduce workgroups
-constexpr int kLowN = 8832;      // grad [0, kLowN): W1, b1, W2, b2 (the column-tile partials)
-// per-column-tile head gradient partials (floats)
-enum : int { HP_WS = 0, HP_BS = 16384, HP_V = 16512, HP_VB = 16640, HP_A = 16641, HP_AB = 17025, HP_N = 17028 };
-constexpr int kHpStride = 17088;  // HP_N rounded up to 64
+constexpr int kWsStride = 132;   // row stride (floats) of the effective shared-head W image (WSE, LDS)
+constexpr int kHwN = 704;        // HWE per net: b_S, w_V, w_A (3 x 128), b_V, b_A (3), padded
+enum : int { HW_BS = 0, HW_V = 128, HW_A = 256, HW_VB = 640, HW_AB = 641 };
+enum : int { SC_DV = 0, SC_DA = 1, SC_LOSS = 4, SC_Q = 5 };  // SC [B][8]: per-sequence head scalars
 
 struct DqArgs {
     int B, T, nct, C0;
@@ -54,19 +50,23 @@ struct DqArgs {
     pm_drqn_stats* stats;
     const int32_t* enable;
     float gamma;
-    float *ZX;   // [3][nct][T][16][1024]     Zx in the recurrence's accumulator layout
-    float *HS;   // [3][nct][T+1][32][128] x2 h_t granules {value, tag} (the hand-off slots; slot 0 unused)
+    float *ZX;   // [3][T][512][B]            Zx = Wih F2 + bih + bhh per (stream, step, gate row, sequence)
     float *F1T;  // [64][C0]                  obs stream F1 (column c = t*B + b)
     float *F2T;  // [128][C0]                 obs stream F2
     float *H;    // [128][C0]                 obs stream h_t, the input hidden of step t
-    float *GS;   // [nct][T][16][64][16]      obs stream activated gates, wave-0 lane layout
-    float *CS;   // [nct][T][16][64][4]       obs stream c_{t+1}
+    float *GC;   // [B][T][5][128]            obs stream activated gates i, f, g, o and c_{t+1} (BPTT scratch)
     float *dZ;   // [512][C0]
-    float *QP;   // [3][nct][16][32][4] x2    partial (V, A0, A1, A2) granules of each workgroup's 8 head rows
-    float *DHP;  // [nct][T][16][32][128] x2  slot t: per-workgroup partial granules of dh_{t+1}
-    float *HP;   // [nct][kHpStride]          head gradient partials per column tile
-    float *LP;   // [nct][4]                  loss / q sums per column tile
-    float *W2P;  // [C0 / 32][kLowN]          W1 / b1 / W2 / b2 gradient partials per column tile
+    float *QT;   // [B][4] x2                 targetB's Q(s_T) per sequence, granules {value, tag}
+    float *DS;   // [128][B]                  obs stream dS (ReLU-masked shared-head gradient)
+    float *SR;   // [128][B]                  obs stream ReLU(S)
+    float *HT;   // [128][B]                  obs stream h_T
+    float *SC;   // [B][8]                    dV, dA0..2, loss, Q(s, a)
+    float *WSE;  // [2][128][kWsStride]       effective W_S of modelB (train mode) and targetB (eval)
+    float *HWE;  // [2][kHwN]                 their effective head vectors
+    float *DZH;  // [B][T][128][4] x2         obs stream dz granules {value, tag}, BPTT -> the dF2 trailer
+    float *dP2;  // [128][C0]                 dF2 through F2's ReLU
+    float *dP1;  // [64][C0]                  dF1 through F1's ReLU
+    float *XT;   // [32][C0]                  obs stream inputs x^T (rows 7..31 zero)
     double* part;
     int64_t* tstep;
     int32_t* flags;  // [0] update epoch (the granule tag base), [1] k_dq_wgrad's ticket, [2] k_drqn_apply's
@@ -87,18 +87,19 @@ struct DqLayout {
 inline int64_t dq_layout(int B, int T, DqArgs* a, void* work) {
     const int64_t nct = B / 32, C0 = (int64_t)T * B;
     DqLayout L;
-    const int64_t oZX = L.add(3 * nct * T * 16 * 1024), oHS = L.add(3 * nct * (T + 1) * 8192), oF1 = L.add(64 * C0),
-                  oF2 = L.add(128 * C0), oH = L.add(128 * C0), oGS = L.add(nct * T * 16 * 1024),
-                  oCS = L.add(nct * T * 16 * 256), odZ = L.add(512 * C0), oQP = L.add(3 * nct * 16 * 256),
-                  oDHP = L.add(nct * T * 16 * 8192), oHP = L.add(nct * kHpStride), oLP = L.add(nct * 4),
-                  oW2P = L.add(C0 / 32 * kLowN), oPart = L.add(2 * kNormBlocks), oTs = L.add(4),
+    const int64_t oZX = L.add(3 * C0 * 512), oF1 = L.add(64 * C0), oF2 = L.add(128 * C0), oH = L.add(128 * C0),
+                  oGC = L.add(C0 * 5 * 128), odZ = L.add(512 * C0), oQT = L.add((int64_t)B * 8),
+                  oDS = L.add(128 * (int64_t)B), oSR = L.add(128 * (int64_t)B), oHT = L.add(128 * (int64_t)B),
+                  oSC = L.add((int64_t)B * 8), oWSE = L.add(2 * 128 * kWsStride), oHWE = L.add(2 * kHwN),
+                  oDZH = L.add(C0 * 1024), odP2 = L.add(128 * C0), odP1 = L.add(64 * C0),
+                  oXT = L.add(32 * C0), oPart = L.add(2 * kNormBlocks), oTs = L.add(4),
                   oFl = L.add(4);
     if (a && work) {
         float* w = static_cast<float*>(work);
         a->B = B; a->T = T; a->nct = (int)nct; a->C0 = (int)C0;
-        a->ZX = w + oZX; a->HS = w + oHS; a->F1T = w + oF1; a->F2T = w + oF2; a->H = w + oH; a->GS = w + oGS;
-        a->CS = w + oCS; a->dZ = w + odZ; a->QP = w + oQP; a->DHP = w + oDHP; a->HP = w + oHP; a->LP = w + oLP;
-        a->W2P = w + oW2P; a->part = reinterpret_cast<double*>(w + oPart);
+        a->ZX = w + oZX; a->F1T = w + oF1; a->F2T = w + oF2; a->H = w + oH; a->GC = w + oGC; a->dZ = w + odZ;
+        a->QT = w + oQT; a->DS = w + oDS; a->SR = w + oSR; a->HT = w + oHT; a->SC = w + oSC; a->WSE = w + oWSE;
+        a->HWE = w + oHWE; a->DZH = w + oDZH; a->dP2 = w + odP2; a->dP1 = w + odP1; a->XT = w + oXT; a->part = reinterpret_cast<double*>(w + oPart);
         a->tstep = reinterpret_cast<int64_t*>(w + oTs); a->flags = reinterpret_cast<int32_t*>(w + oFl);
     }
     return L.total * 4;
@@ -117,6 +118,9 @@ inline int64_t dq_layout(int B, int T, DqArgs* a, void* work) {
     } while (0)
 #endif
 __device__ __forceinline__ bool skipped(const DqArgs& a) { return a.enable && *a.enable == 0; }
+__device__ __forceinline__ float eff_w(const float* P, int mu, int sg, int ep, bool noisy) {
+    return noisy ? P[mu] + P[sg] * P[ep] : P[mu];  // NoisyLinear: mu + sigma * epsilon (train), mu (eval)
+}
 
 // ---------------------------------------------------------------- hand-off primitives
 // In-launch hand-offs move data-tagged granules (MI355X_MICROARCH.md, R2 / handoff-1to1): each
@@ -133,10 +137,6 @@ struct HandoffCtl {
     int limit;     // polls per hand-off before it counts as timed out
 };
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// 4-byte write-through store / L2-coherent load (sc1), for the column-tile partials handed to the
-// workgroups that sum them within the same launch (hand-off table row 1: sc1 on both sides)
-__device__ __forceinline__ void st_wt(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ float ld_wt(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 // two granules {v0, tag}, {v1, tag} with one 16-byte write-through store
 __device__ __forceinline__ void st_g2(__amdgpu_buffer_rsrc_t r, int byte_off, float v0, float v1, uint32_t tag) {
@@ -226,6 +226,24 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
         a.grad[PM_RNN_NPARAM] = 1.0f;      // this replica contributes
         a.grad[PM_RNN_NPARAM + 1] = 0.0f;  // no hand-off has timed out (yet) in this update
     }
+    // the effective head weights the recurrence's workgroups read (modelB in train mode: mu + sigma *
+    // epsilon; targetB in eval mode: mu), W_S in the padded row image k_dq_recur copies to LDS
+    for (int i = blockIdx.x * 256 + tid; i < 2 * (16384 + 644); i += gridDim.x * 256) {
+        const int n = i >= 16384 + 644, j = i - n * (16384 + 644);
+        const float* Pn = n ? a.target : a.params;
+        if (j < 16384) {
+            a.WSE[(n * 128 + (j >> 7)) * kWsStride + (j & 127)] = eff_w(Pn, R_P_SWMU + j, R_P_SWSG + j, R_P_SWEP + j, !n);
+        } else {
+            const int v = j - 16384;  // b_S 128 | w_V 128 | w_A 384 | b_V | b_A 3
+            int mu, sg, ep;
+            if (v < 128) { mu = R_P_SBMU + v; sg = R_P_SBSG + v; ep = R_P_SBEP + v; }
+            else if (v < 256) { mu = R_P_VWMU + v - 128; sg = R_P_VWSG + v - 128; ep = R_P_VWEP + v - 128; }
+            else if (v < 640) { mu = R_P_AWMU + v - 256; sg = R_P_AWSG + v - 256; ep = R_P_AWEP + v - 256; }
+            else if (v == 640) { mu = R_P_VBMU; sg = R_P_VBSG; ep = R_P_VBEP; }
+            else { mu = R_P_ABMU + v - 641; sg = R_P_ABSG + v - 641; ep = R_P_ABEP + v - 641; }
+            a.HWE[n * kHwN + v] = eff_w(Pn, mu, sg, ep, !n);
+        }
+    }
     __shared__ __attribute__((aligned(16))) float F2s[32][132];
     DQ_STAMP(220, blockIdx.x == 0);
     const float* P = s == 2 ? a.target : a.params;
@@ -283,8 +301,10 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
     for (int i = 0; i < 4; ++i)
         *reinterpret_cast<float4*>(&F2s[col][32 * w + 8 * i + 4 * h]) =
             make_float4(f2[4 * i], f2[4 * i + 1], f2[4 * i + 2], f2[4 * i + 3]);
-    if (s == 0 && rq == 0) {  // the obs stream's features for the weight gradients, [unit][column]
+    if (s == 0 && rq == 0) {  // the obs stream's features and inputs for the weight gradients, [unit][column]
         const int64_t C0 = a.C0;
+        if (w == 0 && h == 0)
+            for (int i = 0; i < 7; ++i) a.XT[(int64_t)i * C0 + c] = a.obs[((int64_t)b * T + t) * 7 + i];
 #pragma unroll
         for (int r = 0; r < 16; ++r) a.F2T[(int64_t)(32 * w + rho(r) + 4 * h) * C0 + c] = f2[r];
         if (w < 2)
@@ -308,432 +328,409 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
         z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, bv.z, z, 0, 0, 0);
         z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, bv.w, z, 0, 0, 0);
     }
-    float4* zx = reinterpret_cast<float4*>(a.ZX + ((((int64_t)s * nct + ct) * T + t) * 16 + m) * 1024) + lane;
+    // Zx[s][t][gate row][sequence]: a register's 32 columns are 128 contiguous bytes
+    float* zx = a.ZX + ((int64_t)s * T + t) * 512 * B + b;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) zx[64 * i] = make_float4(z[4 * i], z[4 * i + 1], z[4 * i + 2], z[4 * i + 3]);
+    for (int r = 0; r < 16; ++r) {
+        const int rr = rho(r) + 4 * h;
+        zx[(int64_t)(128 * (rr >> 3) + 8 * m + (rr & 7)) * B] = z[r];
+    }
     DQ_STAMP(222, blockIdx.x == 0);
 }
 
-// ---------------------------------------------------------------- 2: the recurrence (persistent)
+// ---------------------------------------------------------------- 2: the recurrence (sequence-private)
+// One workgroup of 1024 threads owns whole sequences: the recurrence h_{t+1} = f(Zx_t + Whh h_t) of a
+// sequence never leaves its CU, so no step waits on another CU (round 3 split the 512 gate rows over
+// 16 workgroups and paid a cross-CU hand-off per step: 2T + 3 hops of ~3 us). Whh (512 x 128, 256 KB)
+// lives in the workgroup's registers: thread 8u + kg holds rows 128q + u (the four gates of LSTM unit
+// u) x columns 16kg .. 16kg + 15, 64 floats. On gfx950 the f32 VALU issues 32 fmaf per cycle per
+// SIMD, the same rate as the f32 MFMA, so a matrix-vector step on the VALU loses nothing to the
+// matrix cores and needs no 16- or 32-column tile.
+//   forward  per step: 16 fmaf per gate per column from h in LDS, the K eighths summed by a DPP
+//            butterfly (every lane of the unit ends with the sums), the cell on the lanes of its
+//            column, h back to LDS: one barrier per step.
+//   heads    S = W_S h_T (W_S rows in registers from an LDS image), V / A, Q.
+//   BPTT     per step: dz from the saved gates, dh_{t-1} = Whh^T dz as 16 partials per thread, summed
+//            over the wave's unit pairs (DPP row_ror 8), then over the 64 (wave, row) sets through LDS
+//            in a fixed order: one barrier per step.
+// Workgroups [0, B/2): targetB on `next`, sequences 2j and 2j + 1 (two columns); [B/2, B/2 + B):
+// modelB on `obs` (column 0, the one BPTT runs on) and on `next` (column 1) of sequence b. The only
+// cross-workgroup hand-off is targetB's Q(s_T) (one granule pair per sequence, tag E + 1); the
+// target workgroups come first in the grid, so they are resident before any workgroup polls them.
 struct RecurSmem {
-    float red[2][4][16][64];  // the waves' partial accumulators, by step parity: a wave gathers its next
-                              // h from other workgroups and may write a step ahead of a slower wave's read
-    __attribute__((aligned(16))) float dzs[4][64][4];  // BPTT: wave 0's dz fragments for the other waves
-    __attribute__((aligned(16))) float hT[32][132];  // h_T of this column tile [column][unit]
-    float dS[8][32];                                 // dS of this workgroup's 8 shared-head rows
-    float ws[8][128];                                // those rows of the effective W_S
-    __attribute__((aligned(16))) float qs[3][32][4]; // the three streams' summed V / A per column
-    __attribute__((aligned(16))) float dhs[4][64][4];  // BPTT: each wave's sum of 4 producers' dh partials
+    __attribute__((aligned(16))) float ws[128 * kWsStride];  // effective W_S (DMA image of WSE)
+    __attribute__((aligned(16))) float part[2][128][68];     // W^T dz partials [k][set, swizzled], by parity
+    __attribute__((aligned(16))) float hs[2][288];           // h [unit][column], 4 floats of pad per 16 units
+    float sr[2][128];                                        // ReLU(S) per column
+    float qv[2][4];                                          // V, A0..2 per column
+    float dva[4];                                            // dV, dA0..2
 };
 
-__device__ __forceinline__ float eff_w(const float* P, int mu, int sg, int ep, bool noisy) {
-    return noisy ? P[mu] + P[sg] * P[ep] : P[mu];  // NoisyLinear: mu + sigma * epsilon (train), mu (eval)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// sum over the 8 lanes of a unit (lanes 8i .. 8i + 7): quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror; every step adds two equal-order partial sums, so all 8 lanes get the same bits
+__device__ __forceinline__ float sum8(float v) {
+    v += dppf<0xB1>(v);
+    v += dppf<0x4E>(v);
+    v += dppf<0x141>(v);
+    return v;
+}
+__device__ __forceinline__ int hidx(int k) { return 2 * k + 4 * (k >> 4); }  // hs[.][hidx(k) + column]
+
+// p[j] (this thread's partial of output k = 16 kg + j over its unit) summed over all 128 units; the
+// caller's thread (u, kg) gets output u. Wave w's lanes hold units 8w .. 8w + 7 (lane 8i + kg); row r
+// of the wave (16 lanes) holds units 2r, 2r + 1, summed by row_ror 8, giving set 4w + r of 64. The
+// set is stored at column (set + 4 (k >> 4)) & 63 of row k: conflict-free stores, and a reader's 8
+// sets stay two aligned float4s.
+__device__ __forceinline__ float reduce_units(float (&p)[16], float (*part)[68], int lane, int w, int u, int kg) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) p[j] += dppf<0x128>(p[j]);
+    if ((lane & 8) == 0) {
+        const int col = (4 * w + (lane >> 4) + 4 * kg) & 63;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) part[16 * kg + j][col] = p[j];
+    }
+    __syncthreads();
+    const int sw = 4 * (u >> 4);
+    const float4 v0 = *reinterpret_cast<const float4*>(&part[u][(8 * kg + sw) & 63]);
+    const float4 v1 = *reinterpret_cast<const float4*>(&part[u][(8 * kg + 4 + sw) & 63]);
+    const float d = ((((((v0.x + v0.y) + v0.z) + v0.w) + v1.x) + v1.y) + v1.z) + v1.w;
+    return sum8(d);
 }
 
-// Slot layouts (granules, 8 B each):
-//   HS  [grp][T+1][32 col][128 unit]   h_t of a (stream, column tile) group, tag E + t
-//   QP  [grp][16 m][32 col][4]         the V / A partials of workgroup m's 8 shared-head rows, tag E + 1
-//   DHP [ct][T][16 m][32 col][128]     workgroup m's partial of dh_{t+1} (slot t), tag E + t + 1
-__global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
+// The dF2 trailer (workgroups [2B, 3B), one per sequence): the feature layers' backward of the obs
+// stream, dF2_t = Wih^T dz_t, dP2 = dF2 (F2 > 0), then dF1 = W2^T dP2, dP1 = dF1 (F1 > 0) (k_dq_wgrad
+// forms dW2 = dP2 F1^T and dW1 = dP1 x^T as tiles). Wih sits in registers in Whh's fragment layout,
+// so dF2_t is BPTT's dh product on another matrix; each dz_t arrives from the sequence's obs
+// workgroup as granules (tag E + 2 + t) while that workgroup moves on, so the pass trails BPTT by a
+// hand-off instead of following it. It waits only on lower-indexed workgroups (dispatched first).
+__device__ __forceinline__ void dq_df2(const DqArgs& a, RecurSmem& sm, int b, uint32_t E, const HandoffCtl& hc) {
+    const int T = a.T, B = a.B;
+    const int64_t C0 = a.C0;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, u = tid >> 3, kg = tid & 7;
+    DQ_STAMP(8, b == 0);
+    float wr[4][16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4* src = reinterpret_cast<const float4*>(a.params + R_P_WIH + (int64_t)(128 * q + u) * 128 + 16 * kg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float4 v = src[i];
+            wr[q][4 * i] = v.x; wr[q][4 * i + 1] = v.y; wr[q][4 * i + 2] = v.z; wr[q][4 * i + 3] = v.w;
+        }
+    }
+    float* p2s = sm.ws;  // [T][128] dP2 of the sequence (row t read by the dF1 pass one step later)
+    const char* dzh = reinterpret_cast<const char*>(a.DZH) + (int64_t)b * T * 128 * 32;
+    const int j1 = tid >> 4, k16 = tid & 15;  // dF1: row j1, F2 rows 8 k16 .. 8 k16 + 7
+    float w2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w2[i] = a.params[R_P_F2W + (8 * k16 + i) * 64 + j1];
+    // dF1 of step t from the LDS dP2 row, summed over the 16 lanes of the row; lane k16 = 0 stores dP1
+    auto df1_row = [&](int t, float f1m) {
+        const float4 p0 = *reinterpret_cast<const float4*>(&p2s[t * 128 + 8 * k16]);
+        const float4 p1 = *reinterpret_cast<const float4*>(&p2s[t * 128 + 8 * k16 + 4]);
+        float v = w2[0] * p0.x;
+        v = fmaf(w2[1], p0.y, v);
+        v = fmaf(w2[2], p0.z, v);
+        v = fmaf(w2[3], p0.w, v);
+        v = fmaf(w2[4], p1.x, v);
+        v = fmaf(w2[5], p1.y, v);
+        v = fmaf(w2[6], p1.z, v);
+        v = fmaf(w2[7], p1.w, v);
+        v = sum8(v);
+        v += dppf<0x128>(v);  // + the other 8 lanes of the 16-lane row
+        if (k16 == 0) a.dP1[(int64_t)j1 * C0 + (int64_t)t * B + b] = f1m > 0.f ? v : 0.f;
+    };
+    float f1p = 0.f;
+    for (int t = T - 1; t >= 0; --t) {
+        const int64_t cc = (int64_t)t * B + b;
+        const float f2 = a.F2T[(int64_t)u * C0 + cc];
+        const float f1 = a.F1T[(int64_t)j1 * C0 + cc];
+        const uint32_t tag = E + 2 + (uint32_t)t;
+        const int off[2] = {(t * 128 + u) * 32, (t * 128 + u) * 32 + 16};
+        float dz[4];
+        {   // one read of the unit's granules first: when the trailer runs behind BPTT they are there;
+            // otherwise lane 0 waits on the last granule of the wave's units (one store instruction of
+            // the producer's wave w) and the wave reads them again
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint64_t* p = reinterpret_cast<const uint64_t*>(dzh + off[i]);
+                const uint64_t q0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t q1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = ok && (uint32_t)(q0 >> 32) == tag && (uint32_t)(q1 >> 32) == tag;
+                dz[2 * i] = __uint_as_float((uint32_t)q0);
+                dz[2 * i + 1] = __uint_as_float((uint32_t)q1);
+            }
+            if (!__all(ok)) {
+                poll_tags(dzh, ((t * 128 + 8 * w + 7) * 4 + 3) * 8, 1, tag, hc);
+                gather<2, false>(dzh, off, tag, dz, hc);
+            }
+        }
+        float p[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) p[j] = fmaf(wr[3][j], dz[3], fmaf(wr[2][j], dz[2], fmaf(wr[1][j], dz[1], wr[0][j] * dz[0])));
+        const float d = reduce_units(p, sm.part[t & 1], lane, w, u, kg);  // its barrier publishes p2s row t + 1
+        DQ_STAMP(180 + t, b == 0 && t < 20);
+        if (t + 1 < T) df1_row(t + 1, f1p);
+        f1p = f1;
+        const float d2 = f2 > 0.f ? d : 0.f;
+        if (kg == 0) {
+            a.dP2[(int64_t)u * C0 + cc] = d2;
+            p2s[t * 128 + u] = d2;
+        }
+    }
+    __syncthreads();
+    df1_row(0, f1p);
+    DQ_STAMP(7, b == 0);
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
     if (skipped(a)) return;
     __shared__ RecurSmem sm;
-    const int nct = a.nct, T = a.T, B = a.B;
-    int bid = blockIdx.x;
-    const int m = bid & 15;
-    bid >>= 4;
-    const int ct = bid % nct, so = bid / nct;
-    const int s = so == 2 ? 0 : so + 1;  // the next-state streams first: the obs stream's group waits for them
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
-    const bool noisy = s != 2;  // modelB in train mode, targetB in eval mode
-    const float* P = s == 2 ? a.target : a.params;
+    const int T = a.T, B = a.B;
     const int64_t C0 = a.C0;
-    const int bcol = ct * 32 + col;
-    const int grp = s * nct + ct;
-    const uint32_t E = (uint32_t)a.flags[0] << 7;  // this update's tag base (T + 1 < 128)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, u = tid >> 3, kg = tid & 7, myc = kg & 1;
+    const int role = (int)blockIdx.x / B;  // 0 targetB on next, 1 modelB on obs + next, 2 the dF2 trailer
+    const int b = (int)blockIdx.x - role * B;
+    const uint32_t E = (uint32_t)a.flags[0] << 7;  // this update's tag base
     const HandoffCtl hc{a.stats, a.grad + PM_RNN_NPARAM + 1, hand_limit(a.poll_limit)};
-    [[maybe_unused]] const bool so0 = s == 0 && ct == 0 && m == 0, s10 = blockIdx.x == 0;  // stamping blocks (diag)
+    [[maybe_unused]] const bool so0 = (int)blockIdx.x == B, s10 = blockIdx.x == 0;  // stamping blocks (diag)
+    if (role == 2) {
+        dq_df2(a, sm, b, E, hc);
+        return;
+    }
+    const bool tgt = role == 0;
+    const int sc0 = tgt ? 2 : 0, sc1 = tgt ? 2 : 1;  // column 1 of a target workgroup repeats column 0
+    const float* P = tgt ? a.target : a.params;
+    const int net = tgt ? 1 : 0;
     DQ_STAMP(1, so0);
     DQ_STAMP(111, s10);
-    float* HSg = a.HS + (int64_t)grp * (T + 1) * 8192;
-    // this wave's Whh fragments: row 128 q + 8m + j of lane row col (q = col >> 3, j = col & 7), K quarter w
-    float wa[16];
+    // the effective W_S image -> LDS (global_load_lds, 1 KB per wave instruction), lands during the forward
     {
-        const float* wr = P + R_P_WHH + (int64_t)(128 * (col >> 3) + 8 * m + (col & 7)) * 128 + 32 * w + 4 * h;
+        const float* src = a.WSE + (int64_t)net * 128 * kWsStride;
+        for (int k = w; k < 128 * kWsStride / 256; k += 16)
+            __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane), (lds_void*)&sm.ws[256 * k], 16, 0, 0);
+    }
+    // Whh rows 128q + u, columns 16kg .. 16kg + 15
+    float wr[4][16];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float4 v = *reinterpret_cast<const float4*>(wr + 8 * j);
-            wa[4 * j] = v.x; wa[4 * j + 1] = v.y; wa[4 * j + 2] = v.z; wa[4 * j + 3] = v.w;
+    for (int q = 0; q < 4; ++q) {
+        const float4* src = reinterpret_cast<const float4*>(P + R_P_WHH + (int64_t)(128 * q + u) * 128 + 16 * kg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float4 v = src[i];
+            wr[q][4 * i] = v.x; wr[q][4 * i + 1] = v.y; wr[q][4 * i + 2] = v.z; wr[q][4 * i + 3] = v.w;
         }
     }
-    if (s == 0)  // the obs stream's rows of modelB's effective W_S (for dh_T), published by a later barrier
-        for (int k = tid; k < 8 * 128; k += 256) {
-            const int u = 8 * m + (k >> 7), kk = k & 127, o = u * 128 + kk;
-            sm.ws[k >> 7][kk] = eff_w(a.params, R_P_SWMU + o, R_P_SWSG + o, R_P_SWEP + o, true);
-        }
-    // the K-quarter slot offsets of this lane: units 32w + 8j + 4h + {0..3} of column col
-    int hoff[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        hoff[2 * j] = (col * 128 + 32 * w + 8 * j + 4 * h) * 8;
-        hoff[2 * j + 1] = hoff[2 * j] + 16;
-    }
-    // Zx of this wave's unit e = w (registers 4q + w of the tile, one float of each float4 chunk q)
-    const float* zx = a.ZX + ((int64_t)grp * T * 16 + m) * 1024 + lane * 4 + w;
-    float c1 = 0.f;  // c of unit 8m + 4h + w, column col (each wave owns one unit per lane half)
+    // Zx of this lane's column (the cell runs on the lanes of its column only)
+    const float* zx = a.ZX + (int64_t)(myc ? sc1 : sc0) * T * 512 * B + (int64_t)u * B + b;
     float zn[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) zn[q] = zx[q * 256];
+    for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)q * 128 * B];
     // ---------------- forward
+    float cst = 0.f;  // c of (unit u, column myc)
     for (int t = 0; t < T; ++t) {
-        float z[4] = {zn[0], zn[1], zn[2], zn[3]};
-        if (t + 1 < T)
+        float z[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)(t + 1) * 16 * 1024 + q * 256];
-        if (t > 0) {
-            float hv[16];
-            int off[8];
+        for (int q = 0; q < 4; ++q) z[q] = zn[q];
+        if (t + 1 < T) {
+            const int64_t o = (int64_t)(t + 1) * 512 * B;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) off[i] = hoff[i] + t * 32 * 128 * 8;
-            // lanes 0..3 wait for the last granule of this wave's 4 producers, then the K quarter is read once
-            poll_tags(HSg, ((t * 32 + 31) * 128 + 8 * (4 * w + (lane & 3)) + 7) * 8, 4, E + t, hc);
-            gather<8, false>(HSg, off, E + t, hv, hc);  // h_t of the group, this wave's K quarter
-            DQ_STAMP(160 + t, so0 && t < 10);
-            f32x16 acc = {};
-#pragma unroll
-            for (int k = 0; k < 16; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[k], hv[k], acc, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sm.red[t & 1][w][r][lane] = acc[r];
-            __syncthreads();
-            DQ_STAMP(170 + t, so0 && t < 10);
-            // unit e = w: gate q is register 4q + w of every wave's partial
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                z[q] = (((z[q] + sm.red[t & 1][0][4 * q + w][lane]) + sm.red[t & 1][1][4 * q + w][lane]) +
-                        sm.red[t & 1][2][4 * q + w][lane]) + sm.red[t & 1][3][4 * q + w][lane];
+            for (int q = 0; q < 4; ++q) zn[q] = zx[o + (int64_t)q * 128 * B];
         }
-        // the cell of unit 8m + 4h + w (v_exp_f32 / v_rcp_f32 activations, a few ulp)
-        const float gi = sig_hw(z[0]), gf = sig_hw(z[1]), gg = tanh_hw(z[2]), go = sig_hw(z[3]);
-        c1 = gf * c1 + gi * gg;  // cy = forgetgate * cx + ingate * cellgate
-        const float hn = go * tanh_hw(c1);
-        __hip_atomic_store(reinterpret_cast<uint64_t*>(HSg) + ((t + 1) * 32 + col) * 128 + 8 * m + 4 * h + w,
-                           ((uint64_t)(E + t + 1) << 32) | __float_as_uint(hn), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        float g4[4];
+        if (t > 0) {
+            float acc[4][2];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { acc[q][0] = 0.f; acc[q][1] = 0.f; }
+            const float* hp = &sm.hs[t & 1][36 * kg];  // units 16kg .. 16kg + 15, both columns
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float4 hv = *reinterpret_cast<const float4*>(hp + 4 * i);  // (k, c0) (k, c1) (k+1, c0) (k+1, c1)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    acc[q][0] = fmaf(wr[q][2 * i], hv.x, acc[q][0]);
+                    acc[q][1] = fmaf(wr[q][2 * i], hv.y, acc[q][1]);
+                    acc[q][0] = fmaf(wr[q][2 * i + 1], hv.z, acc[q][0]);
+                    acc[q][1] = fmaf(wr[q][2 * i + 1], hv.w, acc[q][1]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc[q][0] = sum8(acc[q][0]);
+                acc[q][1] = sum8(acc[q][1]);
+                g4[q] = z[q] + (myc ? acc[q][1] : acc[q][0]);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) g4[q] = z[q];
+        }
+        // the cell of unit u, column myc (v_exp_f32 / v_rcp_f32 activations, a few ulp)
+        const float gi = sig_hw(g4[0]), gf = sig_hw(g4[1]), gg = tanh_hw(g4[2]), go = sig_hw(g4[3]);
+        cst = gf * cst + gi * gg;  // cy = forgetgate * cx + ingate * cellgate
+        const float hn = go * tanh_hw(cst);
+        if (kg < 2) sm.hs[(t + 1) & 1][hidx(u) + kg] = hn;
+        if (!tgt) {  // the obs column (kg even): BPTT's scratch and the weight gradients' h
+            float* gc = a.GC + ((int64_t)b * T + t) * 640 + u;
+            if (kg == 0) {
+                gc[0] = gi; gc[128] = gf; gc[512] = cst;
+                float* hr = a.H + (int64_t)u * C0 + b;
+                if (t + 1 < T) hr[(int64_t)(t + 1) * B] = hn;
+                if (t == 0) hr[0] = 0.f;
+            } else if (kg == 2) {
+                gc[256] = gg; gc[384] = go;
+            }
+        }
+        __syncthreads();
         DQ_STAMP(10 + t, so0 && t < 30);
         DQ_STAMP(120 + t, s10 && t < 30);
-        if (s == 0) {  // what BPTT and the weight gradients need of the obs stream (plain stores)
-            float* g = a.GS + (((int64_t)ct * T + t) * 16 + m) * 1024 + lane * 4 + w;
-            g[0] = gi; g[256] = gf; g[512] = gg; g[768] = go;
-            a.CS[(((int64_t)ct * T + t) * 16 + m) * 256 + lane * 4 + w] = c1;
-            float* hr = a.H + (int64_t)(8 * m + 4 * h + w) * C0 + bcol;
-            if (t + 1 < T) hr[(int64_t)(t + 1) * B] = hn;
-            if (t == 0) hr[0] = 0.f;
-        }
     }
-    // ---------------- heads: rows 8m .. 8m+7 of the shared head (A rows duplicated x4 in the tile)
-    // the shared head's A fragments (row 8m + (col & 7), duplicated x4; K quarter w), loaded while h_T is polled
-    float wsf[16];
+    // ---------------- heads: S = W_S h_T + b_S, V / A, Q for both columns
+    drain();
+    __syncthreads();  // every wave's share of the W_S image has landed
+    float wsr[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float4 v = *reinterpret_cast<const float4*>(&sm.ws[u * kWsStride + 16 * kg + 4 * i]);
+        wsr[4 * i] = v.x; wsr[4 * i + 1] = v.y; wsr[4 * i + 2] = v.z; wsr[4 * i + 3] = v.w;
+    }
+    const float* HW = a.HWE + net * kHwN;
+    float sv0;  // S + b_S of row u, column 0
     {
-        const int o = (8 * m + (col & 7)) * 128 + 32 * w + 4 * h;
+        float s2[2] = {0.f, 0.f};
+        const float* hp = &sm.hs[T & 1][36 * kg];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int k = o + 8 * j + e;
-                wsf[4 * j + e] = eff_w(P, R_P_SWMU + k, R_P_SWSG + k, R_P_SWEP + k, noisy);
-            }
-    }
-    // wave 0's head weights of S rows 8m + 4h + e: bias, V, A0..2 (effective), loaded while h_T is polled
-    float hw5[4][5];
-    if (w == 0)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int u = 8 * m + 4 * h + e;
-            hw5[e][0] = eff_w(P, R_P_SBMU + u, R_P_SBSG + u, R_P_SBEP + u, noisy);
-            hw5[e][1] = eff_w(P, R_P_VWMU + u, R_P_VWSG + u, R_P_VWEP + u, noisy);
-            hw5[e][2] = eff_w(P, R_P_AWMU + u, R_P_AWSG + u, R_P_AWEP + u, noisy);
-            hw5[e][3] = eff_w(P, R_P_AWMU + 128 + u, R_P_AWSG + 128 + u, R_P_AWEP + 128 + u, noisy);
-            hw5[e][4] = eff_w(P, R_P_AWMU + 256 + u, R_P_AWSG + 256 + u, R_P_AWEP + 256 + u, noisy);
+        for (int i = 0; i < 8; ++i) {
+            const float4 hv = *reinterpret_cast<const float4*>(hp + 4 * i);
+            s2[0] = fmaf(wsr[2 * i], hv.x, s2[0]);
+            s2[1] = fmaf(wsr[2 * i], hv.y, s2[1]);
+            s2[0] = fmaf(wsr[2 * i + 1], hv.z, s2[0]);
+            s2[1] = fmaf(wsr[2 * i + 1], hv.w, s2[1]);
         }
-    f32x16 sacc = {};
-    {
-        float hv[16];
-        int off[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) off[i] = hoff[i] + T * 32 * 128 * 8;
-        poll_tags(HSg, ((T * 32 + 31) * 128 + 8 * (4 * w + (lane & 3)) + 7) * 8, 4, E + T, hc);
-        gather<8, false>(HSg, off, E + T, hv, hc);  // h_T
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            *reinterpret_cast<float4*>(&sm.hT[col][32 * w + 8 * j + 4 * h]) =
-                make_float4(hv[4 * j], hv[4 * j + 1], hv[4 * j + 2], hv[4 * j + 3]);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(wsf[k], hv[k], sacc, 0, 0, 0);
+        const float bs = HW[HW_BS + u];
+        sv0 = sum8(s2[0]) + bs;
+        const float sv1 = sum8(s2[1]) + bs;
+        if (kg < 2) sm.sr[kg][u] = relu(kg ? sv1 : sv0);
     }
-    if (w > 0)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sm.red[T & 1][w][r][lane] = sacc[r];
     __syncthreads();
-    // wave 0: S rows u_e = 8m + 4h + e (registers r = e), their V / A partials
-    float sv[4], sr[4];
-    if (w == 0) {
-        float pv = 0.f, pa0 = 0.f, pa1 = 0.f, pa2 = 0.f;
+    if (w == 0) {  // lane: output o (0 V, 1..3 A), column c, rows 16 pp .. 16 pp + 15
+        const int o = lane & 3, c = (lane >> 2) & 1, pp = lane >> 3;
+        const float* wo = HW + (o == 0 ? HW_V : HW_A + 128 * (o - 1)) + 16 * pp;
+        float acc = 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float z = ((sacc[e] + sm.red[T & 1][1][e][lane]) + sm.red[T & 1][2][e][lane]) + sm.red[T & 1][3][e][lane];
-            sv[e] = z + hw5[e][0];
-            sr[e] = relu(sv[e]);
-            pv = fmaf(hw5[e][1], sr[e], pv);
-            pa0 = fmaf(hw5[e][2], sr[e], pa0);
-            pa1 = fmaf(hw5[e][3], sr[e], pa1);
-            pa2 = fmaf(hw5[e][4], sr[e], pa2);
+        for (int r = 0; r < 16; ++r) acc = fmaf(wo[r], sm.sr[c][16 * pp + r], acc);
+        acc += __shfl_xor(acc, 8);
+        acc += __shfl_xor(acc, 16);
+        acc += __shfl_xor(acc, 32);
+        if (pp == 0) sm.qv[c][o] = acc + (o == 0 ? HW[HW_VB] : HW[HW_AB + o - 1]);
+    }
+    __syncthreads();
+    float q[2][3];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const float v = sm.qv[c][0], x0 = sm.qv[c][1], x1 = sm.qv[c][2], x2 = sm.qv[c][3];
+        const float mean = ((x0 + x1) + x2) / 3.0f;  // A.mean(dim=1)
+        q[c][0] = v + (x0 - mean);
+        q[c][1] = v + (x1 - mean);
+        q[c][2] = v + (x2 - mean);
+    }
+    if (tgt) {  // publish Q_target(s_T)
+        if (tid == 0) {
+            const __amdgpu_buffer_rsrc_t rq = rsrc(a.QT);
+            st_g2(rq, b * 32, q[0][0], q[0][1], E + 1);
+            st_g2(rq, b * 32 + 16, q[0][2], 0.f, E + 1);
         }
-        pv += __shfl_xor(pv, 32);
-        pa0 += __shfl_xor(pa0, 32);
-        pa1 += __shfl_xor(pa1, 32);
-        pa2 += __shfl_xor(pa2, 32);
-        if (h == 0) {
-            const __amdgpu_buffer_rsrc_t rq = rsrc(a.QP + (int64_t)grp * 16 * 256);
-            st_g2(rq, (m * 32 + col) * 32, pv, pa0, E + 1);
-            st_g2(rq, (m * 32 + col) * 32 + 16, pa1, pa2, E + 1);
-        }
+        DQ_STAMP(150, s10);
+        return;
     }
     DQ_STAMP(50, so0);
-    DQ_STAMP(150, s10);
-    if (s != 0) return;  // block-uniform: the next-state streams are done
-    // ---------------- the loss and the head gradients (obs stream)
-    if (w < 3) {  // wave st gathers stream st's 16 partials of this column tile (8 per lane half)
-        const int st = w;
-        const float* QPs = a.QP + (int64_t)(st * nct + ct) * 16 * 256;
-        float p[32];
-#pragma unroll
-        for (int k0 = 0; k0 < 8; k0 += 4) {
-            int off[8];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                off[2 * k] = ((8 * h + k0 + k) * 32 + col) * 32;
-                off[2 * k + 1] = off[2 * k] + 16;
-            }
-            float pp[16];
-            gather<8, true>(QPs, off, E + 1, pp, hc);
-#pragma unroll
-            for (int k = 0; k < 16; ++k) p[4 * k0 + k] = pp[k];
-        }
-        float v = 0.f, x0 = 0.f, x1 = 0.f, x2 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { v += p[4 * k]; x0 += p[4 * k + 1]; x1 += p[4 * k + 2]; x2 += p[4 * k + 3]; }
-        v += __shfl_xor(v, 32);  // + the other half (commutative: both halves agree bit for bit)
-        x0 += __shfl_xor(x0, 32);
-        x1 += __shfl_xor(x1, 32);
-        x2 += __shfl_xor(x2, 32);
-        if (h == 0) *reinterpret_cast<float4*>(&sm.qs[st][col][0]) = make_float4(v, x0, x1, x2);
-    }
-    __syncthreads();
-    float dV = 0.f, dA[3] = {0.f, 0.f, 0.f};
+    // ---------------- the loss and dQ (obs column), wave 0
     if (w == 0) {
-        float q[3][3];
-#pragma unroll
-        for (int st = 0; st < 3; ++st) {
-            const float4 qv = *reinterpret_cast<const float4*>(&sm.qs[st][col][0]);
-            float v = qv.x, x0 = qv.y, x1 = qv.z, x2 = qv.w;
-            const float* Pst = st == 2 ? a.target : a.params;
-            const bool nz = st != 2;
-            v += eff_w(Pst, R_P_VBMU, R_P_VBSG, R_P_VBEP, nz);
-            x0 += eff_w(Pst, R_P_ABMU + 0, R_P_ABSG + 0, R_P_ABEP + 0, nz);
-            x1 += eff_w(Pst, R_P_ABMU + 1, R_P_ABSG + 1, R_P_ABEP + 1, nz);
-            x2 += eff_w(Pst, R_P_ABMU + 2, R_P_ABSG + 2, R_P_ABEP + 2, nz);
-            const float mean = ((x0 + x1) + x2) / 3.0f;  // A.mean(dim=1)
-            q[st][0] = v + (x0 - mean);
-            q[st][1] = v + (x1 - mean);
-            q[st][2] = v + (x2 - mean);
-        }
-        DQ_STAMP(51, so0);
-        const int64_t jl = (int64_t)bcol * T + T - 1;  // the sequence's last step
+        poll_tags(a.QT, b * 32 + 24, 1, E + 1, hc);
+        const int off[2] = {b * 32, b * 32 + 16};
+        float qt[4];
+        gather<2, false>(a.QT, off, E + 1, qt, hc);
+        const int64_t jl = (int64_t)b * T + T - 1;  // the sequence's last step
         const int ac = a.act[jl];
         const float rl = a.rew[jl], dl = a.done[jl] ? 1.f : 0.f;
         const float qa = ac == 0 ? q[0][0] : (ac == 1 ? q[0][1] : q[0][2]);
         const int as = argmax3(q[1]);  // argmax Q_B(next) (first max)
-        const float y = rl + a.gamma * q[2][as] * (1.0f - dl);
+        const float y = rl + a.gamma * qt[as] * (1.0f - dl);
         const float d = qa - y, ad = fabsf(d);
-        float lv = ad < 1.0f ? 0.5f * d * d : ad - 0.5f;  // smooth_l1, beta 1
+        const float lv = ad < 1.0f ? 0.5f * d * d : ad - 0.5f;  // smooth_l1, beta 1
         const float gq = fminf(fmaxf(d, -1.0f), 1.0f) / (float)B;
-        dV = gq;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dA[k] = (k == ac ? gq : 0.f) - gq / 3.0f;
-        if (m == 0) {  // loss / q sums of this column tile (lanes of half 0)
-            float qs = qa;
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) { lv += __shfl_xor(lv, o); qs += __shfl_xor(qs, o); }
-            if (lane == 0) { a.LP[ct * 4 + 0] = lv; a.LP[ct * 4 + 1] = qs; }
+        if (lane < 4) {
+            const float dv = lane == 0 ? gq : (lane - 1 == ac ? gq : 0.f) - gq / 3.0f;
+            sm.dva[lane] = dv;
+            a.SC[b * 8 + SC_DV + lane] = dv;
+        } else if (lane == 4) {
+            a.SC[b * 8 + SC_LOSS] = lv;
+            a.SC[b * 8 + SC_Q] = qa;
         }
-        // dS of rows u_e (modelB's effective V / A weights), the head gradients of those rows
-        float* HPc = a.HP + (int64_t)ct * kHpStride;
-        float gv[4], ga[3][4], gb[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float ds = hw5[e][1] * dV + hw5[e][2] * dA[0] + hw5[e][3] * dA[1] + hw5[e][4] * dA[2];
-            const float dsm = sv[e] > 0.f ? ds : 0.f;
-            sm.dS[4 * h + e][col] = dsm;
-            gv[e] = dV * sr[e];
-            ga[0][e] = dA[0] * sr[e];
-            ga[1][e] = dA[1] * sr[e];
-            ga[2][e] = dA[2] * sr[e];
-            gb[e] = dsm;
-        }
-        // sums over the 32 columns of the half (fixed butterfly)
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                gv[e] += __shfl_xor(gv[e], o);
-                ga[0][e] += __shfl_xor(ga[0][e], o);
-                ga[1][e] += __shfl_xor(ga[1][e], o);
-                ga[2][e] += __shfl_xor(ga[2][e], o);
-                gb[e] += __shfl_xor(gb[e], o);
-            }
-        if (col == 0)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int u = 8 * m + 4 * h + e;
-                HPc[HP_V + u] = gv[e];
-                HPc[HP_A + u] = ga[0][e];
-                HPc[HP_A + 128 + u] = ga[1][e];
-                HPc[HP_A + 256 + u] = ga[2][e];
-                HPc[HP_BS + u] = gb[e];
-            }
-        if (m == 0) {
-            float sb = dV, sa0 = dA[0], sa1 = dA[1], sa2 = dA[2];
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) {
-                sb += __shfl_xor(sb, o); sa0 += __shfl_xor(sa0, o); sa1 += __shfl_xor(sa1, o); sa2 += __shfl_xor(sa2, o);
-            }
-            if (lane == 0) { HPc[HP_VB] = sb; HPc[HP_AB] = sa0; HPc[HP_AB + 1] = sa1; HPc[HP_AB + 2] = sa2; }
-        }
+        DQ_STAMP(51, so0);
     }
-    __syncthreads();  // dS (h_T and ws: earlier barriers)
-    const float* DHc = a.DHP + (int64_t)ct * T * 16 * 8192;
-    const __amdgpu_buffer_rsrc_t rDH = rsrc(DHc);
-    {   // dh_T partial over this workgroup's 8 rows: thread (column, 16 units) -> slot T - 1
-        const int c2 = tid >> 3, u0 = (tid & 7) * 16;
-        float o16[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) o16[k] = 0.f;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const float ds = sm.dS[r][c2];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) o16[k] = fmaf(sm.ws[r][u0 + k], ds, o16[k]);
+    __syncthreads();
+    // dS of row u (modelB's effective V / A weights), through the ReLU; dh_T = W_S^T dS
+    float dh;
+    {
+        const float ds = HW[HW_V + u] * sm.dva[0] + HW[HW_A + u] * sm.dva[1] + HW[HW_A + 128 + u] * sm.dva[2] +
+                         HW[HW_A + 256 + u] * sm.dva[3];
+        const float dsm = sv0 > 0.f ? ds : 0.f;
+        if (kg == 0) {
+            a.DS[(int64_t)u * B + b] = dsm;
+            a.SR[(int64_t)u * B + b] = sm.sr[0][u];
+            a.HT[(int64_t)u * B + b] = sm.hs[T & 1][hidx(u)];
         }
-        const int base = ((((T - 1) * 16 + m) * 32 + c2) * 128 + u0) * 8;
+        float p[16];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) st_g2(rDH, base + 16 * i, o16[2 * i], o16[2 * i + 1], E + T);
-    }
-    {   // dW_S rows (partial over this column tile): thread (k', row half)
-        const int kk = tid & 127, hr = tid >> 7;
-        float g4[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int c2 = 0; c2 < 32; ++c2) {
-            const float hv = sm.hT[c2][kk];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) g4[e] = fmaf(sm.dS[4 * hr + e][c2], hv, g4[e]);
-        }
-        float* HPc = a.HP + (int64_t)ct * kHpStride;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) HPc[HP_WS + (8 * m + 4 * hr + e) * 128 + kk] = g4[e];
+        for (int j = 0; j < 16; ++j) p[j] = wsr[j] * dsm;
+        dh = reduce_units(p, sm.part[T & 1], lane, w, u, kg);
     }
     DQ_STAMP(52, so0);
-    // ---------------- BPTT
-    // Whh^T fragments of this wave's output tile (units u' = 32w + col): k-step r covers gate rows
-    // rho(r) + 4h of this workgroup's tile, i.e. Whh row 128 (r >> 2) + 8m + (r & 3) + 4h
-    float wt[16];
+    // ---------------- BPTT (obs column)
+    const float* gcb = a.GC + (int64_t)b * T * 640 + u;
+    float gn[6];  // gi gf gg go c_t c_{t-1} of the next step down
+    {
+        const float* g = gcb + (int64_t)(T - 1) * 640;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-        wt[r] = a.params[R_P_WHH + (int64_t)(128 * (r >> 2) + 8 * m + (r & 3) + 4 * h) * 128 + 32 * w + col];
-    float dc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int v = 0; v < 5; ++v) gn[v] = g[128 * v];
+        gn[5] = T > 1 ? g[512 - 640] : 0.f;
+    }
+    float dc = 0.f;
+    const __amdgpu_buffer_rsrc_t rdz = rsrc(a.DZH);
     for (int t = T - 1; t >= 0; --t) {
-        float dz[16];
-        float gt[16], cT[4], cP[4];  // wave 0: this step's gates and cells, loaded ahead of the dh wait
-        if (w == 0) {
-            const float4* g4 = reinterpret_cast<const float4*>(a.GS + (((int64_t)ct * T + t) * 16 + m) * 1024) + lane;
+        const float gi = gn[0], gf = gn[1], gg = gn[2], go = gn[3], cT = gn[4], cP = gn[5];
+        if (t > 0) {
+            const float* g = gcb + (int64_t)(t - 1) * 640;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float4 v = g4[64 * i];
-                gt[4 * i] = v.x; gt[4 * i + 1] = v.y; gt[4 * i + 2] = v.z; gt[4 * i + 3] = v.w;
-            }
-            const float4 cn = reinterpret_cast<const float4*>(a.CS + (((int64_t)ct * T + t) * 16 + m) * 256)[lane];
-            const float4 cp = t > 0 ? reinterpret_cast<const float4*>(a.CS + (((int64_t)ct * T + t - 1) * 16 + m) * 256)[lane]
-                                    : make_float4(0.f, 0.f, 0.f, 0.f);
-            cT[0] = cn.x; cT[1] = cn.y; cT[2] = cn.z; cT[3] = cn.w;
-            cP[0] = cp.x; cP[1] = cp.y; cP[2] = cp.z; cP[3] = cp.w;
+            for (int v = 0; v < 5; ++v) gn[v] = g[128 * v];
+            gn[5] = t > 1 ? g[512 - 640] : 0.f;
         }
-        {   // every wave gathers 4 producers' partials of dh_{t+1} for this workgroup's units
-            int off[8];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                off[2 * k] = ((((t * 16 + 4 * w + k) * 32) + col) * 128 + 8 * m + 4 * h) * 8;
-                off[2 * k + 1] = off[2 * k] + 16;
-            }
-            float p[16];
-            poll_tags(DHc, (((t * 16 + 4 * w + (lane & 3)) * 32 + 31) * 128 + 32 * (m >> 2) + 31) * 8, 4, E + t + 1,
-                      hc);
-            gather<8, false>(DHc, off, E + t + 1, p, hc);
-            float d4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                d4[0] += p[4 * k]; d4[1] += p[4 * k + 1]; d4[2] += p[4 * k + 2]; d4[3] += p[4 * k + 3];
-            }
-            *reinterpret_cast<float4*>(&sm.dhs[w][lane][0]) = make_float4(d4[0], d4[1], d4[2], d4[3]);
+        const float tc = tanh_hw(cT);
+        const float dcc = dc + dh * go * (1.0f - tc * tc);
+        const float dz0 = dcc * gg * (gi * (1.0f - gi));
+        const float dz1 = dcc * cP * (gf * (1.0f - gf));
+        const float dz2 = dcc * gi * (1.0f - gg * gg);
+        const float dz3 = dh * tc * (go * (1.0f - go));
+        dc = dcc * gf;
+        if (kg < 4) {
+            const float dzk = kg == 0 ? dz0 : (kg == 1 ? dz1 : (kg == 2 ? dz2 : dz3));
+            a.dZ[(int64_t)(128 * kg + u) * C0 + (int64_t)t * B + b] = dzk;
         }
-        DQ_STAMP(60 + t, so0 && t < 30);
-        __syncthreads();  // the four waves' dh sums (dhs is rewritten only after every wave published)
-        if (w == 0) {
-            float dh[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {  // the 16 producers' partials, in producer order
-                const float4 v = *reinterpret_cast<const float4*>(&sm.dhs[k][lane][0]);
-                dh[0] += v.x; dh[1] += v.y; dh[2] += v.z; dh[3] += v.w;
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float gi = gt[e], gf = gt[4 + e], gg = gt[8 + e], go = gt[12 + e];
-                const float tc = tanh_hw(cT[e]);
-                const float dcc = dc[e] + dh[e] * go * (1.0f - tc * tc);
-                dz[e] = dcc * gg * (gi * (1.0f - gi));
-                dz[4 + e] = dcc * cP[e] * (gf * (1.0f - gf));
-                dz[8 + e] = dcc * gi * (1.0f - gg * gg);
-                dz[12 + e] = dh[e] * tc * (go * (1.0f - go));
-                dc[e] = dcc * gf;
-            }
-            if (t > 0)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    *reinterpret_cast<float4*>(&sm.dzs[i][lane][0]) = make_float4(dz[4 * i], dz[4 * i + 1], dz[4 * i + 2], dz[4 * i + 3]);
+        if (kg == 0) {  // dz of unit u to the dF2 trailer: granules {dz_q, tag}, tag E + 2 + t
+            const int o = (((int)b * T + t) * 128 + u) * 32;
+            st_g2(rdz, o, dz0, dz1, E + 2 + t);
+            st_g2(rdz, o + 16, dz2, dz3, E + 2 + t);
         }
-        const int64_t cc = (int64_t)t * B + bcol;
-        if (t == 0) {  // dh_0 (the zero initial state) is not needed
-            if (w == 0)
+        if (t == 0) break;
+        float p[16];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) a.dZ[(int64_t)(128 * (r >> 2) + 8 * m + 4 * h + (r & 3)) * C0 + cc] = dz[r];
-            break;
-        }
-        __syncthreads();  // dz fragments (reused at the next step only after every wave has published)
-        if (w != 0)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float4 v = *reinterpret_cast<const float4*>(&sm.dzs[i][lane][0]);
-                dz[4 * i] = v.x; dz[4 * i + 1] = v.y; dz[4 * i + 2] = v.z; dz[4 * i + 3] = v.w;
-            }
-        f32x16 acc = {};
-        // r-th k-step: this workgroup's gate rows rho(r) + 4h (the accumulator layout of dz)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wt[r], dz[r], acc, 0, 0, 0);
-        const int base = ((((t - 1) * 16 + m) * 32 + col) * 128 + 32 * w + 4 * h) * 8;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            st_g2(rDH, base + 64 * i, acc[4 * i], acc[4 * i + 1], E + t);
-            st_g2(rDH, base + 64 * i + 16, acc[4 * i + 2], acc[4 * i + 3], E + t);
-        }
-        if (w == 0)  // for the weight gradients, behind the hand-off stores in this wave's queue
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a.dZ[(int64_t)(128 * (r >> 2) + 8 * m + 4 * h + (r & 3)) * C0 + cc] = dz[r];
+        for (int j = 0; j < 16; ++j) p[j] = fmaf(wr[3][j], dz3, fmaf(wr[2][j], dz2, fmaf(wr[1][j], dz1, wr[0][j] * dz0)));
+        dh = reduce_units(p, sm.part[t & 1], lane, w, u, kg);
         DQ_STAMP(90 + t, so0 && t < 30);
     }
     DQ_STAMP(2, so0);
@@ -741,41 +738,42 @@ __global__ __launch_bounds__(256) void k_dq_recur(DqArgs a) {
 
 // ---------------------------------------------------------------- 3: weight gradients
 struct WgSmem {
-    union {
-        float red[16][16][64];          // type A: per-wave partial tiles
-        struct {
-            union {
-                float dZs[512][32];     // type B: this column tile's dZ block (the dF2 B operands)
-                float red2[4][128][33]; // type B: dF2 K-quarter partials, later dF1 partials
-            };
-            float dP2[128][33];
-            float dP1[64][33];
-            float F1s[64][33];
-        } b;
-    };
+    float red[16][16][64];  // per-wave partial tiles
     float rs[16][64];
-    float Xs[7][32];
-    int last;
 };
+
+// One 32 x 32 output tile per workgroup, K split over the 16 waves (8-column chunks round robin, 4 in
+// flight), summed in wave order; the tile's row sums (the bias gradients) ride along.
+//   mat 0: dWih = dZ F2^T (16 x 4 tiles, K = T*B)        row sums -> db_ih = db_hh
+//   mat 1: dWhh = dZ H^T  (16 x 4)
+//   mat 2: dW_S = dS h_T^T (4 x 4, K = B)                row sums -> db_S
+//   mat 3: dW2 = dP2 F1^T (4 x 2, K = T*B)               row sums -> db2
+//   mat 4: dW1 = dP1 x^T  (2 x 1; x^T rows 7..31 zero)    row sums -> db1
+// then one workgroup for the V / A head gradients, the loss and mean Q.
+constexpr int kWgTiles = 64 + 64 + 16 + 8 + 2;
 
 __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
     if (skipped(a)) return;
     __shared__ WgSmem sm;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
     const int64_t C0 = a.C0;
-    const int B = a.B, T = a.T, nct = a.nct;
-    const int nB = a.C0 / 32;
-    int bid = blockIdx.x;
+    const int B = a.B;
+    const int bid = blockIdx.x;
     DQ_STAMP(210, bid == 0);
-    DQ_STAMP(200, bid == kWgA);
-    if (bid < kWgA) {
-        // ---- dWih (mat 0) / dWhh (mat 1) tile: rows g in [32 gt, +32), columns k' in [32 kt, +32)
-        const int mat = bid >> 6, gt = (bid >> 2) & 15, kt = bid & 3;
-        const float* Ar = a.dZ + (int64_t)(32 * gt + col) * C0 + 4 * h;
-        const float* Br = (mat == 0 ? a.F2T : a.H) + (int64_t)(32 * kt + col) * C0 + 4 * h;
+    if (bid < kWgTiles) {
+        int mat, gt, kt;
+        if (bid < 128) { mat = bid >> 6; gt = (bid >> 2) & 15; kt = bid & 3; }
+        else if (bid < 144) { mat = 2; gt = (bid - 128) >> 2; kt = bid & 3; }
+        else if (bid < 152) { mat = 3; gt = (bid - 144) >> 1; kt = bid & 1; }
+        else { mat = 4; gt = bid - 152; kt = 0; }
+        const int64_t ld = mat == 2 ? (int64_t)B : C0;
+        const float* A = mat <= 1 ? a.dZ : (mat == 2 ? a.DS : (mat == 3 ? a.dP2 : a.dP1));
+        const float* Bm = mat == 0 ? a.F2T : (mat == 1 ? a.H : (mat == 2 ? a.HT : (mat == 3 ? a.F1T : a.XT)));
+        const float* Ar = A + (int64_t)(32 * gt + col) * ld + 4 * h;
+        const float* Br = Bm + (int64_t)(32 * kt + col) * ld + 4 * h;
         f32x16 acc = {};
         float rsum = 0.f;
-        const int nch = (int)(C0 / 8);  // 8-column chunks, round robin over the waves, 4 in flight
+        const int nch = (int)(ld / 8);
         for (int kc0 = w; kc0 < nch; kc0 += 64) {
             float4 av[4], bv[4];
 #pragma unroll
@@ -799,181 +797,59 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
         sm.rs[w][lane] = rsum;
         __syncthreads();
         if (w == 0) {
-            float* G = a.grad + (mat == 0 ? R_P_WIH : R_P_WHH);
+            const int ldg = mat <= 2 ? 128 : (mat == 3 ? 64 : 7);
+            float* G = a.grad + (mat == 0 ? R_P_WIH : (mat == 1 ? R_P_WHH : (mat == 2 ? R_P_SWMU : (mat == 3 ? R_P_F2W : R_P_F1W))));
+            if (32 * kt + col < ldg)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float v = sm.red[0][r][lane];
-                for (int k = 1; k < 16; ++k) v += sm.red[k][r][lane];
-                G[(int64_t)(32 * gt + rho(r) + 4 * h) * 128 + 32 * kt + col] = v;
-            }
+                for (int r = 0; r < 16; ++r) {
+                    float v = sm.red[0][r][lane];
+                    for (int k = 1; k < 16; ++k) v += sm.red[k][r][lane];
+                    G[(int64_t)(32 * gt + rho(r) + 4 * h) * ldg + 32 * kt + col] = v;
+                }
             DQ_STAMP(211, bid == 0);
-            if (mat == 0 && kt == 0) {  // db_ih = db_hh = row sums of dZ
+            if (mat != 1 && kt == 0) {  // the bias gradients: row sums
                 float v = sm.rs[0][lane];
                 for (int k = 1; k < 16; ++k) v += sm.rs[k][lane];
                 v += __shfl_xor(v, 32);
-                if (h == 0) { a.grad[R_P_BIH + 32 * gt + col] = v; a.grad[R_P_BHH + 32 * gt + col] = v; }
-            }
-        }
-        return;
-    }
-    bid -= kWgA;
-    if (bid < nB) {
-        // ---- column tile: columns [c0, c0 + 32) (one time step t, batch rows b0 .. b0 + 31)
-        const int64_t c0 = (int64_t)bid * 32;
-        const int t = (int)(c0 / B), b0 = (int)(c0 % B);
-        // the dZ block of the tile (512 rows x 128 B) global -> LDS, 8 rows per wave instruction
-        for (int k = w; k < 64; k += 16) {
-            const int row = 8 * k + (lane >> 3);
-            __builtin_amdgcn_global_load_lds((const void*)(a.dZ + (int64_t)row * C0 + c0 + 4 * (lane & 7)),
-                                             (lds_void*)&sm.b.dZs[8 * k][0], 16, 0, 0);
-        }
-        // dF2 = Wih^T dZ: wave (out tile ot = w & 3, K quarter kq = w >> 2), k = g = 128 kq + 2p + h
-        {
-            const int ot = w & 3, kq = w >> 2;
-            f32x16 acc = {};
-            const float* Wc = a.params + R_P_WIH + 32 * ot + col;
-            float wa64[64];  // this wave's Wih^T operands, all in flight while the dZ block lands
-#pragma unroll
-            for (int p = 0; p < 64; ++p) wa64[p] = Wc[(int64_t)(128 * kq + 2 * p + h) * 128];
-            drain();
-            __syncthreads();  // the dZ block (global_load_lds) from every wave
-#pragma unroll
-            for (int p = 0; p < 64; ++p)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa64[p], sm.b.dZs[128 * kq + 2 * p + h][col], acc, 0, 0, 0);
-            __syncthreads();  // dZs is overlaid by red2
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sm.b.red2[kq][32 * ot + rho(r) + 4 * h][col] = acc[r];
-        }
-        for (int k = tid; k < 64 * 32; k += 1024) sm.b.F1s[k >> 5][k & 31] = a.F1T[(int64_t)(k >> 5) * C0 + c0 + (k & 31)];
-        if (tid < 224) sm.Xs[tid % 7][tid / 7] = a.obs[((int64_t)(b0 + tid / 7) * T + t) * 7 + tid % 7];  // x of the 32 columns
-        __syncthreads();
-        DQ_STAMP(201, bid == 0);
-        for (int k = tid; k < 128 * 32; k += 1024) {
-            const int u = k >> 5, c2 = k & 31;
-            const float v = ((sm.b.red2[0][u][c2] + sm.b.red2[1][u][c2]) + sm.b.red2[2][u][c2]) + sm.b.red2[3][u][c2];
-            sm.b.dP2[u][c2] = a.F2T[(int64_t)u * C0 + c0 + c2] > 0.f ? v : 0.f;  // through the ReLU
-        }
-        __syncthreads();
-        float* Wp = a.W2P + (int64_t)bid * kLowN;
-        if (w < 8) {  // dW2 partial [k'][j] = sum_c dP2[k'][c] F1[j][c]: wave -> tile (k' tile w & 3, j tile w >> 2)
-            const int rt = w & 3, jt = w >> 2;
-            f32x16 acc = {};
-#pragma unroll
-            for (int p = 0; p < 16; ++p)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sm.b.dP2[32 * rt + col][2 * p + h], sm.b.F1s[32 * jt + col][2 * p + h],
-                                                          acc, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) st_wt(&Wp[R_P_F2W + (32 * rt + rho(r) + 4 * h) * 64 + 32 * jt + col], acc[r]);
-        } else if (tid < 512 + 128) {  // db2 partial
-            const int u = tid - 512;
-            float sb = 0.f;
-            for (int c2 = 0; c2 < 32; ++c2) sb += sm.b.dP2[u][c2];
-            st_wt(&Wp[R_P_F2B + u], sb);
-        }
-        {   // dF1 = W2^T dP2: wave (out tile jt = w & 1, K eighth ke = w >> 1), k = k' = 16 ke + 2p + h
-            const int jt = w & 1, ke = w >> 1;
-            f32x16 acc = {};
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const int k = 16 * ke + 2 * p + h;
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.params[R_P_F2W + k * 64 + 32 * jt + col], sm.b.dP2[k][col], acc, 0, 0, 0);
-            }
-            __syncthreads();  // red2 is free again (the dP2 pass is done)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sm.b.red2[ke >> 1][(ke & 1) * 64 + 32 * jt + rho(r) + 4 * h][col] = acc[r];
-        }
-        __syncthreads();
-        for (int k = tid; k < 64 * 32; k += 1024) {
-            const int j = k >> 5, c2 = k & 31;
-            float v = 0.f;
-#pragma unroll
-            for (int ke = 0; ke < 8; ++ke) v += sm.b.red2[ke >> 1][(ke & 1) * 64 + j][c2];
-            sm.b.dP1[j][c2] = sm.b.F1s[j][c2] > 0.f ? v : 0.f;
-        }
-        __syncthreads();
-        DQ_STAMP(204, bid == 0);
-        if (tid < 448) {  // dW1 partial [j][i] = sum_c dP1[j][c] x_i[c]
-            const int j = tid / 7, i = tid % 7;
-            float v = 0.f;
-            for (int c2 = 0; c2 < 32; ++c2) v = fmaf(sm.b.dP1[j][c2], sm.Xs[i][c2], v);
-            st_wt(&Wp[R_P_F1W + j * 7 + i], v);
-        } else if (tid < 512) {
-            const int j = tid - 448;
-            float v = 0.f;
-            for (int c2 = 0; c2 < 32; ++c2) v += sm.b.dP1[j][c2];
-            st_wt(&Wp[R_P_F1B + j], v);
-        }
-        // arrival ticket: the last R column tiles to finish wait for the rest, then each sums a
-        // quarter of the partials in tile order (the earlier arrivers are done, so the wait is short)
-        const int R = min(4, nB);
-        drain();
-        __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            drain();
-            const int k = atomicAdd(a.flags + 1, 1);
-            int slot = k - (nB - R);
-            if (slot >= 0) {
-                const HandoffCtl hc{a.stats, a.grad + PM_RNN_NPARAM + 1, 4 * hand_limit(a.poll_limit)};
-                for (int it = 0;; ++it) {
-                    if (__hip_atomic_load(a.flags + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nB) break;
-                    if (it >= hc.limit) { void_update(hc); slot = -1; break; }
-                    __builtin_amdgcn_s_sleep(2);
+                const int row = 32 * gt + col;
+                if (h == 0) {
+                    if (mat == 0) { a.grad[R_P_BIH + row] = v; a.grad[R_P_BHH + row] = v; }
+                    else if (mat == 2) a.grad[R_P_SBMU + row] = v;
+                    else if (mat == 3) a.grad[R_P_F2B + row] = v;
+                    else a.grad[R_P_F1B + row] = v;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                drain();
             }
-            sm.last = slot;
         }
-        __syncthreads();
-        DQ_STAMP(206, bid == 0);
-        DQ_STAMP(207, sm.last == 0);
-        if (sm.last < 0) return;
-        const int per = (kLowN / R + 3) & ~3, lo = sm.last * per, hi = min(kLowN, lo + per);
-        for (int i0 = lo + tid; i0 < hi; i0 += 4 * 1024) {  // 4 elements x 8 tiles = 32 loads in flight
-            float v[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int k = 0; k < nB; k += 8) {
-                float x[4][8];
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int i = min(i0 + e * 1024, hi - 1);
-                        x[e][j] = k + j < nB ? ld_wt(&a.W2P[(int64_t)(k + j) * kLowN + i]) : 0.f;
-                    }
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        if (k + j < nB) v[e] += x[e][j];  // in tile order
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (i0 + e * 1024 < hi) a.grad[i0 + e * 1024] = v[e];
-        }
-        DQ_STAMP(208, true);
         return;
     }
-    bid -= nB;
-    // ---- head partials: sum over column tiles in order
-    const int per = (HP_N + kWgC - 1) / kWgC, lo = bid * per, hi = min(HP_N, lo + per);
-    for (int i = lo + tid; i < hi; i += 1024) {
+    // ---- the V / A head gradients: dw_o[r] = sum_b dQ_o[b] ReLU(S)[r][b] (o = V, A0..2) and their biases,
+    // the loss and mean Q, each summed over the sequences in order
+    if (tid < 512) {
+        const int o = tid >> 7, r = tid & 127;
+        const float* sr = a.SR + (int64_t)r * B;
         float v = 0.f;
-        for (int k = 0; k < nct; ++k) v += a.HP[(int64_t)k * kHpStride + i];
-        int dst;
-        if (i < HP_BS) dst = R_P_SWMU + i;
-        else if (i < HP_V) dst = R_P_SBMU + i - HP_BS;
-        else if (i < HP_VB) dst = R_P_VWMU + i - HP_V;
-        else if (i == HP_VB) dst = R_P_VBMU;
-        else if (i < HP_AB) dst = R_P_AWMU + i - HP_A;
-        else dst = R_P_ABMU + i - HP_AB;
-        a.grad[dst] = v;
-    }
-    if (bid == 0 && tid == 0) {
-        float ls = 0.f, qs = 0.f;
-        for (int k = 0; k < nct; ++k) { ls += a.LP[k * 4]; qs += a.LP[k * 4 + 1]; }
-        a.stats->loss = ls / (float)B;
-        a.stats->q_mean = qs / (float)B;
+        for (int b0 = 0; b0 < B; b0 += 16) {  // 32 loads in flight, then the 16 fmaf in sequence order
+            float c[16], x[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { c[i] = a.SC[(b0 + i) * 8 + SC_DV + o]; x[i] = sr[b0 + i]; }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v = fmaf(c[i], x[i], v);
+        }
+        a.grad[o == 0 ? R_P_VWMU + r : R_P_AWMU + 128 * (o - 1) + r] = v;
+    } else if (tid < 518) {
+        const int o = tid - 512;  // dV, dA0..2, loss, Q(s, a)
+        float v = 0.f;
+        for (int b0 = 0; b0 < B; b0 += 16) {
+            float c[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) c[i] = a.SC[(b0 + i) * 8 + o];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v += c[i];
+        }
+        if (o == 0) a.grad[R_P_VBMU] = v;
+        else if (o < 4) a.grad[R_P_ABMU + o - 1] = v;
+        else if (o == SC_LOSS) a.stats->loss = v / (float)B;
+        else a.stats->q_mean = v / (float)B;
     }
 }
 
@@ -1150,9 +1026,9 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     a.poll_limit = d->poll_limit;
     hipLaunchKernelGGL(k_dq_embed, dim3(3 * a.nct * a.T * 4), dim3(256), 0, st, a);
     PM_LAUNCHED("k_dq_embed");
-    pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(3 * a.nct * kG), dim3(256), st, a);
+    pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(3 * a.B), dim3(kRecThreads), st, a);
     PM_LAUNCHED("k_dq_recur");
-    hipLaunchKernelGGL(k_dq_wgrad, dim3(kWgA + a.C0 / 32 + kWgC), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(k_dq_wgrad, dim3(kWgTiles + 1), dim3(1024), 0, st, a);
     PM_LAUNCHED("k_dq_wgrad");
     return PM_OK;
 }

@@ -1,20 +1,14 @@
 #!/bin/bash
-# Round 4: DRQN update work — its GPU tests, the RNN bench line (drqn_roofline: update_us, recur_us)
-# and, optionally, the in-kernel stamps of the recurrence (diagnostic library).
-#   gpurun --timeout 900 -- bash tools/gpu_r4_drqn.sh <tag> [stamps]
+# DRQN recurrence rework: the DRQN tests, then the RNN line (update / recurrence times).
+#   gpurun --timeout 600 -- bash tools/gpu_r4_drqn.sh
 set -o pipefail
 export TMPDIR=/tmp
-tag=${1:-r4d}
 mkdir -p gpurun_out
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_drqn.py tests/test_gpu_rnn_selfplay.py tests/test_gpu_comm.py -q -x \
-    --timeout 200 --timeout-method thread > gpurun_out/${tag}_pytest.log 2>&1; rc=$?; tail -n 2 gpurun_out/${tag}_pytest.log
-[ $rc -eq 0 ] || { grep -E "^E |Error|FAILED" gpurun_out/${tag}_pytest.log | head -20; exit 1; }
-timeout -k 10 300 python3 bench.py --workload rnn --no-cpu-baseline > gpurun_out/${tag}_rnn.json 2> gpurun_out/${tag}_rnn.err \
-    || { tail -5 gpurun_out/${tag}_rnn.err; exit 1; }
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_drqn.py -x -v -s --timeout 120 --timeout-method thread \
+    > gpurun_out/r4d_drqn.log 2>&1; rc=$?; tail -n 4 gpurun_out/r4d_drqn.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python3 bench.py --workload rnn --no-cpu-baseline > gpurun_out/r4d_rnn.json 2> gpurun_out/r4d_rnn.err || exit 1
 python3 -c "
-import json; d=json.load(open('gpurun_out/${tag}_rnn.json'))
-print('rnn value', d['value'], 'ms/step', d['ms_per_step'], 'env_update_us', d.get('env_update_us'), 'act_us', d['roofline']['avg_us'])
-print('drqn', {k: d['drqn_roofline'][k] for k in ('update_us', 'recur_us', 'frac')})"
-if [ "$2" = stamps ]; then
-  timeout -k 10 200 python3 tools/drqn_stamps.py > gpurun_out/${tag}_drqn_stamps.txt 2>&1 && echo STAMPS_OK
-fi
+import json; d=json.load(open('gpurun_out/r4d_rnn.json')); print('rnn', d['value'], d['ms_per_step'], json.dumps(d.get('drqn_roofline')))"
+timeout -k 10 120 python3 tools/drqn_stamps.py > gpurun_out/r4d_stamps.txt 2>&1; tail -n 40 gpurun_out/r4d_stamps.txt
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/r4d_prof -o drqn -- python3 tools/drqn_prof.py > gpurun_out/r4d_prof.log 2>&1
+f=$(find gpurun_out/r4d_prof -name '*kernel_stats.csv' | head -n 1); [ -n "$f" ] && cut -d, -f1-4 "$f" | head -n 12

@@ -68,9 +68,11 @@ struct DqArgs {
     float *dP1;  // [64][C0]                  dF1 through F1's ReLU
     float *XT;   // [32][C0]                  obs stream inputs x^T (rows 7..31 zero)
     double* part;
+    double* NP;      // [kWgTiles + 1] per-block sums of squares of the final gradient (local_norm)
     int64_t* tstep;
     int32_t* flags;  // [0] update epoch (the granule tag base), [1] k_dq_wgrad's ticket, [2] k_drqn_apply's
     int poll_limit;  // polls per hand-off wait (pm_drqn.poll_limit: 0 = 2^20; < 0 = none, a test hook)
+    int local_norm;  // 1: one replica (pm_drqn_update): k_dq_wgrad's blocks sum the clip norm's squares
 };
 __device__ __forceinline__ int hand_limit(int pl) { return pl == 0 ? (1 << 20) : (pl < 0 ? 0 : pl); }
 
@@ -92,14 +94,14 @@ inline int64_t dq_layout(int B, int T, DqArgs* a, void* work) {
                   oDS = L.add(128 * (int64_t)B), oSR = L.add(128 * (int64_t)B), oHT = L.add(128 * (int64_t)B),
                   oSC = L.add((int64_t)B * 8), oWSE = L.add(2 * 128 * kWsStride), oHWE = L.add(2 * kHwN),
                   oDZH = L.add(C0 * 1024), odP2 = L.add(128 * C0), odP1 = L.add(64 * C0),
-                  oXT = L.add(32 * C0), oPart = L.add(2 * kNormBlocks), oTs = L.add(4),
+                  oXT = L.add(32 * C0), oPart = L.add(2 * kNormBlocks), oNP = L.add(2 * 256), oTs = L.add(4),
                   oFl = L.add(4);
     if (a && work) {
         float* w = static_cast<float*>(work);
         a->B = B; a->T = T; a->nct = (int)nct; a->C0 = (int)C0;
         a->ZX = w + oZX; a->F1T = w + oF1; a->F2T = w + oF2; a->H = w + oH; a->GC = w + oGC; a->dZ = w + odZ;
         a->QT = w + oQT; a->DS = w + oDS; a->SR = w + oSR; a->HT = w + oHT; a->SC = w + oSC; a->WSE = w + oWSE;
-        a->HWE = w + oHWE; a->DZH = w + oDZH; a->dP2 = w + odP2; a->dP1 = w + odP1; a->XT = w + oXT; a->part = reinterpret_cast<double*>(w + oPart);
+        a->HWE = w + oHWE; a->DZH = w + oDZH; a->dP2 = w + odP2; a->dP1 = w + odP1; a->XT = w + oXT; a->part = reinterpret_cast<double*>(w + oPart); a->NP = reinterpret_cast<double*>(w + oNP);
         a->tstep = reinterpret_cast<int64_t*>(w + oTs); a->flags = reinterpret_cast<int32_t*>(w + oFl);
     }
     return L.total * 4;
@@ -201,89 +203,112 @@ __device__ __forceinline__ void poll_tags(const void* base, int soff, int n, uin
 }
 
 // ---------------------------------------------------------------- 1: embedding + input projection
-// grid: 3 streams x nct column tiles x T steps x 4 row quarters; wave w computes the Zx tile of
-// recurrence workgroup m = 4 * quarter + w. Tile rows: row r' of workgroup m is gate r' >> 3 of LSTM
-// unit 8m + (r' & 7), i.e. Wih / Whh row 128 (r' >> 3) + 8m + (r' & 7).
-__global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
+// grid: 3 streams x nct column tiles x T steps x 4 row quarters (main blocks, 8 waves), then
+// kEmbEff blocks for the effective head weights. In a main block waves 0..3 compute F2 tile w (every
+// wave of the four computes F1 first); then wave w computes half the K of Zx tile m = 4 quarter +
+// (w & 3) (K half w >> 2: 32 MFMAs instead of 64 on one wave), the halves meeting in LDS. Tile rows:
+// row r' of tile m is gate r' >> 3 of LSTM unit 8m + (r' & 7), i.e. Wih row 128 (r' >> 3) + 8m + (r' & 7).
+constexpr int kEmbEff = 16;
+__global__ __launch_bounds__(512) void k_dq_embed(DqArgs a) {
     const int nct = a.nct, T = a.T, B = a.B;
+    const int nMain = 3 * nct * T * 4;
     int bid = blockIdx.x;
-    const int rq = bid & 3;
-    bid >>= 2;
-    const int t = bid % T;
-    bid /= T;
-    const int ct = bid % nct, s = bid / nct;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
-    if (blockIdx.x == 0 && tid == 0) {  // a new tag epoch for k_dq_recur's hand-offs; the wgrad ticket
+    if (blockIdx.x == 0 && tid == 0) {  // a new tag epoch for k_dq_recur's hand-offs; the apply's ticket
         a.flags[0] = a.flags[0] + 1;
         a.flags[1] = 0;
         a.flags[2] = 0;  // k_drqn_apply's arrival counter (monotonic within an apply, generation-based)
     }
     if (skipped(a)) {  // this replica contributes nothing to the all-reduce
-        for (int i = blockIdx.x * 256 + tid; i < PM_RNN_NPARAM + 4; i += gridDim.x * 256) a.grad[i] = 0.f;
+        for (int i = blockIdx.x * 512 + tid; i < PM_RNN_NPARAM + 4; i += gridDim.x * 512) a.grad[i] = 0.f;
         return;
     }
     if (blockIdx.x == 0 && tid == 0) {
         a.grad[PM_RNN_NPARAM] = 1.0f;      // this replica contributes
         a.grad[PM_RNN_NPARAM + 1] = 0.0f;  // no hand-off has timed out (yet) in this update
     }
-    // the effective head weights the recurrence's workgroups read (modelB in train mode: mu + sigma *
-    // epsilon; targetB in eval mode: mu), W_S in the padded row image k_dq_recur copies to LDS
-    for (int i = blockIdx.x * 256 + tid; i < 2 * (16384 + 644); i += gridDim.x * 256) {
-        const int n = i >= 16384 + 644, j = i - n * (16384 + 644);
-        const float* Pn = n ? a.target : a.params;
-        if (j < 16384) {
-            a.WSE[(n * 128 + (j >> 7)) * kWsStride + (j & 127)] = eff_w(Pn, R_P_SWMU + j, R_P_SWSG + j, R_P_SWEP + j, !n);
-        } else {
-            const int v = j - 16384;  // b_S 128 | w_V 128 | w_A 384 | b_V | b_A 3
-            int mu, sg, ep;
-            if (v < 128) { mu = R_P_SBMU + v; sg = R_P_SBSG + v; ep = R_P_SBEP + v; }
-            else if (v < 256) { mu = R_P_VWMU + v - 128; sg = R_P_VWSG + v - 128; ep = R_P_VWEP + v - 128; }
-            else if (v < 640) { mu = R_P_AWMU + v - 256; sg = R_P_AWSG + v - 256; ep = R_P_AWEP + v - 256; }
-            else if (v == 640) { mu = R_P_VBMU; sg = R_P_VBSG; ep = R_P_VBEP; }
-            else { mu = R_P_ABMU + v - 641; sg = R_P_ABSG + v - 641; ep = R_P_ABEP + v - 641; }
-            a.HWE[n * kHwN + v] = eff_w(Pn, mu, sg, ep, !n);
+    if (bid >= nMain) {
+        // the effective head weights the recurrence's workgroups read (modelB in train mode: mu + sigma
+        // * epsilon; targetB in eval mode: mu), W_S in the padded row image k_dq_recur copies to LDS
+        for (int i = (bid - nMain) * 512 + tid; i < 2 * (16384 + 644); i += kEmbEff * 512) {
+            const int n = i >= 16384 + 644, j = i - n * (16384 + 644);
+            const float* Pn = n ? a.target : a.params;
+            if (j < 16384) {
+                a.WSE[(n * 128 + (j >> 7)) * kWsStride + (j & 127)] = eff_w(Pn, R_P_SWMU + j, R_P_SWSG + j, R_P_SWEP + j, !n);
+            } else {
+                const int v = j - 16384;  // b_S 128 | w_V 128 | w_A 384 | b_V | b_A 3
+                int mu, sg, ep;
+                if (v < 128) { mu = R_P_SBMU + v; sg = R_P_SBSG + v; ep = R_P_SBEP + v; }
+                else if (v < 256) { mu = R_P_VWMU + v - 128; sg = R_P_VWSG + v - 128; ep = R_P_VWEP + v - 128; }
+                else if (v < 640) { mu = R_P_AWMU + v - 256; sg = R_P_AWSG + v - 256; ep = R_P_AWEP + v - 256; }
+                else if (v == 640) { mu = R_P_VBMU; sg = R_P_VBSG; ep = R_P_VBEP; }
+                else { mu = R_P_ABMU + v - 641; sg = R_P_ABSG + v - 641; ep = R_P_ABEP + v - 641; }
+                a.HWE[n * kHwN + v] = eff_w(Pn, mu, sg, ep, !n);
+            }
         }
+        return;
     }
+    const int rq = bid & 3;
+    bid >>= 2;
+    const int t = bid % T;
+    bid /= T;
+    const int ct = bid % nct, s = bid / nct;
     __shared__ __attribute__((aligned(16))) float F2s[32][132];
+    __shared__ float zp[4][16][64];  // the K-half-1 partials of the four Zx tiles
     DQ_STAMP(220, blockIdx.x == 0);
     const float* P = s == 2 ? a.target : a.params;
     const int b = ct * 32 + col;
     const int64_t c = (int64_t)t * B + b;
-    float xs[4];
-    tile_inputs((s == 0 ? a.obs : a.next) + ((int64_t)b * T + t) * 7, h, xs);
-    // every weight operand of the wave is loaded up front: the Zx A fragments (64 registers) land
-    // while F1 / F2 compute instead of after the F2 barrier
-    const int m = 4 * rq + w;
-    const float* wr = P + R_P_WIH + (int64_t)(128 * (col >> 3) + 8 * m + (col & 7)) * 128 + 4 * h;
-    float4 av[16];
+    const int m = 4 * rq + (w & 3), kh = w >> 2;
+    DQ_STAMP(227, blockIdx.x == 0 && s == 0);
+    // every load of the block is issued here, before any MFMA (one round trip instead of four):
+    // the Zx A fragments of this wave's K half (all waves); x, W1 / b1, W2, b2 (F waves 0..3); the
+    // Zx bias of tile m (waves 4..7, which form the final sum)
+    const float* wr = P + R_P_WIH + (int64_t)(128 * (col >> 3) + 8 * m + (col & 7)) * 128 + 4 * h + 64 * kh;
+    float4 av[8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) av[j] = *reinterpret_cast<const float4*>(wr + 8 * j);
+    for (int j = 0; j < 8; ++j) av[j] = *reinterpret_cast<const float4*>(wr + 8 * j);
+    float xs[4], f1w[2][4], zb[16];
     float4 w2v[8];
-    {
+    f32x16 f2;
+    if (w < 4) {
+        tile_inputs((s == 0 ? a.obs : a.next) + ((int64_t)b * T + t) * 7, h, xs);
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int row = 32 * jt + col, kk = 2 * s4 + h;
+                f1w[jt][s4] = P[kk == 0 ? R_P_F1B + row : R_P_F1W + row * 7 + kk - 1];
+            }
         const float* w2 = P + R_P_F2W + (32 * w + col) * 64 + 4 * h;
 #pragma unroll
         for (int i = 0; i < 8; ++i) w2v[i] = *reinterpret_cast<const float4*>(w2 + 32 * (i >> 2) + 8 * (i & 3));
-    }
-    // F1 (both 32-row tiles, every wave): input k' = 2 s4 + h, k' = 0 the constant 1 (weight: b1)
-    f32x16 c1[2];
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-        const int row = 32 * jt + col;
-        c1[jt] = f32x16{};
+        for (int r = 0; r < 16; ++r) f2[r] = P[R_P_F2B + 32 * w + rho(r) + 4 * h];
+    } else {
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            const int kk = 2 * s4 + h;
-            const float wv = kk == 0 ? P[R_P_F1B + row] : P[R_P_F1W + row * 7 + kk - 1];
-            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv, xs[s4], c1[jt], 0, 0, 0);
+        for (int r = 0; r < 16; ++r) {
+            const int rr = rho(r) + 4 * h;
+            const int g = 128 * (rr >> 3) + 8 * m + (rr & 7);
+            zb[r] = P[R_P_BIH + g] + P[R_P_BHH + g];
         }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) c1[jt][r] = relu(c1[jt][r]);
     }
-    // F2 tile w: rows 32w + rho(r) + 4h; K = 64 over the two F1 tiles (k = 32 t2 + rho(r) + 4h)
-    f32x16 f2;
+#ifdef PM_DIAG
+    drain();
+    DQ_STAMP(228, blockIdx.x == 0);
+#endif
+    if (w < 4) {
+        // F1 (both 32-row tiles): input k' = 2 s4 + h, k' = 0 the constant 1 (weight: b1)
+        f32x16 c1[2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) f2[r] = P[R_P_F2B + 32 * w + rho(r) + 4 * h];
-    {
+        for (int jt = 0; jt < 2; ++jt) {
+            c1[jt] = f32x16{};
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(f1w[jt][s4], xs[s4], c1[jt], 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c1[jt][r] = relu(c1[jt][r]);
+        }
+        // F2 tile w: rows 32w + rho(r) + 4h; K = 64 over the two F1 tiles (k = 32 t2 + rho(r) + 4h)
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
@@ -294,40 +319,50 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
                 f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, c1[t2][4 * i + 2], f2, 0, 0, 0);
                 f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, c1[t2][4 * i + 3], f2, 0, 0, 0);
             }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) f2[r] = relu(f2[r]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<float4*>(&F2s[col][32 * w + 8 * i + 4 * h]) =
+                make_float4(f2[4 * i], f2[4 * i + 1], f2[4 * i + 2], f2[4 * i + 3]);
+        if (s == 0 && rq == 0) {  // the obs stream's features and inputs for the weight gradients, [unit][column]
+            const int64_t C0 = a.C0;
+            if (w == 0) {  // x^T from the tile operands: half 1 holds x0, x2, x4, x6, half 0 x1, x3, x5
+                if (h) a.XT[c] = xs[0];
+#pragma unroll
+                for (int i = 1; i < 4; ++i) a.XT[(int64_t)(2 * i - 1 + h) * C0 + c] = xs[i];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a.F2T[(int64_t)(32 * w + rho(r) + 4 * h) * C0 + c] = f2[r];
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt)
+                if (w == jt)  // static register index (c1[w] would be a 32-way select per element)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) a.F1T[(int64_t)(32 * jt + rho(r) + 4 * h) * C0 + c] = c1[jt][r];
+        }
     }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) f2[r] = relu(f2[r]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<float4*>(&F2s[col][32 * w + 8 * i + 4 * h]) =
-            make_float4(f2[4 * i], f2[4 * i + 1], f2[4 * i + 2], f2[4 * i + 3]);
-    if (s == 0 && rq == 0) {  // the obs stream's features and inputs for the weight gradients, [unit][column]
-        const int64_t C0 = a.C0;
-        if (w == 0 && h == 0)
-            for (int i = 0; i < 7; ++i) a.XT[(int64_t)i * C0 + c] = a.obs[((int64_t)b * T + t) * 7 + i];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) a.F2T[(int64_t)(32 * w + rho(r) + 4 * h) * C0 + c] = f2[r];
-        if (w < 2)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a.F1T[(int64_t)(32 * w + rho(r) + 4 * h) * C0 + c] = c1[w][r];
-    }
+    DQ_STAMP(223, blockIdx.x == 0);
     __syncthreads();
-    // Zx tile of recurrence workgroup m: K = 128 with k = 8j + 4h + e for k-step (j, e)
-    f32x16 z;
+    DQ_STAMP(224, blockIdx.x == 0);
+    // Zx tile m, K half kh: k = 64 kh + 8j + 4h + e for k-step (j, e)
+    f32x16 z = {};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rr = rho(r) + 4 * h;
-        const int g = 128 * (rr >> 3) + 8 * m + (rr & 7);
-        z[r] = P[R_P_BIH + g] + P[R_P_BHH + g];
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const float4 bv = *reinterpret_cast<const float4*>(&F2s[col][8 * j + 4 * h]);
+    for (int j = 0; j < 8; ++j) {
+        const float4 bv = *reinterpret_cast<const float4*>(&F2s[col][64 * kh + 8 * j + 4 * h]);
         z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, bv.x, z, 0, 0, 0);
         z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, bv.y, z, 0, 0, 0);
         z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, bv.z, z, 0, 0, 0);
         z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, bv.w, z, 0, 0, 0);
     }
+    DQ_STAMP(225, blockIdx.x == 0);
+    if (kh == 0)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) zp[w][r][lane] = z[r];
+    __syncthreads();
+    DQ_STAMP(226, blockIdx.x == 0);
+    if (kh == 0) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] = (zp[w & 3][r][lane] + z[r]) + zb[r];  // (K half 0 + K half 1) + bias
     // Zx[s][t][gate row][sequence]: a register's 32 columns are 128 contiguous bytes
     float* zx = a.ZX + ((int64_t)s * T + t) * 512 * B + b;
 #pragma unroll
@@ -335,7 +370,7 @@ __global__ __launch_bounds__(256) void k_dq_embed(DqArgs a) {
         const int rr = rho(r) + 4 * h;
         zx[(int64_t)(128 * (rr >> 3) + 8 * m + (rr & 7)) * B] = z[r];
     }
-    DQ_STAMP(222, blockIdx.x == 0);
+    PM_STAMP_T(222, 256);
 }
 
 // ---------------------------------------------------------------- 2: the recurrence (sequence-private)
@@ -509,12 +544,13 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
     const int net = tgt ? 1 : 0;
     DQ_STAMP(1, so0);
     DQ_STAMP(111, s10);
-    // the effective W_S image -> LDS (global_load_lds, 1 KB per wave instruction), lands during the forward
-    {
-        const float* src = a.WSE + (int64_t)net * 128 * kWsStride;
-        for (int k = w; k < 128 * kWsStride / 256; k += 16)
-            __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane), (lds_void*)&sm.ws[256 * k], 16, 0, 0);
-    }
+    // Zx of step 0 first (step 0 needs no Whh: h_0 = 0), then Whh, then the W_S image: the loads
+    // complete in issue order, so step 0's cell runs while Whh is still in flight
+    // Zx of this lane's column (the cell runs on the lanes of its column only)
+    const float* zx = a.ZX + (int64_t)(myc ? sc1 : sc0) * T * 512 * B + (int64_t)u * B + b;
+    float zn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)q * 128 * B];
     // Whh rows 128q + u, columns 16kg .. 16kg + 15
     float wr[4][16];
 #pragma unroll
@@ -526,11 +562,12 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
             wr[q][4 * i] = v.x; wr[q][4 * i + 1] = v.y; wr[q][4 * i + 2] = v.z; wr[q][4 * i + 3] = v.w;
         }
     }
-    // Zx of this lane's column (the cell runs on the lanes of its column only)
-    const float* zx = a.ZX + (int64_t)(myc ? sc1 : sc0) * T * 512 * B + (int64_t)u * B + b;
-    float zn[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)q * 128 * B];
+    // the effective W_S image -> LDS (global_load_lds, 1 KB per wave instruction), lands during the forward
+    {
+        const float* src = a.WSE + (int64_t)net * 128 * kWsStride;
+        for (int k = w; k < 128 * kWsStride / 256; k += 16)
+            __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane), (lds_void*)&sm.ws[256 * k], 16, 0, 0);
+    }
     // ---------------- forward
     float cst = 0.f;  // c of (unit u, column myc)
     for (int t = 0; t < T; ++t) {
@@ -799,12 +836,19 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
         if (w == 0) {
             const int ldg = mat <= 2 ? 128 : (mat == 3 ? 64 : 7);
             float* G = a.grad + (mat == 0 ? R_P_WIH : (mat == 1 ? R_P_WHH : (mat == 2 ? R_P_SWMU : (mat == 3 ? R_P_F2W : R_P_F1W))));
+            double sq = 0.0;  // this tile's share of the clip norm (local_norm), sigma gradients (mu x epsilon) included
             if (32 * kt + col < ldg)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     float v = sm.red[0][r][lane];
                     for (int k = 1; k < 16; ++k) v += sm.red[k][r][lane];
-                    G[(int64_t)(32 * gt + rho(r) + 4 * h) * ldg + 32 * kt + col] = v;
+                    const int e = (32 * gt + rho(r) + 4 * h) * ldg + 32 * kt + col;
+                    G[e] = v;
+                    sq += (double)v * (double)v;
+                    if (mat == 2) {
+                        const float gs = v * a.params[R_P_SWEP + e];
+                        sq += (double)gs * (double)gs;
+                    }
                 }
             DQ_STAMP(211, bid == 0);
             if (mat != 1 && kt == 0) {  // the bias gradients: row sums
@@ -817,13 +861,24 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
                     else if (mat == 2) a.grad[R_P_SBMU + row] = v;
                     else if (mat == 3) a.grad[R_P_F2B + row] = v;
                     else a.grad[R_P_F1B + row] = v;
+                    sq += (mat == 0 ? 2.0 : 1.0) * ((double)v * (double)v);
+                    if (mat == 2) {
+                        const float gs = v * a.params[R_P_SBEP + row];
+                        sq += (double)gs * (double)gs;
+                    }
                 }
+            }
+            if (a.local_norm) {
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+                if (lane == 0) a.NP[bid] = sq;
             }
         }
         return;
     }
     // ---- the V / A head gradients: dw_o[r] = sum_b dQ_o[b] ReLU(S)[r][b] (o = V, A0..2) and their biases,
     // the loss and mean Q, each summed over the sequences in order
+    double sq = 0.0;
     if (tid < 512) {
         const int o = tid >> 7, r = tid & 127;
         const float* sr = a.SR + (int64_t)r * B;
@@ -835,7 +890,10 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) v = fmaf(c[i], x[i], v);
         }
-        a.grad[o == 0 ? R_P_VWMU + r : R_P_AWMU + 128 * (o - 1) + r] = v;
+        const int e = o == 0 ? r : 128 * (o - 1) + r;
+        a.grad[(o == 0 ? R_P_VWMU : R_P_AWMU) + e] = v;
+        const float gs = v * a.params[(o == 0 ? R_P_VWEP : R_P_AWEP) + e];
+        sq = (double)v * (double)v + (double)gs * (double)gs;
     } else if (tid < 518) {
         const int o = tid - 512;  // dV, dA0..2, loss, Q(s, a)
         float v = 0.f;
@@ -850,6 +908,20 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
         else if (o < 4) a.grad[R_P_ABMU + o - 1] = v;
         else if (o == SC_LOSS) a.stats->loss = v / (float)B;
         else a.stats->q_mean = v / (float)B;
+        if (o < 4) {
+            const float gs = v * a.params[o == 0 ? R_P_VBEP : R_P_ABEP + o - 1];
+            sq = (double)v * (double)v + (double)gs * (double)gs;
+        }
+    }
+    if (a.local_norm) {  // the block's squares, summed in a fixed tree
+        double* red = reinterpret_cast<double*>(&sm.red[0][0][0]);
+        red[tid] = sq;
+        __syncthreads();
+        for (int k = 512; k > 0; k >>= 1) {
+            if (tid < k) red[tid] += red[tid + k];
+            __syncthreads();
+        }
+        if (tid == 0) a.NP[kWgTiles] = red[0];
     }
 }
 
@@ -911,6 +983,10 @@ __global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* pa
             sq += (double)g[e] * (double)g[e];
         }
     }
+    if (a.local_norm) {  // one replica: k_dq_wgrad's blocks already summed the squares, no arrival needed
+        static_assert(kWgTiles + 1 <= 256, "norm partials");
+        red[threadIdx.x] = (int)threadIdx.x <= kWgTiles ? a.NP[threadIdx.x] : 0.0;
+    } else {
     red[threadIdx.x] = sq;
     __syncthreads();
     for (int kk = 128; kk > 0; kk >>= 1) {
@@ -937,6 +1013,7 @@ __global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* pa
     __syncthreads();
     if (late) return;  // block-uniform
     red[threadIdx.x] = __hip_atomic_load(a.part + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
     for (int kk = 128; kk > 0; kk >>= 1) {  // the same fixed tree in every block
         if (threadIdx.x < kk) red[threadIdx.x] += red[threadIdx.x + kk];
@@ -1014,7 +1091,7 @@ extern "C" int64_t pm_drqn_work_bytes(int32_t batch, int32_t T) {
     return dq_layout(batch, T, nullptr, nullptr);
 }
 
-extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
+static int drqn_grads(const pm_drqn* d, void* stream, int local_norm) {
     if (int rc = check(d)) return rc;
     PM_REQUIRE(d->obs && d->next && d->act && d->rew && d->done, PM_E_ARG, "pm_drqn_grads: null batch");
     hipStream_t st = pm_stream(stream);
@@ -1024,7 +1101,8 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     a.obs = d->obs; a.next = d->next; a.act = d->act; a.rew = d->rew; a.done = d->done;
     a.gamma = (float)d->gamma;
     a.poll_limit = d->poll_limit;
-    hipLaunchKernelGGL(k_dq_embed, dim3(3 * a.nct * a.T * 4), dim3(256), 0, st, a);
+    a.local_norm = local_norm;
+    hipLaunchKernelGGL(k_dq_embed, dim3(3 * a.nct * a.T * 4 + kEmbEff), dim3(512), 0, st, a);
     PM_LAUNCHED("k_dq_embed");
     pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(3 * a.B), dim3(kRecThreads), st, a);
     PM_LAUNCHED("k_dq_recur");
@@ -1033,11 +1111,12 @@ extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) {
     return PM_OK;
 }
 
-extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) {
+static int drqn_apply(const pm_drqn* d, void* stream, int local_norm) {
     if (int rc = check(d)) return rc;
     hipStream_t st = pm_stream(stream);
     DqArgs a{};
     dq_layout(d->batch, d->T, &a, d->work);
+    a.local_norm = local_norm;
     a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats;
     AdamK k{d->lr, d->beta1, d->beta2, d->adam_eps, d->max_norm, d->target_update_interval};
     hipLaunchKernelGGL(k_drqn_apply, dim3(kNormBlocks), dim3(256), 0, st, a, k, d->params, d->target, d->adam_m,
@@ -1046,7 +1125,12 @@ extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) {
     return PM_OK;
 }
 
+extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) { return drqn_grads(d, stream, 0); }
+extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) { return drqn_apply(d, stream, 0); }
+
+// One replica: the weight-gradient blocks sum the clip norm's squares as they store the gradient, so
+// the apply needs no arrival ticket (replicas that all-reduce call pm_drqn_grads / pm_drqn_apply).
 extern "C" int pm_drqn_update(const pm_drqn* d, void* stream) {
-    if (int rc = pm_drqn_grads(d, stream)) return rc;
-    return pm_drqn_apply(d, stream);
+    if (int rc = drqn_grads(d, stream, 1)) return rc;
+    return drqn_apply(d, stream, 1);
 }

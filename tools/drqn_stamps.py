@@ -14,14 +14,14 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-NAMES = {220: "embed start", 222: "embed block 0 end", 1: "recur obs WG start", 111: "recur target WG 0 start"}
+NAMES = {220: "embed start", 222: "embed block 0 end (wave 4)", 1: "recur obs WG start", 111: "recur target WG 0 start"}
 for t in range(20):
     NAMES[10 + t] = f"  obs fwd step {t} done (barrier)"
     NAMES[120 + t] = f"  tgt fwd step {t} done (barrier)"
     NAMES[90 + t] = f"  obs bwd step {t}: dh_(t-1) reduced"
 for t in range(20):
     NAMES[180 + t] = f"  dF2 trailer step {t}: dF2 reduced"
-NAMES.update({8: "dF2 trailer 0 start", 7: "dF2 trailer 0 end", 50: "obs heads: Q formed", 150: "target WG 0: Q published", 51: "obs: target Q gathered, loss",
+NAMES.update({228: "embed b0: first loads landed (diag drain)", 227: "embed b0: after setup", 223: "embed b0: F1/F2 done (thread 0)", 224: "embed b0: F2 barrier", 225: "embed b0: Zx MFMAs done", 226: "embed b0: halves barrier", 8: "dF2 trailer 0 start", 7: "dF2 trailer 0 end", 50: "obs heads: Q formed", 150: "target WG 0: Q published", 51: "obs: target Q gathered, loss",
               52: "obs: dh_T reduced", 2: "recur obs WG end", 210: "wgrad A start", 211: "wgrad A tile done",
               200: "wgrad B start", 201: "wgrad B dF2 done", 204: "wgrad B dF1 done", 206: "wgrad B ticket",
               207: "wgrad last tile: reduce start", 208: "wgrad last tile: reduce end"})

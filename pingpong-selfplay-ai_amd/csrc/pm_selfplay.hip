@@ -756,7 +756,7 @@ struct LearnSmem {
     union {
         float gpart[16][256];  // gradient phase: per-wave partial sums
     } u;
-    float Hs[PM_MAX_BATCH][65];  // ReLU(features(s)) of the batch
+    __attribute__((aligned(16))) float Hs[PM_MAX_BATCH][64];  // ReLU(features(s)) of the batch (LDS DMA rows)
     float qv[PM_MAX_BATCH][12];  // Q_B(s) 0..2 | Q_B(s') 4..6 | Q_T(s') 8..10
     float coef[PM_MAX_BATCH][4]; // dL/d(V, A0, A1, A2) per sample
     float eps_tr[pad256(260)];    // the update's noise (eps section layout)
@@ -836,16 +836,13 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     const float wraw_l = t < B ? sp.isw[t] : 0.f;
     const int64_t id_l = t < B ? sp.idx[t] : 0;
     const float eps_v = t < 260 ? sp.learn_heads[528 + t] : 0.f;
-    // the rows k_env's forward blocks computed (hfeat [B][80]): a quarter of sample t/4 per thread
-    const int hj = t >> 2, hq = (t & 3) * 20;
-    float hv[20];
+    // the rows k_env's forward blocks computed (hfeat [B][80]): sample t's Q block (floats 64..75,
+    // phase 2's operands) to registers here; its 64 features go global -> LDS below, behind them
+    float4 qh[3];
     {
-        const float4* src = reinterpret_cast<const float4*>(sp.hfeat + (size_t)min(hj, B - 1) * 80 + hq);
+        const float4* src = reinterpret_cast<const float4*>(sp.hfeat + (size_t)min(t, B - 1) * 80 + 64);
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const float4 v = src[k];
-            hv[4 * k] = v.x; hv[4 * k + 1] = v.y; hv[4 * k + 2] = v.z; hv[4 * k + 3] = v.w;
-        }
+        for (int k = 0; k < 3; ++k) qh[k] = src[k];
     }
     for (int b = t + kLearn; first && b < nbr; b += kLearn)  // n > 256 * 1024 arenas only
 #pragma unroll
@@ -874,19 +871,14 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         if (ip) sm.plist[wv * 64 + __popcll(m & ((1ull << lane) - 1ull))] = t;
         if (lane == 0) sm.pcnt[wv] = __popcll(m);
     }
-    if (train && hj < B) {
+    if (train && t < B)
 #pragma unroll
-        for (int k = 0; k < 20; ++k) {
-            const int f = hq + k;
-            if (f < 64) sm.Hs[hj][f] = hv[k];
-            else if (f < 76) sm.qv[hj][f - 64] = hv[k];
-        }
-    }
+        for (int k = 0; k < 3; ++k) *reinterpret_cast<float4*>(&sm.qv[t][4 * k]) = qh[k];
 #ifdef PM_DIAG
     PM_STAMP(30);
     asm volatile("" ::"v"(wraw_l), "v"((int)id_l));
     PM_STAMP(31);
-    asm volatile("" ::"v"(hv[0]), "v"(hv[19]));
+    asm volatile("" ::"v"(qh[0].x), "v"(qh[2].w));
     PM_STAMP(32);
     PM_STAMP(33);
 #endif
@@ -906,6 +898,15 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's loads (incl. LDS DMA) landed
     PM_STAMP_T(40, 0); PM_STAMP_T(41, 256); PM_STAMP_T(42, 512); PM_STAMP_T(43, 960);
 #endif
+    // ReLU(features(s)) of the batch: each hfeat row's 64 floats global -> LDS (4 rows per wave
+    // instruction), issued after every register load of this phase so nothing here waits on them; the
+    // first reader is phase 3 (drained before phase 2's barrier, or before the push-row copy)
+    if (train)
+        for (int ci = wv; 4 * ci < B; ci += kLearn / 64) {
+            const int row = min(4 * ci + (lane >> 4), B - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(sp.hfeat + (size_t)row * 80 + 4 * (lane & 15)),
+                                             (lds_void*)&sm.Hs[4 * ci][0], 16, 0, 0);
+        }
     __syncthreads();
     PM_STAMP(1);
 
@@ -930,6 +931,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         if (np > 0 && push_handoff(mode, train)) {  // block-uniform: block 1 computes them
             waited = true;
             if (t == 0 && !push_wait(sp, cs)) sm.void_upd = 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the feature rows' DMA, before rows are overwritten
             __syncthreads();
             PM_STAMP(54);
             const float* pay = sp.hfeat + (size_t)B * 80;
@@ -1005,6 +1007,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             for (int k = 0; k < 4; ++k) sm.red[wv][3 + k] = cf[k];
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the feature rows (phase 3 reads them)
     __syncthreads();
     PM_STAMP(3);
 

@@ -106,9 +106,12 @@ def test_drqn_update_matches_reference(golden, orc):
     assert torch.equal(sd["fc_A.weight_epsilon"], _sd(gr)["fc_A.weight_epsilon"])
 
 
-@pytest.mark.parametrize("B,T", [(32, 3), (96, 5), (64, 1)])
+@pytest.mark.parametrize("B,T", [(32, 3), (96, 5), (64, 1), (256, 8), (32, 64)])
 def test_drqn_against_oracle_ragged(golden, orc, B, T):
-    """Other batch / sequence sizes against the oracle, with a target net that differs from modelB."""
+    """Other batch / sequence sizes against the oracle, with a target net that differs from modelB.
+    (256, 8) is the largest batch: k_dq_recur's 3 x 256 workgroups of 1024 threads are more than the
+    chip holds at once, so the waits on lower-indexed workgroups (target Q, BPTT's dz) run with later
+    workgroups not yet resident; (32, 64) is the longest sequence (T <= 64)."""
     from pongmi.drqn import DRQNLearner
     gr = golden("rnn")
     sd = {k[7:]: v for k, v in gr.items() if k.startswith("params.")}

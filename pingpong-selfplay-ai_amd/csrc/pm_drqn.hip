@@ -879,16 +879,27 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
     // ---- the V / A head gradients: dw_o[r] = sum_b dQ_o[b] ReLU(S)[r][b] (o = V, A0..2) and their biases,
     // the loss and mean Q, each summed over the sequences in order
     double sq = 0.0;
+    // the per-sequence scalars -> LDS once (coalesced), beside each thread's ReLU(S) row loads
+    float* scs = &sm.red[0][0][0];  // [B][8]
+    for (int i = tid; i < B * 8; i += 1024) scs[i] = a.SC[i];
+    __syncthreads();
     if (tid < 512) {
         const int o = tid >> 7, r = tid & 127;
-        const float* sr = a.SR + (int64_t)r * B;
+        const float4* sr = reinterpret_cast<const float4*>(a.SR + (int64_t)r * B);
         float v = 0.f;
-        for (int b0 = 0; b0 < B; b0 += 16) {  // 32 loads in flight, then the 16 fmaf in sequence order
-            float c[16], x[16];
+        for (int b0 = 0; b0 < B; b0 += 64) {  // 16 float4 loads in flight, then the fmaf in sequence order
+            float4 x[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) { c[i] = a.SC[(b0 + i) * 8 + SC_DV + o]; x[i] = sr[b0 + i]; }
+            for (int i = 0; i < 16; ++i) x[i] = b0 + 4 * i < B ? sr[b0 / 4 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v = fmaf(c[i], x[i], v);
+            for (int i = 0; i < 16; ++i) {
+                if (b0 + 4 * i >= B) break;
+                const int b = b0 + 4 * i;
+                v = fmaf(scs[b * 8 + SC_DV + o], x[i].x, v);
+                v = fmaf(scs[(b + 1) * 8 + SC_DV + o], x[i].y, v);
+                v = fmaf(scs[(b + 2) * 8 + SC_DV + o], x[i].z, v);
+                v = fmaf(scs[(b + 3) * 8 + SC_DV + o], x[i].w, v);
+            }
         }
         const int e = o == 0 ? r : 128 * (o - 1) + r;
         a.grad[(o == 0 ? R_P_VWMU : R_P_AWMU) + e] = v;
@@ -897,13 +908,7 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
     } else if (tid < 518) {
         const int o = tid - 512;  // dV, dA0..2, loss, Q(s, a)
         float v = 0.f;
-        for (int b0 = 0; b0 < B; b0 += 16) {
-            float c[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) c[i] = a.SC[(b0 + i) * 8 + o];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) v += c[i];
-        }
+        for (int b = 0; b < B; ++b) v += scs[b * 8 + o];
         if (o == 0) a.grad[R_P_VBMU] = v;
         else if (o < 4) a.grad[R_P_ABMU + o - 1] = v;
         else if (o == SC_LOSS) a.stats->loss = v / (float)B;
@@ -914,7 +919,7 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
         }
     }
     if (a.local_norm) {  // the block's squares, summed in a fixed tree
-        double* red = reinterpret_cast<double*>(&sm.red[0][0][0]);
+        double* red = reinterpret_cast<double*>(&sm.red[0][0][0]) + 1024;  // past scs ([B][8] <= 8 KB)
         red[tid] = sq;
         __syncthreads();
         for (int k = 512; k > 0; k >>= 1) {

@@ -392,8 +392,12 @@ __global__ __launch_bounds__(512) void k_dq_embed(DqArgs a) {
 // modelB on `obs` (column 0, the one BPTT runs on) and on `next` (column 1) of sequence b. The only
 // cross-workgroup hand-off is targetB's Q(s_T) (one granule pair per sequence, tag E + 1); the
 // target workgroups come first in the grid, so they are resident before any workgroup polls them.
+constexpr int kGcLds = (2 * 128 * 68) / 768;  // T up to which the obs workgroup keeps its gate scratch in LDS
+static_assert(128 * kWsStride <= 2 * 128 * 68, "W_S image in ws");
 struct RecurSmem {
-    __attribute__((aligned(16))) float ws[128 * kWsStride];  // effective W_S (DMA image of WSE)
+    // effective W_S (DMA image of WSE); once the heads hold it in registers, the obs workgroup's BPTT
+    // reduction buffer (same shape as part) when part holds the forward's gate scratch
+    __attribute__((aligned(16))) float ws[2 * 128 * 68];
     __attribute__((aligned(16))) float part[2][128][68];     // W^T dz partials [k][set, swizzled], by parity
     __attribute__((aligned(16))) float hs[2][288];           // h [unit][column], 4 floats of pad per 16 units
     float sr[2][128];                                        // ReLU(S) per column
@@ -569,6 +573,8 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
             __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane), (lds_void*)&sm.ws[256 * k], 16, 0, 0);
     }
     // ---------------- forward
+    const bool gl_lds = !tgt && T <= kGcLds;  // block-uniform
+    float* gl = &sm.part[0][0][0];
     float cst = 0.f;  // c of (unit u, column myc)
     for (int t = 0; t < T; ++t) {
         float z[4];
@@ -611,7 +617,11 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         cst = gf * cst + gi * gg;  // cy = forgetgate * cx + ingate * cellgate
         const float hn = go * tanh_hw(cst);
         if (kg < 2) sm.hs[(t + 1) & 1][hidx(u) + kg] = hn;
-        if (!tgt) {  // the obs column (kg even): BPTT's scratch and the weight gradients' h
+        if (!tgt && gl_lds) {  // the obs column (kg even): BPTT's scratch and h in LDS, [t][6][128]
+            float* g = gl + t * 768 + u;
+            if (kg == 0) { g[0] = gi; g[128] = gf; g[512] = cst; g[640] = hn; }
+            else if (kg == 2) { g[256] = gg; g[384] = go; }
+        } else if (!tgt) {  // the same in global memory (long sequences)
             float* gc = a.GC + ((int64_t)b * T + t) * 640 + u;
             if (kg == 0) {
                 gc[0] = gi; gc[128] = gf; gc[512] = cst;
@@ -685,6 +695,10 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         return;
     }
     DQ_STAMP(50, so0);
+    if (gl_lds)  // the weight gradients' H [unit][t * B + b]: h_t, the input hidden of step t (h_0 = 0)
+        for (int t = kg; t < T; t += 8) a.H[(int64_t)u * C0 + (int64_t)t * B + b] = t == 0 ? 0.f : gl[(t - 1) * 768 + 640 + u];
+    // BPTT's reduction buffer: ws once every wave holds its W_S rows (the heads' barriers), part otherwise
+    float (*const red)[128][68] = gl_lds ? reinterpret_cast<float (*)[128][68]>(sm.ws) : sm.part;
     // ---------------- the loss and dQ (obs column), wave 0
     if (w == 0) {
         poll_tags(a.QT, b * 32 + 24, 1, E + 1, hc);
@@ -725,27 +739,29 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         float p[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) p[j] = wsr[j] * dsm;
-        dh = reduce_units(p, sm.part[T & 1], lane, w, u, kg);
+        dh = reduce_units(p, red[T & 1], lane, w, u, kg);
     }
     DQ_STAMP(52, so0);
     // ---------------- BPTT (obs column)
-    const float* gcb = a.GC + (int64_t)b * T * 640 + u;
+    // the saved gates of step t: LDS [t][6][128] or global [t][5][128] (stride sg per step)
+    const float* gcb = gl_lds ? gl + u : a.GC + (int64_t)b * T * 640 + u;
+    const int sg = gl_lds ? 768 : 640;
     float gn[6];  // gi gf gg go c_t c_{t-1} of the next step down
     {
-        const float* g = gcb + (int64_t)(T - 1) * 640;
+        const float* g = gcb + (int64_t)(T - 1) * sg;
 #pragma unroll
         for (int v = 0; v < 5; ++v) gn[v] = g[128 * v];
-        gn[5] = T > 1 ? g[512 - 640] : 0.f;
+        gn[5] = T > 1 ? g[512 - sg] : 0.f;
     }
     float dc = 0.f;
     const __amdgpu_buffer_rsrc_t rdz = rsrc(a.DZH);
     for (int t = T - 1; t >= 0; --t) {
         const float gi = gn[0], gf = gn[1], gg = gn[2], go = gn[3], cT = gn[4], cP = gn[5];
         if (t > 0) {
-            const float* g = gcb + (int64_t)(t - 1) * 640;
+            const float* g = gcb + (int64_t)(t - 1) * sg;
 #pragma unroll
             for (int v = 0; v < 5; ++v) gn[v] = g[128 * v];
-            gn[5] = t > 1 ? g[512 - 640] : 0.f;
+            gn[5] = t > 1 ? g[512 - sg] : 0.f;
         }
         const float tc = tanh_hw(cT);
         const float dcc = dc + dh * go * (1.0f - tc * tc);
@@ -767,7 +783,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         float p[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) p[j] = fmaf(wr[3][j], dz3, fmaf(wr[2][j], dz2, fmaf(wr[1][j], dz1, wr[0][j] * dz0)));
-        dh = reduce_units(p, sm.part[t & 1], lane, w, u, kg);
+        dh = reduce_units(p, red[t & 1], lane, w, u, kg);
         DQ_STAMP(90 + t, so0 && t < 30);
     }
     DQ_STAMP(2, so0);

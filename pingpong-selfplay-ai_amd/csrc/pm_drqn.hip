@@ -389,11 +389,16 @@ __global__ __launch_bounds__(512) void k_dq_embed(DqArgs a) {
 //            over the wave's unit pairs (DPP row_ror 8), then over the 64 (wave, row) sets through LDS
 //            in a fixed order: one barrier per step.
 // Workgroups [0, B/2): targetB on `next`, sequences 2j and 2j + 1 (two columns); [B/2, B/2 + B):
-// modelB on `obs` (column 0, the one BPTT runs on) and on `next` (column 1) of sequence b. The only
-// cross-workgroup hand-off is targetB's Q(s_T) (one granule pair per sequence, tag E + 1); the
-// target workgroups come first in the grid, so they are resident before any workgroup polls them.
+// modelB on `obs` (column 0, the one BPTT runs on) and on `next` (column 1) of sequence b;
+// [3B/2, 5B/2): the dF2 trailer of sequence b. The forward's one cross-workgroup hand-off is targetB's
+// Q(s_T) (a granule pair per sequence, tag E + 1). A workgroup only ever waits on lower-indexed ones,
+// which the dispatcher has placed before it, so the launch cannot deadlock whatever is resident.
+constexpr int kGcLds = (2 * 128 * 68) / 768;  // T up to which the obs workgroup keeps its gate scratch in LDS
+static_assert(128 * kWsStride <= 2 * 128 * 68, "W_S image in ws");
 struct RecurSmem {
-    __attribute__((aligned(16))) float ws[128 * kWsStride];  // effective W_S (DMA image of WSE)
+    // effective W_S (DMA image of WSE); once the heads hold it in registers, the obs workgroup's BPTT
+    // reduction buffer (same shape as part) when part holds the forward's gate scratch
+    __attribute__((aligned(16))) float ws[2 * 128 * 68];
     __attribute__((aligned(16))) float part[2][128][68];     // W^T dz partials [k][set, swizzled], by parity
     __attribute__((aligned(16))) float hs[2][288];           // h [unit][column], 4 floats of pad per 16 units
     float sr[2][128];                                        // ReLU(S) per column
@@ -436,7 +441,7 @@ __device__ __forceinline__ float reduce_units(float (&p)[16], float (*part)[68],
     return sum8(d);
 }
 
-// The dF2 trailer (workgroups [2B, 3B), one per sequence): the feature layers' backward of the obs
+// The dF2 trailer (workgroups [3B/2, 5B/2), one per sequence): the feature layers' backward of the obs
 // stream, dF2_t = Wih^T dz_t, dP2 = dF2 (F2 > 0), then dF1 = W2^T dP2, dP1 = dF1 (F1 > 0) (k_dq_wgrad
 // forms dW2 = dP2 F1^T and dW1 = dP1 x^T as tiles). Wih sits in registers in Whh's fragment layout,
 // so dF2_t is BPTT's dh product on another matrix; each dz_t arrives from the sequence's obs
@@ -529,17 +534,20 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
     const int T = a.T, B = a.B;
     const int64_t C0 = a.C0;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, u = tid >> 3, kg = tid & 7, myc = kg & 1;
-    const int role = (int)blockIdx.x / B;  // 0 targetB on next, 1 modelB on obs + next, 2 the dF2 trailer
-    const int b = (int)blockIdx.x - role * B;
+    // [0, B/2) targetB on next (sequences 2j, 2j + 1 as the two columns), [B/2, 3B/2) modelB on obs and
+    // next of sequence b, [3B/2, 5B/2) the dF2 trailer of sequence b
+    const int nT = B >> 1, bx = (int)blockIdx.x;
+    const int role = bx < nT ? 0 : (bx < nT + B ? 1 : 2);
+    const int b = role == 0 ? 2 * bx : (role == 1 ? bx - nT : bx - nT - B);  // column 0's sequence
     const uint32_t E = (uint32_t)a.flags[0] << 7;  // this update's tag base
     const HandoffCtl hc{a.stats, a.grad + PM_RNN_NPARAM + 1, hand_limit(a.poll_limit)};
-    [[maybe_unused]] const bool so0 = (int)blockIdx.x == B, s10 = blockIdx.x == 0;  // stamping blocks (diag)
+    [[maybe_unused]] const bool so0 = bx == nT, s10 = bx == 0;  // stamping blocks (diag)
     if (role == 2) {
         dq_df2(a, sm, b, E, hc);
         return;
     }
     const bool tgt = role == 0;
-    const int sc0 = tgt ? 2 : 0, sc1 = tgt ? 2 : 1;  // column 1 of a target workgroup repeats column 0
+    const int sc0 = tgt ? 2 : 0, sc1 = tgt ? 2 : 1, bc1 = tgt ? b + 1 : b;  // (stream, sequence) of column 1
     const float* P = tgt ? a.target : a.params;
     const int net = tgt ? 1 : 0;
     DQ_STAMP(1, so0);
@@ -547,7 +555,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
     // Zx of step 0 first (step 0 needs no Whh: h_0 = 0), then Whh, then the W_S image: the loads
     // complete in issue order, so step 0's cell runs while Whh is still in flight
     // Zx of this lane's column (the cell runs on the lanes of its column only)
-    const float* zx = a.ZX + (int64_t)(myc ? sc1 : sc0) * T * 512 * B + (int64_t)u * B + b;
+    const float* zx = a.ZX + (int64_t)(myc ? sc1 : sc0) * T * 512 * B + (int64_t)u * B + (myc ? bc1 : b);
     float zn[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)q * 128 * B];
@@ -569,6 +577,8 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
             __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane), (lds_void*)&sm.ws[256 * k], 16, 0, 0);
     }
     // ---------------- forward
+    const bool gl_lds = !tgt && T <= kGcLds;  // block-uniform
+    float* gl = &sm.part[0][0][0];
     float cst = 0.f;  // c of (unit u, column myc)
     for (int t = 0; t < T; ++t) {
         float z[4];
@@ -611,7 +621,11 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         cst = gf * cst + gi * gg;  // cy = forgetgate * cx + ingate * cellgate
         const float hn = go * tanh_hw(cst);
         if (kg < 2) sm.hs[(t + 1) & 1][hidx(u) + kg] = hn;
-        if (!tgt) {  // the obs column (kg even): BPTT's scratch and the weight gradients' h
+        if (!tgt && gl_lds) {  // the obs column (kg even): BPTT's scratch and h in LDS, [t][6][128]
+            float* g = gl + t * 768 + u;
+            if (kg == 0) { g[0] = gi; g[128] = gf; g[512] = cst; g[640] = hn; }
+            else if (kg == 2) { g[256] = gg; g[384] = go; }
+        } else if (!tgt) {  // the same in global memory (long sequences)
             float* gc = a.GC + ((int64_t)b * T + t) * 640 + u;
             if (kg == 0) {
                 gc[0] = gi; gc[128] = gf; gc[512] = cst;
@@ -676,15 +690,19 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         q[c][2] = v + (x2 - mean);
     }
     if (tgt) {  // publish Q_target(s_T)
-        if (tid == 0) {
+        if (tid < 2) {  // column tid = sequence b + tid
             const __amdgpu_buffer_rsrc_t rq = rsrc(a.QT);
-            st_g2(rq, b * 32, q[0][0], q[0][1], E + 1);
-            st_g2(rq, b * 32 + 16, q[0][2], 0.f, E + 1);
+            st_g2(rq, (b + tid) * 32, q[tid][0], q[tid][1], E + 1);
+            st_g2(rq, (b + tid) * 32 + 16, q[tid][2], 0.f, E + 1);
         }
         DQ_STAMP(150, s10);
         return;
     }
     DQ_STAMP(50, so0);
+    if (gl_lds)  // the weight gradients' H [unit][t * B + b]: h_t, the input hidden of step t (h_0 = 0)
+        for (int t = kg; t < T; t += 8) a.H[(int64_t)u * C0 + (int64_t)t * B + b] = t == 0 ? 0.f : gl[(t - 1) * 768 + 640 + u];
+    // BPTT's reduction buffer: ws once every wave holds its W_S rows (the heads' barriers), part otherwise
+    float (*const red)[128][68] = gl_lds ? reinterpret_cast<float (*)[128][68]>(sm.ws) : sm.part;
     // ---------------- the loss and dQ (obs column), wave 0
     if (w == 0) {
         poll_tags(a.QT, b * 32 + 24, 1, E + 1, hc);
@@ -725,27 +743,29 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         float p[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) p[j] = wsr[j] * dsm;
-        dh = reduce_units(p, sm.part[T & 1], lane, w, u, kg);
+        dh = reduce_units(p, red[T & 1], lane, w, u, kg);
     }
     DQ_STAMP(52, so0);
     // ---------------- BPTT (obs column)
-    const float* gcb = a.GC + (int64_t)b * T * 640 + u;
+    // the saved gates of step t: LDS [t][6][128] or global [t][5][128] (stride sg per step)
+    const float* gcb = gl_lds ? gl + u : a.GC + (int64_t)b * T * 640 + u;
+    const int sg = gl_lds ? 768 : 640;
     float gn[6];  // gi gf gg go c_t c_{t-1} of the next step down
     {
-        const float* g = gcb + (int64_t)(T - 1) * 640;
+        const float* g = gcb + (int64_t)(T - 1) * sg;
 #pragma unroll
         for (int v = 0; v < 5; ++v) gn[v] = g[128 * v];
-        gn[5] = T > 1 ? g[512 - 640] : 0.f;
+        gn[5] = T > 1 ? g[512 - sg] : 0.f;
     }
     float dc = 0.f;
     const __amdgpu_buffer_rsrc_t rdz = rsrc(a.DZH);
     for (int t = T - 1; t >= 0; --t) {
         const float gi = gn[0], gf = gn[1], gg = gn[2], go = gn[3], cT = gn[4], cP = gn[5];
         if (t > 0) {
-            const float* g = gcb + (int64_t)(t - 1) * 640;
+            const float* g = gcb + (int64_t)(t - 1) * sg;
 #pragma unroll
             for (int v = 0; v < 5; ++v) gn[v] = g[128 * v];
-            gn[5] = t > 1 ? g[512 - 640] : 0.f;
+            gn[5] = t > 1 ? g[512 - sg] : 0.f;
         }
         const float tc = tanh_hw(cT);
         const float dcc = dc + dh * go * (1.0f - tc * tc);
@@ -767,7 +787,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         float p[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) p[j] = fmaf(wr[3][j], dz3, fmaf(wr[2][j], dz2, fmaf(wr[1][j], dz1, wr[0][j] * dz0)));
-        dh = reduce_units(p, sm.part[t & 1], lane, w, u, kg);
+        dh = reduce_units(p, red[t & 1], lane, w, u, kg);
         DQ_STAMP(90 + t, so0 && t < 30);
     }
     DQ_STAMP(2, so0);
@@ -1109,7 +1129,7 @@ static int drqn_grads(const pm_drqn* d, void* stream, int local_norm) {
     a.local_norm = local_norm;
     hipLaunchKernelGGL(k_dq_embed, dim3(3 * a.nct * a.T * 4 + kEmbEff), dim3(512), 0, st, a);
     PM_LAUNCHED("k_dq_embed");
-    pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(3 * a.B), dim3(kRecThreads), st, a);
+    pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(a.B / 2 + 2 * a.B), dim3(kRecThreads), st, a);
     PM_LAUNCHED("k_dq_recur");
     hipLaunchKernelGGL(k_dq_wgrad, dim3(kWgTiles + 1), dim3(1024), 0, st, a);
     PM_LAUNCHED("k_dq_wgrad");

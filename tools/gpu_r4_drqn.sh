@@ -11,4 +11,4 @@ python3 -c "
 import json; d=json.load(open('gpurun_out/r4d_rnn.json')); print('rnn', d['value'], d['ms_per_step'], json.dumps(d.get('drqn_roofline')))"
 timeout -k 10 120 python3 tools/drqn_stamps.py > gpurun_out/r4d_stamps.txt 2>&1; tail -n 40 gpurun_out/r4d_stamps.txt
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/r4d_prof -o drqn -- python3 tools/drqn_prof.py > gpurun_out/r4d_prof.log 2>&1
-f=$(find gpurun_out/r4d_prof -name '*kernel_stats.csv' | head -n 1); [ -n "$f" ] && cut -d, -f1-4 "$f" | head -n 12
+echo DRQN_PROF_DONE

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 L=pingpong-selfplay-ai_amd/pongmi
 for rep in 1 2; do
-for v in base fd2 fd4; do
+for v in base fd1 fd2; do
   lib=$L/libpongmi.so; [ $v != base ] && lib=$L/libpongmi_$v.so
   PONGMI_LIB=$(pwd)/$lib timeout -k 10 200 python3 bench.py --no-cpu-baseline > gpurun_out/r4fd_${v}_$rep.json 2> gpurun_out/r4fd_${v}_$rep.err || exit 1
   python3 -c "

@@ -347,11 +347,14 @@ extern "C" int pm_rnn_selfplay_act_part(const pm_rnn_selfplay* sp, int32_t part,
     return act_part(sp, part, 0, stream);
 }
 
-extern "C" int pm_rnn_selfplay_env(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {
-    if (int rc = check(sp)) return rc;
-    hipStream_t st = pm_stream(stream);
+namespace {
+int rsp_env_tick(const pm_rnn_selfplay* sp, hipStream_t st) {
     hipLaunchKernelGGL(k_rsp_env, dim3(pm_blocks(sp->n, kBlock)), dim3(kBlock), 0, st, *sp);
     PM_LAUNCHED("k_rsp_env");
+    return PM_OK;
+}
+// the episode-table append and the update's batch sample (after k_rsp_env, same stream)
+int rsp_append_sample(const pm_rnn_selfplay* sp, const pm_drqn* d, hipStream_t st) {
     hipLaunchKernelGGL(k_rsp_append, dim3(1), dim3(kAppend), 0, st, *sp);
     PM_LAUNCHED("k_rsp_append");
     if (d) {
@@ -362,6 +365,14 @@ extern "C" int pm_rnn_selfplay_env(const pm_rnn_selfplay* sp, const pm_drqn* d, 
         PM_LAUNCHED("k_rsp_sample");
     }
     return PM_OK;
+}
+}  // namespace
+
+extern "C" int pm_rnn_selfplay_env(const pm_rnn_selfplay* sp, const pm_drqn* d, void* stream) {
+    if (int rc = check(sp)) return rc;
+    hipStream_t st = pm_stream(stream);
+    if (int rc = rsp_env_tick(sp, st)) return rc;
+    return rsp_append_sample(sp, d, st);
 }
 
 extern "C" int pm_rnn_selfplay_sample(const pm_rnn_selfplay* sp, const pm_drqn* d, int32_t u, void* stream) {
@@ -411,14 +422,19 @@ int finish_overlap(const pm_rnn_selfplay* sp, const pm_drqn* d, pm_comm* comm, i
     PM_REQUIRE(side_stream && side_stream != stream, PM_E_ARG, "pm_rnn_selfplay_step_overlap: needs a second stream");
     hipEvent_t fork, join;
     if (int rc = step_events(fork, join)) return rc;
+    PM_REQUIRE(d->T == sp->T, PM_E_ARG, "pm_rnn_selfplay: learner T %d != %d", d->T, sp->T);  // before any launch
     hipStream_t st = pm_stream(stream), side = pm_stream(side_stream);
-    if (int rc = pm_rnn_selfplay_env(sp, d, stream)) return rc;
+    // the fork follows the env tick: side A reads only what k_rsp_env writes (observations, opponent
+    // ids, reset flags) and its own (h, c), so the episode-table append and the batch sample run
+    // beside it instead of in front of it
+    if (int rc = rsp_env_tick(sp, st)) return rc;
     hipError_t e = hipEventRecord(fork, st);
     if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
     PM_REQUIRE(e == hipSuccess, (int)e, "step_overlap fork: %s", hipGetErrorString(e));
     if (int rc = act_part(sp, PM_ACT_A, side_a_blocks(), side_stream)) return rc;
     e = hipEventRecord(join, side);
     PM_REQUIRE(e == hipSuccess, (int)e, "step_overlap join record: %s", hipGetErrorString(e));
+    if (int rc = rsp_append_sample(sp, d, st)) return rc;
     for (int u = 0; u < updates; ++u) {
         if (u)
             if (int rc = pm_rnn_selfplay_sample(sp, d, u, stream)) return rc;

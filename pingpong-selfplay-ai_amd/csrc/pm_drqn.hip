@@ -552,8 +552,8 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
     const int net = tgt ? 1 : 0;
     DQ_STAMP(1, so0);
     DQ_STAMP(111, s10);
-    // Zx of step 0 first (step 0 needs no Whh: h_0 = 0), then Whh, then the W_S image: the loads
-    // complete in issue order, so step 0's cell runs while Whh is still in flight
+    // Zx of step 0 first (step 0 needs no Whh: h_0 = 0), then Whh: the loads complete in issue
+    // order, so step 0's cell runs while Whh is still in flight
     // Zx of this lane's column (the cell runs on the lanes of its column only)
     const float* zx = a.ZX + (int64_t)(myc ? sc1 : sc0) * T * 512 * B + (int64_t)u * B + (myc ? bc1 : b);
     float zn[4];
@@ -570,53 +570,13 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
             wr[q][4 * i] = v.x; wr[q][4 * i + 1] = v.y; wr[q][4 * i + 2] = v.z; wr[q][4 * i + 3] = v.w;
         }
     }
-    // the effective W_S image -> LDS (global_load_lds, 1 KB per wave instruction), lands during the forward
-    {
-        const float* src = a.WSE + (int64_t)net * 128 * kWsStride;
-        for (int k = w; k < 128 * kWsStride / 256; k += 16)
-            __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane), (lds_void*)&sm.ws[256 * k], 16, 0, 0);
-    }
     // ---------------- forward
     const bool gl_lds = !tgt && T <= kGcLds;  // block-uniform
     float* gl = &sm.part[0][0][0];
     float cst = 0.f;  // c of (unit u, column myc)
-    for (int t = 0; t < T; ++t) {
-        float z[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) z[q] = zn[q];
-        if (t + 1 < T) {
-            const int64_t o = (int64_t)(t + 1) * 512 * B;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) zn[q] = zx[o + (int64_t)q * 128 * B];
-        }
-        float g4[4];
-        if (t > 0) {
-            float acc[4][2];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { acc[q][0] = 0.f; acc[q][1] = 0.f; }
-            const float* hp = &sm.hs[t & 1][36 * kg];  // units 16kg .. 16kg + 15, both columns
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float4 hv = *reinterpret_cast<const float4*>(hp + 4 * i);  // (k, c0) (k, c1) (k+1, c0) (k+1, c1)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    acc[q][0] = fmaf(wr[q][2 * i], hv.x, acc[q][0]);
-                    acc[q][1] = fmaf(wr[q][2 * i], hv.y, acc[q][1]);
-                    acc[q][0] = fmaf(wr[q][2 * i + 1], hv.z, acc[q][0]);
-                    acc[q][1] = fmaf(wr[q][2 * i + 1], hv.w, acc[q][1]);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                acc[q][0] = sum8(acc[q][0]);
-                acc[q][1] = sum8(acc[q][1]);
-                g4[q] = z[q] + (myc ? acc[q][1] : acc[q][0]);
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) g4[q] = z[q];
-        }
-        // the cell of unit u, column myc (v_exp_f32 / v_rcp_f32 activations, a few ulp)
+    // the cell of unit u, column myc (v_exp_f32 / v_rcp_f32 activations, a few ulp), then h to LDS
+    // and the obs column's scratch; one barrier
+    auto cell = [&](int t, const float (&g4)[4]) {
         const float gi = sig_hw(g4[0]), gf = sig_hw(g4[1]), gg = tanh_hw(g4[2]), go = sig_hw(g4[3]);
         cst = gf * cst + gi * gg;  // cy = forgetgate * cx + ingate * cellgate
         const float hn = go * tanh_hw(cst);
@@ -639,6 +599,60 @@ __global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
         __syncthreads();
         DQ_STAMP(10 + t, so0 && t < 30);
         DQ_STAMP(120 + t, s10 && t < 30);
+    };
+    {   // step 0, outside the loop (h_0 = 0: the gates are Zx alone), so its wait covers Zx only
+        float z[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z[q] = zn[q];
+        if (T > 1)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)512 * B + (int64_t)q * 128 * B];
+        cell(0, z);
+        // the effective W_S image -> LDS (global_load_lds, 1 KB per wave instruction), issued after
+        // step 0 (issued before it, the copy made step 0's Zx wait a vmcnt(0) behind Whh and itself);
+        // it lands beside Whh, which step 1 waits for anyway. kWsPieces per wave, the last clamped.
+        {
+            constexpr int kPieces = 128 * kWsStride / 256, kWsPieces = (kPieces + 15) / 16;
+            const float* src = a.WSE + (int64_t)net * 128 * kWsStride;
+#pragma unroll
+            for (int j = 0; j < kWsPieces; ++j) {
+                const int k = min(w + 16 * j, kPieces - 1);
+                __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane), (lds_void*)&sm.ws[256 * k], 16, 0, 0);
+            }
+        }
+    }
+    for (int t = 1; t < T; ++t) {
+        float z[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z[q] = zn[q];
+        if (t + 1 < T) {
+            const int64_t o = (int64_t)(t + 1) * 512 * B;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) zn[q] = zx[o + (int64_t)q * 128 * B];
+        }
+        float acc[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { acc[q][0] = 0.f; acc[q][1] = 0.f; }
+        const float* hp = &sm.hs[t & 1][36 * kg];  // units 16kg .. 16kg + 15, both columns
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 hv = *reinterpret_cast<const float4*>(hp + 4 * i);  // (k, c0) (k, c1) (k+1, c0) (k+1, c1)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc[q][0] = fmaf(wr[q][2 * i], hv.x, acc[q][0]);
+                acc[q][1] = fmaf(wr[q][2 * i], hv.y, acc[q][1]);
+                acc[q][0] = fmaf(wr[q][2 * i + 1], hv.z, acc[q][0]);
+                acc[q][1] = fmaf(wr[q][2 * i + 1], hv.w, acc[q][1]);
+            }
+        }
+        float g4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            acc[q][0] = sum8(acc[q][0]);
+            acc[q][1] = sum8(acc[q][1]);
+            g4[q] = z[q] + (myc ? acc[q][1] : acc[q][0]);
+        }
+        cell(t, g4);
     }
     // ---------------- heads: S = W_S h_T + b_S, V / A, Q for both columns
     drain();

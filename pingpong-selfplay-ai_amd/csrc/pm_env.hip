@@ -87,6 +87,132 @@ static __device__ unsigned long long pm_k1_diag[8][4096];
 // AR (autoreset): 0 none, 1 reset + full term rows (term row = the step's pre-reset observation),
 // 2 reset + term rows written for done arenas only (the other rows are left as they were).
 // WT: write-through outputs (pm_dev.h st_out), chosen by the arena count at launch.
+//
+// k_env_step_w (round 5, the default): the same tick with WAVE-level observation staging. Every wave
+// stages its own 64 rows in a private LDS slice and reads them back as float4s (the LDS operations of
+// one wave complete in issue order), so no workgroup barrier sits between a wave's tick and its
+// stores and each wave's serial chain is its own: load -> draw + tick -> LDS row staging -> one store
+// burst (observation float4s, state, rewards, done). The block variant above waited at
+// __syncthreads for the block's slowest wave (median 416, p90 1 332 cycles) between its state stores
+// and its observation stores (profiles/r4_k1_experiments.txt). PONGMI_K1_STG=0 selects it (A/B).
+template <int AR, bool INJ, bool WT>
+__global__ __launch_bounds__(kBlock) void k_env_step_w(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
+                                                       const int8_t* __restrict__ aB, float* __restrict__ obsA,
+                                                       float* __restrict__ obsB, float* __restrict__ rA,
+                                                       float* __restrict__ rB, uint8_t* __restrict__ done,
+                                                       float* __restrict__ tobsA, float* __restrict__ tobsB,
+                                                       const double* __restrict__ inject, int inject_cap,
+                                                       uint64_t seed, uint64_t ctr, int32_t* status, int n) {
+    __shared__ __attribute__((aligned(16))) float lds[4][kBlock][7];
+    constexpr bool DRAW = AR && !INJ;
+    const int t = threadIdx.x;
+    const int lane = t & 63, w0 = t & ~63;
+    const int iw = blockIdx.x * kBlock + w0;  // first arena of this wave
+    if (iw >= n) return;                      // whole wave past the end (no barrier in this kernel)
+    const int i = iw + lane;
+    const int wrows = min(64, n - iw);
+    const bool full_term = tobsA && AR != 2;
+    float oA[7] = {0}, oB[7] = {0}, tA[7], tB[7];
+    int d = 0;
+    Arena a{};
+    float ra = 0.f, rb = 0.f;
+    K1_STAMP(0);
+    if (i < n) {
+        int32_t ns = 0;
+        ServeDraw sv{};
+        if (INJ) ns = __builtin_nontemporal_load(&s.serves[i]);
+        a = load_arena(s, i);
+        const int xa = aA[i], xb = aB[i];
+        if (DRAW) {
+            sv = serve_draw(p, (uint32_t)i, (uint32_t)ctr, seed, TAG_SERVE_STEP, (uint32_t)(ctr >> 32));
+            asm volatile("" ::"v"(sv.vx), "v"(sv.vy), "v"(sv.spin), "v"(sv.rad));
+        }
+#ifdef PM_DIAG
+        K1_DRAIN();
+        K1_STAMP(1);
+#endif
+        d = tick(p, a, xa, xb, ra, rb);
+        K1_STAMP(2);
+        observe(a, oA, oB);
+        if (full_term) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) { lds[2][t][k] = oA[k]; lds[3][t][k] = oB[k]; }
+        }
+        if constexpr (DRAW) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) { tA[k] = oA[k]; tB[k] = oB[k]; }
+            serve_finish(sv);  // the rare |angle| >= 135 degree redo
+            Arena r = a;
+            serve(r, sv.vx, sv.vy, sv.spin);
+            a.x = d ? r.x : a.x; a.y = d ? r.y : a.y; a.vx = d ? r.vx : a.vx; a.vy = d ? r.vy : a.vy;
+            a.spin = d ? r.spin : a.spin; a.top = d ? r.top : a.top; a.bot = d ? r.bot : a.bot;
+            a.sA = d ? 0 : a.sA; a.sB = d ? 0 : a.sB; a.bounces = d ? 0 : a.bounces;
+            observe(a, oA, oB);
+        } else if (AR && d) {
+            if (AR == 2 && tobsA) {
+                store_row7(tobsA + (size_t)i * 7, oA);
+                store_row7(tobsB + (size_t)i * 7, oB);
+            }
+            const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
+            serve(a, r[0], r[1], r[2]);
+            s.serves[i] = ns + 1;
+            observe(a, oA, oB);
+        }
+    }
+    K1_STAMP(3);
+    // the wave's rows: LDS slice [w0, w0 + 64) of each staging array, 1 792 B, 16-B aligned
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { lds[0][t][k] = oA[k]; lds[1][t][k] = oB[k]; }
+    // wave-scope ordering only: the rows are read back by lanes of the same wave
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    K1_STAMP(4);
+    const int nq = full_term ? 4 : 2;
+    float* const dsts[4] = {obsA, obsB, tobsA, tobsB};
+    const size_t rowoff = (size_t)iw * 7;
+    bool vec = wrows == 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (q < nq) vec = vec && ((((uintptr_t)(dsts[q] + rowoff)) & 15) == 0);
+    if (vec) {
+        // read every float4 first, then one burst of stores: observations, state, rewards, done
+        float4 f[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q < nq) {
+                const float4* s4 = reinterpret_cast<const float4*>(&lds[q][w0][0]);
+                f[q][0] = s4[lane];
+                if (lane < 48) f[q][1] = s4[64 + lane];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q < nq) {
+                float4* d4 = reinterpret_cast<float4*>(dsts[q] + rowoff);
+                st_f4<WT>(d4 + lane, f[q][0]);
+                if (lane < 48) st_f4<WT>(d4 + 64 + lane, f[q][1]);
+            }
+        }
+    } else {
+        for (int q = 0; q < nq; ++q)
+            for (int e = lane; e < wrows * 7; e += 64) dsts[q][rowoff + e] = (&lds[q][w0][0])[e];
+    }
+    if (i < n) {
+        store_arena<WT>(s, i, a);
+        st_out<WT>(&rA[i], ra);
+        st_out<WT>(&rB[i], rb);
+        done[i] = (uint8_t)d;
+        if (DRAW && AR == 2 && tobsA && d) {
+            store_row7(tobsA + (size_t)i * 7, tA);
+            store_row7(tobsB + (size_t)i * 7, tB);
+        }
+    }
+    K1_STAMP(5);
+    K1_DRAIN();
+    K1_STAMP(6);
+}
+
 template <int AR, bool INJ, bool WT>
 __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
                                                      const int8_t* __restrict__ aB, float* __restrict__ obsA,
@@ -203,6 +329,15 @@ int k1_write_through(int32_t n) {
     return forced >= 0 ? (forced != 0) : (n <= kK1WtMax);
 }
 
+// Wave-level observation staging (k_env_step_w) unless PONGMI_K1_STG=0 (the block-barrier A/B).
+int k1_wave_staging() {
+    static const int v = [] {
+        const char* e = getenv("PONGMI_K1_STG");
+        return e && *e ? (atoi(e) != 0) : 1;
+    }();
+    return v;
+}
+
 bool state_ok(const pm_env_state* s) {
     return s && s->x && s->y && s->vx && s->vy && s->spin && s->top && s->bot && s->scoreA && s->scoreB &&
            s->bounces && s->serves;
@@ -238,14 +373,21 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
     using K = decltype(&k_env_step<0, false, false>);
-    static const K kernels[2][3][2] = {
-        {{k_env_step<0, false, false>, k_env_step<0, true, false>},
-         {k_env_step<1, false, false>, k_env_step<1, true, false>},
-         {k_env_step<2, false, false>, k_env_step<2, true, false>}},
-        {{k_env_step<0, false, true>, k_env_step<0, true, true>},
-         {k_env_step<1, false, true>, k_env_step<1, true, true>},
-         {k_env_step<2, false, true>, k_env_step<2, true, true>}}};
-    pm_launch(PM_TIMER_ENV_STEP, kernels[k1_write_through(n)][autoreset][inject != nullptr], dim3(pm_blocks(n, kBlock)),
+    static const K kernels[2][2][3][2] = {
+        {{{k_env_step<0, false, false>, k_env_step<0, true, false>},
+          {k_env_step<1, false, false>, k_env_step<1, true, false>},
+          {k_env_step<2, false, false>, k_env_step<2, true, false>}},
+         {{k_env_step<0, false, true>, k_env_step<0, true, true>},
+          {k_env_step<1, false, true>, k_env_step<1, true, true>},
+          {k_env_step<2, false, true>, k_env_step<2, true, true>}}},
+        {{{k_env_step_w<0, false, false>, k_env_step_w<0, true, false>},
+          {k_env_step_w<1, false, false>, k_env_step_w<1, true, false>},
+          {k_env_step_w<2, false, false>, k_env_step_w<2, true, false>}},
+         {{k_env_step_w<0, false, true>, k_env_step_w<0, true, true>},
+          {k_env_step_w<1, false, true>, k_env_step_w<1, true, true>},
+          {k_env_step_w<2, false, true>, k_env_step_w<2, true, true>}}}};
+    pm_launch(PM_TIMER_ENV_STEP, kernels[k1_wave_staging()][k1_write_through(n)][autoreset][inject != nullptr],
+              dim3(pm_blocks(n, kBlock)),
               dim3(kBlock), pm_stream(stream), *p, *s, aA, aB, obsA, obsB, rA, rB, done, term_obsA, term_obsB, inject,
               inject_cap, seed, counter, status, n);
     PM_LAUNCHED("k_env_step");

@@ -1,0 +1,75 @@
+#!/bin/bash
+# One parameterised GPU runner (round 5; replaces the per-round tools/gpu_r*.sh one-offs, which stay
+# only as the record of what earlier rounds ran). Every GPU step has its own time limit and the steps
+# are chained with &&: the first failure, timeout or fault ends the call.
+#
+#   gpurun --timeout 900 -- bash tools/gpu.sh <tag> <task> [<task> ...]
+#
+# tasks:
+#   suite      the whole `-m gpu` suite + smoke()
+#   env        tests/test_gpu_env.py only (K1 parity)
+#   k1         K1 A/B: graph-timed floor probe (tools/k1_floor), product K1 with PONGMI_K1_STG=1 / 0
+#              (tools/k1_time.py, bench.time_env_step), then rocprofv3 kernel traces of both
+#   k1stamp    per-wave K1 phase cycles (diag build, tools/k1_stamps.py)
+#   bench      python bench.py (the driver's default line)
+#   rnn        python bench.py --workload rnn
+#   infer      python bench.py --workload infer
+#   prof       rocprofv3 --kernel-trace --stats of the default bench (no CPU legs)
+#   pmc        the FETCH_SIZE / WRITE_SIZE passes of the default bench (tools/pmc_passes.sh)
+#   pmcrnn     the same for the RNN bench (tools/pmc_rnn_passes.sh)
+#   drqn       tests/test_gpu_drqn.py + tools/drqn_time.py
+#   pytest:<path>[::sel]  one test file / selection
+set -o pipefail
+export TMPDIR=/tmp
+tag=${1:?tag}; shift
+mkdir -p gpurun_out
+PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+run_task() {
+  case "$1" in
+    suite)
+      timeout -k 10 420 $PYT tests -m gpu > gpurun_out/${tag}_suite.log 2>&1 && tail -1 gpurun_out/${tag}_suite.log &&
+      timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 && echo SMOKE_OK ;;
+    env)
+      timeout -k 10 300 $PYT tests/test_gpu_env.py > gpurun_out/${tag}_env.log 2>&1 && tail -1 gpurun_out/${tag}_env.log ;;
+    k1)
+      timeout -k 10 120 ./tools/k1_floor 65536 > gpurun_out/${tag}_k1_floor.jsonl 2>&1 && cat gpurun_out/${tag}_k1_floor.jsonl &&
+      for stg in 1 0 1 0; do
+        echo "== PONGMI_K1_STG=$stg" >> gpurun_out/${tag}_k1_time.txt
+        PONGMI_K1_STG=$stg timeout -k 10 120 python3 tools/k1_time.py 65536 >> gpurun_out/${tag}_k1_time.txt 2>&1 || return 1
+      done && cat gpurun_out/${tag}_k1_time.txt &&
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_floor -o k -- \
+          ./tools/k1_floor 65536 > gpurun_out/${tag}_prof_floor.log 2>&1 &&
+      for stg in 1 0; do
+        PONGMI_K1_STG=$stg timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d gpurun_out/${tag}_prof_k1_stg$stg -o k -- python3 tools/k1_time.py 65536 \
+            > gpurun_out/${tag}_prof_k1_stg$stg.log 2>&1 || return 1
+      done && echo K1_OK ;;
+    k1stamp)
+      timeout -k 10 120 python3 tools/k1_stamps.py > gpurun_out/${tag}_k1_stamps.txt 2>&1 && cat gpurun_out/${tag}_k1_stamps.txt ;;
+    bench)
+      timeout -k 10 300 python3 bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err && echo BENCH_OK ;;
+    rnn)
+      timeout -k 10 300 python3 bench.py --workload rnn > gpurun_out/${tag}_rnn.json 2> gpurun_out/${tag}_rnn.err && echo RNN_OK ;;
+    infer)
+      timeout -k 10 300 python3 bench.py --workload infer > gpurun_out/${tag}_infer.json 2> gpurun_out/${tag}_infer.err && echo INFER_OK ;;
+    prof)
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof -o k -- \
+          python3 bench.py --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 && echo PROF_OK ;;
+    pmc)
+      timeout -k 10 600 bash tools/pmc_passes.sh ${tag} && echo PMC_OK ;;
+    pmcrnn)
+      timeout -k 10 600 bash tools/pmc_rnn_passes.sh ${tag} && echo PMCRNN_OK ;;
+    drqn)
+      timeout -k 10 300 $PYT tests/test_gpu_drqn.py > gpurun_out/${tag}_drqn.log 2>&1 && tail -1 gpurun_out/${tag}_drqn.log &&
+      timeout -k 10 120 python3 tools/drqn_time.py > gpurun_out/${tag}_drqn_time.txt 2>&1 && cat gpurun_out/${tag}_drqn_time.txt ;;
+    pytest:*)
+      sel=${1#pytest:}
+      timeout -k 10 400 $PYT "$sel" > gpurun_out/${tag}_pytest.log 2>&1 && tail -1 gpurun_out/${tag}_pytest.log ;;
+    *) echo "unknown task $1"; return 2 ;;
+  esac
+}
+for t in "$@"; do
+  echo "### $t"
+  run_task "$t" || { echo "FAILED: $t"; exit 1; }
+done
+echo ALL_OK

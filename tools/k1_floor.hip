@@ -1,0 +1,147 @@
+// K1 floor, measured the way the bench times K1: 50 back-to-back launches captured in one HIP graph,
+// HIP events around 40 replays (no host launch in the timed interval), 65 536 arenas unless given.
+// Not the product: it prices what a kernel with K1's shape costs before any tick arithmetic
+// (DESIGN.md, K1). Each skeleton moves exactly K1's bytes with K1's access widths:
+//   empty       256 blocks x 256 threads, no memory traffic
+//   loads       K1's loads (7 f64 + 3 i32 state, 2 i8 actions per arena), one dword stored per wave
+//   stores      K1's stores (state, rewards, done, both observation rows through wave-level LDS
+//               staging), nothing loaded
+//   copy        loads + stores, the state stored back unchanged: K1 minus the serve draw and tick
+// Run it bare (graph events) and under rocprofv3 --kernel-trace --stats (per-launch durations).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/k1_floor.hip -o tools/k1_floor && ./tools/k1_floor [n]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x)                                                                                        \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); }   \
+    } while (0)
+
+struct St {
+    double *x, *y, *vx, *vy, *spin, *top, *bot;
+    int *sA, *sB, *bn;
+    const signed char *aA, *aB;
+    float *obsA, *obsB, *rA, *rB;
+    unsigned char* done;
+};
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st4(float4* p, float4 v) {
+    const f4v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+}
+template <typename T>
+__device__ __forceinline__ void stw(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__global__ __launch_bounds__(256) void k_empty(St s, int n) {
+    if (n < 0 && threadIdx.x == 0) s.rA[0] = 1.f;  // never true
+}
+
+// MODE 1 loads, 2 stores, 3 copy
+template <int MODE>
+__global__ __launch_bounds__(256) void k_skel(St s, int n) {
+    __shared__ __attribute__((aligned(16))) float lds[2][256][7];
+    const int t = threadIdx.x, lane = t & 63, w0 = t & ~63;
+    const int iw = blockIdx.x * 256 + w0;
+    if (iw >= n) return;
+    const int i = iw + lane;
+    double x = 0.5, y = 0.5, vx = 0.01, vy = 0.02, sp = 0.0, top = 0.5, bot = 0.5;
+    int a = 0, b = 0, c = 0, xa = 1, xb = 2;
+    if (MODE & 1) {
+        x = s.x[i]; y = s.y[i]; vx = s.vx[i]; vy = s.vy[i]; sp = s.spin[i]; top = s.top[i]; bot = s.bot[i];
+        a = s.sA[i]; b = s.sB[i]; c = s.bn[i]; xa = s.aA[i]; xb = s.aB[i];
+    }
+    if (MODE == 1) {
+        const double z = x + y + vx + vy + sp + top + bot + (double)(a + b + c + xa + xb);
+        if (lane == 0) stw(&s.rA[i], (float)z);
+        return;
+    }
+    const float oA[7] = {(float)x, (float)(1.0 - y), (float)vx, (float)(-vy), (float)top, (float)bot, (float)sp};
+    const float oB[7] = {(float)x, (float)y, (float)vx, (float)vy, (float)bot, (float)top, (float)sp};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { lds[0][t][k] = oA[k]; lds[1][t][k] = oB[k]; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float4 f[2][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const float4* s4 = reinterpret_cast<const float4*>(&lds[q][w0][0]);
+        f[q][0] = s4[lane];
+        if (lane < 48) f[q][1] = s4[64 + lane];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        float4* d4 = reinterpret_cast<float4*>((q ? s.obsB : s.obsA) + (size_t)iw * 7);
+        st4(d4 + lane, f[q][0]);
+        if (lane < 48) st4(d4 + 64 + lane, f[q][1]);
+    }
+    stw(&s.x[i], x); stw(&s.y[i], y); stw(&s.vx[i], vx); stw(&s.vy[i], vy); stw(&s.spin[i], sp);
+    stw(&s.top[i], top); stw(&s.bot[i], bot); stw(&s.sA[i], a); stw(&s.sB[i], b); stw(&s.bn[i], c);
+    stw(&s.rA[i], (float)xa); stw(&s.rB[i], (float)xb);
+    s.done[i] = (unsigned char)((xa ^ xb) & 1);
+}
+
+typedef void (*Fn)(St, int);
+
+static double graph_us(Fn fn, St s, int n, hipStream_t st, int per_graph = 50, int replays = 40, int warm = 100) {
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+    for (int k = 0; k < per_graph; ++k) hipLaunchKernelGGL(fn, dim3((n + 255) / 256), dim3(256), 0, st, s, n);
+    CK(hipStreamEndCapture(st, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    for (int k = 0; k < warm; ++k) CK(hipGraphLaunch(ge, st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, st));
+    for (int k = 0; k < replays; ++k) CK(hipGraphLaunch(ge, st));
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+    return ms * 1e3 / (per_graph * replays);
+}
+
+int main(int argc, char** argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 65536;
+    St s;
+    double* f;
+    int* it;
+    CK(hipMalloc(&f, sizeof(double) * 7 * n));
+    CK(hipMalloc(&it, sizeof(int) * 3 * n));
+    CK(hipMemset(f, 0, sizeof(double) * 7 * n));
+    CK(hipMemset(it, 0, sizeof(int) * 3 * n));
+    s.x = f; s.y = f + n; s.vx = f + 2 * (size_t)n; s.vy = f + 3 * (size_t)n; s.spin = f + 4 * (size_t)n;
+    s.top = f + 5 * (size_t)n; s.bot = f + 6 * (size_t)n;
+    s.sA = it; s.sB = it + n; s.bn = it + 2 * (size_t)n;
+    signed char* acts;
+    CK(hipMalloc(&acts, 2 * n));
+    CK(hipMemset(acts, 1, 2 * n));
+    s.aA = acts; s.aB = acts + n;
+    float* o;
+    CK(hipMalloc(&o, sizeof(float) * 16 * (size_t)n));
+    s.obsA = o; s.obsB = o + 7 * (size_t)n; s.rA = o + 14 * (size_t)n; s.rB = o + 15 * (size_t)n;
+    CK(hipMalloc(&s.done, n));
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    const struct { const char* name; Fn fn; double bytes; } ks[] = {
+        {"empty", k_empty, 0.0},
+        {"loads", k_skel<1>, 70.0 * n},
+        {"stores", k_skel<2>, 133.0 * n},
+        {"copy", k_skel<3>, 203.0 * n},
+    };
+    for (int rep = 0; rep < 2; ++rep)
+        for (const auto& k : ks) {
+            const double us = graph_us(k.fn, s, n, st);
+            printf("{\"n\": %d, \"rep\": %d, \"kernel\": \"%s\", \"graph_us\": %.3f, \"bytes\": %.0f, \"frac_of_8TBs\": %.4f}\n",
+                   n, rep, k.name, us, k.bytes, k.bytes / (us * 1e-6) / 8e12);
+            fflush(stdout);
+        }
+    return 0;
+}

@@ -459,6 +459,72 @@ def drqn_update(sd, target_sd, adam, step, batch, lr=1e-4, gamma=0.99, max_norm=
     return new, info
 
 
+def clip_adam_f32(p, m, v, g, norm, at, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8, max_norm=1.0):
+    """clip_grad_norm_(max_norm) + torch's Adam step (train_rnn_iterative.py:509-516) restated in
+    float32 in the device apply's operation order (k_drqn_apply), the clip coefficient from a given
+    pre-clip norm: min(1, max_norm / (norm + 1e-6)); m.lerp_(g, 1 - b1); v.mul_(b2).addcmul_(g, g, 1 - b2);
+    p -= lr / bc1 * m / (sqrt(v) / sqrt(bc2) + eps). Returns (p, m, v, coef)."""
+    f = np.float32
+    coef = f(max_norm / (np.float64(f(norm)) + 1e-6))
+    coef = min(coef, f(1.0))
+    bc1, bc2 = 1.0 - b1 ** at, 1.0 - b2 ** at
+    step_size, bc2s = f(lr / bc1), f(np.sqrt(bc2))
+    gc = np.asarray(g, f) * coef
+    m = np.asarray(m, f) + f(1.0 - b1) * (gc - np.asarray(m, f))
+    v = np.asarray(v, f) * f(b2) + f(1.0 - b2) * gc * gc
+    denom = np.sqrt(v) / bc2s + f(eps)
+    return np.asarray(p, f) - step_size * (m / denom), m, v, coef
+
+
+def drqn_sigma_map(layout):
+    """For the packed QNetRNN block (`layout` = [(key, shape)] in block order, pongmi.rnn.PARAM_LAYOUT):
+    (sigma offsets, their mu offsets, their epsilon offsets), one entry per NoisyLinear sigma element."""
+    off, o = {}, 0
+    for k, s in layout:
+        off[k] = (o, int(np.prod(s)))
+        o += int(np.prod(s))
+    sig, mu, ep = [], [], []
+    for k, (o0, n) in off.items():
+        if k.endswith("_sigma"):
+            base = k[:-len("_sigma")]
+            sig.append(np.arange(o0, o0 + n))
+            mu.append(np.arange(off[base + "_mu"][0], off[base + "_mu"][0] + n))
+            ep.append(np.arange(off[base + "_epsilon"][0], off[base + "_epsilon"][0] + n))
+    return np.concatenate(sig), np.concatenate(mu), np.concatenate(ep)
+
+
+def drqn_apply_packed_f32(params, m, v, gbuf, steps, adam_t, layout, nparam, lr=1e-4, max_norm=1.0, interval=2000,
+                          target=None):
+    """The sharded DRQN apply (k_drqn_apply, after the all-reduce of the packed exchange buffer
+    `gbuf` = [nparam gradients (sigma slots 0) | contributing ranks | void count | ...]) restated in
+    float32 on packed blocks: no contributing rank -> nothing; a void count -> nothing (status 8);
+    else sigma gradient = summed mu gradient x epsilon, g = grad x (1 / ranks), the norm of that
+    global g (float64 sum of squares), clip + Adam (clip_adam_f32), the target copied every
+    `interval` steps. Returns dict(params, m, v, target, steps, adam_t, status, norm, coef, g)."""
+    f = np.float32
+    p, m, v = np.array(params, f), np.array(m, f), np.array(v, f)
+    tgt = None if target is None else np.array(target, f)
+    ranks = f(gbuf[nparam])
+    out = dict(params=p, m=m, v=v, target=tgt, steps=steps, adam_t=adam_t, status=0, norm=None, coef=None, g=None)
+    if not ranks > 0:
+        return out
+    if f(gbuf[nparam + 1]) != 0:
+        out["status"] = 8
+        return out
+    graw = np.array(gbuf[:nparam], f)
+    sig, mu, ep = drqn_sigma_map(layout)
+    graw[sig] = graw[mu] * p[ep]
+    g = graw * (f(1.0) / ranks)
+    norm = f(np.sqrt(np.sum(g.astype(np.float64) ** 2)))
+    at, ts = adam_t + 1, steps + 1
+    p2, m2, v2, coef = clip_adam_f32(p[:nparam], m, v, g, norm, at, lr=lr, max_norm=max_norm)
+    p[:nparam] = p2
+    if tgt is not None and ts % interval == 0:
+        tgt[:] = p
+    out.update(params=p, m=m2, v=v2, target=tgt, steps=ts, adam_t=at, norm=norm, coef=coef, g=g)
+    return out
+
+
 # ----------------------------------------------------------------------------- PER (numpy)
 def per_sample(prios, size, bs, beta, uniforms, alpha=0.6):
     """PrioritizedReplay.sample (scripts/train_iterative.py:64-73) with np.random.choice's own

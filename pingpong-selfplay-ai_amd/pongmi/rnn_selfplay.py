@@ -54,6 +54,31 @@ def ring_depth(n, memory_size, mean_len=40, margin=512):
     return d
 
 
+def sharded_rnn_vector_step(L, allreduce, updates):
+    """One vector step of a sharded QNetRNN learner as its launch sequence (RNNSelfPlayLearner.step
+    for world > 1 with a torch.distributed all-reduce; the Python twin of
+    pm_rnn_selfplay_step_sharded, csrc/pm_comm.cpp, whose all-reduce is libpongmi's RCCL call):
+
+      rollout (fold + act + env + sequence store + update 0's batch sample);
+      per update u: [sample(u) (u > 0)] + learner.grads() + allreduce(learner.grad) + learner.apply().
+
+    learner.grad is the packed exchange buffer: [0, PM_RNN_NPARAM) this rank's gradient (the
+    NoisyLinear sigma slots left zero: sigma gradients are mu gradient x epsilon, formed after the
+    sum), [PM_RNN_NPARAM] 1 if the rank contributed (its buffer was ready), [PM_RNN_NPARAM + 1] 1 if a
+    hand-off timed out on it (the update is then void on every rank). After the SUM every rank's
+    apply divides by the contributing-rank count, forms the sigma gradients, clips on the norm of
+    that summed gradient (train_rnn_iterative.py:509, clip_grad_norm_ on the global gradient) and
+    takes the identical Adam step (:510-516). `L` needs only these launch methods, so the CPU tests
+    drive this same sequence over gloo with oracle-backed shards."""
+    L.rollout()
+    for u in range(updates):
+        if u:
+            L.sample(u)
+        L.learner.grads()
+        allreduce(L.learner.grad)  # one all-reduce per update: 174 984 grads + rank count + void count
+        L.learner.apply()
+
+
 class RNNSelfPlayLearner:
     def __init__(self, env_kw, n_arenas, modelB_state, modelA_state=None, pool_states=(), *, batch=64, trace_length=8,
                  memory_size=200_000, min_episodes_for_training_start=10, depth=None, gamma=0.99, lr=1e-4,
@@ -264,13 +289,7 @@ class RNNSelfPlayLearner:
             check(self.lib.pm_rnn_selfplay_step_multi(ctypes.byref(self.sp), ctypes.byref(self.learner.desc), U,
                                                       stream_ptr()), "pm_rnn_selfplay_step_multi")
             return
-        self.rollout()
-        for u in range(U):
-            if u:
-                self.sample(u)
-            self.learner.grads()
-            self.allreduce(self.learner.grad)  # one RCCL all-reduce per update: 174 984 grads + rank count
-            self.learner.apply()
+        sharded_rnn_vector_step(self, self.allreduce, U)
 
     def check_status(self, c=None, log=print):
         """Device error bits (pm_rnn_ctrl.status): bit 0 (a sample read an overwritten ring step) means

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 19
+#define PM_ABI_VERSION 20
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -280,7 +280,11 @@ typedef struct pm_drqn {
                              * replica) and at [PM_RNN_NPARAM + 1] the number of ranks whose update
                              * timed out — all summed by the all-reduce; apply divides by the first
                              * and does nothing when the second is non-zero */
-    void *work;             /* pm_drqn_work_bytes(batch, T) bytes, 16-byte aligned */
+    void *work;             /* pm_drqn_work_bytes(batch, T) bytes, 16-byte aligned, ZERO-FILLED before the
+                             * first pm_drqn_* call that uses it (pm_drqn_init does it): the in-launch
+                             * hand-offs match granule tags against an epoch kept in the workspace, and
+                             * a stale granule whose tag happened to match (hipMalloc / reused memory)
+                             * would be read before its producer wrote it */
     pm_drqn_stats *stats;
     const float *obs, *next; /* [batch][T][7] */
     const int32_t *act;      /* [batch][T] */
@@ -297,6 +301,9 @@ typedef struct pm_drqn {
 } pm_drqn;
 
 int64_t pm_drqn_work_bytes(int32_t batch, int32_t T);
+/* Zero-fill d->work (pm_drqn_work_bytes(d->batch, d->T) bytes) on the stream (ABI 20): call once after
+ * allocating the workspace, before the first pm_drqn_grads / pm_drqn_update on it. */
+int pm_drqn_init(const pm_drqn *d, void *stream);
 /* Forward + BPTT: grad <- d loss / d params of this replica's batch, grad[PM_RNN_NPARAM] <- 1
  * (all zero when *enable == 0). The NoisyLinear sigma slots are left for pm_drqn_apply, which
  * forms them as mu gradient x epsilon (linear, identical epsilon on every rank). */
@@ -304,7 +311,11 @@ int pm_drqn_grads(const pm_drqn *d, void *stream);
 /* grad / grad[PM_RNN_NPARAM] -> clip_grad_norm_ -> Adam step -> target sync; stats updated.
  * Nothing happens when grad[PM_RNN_NPARAM] == 0. */
 int pm_drqn_apply(const pm_drqn *d, void *stream);
-/* pm_drqn_grads then pm_drqn_apply. */
+/* pm_drqn_grads then pm_drqn_apply, the clip norm summed by the weight-gradient tiles as they store
+ * (no arrival ticket). Its fp64 summation order differs from pm_drqn_apply's per-slice sum, so the two
+ * single-replica paths give bit-identical parameters while the clip coefficient clamps to 1 and agree
+ * to ~1e-6 relative when the clip is active (each is bitwise to the float32 clip + Adam restatement
+ * given its own norm). */
 int pm_drqn_update(const pm_drqn *d, void *stream);
 
 /* ---------------------------------------------------------------- QNetRNN self-play (K7) */

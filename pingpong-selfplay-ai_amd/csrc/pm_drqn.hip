@@ -1164,6 +1164,14 @@ static int drqn_apply(const pm_drqn* d, void* stream, int local_norm) {
     return PM_OK;
 }
 
+extern "C" int pm_drqn_init(const pm_drqn* d, void* stream) {
+    if (int rc = check(d)) return rc;
+    const int64_t bytes = dq_layout(d->batch, d->T, nullptr, nullptr);
+    PM_REQUIRE(hipMemsetAsync(d->work, 0, (size_t)bytes, pm_stream(stream)) == hipSuccess, PM_E_LAUNCH,
+               "pm_drqn_init: hipMemsetAsync failed");
+    return PM_OK;
+}
+
 extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) { return drqn_grads(d, stream, 0); }
 extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) { return drqn_apply(d, stream, 0); }
 

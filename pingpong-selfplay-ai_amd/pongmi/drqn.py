@@ -40,9 +40,9 @@ class DRQNLearner:
         nbytes = self.lib.pm_drqn_work_bytes(self.batch, self.T)
         if nbytes < 0:
             raise ValueError("invalid batch / T")
-        # zeroed once: the hand-off slots' tags and the tag epoch (flags[0]) must not start as whatever
-        # the allocator hands back (a stale granule whose tag matched would be read before its producer)
-        self.work = torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=self.device)
+        # zero-filled before first use (pm_drqn_init below): the hand-off slots' tags and the tag epoch
+        # (flags[0]) must not start as whatever the allocator hands back
+        self.work = torch.empty((nbytes + 15) // 16 * 4, dtype=torch.float32, device=self.device)
         self.stats_buf = torch.zeros(ctypes.sizeof(_lib.DrqnStats), dtype=torch.uint8, device=self.device)
         self.obs = torch.zeros((self.batch, self.T, 7), dtype=torch.float32, device=self.device)
         self.next = torch.zeros_like(self.obs)
@@ -61,6 +61,7 @@ class DRQNLearner:
             float(betas[1]), float(eps), float(max_norm)
         d.poll_limit = int(poll_limit)  # 0: the library default; < 0 is the tests' forced-timeout hook
         self.desc = d
+        self._call(self.lib.pm_drqn_init)  # the workspace zero-filled by the library (pongmi.h, ABI 20)
 
     def _block(self, m):
         if isinstance(m, torch.Tensor):

@@ -1,15 +1,13 @@
 """K6 — the DRQN update (pm_drqn_update) against train_step_rnn run on the reference QNetRNN with
-torch autograd (tests/golden/drqn.npz) and against the float64 oracle (oracle.drqn_update).
+torch autograd (tests/golden/drqn.npz) and against the float64 oracle (oracle.drqn_grads).
 
 Tolerances (fp32 on the device; exact-f32 MFMA sums in a different order than torch's CPU GEMMs):
-loss / pre-clip norm rtol 1e-4; gradients rtol 1e-3 with atol 1e-5 x the tensor's largest
-magnitude (the same bar the oracle meets against the reference). Parameters after clipped Adam
-steps, as a band check: Adam normalises every element's step to ~lr = 1e-4 x sign(m), so an element
-whose float64 gradient at some step is within the gradient tolerance of zero (|g| <= 2e-5 x the
-tensor's largest |g|: the sign is a rounding decision) may move by up to 2 lr per step the other
-way — the band, counted and printed; every other element must be within 1e-6 + 1e-5 |ref|, with no
-fraction allowed to escape. The apply itself (clip + Adam given the device's gradient and norm) is
-pinned bit for bit by test_drqn_clip_adam_exact.
+loss / pre-clip norm rtol 1e-4; gradients rtol 5e-4 with atol 1e-5 x the tensor's largest magnitude
+(round 5: the kernel's measured worst was 0.40 of the round-4 bar of rtol 1e-3). Parameters are
+pinned by composition, with no sign band: every update's gradient is checked against the oracle run
+from the device's OWN pre-update parameters (so Adam's sign-of-rounding cannot drift the two apart),
+and clip + Adam given that gradient and the device's pre-clip norm is checked bit for bit against
+the float32 restatement oracle.clip_adam_f32 — every parameter, both moments, every update.
 """
 import numpy as np
 import pytest
@@ -38,47 +36,59 @@ def _grads(L):
     return out
 
 
-BAND_REL = 2e-5  # twice the gradient check's atol (1e-5 x the tensor's largest |g|)
-
-
-def _band(grads_per_step, k):
-    """Elements of parameter k whose float64 gradient at any step is within BAND_REL x the tensor's
-    largest |g| of zero: their Adam direction is a rounding decision."""
-    band = None
-    for g in grads_per_step:
-        g = np.asarray(g[k], np.float64)
-        b = np.abs(g) <= BAND_REL * np.abs(g).max()
-        band = b if band is None else band | b
-    return band
-
-
-def _assert_params(got, ref, what, steps, band, tally=None):
-    got, ref = np.asarray(got, np.float64).reshape(-1), np.asarray(ref, np.float64).reshape(-1)
-    band = np.asarray(band).reshape(-1)
-    np.testing.assert_allclose(got[band], ref[band], rtol=0, atol=steps * 2e-4 * 1.01, err_msg=f"{what} (band)")
-    np.testing.assert_allclose(got[~band], ref[~band], rtol=1e-5, atol=1e-6, err_msg=what)
-    if tally is not None:
-        tally[0] += int(band.sum())
-        tally[1] += band.size
-        err = np.abs(got - ref) / (1e-6 + 1e-5 * np.abs(ref))
-        tally[2] = max(tally[2], float(np.max(err[~band], initial=0.0)))
-        tally[3] += int((err[band] > 1.0).sum())  # band elements that did use the band
-
-
 def _assert_grads(got, ref, what):
     worst = 0.0
     for k, r in ref.items():
         tol = 1e-5 * np.abs(r).max() + 1e-9
-        np.testing.assert_allclose(got[k], r, rtol=1e-3, atol=tol, err_msg=f"{what}: {k}")
-        worst = max(worst, float(np.max(np.abs(got[k] - r) / (tol + 1e-3 * np.abs(r)))))
-    print(f"\n{what}: gradient error / tolerance (rtol 1e-3, atol 1e-5 max|g|) max {worst:.4f}")
+        np.testing.assert_allclose(got[k], r, rtol=GRAD_RTOL, atol=tol, err_msg=f"{what}: {k}")
+        worst = max(worst, float(np.max(np.abs(got[k] - r) / (tol + GRAD_RTOL * np.abs(r)))))
+    print(f"\n{what}: gradient error / tolerance (rtol {GRAD_RTOL}, atol 1e-5 max|g|) max {worst:.4f}")
+    return worst
+
+
+def _f64(sd):
+    return {k: np.asarray(v, np.float64) for k, v in sd.items()}
+
+
+def _assert_apply_exact(L, p0, m0, v0, at, what):
+    """clip + Adam of the update just applied, given its own gradient (L.grad after apply: sigma slots
+    formed) and pre-clip norm, equals oracle.clip_adam_f32 bit for bit; the norm is the fp64 norm of
+    that gradient."""
+    from pongmi._lib import PM_RNN_NPARAM
+    st = L.stats()
+    g = L.grad.cpu().numpy()[:PM_RNN_NPARAM]
+    np.testing.assert_allclose(st["norm"], np.sqrt(np.sum(g.astype(np.float64) ** 2)), rtol=1e-6, err_msg=what)
+    p, m, v, _ = orc_mod().clip_adam_f32(p0, m0, v0, g, st["norm"], at, max_norm=L.desc.max_norm, lr=L.desc.lr)
+    np.testing.assert_array_equal(L.adam_m.cpu().numpy(), m, err_msg=f"exp_avg, {what}")
+    np.testing.assert_array_equal(L.adam_v.cpu().numpy(), v, err_msg=f"exp_avg_sq, {what}")
+    np.testing.assert_array_equal(L.params.cpu().numpy()[:PM_RNN_NPARAM], p, err_msg=f"params, {what}")
+
+
+def orc_mod():
+    from oracle import oracle
+    return oracle
+
+
+def _snap(L):
+    from pongmi._lib import PM_RNN_NPARAM
+    return (L.params.cpu().numpy()[:PM_RNN_NPARAM].copy(), L.adam_m.cpu().numpy().copy(),
+            L.adam_v.cpu().numpy().copy())
+
+
+GRAD_RTOL = 5e-4
 
 
 def test_drqn_update_matches_reference(golden, orc):
+    """Three updates on the reference's fixture batches: loss and pre-clip norm vs the reference's
+    autograd run every update, update 0's gradients vs autograd; every update's gradient vs the float64
+    oracle from the device's own pre-update parameters, and its clip + Adam bit for bit."""
     from pongmi.drqn import DRQNLearner
     gr, gd = golden("rnn"), golden("drqn")
     L = DRQNLearner(_sd(gr), batch=64, T=8)
+    worst = 0.0
     for k in range(3):
+        p0, m0, v0 = _snap(L)
+        sd_before = _f64(L.state_dict())
         L.update(*(torch.from_numpy(x) for x in _batch(gd, k)))
         st = L.stats()
         assert st["steps"] == k + 1
@@ -86,22 +96,12 @@ def test_drqn_update_matches_reference(golden, orc):
         np.testing.assert_allclose(st["norm"], gd[f"u{k}_norm"], rtol=1e-4)
         if k == 0:
             _assert_grads(_grads(L), {k2[len("u0_grad."):]: v for k2, v in gd.items() if k2.startswith("u0_grad.")},
-                          "update 0")
-    # the band: the float64 oracle's gradients of the same three updates
-    p64 = {k: v.numpy().astype(np.float64) for k, v in _sd(gr).items()}
-    adam, gsteps = {}, []
-    for k in range(3):
-        p64, info = orc.drqn_update(p64, {k2: v.numpy().astype(np.float64) for k2, v in _sd(gr).items()}, adam, k + 1,
-                                    _batch(gd, k))
-        gsteps.append(info["grads"])
-    sd = L.state_dict()
-    tally = [0, 0, 0.0, 0]
-    for k in (n[len("final_sub."):] for n in gd if n.startswith("final_sub.")):
-        _assert_params(sd[k].numpy().reshape(-1)[::8], gd["final_sub." + k], k, 3, _band(gsteps, k).reshape(-1)[::8],
-                       tally)
-    print(f"\nparameters after 3 updates: {tally[0]} of {tally[1]} elements in the sign band, {tally[3]} of them "
-          f"beyond 1e-6 + 1e-5 |ref|; worst off-band error / (1e-6 + 1e-5 |ref|) {tally[2]:.4f}")
+                          "update 0 vs autograd")
+        info = orc.drqn_grads(sd_before, _f64(_sd(gr)), *_batch(gd, k))
+        worst = max(worst, _assert_grads(_grads(L), info["grads"], f"update {k} vs oracle (device's own parameters)"))
+        _assert_apply_exact(L, p0, m0, v0, k + 1, f"update {k}")
     # targetB untouched (interval 2000), epsilon buffers unchanged
+    sd = L.state_dict()
     assert torch.equal(L.target_state_dict()["lstm.weight_hh_l0"], _sd(gr)["lstm.weight_hh_l0"])
     assert torch.equal(sd["fc_A.weight_epsilon"], _sd(gr)["fc_A.weight_epsilon"])
 
@@ -129,16 +129,10 @@ def test_drqn_against_oracle_ragged(golden, orc, B, T):
     info = orc.drqn_grads({k: v.astype(np.float64) for k, v in sd.items()},
                           {k: v.astype(np.float64) for k, v in tsd.items()}, obs, act, rew, nxt, done)
     np.testing.assert_allclose(L.stats()["loss"], info["loss"], rtol=1e-4)
+    p0, m0, v0 = _snap(L)
     L.apply()  # the sigma gradients (mu gradient x epsilon) are formed after the all-reduce, in apply
     _assert_grads(_grads(L), info["grads"], f"B={B} T={T}")
-    new, _ = orc.drqn_update({k: v.astype(np.float64) for k, v in sd.items()},
-                             {k: v.astype(np.float64) for k, v in tsd.items()}, {}, 1, (obs, act, rew, nxt, done))
-    got = L.state_dict()
-    tally = [0, 0, 0.0, 0]
-    for k in orc.RNN_PARAM_KEYS:
-        _assert_params(got[k].numpy(), new[k], k, 1, _band([info["grads"]], k), tally)
-    print(f"B={B} T={T}: {tally[0]} of {tally[1]} parameters in the sign band, {tally[3]} of them beyond "
-          f"1e-6 + 1e-5 |ref|; worst off-band error / (1e-6 + 1e-5 |ref|) {tally[2]:.4f}")
+    _assert_apply_exact(L, p0, m0, v0, 1, f"B={B} T={T}")
 
 
 def test_drqn_deterministic_world_and_target_sync(golden):
@@ -179,42 +173,48 @@ def test_drqn_disabled_replica_contributes_nothing(golden):
     np.testing.assert_allclose(L.stats()["loss"], gd["u0_loss"], rtol=1e-4)
 
 
-def _adam_f32(p, m, v, g, norm, at, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8, max_norm=1.0):
-    """torch's clip_grad_norm_ + Adam step restated in float32 in the kernel's operation order (the
-    clip coefficient from the device's own pre-clip norm, which is an fp64 sum in a fixed tree)."""
-    f = np.float32
-    coef = f(max_norm / (np.float64(f(norm)) + 1e-6))
-    coef = min(coef, f(1.0))
-    bc1, bc2 = 1.0 - b1 ** at, 1.0 - b2 ** at
-    step_size, bc2s = f(lr / bc1), f(np.sqrt(bc2))
-    gc = g.astype(f) * coef
-    m = m + f(1.0 - b1) * (gc - m)
-    v = v * f(b2) + f(1.0 - b2) * gc * gc
-    denom = np.sqrt(v) / bc2s + f(eps)
-    return p - step_size * (m / denom), m, v
-
-
 def test_drqn_clip_adam_exact(golden):
     """The clip + Adam half of train_step_rnn is exact: given the update's own gradient (read back
     after apply, sigma slots formed) and its pre-clip norm, every parameter and both Adam moments
     equal a float32 restatement bit for bit, over three updates; the norm equals the fp64 norm of
     that gradient. With the gradients checked against autograd / the oracle above, this pins the
-    parameters without the Adam sign-of-rounding escape (_assert_params)."""
+    parameters with no sign-of-rounding band."""
     from pongmi._lib import PM_RNN_NPARAM
     from pongmi.drqn import DRQNLearner
     gr, gd = golden("rnn"), golden("drqn")
     L = DRQNLearner(_sd(gr), batch=64, T=8)
     for k in range(3):
-        p0 = L.params.cpu().numpy()[:PM_RNN_NPARAM].copy()
-        m0, v0 = L.adam_m.cpu().numpy().copy(), L.adam_v.cpu().numpy().copy()
+        p0, m0, v0 = _snap(L)
         L.update(*(torch.from_numpy(x) for x in _batch(gd, k)))
+        _assert_apply_exact(L, p0, m0, v0, k + 1, f"update {k}")
+
+
+def test_drqn_clip_active_both_norm_paths(golden, orc):
+    """max_norm small enough that the clip scales every gradient: the single-replica
+    update (pm_drqn_update: the clip norm summed by k_dq_wgrad's tiles) and the replica path
+    (pm_drqn_grads -> pm_drqn_apply: the norm summed per parameter slice after the all-reduce) each
+    equal the float32 clip + Adam restatement bit for bit given their own gradient and norm; the two
+    norms agree to 1e-6 (different fp64 summation orders), so their parameters agree to an ulp-level
+    tolerance, not bitwise."""
+    from pongmi._lib import PM_RNN_NPARAM
+    from pongmi.drqn import DRQNLearner
+    gr, gd = golden("rnn"), golden("drqn")
+    b = tuple(torch.from_numpy(x) for x in _batch(gd, 0))
+    outs = []
+    for split in (False, True):
+        L = DRQNLearner(_sd(gr), batch=64, T=8, max_norm=0.01)
+        p0, m0, v0 = _snap(L)
+        if split:
+            L.grads(*b)
+            L.apply()
+        else:
+            L.update(*b)
         st = L.stats()
-        g = L.grad.cpu().numpy()[:PM_RNN_NPARAM]
-        np.testing.assert_allclose(st["norm"], np.sqrt(np.sum(g.astype(np.float64) ** 2)), rtol=1e-6)
-        p, m, v = _adam_f32(p0, m0, v0, g, st["norm"], k + 1)
-        np.testing.assert_array_equal(L.adam_m.cpu().numpy(), m, err_msg=f"exp_avg, update {k}")
-        np.testing.assert_array_equal(L.adam_v.cpu().numpy(), v, err_msg=f"exp_avg_sq, update {k}")
-        np.testing.assert_array_equal(L.params.cpu().numpy()[:PM_RNN_NPARAM], p, err_msg=f"params, update {k}")
+        assert 0.01 / (st["norm"] + 1e-6) < 1.0  # the clip is active
+        _assert_apply_exact(L, p0, m0, v0, 1, "split" if split else "fused")
+        outs.append((st["norm"], L.params.cpu().numpy()[:PM_RNN_NPARAM].copy()))
+    np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-6)
+    np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-9)
 
 
 def test_drqn_timeout_voids_update(golden):

@@ -88,132 +88,17 @@ static __device__ unsigned long long pm_k1_diag[8][4096];
 // 2 reset + term rows written for done arenas only (the other rows are left as they were).
 // WT: write-through outputs (pm_dev.h st_out), chosen by the arena count at launch.
 //
-// k_env_step_w (round 5, the default): the same tick with WAVE-level observation staging. Every wave
-// stages its own 64 rows in a private LDS slice and reads them back as float4s (the LDS operations of
-// one wave complete in issue order), so no workgroup barrier sits between a wave's tick and its
-// stores and each wave's serial chain is its own: load -> draw + tick -> LDS row staging -> one store
-// burst (observation float4s, state, rewards, done). The block variant above waited at
-// __syncthreads for the block's slowest wave (median 416, p90 1 332 cycles) between its state stores
-// and its observation stores (profiles/r4_k1_experiments.txt). PONGMI_K1_STG=0 selects it (A/B).
-template <int AR, bool INJ, bool WT>
-__global__ __launch_bounds__(kBlock) void k_env_step_w(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
-                                                       const int8_t* __restrict__ aB, float* __restrict__ obsA,
-                                                       float* __restrict__ obsB, float* __restrict__ rA,
-                                                       float* __restrict__ rB, uint8_t* __restrict__ done,
-                                                       float* __restrict__ tobsA, float* __restrict__ tobsB,
-                                                       const double* __restrict__ inject, int inject_cap,
-                                                       uint64_t seed, uint64_t ctr, int32_t* status, int n) {
-    __shared__ __attribute__((aligned(16))) float lds[4][kBlock][7];
-    constexpr bool DRAW = AR && !INJ;
-    const int t = threadIdx.x;
-    const int lane = t & 63, w0 = t & ~63;
-    const int iw = blockIdx.x * kBlock + w0;  // first arena of this wave
-    if (iw >= n) return;                      // whole wave past the end (no barrier in this kernel)
-    const int i = iw + lane;
-    const int wrows = min(64, n - iw);
-    const bool full_term = tobsA && AR != 2;
-    float oA[7] = {0}, oB[7] = {0}, tA[7], tB[7];
-    int d = 0;
-    Arena a{};
-    float ra = 0.f, rb = 0.f;
-    K1_STAMP(0);
-    if (i < n) {
-        int32_t ns = 0;
-        ServeDraw sv{};
-        if (INJ) ns = __builtin_nontemporal_load(&s.serves[i]);
-        a = load_arena(s, i);
-        const int xa = aA[i], xb = aB[i];
-        if (DRAW) {
-            sv = serve_draw(p, (uint32_t)i, (uint32_t)ctr, seed, TAG_SERVE_STEP, (uint32_t)(ctr >> 32));
-            asm volatile("" ::"v"(sv.vx), "v"(sv.vy), "v"(sv.spin), "v"(sv.rad));
-        }
-#ifdef PM_DIAG
-        K1_DRAIN();
-        K1_STAMP(1);
-#endif
-        d = tick(p, a, xa, xb, ra, rb);
-        K1_STAMP(2);
-        observe(a, oA, oB);
-        if (full_term) {
-#pragma unroll
-            for (int k = 0; k < 7; ++k) { lds[2][t][k] = oA[k]; lds[3][t][k] = oB[k]; }
-        }
-        if constexpr (DRAW) {
-#pragma unroll
-            for (int k = 0; k < 7; ++k) { tA[k] = oA[k]; tB[k] = oB[k]; }
-            serve_finish(sv);  // the rare |angle| >= 135 degree redo
-            Arena r = a;
-            serve(r, sv.vx, sv.vy, sv.spin);
-            a.x = d ? r.x : a.x; a.y = d ? r.y : a.y; a.vx = d ? r.vx : a.vx; a.vy = d ? r.vy : a.vy;
-            a.spin = d ? r.spin : a.spin; a.top = d ? r.top : a.top; a.bot = d ? r.bot : a.bot;
-            a.sA = d ? 0 : a.sA; a.sB = d ? 0 : a.sB; a.bounces = d ? 0 : a.bounces;
-            observe(a, oA, oB);
-        } else if (AR && d) {
-            if (AR == 2 && tobsA) {
-                store_row7(tobsA + (size_t)i * 7, oA);
-                store_row7(tobsB + (size_t)i * 7, oB);
-            }
-            const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
-            serve(a, r[0], r[1], r[2]);
-            s.serves[i] = ns + 1;
-            observe(a, oA, oB);
-        }
-    }
-    K1_STAMP(3);
-    // the wave's rows: LDS slice [w0, w0 + 64) of each staging array, 1 792 B, 16-B aligned
-#pragma unroll
-    for (int k = 0; k < 7; ++k) { lds[0][t][k] = oA[k]; lds[1][t][k] = oB[k]; }
-    // wave-scope ordering only: the rows are read back by lanes of the same wave
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    K1_STAMP(4);
-    const int nq = full_term ? 4 : 2;
-    float* const dsts[4] = {obsA, obsB, tobsA, tobsB};
-    const size_t rowoff = (size_t)iw * 7;
-    bool vec = wrows == 64;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        if (q < nq) vec = vec && ((((uintptr_t)(dsts[q] + rowoff)) & 15) == 0);
-    if (vec) {
-        // read every float4 first, then one burst of stores: observations, state, rewards, done
-        float4 f[4][2];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (q < nq) {
-                const float4* s4 = reinterpret_cast<const float4*>(&lds[q][w0][0]);
-                f[q][0] = s4[lane];
-                if (lane < 48) f[q][1] = s4[64 + lane];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (q < nq) {
-                float4* d4 = reinterpret_cast<float4*>(dsts[q] + rowoff);
-                st_f4<WT>(d4 + lane, f[q][0]);
-                if (lane < 48) st_f4<WT>(d4 + 64 + lane, f[q][1]);
-            }
-        }
-    } else {
-        for (int q = 0; q < nq; ++q)
-            for (int e = lane; e < wrows * 7; e += 64) dsts[q][rowoff + e] = (&lds[q][w0][0])[e];
-    }
-    if (i < n) {
-        store_arena<WT>(s, i, a);
-        st_out<WT>(&rA[i], ra);
-        st_out<WT>(&rB[i], rb);
-        done[i] = (uint8_t)d;
-        if (DRAW && AR == 2 && tobsA && d) {
-            store_row7(tobsA + (size_t)i * 7, tA);
-            store_row7(tobsB + (size_t)i * 7, tB);
-        }
-    }
-    K1_STAMP(5);
-    K1_DRAIN();
-    K1_STAMP(6);
-}
-
-template <int AR, bool INJ, bool WT>
+// PRO (round 5, the default): the prologue is ordered for latency. Every lane loads from a clamped
+// index (i < n ? i : n - 1), so no bounds branch splits the kernel-argument loads into two dependent
+// scalar rounds (bound n first, then the pointers: ~2 scalar-cache round trips before the first
+// vector load), and a scheduling barrier keeps every state / action load ahead of the serve draw —
+// without it the compiler interleaved ~100 Philox instructions in front of the state loads and ~200
+// in front of the score loads. Stores stay guarded by i < n. PONGMI_K1_PRO=0 selects the round-4
+// prologue (A/B). Round-5 measurements that were NOT kept (profiles/r5_k1_experiments.txt): wave-level
+// observation staging without the workgroup barrier (one store burst 4.25 us, state stores first
+// 4.19 us, against 4.11 us with the barrier), and 16-B per-lane state accesses (field pairs / quads per
+// instruction: the copy skeleton 4.12 against 3.53 us).
+template <int AR, bool INJ, bool WT, bool PRO>
 __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
                                                      const int8_t* __restrict__ aB, float* __restrict__ obsA,
                                                      float* __restrict__ obsB, float* __restrict__ rA,
@@ -230,12 +115,14 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
     float oA[7] = {0}, oB[7] = {0}, tA[7], tB[7];
     int tdone = 0;
     K1_STAMP(0);
-    if (i < n) {
+    if (PRO || i < n) {
+        const int il = PRO ? (i < n ? i : n - 1) : i;  // the loads' index (clamped: no bounds branch)
         int32_t ns = 0;
         ServeDraw sv{};
-        if (INJ) ns = __builtin_nontemporal_load(&s.serves[i]);
-        Arena a = load_arena(s, i);
-        const int xa = aA[i], xb = aB[i];
+        if (INJ) ns = __builtin_nontemporal_load(&s.serves[il]);
+        Arena a = load_arena(s, il);
+        const int xa = aA[il], xb = aB[il];
+        if (PRO) __builtin_amdgcn_sched_barrier(0);  // every load issued before the draw's first instruction
         // the step-keyed draw depends on no load: it runs while the state is in flight, and is
         // pinned complete ahead of the tick (the compiler would sink it into the done lanes' path)
         if (DRAW) {
@@ -265,20 +152,22 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
             a.sA = d ? 0 : a.sA; a.sB = d ? 0 : a.sB; a.bounces = d ? 0 : a.bounces;
             observe(a, oA, oB);
         } else if (AR && d) {  // parity mode: the injected serve of done arenas
-            if (AR == 2 && tobsA) {
+            if (AR == 2 && tobsA && i < n) {
                 store_row7(tobsA + (size_t)i * 7, oA);
                 store_row7(tobsB + (size_t)i * 7, oB);
             }
-            const double* r = inject + ((size_t)i * inject_cap + (ns % inject_cap)) * 3;
+            const double* r = inject + ((size_t)il * inject_cap + (ns % inject_cap)) * 3;
             serve(a, r[0], r[1], r[2]);
-            s.serves[i] = ns + 1;
+            if (i < n) s.serves[i] = ns + 1;
             observe(a, oA, oB);
         }
-        store_arena<WT>(s, i, a);
-        st_out<WT>(&rA[i], ra);
-        st_out<WT>(&rB[i], rb);
-        done[i] = (uint8_t)d;
-        tdone = d;
+        if (i < n) {
+            store_arena<WT>(s, i, a);
+            st_out<WT>(&rA[i], ra);
+            st_out<WT>(&rB[i], rb);
+            done[i] = (uint8_t)d;
+            tdone = d;
+        }
     }
     K1_STAMP(3);
 #pragma unroll
@@ -329,10 +218,10 @@ int k1_write_through(int32_t n) {
     return forced >= 0 ? (forced != 0) : (n <= kK1WtMax);
 }
 
-// Wave-level observation staging (k_env_step_w) unless PONGMI_K1_STG=0 (the block-barrier A/B).
-int k1_wave_staging() {
+// K1 prologue (PONGMI_K1_PRO, A/B): 1 (default) = clamped loads ahead of the draw, 0 = round 4's.
+int k1_prologue() {
     static const int v = [] {
-        const char* e = getenv("PONGMI_K1_STG");
+        const char* e = getenv("PONGMI_K1_PRO");
         return e && *e ? (atoi(e) != 0) : 1;
     }();
     return v;
@@ -372,21 +261,17 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
     PM_REQUIRE(autoreset >= 0 && autoreset <= 2, PM_E_ARG, "pm_env_step: autoreset=%d not in {0,1,2}", autoreset);
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
-    using K = decltype(&k_env_step<0, false, false>);
-    static const K kernels[2][2][3][2] = {
-        {{{k_env_step<0, false, false>, k_env_step<0, true, false>},
-          {k_env_step<1, false, false>, k_env_step<1, true, false>},
-          {k_env_step<2, false, false>, k_env_step<2, true, false>}},
-         {{k_env_step<0, false, true>, k_env_step<0, true, true>},
-          {k_env_step<1, false, true>, k_env_step<1, true, true>},
-          {k_env_step<2, false, true>, k_env_step<2, true, true>}}},
-        {{{k_env_step_w<0, false, false>, k_env_step_w<0, true, false>},
-          {k_env_step_w<1, false, false>, k_env_step_w<1, true, false>},
-          {k_env_step_w<2, false, false>, k_env_step_w<2, true, false>}},
-         {{k_env_step_w<0, false, true>, k_env_step_w<0, true, true>},
-          {k_env_step_w<1, false, true>, k_env_step_w<1, true, true>},
-          {k_env_step_w<2, false, true>, k_env_step_w<2, true, true>}}}};
-    pm_launch(PM_TIMER_ENV_STEP, kernels[k1_wave_staging()][k1_write_through(n)][autoreset][inject != nullptr],
+    using K = decltype(&k_env_step<0, false, false, true>);
+#define PM_K1_SET(PRO)                                                                               \
+    {{{k_env_step<0, false, false, PRO>, k_env_step<0, true, false, PRO>},                           \
+      {k_env_step<1, false, false, PRO>, k_env_step<1, true, false, PRO>},                           \
+      {k_env_step<2, false, false, PRO>, k_env_step<2, true, false, PRO>}},                          \
+     {{k_env_step<0, false, true, PRO>, k_env_step<0, true, true, PRO>},                             \
+      {k_env_step<1, false, true, PRO>, k_env_step<1, true, true, PRO>},                             \
+      {k_env_step<2, false, true, PRO>, k_env_step<2, true, true, PRO>}}}
+    static const K kernels[2][2][3][2] = {PM_K1_SET(false), PM_K1_SET(true)};
+#undef PM_K1_SET
+    pm_launch(PM_TIMER_ENV_STEP, kernels[k1_prologue()][k1_write_through(n)][autoreset][inject != nullptr],
               dim3(pm_blocks(n, kBlock)),
               dim3(kBlock), pm_stream(stream), *p, *s, aA, aB, obsA, obsB, rA, rB, done, term_obsA, term_obsB, inject,
               inject_cap, seed, counter, status, n);

@@ -94,7 +94,11 @@ __device__ __forceinline__ RingNodes ring_nodes(const PushRange& pr, int64_t g) 
 // in double from +, -, *, / and exact scalings only — ln p by the atanh series on m in
 // [sqrt(1/2), sqrt(2)), exp by a Cody-Waite split and its Taylor series — then rounded once to float:
 // within an ulp of numpy's powf (the reference's arithmetic), and a fixed sequence of correctly
-// rounded operations, so the oracle (oracle.det_pow_f32) restates every leaf bit for bit.
+// rounded operations, so the oracle (oracle.det_pow_f32) restates every leaf bit for bit; equal to
+// the correctly rounded pow on every input and within 1 ulp of numpy's float32 power
+// (tests/test_oracle_golden.py::test_det_pow_within_one_ulp_of_numpy_power). Non-positive and NaN
+// priorities give a 0 leaf (never sampled); the learner latches pm_ctrl.status bit 1 for a NaN one,
+// where the reference's numpy would carry the NaN into np.random.choice (which raises).
 __device__ __forceinline__ float prio_pow(float p, float alpha) {
     if (!(p > 0.f)) return 0.f;
     int e;

@@ -694,6 +694,7 @@ __device__ __forceinline__ void push_rows_fwd(const pm_selfplay& sp, const float
 // an update before the replay holds a batch.
 constexpr int kPushPollMax = 20000;
 constexpr int PM_CTRL_PUSH_TIMEOUT = 1;
+constexpr int PM_CTRL_NAN_PRIO = 2;  // a NaN |TD error| was scattered (its PER leaf is 0: never sampled)
 __device__ __forceinline__ bool push_handoff(int mode, bool train) { return (mode & PM_UPD_FIRST) && train; }
 __device__ __forceinline__ int* push_flag(const pm_selfplay& sp) {
     return reinterpret_cast<int*>(sp.hfeat + (size_t)2 * sp.batch * 80);
@@ -1017,6 +1018,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         if (act && sm.hwin[slot] == t) {
             sp.prios[id] = prio;
             tree.leaf[id] = prio_pow(prio, (float)sp.alpha);
+            if (prio != prio) atomicOr(&sp.ctrl->status, PM_CTRL_NAN_PRIO);
         }
         mpx = sm.red[0][2];
         for (int w = 1; w < 16; ++w) mpx = fmaxf(mpx, sm.red[w][2]);
@@ -1694,6 +1696,7 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
     if (act && sm.hwin[slot] == t) {
         sp.prios[id] = prio;
         tree.leaf[id] = prio_pow(prio, (float)sp.alpha);
+        if (prio != prio) atomicOr(&sp.ctrl->status, PM_CTRL_NAN_PRIO);
     }
     {
         float mpx = sm.red[0][2];

@@ -8,8 +8,8 @@
 # tasks:
 #   suite      the whole `-m gpu` suite + smoke()
 #   env        tests/test_gpu_env.py only (K1 parity)
-#   k1         K1 A/B: graph-timed floor probe (tools/k1_floor), product K1 with PONGMI_K1_STG=1 / 0
-#              (tools/k1_time.py, bench.time_env_step), then rocprofv3 kernel traces of both
+#   k1         K1 A/B: parity of the A/B variant, graph-timed floor probe (tools/k1_floor), product K1 with
+#              PONGMI_K1_PRO=1 / 0 (tools/k1_time.py, bench.time_env_step), rocprofv3 kernel traces
 #   k1stamp    per-wave K1 phase cycles (diag build, tools/k1_stamps.py)
 #   bench      python bench.py (the driver's default line)
 #   rnn        python bench.py --workload rnn
@@ -32,20 +32,23 @@ run_task() {
     env)
       timeout -k 10 300 $PYT tests/test_gpu_env.py > gpurun_out/${tag}_env.log 2>&1 && tail -1 gpurun_out/${tag}_env.log ;;
     k1)
+      PONGMI_K1_PRO=0 timeout -k 10 300 $PYT tests/test_gpu_env.py > gpurun_out/${tag}_env_pro0.log 2>&1 &&
+          tail -1 gpurun_out/${tag}_env_pro0.log &&
       timeout -k 10 120 ./tools/k1_floor 65536 > gpurun_out/${tag}_k1_floor.jsonl 2>&1 && cat gpurun_out/${tag}_k1_floor.jsonl &&
-      for stg in 1 0 1 0; do
-        echo "== PONGMI_K1_STG=$stg" >> gpurun_out/${tag}_k1_time.txt
-        PONGMI_K1_STG=$stg timeout -k 10 120 python3 tools/k1_time.py 65536 >> gpurun_out/${tag}_k1_time.txt 2>&1 || return 1
-      done && cat gpurun_out/${tag}_k1_time.txt &&
-      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_floor -o k -- \
-          ./tools/k1_floor 65536 > gpurun_out/${tag}_prof_floor.log 2>&1 &&
-      for stg in 1 0; do
-        PONGMI_K1_STG=$stg timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
-            -d gpurun_out/${tag}_prof_k1_stg$stg -o k -- python3 tools/k1_time.py 65536 \
-            > gpurun_out/${tag}_prof_k1_stg$stg.log 2>&1 || return 1
+      for pro in 1 0 1 0; do
+        echo "== PONGMI_K1_PRO=$pro" >> gpurun_out/${tag}_k1_time.txt
+        PONGMI_K1_PRO=$pro timeout -k 10 120 python3 tools/k1_time.py 65536 262144 >> gpurun_out/${tag}_k1_time.txt 2>&1 || return 1
+      done && grep -v amdgpu.ids gpurun_out/${tag}_k1_time.txt &&
+      for pro in 1 0; do
+        PONGMI_K1_PRO=$pro timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d gpurun_out/${tag}_prof_k1_pro$pro -o k -- python3 tools/k1_time.py 65536 \
+            > gpurun_out/${tag}_prof_k1_pro$pro.log 2>&1 || return 1
       done && echo K1_OK ;;
     k1stamp)
-      timeout -k 10 120 python3 tools/k1_stamps.py > gpurun_out/${tag}_k1_stamps.txt 2>&1 && cat gpurun_out/${tag}_k1_stamps.txt ;;
+      for pro in 1 0; do
+        PONGMI_K1_PRO=$pro timeout -k 10 120 python3 tools/k1_stamps.py > gpurun_out/${tag}_k1_stamps_pro$pro.txt 2>&1 &&
+            grep -v amdgpu.ids gpurun_out/${tag}_k1_stamps_pro$pro.txt || return 1
+      done ;;
     bench)
       timeout -k 10 300 python3 bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err && echo BENCH_OK ;;
     rnn)

@@ -84,6 +84,80 @@ __global__ __launch_bounds__(256) void k_skel(St s, int n) {
     s.done[i] = (unsigned char)((xa ^ xb) & 1);
 }
 
+// The same bytes with 16-B accesses per lane (timing only: values are not transposed back to their
+// arenas). f64 fields in pairs: even lanes move field a of arenas (2k, 2k + 1), odd lanes field b —
+// one dwordx4 per lane covers two fields of 32 lane pairs, 4 instructions for 7 fields instead of 7;
+// 4-B fields in quads: lane 4k + j moves field j of arenas 4k .. 4k + 3 (sA, sB, bounces, rA | rB);
+// done: lanes 16k move 16 arenas' bytes. MODE 5 loads only, 6 stores only, 7 both.
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16(void* p, i4v v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void k_skel16(St s, int n) {
+    __shared__ __attribute__((aligned(16))) float lds[2][256][7];
+    const int t = threadIdx.x, lane = t & 63, w0 = t & ~63;
+    const int iw = blockIdx.x * 256 + w0;
+    if (iw >= n) return;
+    const int odd = lane & 1, pr = iw + (lane & ~1);   // pair base arena
+    const int q = lane & 3, qb = iw + (lane & ~3);     // quad base arena
+    double* const fa[4] = {s.x, s.vx, s.spin, s.bot};
+    double* const fb[4] = {s.y, s.vy, s.top, nullptr};
+    i4v v[4];
+    i4v iv = {0, 0, 0, 0};
+    if (MODE & 1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double* src = odd ? fb[k] : fa[k];
+            if (src) v[k] = *reinterpret_cast<const i4v*>(src + pr);
+            else v[k] = i4v{0, 0, 0, 0};
+        }
+        int* const fi[4] = {s.sA, s.sB, s.bn, nullptr};
+        if (fi[q]) iv = *reinterpret_cast<const i4v*>(fi[q] + qb);
+        const int xa = s.aA[iw + lane], xb = s.aB[iw + lane];
+        iv.w += xa + xb;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = i4v{lane, k, 1, 2};
+    }
+    if (MODE == 5) {
+        int z = iv.x + iv.w;
+        for (int k = 0; k < 4; ++k) z += v[k].x + v[k].w;
+        if (lane == 0) stw(&s.rA[iw], (float)z);
+        return;
+    }
+    const float f0 = __int_as_float(v[0].x), f1 = __int_as_float(v[1].y);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { lds[0][t][k] = f0 + k; lds[1][t][k] = f1 + k; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float4 f[2][2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+        const float4* s4 = reinterpret_cast<const float4*>(&lds[qq][w0][0]);
+        f[qq][0] = s4[lane];
+        if (lane < 48) f[qq][1] = s4[64 + lane];
+    }
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+        float4* d4 = reinterpret_cast<float4*>((qq ? s.obsB : s.obsA) + (size_t)iw * 7);
+        st4(d4 + lane, f[qq][0]);
+        if (lane < 48) st4(d4 + 64 + lane, f[qq][1]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double* dst = odd ? fb[k] : fa[k];
+        if (dst) st16(dst + pr, v[k]);
+    }
+    float* const fo[4] = {reinterpret_cast<float*>(s.sA), reinterpret_cast<float*>(s.sB),
+                          reinterpret_cast<float*>(s.bn), s.rA};
+    st16(fo[q] + qb, iv);
+    if (q == 0) st16(s.rB + qb, iv);
+    if ((lane & 15) == 0) st16(s.done + iw + lane, iv);
+}
+
 typedef void (*Fn)(St, int);
 
 static double graph_us(Fn fn, St s, int n, hipStream_t st, int per_graph = 50, int replays = 40, int warm = 100) {
@@ -135,6 +209,9 @@ int main(int argc, char** argv) {
         {"loads", k_skel<1>, 70.0 * n},
         {"stores", k_skel<2>, 133.0 * n},
         {"copy", k_skel<3>, 203.0 * n},
+        {"loads16", k_skel16<5>, 70.0 * n},
+        {"stores16", k_skel16<6>, 133.0 * n},
+        {"copy16", k_skel16<7>, 203.0 * n},
     };
     for (int rep = 0; rep < 2; ++rep)
         for (const auto& k : ks) {

@@ -5,9 +5,8 @@ diagnostic library's s_memtime stamps (libpongmi_diag.so; never the product libr
 
 Phases (lane 0 of every wave): 0 start | 1 every load landed (a vmcnt(0) drain: diag only) |
 2 draw + tick done | 3 reset select + state/reward stores issued | 4 LDS staging + barrier |
-5 observation rows + term rows issued | 6 every store drained (the block-staged k_env_step,
-PONGMI_K1_STG=0). The default wave-staged k_env_step_w stamps 3 after the reset select, 4 after its
-wave's LDS staging and 5 after its single store burst."""
+5 observation rows + term rows issued | 6 every store drained. PONGMI_K1_PRO=0 selects round 4's
+prologue (A/B)."""
 import ctypes
 import os
 import sys
@@ -36,12 +35,8 @@ for _ in range(200):
     env.step(aA, aB)
 torch.cuda.synchronize()
 nw = min(4096, (n + 63) // 64)
-if os.environ.get("PONGMI_K1_STG", "1") not in ("", "0"):  # k_env_step_w (round 5): wave-level staging
-    names = ["loads landed", "draw + tick", "reset select + observe", "LDS row staging (wave)", "one store burst issued",
-             "stores drained"]
-else:  # k_env_step: block staging behind __syncthreads
-    names = ["loads landed", "draw + tick", "reset + state stores issued", "LDS + barrier", "obs/term stores issued",
-             "stores drained"]
+names = ["loads landed", "draw + tick", "reset + state stores issued", "LDS + barrier", "obs/term stores issued",
+         "stores drained"]
 acc = [[] for _ in names]
 starts, spans = [], []
 buf = (ctypes.c_uint64 * (8 * 4096))()

@@ -98,7 +98,7 @@ static __device__ unsigned long long pm_k1_diag[8][4096];
 // observation staging without the workgroup barrier (one store burst 4.25 us, state stores first
 // 4.19 us, against 4.11 us with the barrier), and 16-B per-lane state accesses (field pairs / quads per
 // instruction: the copy skeleton 4.12 against 3.53 us).
-template <int AR, bool INJ, bool WT, bool PRO>
+template <int AR, bool INJ, bool WT, int PRO>
 __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_state s, const int8_t* __restrict__ aA,
                                                      const int8_t* __restrict__ aB, float* __restrict__ obsA,
                                                      float* __restrict__ obsB, float* __restrict__ rA,
@@ -115,14 +115,14 @@ __global__ __launch_bounds__(kBlock) void k_env_step(pm_env_params p, pm_env_sta
     float oA[7] = {0}, oB[7] = {0}, tA[7], tB[7];
     int tdone = 0;
     K1_STAMP(0);
-    if (PRO || i < n) {
-        const int il = PRO ? (i < n ? i : n - 1) : i;  // the loads' index (clamped: no bounds branch)
+    if ((PRO & 1) || i < n) {
+        const int il = (PRO & 1) ? (i < n ? i : n - 1) : i;  // the loads' index (clamped: no bounds branch)
         int32_t ns = 0;
         ServeDraw sv{};
         if (INJ) ns = __builtin_nontemporal_load(&s.serves[il]);
         Arena a = load_arena(s, il);
         const int xa = aA[il], xb = aB[il];
-        if (PRO) __builtin_amdgcn_sched_barrier(0);  // every load issued before the draw's first instruction
+        if (PRO & 2) __builtin_amdgcn_sched_barrier(0);  // every load issued before the draw's first instruction
         // the step-keyed draw depends on no load: it runs while the state is in flight, and is
         // pinned complete ahead of the tick (the compiler would sink it into the done lanes' path)
         if (DRAW) {
@@ -218,11 +218,13 @@ int k1_write_through(int32_t n) {
     return forced >= 0 ? (forced != 0) : (n <= kK1WtMax);
 }
 
-// K1 prologue (PONGMI_K1_PRO, A/B): 1 (default) = clamped loads ahead of the draw, 0 = round 4's.
+// K1 prologue (PONGMI_K1_PRO, A/B; bit 0 clamped loads, bit 1 loads ahead of the draw): 3 (default)
+// both, 0 round 4's.
 int k1_prologue() {
     static const int v = [] {
         const char* e = getenv("PONGMI_K1_PRO");
-        return e && *e ? (atoi(e) != 0) : 1;
+        const int x = e && *e ? atoi(e) : 3;
+        return x >= 0 && x <= 3 ? x : 3;
     }();
     return v;
 }
@@ -261,7 +263,7 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
     PM_REQUIRE(autoreset >= 0 && autoreset <= 2, PM_E_ARG, "pm_env_step: autoreset=%d not in {0,1,2}", autoreset);
     PM_REQUIRE(!inject || inject_cap > 0, PM_E_ARG, "pm_env_step: inject without capacity");
     PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step: speed_scale_every must be > 0");
-    using K = decltype(&k_env_step<0, false, false, true>);
+    using K = decltype(&k_env_step<0, false, false, 3>);
 #define PM_K1_SET(PRO)                                                                               \
     {{{k_env_step<0, false, false, PRO>, k_env_step<0, true, false, PRO>},                           \
       {k_env_step<1, false, false, PRO>, k_env_step<1, true, false, PRO>},                           \
@@ -269,7 +271,7 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
      {{k_env_step<0, false, true, PRO>, k_env_step<0, true, true, PRO>},                             \
       {k_env_step<1, false, true, PRO>, k_env_step<1, true, true, PRO>},                             \
       {k_env_step<2, false, true, PRO>, k_env_step<2, true, true, PRO>}}}
-    static const K kernels[2][2][3][2] = {PM_K1_SET(false), PM_K1_SET(true)};
+    static const K kernels[4][2][3][2] = {PM_K1_SET(0), PM_K1_SET(1), PM_K1_SET(2), PM_K1_SET(3)};
 #undef PM_K1_SET
     pm_launch(PM_TIMER_ENV_STEP, kernels[k1_prologue()][k1_write_through(n)][autoreset][inject != nullptr],
               dim3(pm_blocks(n, kBlock)),

@@ -32,20 +32,22 @@ run_task() {
     env)
       timeout -k 10 300 $PYT tests/test_gpu_env.py > gpurun_out/${tag}_env.log 2>&1 && tail -1 gpurun_out/${tag}_env.log ;;
     k1)
-      PONGMI_K1_PRO=0 timeout -k 10 300 $PYT tests/test_gpu_env.py > gpurun_out/${tag}_env_pro0.log 2>&1 &&
-          tail -1 gpurun_out/${tag}_env_pro0.log &&
+      for pro in ${K1_PARITY_PROS:-0}; do
+        PONGMI_K1_PRO=$pro timeout -k 10 300 $PYT tests/test_gpu_env.py > gpurun_out/${tag}_env_pro$pro.log 2>&1 &&
+            tail -1 gpurun_out/${tag}_env_pro$pro.log || return 1
+      done &&
       timeout -k 10 120 ./tools/k1_floor 65536 > gpurun_out/${tag}_k1_floor.jsonl 2>&1 && cat gpurun_out/${tag}_k1_floor.jsonl &&
-      for pro in 1 0 1 0; do
+      for pro in ${K1_PROS:-3 0 3 0}; do
         echo "== PONGMI_K1_PRO=$pro" >> gpurun_out/${tag}_k1_time.txt
         PONGMI_K1_PRO=$pro timeout -k 10 120 python3 tools/k1_time.py 65536 262144 >> gpurun_out/${tag}_k1_time.txt 2>&1 || return 1
       done && grep -v amdgpu.ids gpurun_out/${tag}_k1_time.txt &&
-      for pro in 1 0; do
+      for pro in ${K1_PROF_PROS:-3 0}; do
         PONGMI_K1_PRO=$pro timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
             -d gpurun_out/${tag}_prof_k1_pro$pro -o k -- python3 tools/k1_time.py 65536 \
             > gpurun_out/${tag}_prof_k1_pro$pro.log 2>&1 || return 1
       done && echo K1_OK ;;
     k1stamp)
-      for pro in 1 0; do
+      for pro in ${K1_PROF_PROS:-3 0}; do
         PONGMI_K1_PRO=$pro timeout -k 10 120 python3 tools/k1_stamps.py > gpurun_out/${tag}_k1_stamps_pro$pro.txt 2>&1 &&
             grep -v amdgpu.ids gpurun_out/${tag}_k1_stamps_pro$pro.txt || return 1
       done ;;

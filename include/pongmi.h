@@ -456,7 +456,9 @@ typedef struct pm_ctrl {
     int64_t win_A, ep_A, win_P, ep_P; /* wins / episodes of B vs modelA and vs pool (:247-248) */
     double reward_B;         /* sum of rB over finished episodes                          */
     int32_t status;          /* bit 0: the push-row hand-off inside k_learn timed out; the learner
-                                computes those rows itself from then on (results unchanged)      */
+                                computes those rows itself from then on (results unchanged);
+                                bit 1: an update scattered a NaN priority (a diverged loss: its PER
+                                leaf is 0, never sampled; the reference's np.random.choice raises) */
     int32_t max_bits;        /* pm_selfplay_commit scratch: float bits of max(prios); 0 between steps */
 } pm_ctrl;
 

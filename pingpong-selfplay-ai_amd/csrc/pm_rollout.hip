@@ -646,13 +646,11 @@ __global__ __launch_bounds__(kR16Block) __attribute__((amdgpu_waves_per_eu(4, 4)
     rollout16_body<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
 }
 
-// 16-arena tiles: PONGMI_ROLL16 bit 0 = the inference launch, bit 1 = the collecting launch (A/B only)
+// 16-arena tiles: PONGMI_ROLL16 bit 0 = the inference launch, bit 1 = the collecting launch (A/B);
+// default 1. Read at every launch (one getenv), so a test can cover all four kernels in one process.
 int roll16() {
-    static const int v = [] {
-        const char* e = getenv("PONGMI_ROLL16");
-        return e && *e ? atoi(e) : 1;
-    }();
-    return v;
+    const char* e = getenv("PONGMI_ROLL16");
+    return e && *e ? atoi(e) : 1;
 }
 
 }  // namespace

@@ -770,6 +770,7 @@ struct LearnSmem {
     int plist[PM_MAX_BATCH];     // samples whose row is in this step's push range, per wave slot
     int pcnt[16];
     int void_upd;                // the push-row hand-off timed out: this update trains nothing
+    float loss_out;              // the update's loss, committed to the control block at the kernel's end
     ApplySmem ap;
 };
 
@@ -952,13 +953,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     PM_STAMP(2);
     if (sm.void_upd) train = act = false;  // block-uniform: the hand-off timed out
     ep_fin = sm.ctot[0];
-    if (first && t == 0) {  // rollout bookkeeping (:245-249)
-        c->ep_step = ep_fin;
-        c->episodes = cs.episodes + ep_fin;
-        c->ep_A = cs.ep_A + sm.ctot[1]; c->win_A = cs.win_A + sm.ctot[2];
-        c->ep_P = cs.ep_P + sm.ctot[3]; c->win_P = cs.win_P + sm.ctot[4];
-        c->reward_B = cs.reward_B + (double)sm.ctot[5];
-    }
+    // the rollout bookkeeping (:245-249) is committed at the kernel's end (commit_counters): stored
+    // here, wave 0's vmcnt(0) before phase 2's barrier waited for these stores' acknowledgements
 
     // ---- phase 2: double-DQN targets, loss, priorities, bias grads
     float lossp = 0.f, prio = 0.f;
@@ -1025,8 +1021,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         if (t == 0) {
             float l = 0.f;
             for (int w = 0; w < 16; ++w) l += sm.red[w][1];
-            c->last_loss = l / (float)B;
-            c->max_prio = fmaxf(cs.max_prio, mpx);  // n > batch pushes of max_prio survive the scatter
+            sm.loss_out = l / (float)B;  // committed at the kernel's end, with the counters
         }
         const int col = t & 63;
         float g[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1137,6 +1132,19 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         __syncthreads();
     }
     if (sp.fuse_apply) apply_finish(sp, sm.ap, cs, mode);  // unsharded: Adam ran with the gradients (phase 4)
+    if (t == 0) {  // the counters, last: no store of theirs sits in front of a phase's vmcnt(0) wait
+        if (first) {  // rollout bookkeeping (:245-249)
+            c->ep_step = ep_fin;
+            c->episodes = cs.episodes + ep_fin;
+            c->ep_A = cs.ep_A + sm.ctot[1]; c->win_A = cs.win_A + sm.ctot[2];
+            c->ep_P = cs.ep_P + sm.ctot[3]; c->win_P = cs.win_P + sm.ctot[4];
+            c->reward_B = cs.reward_B + (double)sm.ctot[5];
+        }
+        if (train) {
+            c->last_loss = sm.loss_out;
+            c->max_prio = max_prio_next;  // n > batch pushes of max_prio survive the scatter
+        }
+    }
     PM_STAMP(7);
 }
 

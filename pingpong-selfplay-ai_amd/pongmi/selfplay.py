@@ -299,10 +299,13 @@ class SelfPlayLearner:
 
     def check_status(self, c=None):
         """Device error bits (pm_ctrl.status): bit 0 = an update's push-row hand-off inside k_learn
-        timed out (its push rows were not computed: that update is void). Raises on any bit."""
+        timed out (its push rows were not computed: that update is void); bit 1 = an update scattered
+        a NaN priority (the loss diverged; the reference's sampler would raise on the NaN
+        probabilities). Raises on any bit."""
         st = int((c or self.counters())["status"])
         if st:
-            raise _lib.PongmiError(f"self-play learner: device status {st} (bit 0: push-row hand-off timed out)")
+            raise _lib.PongmiError(f"self-play learner: device status {st} (bit 0: push-row hand-off timed out; "
+                                   f"bit 1: NaN priority scattered)")
 
     def set_epsilon(self, eps):
         c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))

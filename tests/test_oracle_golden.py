@@ -221,3 +221,22 @@ def test_per_tree_restatement_vs_choice_outside_band(orc, size):
     ref, _ = orc.per_sample(pr, size, 512, 0.5, u)
     band = orc.per_boundary_band(pr, size, u)
     assert np.array_equal(idx[~band], ref[~band]) and np.all(pr[idx] > 0)
+
+
+@pytest.mark.parametrize("alpha", [0.6, 0.4, 0.5, 1.0])
+def test_det_pow_within_one_ulp_of_numpy_power(orc, alpha):
+    """The PER leaf prio ** alpha (csrc/pm_per.h prio_pow, restated by oracle.det_pow_f32) against the
+    reference's arithmetic, numpy's float32 power (scripts/train_iterative.py:67), over 1e-30 .. 1e30
+    log-spaced (2e6 priorities): at most 1 ulp apart everywhere, and equal to the correctly rounded
+    value (float64 pow rounded once to float32) on every input. Non-positive priorities give a 0 leaf
+    (never sampled); a NaN priority gives a 0 leaf too, and the learner latches pm_ctrl.status bit 1
+    (SelfPlayLearner.check_status raises), where numpy would propagate the NaN into the sample."""
+    p = np.logspace(-30, 30, 2_000_001).astype(np.float32)
+    d = orc.det_pow_f32(p, alpha)
+    ref = np.power(p, np.float32(alpha))
+    ulp = np.abs(d.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 1
+    exact = (p.astype(np.float64) ** np.float64(np.float32(alpha))).astype(np.float32)
+    assert np.array_equal(d, exact)
+    edge = orc.det_pow_f32(np.array([0.0, -1.0, np.nan], np.float32), alpha)
+    assert np.array_equal(edge, np.zeros(3, np.float32))

@@ -11,12 +11,15 @@
 #   k1         K1 A/B: parity of the A/B variant, graph-timed floor probe (tools/k1_floor), product K1 with
 #              PONGMI_K1_PRO=1 / 0 (tools/k1_time.py, bench.time_env_step), rocprofv3 kernel traces
 #   k1stamp    per-wave K1 phase cycles (diag build, tools/k1_stamps.py)
+#   stamps     diag build: k_learn phase stamps of the overlapped step (tools/stamps.py) and k_actenv's
+#              per-block timeline (tools/env_blocks.py)
 #   bench      python bench.py (the driver's default line)
 #   rnn        python bench.py --workload rnn
 #   infer      python bench.py --workload infer
 #   prof       rocprofv3 --kernel-trace --stats of the default bench (no CPU legs)
 #   pmc        the FETCH_SIZE / WRITE_SIZE passes of the default bench (tools/pmc_passes.sh)
 #   pmcrnn     the same for the RNN bench (tools/pmc_rnn_passes.sh)
+#   pmcinfer   the same for the configs[1] inference rollout (2 000-step launches)
 #   drqn       tests/test_gpu_drqn.py + tools/drqn_time.py
 #   pytest:<path>[::sel]  one test file / selection
 set -o pipefail
@@ -51,6 +54,9 @@ run_task() {
         PONGMI_K1_PRO=$pro timeout -k 10 120 python3 tools/k1_stamps.py > gpurun_out/${tag}_k1_stamps_pro$pro.txt 2>&1 &&
             grep -v amdgpu.ids gpurun_out/${tag}_k1_stamps_pro$pro.txt || return 1
       done ;;
+    stamps)
+      timeout -k 10 180 python3 tools/stamps.py > gpurun_out/${tag}_stamps.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_stamps.txt &&
+      timeout -k 10 180 python3 tools/env_blocks.py > gpurun_out/${tag}_env_blocks.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_env_blocks.txt ;;
     bench)
       timeout -k 10 300 python3 bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err && echo BENCH_OK ;;
     rnn)
@@ -64,6 +70,13 @@ run_task() {
       timeout -k 10 600 bash tools/pmc_passes.sh ${tag} && echo PMC_OK ;;
     pmcrnn)
       timeout -k 10 600 bash tools/pmc_rnn_passes.sh ${tag} && echo PMCRNN_OK ;;
+    pmcinfer)  # configs[1]: 2 000-step launches of the K9 rollout (the committed infer profile's shape)
+      for c in "fetch FETCH_SIZE GRBM_GUI_ACTIVE" "write WRITE_SIZE GRBM_GUI_ACTIVE"; do
+        set -- $c
+        timeout -k 10 240 rocprofv3 --pmc $2 $3 --output-format csv -d gpurun_out/pmc_${tag}inf_$1 -o p -- \
+            python3 bench.py --workload infer --steps 2000 --infer-chunk 2000 --no-cpu-baseline \
+            > gpurun_out/pmc_${tag}inf_$1.log 2>&1 || return 1
+      done && echo PMCINFER_OK ;;
     drqn)
       timeout -k 10 300 $PYT tests/test_gpu_drqn.py > gpurun_out/${tag}_drqn.log 2>&1 && tail -1 gpurun_out/${tag}_drqn.log &&
       timeout -k 10 120 python3 tools/drqn_time.py > gpurun_out/${tag}_drqn_time.txt 2>&1 && cat gpurun_out/${tag}_drqn_time.txt ;;

@@ -248,10 +248,21 @@ def cpu_baseline(n, nets, seconds=12.0, epsilon=0.08):
             cpu.step()
             steps += 1
         dt = time.perf_counter() - t0
-    return {"value": round(n * steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+    v = n * steps / dt
+    return {"value": round(v, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/cpu_selfplay.py: {steps} vector steps x {n} arenas (full DQN loop, PER cap 1e6, "
                       f"batch 256, eps {epsilon}, pool {len(pool)}), {dt:.1f} s on 1 host core",
-            "weights": wdesc}
+            "weights": wdesc,
+            # calibration to the reference's own loop (measured in the survey container, one
+            # thread): train_iterative.py's step body = 1 env step + 1 PER update of 256 per env step
+            "reference_python_measured": {"steps_per_s": {"small_buffer": 398, "fill_100k": 209, "fill_1e6": 75},
+                                          "note": "train_iterative.py step body, 1 env step + 1 update per step, "
+                                                  "1 CPU thread (SURVEY 6)"},
+            "port_vs_reference_loop": {"small_buffer": round(v / 398, 1), "fill_100k": round(v / 209, 1),
+                                       "fill_1e6": round(v / 75, 1),
+                                       "note": "env-steps/s ratio; the port batches 65 536 arenas and runs one update "
+                                               "per vector step (the bench's U = 1), the reference one update per env "
+                                               "step"}}
 
 
 def _config0_worker(seconds, seed, q):
@@ -674,7 +685,7 @@ def run_infer(args, dist, rank, world):
             out["roofline"]["kernel"] = (f"{'k_rollout16_push' if tile16 else 'k_rollout_push'} (both players' QNet "
                                          f"forward + env tick + replay push, {chunk} vector steps per launch)")
             # HBM bytes per launch from the committed counter passes (profiles/r3_collect_pmc.json,
-            # tools/gpu_r3_collect_pmc.sh: 65 536 arenas, 15-step launches); None at other shapes
+            # round 3: 65 536 arenas, 15-step launches); None at other shapes
             tb = pmc_traffic("k_rollout_push", "r3_collect_pmc.json")
             out["roofline"]["traffic"] = tb if (n, chunk) == (65536, 15) else None
             out["roofline"]["algorithmic_bytes"] = n * chunk * REPLAY_BYTES + n * (136 + 56)

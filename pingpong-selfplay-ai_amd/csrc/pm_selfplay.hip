@@ -753,6 +753,228 @@ __device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, 
     if (t == 0) st_out<true>(push_flag(sp), push_token(cs));
 }
 
+// ---- the sum-tree refresh block (round 5): block 1, after the push rows, refreshes every tree node
+// the update changes, so the learner's chain ends with its gradients, Adam and the head folds.
+// The learner refreshed them itself in two dependent global round trips behind its own stores
+// (scatter stores acknowledged -> the touched level-1 nodes' leaves loaded -> level-1 stores
+// acknowledged -> the touched level-2 nodes' children loaded: ~8 us of its ~24 us). Block 1 knows
+// which nodes those are from the sample indices and the control block alone, so it loads their
+// inputs into LDS long before the update's priorities exist:
+//   - entries: the B sampled indices, plus (LAST) the next push range's segment ends (its partial
+//     level-1 / level-2 nodes); one level-1 slot per distinct sub-block and one level-2 slot per
+//     distinct chunk (LDS hash sets), a chunk's 16 positions mapped to the level-1 slots inside it;
+//   - LDS DMA: the 64 leaves of every level-1 slot, the 16 level-1 nodes of every level-2 slot;
+//   - the learner publishes, as tagged 8-byte granules (hfeat's hand-off rows, MI355X_MICROARCH.md
+//     handoff-1to1: one sc1 store each, no flag, no fence), each sample's new leaf prio ** alpha, the
+//     next push's max priority and whether the update scattered; block 1 applies the scatter's
+//     winners (the last duplicate of an index, as the learner's hash) to its LDS leaves, sums every
+//     level-1 slot from LDS with the pending push substituted (per_quarter's order), then every
+//     level-2 slot from LDS with the refreshed / pushed children substituted (per_chunk_sum's order),
+//     and writes the wholly pushed nodes as the learner did (constants).
+// Same functions, same orders: the tree stays bit-identical to a rebuild
+// (test_sum_tree_incremental_equals_rebuild). The granule tag is an epoch word block 1 bumps at
+// its end (both blocks read it at their start; the next launch's tag is new). A poll that never
+// completes (bounded) sets ctrl.status bit 2 and leaves the tree alone. PONGMI_TR=0 (A/B) keeps the
+// refresh in the learner.
+constexpr int kTrSlots = PM_MAX_BATCH + 8;  // distinct level-1 / level-2 nodes: samples + <= 4 push edges (x8 rows)
+constexpr int kTrHash = 1024;                // open-addressing sets keyed by node id
+constexpr uint32_t kTrEmpty = 0xFFFFFFFFu;
+constexpr int kTrPollMax = 20000;
+constexpr int PM_CTRL_TREE_TIMEOUT = 4;
+struct TreeRefreshSmem {
+    __attribute__((aligned(16))) float lf[kTrSlots][PER_SUB];   // leaves of every level-1 slot (LDS DMA)
+    __attribute__((aligned(16))) double ls[kTrSlots][PER_FAN];  // level-1 nodes of every level-2 slot (LDS DMA)
+    double subv[kTrSlots];                                     // refreshed level-1 nodes
+    uint32_t subid[kTrSlots], chid[kTrSlots];
+    int16_t cmap[kTrSlots][PER_FAN];  // level-2 slot x position -> level-1 slot inside it (-1: none)
+    uint32_t skey[kTrHash];
+    int sslot[kTrHash];
+    uint32_t ckey[kTrHash];
+    int cslot[kTrHash];
+    uint32_t ikey[512];  // sampled index -> winning sample (the last duplicate, as the learner's hash)
+    int iwin[512];
+    uint32_t eidx[kTrSlots];  // entries: sampled indices, then the push edges
+    int esub[kTrSlots];
+    float leaf_new[PM_MAX_BATCH];
+    float maxp_next;
+    int scattered, ok, nsub, nch;
+};
+__device__ __forceinline__ uint64_t* tr_granules(const pm_selfplay& sp) {
+    return reinterpret_cast<uint64_t*>(sp.hfeat + (size_t)(2 * sp.batch + 1) * 80);
+}
+__device__ __forceinline__ uint32_t* tr_epoch(const pm_selfplay& sp) {
+    return reinterpret_cast<uint32_t*>(sp.hfeat + (size_t)2 * sp.batch * 80) + 1;
+}
+__device__ __forceinline__ void tr_publish(const pm_selfplay& sp, int k, uint32_t v, uint32_t tag) {
+    __hip_atomic_store(tr_granules(sp) + k, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int tr_hash(uint32_t k, int bits) { return (int)((k * 2654435761u) >> (32 - bits)); }
+__device__ __forceinline__ int tr_insert(uint32_t* key, uint32_t k, int bits) {
+    const int mask = (1 << bits) - 1;
+    int h = tr_hash(k, bits);
+    for (;;) {
+        const uint32_t old = atomicCAS(&key[h], kTrEmpty, k);
+        if (old == kTrEmpty || old == k) return h;
+        h = (h + 1) & mask;
+    }
+}
+__device__ __forceinline__ int tr_lookup(const uint32_t* key, uint32_t k, int bits) {  // -1: absent
+    const int mask = (1 << bits) - 1;
+    for (int h = tr_hash(k, bits);; h = (h + 1) & mask) {
+        const uint32_t v = key[h];
+        if (v == k) return h;
+        if (v == kTrEmpty) return -1;
+    }
+}
+
+__device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, TreeRefreshSmem& sm) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
+    PM_STAMP_ANY(55);
+    const pm_ctrl cs = *sp.ctrl;
+    const PerTree tree = per_tree(sp.per_work, sp.cap);
+    const uint32_t tag = __hip_atomic_load(tr_epoch(sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const bool last = mode & PM_UPD_LAST;
+    const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
+    const int ns = s_after >= B ? B : 0;  // an update that cannot train scatters nothing
+    const int64_t npos = (cs.pos + sp.n) % sp.cap;
+    const int64_t end1 = npos + sp.n < sp.cap ? npos + sp.n : sp.cap;
+    const int64_t end2 = npos + sp.n - sp.cap;  // > 0: the wrapped part [0, end2)
+    const int nedge = last ? (end2 > 0 ? 4 : 2) : 0;
+    const int ne = ns + nedge;
+    for (int k = t; k < kTrHash; k += kLearn) { sm.skey[k] = kTrEmpty; sm.ckey[k] = kTrEmpty; }
+    for (int k = t; k < 512; k += kLearn) { sm.ikey[k] = kTrEmpty; sm.iwin[k] = -1; }
+    for (int k = t; k < kTrSlots * PER_FAN; k += kLearn) (&sm.cmap[0][0])[k] = -1;
+    if (t == 0) { sm.nsub = 0; sm.nch = 0; sm.ok = 1; }
+    if (t < ne) {
+        const int64_t e = t < ns ? sp.idx[t] : (t - ns == 0 ? npos : t - ns == 1 ? end1 - 1 : t - ns == 2 ? 0 : end2 - 1);
+        sm.eidx[t] = (uint32_t)e;
+    }
+    __syncthreads();
+    if (t < ne) {
+        tr_insert(sm.skey, sm.eidx[t] / PER_SUB, 10);
+        if (t < ns) atomicMax(&sm.iwin[tr_insert(sm.ikey, sm.eidx[t], 9)], t);
+    }
+    __syncthreads();
+    if (t < kTrHash && sm.skey[t] != kTrEmpty) {  // compact: one level-1 slot per distinct sub-block
+        const int s = atomicAdd(&sm.nsub, 1);
+        sm.sslot[t] = s;
+        sm.subid[s] = sm.skey[t];
+    }
+    __syncthreads();
+    const int nsub = sm.nsub;
+    if (t < ne) sm.esub[t] = sm.sslot[tr_lookup(sm.skey, sm.eidx[t] / PER_SUB, 10)];
+    if (t < nsub) tr_insert(sm.ckey, sm.subid[t] / PER_FAN, 10);
+    __syncthreads();
+    if (t < kTrHash && sm.ckey[t] != kTrEmpty) {
+        const int c = atomicAdd(&sm.nch, 1);
+        sm.cslot[t] = c;
+        sm.chid[c] = sm.ckey[t];
+    }
+    __syncthreads();
+    const int nch = sm.nch;
+    if (t < nsub) sm.cmap[sm.cslot[tr_lookup(sm.ckey, sm.subid[t] / PER_FAN, 10)]][sm.subid[t] % PER_FAN] = (int16_t)t;
+    // LDS DMA: wave instruction i moves 1 KB: level-1 slots 4i .. 4i + 3 (64 leaves each) / level-2
+    // slots 8i .. 8i + 7 (16 nodes each); lanes past the count re-read the last slot
+    for (int i = wv; 4 * i < nsub; i += kLearn / 64) {
+        const int s = min(4 * i + (lane >> 4), nsub - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(tree.leaf + (size_t)sm.subid[s] * PER_SUB + 4 * (lane & 15)),
+                                         (lds_void*)&sm.lf[4 * i][0], 16, 0, 0);
+    }
+    for (int i = wv; 8 * i < nch; i += kLearn / 64) {
+        const int c = min(8 * i + (lane >> 3), nch - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(tree.sub + (size_t)sm.chid[c] * PER_FAN + 2 * (lane & 7)),
+                                         (lds_void*)&sm.ls[8 * i][0], 16, 0, 0);
+    }
+    PM_STAMP_ANY(56);
+    // the learner's granules: [0, B) each sample's new leaf, B the next push's max priority, B + 1 flags
+    if (t < B + 2) {
+        uint64_t g = 0;
+        bool got = false;
+        for (int it = 0; it < kTrPollMax; ++it) {
+            g = __hip_atomic_load(tr_granules(sp) + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(g >> 32) == tag) { got = true; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!got) sm.ok = 0;
+        const uint32_t v = (uint32_t)g;
+        if (t < B) sm.leaf_new[t] = __uint_as_float(v);
+        else if (t == B) sm.maxp_next = __uint_as_float(v);
+        else sm.scattered = (int)(v & 1u);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS DMA landed
+    __syncthreads();
+    PM_STAMP_ANY(57);
+    if (!sm.ok) {  // block-uniform: the learner's granules never came; the tree is left as it was
+        if (t == 0) {
+            atomicOr(&sp.ctrl->status, PM_CTRL_TREE_TIMEOUT);
+            __hip_atomic_store(tr_epoch(sp), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    if (sm.scattered && t < ns && sm.iwin[tr_lookup(sm.ikey, sm.eidx[t], 9)] == t)
+        sm.lf[sm.esub[t]][sm.eidx[t] % PER_SUB] = sm.leaf_new[t];  // the scatter's winner (:74-76)
+    const PushRange next = last ? PushRange{npos, sp.n, sp.cap, prio_pow(push_prio(s_after, sm.maxp_next), (float)sp.alpha)}
+                                : PushRange{0, 0, sp.cap, 0.f};
+    __syncthreads();
+    // level 1: 4 lanes per slot (one quarter each, per_quarter's order), combined as per_combine
+    for (int base = 0; base < 4 * nsub; base += kLearn) {
+        const int k = base + t, s = min(k >> 2, nsub - 1), q = k & 3;
+        const int64_t lo = (int64_t)sm.subid[s] * PER_SUB + 16 * q;
+        const int64_t d0 = next.dist(lo);
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            int64_t d = d0 + i;
+            if (d >= next.cap) d -= next.cap;
+            acc += lo + i < next.cap ? (double)(d < next.n ? next.pval : sm.lf[s][16 * q + i]) : 0.0;
+        }
+        const int b4 = lane & ~3;
+        const double v = per_combine(__shfl(acc, b4), __shfl(acc, b4 + 1), __shfl(acc, b4 + 2), __shfl(acc, b4 + 3));
+        if (q == 0 && k < 4 * nsub) {
+            sm.subv[s] = v;
+            tree.sub[sm.subid[s]] = v;
+        }
+    }
+    const double csub = per_sub_pushed_sum(next);
+    {   // the wholly pushed level-1 nodes of the next push: one constant
+        const RingNodes rn = ring_nodes(next, PER_SUB);
+        for (int64_t k = t; k < rn.count(); k += kLearn) {
+            const int64_t sb = rn.at(k);
+            if (per_sub_pushed(sb, next)) tree.sub[sb] = csub;
+        }
+    }
+    __syncthreads();
+    PM_STAMP_ANY(58);
+    // level 2: every chunk slot from LDS, its refreshed / pushed children substituted (per_chunk_sum)
+    if (t < nch) {
+        const int64_t c0 = (int64_t)sm.chid[t] * PER_FAN;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < PER_FAN; ++k) {
+            const int64_t sb = c0 + k;
+            const int m = sm.cmap[t][k];
+            const double v = m >= 0 ? sm.subv[m] : (per_sub_pushed(sb, next) ? csub : sm.ls[t][k]);
+            acc += sb < tree.nsub ? v : 0.0;
+        }
+        tree.chunk[sm.chid[t]] = acc;
+    }
+    {   // the next push's other level-2 nodes: inside a segment (no edge in them), all children pushed
+        const RingNodes rn = ring_nodes(next, PER_CHUNK);
+        for (int64_t k = t; k < rn.count(); k += kLearn) {
+            const int64_t ch = rn.at(k);
+            if (tr_lookup(sm.ckey, (uint32_t)ch, 10) >= 0) continue;  // refreshed above
+            double acc = 0.0;
+            for (int j = 0; j < PER_FAN; ++j) {
+                const int64_t sb = ch * PER_FAN + j;
+                acc += sb < tree.nsub ? (per_sub_pushed(sb, next) ? csub : tree.sub[sb]) : 0.0;
+            }
+            tree.chunk[ch] = acc;
+        }
+    }
+    PM_STAMP_ANY(59);
+    if (t == 0) __hip_atomic_store(tr_epoch(sp), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct LearnSmem {
     union {
         float gpart[16][256];  // gradient phase: per-wave partial sums
@@ -780,6 +1002,7 @@ union LearnShared {
     LearnSmem learn;
     ActShared act;
     PushFwdSmem pf;
+    TreeRefreshSmem tr;
 };
 static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 
@@ -792,11 +1015,15 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // push k_env just made, which this kernel computes; it sums the rollout's episode counters); LAST =
 // the step's last update (refreshes the sum tree for the next push, commits the step). U = 1: both.
 // Block 1 is push_fwd_block; the side-A act blocks (launches with side blocks) follow it.
-__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode) {
+__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode, int tr) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     if (blockIdx.x > 0) {
         if (blockIdx.x == 1) {
             push_fwd_block(sp, mode, shm.pf);
+            if (tr) {
+                __syncthreads();  // the push rows' LDS is reused
+                tree_block(sp, mode, shm.tr);
+            }
             return;
         }
         const int sb = (int)blockIdx.x - 2;  // side block index
@@ -838,6 +1065,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     const float wraw_l = t < B ? sp.isw[t] : 0.f;
     const int64_t id_l = t < B ? sp.idx[t] : 0;
     const float eps_v = t < 260 ? sp.learn_heads[528 + t] : 0.f;
+    const uint32_t tr_tag = tr ? __hip_atomic_load(tr_epoch(sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     // the rows k_env's forward blocks computed (hfeat [B][80]): sample t's Q block (floats 64..75,
     // phase 2's operands) to registers here; its 64 features go global -> LDS below, behind them
     float4 qh[3];
@@ -1011,13 +1239,22 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     // ---- phase 3: priority scatter; head gradients (16 waves x 16 samples, fixed-order combine)
     float mpx = 0.f;
     if (train) {
-        if (act && sm.hwin[slot] == t) {
-            sp.prios[id] = prio;
-            tree.leaf[id] = prio_pow(prio, (float)sp.alpha);
-            if (prio != prio) atomicOr(&sp.ctrl->status, PM_CTRL_NAN_PRIO);
-        }
         mpx = sm.red[0][2];
         for (int w = 1; w < 16; ++w) mpx = fmaxf(mpx, sm.red[w][2]);
+    }
+    const float leaf_v = act ? prio_pow(prio, (float)sp.alpha) : 0.f;
+    if (tr) {  // the tree-refresh block's inputs (tree_block): every sample's leaf, the next push's max
+               // priority and whether this update scatters, as tagged granules
+        if (t < B) tr_publish(sp, t, __float_as_uint(leaf_v), tr_tag);
+        if (t == B) tr_publish(sp, B, __float_as_uint(train ? fmaxf(cs.max_prio, mpx) : cs.max_prio), tr_tag);
+        if (t == B + 1) tr_publish(sp, B + 1, train ? 1u : 0u, tr_tag);
+    }
+    if (train) {
+        if (act && sm.hwin[slot] == t) {
+            sp.prios[id] = prio;
+            tree.leaf[id] = leaf_v;
+            if (prio != prio) atomicOr(&sp.ctrl->status, PM_CTRL_NAN_PRIO);
+        }
         if (t == 0) {
             float l = 0.f;
             for (int w = 0; w < 16; ++w) l += sm.red[w][1];
@@ -1039,7 +1276,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         for (int r = 0; r < 4; ++r) sm.u.gpart[wv][r * 64 + col] = g[r];
     }
     const float max_prio_next = train ? fmaxf(cs.max_prio, mpx) : cs.max_prio;
-    __threadfence_block();  // readers are this workgroup: no agent-scope L2 writeback
+    if (!tr) __threadfence_block();  // phase 4 re-reads the scattered leaves (this workgroup: no L2 writeback)
     __syncthreads();
     PM_STAMP(4);
 
@@ -1080,19 +1317,20 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             }
         }
         PM_STAMP(8); PM_STAMP_T(9, 960);
-        // level-1 nodes of the scatter: 4 lanes per sampled index (duplicates recompute the same
-        // node from the same leaves: identical values)
-        const int j = min(t >> 2, B - 1);
-        const int64_t sb = sm.sidx[j] / PER_SUB;
-        const double v = per_sub_sum4(tree.leaf, sb, next);
-        if ((t & 3) == 0) tree.sub[sb] = v;
+        if (!tr) {  // level-1 nodes of the scatter: 4 lanes per sampled index (duplicates recompute the
+                    // same node from the same leaves: identical values)
+            const int j = min(t >> 2, B - 1);
+            const int64_t sb = sm.sidx[j] / PER_SUB;
+            const double v = per_sub_sum4(tree.leaf, sb, next);
+            if ((t & 3) == 0) tree.sub[sb] = v;
+        }
         PM_STAMP(10); PM_STAMP_T(11, 960);
     } else {
         for (int k = t; k < kGradN; k += kLearn) sm.ap.g[k] = 0.f;
     }
     if (t == 0) { sm.ap.g[kGradN] = (float)ep_fin; sm.ap.g[kGradN + 1] = train ? 1.f : 0.f; }
-    {   // level-1 nodes of the next push: wholly pushed ones are one constant; the <= 4 partially
-        // pushed ones at the segment ends are summed from the leaves by 4 lanes of wave 0 each
+    if (!tr) {  // level-1 nodes of the next push: wholly pushed ones are one constant; the <= 4 partially
+                // pushed ones at the segment ends are summed from the leaves by 4 lanes of wave 0 each
         const RingNodes rn = ring_nodes(next, PER_SUB);
         const double csub = per_sub_pushed_sum(next);
         for (int64_t k = t; k < rn.count(); k += kLearn) {
@@ -1109,17 +1347,17 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         }
     }
     PM_STAMP(14); PM_STAMP_T(15, 960);
-    __threadfence_block();  // readers are this workgroup: no agent-scope L2 writeback
+    if (!tr) __threadfence_block();  // phase 5 re-reads the level-1 nodes (this workgroup: no L2 writeback)
     __syncthreads();
     PM_STAMP(5);
     for (int k = t; k < kGradN + 2; k += kLearn) sp.grad[k] = sm.ap.g[k];
     // ---- phase 5: level-2 nodes over the refreshed sub-blocks; beside them (fused) the target sync
     // and the three head folds of derive_weights, which run on threads 256.. (level 2's are < 256)
-    if (act && sm.hwin[slot] == t) {
+    if (!tr && act && sm.hwin[slot] == t) {
         const int64_t ch = id / PER_CHUNK;
         tree.chunk[ch] = per_chunk_sum(tree, ch);
     }
-    {
+    if (!tr) {
         const RingNodes rn = ring_nodes(next, PER_CHUNK);
         for (int64_t k = t; k < rn.count(); k += kLearn) {
             const int64_t ch = rn.at(k);
@@ -1905,11 +2143,21 @@ ActGrid learn_act_grid(const pm_selfplay* sp) {
     return ActGrid{sp->n, sp->n_pool + 1, std::min(4 * sp->chunk_A, kListMax), std::min(4 * sp->chunk_P, kListMax), 0};
 }
 
+// The sum-tree refresh in block 1 (tree_block) unless PONGMI_TR=0 (the learner's own refresh, A/B).
+int tree_refresh_block() {
+    static const int v = [] {
+        const char* e = getenv("PONGMI_TR");
+        return e && *e ? (atoi(e) != 0) : 1;
+    }();
+    return v;
+}
+
 int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st, int mode = PM_UPD_FIRST | PM_UPD_LAST) {
     const ActGrid g = learn_act_grid(sp);
     unsigned blocks = 2u + (with_act ? (unsigned)g.blocks() : 0u);  // learner, push-row block, side blocks
     if (with_act && sp->featB) blocks += (unsigned)((feat_ntiles(sp->n) + kFeatTilesLearn - 1) / kFeatTilesLearn);
-    pm_launch(PM_TIMER_LEARN, k_learn, dim3(blocks), dim3(kLearn), st, *sp, g.chunk0, g.chunk1, mode);
+    pm_launch(PM_TIMER_LEARN, k_learn, dim3(blocks), dim3(kLearn), st, *sp, g.chunk0, g.chunk1, mode,
+              tree_refresh_block());
     PM_LAUNCHED("k_learn");
     return PM_OK;
 }

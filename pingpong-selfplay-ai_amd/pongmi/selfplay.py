@@ -133,7 +133,8 @@ class SelfPlayLearner:
         self.isw = torch.zeros(self.batch, **f32)
         self.grad = torch.zeros(PM_GRAD_LEN, **f32)  # the packed exchange buffer (include/pongmi.h PM_GRAD_*)
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
-        self.hfeat = torch.zeros((2 * self.batch + 1, 80), **f32)  # + the push-row hand-off rows and flag
+        # + the push-row hand-off rows and flag, the tree-refresh epoch and granules (pongmi.h, ABI 21)
+        self.hfeat = torch.zeros((2 * self.batch + 8, 80), **f32)
         self.learn_heads = torch.zeros(3 * 264, **f32)
         self.obsA = torch.zeros((n, 7), **f32)
         self.obsB = torch.zeros((n, 7), **f32)
@@ -301,11 +302,12 @@ class SelfPlayLearner:
         """Device error bits (pm_ctrl.status): bit 0 = an update's push-row hand-off inside k_learn
         timed out (its push rows were not computed: that update is void); bit 1 = an update scattered
         a NaN priority (the loss diverged; the reference's sampler would raise on the NaN
-        probabilities). Raises on any bit."""
+        probabilities); bit 2 = k_learn's tree-refresh block timed out waiting for the learner (the
+        sum tree is stale). Raises on any bit."""
         st = int((c or self.counters())["status"])
         if st:
             raise _lib.PongmiError(f"self-play learner: device status {st} (bit 0: push-row hand-off timed out; "
-                                   f"bit 1: NaN priority scattered)")
+                                   f"bit 1: NaN priority scattered; bit 2: tree refresh timed out)")
 
     def set_epsilon(self, eps):
         c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))

@@ -30,7 +30,8 @@ NAMES = {
     35: "ph0 before prologue", 34: "ph0 after prologue", 40: "ph0 w0 loads landed",
     41: "ph0 w4 loads landed", 42: "ph0 w8 loads landed", 43: "ph0 w15 loads landed",
     50: "push blk start", 51: "push blk loads", 52: "push blk fwd done", 53: "push blk stores drained",
-    54: "learn push flag seen",
+    54: "learn push flag seen", 55: "tree blk start", 56: "tree blk prefetch issued",
+    57: "tree blk granules + DMA in", 58: "tree blk level 1 done", 59: "tree blk level 2 done",
     5: "learn tree level1", 6: "learn tree level2", 20: "apply adam", 21: "apply derive", 7: "learn end",
 }
 

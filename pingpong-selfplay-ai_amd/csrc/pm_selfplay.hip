@@ -921,18 +921,28 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
         const int k = base + t, s = min(k >> 2, nsub - 1), q = k & 3;
         const int64_t lo = (int64_t)sm.subid[s] * PER_SUB + 16 * q;
         const int64_t d0 = next.dist(lo);
+        float v[16];  // the quarter's 16 leaves, read before any select (no load under a branch)
+        const float4* l4 = reinterpret_cast<const float4*>(&sm.lf[s][16 * q]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 x = l4[j];
+            v[4 * j] = x.x; v[4 * j + 1] = x.y; v[4 * j + 2] = x.z; v[4 * j + 3] = x.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(v[j]));  // read unconditionally, then selected
         double acc = 0.0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             int64_t d = d0 + i;
-            if (d >= next.cap) d -= next.cap;
-            acc += lo + i < next.cap ? (double)(d < next.n ? next.pval : sm.lf[s][16 * q + i]) : 0.0;
+            d = d >= next.cap ? d - next.cap : d;
+            const double x = (double)(d < next.n ? next.pval : v[i]);
+            acc += lo + i < next.cap ? x : 0.0;
         }
         const int b4 = lane & ~3;
-        const double v = per_combine(__shfl(acc, b4), __shfl(acc, b4 + 1), __shfl(acc, b4 + 2), __shfl(acc, b4 + 3));
+        const double node = per_combine(__shfl(acc, b4), __shfl(acc, b4 + 1), __shfl(acc, b4 + 2), __shfl(acc, b4 + 3));
         if (q == 0 && k < 4 * nsub) {
-            sm.subv[s] = v;
-            tree.sub[sm.subid[s]] = v;
+            sm.subv[s] = node;
+            tree.sub[sm.subid[s]] = node;
         }
     }
     const double csub = per_sub_pushed_sum(next);
@@ -948,12 +958,24 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
     // level 2: every chunk slot from LDS, its refreshed / pushed children substituted (per_chunk_sum)
     if (t < nch) {
         const int64_t c0 = (int64_t)sm.chid[t] * PER_FAN;
+        // every operand read unconditionally first (the compiler otherwise sinks each LDS read into
+        // its own branch), then selected in per_chunk_sum's order
+        double old[PER_FAN], fresh[PER_FAN];
+        int m[PER_FAN];
+#pragma unroll
+        for (int k = 0; k < PER_FAN; ++k) {
+            m[k] = sm.cmap[t][k];
+            old[k] = sm.ls[t][k];
+        }
+#pragma unroll
+        for (int k = 0; k < PER_FAN; ++k) fresh[k] = sm.subv[m[k] >= 0 ? m[k] : 0];
+#pragma unroll
+        for (int k = 0; k < PER_FAN; ++k) asm volatile("" : "+v"(old[k]), "+v"(fresh[k]));
         double acc = 0.0;
 #pragma unroll
         for (int k = 0; k < PER_FAN; ++k) {
             const int64_t sb = c0 + k;
-            const int m = sm.cmap[t][k];
-            const double v = m >= 0 ? sm.subv[m] : (per_sub_pushed(sb, next) ? csub : sm.ls[t][k]);
+            const double v = m[k] >= 0 ? fresh[k] : (per_sub_pushed(sb, next) ? csub : old[k]);
             acc += sb < tree.nsub ? v : 0.0;
         }
         tree.chunk[sm.chid[t]] = acc;

@@ -913,14 +913,20 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
     }
     if (sm.scattered && t < ns && sm.iwin[tr_lookup(sm.ikey, sm.eidx[t], 9)] == t)
         sm.lf[sm.esub[t]][sm.eidx[t] % PER_SUB] = sm.leaf_new[t];  // the scatter's winner (:74-76)
-    const PushRange next = last ? PushRange{npos, sp.n, sp.cap, prio_pow(push_prio(s_after, sm.maxp_next), (float)sp.alpha)}
-                                : PushRange{0, 0, sp.cap, 0.f};
+    const float pval = last ? prio_pow(push_prio(s_after, sm.maxp_next), (float)sp.alpha) : 0.f;
+    const PushRange next = last ? PushRange{npos, sp.n, sp.cap, pval} : PushRange{0, 0, sp.cap, 0.f};
+    // the next push in 32-bit bounds (cap < 2^31): entries [q1lo, q1hi) and [0, q2hi); wholly pushed
+    // level-1 nodes [p1lo, p1hi) and [0, p2hi) — what per_leaf / per_sub_pushed decide, without
+    // their 64-bit ring arithmetic per element
+    const int cap32 = (int)sp.cap;
+    const int q1lo = last ? (int)npos : 0, q1hi = last ? (int)end1 : 0, q2hi = last && end2 > 0 ? (int)end2 : 0;
+    const int p1lo = (q1lo + PER_SUB - 1) / PER_SUB, p1hi = q1hi / PER_SUB, p2hi = q2hi / PER_SUB;
+    PM_STAMP_ANY(60);
     __syncthreads();
     // level 1: 4 lanes per slot (one quarter each, per_quarter's order), combined as per_combine
     for (int base = 0; base < 4 * nsub; base += kLearn) {
         const int k = base + t, s = min(k >> 2, nsub - 1), q = k & 3;
-        const int64_t lo = (int64_t)sm.subid[s] * PER_SUB + 16 * q;
-        const int64_t d0 = next.dist(lo);
+        const int lo = (int)sm.subid[s] * PER_SUB + 16 * q;
         float v[16];  // the quarter's 16 leaves, read before any select (no load under a branch)
         const float4* l4 = reinterpret_cast<const float4*>(&sm.lf[s][16 * q]);
 #pragma unroll
@@ -929,14 +935,14 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
             v[4 * j] = x.x; v[4 * j + 1] = x.y; v[4 * j + 2] = x.z; v[4 * j + 3] = x.w;
         }
 #pragma unroll
-        for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(v[j]));  // read unconditionally, then selected
+        for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(v[j]));
         double acc = 0.0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            int64_t d = d0 + i;
-            d = d >= next.cap ? d - next.cap : d;
-            const double x = (double)(d < next.n ? next.pval : v[i]);
-            acc += lo + i < next.cap ? x : 0.0;
+            const int e = lo + i;
+            const bool pushed = (e >= q1lo && e < q1hi) || e < q2hi;
+            const double x = (double)(pushed ? pval : v[i]);
+            acc += e < cap32 ? x : 0.0;  // past cap: no leaf
         }
         const int b4 = lane & ~3;
         const double node = per_combine(__shfl(acc, b4), __shfl(acc, b4 + 1), __shfl(acc, b4 + 2), __shfl(acc, b4 + 3));
@@ -945,19 +951,19 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
             tree.sub[sm.subid[s]] = node;
         }
     }
+    PM_STAMP_ANY(61);
     const double csub = per_sub_pushed_sum(next);
     {   // the wholly pushed level-1 nodes of the next push: one constant
-        const RingNodes rn = ring_nodes(next, PER_SUB);
-        for (int64_t k = t; k < rn.count(); k += kLearn) {
-            const int64_t sb = rn.at(k);
-            if (per_sub_pushed(sb, next)) tree.sub[sb] = csub;
-        }
+        const int n1 = p1hi > p1lo ? p1hi - p1lo : 0;
+        for (int k = t; k < n1 + p2hi; k += kLearn) tree.sub[k < n1 ? p1lo + k : k - n1] = csub;
     }
+    PM_STAMP_ANY(62);
     __syncthreads();
     PM_STAMP_ANY(58);
     // level 2: every chunk slot from LDS, its refreshed / pushed children substituted (per_chunk_sum)
+    const int nsub_tree = (int)tree.nsub;
     if (t < nch) {
-        const int64_t c0 = (int64_t)sm.chid[t] * PER_FAN;
+        const int c0 = (int)sm.chid[t] * PER_FAN;
         // every operand read unconditionally first (the compiler otherwise sinks each LDS read into
         // its own branch), then selected in per_chunk_sum's order
         double old[PER_FAN], fresh[PER_FAN];
@@ -974,23 +980,25 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
         double acc = 0.0;
 #pragma unroll
         for (int k = 0; k < PER_FAN; ++k) {
-            const int64_t sb = c0 + k;
-            const double v = m[k] >= 0 ? fresh[k] : (per_sub_pushed(sb, next) ? csub : old[k]);
-            acc += sb < tree.nsub ? v : 0.0;
+            const int sb = c0 + k;
+            const bool pushed = (sb >= p1lo && sb < p1hi) || sb < p2hi;
+            const double v = m[k] >= 0 ? fresh[k] : (pushed ? csub : old[k]);
+            acc += sb < nsub_tree ? v : 0.0;
         }
         tree.chunk[sm.chid[t]] = acc;
     }
-    {   // the next push's other level-2 nodes: inside a segment (no edge in them), all children pushed
-        const RingNodes rn = ring_nodes(next, PER_CHUNK);
-        for (int64_t k = t; k < rn.count(); k += kLearn) {
-            const int64_t ch = rn.at(k);
-            if (tr_lookup(sm.ckey, (uint32_t)ch, 10) >= 0) continue;  // refreshed above
-            double acc = 0.0;
-            for (int j = 0; j < PER_FAN; ++j) {
-                const int64_t sb = ch * PER_FAN + j;
-                acc += sb < tree.nsub ? (per_sub_pushed(sb, next) ? csub : tree.sub[sb]) : 0.0;
-            }
-            tree.chunk[ch] = acc;
+    PM_STAMP_ANY(63);
+    if (last) {  // the next push's other level-2 nodes: inside a segment (every boundary chunk holds an
+                 // edge entry, so it has a slot), all 16 children wholly pushed: one constant
+        double cc = 0.0;
+#pragma unroll
+        for (int k = 0; k < PER_FAN; ++k) cc += csub;
+        const int c1lo = q1lo / PER_CHUNK, c1hi = (q1hi - 1) / PER_CHUNK + 1;
+        const int c2hi = q2hi > 0 ? (q2hi - 1) / PER_CHUNK + 1 : 0;
+        const int n1 = c1hi > c1lo ? c1hi - c1lo : 0;
+        for (int k = t; k < n1 + c2hi; k += kLearn) {
+            const int ch = k < n1 ? c1lo + k : k - n1;
+            if (tr_lookup(sm.ckey, (uint32_t)ch, 10) < 0) tree.chunk[ch] = cc;
         }
     }
     PM_STAMP_ANY(59);

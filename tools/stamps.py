@@ -32,6 +32,8 @@ NAMES = {
     50: "push blk start", 51: "push blk loads", 52: "push blk fwd done", 53: "push blk stores drained",
     54: "learn push flag seen", 55: "tree blk start", 56: "tree blk prefetch issued",
     57: "tree blk granules + DMA in", 58: "tree blk level 1 done", 59: "tree blk level 2 done",
+    60: "tree blk winners + pval (t0)", 61: "tree blk level-1 sums (t0)", 62: "tree blk pushed subs (t0)",
+    63: "tree blk chunk slots (t0)",
     5: "learn tree level1", 6: "learn tree level2", 20: "apply adam", 21: "apply derive", 7: "learn end",
 }
 

@@ -39,6 +39,12 @@ static __device__ unsigned long long pm_diag_blk[8][4096];
     do {                                                                                           \
         if (threadIdx.x == 0 && blockIdx.x < 4096) pm_diag_blk[(k)][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// latest end over the blocks of one role (block-wide: a barrier, then thread 0's atomic max)
+#define PM_STAMP_MAX(slot)                                                                              \
+    do {                                                                                                \
+        __syncthreads();                                                                                \
+        if (threadIdx.x == 0) atomicMax(&pm_diag_buf[(slot)], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+    } while (0)
 #define PM_STAMP_T(slot, tid)                                                                            \
     do {                                                                                                 \
         if (threadIdx.x == (tid) && blockIdx.x == 0) pm_diag_buf[(slot)] = __builtin_amdgcn_s_memrealtime(); \
@@ -52,6 +58,9 @@ static __device__ unsigned long long pm_diag_blk[8][4096];
     } while (0)
 #define PM_STAMP_T(slot, tid) \
     do {                      \
+    } while (0)
+#define PM_STAMP_MAX(slot) \
+    do {                   \
     } while (0)
 #define PM_STAMP_ANY(slot) \
     do {                   \

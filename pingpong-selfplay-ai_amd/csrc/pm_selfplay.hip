@@ -1062,6 +1062,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB), started at once
             const int t0 = fb * kFeatTilesLearn;
             feat_tiles(shm.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + kFeatTilesLearn, feat_ntiles(sp.n)), sp.featB);
+            PM_STAMP_MAX(67);
             return;
         }
         // the learner's load phase is latency-bound under these blocks' staging burst; they have slack
@@ -1070,6 +1071,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
         act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,
                   sb, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
+        PM_STAMP_MAX(66);
         return;
     }
     LearnSmem& sm = shm.learn;

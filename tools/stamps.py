@@ -33,7 +33,8 @@ NAMES = {
     54: "learn push flag seen", 55: "tree blk start", 56: "tree blk prefetch issued",
     57: "tree blk granules + DMA in", 58: "tree blk level 1 done", 59: "tree blk level 2 done",
     60: "tree blk winners + pval (t0)", 61: "tree blk level-1 sums (t0)", 62: "tree blk pushed subs (t0)",
-    63: "tree blk chunk slots (t0)",
+    63: "tree blk chunk slots (t0)", 66: "learn launch: side-A act blocks end (max)",
+    67: "learn launch: feature blocks end (max)",
     5: "learn tree level1", 6: "learn tree level2", 20: "apply adam", 21: "apply derive", 7: "learn end",
 }
 

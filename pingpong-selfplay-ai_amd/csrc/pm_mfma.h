@@ -316,6 +316,65 @@ __device__ __forceinline__ void tile_heads(const float* hf, const f32x16 (&c2)[2
     q[2] = v + (a2 - mean);
 }
 
+// Layer 1 (both 32-row tiles) and layer-2 tile jt of tile_hidden (pm_mfma.h), MFMA for MFMA in the same
+// order: the two layer-2 tiles are independent accumulator chains, so a wave computing one of them
+// produces exactly the registers tile_hidden gives for it.
+template <typename F>
+__device__ __forceinline__ void hidden_half(const float* lw, const float (&xs)[4], int lane, int jt, f32x16& c2,
+                                            F&& valu) {
+    const int h = lane >> 5;
+    f32x16 c1[2];
+    const f32x16 zero = {};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const float4 w = reinterpret_cast<const float4*>(lw + F_W1)[t * 64 + lane];
+        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, xs[0], zero, 0, 0, 0);
+        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, xs[1], c1[t], 0, 0, 0);
+        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, xs[2], c1[t], 0, 0, 0);
+        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, xs[3], c1[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) c1[t][r] = relu(c1[t][r]);
+    {
+        const float4* b = reinterpret_cast<const float4*>(lw + F_B2 + (jt * 2 + h) * 16);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 v = b[q4];
+            c2[4 * q4 + 0] = v.x; c2[4 * q4 + 1] = v.y; c2[4 * q4 + 2] = v.z; c2[4 * q4 + 3] = v.w;
+        }
+    }
+    const float4* w2 = reinterpret_cast<const float4*>(lw + F_W2) + lane + jt * 8 * 64;
+    float4 wcur = w2[0];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {  // g = t * 4 + rq (tile_hidden's g8 for this jt)
+        const int t = g >> 2, rq = g & 3;
+        const float4 wnext = w2[((g + 1) & 7) * 64];
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.x, c1[t][4 * rq + 0], c2, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.y, c1[t][4 * rq + 1], c2, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.z, c1[t][4 * rq + 2], c2, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.w, c1[t][4 * rq + 3], c2, 0, 0, 0);
+        valu(g);  // independent VALU work, scheduled between this group's dependent MFMAs
+        wcur = wnext;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// tile_heads' fmaf chains over the rows of one layer-2 tile (t = the tile), continuing from acc.
+__device__ __forceinline__ void heads_half(const float* hf, const f32x16& c2, int lane, int t, float (&acc)[4]) {
+    const float4* hw = reinterpret_cast<const float4*>(hf + (lane >> 5) * 128) + t * 16;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float x = relu(c2[r]);
+        const float4 w = hw[r];
+        acc[0] = fmaf(w.x, x, acc[0]);
+        acc[1] = fmaf(w.y, x, acc[1]);
+        acc[2] = fmaf(w.z, x, acc[2]);
+        acc[3] = fmaf(w.w, x, acc[3]);
+    }
+}
+
 // layer-1 B operands of this lane for observation row o: input k' = 2s + h, k' = 0 -> 1.0 (bias),
 // k' >= 1 -> o[k' - 1]
 __device__ __forceinline__ void tile_inputs(const float* __restrict__ o, int h, float (&xs)[4]) {
@@ -335,7 +394,7 @@ struct TilePre {
 // QNet forward + action for `count` arenas listed in LDS `list` (arena indices), weights staged in
 // LDS `lw`. Each wave takes tiles wave, wave + nwaves, ... Wave-uniform control flow throughout.
 __device__ __forceinline__ void run_tiles(const float* lw, const float* __restrict__ obs, const int* list, int count,
-                                          const TileOut& out, const TilePre& pre) {
+                                          const TileOut& out, const TilePre pre) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int h = lane >> 5, col = lane & 31;
     const int ntiles = (count + 31) >> 5;
@@ -410,20 +469,27 @@ struct ActGrid {
 };
 
 constexpr int kActBlock = 256;
-constexpr int kListMax = 4096;  // max chunk size
+constexpr int kListMax = 4096;        // max chunk size (the act kernels' 256-thread blocks)
+constexpr int kListMaxLearn = 16384;  // k_learn's 1024-thread side-A blocks (16 ids per thread)
 
-struct ActShared {
+template <int LIST>
+struct ActSharedT {
+    static constexpr int kList = LIST;
     float lw[kLwFloats];  // fragment image, padded to whole 1 KB wave chunks
-    int list[kListMax];
+    int list[LIST];
     int count;
     int wtot[16];  // one per wave: up to 1024-thread blocks (k_learn's side-A act blocks)
-    int lpre[16], loff[16], lcnt[16];  // per 256-arena segment of the env kernel's opponent lists
+    int lpre[LIST / 256], loff[LIST / 256], lcnt[LIST / 256];  // per 256-arena segment of the env kernel's lists
 };
+using ActShared = ActSharedT<kListMax>;
+using ActSharedLearn = ActSharedT<kListMaxLearn>;
+static_assert(kListMaxLearn / 256 <= 64, "one lane per list segment in act_block's scan");
 
 // Block-wide body of the grouped act kernel for grid block b (blockDim.x == kActBlock). side B:
 // eps-greedy on obsB with w_B; side A: greedy on obsA with w_opp[net]. opp == nullptr -> every
 // arena plays net 0.
-__device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const float* __restrict__ w_opp,
+template <class Sh>
+__device__ __forceinline__ void act_block(Sh& sh, const ActGrid& g, const float* __restrict__ w_opp,
                                           const int32_t* __restrict__ opp, const float* __restrict__ w_B,
                                           const float* __restrict__ obsA, const float* __restrict__ obsB,
                                           TileOut outA, TileOut outB, int b,
@@ -457,7 +523,7 @@ __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const
     if (compact && !lists) compact_load(opp, lo, hi, ids);
     PM_BLK(4);
     if (lists) {
-        const int g0 = lo >> 8, G = (hi - lo + 255) >> 8;  // <= kListMax / 256 = 16 segments
+        const int g0 = lo >> 8, G = (hi - lo + 255) >> 8;  // <= Sh::kList / 256 segments (<= 64)
         if (threadIdx.x < 64) {
             const int lane = threadIdx.x;
             const int v = lane < G ? opp_cnt[(size_t)(g0 + lane) * g.n_opp + net] : 0;
@@ -472,8 +538,8 @@ __device__ __forceinline__ void act_block(ActShared& sh, const ActGrid& g, const
             if (lane == 63) sh.count = incl;
         }
         __syncthreads();
-        const int seg = threadIdx.x >> 4, j0 = threadIdx.x & 15;  // 16 threads per segment
-        if (seg < G) {
+        const int j0 = threadIdx.x & 15;  // 16 threads per segment
+        for (int seg = threadIdx.x >> 4; seg < G; seg += blockDim.x >> 4) {
             const int c = sh.lcnt[seg], dst = sh.lpre[seg];
             const int32_t* src = opp_list + (size_t)(g0 + seg) * 256 + sh.loff[seg];
             int v[16];

@@ -101,51 +101,6 @@ __device__ __forceinline__ void fetch_heads_async(const float* __restrict__ ws, 
         : "memory", "m0");
 }
 
-// Layer 1 (both 32-row tiles) and layer-2 tile jt of tile_hidden (pm_mfma.h), MFMA for MFMA in the same
-// order: the two layer-2 tiles are independent accumulator chains, so a wave computing one of them
-// produces exactly the registers tile_hidden gives for it.
-template <typename F>
-__device__ __forceinline__ void hidden_half(const float* lw, const float (&xs)[4], int lane, int jt, f32x16& c2,
-                                            F&& valu) {
-    const int h = lane >> 5;
-    f32x16 c1[2];
-    const f32x16 zero = {};
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const float4 w = reinterpret_cast<const float4*>(lw + F_W1)[t * 64 + lane];
-        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, xs[0], zero, 0, 0, 0);
-        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, xs[1], c1[t], 0, 0, 0);
-        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, xs[2], c1[t], 0, 0, 0);
-        c1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, xs[3], c1[t], 0, 0, 0);
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) c1[t][r] = relu(c1[t][r]);
-    {
-        const float4* b = reinterpret_cast<const float4*>(lw + F_B2 + (jt * 2 + h) * 16);
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-            const float4 v = b[q4];
-            c2[4 * q4 + 0] = v.x; c2[4 * q4 + 1] = v.y; c2[4 * q4 + 2] = v.z; c2[4 * q4 + 3] = v.w;
-        }
-    }
-    const float4* w2 = reinterpret_cast<const float4*>(lw + F_W2) + lane + jt * 8 * 64;
-    float4 wcur = w2[0];
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {  // g = t * 4 + rq (tile_hidden's g8 for this jt)
-        const int t = g >> 2, rq = g & 3;
-        const float4 wnext = w2[((g + 1) & 7) * 64];
-        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.x, c1[t][4 * rq + 0], c2, 0, 0, 0);
-        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.y, c1[t][4 * rq + 1], c2, 0, 0, 0);
-        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.z, c1[t][4 * rq + 2], c2, 0, 0, 0);
-        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(wcur.w, c1[t][4 * rq + 3], c2, 0, 0, 0);
-        valu(g);  // independent VALU work, scheduled between this group's dependent MFMAs
-        wcur = wnext;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
 // serve_draw (pm_dev.h) for the step-keyed stream, split into four stages so that its integer and fp64
 // work fills the gaps of the dependent MFMA chain: the same expressions in the same order, so the
 // draw is bit-identical. Every lane draws, done or not (the select happens after the tick).
@@ -171,20 +126,6 @@ struct StagedServe {
         }
     }
 };
-
-// tile_heads' fmaf chains over the rows of one layer-2 tile (t = the tile), continuing from acc.
-__device__ __forceinline__ void heads_half(const float* hf, const f32x16& c2, int lane, int t, float (&acc)[4]) {
-    const float4* hw = reinterpret_cast<const float4*>(hf + (lane >> 5) * 128) + t * 16;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const float x = relu(c2[r]);
-        const float4 w = hw[r];
-        acc[0] = fmaf(w.x, x, acc[0]);
-        acc[1] = fmaf(w.y, x, acc[1]);
-        acc[2] = fmaf(w.z, x, acc[2]);
-        acc[3] = fmaf(w.w, x, acc[3]);
-    }
-}
 
 // The collecting rollout's replay target (pm_roll_replay, device side).
 struct RollPush {

@@ -14,6 +14,7 @@
 // Every loop counter lives in the device control block (pm_ctrl), so a whole vector step can be
 // replayed from a captured graph.
 #include <algorithm>
+#include <cmath>
 
 #include "pm_host.h"
 #include "pm_mfma.h"
@@ -26,6 +27,12 @@ using namespace pm;
 // wave's instruction stream reaches it (no drain: stores still in flight are not waited for);
 // PM_ENV_STAMP_DRAIN first waits for every outstanding memory operation of the wave.
 static __device__ unsigned long long pm_diag_env[8][1024];
+// k_learn's side blocks: [0] begin, [1] after the act blocks' sleep, [2] end, [3] role | rows << 16
+static __device__ unsigned long long pm_diag_side[4][1024];
+#define PM_SIDE(k, sb, v)                                                        \
+    do {                                                                         \
+        if (threadIdx.x == 0 && (sb) < 1024) pm_diag_side[(k)][(sb)] = (v);      \
+    } while (0)
 #define PM_ENV_STAMP(k, blk)                                                                   \
     do {                                                                                       \
         asm volatile("" ::: "memory");                                                         \
@@ -37,6 +44,9 @@ static __device__ unsigned long long pm_diag_env[8][1024];
         if (threadIdx.x == 0 && (blk) < 1024) pm_diag_env[(k)][(blk)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
+#define PM_SIDE(k, sb, v) \
+    do {                  \
+    } while (0)
 #define PM_ENV_STAMP(k, blk) \
     do {                     \
     } while (0)
@@ -77,9 +87,12 @@ __device__ __forceinline__ PushRange push_of(const pm_selfplay& sp, int64_t pos,
 // push has not landed yet (update 0, drawn beside k_env: the tree accounts for it and its leaves read
 // as the pushed value); otherwise (updates 1..U-1) the replay is as k_env left it. The fill is the
 // post-push one either way: pos/size advance only when the step commits.
-template <class Hook = NoHook>
+// NS: samples per block (PER_BS, or 32 for the split forward of k_actenv's sampler blocks: lanes of the
+// block's upper half then descend for samples no output is taken from).
+template <int NS = PER_BS, class Hook = NoHook>
 __device__ __forceinline__ void sample_block(const pm_selfplay& sp, int b, bool pending, PerSampleSmem& sm,
                                              int64_t* sidx = nullptr, Hook l2done = Hook()) {
+    static_assert(NS == PER_BS || NS == PER_BS / 2, "64 or 32 samples per block");
     const pm_ctrl* c = sp.ctrl;
     const int64_t s = c->size + sp.n;
     const int64_t size = s < sp.cap ? s : sp.cap;
@@ -87,7 +100,8 @@ __device__ __forceinline__ void sample_block(const pm_selfplay& sp, int b, bool 
     const PushRange pr = pending ? push_of(sp, c->pos, c->size, c->max_prio) : PushRange{0, 0, sp.cap, 0.f};
     const uint64_t key = sp.seed_env;
     per_sample_block(
-        size >= sp.batch, size, per_tree(sp.per_work, sp.cap), pr, beta_of(sp, frame), b * PER_BS, sp.batch, sm,
+        size >= sp.batch, size, per_tree(sp.per_work, sp.cap), pr, beta_of(sp, frame), b * NS,
+        min(sp.batch, b * NS + NS), sm,
         [&](int j) {
             const U4 r = philox64((uint32_t)j, TAG_PER, (uint64_t)frame, key);
             return u53(r.x, r.y);
@@ -95,7 +109,7 @@ __device__ __forceinline__ void sample_block(const pm_selfplay& sp, int b, bool 
         [&](int j, int64_t idx, float w) {
             sp.idx[j] = idx;
             sp.isw[j] = w;
-            if (sidx) sidx[j - b * PER_BS] = idx;
+            if (sidx) sidx[j - b * NS] = idx;
         },
         l2done);
 }
@@ -255,6 +269,99 @@ __device__ __forceinline__ void sample_fwd_block(const pm_selfplay& sp, int b, S
     float rb[2];
     batch_row_fwd(sp, sm.lw, sm.hf, sm.hf + 264, id, nxt, lane, c2, qb, qt, rb);
     if (mine) store_hfeat(sp.hfeat, j, nxt, lane, c2, qb, qt, rb);
+}
+
+// The split variant (PONGMI_SFB=32, the default): block b draws samples [32 b, 32 b + 32) and its 4 waves
+// split the forward of the 2 tiles (s rows, s' rows) by layer-2 tile, as k_rollout16 does (pm_mfma.h
+// hidden_half / heads_half): wave 2 k + jt computes layer-2 tile jt of tile k (24 MFMAs deep instead of
+// 40); wave jt = 0 runs the head chains over its 32 units and hands the partial sums to wave jt = 1
+// through LDS, which continues them in tile_heads' order. Every stored value is bit-identical to
+// sample_fwd_block's. s rows need only Q_B (store_hfeat stores Q_T of s' rows only).
+struct SampleFwd32Smem {
+    PerSampleSmem per;
+    float lw[kLwFloats];
+    float hf[pad256(2 * 264)];
+    int64_t sidx[PER_BS / 2];
+    float part[2][64][8];  // [tile][lane]: Q_B chains 0..3, Q_T chains 4..7 after layer-2 tile 0
+};
+__device__ __forceinline__ void sample_fwd_block32(const pm_selfplay& sp, int b, SampleFwd32Smem& sm) {
+    constexpr int NS = PER_BS / 2;
+    sample_block<NS>(sp, b, true, sm.per, sm.sidx, [&] {
+        stage_frags_lds(sp.w_B, sm.lw, b * 5);
+        copy_lds_f32x4<2 * 264>(sp.learn_heads, sm.hf);
+    });
+    if (!learner_active(sp)) return;  // block-uniform
+    __syncthreads();  // sidx, staged weights
+    PM_BLK(1);
+    const int lane = threadIdx.x & 63, B = sp.batch;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool nxt = (wv >> 1) != 0;  // wave-uniform: tile 0 = s rows, tile 1 = s' rows
+    const int jt = wv & 1;
+    const int j = b * NS + (lane & 31);
+    const int64_t id = sm.sidx[min(j, B - 1) - b * NS];
+    const pm_ctrl* c = sp.ctrl;
+    const bool mine = j < B && !push_of(sp, c->pos, c->size, c->max_prio).covers(id);
+    float xs[4];
+    const float* tr = sp.trans + id * PM_TRANS_F;
+    tile_inputs(tr + (nxt ? 8 : 0), lane >> 5, xs);
+    const float rb0 = tr[7], rb1 = tr[15];
+    f32x16 c2;
+    hidden_half(sm.lw, xs, lane, jt, c2, [](int) {});
+    const float* hf0 = sm.hf;
+    const float* hf1 = sm.hf + 264;
+    float ab[4] = {0.f, 0.f, 0.f, 0.f}, at[4] = {0.f, 0.f, 0.f, 0.f};
+    float* row = sp.hfeat + (size_t)j * 80;
+    const int h = lane >> 5;
+    if (jt == 0) {
+        heads_half(hf0, c2, lane, 0, ab);
+        if (nxt) heads_half(hf1, c2, lane, 0, at);
+        *reinterpret_cast<float4*>(&sm.part[nxt][lane][0]) = make_float4(ab[0], ab[1], ab[2], ab[3]);
+        if (nxt) *reinterpret_cast<float4*>(&sm.part[nxt][lane][4]) = make_float4(at[0], at[1], at[2], at[3]);
+    }
+    if (mine && !nxt) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) row[32 * jt + rho(q) + 4 * h] = relu(c2[q]);
+    }
+    __syncthreads();  // the chains over layer-2 tile 0
+    if (jt == 0) return;
+    auto finish = [&](float (&acc)[4], const float* hf, float (&q)[3]) {
+        float v = acc[0], a0 = acc[1], a1 = acc[2], a2 = acc[3];
+        v += __shfl_xor(v, 32);
+        a0 += __shfl_xor(a0, 32);
+        a1 += __shfl_xor(a1, 32);
+        a2 += __shfl_xor(a2, 32);
+        v += hf[256];
+        a0 += hf[257];
+        a1 += hf[258];
+        a2 += hf[259];
+        const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
+        q[0] = v + (a0 - mean);
+        q[1] = v + (a1 - mean);
+        q[2] = v + (a2 - mean);
+    };
+    {
+        const float4 pa = *reinterpret_cast<const float4*>(&sm.part[nxt][lane][0]);
+        ab[0] = pa.x; ab[1] = pa.y; ab[2] = pa.z; ab[3] = pa.w;
+    }
+    heads_half(hf0, c2, lane, 1, ab);
+    float qb[3], qt[3];
+    finish(ab, hf0, qb);
+    if (nxt) {
+        const float4 pt = *reinterpret_cast<const float4*>(&sm.part[nxt][lane][4]);
+        at[0] = pt.x; at[1] = pt.y; at[2] = pt.z; at[3] = pt.w;
+        heads_half(hf1, c2, lane, 1, at);
+        finish(at, hf1, qt);
+    }
+    if (mine && h == 0) {
+        if (!nxt) {
+            row[64] = qb[0]; row[65] = qb[1]; row[66] = qb[2];
+            row[67] = rb0;  // reward
+            row[71] = rb1;  // action | done << 8 (float bits)
+        } else {
+            row[68] = qb[0]; row[69] = qb[1]; row[70] = qb[2];
+            row[72] = qt[0]; row[73] = qt[1]; row[74] = qt[2];
+        }
+    }
 }
 
 __device__ __forceinline__ void write_opp_lists(const pm_selfplay& sp, OppListSmem& sm, int blk, int i, bool valid,
@@ -468,13 +575,17 @@ __global__ __launch_bounds__(kBlock) void k_env(const pm_selfplay sp) {
 union ActEnvShared {
     ActEnvSmem ae;
     SampleFwdSmem sf;
+    SampleFwd32Smem sf32;
 };
+// NS: samples per sampler block (64: sample_fwd_block, 32: sample_fwd_block32).
+template <int NS>
 __global__ __launch_bounds__(kBlock) void k_actenv(const pm_selfplay sp) {
     __shared__ __attribute__((aligned(16))) ActEnvShared sh;
-    const int nsb = (sp.batch + PER_BS - 1) / PER_BS;
+    const int nsb = (sp.batch + NS - 1) / NS;
     if ((int)blockIdx.x < nsb) {
         PM_BLK(0);
-        sample_fwd_block(sp, (int)blockIdx.x, sh.sf);
+        if constexpr (NS == PER_BS) sample_fwd_block(sp, (int)blockIdx.x, sh.sf);
+        else sample_fwd_block32(sp, (int)blockIdx.x, sh.sf32);
         PM_BLK_END();
         return;
     }
@@ -669,8 +780,10 @@ __device__ __forceinline__ void push_rows_fwd(const pm_selfplay& sp, const float
     const int rr = min(wv * 32 + (lane & 31), 2 * np - 1);
     const bool nxt = rr >= np;
     const int k = nxt ? rr - np : rr;
+    // selects, not pre[w]: a dynamically indexed array is a scratch store + load round trip
     const int w = k >= pre[3] ? 3 : k >= pre[2] ? 2 : k >= pre[1] ? 1 : 0;
-    const int j = plist[w * 64 + k - pre[w]];
+    const int pw = k >= pre[3] ? pre[3] : k >= pre[2] ? pre[2] : k >= pre[1] ? pre[1] : 0;
+    const int j = plist[w * 64 + k - pw];
     f32x16 c2[2];
     float qb[3], qt[3], rb[2];
     batch_row_fwd(sp, lw, hf, hf + 264, sidx[j], nxt, lane, c2, qb, qt, rb);
@@ -1010,7 +1123,9 @@ struct LearnSmem {
         float gpart[16][256];  // gradient phase: per-wave partial sums
     } u;
     __attribute__((aligned(16))) float Hs[PM_MAX_BATCH][64];  // ReLU(features(s)) of the batch (LDS DMA rows)
-    float qv[PM_MAX_BATCH][12];  // Q_B(s) 0..2 | Q_B(s') 4..6 | Q_T(s') 8..10
+    // hfeat row floats 64..75 of each sample as three float4 planes (LDS DMA: lane t's 16 B at
+    // base + 16 t): Q_B(s) 0..2 | r 3 | Q_B(s') 4..6 | action|done bits 7 | Q_T(s') 8..10
+    __attribute__((aligned(16))) float qv4[3][PM_MAX_BATCH][4];
     float coef[PM_MAX_BATCH][4]; // dL/d(V, A0, A1, A2) per sample
     float eps_tr[pad256(260)];    // the update's noise (eps section layout)
     int64_t sidx[PM_MAX_BATCH];
@@ -1030,7 +1145,7 @@ struct LearnSmem {
 // the sum-tree refresh. Single workgroup of 1024 threads; global loads are issued up front.
 union LearnShared {
     LearnSmem learn;
-    ActShared act;
+    ActSharedLearn act;
     PushFwdSmem pf;
     TreeRefreshSmem tr;
 };
@@ -1045,7 +1160,7 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // push k_env just made, which this kernel computes; it sums the rollout's episode counters); LAST =
 // the step's last update (refreshes the sum tree for the next push, commits the step). U = 1: both.
 // Block 1 is push_fwd_block; the side-A act blocks (launches with side blocks) follow it.
-__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode, int tr) {
+__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode, int tr, int ftiles) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     if (blockIdx.x > 0) {
         if (blockIdx.x == 1) {
@@ -1057,21 +1172,27 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             return;
         }
         const int sb = (int)blockIdx.x - 2;  // side block index
+        PM_SIDE(0, sb, __builtin_amdgcn_s_memrealtime());
         const ActGrid g{sp.n, sp.n_pool + 1, chunkA, chunkP, 0};
         const int fb = sb - g.blocks();
         if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB), started at once
-            const int t0 = fb * kFeatTilesLearn;
-            feat_tiles(shm.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + kFeatTilesLearn, feat_ntiles(sp.n)), sp.featB);
+            const int t0 = fb * ftiles;
+            feat_tiles(shm.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + ftiles, feat_ntiles(sp.n)), sp.featB);
             PM_STAMP_MAX(67);
+            PM_SIDE(2, sb, __builtin_amdgcn_s_memrealtime());
+            PM_SIDE(3, sb, 1ull | ((unsigned long long)(min(t0 + ftiles, feat_ntiles(sp.n)) - t0) << 16));
             return;
         }
         // the learner's load phase is latency-bound under these blocks' staging burst; they have slack
         // (the learner is the longer of the two), so they start after its loads are in flight
         __builtin_amdgcn_s_sleep(127);
+        PM_SIDE(1, sb, __builtin_amdgcn_s_memrealtime());
         const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
         act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,
                   sb, sp.n_pool + 1 <= kListNets ? sp.opp_list : nullptr, sp.opp_cnt);
         PM_STAMP_MAX(66);
+        PM_SIDE(2, sb, __builtin_amdgcn_s_memrealtime());
+        PM_SIDE(3, sb, 0ull | ((unsigned long long)shm.act.count << 16));
         return;
     }
     LearnSmem& sm = shm.learn;
@@ -1099,12 +1220,14 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     const float eps_v = t < 260 ? sp.learn_heads[528 + t] : 0.f;
     const uint32_t tr_tag = tr ? __hip_atomic_load(tr_epoch(sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     // the rows k_env's forward blocks computed (hfeat [B][80]): sample t's Q block (floats 64..75,
-    // phase 2's operands) to registers here; its 64 features go global -> LDS below, behind them
-    float4 qh[3];
-    {
+    // phase 2's operands) global -> LDS (qv4 planes) here; its 64 features go global -> LDS below.
+    // (Round 4 loaded it to registers: the compiler kept the float4[3] in scratch, a store that
+    // waited for the load's round trip at the top of the phase.)
+    if (t < PM_MAX_BATCH) {  // wave-uniform: waves 0..3
         const float4* src = reinterpret_cast<const float4*>(sp.hfeat + (size_t)min(t, B - 1) * 80 + 64);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) qh[k] = src[k];
+        for (int k = 0; k < 3; ++k)
+            __builtin_amdgcn_global_load_lds((const void*)(src + k), (lds_void*)&sm.qv4[k][wv * 64][0], 16, 0, 0);
     }
     for (int b = t + kLearn; first && b < nbr; b += kLearn)  // n > 256 * 1024 arenas only
 #pragma unroll
@@ -1133,14 +1256,10 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         if (ip) sm.plist[wv * 64 + __popcll(m & ((1ull << lane) - 1ull))] = t;
         if (lane == 0) sm.pcnt[wv] = __popcll(m);
     }
-    if (train && t < B)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) *reinterpret_cast<float4*>(&sm.qv[t][4 * k]) = qh[k];
 #ifdef PM_DIAG
     PM_STAMP(30);
     asm volatile("" ::"v"(wraw_l), "v"((int)id_l));
     PM_STAMP(31);
-    asm volatile("" ::"v"(qh[0].x), "v"(qh[2].w));
     PM_STAMP(32);
     PM_STAMP(33);
 #endif
@@ -1203,12 +1322,13 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
                 const int j = sm.plist[w * 64 + q - pre[w]];
                 const float v = __hip_atomic_load(pay + (size_t)j * 80 + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (f < 64) sm.Hs[j][f] = v;
-                else sm.qv[j][f - 64] = v;
+                else sm.qv4[(f - 64) >> 2][j][f & 3] = v;
             }
         }
     }
     float wmax = sm.red[0][0];
     for (int w = 1; w < 16; ++w) wmax = fmaxf(wmax, sm.red[w][0]);
+    if (t < PM_MAX_BATCH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the qv4 DMA (waves 0..3)
     __syncthreads();
     PM_STAMP(2);
     if (sm.void_upd) train = act = false;  // block-uniform: the hand-off timed out
@@ -1221,12 +1341,15 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     float cf[4] = {0.f, 0.f, 0.f, 0.f};
     int slot = 0;
     if (act) {
-        const float rwd = sm.qv[t][3];
-        const int bits = __float_as_int(sm.qv[t][7]);
+        const float4 v0 = *reinterpret_cast<const float4*>(sm.qv4[0][t]);
+        const float4 v1 = *reinterpret_cast<const float4*>(sm.qv4[1][t]);
+        const float4 v2 = *reinterpret_cast<const float4*>(sm.qv4[2][t]);
+        const float rwd = v0.w;
+        const int bits = __float_as_int(v1.w);
         const int a = bits & 0xff, dn = (bits >> 8) & 1;
-        const float qs[3] = {sm.qv[t][0], sm.qv[t][1], sm.qv[t][2]};
-        const float qn[3] = {sm.qv[t][4], sm.qv[t][5], sm.qv[t][6]};
-        const float qt[3] = {sm.qv[t][8], sm.qv[t][9], sm.qv[t][10]};
+        const float qs[3] = {v0.x, v0.y, v0.z};
+        const float qn[3] = {v1.x, v1.y, v1.z};
+        const float qt[3] = {v2.x, v2.y, v2.z};
         const float q = qs[a];                                            // modelB(s).gather(a)   (:152)
         const float nq = qt[argmax3(qn)];                                 // targetB(ns)[argmax modelB(ns)]
         const float tgt = rwd + (float)sp.gamma * nq * (dn ? 0.f : 1.f);  // r + gamma*nq*(~d)     (:156)
@@ -2171,8 +2294,55 @@ bool multi_ok(const pm_selfplay* sp) {
            (sp->cap + PER_CHUNK - 1) / PER_CHUNK <= kMultiChunks && ((uintptr_t)sp->frow & 15) == 0;
 }
 
-ActGrid learn_act_grid(const pm_selfplay* sp) {
-    return ActGrid{sp->n, sp->n_pool + 1, std::min(4 * sp->chunk_A, kListMax), std::min(4 * sp->chunk_P, kListMax), 0};
+// k_learn's side blocks (launches with the next step's side-A act): one CU each (the launch's LDS), so
+// they run in ONE round beside the learner only if they fit the CUs the learner and block 1 leave, and
+// they end together only if their work is even. PONGMI_SIDE=1 (default) sizes them from the opponent
+// draw's expected rows: each net's chunk (a multiple of 256 arenas, so the act reads the env kernel's
+// lists) is expected to hold kSideRows rows (~15 full 32-row tiles for 16 waves), and the feature
+// tiles are spread over the CUs left (>= 16 per block). At configs[2] (pool 8, ratio 0.33): 86 modelA
+// blocks (768 arenas, ~515 rows), 48 pool blocks (11 776 arenas, ~486 rows), 114 feature blocks of 18
+// tiles: 250 blocks. PONGMI_SIDE=0: the round-4 grid (4x the act kernel's chunks up to 4 096 arenas,
+// 16 feature tiles: 64 + 128 + 128 side blocks, two rounds; measured r5m: modelA blocks of ~705 rows
+// end 22 us after the learner starts, the second round's feature blocks 23.8 us, the learner ~19 us).
+struct LearnGrid {
+    ActGrid g;
+    int ftiles;
+};
+constexpr int kSideRows = 480;
+int side_mode() {
+    static const int v = [] {
+        const char* e = getenv("PONGMI_SIDE");
+        return e && *e ? atoi(e) : 1;
+    }();
+    return v;
+}
+int device_cus() {
+    static const int v = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return cus;
+    }();
+    return v;
+}
+int side_chunk(double p) {
+    if (!(p > 0.0)) return kListMaxLearn;
+    const double c = std::ceil(kSideRows / p / 256.0) * 256.0;
+    return c >= kListMaxLearn ? kListMaxLearn : (c < 256.0 ? 256 : (int)c);
+}
+LearnGrid learn_grid(const pm_selfplay* sp) {
+    const int ntiles = feat_ntiles(sp->n);
+    if (side_mode() == 0)
+        return LearnGrid{ActGrid{sp->n, sp->n_pool + 1, std::min(4 * sp->chunk_A, kListMax),
+                                 std::min(4 * sp->chunk_P, kListMax), 0},
+                         kFeatTilesLearn};
+    const double pp = sp->n_pool > 0 ? sp->pool_ratio : 0.0;
+    const ActGrid g{sp->n, sp->n_pool + 1, side_chunk(1.0 - pp), side_chunk(sp->n_pool > 0 ? pp / sp->n_pool : 0.0), 0};
+    const int left = device_cus() - 2 - g.blocks();
+    int ft = left > 0 ? (ntiles + left - 1) / left : ntiles;
+    ft = std::max(ft, kFeatTilesLearn);
+    return LearnGrid{g, std::min(ft, std::max(ntiles, 1))};
 }
 
 // The sum-tree refresh in block 1 (tree_block) unless PONGMI_TR=0 (the learner's own refresh, A/B).
@@ -2185,11 +2355,12 @@ int tree_refresh_block() {
 }
 
 int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st, int mode = PM_UPD_FIRST | PM_UPD_LAST) {
-    const ActGrid g = learn_act_grid(sp);
+    const LearnGrid lg = learn_grid(sp);
+    const ActGrid& g = lg.g;
     unsigned blocks = 2u + (with_act ? (unsigned)g.blocks() : 0u);  // learner, push-row block, side blocks
-    if (with_act && sp->featB) blocks += (unsigned)((feat_ntiles(sp->n) + kFeatTilesLearn - 1) / kFeatTilesLearn);
+    if (with_act && sp->featB) blocks += (unsigned)((feat_ntiles(sp->n) + lg.ftiles - 1) / lg.ftiles);
     pm_launch(PM_TIMER_LEARN, k_learn, dim3(blocks), dim3(kLearn), st, *sp, g.chunk0, g.chunk1, mode,
-              tree_refresh_block());
+              tree_refresh_block(), lg.ftiles);
     PM_LAUNCHED("k_learn");
     return PM_OK;
 }
@@ -2219,8 +2390,16 @@ extern "C" int pm_selfplay_env(const pm_selfplay* sp, void* stream) {
 extern "C" int pm_selfplay_actenv(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
-    const unsigned nsb = (unsigned)((sp->batch + PER_BS - 1) / PER_BS);
-    pm_launch(PM_TIMER_ACTENV, k_actenv, dim3(nsb + pm_blocks(sp->n, kBlock)), dim3(kBlock), pm_stream(stream), *sp);
+    // PONGMI_SFB: samples per sampler block, 32 (split forward, default) or 64 (round-4 blocks)
+    static const int sfb = [] {
+        const char* e = getenv("PONGMI_SFB");
+        return e && atoi(e) == 64 ? 64 : 32;
+    }();
+    const unsigned nsb = (unsigned)((sp->batch + sfb - 1) / sfb);
+    if (sfb == 64)
+        pm_launch(PM_TIMER_ACTENV, k_actenv<64>, dim3(nsb + pm_blocks(sp->n, kBlock)), dim3(kBlock), pm_stream(stream), *sp);
+    else
+        pm_launch(PM_TIMER_ACTENV, k_actenv<32>, dim3(nsb + pm_blocks(sp->n, kBlock)), dim3(kBlock), pm_stream(stream), *sp);
     PM_LAUNCHED("k_actenv");
     return PM_OK;
 }
@@ -2320,6 +2499,9 @@ extern "C" int pm_selfplay_step_overlap(const pm_selfplay* sp, void* stream) {
 }
 
 #ifdef PM_DIAG
+extern "C" int pm_diag_read_side(uint64_t* out) {  // [4][1024]: k_learn side blocks (begin, after sleep, end, role | rows)
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_side), sizeof(uint64_t) * 4 * 1024);
+}
 extern "C" int pm_diag_read(uint64_t* out, int32_t n) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_buf), sizeof(uint64_t) * (n < 256 ? n : 256));
     return e == hipSuccess ? 0 : (int)e;

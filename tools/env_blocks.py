@@ -39,7 +39,8 @@ def main():
     nb = (n + 255) // 256
     buf = (ctypes.c_uint64 * (8 * 1024))()
     blk = (ctypes.c_uint64 * (8 * 4096))()
-    nsb = (256 + 63) // 64  # sampler blocks of the fused kernel (k_actenv, PER_BS = 64)
+    sfb = 64 if os.environ.get("PONGMI_SFB") == "64" else 32  # samples per k_actenv sampler block
+    nsb = (256 + sfb - 1) // sfb
     acc, samp, staged = [], [], []
     for _ in range(20):
         if L.overlap:  # the production step's launches, read right after the fused act + env kernel

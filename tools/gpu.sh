@@ -21,6 +21,9 @@
 #   pmcrnn     the same for the RNN bench (tools/pmc_rnn_passes.sh)
 #   pmcinfer   the same for the configs[1] inference rollout (2 000-step launches)
 #   drqn       tests/test_gpu_drqn.py + tools/drqn_time.py
+#   side       k_learn's side blocks (act / feature) per role, under PONGMI_SIDE 1 / 0 (diag build)
+#   roll       k_rollout16 per-step phase cycles (tools/roll_stamps.py, diag build)
+#   ab:VAR=v1,v2  tests/test_gpu_selfplay.py under each value, then the default bench interleaved twice
 #   pytest:<path>[::sel]  one test file / selection
 set -o pipefail
 export TMPDIR=/tmp
@@ -80,6 +83,25 @@ run_task() {
     drqn)
       timeout -k 10 300 $PYT tests/test_gpu_drqn.py > gpurun_out/${tag}_drqn.log 2>&1 && tail -1 gpurun_out/${tag}_drqn.log &&
       timeout -k 10 120 python3 tools/drqn_time.py > gpurun_out/${tag}_drqn_time.txt 2>&1 && cat gpurun_out/${tag}_drqn_time.txt ;;
+    ab:*)  # ab:VAR=v1,v2 — tests/test_gpu_selfplay.py under each value, then the bench interleaved twice
+      spec=${1#ab:}; var=${spec%%=*}; vals=${spec#*=}
+      for v in ${vals//,/ }; do
+        env $var=$v timeout -k 10 300 $PYT tests/test_gpu_selfplay.py > gpurun_out/${tag}_ab_${var}_$v.log 2>&1 &&
+            echo "$var=$v $(tail -1 gpurun_out/${tag}_ab_${var}_$v.log)" || return 1
+      done &&
+      for rep in 1 2; do
+        for v in ${vals//,/ }; do
+          env $var=$v timeout -k 10 200 python3 bench.py --no-cpu-baseline > gpurun_out/${tag}_ab_${var}_${v}_$rep.json 2>/dev/null &&
+              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e9,4), d['ms_per_step'])" gpurun_out/${tag}_ab_${var}_${v}_$rep.json)" || return 1
+        done
+      done ;;
+    side)  # k_learn's side-block timeline (diag build), under each PONGMI_SIDE grid
+      for v in ${SIDE_MODES:-1 0}; do
+        PONGMI_SIDE=$v timeout -k 10 180 python3 tools/side_blocks.py > gpurun_out/${tag}_side_$v.txt 2>&1 &&
+            echo "PONGMI_SIDE=$v" && grep -v amdgpu.ids gpurun_out/${tag}_side_$v.txt || return 1
+      done ;;
+    roll)  # k_rollout16 per-step phase cycles (diag build)
+      timeout -k 10 120 python3 tools/roll_stamps.py > gpurun_out/${tag}_roll_stamps.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_roll_stamps.txt ;;
     pytest:*)
       sel=${1#pytest:}
       timeout -k 10 400 $PYT "$sel" > gpurun_out/${tag}_pytest.log 2>&1 && tail -1 gpurun_out/${tag}_pytest.log ;;

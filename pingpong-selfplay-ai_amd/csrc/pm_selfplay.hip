@@ -1160,7 +1160,7 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // push k_env just made, which this kernel computes; it sums the rollout's episode counters); LAST =
 // the step's last update (refreshes the sum tree for the next push, commits the step). U = 1: both.
 // Block 1 is push_fwd_block; the side-A act blocks (launches with side blocks) follow it.
-__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode, int tr, int ftiles) {
+__global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode, int tr, int ftiles, int sleepf) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     if (blockIdx.x > 0) {
         if (blockIdx.x == 1) {
@@ -1175,7 +1175,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         PM_SIDE(0, sb, __builtin_amdgcn_s_memrealtime());
         const ActGrid g{sp.n, sp.n_pool + 1, chunkA, chunkP, 0};
         const int fb = sb - g.blocks();
-        if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB), started at once
+        if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB)
+            if (sleepf & 2) __builtin_amdgcn_s_sleep(127);
             const int t0 = fb * ftiles;
             feat_tiles(shm.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + ftiles, feat_ntiles(sp.n)), sp.featB);
             PM_STAMP_MAX(67);
@@ -1183,9 +1184,9 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             PM_SIDE(3, sb, 1ull | ((unsigned long long)(min(t0 + ftiles, feat_ntiles(sp.n)) - t0) << 16));
             return;
         }
-        // the learner's load phase is latency-bound under these blocks' staging burst; they have slack
-        // (the learner is the longer of the two), so they start after its loads are in flight
-        __builtin_amdgcn_s_sleep(127);
+        // the learner's load phase is latency-bound under the side blocks' staging bursts: the role
+        // with slack starts after its loads are in flight (side_sleep: the feature blocks by default)
+        if (sleepf & 1) __builtin_amdgcn_s_sleep(127);
         PM_SIDE(1, sb, __builtin_amdgcn_s_memrealtime());
         const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
         act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,
@@ -2309,6 +2310,17 @@ struct LearnGrid {
     int ftiles;
 };
 constexpr int kSideRows = 480;
+// Which side blocks start with a ~3.4 us s_sleep, so the learner's load phase is not queued behind
+// their staging bursts (PONGMI_SIDE_SLEEP: bit 0 act blocks, bit 1 feature blocks). Default 2 since
+// the one-round grid: the feature blocks have the slack (r5o, same box, two interleaved passes:
+// 2 -> 1.79 / 1.81 G env-steps/s, 0 -> 1.81 / 1.77, 1 (round 4) -> 1.76 / 1.75, 3 -> 1.75 / 1.75).
+int side_sleep() {
+    static const int v = [] {
+        const char* e = getenv("PONGMI_SIDE_SLEEP");
+        return e && *e ? atoi(e) : 2;
+    }();
+    return v;
+}
 int side_mode() {
     static const int v = [] {
         const char* e = getenv("PONGMI_SIDE");
@@ -2360,7 +2372,7 @@ int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st, int mode 
     unsigned blocks = 2u + (with_act ? (unsigned)g.blocks() : 0u);  // learner, push-row block, side blocks
     if (with_act && sp->featB) blocks += (unsigned)((feat_ntiles(sp->n) + lg.ftiles - 1) / lg.ftiles);
     pm_launch(PM_TIMER_LEARN, k_learn, dim3(blocks), dim3(kLearn), st, *sp, g.chunk0, g.chunk1, mode,
-              tree_refresh_block(), lg.ftiles);
+              tree_refresh_block(), lg.ftiles, side_sleep());
     PM_LAUNCHED("k_learn");
     return PM_OK;
 }

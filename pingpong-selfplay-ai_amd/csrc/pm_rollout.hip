@@ -357,9 +357,45 @@ struct Roll16Shared {
     __attribute__((aligned(16))) float h1s[2][4][4][16][4];   // [p][g][s >> 2][col][s & 3]: layer-2 B of instruction s
     __attribute__((aligned(16))) float c2s[2][2][8][16][4];   // [p][h][q >> 2][col][q & 3]: ReLU(layer 2), chain order
     float ob[2][16][8];                                       // [p][col]: the observations of the step
+    // the draws of step st (buffer st & 1), made by wave 1 during step st - 1's heads + tick (an idle
+    // window of that wave): the step-keyed serve (used if the arena's episode ends) and player B's
+    // epsilon branch (-1: the argmax stands, else the random action)
+    ServeDraw sdraw[2][16];
+    int epsa[2][16];
+    // MH (heads on the matrix cores): the head weights by output, opw[set][h][j][q] = weight of output
+    // j (V, A0, A1, A2) at chain position q of half h; set 0 = modelA (once), 1 + b = modelB of step
+    // buffer b (rearranged from hfB by wave 7 while it is idle)
+    __attribute__((aligned(16))) float opw[3][2][4][32];
 };
 
-template <bool PUSH>
+// Head weights (F_H order, 260 floats) -> opw[set]: output-major per half (one wave).
+__device__ __forceinline__ void roll16_opw(Roll16Shared& sm, int set, const float* hf) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int idx = it * 64 + lane, h = idx >> 7, j = (idx >> 5) & 3, q = idx & 31;
+        sm.opw[set][h][j][q] = hf[(h * 32 + q) * 4 + j];
+    }
+}
+
+// Step ctr's per-arena draws into buffer b (wave 1; lane group 0: the step-keyed serve, the same
+// StagedServe stages as the stepped path; lane group 1: player B's epsilon branch, philox64 keyed
+// as K1's act draw). Pure functions of (arena, step, seed): drawn a step ahead, bit-identical.
+__device__ __forceinline__ void roll16_draws(const pm_env_params& p, Roll16Shared& sm, int i, uint64_t ctr, int b,
+                                             double eps, uint64_t seed, int g) {
+    const int col = threadIdx.x & 15;
+    if (g == 0) {
+        StagedServe sv;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sv.stage(k, p, (uint32_t)i, ctr, seed);
+        sm.sdraw[b][col] = sv.d;
+    } else if (g == 1) {
+        const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed);
+        sm.epsa[b][col] = u53(rr.x, rr.y) < eps ? (int)below(rr.z, 3u) : -1;
+    }
+}
+
+template <bool PUSH, bool MH>
 __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_env_state& s, const float* __restrict__ wA,
                                                const float* __restrict__ wB, const float* __restrict__ ws, double eps,
                                                uint64_t seed_env, uint64_t counter0, int steps, float* __restrict__ obsA,
@@ -389,6 +425,7 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     }
     if (t < 260) sm.hfA[t] = t < 256 ? wA[PLAIN + F_H + t] : wA[PLAIN + F_BH + t - 256];
     if (wv == 7) fetch_heads(ws, 0, sm.hfB[0], lane);
+    if (wv == 1) roll16_draws(p, sm, i, counter0, 0, eps, seed_env, g);
     // ---- wave 0 keeps the 16 arenas (every lane group a copy) and ticks them
     Arena a{};
     int fin = 0, winB = 0, ptA = 0, ptB = 0, winE = 0, rsum = 0;
@@ -406,6 +443,8 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (MH && wv == 7) roll16_opw(sm, 1, sm.hfB[0]);  // its own fetch of hfB[0] has landed (same wave)
+    if (MH && wv == 6) roll16_opw(sm, 0, wA + PLAIN + F_H);  // modelA's heads straight from global
     __syncthreads();
     const float4* im2 = reinterpret_cast<const float4*>(sm.img2[player][rt][0][lane]);
 #ifdef PM_DIAG
@@ -442,7 +481,7 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
         }
         const float4 bi = *reinterpret_cast<const float4*>(sm.b2v[player][rt][g]);
         f32x4v16 c2 = {bi.x, bi.y, bi.z, bi.w};
-        StagedServe sv;
+
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
             const float4 w = im2[s4 * 64];
@@ -450,7 +489,6 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, bs[4 * s4 + 1], c2, 0, 0, 0);
             c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, bs[4 * s4 + 2], c2, 0, 0, 0);
             c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, bs[4 * s4 + 3], c2, 0, 0, 0);
-            if (wv == 0) sv.stage(s4, p, (uint32_t)i, ctr, seed_env);  // the serve draw in the chain's gaps
             __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
@@ -459,10 +497,58 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             sm.c2s[player][(u >> 2) & 1][q >> 2][col][q & 3] = relu(c2[r]);
         }
         if (wv == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next step's heads landed
+        float hw4[32];  // MH, wave 0: lane 32 pp + 16 h + 4 cg + j's A operands, the weights of output j
+        if (MH && wv == 0) {  // of player pp's half h (read before barrier B: the latency hides under it)
+            const float* src = sm.opw[(lane >> 5) ? 1 + (st & 1) : 0][(lane >> 4) & 1][lane & 3];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float4 w = *reinterpret_cast<const float4*>(src + 4 * k);
+                hw4[4 * k] = w.x; hw4[4 * k + 1] = w.y; hw4[4 * k + 2] = w.z; hw4[4 * k + 3] = w.w;
+            }
+        }
         ROLL_T(2);        // layer 2 + staging
         __syncthreads();  // (B) both players' layer 2
         ROLL_T(3);
+        int aA = 0, aB = 0;
+        if (MH && wv == 0) {
+            // heads on the matrix cores: one chain of 32 v_mfma_f32_4x4x1_16b_f32 (a k-ordered fmaf
+            // chain bit for bit, tools/mfma4_probe.hip) covers every (player, half, column): block b =
+            // lanes 4b..4b+3 = (pp, h, column group cg) multiplies the 4 outputs' weights (A: lane
+            // 4b + j supplies output j) by 4 columns' ReLU(layer 2) (B: lane 4b + j supplies column
+            // 4 cg + j), so lane 32 pp + 16 h + col ends with the four partial sums of tile_heads' half
+            // chains for its column, in the VALU path's lanes and the same fmaf order
+            const int hp = lane >> 5, hh = (lane >> 4) & 1;
+            const float* hf = hp ? sm.hfB[st & 1] : sm.hfA;
+            float xb[32];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float4 x = *reinterpret_cast<const float4*>(sm.c2s[hp][hh][k][col]);
+                xb[4 * k] = x.x; xb[4 * k + 1] = x.y; xb[4 * k + 2] = x.z; xb[4 * k + 3] = x.w;
+            }
+            f32x4v16 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 32; ++q) acc = __builtin_amdgcn_mfma_f32_4x4x1f32(hw4[q], xb[q], acc, 0, 0, 0);
+            float v = acc[0], a0 = acc[1], a1 = acc[2], a2 = acc[3];
+            v += __shfl_xor(v, 16);  // + the other half (both lanes get the same bits)
+            a0 += __shfl_xor(a0, 16);
+            a1 += __shfl_xor(a1, 16);
+            a2 += __shfl_xor(a2, 16);
+            v += hf[256];
+            a0 += hf[257];
+            a1 += hf[258];
+            a2 += hf[259];
+            const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
+            const float qv[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
+            int act = argmax3(qv);
+            if (hp) {  // random.random() < eps ? randint(0, 2) : argmax (train_iterative.py:126-130)
+                const int ea = sm.epsa[st & 1][col];
+                if (ea >= 0) act = ea;
+            }
+            aA = __shfl(act, col);
+            aB = __shfl(act, 32 + col);
+        }
         if (wv == 0) {
+          if constexpr (!MH) {
             // heads: lane 32 hp + 16 hh + col runs half hh's four chains of player hp, column col
             const int hp = lane >> 5, hh = (lane >> 4) & 1;
             const float* hf = hp ? sm.hfB[st & 1] : sm.hfA;
@@ -493,10 +579,12 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             const float q[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
             int act = argmax3(q);
             if (hp) {  // random.random() < eps ? randint(0, 2) : argmax (train_iterative.py:126-130)
-                const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed_env);
-                if (u53(rr.x, rr.y) < eps) act = (int)below(rr.z, 3u);
+                const int ea = sm.epsa[st & 1][col];
+                if (ea >= 0) act = ea;
             }
-            const int aA = __shfl(act, col), aB = __shfl(act, 32 + col);
+            aA = __shfl(act, col);
+            aB = __shfl(act, 32 + col);
+          }
             ROLL_T(4);    // heads + actions
             float sB[7];  // the step's observation of B (memory.push's s)
 #pragma unroll
@@ -529,8 +617,9 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             if (d) {  // env.reset() with K1's step-keyed production serve
                 fin += 1;
                 winB += rB > 0.f ? 1 : 0;
-                serve_finish(sv.d);
-                serve(a, sv.d.vx, sv.d.vy, sv.d.spin);
+                ServeDraw sd = sm.sdraw[st & 1][col];
+                serve_finish(sd);
+                serve(a, sd.vx, sd.vy, sd.spin);
             }
             float oA[7], oB[7];
             observe(a, oA, oB);
@@ -538,6 +627,10 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
 #pragma unroll
                 for (int k = 0; k < 7; ++k) sm.ob[g][col][k] = g ? oB[k] : oA[k];
             ROLL_T(5);    // tick (+ push) + next observations
+        } else if (wv == 1 && st + 1 < steps) {
+            roll16_draws(p, sm, i, ctr + 1, (st + 1) & 1, eps, seed_env, g);  // the next step's draws
+        } else if (MH && wv == 7 && st + 1 < steps) {
+            roll16_opw(sm, 1 + ((st + 1) & 1), sm.hfB[(st + 1) & 1]);  // the next step's heads (landed before barrier B)
         }
         __syncthreads();  // (C) the next observations
         ROLL_T(6);
@@ -570,25 +663,28 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     if (lane < NS) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane), (unsigned long long)mv);
 }
 
+template <bool MH>
 __global__ __launch_bounds__(kR16Block) void k_rollout16(const pm_env_params p, const pm_env_state s,
                                                          const float* __restrict__ wA, const float* __restrict__ wB,
                                                          const float* __restrict__ ws, double eps, uint64_t seed_env,
                                                          uint64_t counter0, int steps, float* __restrict__ obsA,
                                                          float* __restrict__ obsB, long long* __restrict__ stats,
                                                          int n) {
-    rollout16_body<false>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
+    rollout16_body<false, MH>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
 }
 // the collecting launch runs 65 536 arenas (4 096 blocks): two blocks per CU (4 waves per SIMD) need
 // <= 128 registers
+template <bool MH>
 __global__ __launch_bounds__(kR16Block) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_rollout16_push(
     const pm_env_params p, const pm_env_state s, const float* __restrict__ wA, const float* __restrict__ wB,
     const float* __restrict__ ws, double eps, uint64_t seed_env, uint64_t counter0, int steps,
     float* __restrict__ obsA, float* __restrict__ obsB, long long* __restrict__ stats, int n, const RollPush rp) {
-    rollout16_body<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
+    rollout16_body<true, MH>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
 }
 
-// 16-arena tiles: PONGMI_ROLL16 bit 0 = the inference launch, bit 1 = the collecting launch (A/B);
-// default 1. Read at every launch (one getenv), so a test can cover all four kernels in one process.
+// 16-arena tiles: PONGMI_ROLL16 bit 0 = the inference launch, bit 1 = the collecting launch (A/B),
+// bit 2 = the round-4 VALU head chains instead of the MFMA ones in the inference launch (A/B); default 1. Read at every
+// launch (one getenv), so a test can cover every kernel in one process.
 int roll16() {
     const char* e = getenv("PONGMI_ROLL16");
     return e && *e ? atoi(e) : 1;
@@ -613,10 +709,12 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
     hipLaunchKernelGGL(k_rollout_heads, dim3(steps), dim3(kHeadsBlock), 0, st, paramsB, seed_net, counter0, heads_ws);
     PM_LAUNCHED("k_rollout_heads");
     const dim3 grid(pm_blocks(n, 32)), block(kRollBlock);
-    if (rp && (roll16() & 2)) {
-        pm_launch(PM_TIMER_ROLLOUT, k_rollout16_push, dim3(pm_blocks(n, 16)), dim3(kR16Block), st, *p, *s, wA, wB,
-                  (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
-                  reinterpret_cast<long long*>(stats), n, *rp);
+    const int r16 = roll16();
+    if (rp && (r16 & 2)) {
+        // VALU heads here: the MFMA heads' operands do not fit this kernel's 128-register cap (2 blocks per CU)
+        pm_launch(PM_TIMER_ROLLOUT, k_rollout16_push<false>, dim3(pm_blocks(n, 16)),
+                  dim3(kR16Block), st, *p, *s, wA, wB, (const float*)heads_ws, (double)epsilon, seed_env, counter0,
+                  (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n, *rp);
         PM_LAUNCHED("k_rollout16_push");
         if (per_work) return per_launch_nodes(per_work, rp->cap, st);
         return PM_OK;
@@ -629,10 +727,10 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
         if (per_work) return per_launch_nodes(per_work, rp->cap, st);
         return PM_OK;
     }
-    if (roll16() & 1) {
-        pm_launch(PM_TIMER_ROLLOUT, k_rollout16, dim3(pm_blocks(n, 16)), dim3(kR16Block), st, *p, *s, wA, wB,
-                  (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
-                  reinterpret_cast<long long*>(stats), n);
+    if (r16 & 1) {
+        pm_launch(PM_TIMER_ROLLOUT, (r16 & 4) ? k_rollout16<false> : k_rollout16<true>, dim3(pm_blocks(n, 16)),
+                  dim3(kR16Block), st, *p, *s, wA, wB, (const float*)heads_ws, (double)epsilon, seed_env, counter0,
+                  (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n);
         PM_LAUNCHED("k_rollout16");
         return PM_OK;
     }

@@ -375,6 +375,24 @@ __device__ __forceinline__ void heads_half(const float* hf, const f32x16& c2, in
     }
 }
 
+// tile_heads' tail after the chains (heads_half over both layer-2 tiles): the cross-half add, the
+// biases and Q = V + (A - mean(A)).
+__device__ __forceinline__ void heads_finish(const float (&acc)[4], const float* hf, float (&q)[3]) {
+    float v = acc[0], a0 = acc[1], a1 = acc[2], a2 = acc[3];
+    v += __shfl_xor(v, 32);
+    a0 += __shfl_xor(a0, 32);
+    a1 += __shfl_xor(a1, 32);
+    a2 += __shfl_xor(a2, 32);
+    v += hf[256];
+    a0 += hf[257];
+    a1 += hf[258];
+    a2 += hf[259];
+    const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
+    q[0] = v + (a0 - mean);
+    q[1] = v + (a1 - mean);
+    q[2] = v + (a2 - mean);
+}
+
 // layer-1 B operands of this lane for observation row o: input k' = 2s + h, k' = 0 -> 1.0 (bias),
 // k' >= 1 -> o[k' - 1]
 __device__ __forceinline__ void tile_inputs(const float* __restrict__ o, int h, float (&xs)[4]) {

@@ -324,33 +324,18 @@ __device__ __forceinline__ void sample_fwd_block32(const pm_selfplay& sp, int b,
     }
     __syncthreads();  // the chains over layer-2 tile 0
     if (jt == 0) return;
-    auto finish = [&](float (&acc)[4], const float* hf, float (&q)[3]) {
-        float v = acc[0], a0 = acc[1], a1 = acc[2], a2 = acc[3];
-        v += __shfl_xor(v, 32);
-        a0 += __shfl_xor(a0, 32);
-        a1 += __shfl_xor(a1, 32);
-        a2 += __shfl_xor(a2, 32);
-        v += hf[256];
-        a0 += hf[257];
-        a1 += hf[258];
-        a2 += hf[259];
-        const float mean = ((a0 + a1) + a2) / 3.0f;  // A.mean(dim=1)
-        q[0] = v + (a0 - mean);
-        q[1] = v + (a1 - mean);
-        q[2] = v + (a2 - mean);
-    };
     {
         const float4 pa = *reinterpret_cast<const float4*>(&sm.part[nxt][lane][0]);
         ab[0] = pa.x; ab[1] = pa.y; ab[2] = pa.z; ab[3] = pa.w;
     }
     heads_half(hf0, c2, lane, 1, ab);
     float qb[3], qt[3];
-    finish(ab, hf0, qb);
+    heads_finish(ab, hf0, qb);
     if (nxt) {
         const float4 pt = *reinterpret_cast<const float4*>(&sm.part[nxt][lane][4]);
         at[0] = pt.x; at[1] = pt.y; at[2] = pt.z; at[3] = pt.w;
         heads_half(hf1, c2, lane, 1, at);
-        finish(at, hf1, qt);
+        heads_finish(at, hf1, qt);
     }
     if (mine && h == 0) {
         if (!nxt) {
@@ -834,8 +819,84 @@ struct PushFwdSmem {
     int64_t sidx[PM_MAX_BATCH];
     int plist[PM_MAX_BATCH];
     int pcnt[16];
+    float part[8][64][8];  // push_rows_fwd2: the head chains after layer-2 tile 0, per tile pair of waves
 };
-__device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, PushFwdSmem& sm) {
+
+// push_rows_fwd on block 1's 16 waves, two per 32-row tile (hidden_half / heads_half, as
+// sample_fwd_block32): wave 2k + jt computes layer-2 tile jt of tile 8 it + k (24 MFMAs deep instead
+// of 40); wave jt = 0 runs the head chains over its 32 units and hands them to wave jt = 1 through
+// LDS, which continues them in tile_heads' order. Bit-identical rows to push_rows_fwd.
+__device__ __forceinline__ void push_rows_fwd2(const pm_selfplay& sp, PushFwdSmem& sm, int wv, int lane, float* pay) {
+    int pre[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) pre[w + 1] = pre[w] + sm.pcnt[w];
+    const int np = pre[4];
+    const int ntile = (2 * np + 31) >> 5;
+    const int jt = wv & 1, h = lane >> 5;
+    const float* hf0 = sm.hf;
+    const float* hf1 = sm.hf + 264;
+    for (int it = 0; it * 8 < ntile; ++it) {  // block-uniform
+        const int tile = it * 8 + (wv >> 1);
+        const bool act = tile < ntile;  // wave-uniform
+        f32x16 c2 = {};
+        float ab[4] = {0.f, 0.f, 0.f, 0.f}, at[4] = {0.f, 0.f, 0.f, 0.f};
+        float rb0 = 0.f, rb1 = 0.f;
+        bool nxt = false, mine = false;
+        int j = 0;
+        if (act) {
+            const int r0 = tile * 32 + (lane & 31);
+            const int rr = min(r0, 2 * np - 1);
+            nxt = rr >= np;
+            const int k = nxt ? rr - np : rr;
+            const int w = k >= pre[3] ? 3 : k >= pre[2] ? 2 : k >= pre[1] ? 1 : 0;
+            const int pw = k >= pre[3] ? pre[3] : k >= pre[2] ? pre[2] : k >= pre[1] ? pre[1] : 0;
+            j = sm.plist[w * 64 + k - pw];
+            mine = r0 < 2 * np;
+            const float* tr = sp.trans + sm.sidx[j] * PM_TRANS_F;
+            float xs[4];
+            tile_inputs(tr + (nxt ? 8 : 0), h, xs);
+            rb0 = tr[7];
+            rb1 = tr[15];
+            hidden_half(sm.lw, xs, lane, jt, c2, [](int) {});
+            float* row = pay + (size_t)j * 80;
+            if (mine && !nxt) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) st_out<true>(&row[32 * jt + rho(q) + 4 * h], relu(c2[q]));
+            }
+            if (jt == 0) {
+                heads_half(hf0, c2, lane, 0, ab);
+                heads_half(hf1, c2, lane, 0, at);
+                *reinterpret_cast<float4*>(&sm.part[wv >> 1][lane][0]) = make_float4(ab[0], ab[1], ab[2], ab[3]);
+                *reinterpret_cast<float4*>(&sm.part[wv >> 1][lane][4]) = make_float4(at[0], at[1], at[2], at[3]);
+            }
+        }
+        __syncthreads();  // the chains over layer-2 tile 0
+        if (act && jt == 1) {
+            const float4 pb = *reinterpret_cast<const float4*>(&sm.part[wv >> 1][lane][0]);
+            const float4 pt = *reinterpret_cast<const float4*>(&sm.part[wv >> 1][lane][4]);
+            ab[0] = pb.x; ab[1] = pb.y; ab[2] = pb.z; ab[3] = pb.w;
+            at[0] = pt.x; at[1] = pt.y; at[2] = pt.z; at[3] = pt.w;
+            heads_half(hf0, c2, lane, 1, ab);
+            heads_half(hf1, c2, lane, 1, at);
+            float qb[3], qt[3];
+            heads_finish(ab, hf0, qb);
+            heads_finish(at, hf1, qt);
+            float* row = pay + (size_t)j * 80;
+            if (mine && h == 0) {
+                if (!nxt) {
+                    st_out<true>(&row[64], qb[0]); st_out<true>(&row[65], qb[1]); st_out<true>(&row[66], qb[2]);
+                    st_out<true>(&row[67], rb0);  // reward
+                    st_out<true>(&row[71], rb1);  // action | done << 8 (float bits)
+                } else {
+                    st_out<true>(&row[68], qb[0]); st_out<true>(&row[69], qb[1]); st_out<true>(&row[70], qb[2]);
+                    st_out<true>(&row[72], qt[0]); st_out<true>(&row[73], qt[1]); st_out<true>(&row[74], qt[2]);
+                }
+            }
+        }
+        if ((it + 1) * 8 < ntile) __syncthreads();  // block-uniform: part is reused
+    }
+}
+__device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, PushFwdSmem& sm, bool push2) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
     PM_STAMP_ANY(50);
     stage_frags_lds(sp.w_B, sm.lw, 0);
@@ -856,9 +917,12 @@ __device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, 
     __syncthreads();
     PM_STAMP_ANY(51);
     float* pay = sp.hfeat + (size_t)B * 80;
-    push_rows_fwd(sp, sm.lw, sm.hf, sm.sidx, sm.plist, sm.pcnt, wv, lane,
-                  [&](int j, bool nxt, int ln, const f32x16 (&c2)[2], const float (&qb)[3], const float (&qt)[3],
-                      const float (&rb)[2]) { store_hfeat<true>(pay, j, nxt, ln, c2, qb, qt, rb); });
+    if (push2)
+        push_rows_fwd2(sp, sm, wv, lane, pay);
+    else
+        push_rows_fwd(sp, sm.lw, sm.hf, sm.sidx, sm.plist, sm.pcnt, wv, lane,
+                      [&](int j, bool nxt, int ln, const f32x16 (&c2)[2], const float (&qb)[3], const float (&qt)[3],
+                          const float (&rb)[2]) { store_hfeat<true>(pay, j, nxt, ln, c2, qb, qt, rb); });
     PM_STAMP_ANY(52);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are complete
     __syncthreads();
@@ -1162,9 +1226,11 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // Block 1 is push_fwd_block; the side-A act blocks (launches with side blocks) follow it.
 __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode, int tr, int ftiles, int sleepf) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
+    const bool push2 = (tr & 2) != 0;  // tr: bit 0 the tree-refresh block, bit 1 push_rows_fwd2
+    tr &= 1;
     if (blockIdx.x > 0) {
         if (blockIdx.x == 1) {
-            push_fwd_block(sp, mode, shm.pf);
+            push_fwd_block(sp, mode, shm.pf, push2);
             if (tr) {
                 __syncthreads();  // the push rows' LDS is reused
                 tree_block(sp, mode, shm.tr);
@@ -1276,10 +1342,6 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
         if (lane == 0) sm.red[wv][0] = m;
     }
-#ifdef PM_DIAG
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's loads (incl. LDS DMA) landed
-    PM_STAMP_T(40, 0); PM_STAMP_T(41, 256); PM_STAMP_T(42, 512); PM_STAMP_T(43, 960);
-#endif
     // ReLU(features(s)) of the batch: each hfeat row's 64 floats global -> LDS (4 rows per wave
     // instruction), issued after every register load of this phase so nothing here waits on them; the
     // first reader is phase 3 (drained before phase 2's barrier, or before the push-row copy)
@@ -1289,6 +1351,11 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             __builtin_amdgcn_global_load_lds((const void*)(sp.hfeat + (size_t)row * 80 + 4 * (lane & 15)),
                                              (lds_void*)&sm.Hs[4 * ci][0], 16, 0, 0);
         }
+#ifdef PM_DIAG
+    // (after the feature rows' DMA is issued, as in the product build: the stamps include it landing)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's loads (incl. LDS DMA) landed
+    PM_STAMP_T(40, 0); PM_STAMP_T(41, 256); PM_STAMP_T(42, 512); PM_STAMP_T(43, 960);
+#endif
     __syncthreads();
     PM_STAMP(1);
 
@@ -1304,6 +1371,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         long long s = 0;                     // (same sum, same order as thread 0's ctot[0])
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][0];
         sm.ap.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)(float)s);
+        PM_STAMP_T(37, kLearn - 1);
     }
     if (train) {  // rows in the push range (s rows then s' rows)
         int pre[5] = {0, 0, 0, 0, 0};
@@ -1313,6 +1381,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         if (np > 0 && push_handoff(mode, train)) {  // block-uniform: block 1 computes them
             waited = true;
             if (t == 0 && !push_wait(sp, cs)) sm.void_upd = 1;
+            PM_STAMP_T(36, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the feature rows' DMA, before rows are overwritten
             __syncthreads();
             PM_STAMP(54);
@@ -2361,7 +2430,8 @@ LearnGrid learn_grid(const pm_selfplay* sp) {
 int tree_refresh_block() {
     static const int v = [] {
         const char* e = getenv("PONGMI_TR");
-        return e && *e ? (atoi(e) != 0) : 1;
+        const char* p = getenv("PONGMI_PUSH2");  // block 1's push rows on two waves per tile (default 1)
+        return (e && *e ? (atoi(e) != 0) : 1) | ((p && *p ? (atoi(p) != 0) : 1) << 1);
     }();
     return v;
 }

@@ -30,7 +30,7 @@ NAMES = {
     35: "ph0 before prologue", 34: "ph0 after prologue", 40: "ph0 w0 loads landed",
     41: "ph0 w4 loads landed", 42: "ph0 w8 loads landed", 43: "ph0 w15 loads landed",
     50: "push blk start", 51: "push blk loads", 52: "push blk fwd done", 53: "push blk stores drained",
-    54: "learn push flag seen", 55: "tree blk start", 56: "tree blk prefetch issued",
+    54: "learn push flag seen", 36: "ph1 push token polled (t0)", 37: "ph1 eps-decay pow done (t1023)", 55: "tree blk start", 56: "tree blk prefetch issued",
     57: "tree blk granules + DMA in", 58: "tree blk level 1 done", 59: "tree blk level 2 done",
     60: "tree blk winners + pval (t0)", 61: "tree blk level-1 sums (t0)", 62: "tree blk pushed subs (t0)",
     63: "tree blk chunk slots (t0)", 66: "learn launch: side-A act blocks end (max)",
@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--arenas", type=int, default=65536)
+    ap.add_argument("--plain", action="store_true", help="the plain step (k_learn without side blocks)")
     args = ap.parse_args()
     import bench
     from pongmi import _lib
@@ -53,7 +54,7 @@ def main():
     sdB, sdA = bench.synthetic_qnet(1), bench.synthetic_qnet(2)
     pool = [bench.synthetic_qnet(100 + k) for k in range(8)]
     L = SelfPlayLearner(bench.ENV_KW, args.arenas, sdB, sdA, pool, batch=256, memory_size=1_000_000,
-                        epsilon=0.08, seed=7)
+                        epsilon=0.08, seed=7, overlap=not args.plain)
     for _ in range(args.warmup):
         L.step()
     torch.cuda.synchronize()

@@ -1226,7 +1226,8 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // Block 1 is push_fwd_block; the side-A act blocks (launches with side blocks) follow it.
 __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode, int tr, int ftiles, int sleepf) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
-    const bool push2 = (tr & 2) != 0;  // tr: bit 0 the tree-refresh block, bit 1 push_rows_fwd2
+    // tr: bit 0 the tree-refresh block, bit 1 push_rows_fwd2, bit 2 the apply's noise in phase 2
+    const bool push2 = (tr & 2) != 0, late_noise = (tr & 4) != 0;
     tr &= 1;
     if (blockIdx.x > 0) {
         if (blockIdx.x == 1) {
@@ -1301,13 +1302,14 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         for (int k = 0; k < 6; ++k) part[k] += sp.partials[(size_t)b * 8 + k];
     const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
     bool train = s_after >= B;  // cleared (block-uniformly) if the push rows never arrive: a void update
+    const bool train0 = train;  // as phase 0 found it (the apply's noise counter)
     bool act = train && t < B;
     if (t == 0) sm.void_upd = 0;
     // fused: the optimizer's scalar prologue on waves with slack in this load phase (they are not
     // on the dependent idx -> replay-row path of waves 0-3): the Adam bias corrections (two fp64
     // pow) on the last thread, both NoisyNet draws of the apply on the upper half of the block
     PM_STAMP(35);
-    if (sp.fuse_apply) {
+    if (sp.fuse_apply && !late_noise) {
         if (t >= kLearn - 2) adam_const_lane(sp, cs.train_steps + 1, sm.ap, t - (kLearn - 2));
         gen_both_noises_on(sp, sm.ap, cs.step + 1, (uint64_t)(cs.train_steps + (train ? 1 : 0)) + 1, kLearn / 2);
     }
@@ -1441,6 +1443,13 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             slot = (slot + 1) & 511;
         }
         atomicMax(&sm.hwin[slot], t);
+    } else if (sp.fuse_apply && late_noise && t >= kLearn / 2) {
+        // the apply's scalar prologue on waves this phase leaves idle (late_noise; else in phase 0):
+        // Adam's bias corrections (two fp64 pow) and both NoisyNet draws, consumed from phase 4 on.
+        // (the train-step counter: `train` as phase 1 settled it, as the phase-0 draw would have it
+        // when no hand-off timed out)
+        if (t >= kLearn - 2) adam_const_lane(sp, cs.train_steps + 1, sm.ap, t - (kLearn - 2));
+        gen_both_noises_on(sp, sm.ap, cs.step + 1, (uint64_t)(cs.train_steps + (train0 ? 1 : 0)) + 1, kLearn / 2);
     }
     {
         float s = lossp, mp = prio;
@@ -2431,7 +2440,9 @@ int tree_refresh_block() {
     static const int v = [] {
         const char* e = getenv("PONGMI_TR");
         const char* p = getenv("PONGMI_PUSH2");  // block 1's push rows on two waves per tile (default 1)
-        return (e && *e ? (atoi(e) != 0) : 1) | ((p && *p ? (atoi(p) != 0) : 1) << 1);
+        const char* q = getenv("PONGMI_LATE_NOISE");  // the apply's noise / Adam constants in phase 2 (default 1)
+        return (e && *e ? (atoi(e) != 0) : 1) | ((p && *p ? (atoi(p) != 0) : 1) << 1) |
+               ((q && *q ? (atoi(q) != 0) : 1) << 2);
     }();
     return v;
 }

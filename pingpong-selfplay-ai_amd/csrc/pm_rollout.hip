@@ -271,6 +271,166 @@ __device__ __forceinline__ void rollout_body(const pm_env_params& p, const pm_en
     if (wv == 0 && lane < NS) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane), (unsigned long long)mv);
 }
 
+// rollout_body with the arena ticked once (round 5, the collecting launch's default): the four waves'
+// forwards as above, but only wave 3 keeps the fp64 arena; it ticks, pushes, and publishes both
+// players' next observations in LDS (a third barrier per step), and waves 0-1, idle during the tick,
+// draw the next step's step-keyed serves and player B's epsilon branch into LDS (pure functions of
+// arena, step and seed, as K9 does). rollout_body ticks every arena in all 8 half-waves and draws
+// every serve in all four waves: at 65 536 arenas the launch is bound by that replicated VALU work.
+// Bit-identical: the same tick, draws, forwards and head chains, in the same order.
+struct Roll1Shared {
+    RollShared r;
+    float ob[2][32][8];       // [player][column]: the step's observations
+    ServeDraw sdraw[2][32];   // [step & 1][column]
+    int epsa[2][32];          // [step & 1][column]: -1 = argmax stands, else player B's random action
+};
+__device__ __forceinline__ void roll1_draws(const pm_env_params& p, Roll1Shared& sm, int i, uint64_t ctr, int b,
+                                            double eps, uint64_t seed, int wv, int lane) {
+    const int col = lane & 31;
+    if (wv == 0 && lane < 32) {
+        StagedServe sv;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sv.stage(k, p, (uint32_t)i, ctr, seed);
+        sm.sdraw[b][col] = sv.d;
+    } else if (wv == 1 && lane < 32) {
+        const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed);
+        sm.epsa[b][col] = u53(rr.x, rr.y) < eps ? (int)below(rr.z, 3u) : -1;
+    }
+}
+template <bool PUSH>
+__device__ __forceinline__ void rollout_body1(const pm_env_params& p, const pm_env_state& s, const float* __restrict__ wA,
+                                              const float* __restrict__ wB, const float* __restrict__ ws, double eps,
+                                              uint64_t seed_env, uint64_t counter0, int steps, float* __restrict__ obsA,
+                                              float* __restrict__ obsB, long long* __restrict__ stats, int n,
+                                              const RollPush& rp) {
+    __shared__ __attribute__((aligned(16))) Roll1Shared sm;
+    const int lane = threadIdx.x & 63, col = lane & 31;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int player = wv >> 1, half = wv & 1;
+    const int i = blockIdx.x * 32 + col;
+    const bool valid = i < n;
+    stage_frags_lds(wA, sm.r.lw, blockIdx.x);
+    stage_frags_lds(wB, sm.r.lwB, blockIdx.x + kLwChunks / 2);
+    if (wv == 3) fetch_heads(ws, 0, sm.r.hf[0], lane);
+    Arena a{};
+    int fin = 0, winB = 0, ptA = 0, ptB = 0, winE = 0, rsum = 0;
+    float er = 0.f, leafv = 0.f;
+    if (wv == 3) {
+        a = load_arena(s, valid ? i : n - 1);
+        float oA[7], oB[7];
+        observe(a, oA, oB);
+        if (lane < 32)
+#pragma unroll
+            for (int k = 0; k < 7; ++k) { sm.ob[0][col][k] = oA[k]; sm.ob[1][col][k] = oB[k]; }
+        if constexpr (PUSH) {
+            er = rp.ep_reward[valid ? i : n - 1];
+            leafv = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(prio_pow(rp.prio, rp.alpha))));
+        }
+    }
+    roll1_draws(p, sm, i, counter0, 0, eps, seed_env, wv, lane);
+    const float* lw = player ? sm.r.lwB : sm.r.lw;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // both images, step 0's heads, observations and draws in LDS
+    for (int st = 0; st < steps; ++st) {
+        const uint64_t ctr = counter0 + (uint64_t)st;
+        if (wv == 3 && st + 1 < steps) fetch_heads_async(ws, st + 1, sm.r.hf[(st + 1) & 1], lane);
+        float xs[4];
+        tile_inputs(sm.ob[player][col], lane >> 5, xs);
+        f32x16 c2;
+        hidden_half(lw, xs, lane, half, c2, [](int) {});
+        const float* hf = player ? sm.r.hf[st & 1] : sm.r.lw + F_H;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        if (half == 0) {
+            heads_half(hf, c2, lane, 0, acc);
+            *reinterpret_cast<float4*>(&sm.r.part[st & 1][player][lane][0]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        }
+        __syncthreads();  // the chains over layer-2 tile 0
+        if (half == 1) {
+            const float4 pa = *reinterpret_cast<const float4*>(&sm.r.part[st & 1][player][lane][0]);
+            acc[0] = pa.x; acc[1] = pa.y; acc[2] = pa.z; acc[3] = pa.w;
+            heads_half(hf, c2, lane, 1, acc);
+            float q[3];
+            heads_finish(acc, hf, q);
+            int act = argmax3(q);
+            if (player) {  // random.random() < eps ? randint(0, 2) : argmax (train_iterative.py:126-130)
+                const int ea = sm.epsa[st & 1][col];
+                if (ea >= 0) act = ea;
+            }
+            if (lane < 32) sm.r.act[st & 1][player][col] = act;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 3: the next step's heads (and its stores)
+        __syncthreads();  // both players' actions
+        if (wv == 3) {
+            const int aA = sm.r.act[st & 1][0][col], aB = sm.r.act[st & 1][1][col];
+            float oB[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) oB[k] = sm.ob[1][col][k];  // the step's observation of B (push's s)
+            float rA, rB;
+            const int d = tick(p, a, aA, aB, rA, rB);
+            ptA += rA > 0.f ? 1 : 0;
+            ptB += rB > 0.f ? 1 : 0;
+            if constexpr (PUSH) {
+                er += rB;  // ep_reward += rB (:245)
+                if (d) {
+                    winE += er > 0.f ? 1 : 0;
+                    rsum += (int)er;
+                }
+                if (valid) {  // memory.push((oB, aB, rB, nB, done)): lanes < 32 s, lanes >= 32 s'
+                    float nA[7], nB[7];
+                    observe(a, nA, nB);  // the terminal observation, before the serve
+                    int64_t slot = rp.pos + (int64_t)st * n + i;
+                    if (slot >= rp.cap) slot -= rp.cap;
+                    float4* row = reinterpret_cast<float4*>(rp.trans + slot * PM_TRANS_F) + (lane >> 5) * 2;
+                    const bool hi = lane >= 32;
+                    st_f4<false>(row, hi ? make_float4(nB[0], nB[1], nB[2], nB[3]) : make_float4(oB[0], oB[1], oB[2], oB[3]));
+                    st_f4<false>(row + 1, hi ? make_float4(nB[4], nB[5], nB[6], __int_as_float(aB | (d << 8)))
+                                             : make_float4(oB[4], oB[5], oB[6], rB));
+                    if (!hi) rp.prios[slot] = rp.prio;
+                    else if (rp.leaf) rp.leaf[slot] = leafv;
+                }
+                if (d) er = 0.f;
+            }
+            if (d) {  // env.reset() with K1's step-keyed production serve
+                fin += 1;
+                winB += rB > 0.f ? 1 : 0;
+                ServeDraw sd = sm.sdraw[st & 1][col];
+                serve_finish(sd);  // the rare |angle| >= 135 degree redo
+                serve(a, sd.vx, sd.vy, sd.spin);
+            }
+            float oA[7], nB2[7];
+            observe(a, oA, nB2);
+            if (lane < 32)
+#pragma unroll
+                for (int k = 0; k < 7; ++k) { sm.ob[0][col][k] = oA[k]; sm.ob[1][col][k] = nB2[k]; }
+        } else if (st + 1 < steps) {
+            roll1_draws(p, sm, i, ctr + 1, (st + 1) & 1, eps, seed_env, wv, lane);  // the next step's draws
+        }
+        __syncthreads();  // (C) the next observations
+    }
+    if (wv == 3 && lane < 32 && valid) {  // wave 3 writes the arenas and their observations
+        store_arena(s, i, a);
+        float oA[7], oB[7];
+        observe(a, oA, oB);
+        store_row7(obsA + (size_t)i * 7, oA);
+        store_row7(obsB + (size_t)i * 7, oB);
+        if constexpr (PUSH) rp.ep_reward[i] = er;
+    }
+    if (!stats) return;  // block-uniform
+    constexpr int NS = PUSH ? 6 : 4;
+    const bool mine = wv == 3 && lane < 32 && valid;  // one lane per arena
+    long long v[6] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0, mine ? winE : 0,
+                      mine ? rsum : 0};
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    }
+    long long mv = v[0];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) mv = lane == k ? v[k] : mv;
+    if (wv == 3 && lane < NS) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane), (unsigned long long)mv);
+}
+
 // The inference launch keeps the compiler's own register budget (2 waves per SIMD with the MFMA
 // accumulators in AGPRs: 3.14 us per vector step at 4 096 arenas). The collecting launch runs 65 536
 // arenas, 16 blocks per CU queued: capped at 168 registers it fits 3 waves per SIMD, 19.9 against
@@ -290,6 +450,21 @@ __global__ __launch_bounds__(kRollBlock) __attribute__((amdgpu_waves_per_eu(3, 3
     const float* __restrict__ ws, double eps, uint64_t seed_env, uint64_t counter0, int steps,
     float* __restrict__ obsA, float* __restrict__ obsB, long long* __restrict__ stats, int n, const RollPush rp) {
     rollout_body<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
+}
+// the one-tick bodies (rollout_body1)
+__global__ __launch_bounds__(kRollBlock) void k_rollout1(const pm_env_params p, const pm_env_state s,
+                                                         const float* __restrict__ wA, const float* __restrict__ wB,
+                                                         const float* __restrict__ ws, double eps, uint64_t seed_env,
+                                                         uint64_t counter0, int steps, float* __restrict__ obsA,
+                                                         float* __restrict__ obsB, long long* __restrict__ stats,
+                                                         int n) {
+    rollout_body1<false>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
+}
+__global__ __launch_bounds__(kRollBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_rollout_push1(
+    const pm_env_params p, const pm_env_state s, const float* __restrict__ wA, const float* __restrict__ wB,
+    const float* __restrict__ ws, double eps, uint64_t seed_env, uint64_t counter0, int steps,
+    float* __restrict__ obsA, float* __restrict__ obsB, long long* __restrict__ stats, int n, const RollPush rp) {
+    rollout_body1<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -683,7 +858,8 @@ __global__ __launch_bounds__(kR16Block) __attribute__((amdgpu_waves_per_eu(4, 4)
 }
 
 // 16-arena tiles: PONGMI_ROLL16 bit 0 = the inference launch, bit 1 = the collecting launch (A/B),
-// bit 2 = the round-4 VALU head chains instead of the MFMA ones in the inference launch (A/B); default 1. Read at every
+// bit 2 = the round-4 VALU head chains instead of the MFMA ones in the inference launch (A/B), bit 3 =
+// the 32-arena-tile kernels with the replicated tick (rollout_body) instead of rollout_body1; default 1. Read at every
 // launch (one getenv), so a test can cover every kernel in one process.
 int roll16() {
     const char* e = getenv("PONGMI_ROLL16");
@@ -720,9 +896,9 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
         return PM_OK;
     }
     if (rp) {
-        pm_launch(PM_TIMER_ROLLOUT, k_rollout_push, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
-                  (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n,
-                  *rp);
+        pm_launch(PM_TIMER_ROLLOUT, (r16 & 8) ? k_rollout_push : k_rollout_push1, grid, block, st, *p, *s, wA, wB,
+                  (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
+                  reinterpret_cast<long long*>(stats), n, *rp);
         PM_LAUNCHED("k_rollout_push");
         if (per_work) return per_launch_nodes(per_work, rp->cap, st);
         return PM_OK;
@@ -734,8 +910,9 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
         PM_LAUNCHED("k_rollout16");
         return PM_OK;
     }
-    pm_launch(PM_TIMER_ROLLOUT, k_rollout, grid, block, st, *p, *s, wA, wB, (const float*)heads_ws,
-              (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n);
+    pm_launch(PM_TIMER_ROLLOUT, (r16 & 8) ? k_rollout : k_rollout1, grid, block, st, *p, *s, wA, wB,
+              (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
+              reinterpret_cast<long long*>(stats), n);
     PM_LAUNCHED("k_rollout");
     return PM_OK;
 }

@@ -196,13 +196,19 @@ __global__ __launch_bounds__(kAppend) void k_rsp_append(const pm_rnn_selfplay sp
         sp.seq_eps[2 * slot] = src[0];
         sp.seq_eps[2 * slot + 1] = src[1];
     }
+    // the six counter sums, one thread each (one thread summing all 96 from LDS had its loads hoisted
+    // into registers past the 128-VGPR cap: 324 B of scratch per lane)
+    __shared__ long long tots[6];
+    if (t < 6) {
+        long long v = 0;
+        for (int w = 0; w < kAppend / 64; ++w) v += wred[w][t];
+        tots[t] = v;
+    }
+    __syncthreads();
     if (t == 0) {
         long long tot[6];
-        for (int k = 0; k < 6; ++k) {
-            long long v = 0;
-            for (int w = 0; w < kAppend / 64; ++w) v += wred[w][k];
-            tot[k] = v;
-        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) tot[k] = tots[k];
         // deque(maxlen=seq_cap) keeps the newest seq_cap episodes; an episode that finished more than
         // depth / 2 steps ago also leaves (its steps are about to leave the ring): entries [0, E(s))
         // finished at or before step s, E(s) = seq_mark[s % depth] (header: ring safety)

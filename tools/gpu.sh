@@ -24,6 +24,7 @@
 #   side       k_learn's side blocks (act / feature) per role, under PONGMI_SIDE 1 / 0 (diag build)
 #   roll       k_rollout16 per-step phase cycles (tools/roll_stamps.py, diag build)
 #   ab:VAR=v1,v2  tests/test_gpu_selfplay.py under each value, then the default bench interleaved twice
+#   drqnab:VAR=v1,v2  tests/test_gpu_drqn.py under v1, then tools/drqn_time.py interleaved three times
 #   pytest:<path>[::sel]  one test file / selection
 set -o pipefail
 export TMPDIR=/tmp
@@ -99,6 +100,15 @@ run_task() {
       for v in ${SIDE_MODES:-1 0}; do
         PONGMI_SIDE=$v timeout -k 10 180 python3 tools/side_blocks.py > gpurun_out/${tag}_side_$v.txt 2>&1 &&
             echo "PONGMI_SIDE=$v" && grep -v amdgpu.ids gpurun_out/${tag}_side_$v.txt || return 1
+      done ;;
+    drqnab:*)  # drqnab:VAR=v1,v2 — tests/test_gpu_drqn.py under v1, then tools/drqn_time.py interleaved three times
+      spec=${1#drqnab:}; var=${spec%%=*}; vals=${spec#*=}; first=${vals%%,*}
+      env $var=$first timeout -k 10 300 $PYT tests/test_gpu_drqn.py > gpurun_out/${tag}_drqnab.log 2>&1 &&
+          echo "$var=$first $(tail -1 gpurun_out/${tag}_drqnab.log)" || return 1
+      for rep in 1 2 3; do
+        for v in ${vals//,/ }; do
+          env $var=$v timeout -k 10 120 python3 tools/drqn_time.py 2>/dev/null | tail -1 | sed "s/^/$var=$v /" || return 1
+        done
       done ;;
     roll)  # k_rollout16 per-step phase cycles (diag build)
       timeout -k 10 120 python3 tools/roll_stamps.py > gpurun_out/${tag}_roll_stamps.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_roll_stamps.txt ;;

@@ -72,6 +72,57 @@ static __device__ unsigned long long pm_diag_blk[8][4096];
 
 namespace pm {
 
+// ----------------------------------------------------------------------------- wave reductions
+// A wave's butterfly reduction `for (o = 32; o; o >>= 1) v = op(v, __shfl_xor(v, o))` on the DPP
+// and scalar paths instead of six ds_bpermute round trips (~2 us for six int64 chains in the learner's
+// phase 0). Bit-identical for a commutative op: after the xor-1 / xor-2 steps (quad_perm) every quad
+// holds one value, so the half-row / row mirrors pair each lane with a lane holding its xor-4 / xor-8
+// partner's value; the last two steps are (a0 + a16) + (a32 + a48) from four readlanes, which every
+// lane of the butterfly ends with too. Full waves only (every lane active). Result wave-uniform.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(dpp_i32<CTRL>(__float_as_int(v)));
+}
+template <int CTRL>
+__device__ __forceinline__ long long dpp_i64(long long v) {
+    const int lo = dpp_i32<CTRL>((int)(unsigned long long)v), hi = dpp_i32<CTRL>((int)((unsigned long long)v >> 32));
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    return __longlong_as_double(dpp_i64<CTRL>(__double_as_longlong(v)));
+}
+__device__ __forceinline__ int lane_i32(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float lane_f32(float v, int l) { return __int_as_float(lane_i32(__float_as_int(v), l)); }
+__device__ __forceinline__ long long lane_i64(long long v, int l) {
+    const unsigned lo = (unsigned)lane_i32((int)(unsigned long long)v, l);
+    const unsigned hi = (unsigned)lane_i32((int)((unsigned long long)v >> 32), l);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double lane_f64(double v, int l) { return __longlong_as_double(lane_i64(__double_as_longlong(v), l)); }
+#define PM_WAVE_RED(T, SUF, OP)                                                                   \
+    __device__ __forceinline__ T wave_##OP(T v) {                                                 \
+        v = pm_op_##OP(v, dpp_##SUF<0xB1>(v));  /* quad_perm [1,0,3,2]: xor 1 */                   \
+        v = pm_op_##OP(v, dpp_##SUF<0x4E>(v));  /* quad_perm [2,3,0,1]: xor 2 */                   \
+        v = pm_op_##OP(v, dpp_##SUF<0x141>(v)); /* row_half_mirror: = xor 4 here */                \
+        v = pm_op_##OP(v, dpp_##SUF<0x140>(v)); /* row_mirror: = xor 8 here */                     \
+        return pm_op_##OP(pm_op_##OP(lane_##SUF(v, 0), lane_##SUF(v, 16)),                        \
+                          pm_op_##OP(lane_##SUF(v, 32), lane_##SUF(v, 48)));                      \
+    }
+template <class T>
+__device__ __forceinline__ T pm_op_sum(T a, T b) { return a + b; }
+__device__ __forceinline__ float pm_op_max(float a, float b) { return fmaxf(a, b); }
+PM_WAVE_RED(long long, i64, sum)
+PM_WAVE_RED(int, i32, sum)
+PM_WAVE_RED(float, f32, sum)
+PM_WAVE_RED(double, f64, sum)
+PM_WAVE_RED(float, f32, max)
+#undef PM_WAVE_RED
+
 // ----------------------------------------------------------------------------- RNG
 enum : uint32_t { TAG_SERVE = 1, TAG_ACT = 2, TAG_OPP = 3, TAG_NOISE_ACT = 4, TAG_PER = 5, TAG_NOISE_TRAIN = 6, TAG_NOISE_RNN = 7, TAG_SEQ = 8,
                   TAG_SERVE_STEP = 9 };

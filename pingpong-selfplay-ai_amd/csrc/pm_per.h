@@ -57,12 +57,6 @@ struct PushRange {
     __device__ __forceinline__ bool covers(int64_t e) const { return dist(e) < n; }
 };
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
 __device__ __forceinline__ double wave_incl_scan(double v, int lane) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {

@@ -86,8 +86,7 @@ __global__ __launch_bounds__(1024) void k_per_normalize(float* __restrict__ w, i
     __shared__ float red[16];
     float m = 0.f;
     for (int j = threadIdx.x; j < bs; j += 1024) m = fmaxf(m, w[j]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
     float mx = red[0];

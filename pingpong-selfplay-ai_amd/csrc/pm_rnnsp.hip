@@ -92,9 +92,7 @@ __global__ __launch_bounds__(kBlock) void k_rsp_env(const pm_rnn_selfplay sp) {
         const bool win = er > 0.f;  // win_flag = episode_reward_b > 0 (:783)
         const unsigned long long mf = __ballot(fin), mA = __ballot(fin && o == 0), mwA = __ballot(fin && o == 0 && win);
         const unsigned long long mP = __ballot(fin && o != 0), mwP = __ballot(fin && o != 0 && win);
-        int rs = fin ? (int)er : 0;
-#pragma unroll
-        for (int s = 32; s > 0; s >>= 1) rs += __shfl_xor(rs, s);
+        const int rs = wave_sum(fin ? (int)er : 0);
         if (lane == 0) {
             red[wv][0] = __popcll(mf); red[wv][1] = __popcll(mA); red[wv][2] = __popcll(mwA);
             red[wv][3] = __popcll(mP); red[wv][4] = __popcll(mwP); red[wv][5] = rs;
@@ -169,9 +167,7 @@ __global__ __launch_bounds__(kAppend) void k_rsp_append(const pm_rnn_selfplay sp
     }
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-        long long v = p[k];
-#pragma unroll
-        for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
+        const long long v = wave_sum(p[k]);
         if (lane == 0) wred[wv][k] = v;
     }
     off[t + 1] = (int)p[6];  // stored episodes of env block t

@@ -261,10 +261,7 @@ __device__ __forceinline__ void rollout_body(const pm_env_params& p, const pm_en
     long long v[6] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0, mine ? winE : 0,
                       mine ? rsum : 0};
 #pragma unroll
-    for (int k = 0; k < NS; ++k) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
-    }
+    for (int k = 0; k < NS; ++k) v[k] = wave_sum(v[k]);
     long long mv = v[0];
 #pragma unroll
     for (int k = 1; k < NS; ++k) mv = lane == k ? v[k] : mv;
@@ -421,10 +418,7 @@ __device__ __forceinline__ void rollout_body1(const pm_env_params& p, const pm_e
     long long v[6] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0, mine ? winE : 0,
                       mine ? rsum : 0};
 #pragma unroll
-    for (int k = 0; k < NS; ++k) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
-    }
+    for (int k = 0; k < NS; ++k) v[k] = wave_sum(v[k]);
     long long mv = v[0];
 #pragma unroll
     for (int k = 1; k < NS; ++k) mv = lane == k ? v[k] : mv;
@@ -829,9 +823,7 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     long long v[6] = {mine ? fin : 0, mine ? winB : 0, mine ? ptA : 0, mine ? ptB : 0, mine ? winE : 0,
                       mine ? rsum : 0};
 #pragma unroll
-    for (int k = 0; k < NS; ++k)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    for (int k = 0; k < NS; ++k) v[k] = wave_sum(v[k]);
     long long mv = v[0];
 #pragma unroll
     for (int k = 1; k < NS; ++k) mv = lane == k ? v[k] : mv;

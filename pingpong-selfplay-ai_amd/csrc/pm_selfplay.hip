@@ -488,9 +488,7 @@ __device__ __forceinline__ void env_block(const pm_selfplay& sp, int blk, EnvSme
         const bool win = er > 0.f;
         const unsigned long long mf = __ballot(fin), mA = __ballot(fin && o == 0), mwA = __ballot(fin && o == 0 && win);
         const unsigned long long mP = __ballot(fin && o != 0), mwP = __ballot(fin && o != 0 && win);
-        int rs = fin ? (int)er : 0;
-#pragma unroll
-        for (int s = 32; s > 0; s >>= 1) rs += __shfl_xor(rs, s);
+        const int rs = wave_sum(fin ? (int)er : 0);
         if (lane == 0) {
             sm.red[wv][0] = __popcll(mf); sm.red[wv][1] = __popcll(mA); sm.red[wv][2] = __popcll(mwA);
             sm.red[wv][3] = __popcll(mP); sm.red[wv][4] = __popcll(mwP); sm.red[wv][5] = rs;
@@ -1325,7 +1323,8 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         if (ip) sm.plist[wv * 64 + __popcll(m & ((1ull << lane) - 1ull))] = t;
         if (lane == 0) sm.pcnt[wv] = __popcll(m);
     }
-#ifdef PM_DIAG
+    PM_STAMP(16);  // (NOWAIT build: wave 0 had idx and the control block)
+#if defined(PM_DIAG) && !defined(PM_DIAG_NOWAIT)
     PM_STAMP(30);
     asm volatile("" ::"v"(wraw_l), "v"((int)id_l));
     PM_STAMP(31);
@@ -1334,16 +1333,16 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
 #endif
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) part[k] += __shfl_xor(part[k], o);
-        if (lane == 0) sm.cnt[wv][k] = part[k];
+        const long long s = wave_sum(part[k]);
+        if (lane == 0) sm.cnt[wv][k] = s;
     }
+    PM_STAMP(17);  // (NOWAIT: the partials)
     {
-        float m = wraw;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const float m = wave_max(wraw);
         if (lane == 0) sm.red[wv][0] = m;
     }
+    PM_STAMP(18);  // (NOWAIT: isw)
+    PM_STAMP_T(19, 960);  // the last wave reaches the DMA issue
     // ReLU(features(s)) of the batch: each hfeat row's 64 floats global -> LDS (4 rows per wave
     // instruction), issued after every register load of this phase so nothing here waits on them; the
     // first reader is phase 3 (drained before phase 2's barrier, or before the push-row copy)
@@ -1353,8 +1352,9 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             __builtin_amdgcn_global_load_lds((const void*)(sp.hfeat + (size_t)row * 80 + 4 * (lane & 15)),
                                              (lds_void*)&sm.Hs[4 * ci][0], 16, 0, 0);
         }
-#ifdef PM_DIAG
-    // (after the feature rows' DMA is issued, as in the product build: the stamps include it landing)
+#if defined(PM_DIAG) && !defined(PM_DIAG_NOWAIT)
+    // (after the feature rows' DMA is issued, as in the product build: the stamps include it landing;
+    // PM_DIAG_NOWAIT drops this wait, so the timeline's later phases run as in the product build)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's loads (incl. LDS DMA) landed
     PM_STAMP_T(40, 0); PM_STAMP_T(41, 256); PM_STAMP_T(42, 512); PM_STAMP_T(43, 960);
 #endif
@@ -1452,14 +1452,9 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         gen_both_noises_on(sp, sm.ap, cs.step + 1, (uint64_t)(cs.train_steps + (train0 ? 1 : 0)) + 1, kLearn / 2);
     }
     {
-        float s = lossp, mp = prio;
+        const float s = wave_sum(lossp), mp = wave_max(prio);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            s += __shfl_xor(s, o);
-            mp = fmaxf(mp, __shfl_xor(mp, o));
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cf[k] += __shfl_xor(cf[k], o);
-        }
+        for (int k = 0; k < 4; ++k) cf[k] = wave_sum(cf[k]);
         if (lane == 0) {
             sm.red[wv][1] = s; sm.red[wv][2] = mp;
 #pragma unroll
@@ -1675,8 +1670,7 @@ __global__ __launch_bounds__(256) void k_prio_max(const pm_selfplay sp) {
         m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
     }
     if (blockIdx.x == 0 && threadIdx.x < size - 4 * n4) m = fmaxf(m, sp.prios[4 * n4 + threadIdx.x]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2115,9 +2109,7 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
     if (act) sp.isw[t] = wraw;
     const int64_t id = act ? sm.sidx[t] : 0;
     {
-        float m = wraw;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const float m = wave_max(wraw);
         if (lane == 0) sm.red[wv][0] = m;
     }
     __syncthreads();
@@ -2162,14 +2154,9 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
         gen_both_noises_on(sp, sm.ap, c_step + 1, (uint64_t)(ts + 1) + 1, kLearn / 2);  // both noises
     }
     {
-        float s = lossp, mp = prio;
+        const float s = wave_sum(lossp), mp = wave_max(prio);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            s += __shfl_xor(s, o);
-            mp = fmaxf(mp, __shfl_xor(mp, o));
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cf[k] += __shfl_xor(cf[k], o);
-        }
+        for (int k = 0; k < 4; ++k) cf[k] = wave_sum(cf[k]);
         if (lane == 0) {
             sm.red[wv][1] = s; sm.red[wv][2] = mp;
 #pragma unroll

@@ -87,13 +87,13 @@ run_task() {
     ab:*)  # ab:VAR=v1,v2 — tests/test_gpu_selfplay.py under each value, then the bench interleaved twice
       spec=${1#ab:}; var=${spec%%=*}; vals=${spec#*=}
       for v in ${vals//,/ }; do
-        env $var=$v timeout -k 10 300 $PYT tests/test_gpu_selfplay.py > gpurun_out/${tag}_ab_${var}_$v.log 2>&1 &&
-            echo "$var=$v $(tail -1 gpurun_out/${tag}_ab_${var}_$v.log)" || return 1
+        env $var=$v timeout -k 10 300 $PYT tests/test_gpu_selfplay.py > gpurun_out/${tag}_ab_${var}_${v//\//_}.log 2>&1 &&
+            echo "$var=$v $(tail -1 gpurun_out/${tag}_ab_${var}_${v//\//_}.log)" || return 1
       done &&
       for rep in 1 2; do
         for v in ${vals//,/ }; do
-          env $var=$v timeout -k 10 200 python3 bench.py --no-cpu-baseline > gpurun_out/${tag}_ab_${var}_${v}_$rep.json 2>/dev/null &&
-              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e9,4), d['ms_per_step'])" gpurun_out/${tag}_ab_${var}_${v}_$rep.json)" || return 1
+          env $var=$v timeout -k 10 200 python3 bench.py --no-cpu-baseline > gpurun_out/${tag}_ab_${var}_${v//\//_}_$rep.json 2>/dev/null &&
+              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e9,4), d['ms_per_step'])" gpurun_out/${tag}_ab_${var}_${v//\//_}_$rep.json)" || return 1
         done
       done ;;
     side)  # k_learn's side-block timeline (diag build), under each PONGMI_SIDE grid

@@ -14,7 +14,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["PONGMI_LIB"] = os.path.join(ROOT, "pingpong-selfplay-ai_amd", "pongmi", "libpongmi_diag.so")
+os.environ["PONGMI_LIB"] = os.environ.get(  # PONGMI_DIAG_LIB: another diagnostic build (e.g. -DPM_DIAG_NOWAIT)
+    "PONGMI_DIAG_LIB", os.path.join(ROOT, "pingpong-selfplay-ai_amd", "pongmi", "libpongmi_diag.so"))
 sys.path.insert(0, os.path.join(ROOT, "pingpong-selfplay-ai_amd"))
 sys.path.insert(0, ROOT)
 
@@ -30,6 +31,7 @@ NAMES = {
     35: "ph0 before prologue", 34: "ph0 after prologue", 40: "ph0 w0 loads landed",
     41: "ph0 w4 loads landed", 42: "ph0 w8 loads landed", 43: "ph0 w15 loads landed",
     50: "push blk start", 51: "push blk loads", 52: "push blk fwd done", 53: "push blk stores drained",
+    16: "ph0 w0: idx + ctrl in", 17: "ph0 w0: partials in", 18: "ph0 w0: isw in", 19: "ph0 w15 at DMA issue",
     54: "learn push flag seen", 36: "ph1 push token polled (t0)", 37: "ph1 eps-decay pow done (t1023)", 55: "tree blk start", 56: "tree blk prefetch issued",
     57: "tree blk granules + DMA in", 58: "tree blk level 1 done", 59: "tree blk level 2 done",
     60: "tree blk winners + pval (t0)", 61: "tree blk level-1 sums (t0)", 62: "tree blk pushed subs (t0)",

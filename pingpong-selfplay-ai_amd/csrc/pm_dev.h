@@ -122,6 +122,18 @@ PM_WAVE_RED(float, f32, sum)
 PM_WAVE_RED(double, f64, sum)
 PM_WAVE_RED(float, f32, max)
 #undef PM_WAVE_RED
+// Inclusive prefix sum of a full wave on DPP: Hillis-Steele within each 16-lane row (row_shr 1/2/4/8,
+// lanes shifted in from outside the row read 0), then the row carries (row_bcast:15 into rows 1 and 3,
+// row_bcast:31 into rows 2 and 3). Integers only (the association differs from a lane-serial scan).
+__device__ __forceinline__ int wave_incl_scan_i32(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
 
 // ----------------------------------------------------------------------------- RNG
 enum : uint32_t { TAG_SERVE = 1, TAG_ACT = 2, TAG_OPP = 3, TAG_NOISE_ACT = 4, TAG_PER = 5, TAG_NOISE_TRAIN = 6, TAG_NOISE_RNN = 7, TAG_SEQ = 8,

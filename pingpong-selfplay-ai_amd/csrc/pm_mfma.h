@@ -155,12 +155,7 @@ __device__ __forceinline__ void write_opp_lists(int nn, int32_t* opp_list, int32
                 acc += c;
             }
         }
-        int inc = acc;  // inclusive scan of the net counts across the wave (nn <= 64)
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(inc, d);
-            if (lane >= d) inc += v;
-        }
+        const int inc = wave_incl_scan_i32(acc);  // inclusive scan of the net counts across the wave (nn <= 64)
         if (lane < nn) { sm.ncnt[lane] = acc; sm.noff[lane] = inc - acc; }
     }
     __syncthreads();
@@ -194,12 +189,7 @@ __device__ __forceinline__ void compact_scan(const int (&v)[16], int net, int lo
 #pragma unroll
     for (int r = 0; r < 16; ++r) mask |= (v[r] == net ? 1u : 0u) << r;
     const int c = __popc(mask);
-    int incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(incl, o);
-        if (lane >= o) incl += u;
-    }
+    const int incl = wave_incl_scan_i32(c);
     if (lane == 63) wtot[wv] = incl;
     __syncthreads();
     int off = 0, total = 0;
@@ -546,12 +536,7 @@ __device__ __forceinline__ void act_block(Sh& sh, const ActGrid& g, const float*
             const int lane = threadIdx.x;
             const int v = lane < G ? opp_cnt[(size_t)(g0 + lane) * g.n_opp + net] : 0;
             const int c = v & 0xFFFF;
-            int incl = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int u = __shfl_up(incl, o);
-                if (lane >= o) incl += u;
-            }
+            const int incl = wave_incl_scan_i32(c);
             if (lane < G) { sh.lpre[lane] = incl - c; sh.loff[lane] = v >> 16; sh.lcnt[lane] = c; }
             if (lane == 63) sh.count = incl;
         }

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 21
+#define PM_ABI_VERSION 22
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -484,11 +484,13 @@ typedef struct pm_selfplay {
     int64_t *partials;       /* [ceil(n/256)][8] per-block episode counters of the rollout          */
     float *obsA, *obsB;      /* [n][7] observations of the current step (written by the env kernel) */
     int8_t *aA, *aB;         /* [n] actions of the current step (written by the act kernel)        */
-    float *hfeat;            /* [2 * batch + 8][80], zero-filled before the first step: batch forward
+    float *hfeat;            /* [4 * batch + 8][80], zero-filled before the first step: batch forward
                                 scratch: rows [0, batch) features of s, Q values at 64.. (stable rows);
                                 rows [batch, 2 batch) the push rows k_learn's block 1 hands to the
                                 learner; row 2 batch word 0 its flag, word 1 the tree-refresh epoch;
-                                rows 2 batch + 1 .. the learner -> tree-refresh granules (ABI 21) */
+                                rows 2 batch + 1 .. the learner -> tree-refresh granules (ABI 21);
+                                rows [2 batch + 8, 4 batch + 8) the push rows as tagged 8-byte
+                                granules, [batch][76] (ABI 22) */
     float *learn_heads;      /* [3][264] next update's modelB heads (fresh noise) and targetB heads in
                                 MFMA fragment order, and that noise (epsilon-buffer layout)        */
     pm_ctrl *ctrl;

@@ -796,6 +796,27 @@ __device__ __forceinline__ int* push_flag(const pm_selfplay& sp) {
     return reinterpret_cast<int*>(sp.hfeat + (size_t)2 * sp.batch * 80);
 }
 __device__ __forceinline__ int push_token(const pm_ctrl& cs) { return (int)((uint32_t)cs.step + 1u); }
+// the tree-refresh epoch (tree_block): word 1 of the flag row
+__device__ __forceinline__ uint32_t* tr_epoch(const pm_selfplay& sp) {
+    return reinterpret_cast<uint32_t*>(sp.hfeat + (size_t)2 * sp.batch * 80) + 1;
+}
+// The push rows as tagged 8-byte granules {tag, float bits} (round 5; tr bit 3, PONGMI_PUSHG): sample
+// j's hfeat floats 0..74 at granule j * 76 + f of hfeat rows [2B + 8, 4B + 8) (ABI 22). The data is
+// the flag: block 1 stores each granule once (sc1), with no drain, and the learner's loads of them are
+// the poll, which saves the payload drain, the flag store's trip and the flag poll's (~2 us; MI355X
+// guide: handoff-1to1 vs handoff-flag). The tag is this launch's tree-refresh epoch + 1 (tr_epoch:
+// bumped by block 1 at the end of every launch with the tree block, so never reused by a later
+// launch, checkpoint restores included). The flag word is still stored, right after block 1 read the
+// control block: a learner that needed no rows waits for it before its commit; one that
+// saw a granule of this launch's tag knows block 1 read this step's control block.
+constexpr int kPushGF = 76;  // granule stride per sample (floats 0..74 used)
+constexpr int kPushGN = 75;
+__device__ __forceinline__ uint64_t* push_granules(const pm_selfplay& sp) {
+    return reinterpret_cast<uint64_t*>(sp.hfeat + (size_t)(2 * sp.batch + 8) * 80);
+}
+__device__ __forceinline__ void push_publish(uint64_t* g, uint32_t tag, float v) {
+    __hip_atomic_store(g, ((uint64_t)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // One lane polls for block 1's token of this update (bounded). false: it never came (status bit 0 set).
 __device__ __forceinline__ bool push_wait(const pm_selfplay& sp, const pm_ctrl& cs) {
@@ -824,7 +845,14 @@ struct PushFwdSmem {
 // sample_fwd_block32): wave 2k + jt computes layer-2 tile jt of tile 8 it + k (24 MFMAs deep instead
 // of 40); wave jt = 0 runs the head chains over its 32 units and hands them to wave jt = 1 through
 // LDS, which continues them in tile_heads' order. Bit-identical rows to push_rows_fwd.
-__device__ __forceinline__ void push_rows_fwd2(const pm_selfplay& sp, PushFwdSmem& sm, int wv, int lane, float* pay) {
+__device__ __forceinline__ void push_rows_fwd2(const pm_selfplay& sp, PushFwdSmem& sm, int wv, int lane, float* pay,
+                                               uint32_t gtag) {
+    uint64_t* pg = push_granules(sp);
+    // hfeat float f of sample j: a payload-row word (drained + flag) or a tagged granule
+    auto put = [&](int j, int f, float v) {
+        if (gtag) push_publish(pg + (size_t)j * kPushGF + f, gtag, v);
+        else st_out<true>(pay + (size_t)j * 80 + f, v);
+    };
     int pre[5] = {0, 0, 0, 0, 0};
 #pragma unroll
     for (int w = 0; w < 4; ++w) pre[w + 1] = pre[w] + sm.pcnt[w];
@@ -856,10 +884,9 @@ __device__ __forceinline__ void push_rows_fwd2(const pm_selfplay& sp, PushFwdSme
             rb0 = tr[7];
             rb1 = tr[15];
             hidden_half(sm.lw, xs, lane, jt, c2, [](int) {});
-            float* row = pay + (size_t)j * 80;
             if (mine && !nxt) {
 #pragma unroll
-                for (int q = 0; q < 16; ++q) st_out<true>(&row[32 * jt + rho(q) + 4 * h], relu(c2[q]));
+                for (int q = 0; q < 16; ++q) put(j, 32 * jt + rho(q) + 4 * h, relu(c2[q]));
             }
             if (jt == 0) {
                 heads_half(hf0, c2, lane, 0, ab);
@@ -879,27 +906,27 @@ __device__ __forceinline__ void push_rows_fwd2(const pm_selfplay& sp, PushFwdSme
             float qb[3], qt[3];
             heads_finish(ab, hf0, qb);
             heads_finish(at, hf1, qt);
-            float* row = pay + (size_t)j * 80;
             if (mine && h == 0) {
                 if (!nxt) {
-                    st_out<true>(&row[64], qb[0]); st_out<true>(&row[65], qb[1]); st_out<true>(&row[66], qb[2]);
-                    st_out<true>(&row[67], rb0);  // reward
-                    st_out<true>(&row[71], rb1);  // action | done << 8 (float bits)
+                    put(j, 64, qb[0]); put(j, 65, qb[1]); put(j, 66, qb[2]);
+                    put(j, 67, rb0);  // reward
+                    put(j, 71, rb1);  // action | done << 8 (float bits)
                 } else {
-                    st_out<true>(&row[68], qb[0]); st_out<true>(&row[69], qb[1]); st_out<true>(&row[70], qb[2]);
-                    st_out<true>(&row[72], qt[0]); st_out<true>(&row[73], qt[1]); st_out<true>(&row[74], qt[2]);
+                    put(j, 68, qb[0]); put(j, 69, qb[1]); put(j, 70, qb[2]);
+                    put(j, 72, qt[0]); put(j, 73, qt[1]); put(j, 74, qt[2]);
                 }
             }
         }
         if ((it + 1) * 8 < ntile) __syncthreads();  // block-uniform: part is reused
     }
 }
-__device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, PushFwdSmem& sm, bool push2) {
+__device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, PushFwdSmem& sm, bool push2, bool pushg) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
     PM_STAMP_ANY(50);
     stage_frags_lds(sp.w_B, sm.lw, 0);
     copy_lds_f32x4<2 * 264>(sp.learn_heads, sm.hf);
     const int64_t id = t < B ? sp.idx[t] : 0;
+    const uint32_t gtag = pushg ? __hip_atomic_load(tr_epoch(sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     __builtin_amdgcn_sched_barrier(0);
     const pm_ctrl cs = *sp.ctrl;
     const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
@@ -907,6 +934,7 @@ __device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, 
         if ((mode & PM_UPD_FIRST) && t == 0) st_out<true>(push_flag(sp), push_token(cs));
         return;
     }
+    if (pushg && t == 0) st_out<true>(push_flag(sp), push_token(cs));  // block 1 read the control block
     const bool ip = t < B && push_of(sp, cs.pos, cs.size, cs.max_prio).covers(id);
     const unsigned long long m = __ballot(ip);
     if (ip) sm.plist[wv * 64 + __popcll(m & ((1ull << lane) - 1ull))] = t;
@@ -916,12 +944,13 @@ __device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, 
     PM_STAMP_ANY(51);
     float* pay = sp.hfeat + (size_t)B * 80;
     if (push2)
-        push_rows_fwd2(sp, sm, wv, lane, pay);
+        push_rows_fwd2(sp, sm, wv, lane, pay, gtag);
     else
         push_rows_fwd(sp, sm.lw, sm.hf, sm.sidx, sm.plist, sm.pcnt, wv, lane,
                       [&](int j, bool nxt, int ln, const f32x16 (&c2)[2], const float (&qb)[3], const float (&qt)[3],
                           const float (&rb)[2]) { store_hfeat<true>(pay, j, nxt, ln, c2, qb, qt, rb); });
     PM_STAMP_ANY(52);
+    if (pushg) return;  // block-uniform: the granules need no drain, the flag is out
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are complete
     __syncthreads();
     PM_STAMP_ANY(53);
@@ -976,9 +1005,6 @@ struct TreeRefreshSmem {
 };
 __device__ __forceinline__ uint64_t* tr_granules(const pm_selfplay& sp) {
     return reinterpret_cast<uint64_t*>(sp.hfeat + (size_t)(2 * sp.batch + 1) * 80);
-}
-__device__ __forceinline__ uint32_t* tr_epoch(const pm_selfplay& sp) {
-    return reinterpret_cast<uint32_t*>(sp.hfeat + (size_t)2 * sp.batch * 80) + 1;
 }
 __device__ __forceinline__ void tr_publish(const pm_selfplay& sp, int k, uint32_t v, uint32_t tag) {
     __hip_atomic_store(tr_granules(sp) + k, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1222,14 +1248,18 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // push k_env just made, which this kernel computes; it sums the rollout's episode counters); LAST =
 // the step's last update (refreshes the sum tree for the next push, commits the step). U = 1: both.
 // Block 1 is push_fwd_block; the side-A act blocks (launches with side blocks) follow it.
+// PG: the push rows as tagged granules (tr bit 3; a separate instantiation: the flag consumer's
+// branch beside the granule sweep made the compiler wait for every granule load in turn).
+template <bool PG>
 __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chunkA, int chunkP, int mode, int tr, int ftiles, int sleepf) {
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     // tr: bit 0 the tree-refresh block, bit 1 push_rows_fwd2, bit 2 the apply's noise in phase 2
     const bool push2 = (tr & 2) != 0, late_noise = (tr & 4) != 0;
+    constexpr bool pushg = PG;
     tr &= 1;
     if (blockIdx.x > 0) {
         if (blockIdx.x == 1) {
-            push_fwd_block(sp, mode, shm.pf, push2);
+            push_fwd_block(sp, mode, shm.pf, push2, pushg);
             if (tr) {
                 __syncthreads();  // the push rows' LDS is reused
                 tree_block(sp, mode, shm.tr);
@@ -1369,7 +1399,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][t];
         sm.ctot[t] = s;  // read after the next barrier
     }
-    if (sp.fuse_apply && first && t == kLearn - 1) {  // the per-episode epsilon decay (:261) beside the forward
+    if (sp.fuse_apply && first && !late_noise && t == kLearn - 1) {  // the per-episode epsilon decay (:261) beside the forward
         long long s = 0;                     // (same sum, same order as thread 0's ctot[0])
         for (int w = 0; w < 16; ++w) s += sm.cnt[w][0];
         sm.ap.eps_next = cs.epsilon * pow(sp.epsilon_decay, (double)(float)s);
@@ -1382,6 +1412,59 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         const int np = pre[4];
         if (np > 0 && push_handoff(mode, train)) {  // block-uniform: block 1 computes them
             waited = true;
+            if constexpr (PG) {  // the granules: up to 4 per thread in flight, re-polled until their tags match
+                const uint64_t* pg = push_granules(sp);
+                const int tot = np * kPushGN;
+                uint64_t g[4];
+                int jf[4];
+                auto issue = [&](int k0) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int k = k0 + u * kLearn;
+                        g[u] = (uint64_t)tr_tag << 32;  // past the end: no load (reads as arrived)
+                        jf[u] = 0;
+                        if (k < tot) {
+                            const int q = k / kPushGN, f = k - q * kPushGN;
+                            const int w = q >= pre[3] ? 3 : q >= pre[2] ? 2 : q >= pre[1] ? 1 : 0;
+                            const int pw = q >= pre[3] ? pre[3] : q >= pre[2] ? pre[2] : q >= pre[1] ? pre[1] : 0;
+                            jf[u] = sm.plist[w * 64 + q - pw] * kPushGF + f;
+                            g[u] = __hip_atomic_load(pg + jf[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                };
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the feature rows' DMA, before rows are overwritten
+                issue(t);  // the first round trip rides under the barrier
+                __syncthreads();
+                PM_STAMP(54);
+                for (int k0 = t; k0 < tot; k0 += 4 * kLearn) {
+                    if (k0 != t) issue(k0);
+                    for (int it = 0;; ++it) {
+                        bool done = true;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) done &= (uint32_t)(g[u] >> 32) == tr_tag;
+                        if (done) break;
+                        if (it == kPushPollMax) {  // never came: this update trains nothing (status bit 0)
+                            sm.void_upd = 1;
+                            sp.ctrl->status = cs.status | PM_CTRL_PUSH_TIMEOUT;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if ((uint32_t)(g[u] >> 32) != tr_tag)
+                                g[u] = __hip_atomic_load(pg + jf[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (k0 + u * kLearn >= tot) break;
+                        const int j = jf[u] / kPushGF, f = jf[u] - j * kPushGF;
+                        const float v = __uint_as_float((uint32_t)g[u]);
+                        if (f < 64) sm.Hs[j][f] = v;
+                        else sm.qv4[(f - 64) >> 2][j][f & 3] = v;
+                    }
+                }
+                PM_STAMP_T(36, 0);
+            } else {
             if (t == 0 && !push_wait(sp, cs)) sm.void_upd = 1;
             PM_STAMP_T(36, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the feature rows' DMA, before rows are overwritten
@@ -1395,6 +1478,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
                 const float v = __hip_atomic_load(pay + (size_t)j * 80 + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (f < 64) sm.Hs[j][f] = v;
                 else sm.qv4[(f - 64) >> 2][j][f & 3] = v;
+            }
             }
         }
     }
@@ -1448,7 +1532,22 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         // Adam's bias corrections (two fp64 pow) and both NoisyNet draws, consumed from phase 4 on.
         // (the train-step counter: `train` as phase 1 settled it, as the phase-0 draw would have it
         // when no hand-off timed out)
-        if (t >= kLearn - 2) adam_const_lane(sp, cs.train_steps + 1, sm.ap, t - (kLearn - 2));
+        // (and the per-episode epsilon decay (:261), one fp64 pow per lane in one instruction stream:
+        // lane 61 decay^D, lanes 62 / 63 the Adam corrections)
+        if (t >= kLearn - 3) {
+            const int which = t - (kLearn - 2);  // -1: the epsilon decay
+            long long s = 0;                     // (same sum, same order as thread 0's ctot[0])
+            for (int w = 0; w < 16; ++w) s += sm.cnt[w][0];
+            const double base = which < 0 ? sp.epsilon_decay : which ? sp.beta2 : sp.beta1;
+            const double ex = which < 0 ? (double)(float)s : (double)(cs.train_steps + 1);
+            const double p = pow(base, ex);
+            if (which < 0) {
+                if (first) sm.ap.eps_next = cs.epsilon * p;
+            } else {
+                const double bc = 1.0 - p;
+                sm.ap.ak[which] = which ? (float)sqrt(bc) : (float)(sp.lr / bc);
+            }
+        }
         gen_both_noises_on(sp, sm.ap, cs.step + 1, (uint64_t)(cs.train_steps + (train0 ? 1 : 0)) + 1, kLearn / 2);
     }
     {
@@ -2436,8 +2535,10 @@ int tree_refresh_block() {
         const char* e = getenv("PONGMI_TR");
         const char* p = getenv("PONGMI_PUSH2");  // block 1's push rows on two waves per tile (default 1)
         const char* q = getenv("PONGMI_LATE_NOISE");  // the apply's noise / Adam constants in phase 2 (default 1)
-        return (e && *e ? (atoi(e) != 0) : 1) | ((p && *p ? (atoi(p) != 0) : 1) << 1) |
-               ((q && *q ? (atoi(q) != 0) : 1) << 2);
+        const char* g = getenv("PONGMI_PUSHG");  // push rows as tagged granules (default 1; needs TR and PUSH2)
+        const int tr = e && *e ? (atoi(e) != 0) : 1, p2 = p && *p ? (atoi(p) != 0) : 1;
+        const int pg = (g && *g ? (atoi(g) != 0) : 1) && tr && p2;
+        return tr | (p2 << 1) | ((q && *q ? (atoi(q) != 0) : 1) << 2) | (pg << 3);
     }();
     return v;
 }
@@ -2447,8 +2548,9 @@ int launch_learn(const pm_selfplay* sp, bool with_act, hipStream_t st, int mode 
     const ActGrid& g = lg.g;
     unsigned blocks = 2u + (with_act ? (unsigned)g.blocks() : 0u);  // learner, push-row block, side blocks
     if (with_act && sp->featB) blocks += (unsigned)((feat_ntiles(sp->n) + lg.ftiles - 1) / lg.ftiles);
-    pm_launch(PM_TIMER_LEARN, k_learn, dim3(blocks), dim3(kLearn), st, *sp, g.chunk0, g.chunk1, mode,
-              tree_refresh_block(), lg.ftiles, side_sleep());
+    const int tr = tree_refresh_block();
+    pm_launch(PM_TIMER_LEARN, (tr & 8) ? k_learn<true> : k_learn<false>, dim3(blocks), dim3(kLearn), st, *sp, g.chunk0,
+              g.chunk1, mode, tr, lg.ftiles, side_sleep());
     PM_LAUNCHED("k_learn");
     return PM_OK;
 }

@@ -134,7 +134,7 @@ class SelfPlayLearner:
         self.grad = torch.zeros(PM_GRAD_LEN, **f32)  # the packed exchange buffer (include/pongmi.h PM_GRAD_*)
         self.partials = torch.zeros(((n + 255) // 256) * 8, dtype=torch.int64, device=dev)
         # + the push-row hand-off rows and flag, the tree-refresh epoch and granules (pongmi.h, ABI 21)
-        self.hfeat = torch.zeros((2 * self.batch + 8, 80), **f32)
+        self.hfeat = torch.zeros((4 * self.batch + 8, 80), **f32)
         self.learn_heads = torch.zeros(3 * 264, **f32)
         self.obsA = torch.zeros((n, 7), **f32)
         self.obsB = torch.zeros((n, 7), **f32)

@@ -11,6 +11,7 @@
 #   k1         K1 A/B: parity of the A/B variant, graph-timed floor probe (tools/k1_floor), product K1 with
 #              PONGMI_K1_PRO=1 / 0 (tools/k1_time.py, bench.time_env_step), rocprofv3 kernel traces
 #   k1stamp    per-wave K1 phase cycles (diag build, tools/k1_stamps.py)
+#   stampsnw   tools/stamps.py on the PM_DIAG_NOWAIT diag build (libpongmi_diag_nw.so)
 #   stamps     diag build: k_learn phase stamps of the overlapped step (tools/stamps.py) and k_actenv's
 #              per-block timeline (tools/env_blocks.py)
 #   bench      python bench.py (the driver's default line)
@@ -61,6 +62,10 @@ run_task() {
     stamps)
       timeout -k 10 180 python3 tools/stamps.py > gpurun_out/${tag}_stamps.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_stamps.txt &&
       timeout -k 10 180 python3 tools/env_blocks.py > gpurun_out/${tag}_env_blocks.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_env_blocks.txt ;;
+    stampsnw)  # the same k_learn stamps from the PM_DIAG_NOWAIT diag build (no vmcnt waits at the stamps;
+               # make -C pingpong-selfplay-ai_amd/csrc DIAG_OUT=../pongmi/libpongmi_diag_nw.so BUILD=_build_nw EXTRA=-DPM_DIAG_NOWAIT diag)
+      PONGMI_DIAG_LIB=$PWD/pingpong-selfplay-ai_amd/pongmi/libpongmi_diag_nw.so timeout -k 10 180 python3 tools/stamps.py \
+          > gpurun_out/${tag}_stamps_nw.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_stamps_nw.txt ;;
     bench)
       timeout -k 10 300 python3 bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err && echo BENCH_OK ;;
     rnn)

@@ -122,6 +122,21 @@ PM_WAVE_RED(float, f32, sum)
 PM_WAVE_RED(double, f64, sum)
 PM_WAVE_RED(float, f32, max)
 #undef PM_WAVE_RED
+// Quad broadcasts on DPP (quad_perm [I,I,I,I]): lane (lane & ~3) + I's value in every lane of the
+// quad, as __shfl(v, (lane & ~3) + I) without the LDS crossbar. quad_sel: the quad-uniform lane src's.
+// Full waves only.
+template <int I>
+__device__ __forceinline__ double quad_f64(double v) { return dpp_f64<I * 0x55>(v); }
+template <int I>
+__device__ __forceinline__ int quad_i32(int v) { return dpp_i32<I * 0x55>(v); }
+__device__ __forceinline__ double quad_sel_f64(double v, int src) {
+    const double a = quad_f64<0>(v), b = quad_f64<1>(v), c = quad_f64<2>(v), d = quad_f64<3>(v);
+    return src == 0 ? a : src == 1 ? b : src == 2 ? c : d;
+}
+__device__ __forceinline__ int quad_sel_i32(int v, int src) {
+    const int a = quad_i32<0>(v), b = quad_i32<1>(v), c = quad_i32<2>(v), d = quad_i32<3>(v);
+    return src == 0 ? a : src == 1 ? b : src == 2 ? c : d;
+}
 // Inclusive prefix sum of a full wave on DPP: Hillis-Steele within each 16-lane row (row_shr 1/2/4/8,
 // lanes shifted in from outside the row read 0), then the row carries (row_bcast:15 into rows 1 and 3,
 // row_bcast:31 into rows 2 and 3). Integers only (the association differs from a lane-serial scan).

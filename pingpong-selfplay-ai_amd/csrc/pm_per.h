@@ -155,9 +155,9 @@ __device__ __forceinline__ double per_sub_sum(const float* __restrict__ leaf, in
 }
 // Level-1 node by 4 consecutive lanes (lane & 3 = quarter); the node lands in every lane of the group.
 __device__ __forceinline__ double per_sub_sum4(const float* __restrict__ leaf, int64_t sb, const PushRange pr) {
-    const int lane = threadIdx.x & 63, base = lane & ~3;
+    const int lane = threadIdx.x & 63;
     const double q = per_quarter(leaf, sb, lane & 3, pr);
-    return per_combine(__shfl(q, base), __shfl(q, base + 1), __shfl(q, base + 2), __shfl(q, base + 3));
+    return per_combine(quad_f64<0>(q), quad_f64<1>(q), quad_f64<2>(q), quad_f64<3>(q));
 }
 
 // A level-1 node wholly inside the push range: the same sums over 16 copies of the pushed leaf.
@@ -247,7 +247,7 @@ __device__ __forceinline__ int per_group_find(const double (&v)[NV], double x, d
     double acc = 0.0;
 #pragma unroll
     for (int e = 0; e < NV; ++e) acc += v[e];
-    const double s0 = __shfl(acc, g0), s1 = __shfl(acc, g0 + 1), s2 = __shfl(acc, g0 + 2);
+    const double s0 = quad_f64<0>(acc), s1 = quad_f64<1>(acc), s2 = quad_f64<2>(acc);
     const double ex = q == 0 ? 0.0 : (q == 1 ? s0 : (q == 2 ? s0 + s1 : (s0 + s1) + s2));
     int hit = -1, nz = -1;
     double hb = 0.0, hv = 0.0, nb = 0.0, nv = 0.0, run = ex;
@@ -270,9 +270,9 @@ __device__ __forceinline__ int per_group_find(const double (&v)[NV], double x, d
         hv = nz < 0 ? 0.0 : nv;
     }
     // every lane computed its candidate; take lane src's (the branch above is group-uniform)
-    const int kk = __shfl(k, g0 + src);
-    before = __shfl(hb, g0 + src);
-    val = __shfl(hv, g0 + src);
+    const int kk = quad_sel_i32(k, src);
+    before = quad_sel_f64(hb, src);
+    val = quad_sel_f64(hv, src);
     return src * NV + kk;
 }
 

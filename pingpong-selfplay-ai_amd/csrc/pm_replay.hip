@@ -126,7 +126,6 @@ int per_launch_build(const float* prios, int64_t cap, float alpha, const pm_ctrl
 }
 int per_launch_nodes(void* work, int64_t cap, hipStream_t st) {
     const PerTree tr = per_tree(work, cap);
-    const auto grid = [](int64_t n) { return (unsigned)(n > 0 ? (n + 255) / 256 : 1); };
     hipLaunchKernelGGL(k_per_nodes, dim3((unsigned)((tr.nsub + 63) / 64)), dim3(256), 0, st, cap, 0.f,
                        (const pm_ctrl*)nullptr, (int64_t)0, tr);
     PM_LAUNCHED("k_per_nodes");

@@ -1145,8 +1145,7 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
             const double x = (double)(pushed ? pval : v[i]);
             acc += e < cap32 ? x : 0.0;  // past cap: no leaf
         }
-        const int b4 = lane & ~3;
-        const double node = per_combine(__shfl(acc, b4), __shfl(acc, b4 + 1), __shfl(acc, b4 + 2), __shfl(acc, b4 + 3));
+        const double node = per_combine(quad_f64<0>(acc), quad_f64<1>(acc), quad_f64<2>(acc), quad_f64<3>(acc));
         if (q == 0 && k < 4 * nsub) {
             sm.subv[s] = node;
             tree.sub[sm.subid[s]] = node;
@@ -1898,9 +1897,9 @@ __device__ __forceinline__ double multi_quarter(const float* leaf, int64_t sb, i
     return acc;
 }
 __device__ __forceinline__ double multi_sub_sum4(const float* leaf, int64_t sb, int64_t cap) {
-    const int lane = threadIdx.x & 63, base = lane & ~3;
+    const int lane = threadIdx.x & 63;
     const double q = multi_quarter(leaf, sb, lane & 3, cap);
-    return per_combine(__shfl(q, base), __shfl(q, base + 1), __shfl(q, base + 2), __shfl(q, base + 3));
+    return per_combine(quad_f64<0>(q), quad_f64<1>(q), quad_f64<2>(q), quad_f64<3>(q));
 }
 __device__ __forceinline__ double multi_chunk_sum(const PerTree& t, int64_t c) {
     typedef double f64x2v __attribute__((ext_vector_type(2)));
@@ -2000,7 +1999,7 @@ __device__ __forceinline__ int group_find16f(const float (&f)[16], int64_t lo, i
     double acc = 0.0;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc += lv(e);
-    const double s0 = __shfl(acc, g0), s1 = __shfl(acc, g0 + 1), s2 = __shfl(acc, g0 + 2);
+    const double s0 = quad_f64<0>(acc), s1 = quad_f64<1>(acc), s2 = quad_f64<2>(acc);
     const double ex = q == 0 ? 0.0 : (q == 1 ? s0 : (q == 2 ? s0 + s1 : (s0 + s1) + s2));
     int hit = -1, nz = -1;
     double hb = 0.0, hv = 0.0, nb = 0.0, nv = 0.0, run = ex;
@@ -2023,9 +2022,9 @@ __device__ __forceinline__ int group_find16f(const float (&f)[16], int64_t lo, i
         hb = nz < 0 ? ex : nb;
         hv = nz < 0 ? 0.0 : nv;
     }
-    const int kk = __shfl(k, g0 + src);
-    before = __shfl(hb, g0 + src);
-    val = __shfl(hv, g0 + src);
+    const int kk = quad_sel_i32(k, src);
+    before = quad_sel_f64(hb, src);
+    val = quad_sel_f64(hv, src);
     return src * 16 + kk;
 }
 

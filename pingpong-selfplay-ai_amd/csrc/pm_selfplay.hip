@@ -920,7 +920,9 @@ __device__ __forceinline__ void push_rows_fwd2(const pm_selfplay& sp, PushFwdSme
         if ((it + 1) * 8 < ntile) __syncthreads();  // block-uniform: part is reused
     }
 }
-__device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, PushFwdSmem& sm, bool push2, bool pushg) {
+// Returns the control block as block 1 read it (the tree refresh uses the same copy: the learner
+// waits for block 1's token or granules, which follow this read, before it commits the next step's).
+__device__ __forceinline__ pm_ctrl push_fwd_block(const pm_selfplay& sp, int mode, PushFwdSmem& sm, bool push2, bool pushg) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
     PM_STAMP_ANY(50);
     stage_frags_lds(sp.w_B, sm.lw, 0);
@@ -932,7 +934,7 @@ __device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, 
     const int64_t s_after = cs.size + sp.n < sp.cap ? cs.size + sp.n : sp.cap;
     if (!push_handoff(mode, s_after >= B)) {  // block-uniform: no rows to compute
         if ((mode & PM_UPD_FIRST) && t == 0) st_out<true>(push_flag(sp), push_token(cs));
-        return;
+        return cs;
     }
     if (pushg && t == 0) st_out<true>(push_flag(sp), push_token(cs));  // block 1 read the control block
     const bool ip = t < B && push_of(sp, cs.pos, cs.size, cs.max_prio).covers(id);
@@ -950,11 +952,12 @@ __device__ __forceinline__ void push_fwd_block(const pm_selfplay& sp, int mode, 
                       [&](int j, bool nxt, int ln, const f32x16 (&c2)[2], const float (&qb)[3], const float (&qt)[3],
                           const float (&rb)[2]) { store_hfeat<true>(pay, j, nxt, ln, c2, qb, qt, rb); });
     PM_STAMP_ANY(52);
-    if (pushg) return;  // block-uniform: the granules need no drain, the flag is out
+    if (pushg) return cs;  // block-uniform: the granules need no drain, the flag is out
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are complete
     __syncthreads();
     PM_STAMP_ANY(53);
     if (t == 0) st_out<true>(push_flag(sp), push_token(cs));
+    return cs;
 }
 
 // ---- the sum-tree refresh block (round 5): block 1, after the push rows, refreshes every tree node
@@ -1028,10 +1031,9 @@ __device__ __forceinline__ int tr_lookup(const uint32_t* key, uint32_t k, int bi
     }
 }
 
-__device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, TreeRefreshSmem& sm) {
+__device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, TreeRefreshSmem& sm, const pm_ctrl& cs) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
     PM_STAMP_ANY(55);
-    const pm_ctrl cs = *sp.ctrl;
     const PerTree tree = per_tree(sp.per_work, sp.cap);
     const uint32_t tag = __hip_atomic_load(tr_epoch(sp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const bool last = mode & PM_UPD_LAST;
@@ -1258,10 +1260,10 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     tr &= 1;
     if (blockIdx.x > 0) {
         if (blockIdx.x == 1) {
-            push_fwd_block(sp, mode, shm.pf, push2, pushg);
+            const pm_ctrl cs = push_fwd_block(sp, mode, shm.pf, push2, pushg);
             if (tr) {
                 __syncthreads();  // the push rows' LDS is reused
-                tree_block(sp, mode, shm.tr);
+                tree_block(sp, mode, shm.tr, cs);
             }
             return;
         }

@@ -1164,30 +1164,27 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
     PM_STAMP_ANY(58);
     // level 2: every chunk slot from LDS, its refreshed / pushed children substituted (per_chunk_sum)
     const int nsub_tree = (int)tree.nsub;
-    if (t < nch) {
-        const int c0 = (int)sm.chid[t] * PER_FAN;
-        // every operand read unconditionally first (the compiler otherwise sinks each LDS read into
-        // its own branch), then selected in per_chunk_sum's order
-        double old[PER_FAN], fresh[PER_FAN];
-        int m[PER_FAN];
-#pragma unroll
-        for (int k = 0; k < PER_FAN; ++k) {
-            m[k] = sm.cmap[t][k];
-            old[k] = sm.ls[t][k];
-        }
-#pragma unroll
-        for (int k = 0; k < PER_FAN; ++k) fresh[k] = sm.subv[m[k] >= 0 ? m[k] : 0];
-#pragma unroll
-        for (int k = 0; k < PER_FAN; ++k) asm volatile("" : "+v"(old[k]), "+v"(fresh[k]));
+    static_assert(PER_FAN == 16, "one DPP row per level-2 node");
+    // one 16-lane DPP row per chunk slot: lane k of the row reads child k (consecutive LDS words; a
+    // thread per slot reading its 16 children strided 128 B apart was a 32-way bank conflict per
+    // read), and the row's lane 0 folds the 16 terms in per_chunk_sum's order (row_shl:k)
+    for (int base = wv * 4; base < nch; base += kLearn / 16) {  // wave-uniform
+        const int slot = min(base + (lane >> 4), nch - 1), k = lane & 15;
+        const int m = sm.cmap[slot][k];
+        const double old = sm.ls[slot][k];
+        const double fresh = sm.subv[m >= 0 ? m : 0];
+        const int sb = (int)sm.chid[slot] * PER_FAN + k;
+        const bool pushed = (sb >= p1lo && sb < p1hi) || sb < p2hi;
+        const double v = m >= 0 ? fresh : (pushed ? csub : old);
+        const double x = sb < nsub_tree ? v : 0.0;
         double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < PER_FAN; ++k) {
-            const int sb = c0 + k;
-            const bool pushed = (sb >= p1lo && sb < p1hi) || sb < p2hi;
-            const double v = m[k] >= 0 ? fresh[k] : (pushed ? csub : old[k]);
-            acc += sb < nsub_tree ? v : 0.0;
-        }
-        tree.chunk[sm.chid[t]] = acc;
+        acc += x;
+        acc += dpp_f64<0x101>(x); acc += dpp_f64<0x102>(x); acc += dpp_f64<0x103>(x);
+        acc += dpp_f64<0x104>(x); acc += dpp_f64<0x105>(x); acc += dpp_f64<0x106>(x);
+        acc += dpp_f64<0x107>(x); acc += dpp_f64<0x108>(x); acc += dpp_f64<0x109>(x);
+        acc += dpp_f64<0x10A>(x); acc += dpp_f64<0x10B>(x); acc += dpp_f64<0x10C>(x);
+        acc += dpp_f64<0x10D>(x); acc += dpp_f64<0x10E>(x); acc += dpp_f64<0x10F>(x);
+        if (k == 0 && base + (lane >> 4) < nch) tree.chunk[sm.chid[slot]] = acc;
     }
     PM_STAMP_ANY(63);
     if (last) {  // the next push's other level-2 nodes: inside a segment (every boundary chunk holds an

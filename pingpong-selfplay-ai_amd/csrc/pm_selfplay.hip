@@ -2528,8 +2528,10 @@ LearnGrid learn_grid(const pm_selfplay* sp) {
 }
 
 // The sum-tree refresh in block 1 (tree_block) unless PONGMI_TR=0 (the learner's own refresh, A/B).
+// Read per launch (a getenv per k_learn launch is host work beside the GPU's): the variants are
+// bitwise equal (test_learner_variants_are_bitwise_identical switches them between launches).
 int tree_refresh_block() {
-    static const int v = [] {
+    const int v = [] {
         const char* e = getenv("PONGMI_TR");
         const char* p = getenv("PONGMI_PUSH2");  // block 1's push rows on two waves per tile (default 1)
         const char* q = getenv("PONGMI_LATE_NOISE");  // the apply's noise / Adam constants in phase 2 (default 1)

@@ -391,6 +391,32 @@ def test_overlapped_step_is_bitwise_identical(golden):
     assert A.counters() == B.counters()
 
 
+@pytest.mark.parametrize("knobs", [{"PONGMI_PUSHG": "0"}, {"PONGMI_TR": "0"}, {"PONGMI_PUSH2": "0"},
+                                   {"PONGMI_LATE_NOISE": "0"}, {"PONGMI_TR": "0", "PONGMI_PUSH2": "0"}])
+def test_learner_variants_are_bitwise_identical(golden, monkeypatch, knobs):
+    """k_learn's placement knobs (read per launch) move work between blocks and never change a
+    result: the push rows as drained rows + flag instead of tagged granules (PUSHG=0, the
+    k_learn<false> instantiation), the learner's own tree refresh instead of block 1's (TR=0), one wave
+    per push-row tile (PUSH2=0), the apply's noise in phase 0 (LATE_NOISE=0). A push range of a
+    quarter of the replay puts many sampled rows on the hand-off."""
+    kw = dict(n=4096, batch=256, cap=16384, seed=31, n_pool=3)
+    A = _learner(golden, **kw)
+    B = _learner(golden, **kw)
+    for _ in range(24):
+        for k, v in knobs.items():
+            monkeypatch.setenv(k, v)
+        A.step()
+        for k in knobs:
+            monkeypatch.delenv(k)
+        B.step()
+    torch.cuda.synchronize()
+    for name in ("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "opp", "w_B",
+                 "learn_heads", "per_work", "idx", "isw", "aA", "aB", "obsA", "obsB", "ep_reward"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    ca, cb = A.counters(), B.counters()
+    assert ca == cb and ca["train_steps"] == 24 and ca["status"] == 0
+
+
 def test_production_step_equals_plain_at_full_size(golden):
     """The bench's production step (overlapped, features ahead, fused apply) at configs[2]'s full
     size equals the plain three-kernel step bit for bit, across the replay ring's first wrap

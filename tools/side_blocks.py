@@ -27,6 +27,7 @@ def main():
     lib = _lib.load()
     lib.pm_diag_read_side.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.pm_diag_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
+    lib.pm_diag_read_blk.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     n = 65536
     sdB, sdA = bench.synthetic_qnet(1), bench.synthetic_qnet(2)
     pool = [bench.synthetic_qnet(100 + k) for k in range(8)]
@@ -50,15 +51,20 @@ def main():
     nfeat = (ntiles + ft - 1) // ft
     side = (ctypes.c_uint64 * (4 * 1024))()
     buf = (ctypes.c_uint64 * 256)()
-    rows = []
+    rows, tiles = [], []
+    blk = (ctypes.c_uint64 * (8 * 4096))()
     for _ in range(20):
         L.step()
         torch.cuda.synchronize()
         lib.pm_diag_read_side(side)
         lib.pm_diag_read(buf, 256)
+        lib.pm_diag_read_blk(blk)  # act_block's PM_BLK stamps of the side-A blocks (grid blocks 2 ..)
+        b = np.array(blk[:], dtype=np.int64).reshape(8, 4096)[:, 2:2 + nact]
         a = np.array(side[:], dtype=np.int64).reshape(4, 1024)[:, :nact + nfeat]
         t0 = int(buf[0])  # learner start
         rows.append(((a[0] - t0) * 0.01, (a[1] - t0) * 0.01, (a[2] - t0) * 0.01, a[3] >> 16))
+        tiles.append(((b[4] - t0) * 0.01, (b[1] - t0) * 0.01, (b[5] - t0) * 0.01, (b[6] - t0) * 0.01,
+                      (b[7] - t0) * 0.01))
     beg = np.median(np.stack([r[0] for r in rows]), axis=0)
     slp = np.median(np.stack([r[1] for r in rows]), axis=0)
     end = np.median(np.stack([r[2] for r in rows]), axis=0)
@@ -77,6 +83,13 @@ def main():
     line("modelA", idx < na0)
     line("pool", (idx >= na0) & (idx < nact))
     line("feature", idx >= nact)
+    # act blocks' inner phases (block thread 0 = wave 0): staging issued, lists / compaction done +
+    # barrier, wave 0's first tile operands landed, its hidden layers, its heads
+    tl = [np.median(np.stack([r[k] for r in tiles]), axis=0) for k in range(5)]
+    for name, sel in (("modelA", np.arange(nact) < na0), ("pool", np.arange(nact) >= na0)):
+        for lab, v in zip(("staged", "listed", "tile0 in", "tile0 hid", "tile0 heads"), tl):
+            x = v[sel]
+            print(f"  {name:8s} {lab:11s} {x.min():7.2f} {np.median(x):7.2f} {np.percentile(x, 90):7.2f} {x.max():7.2f}")
     late = np.argsort(end)[-8:]
     print("  latest 8 blocks (side index, role, begin, end, rows):",
           [(int(i), "A" if i < na0 else ("P" if i < nact else "F"), round(float(beg[i]), 2), round(float(end[i]), 2),

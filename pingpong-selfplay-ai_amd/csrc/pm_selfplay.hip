@@ -1246,6 +1246,11 @@ static_assert(sizeof(LearnShared) <= 160 * 1024, "k_learn LDS");
 // push k_env just made, which this kernel computes; it sums the rollout's episode counters); LAST =
 // the step's last update (refreshes the sum tree for the next push, commits the step). U = 1: both.
 // Block 1 is push_fwd_block; the side-A act blocks (launches with side blocks) follow it.
+// A side block's start delay: n x s_sleep 16 (1 024 clocks each; n = 8 ~ the former s_sleep 127)
+__device__ __forceinline__ void side_nap(int n) {
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(16);
+}
+
 // PG: the push rows as tagged granules (tr bit 3; a separate instantiation: the flag consumer's
 // branch beside the granule sweep made the compiler wait for every granule load in turn).
 template <bool PG>
@@ -1269,7 +1274,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         const ActGrid g{sp.n, sp.n_pool + 1, chunkA, chunkP, 0};
         const int fb = sb - g.blocks();
         if (fb >= 0) {  // block-uniform: modelB's features for the next step (sp.featB)
-            if (sleepf & 2) __builtin_amdgcn_s_sleep(127);
+            if (sleepf & 2) side_nap(sleepf >> 8);
             const int t0 = fb * ftiles;
             feat_tiles(shm.act.lw, sp.w_B, sp.obsB, sp.n, t0, min(t0 + ftiles, feat_ntiles(sp.n)), sp.featB);
             PM_STAMP_MAX(67);
@@ -1279,7 +1284,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
         }
         // the learner's load phase is latency-bound under the side blocks' staging bursts: the role
         // with slack starts after its loads are in flight (side_sleep: the feature blocks by default)
-        if (sleepf & 1) __builtin_amdgcn_s_sleep(127);
+        if (sleepf & 1) side_nap(sleepf >> 8);
         PM_SIDE(1, sb, __builtin_amdgcn_s_memrealtime());
         const TileOut outA{sp.aA, nullptr, -1.0, 0, 0};
         act_block(shm.act, g, sp.w_opp, sp.n_pool > 0 ? sp.opp : nullptr, nullptr, sp.obsA, nullptr, outA, outA,
@@ -2484,12 +2489,12 @@ constexpr int kSideRows = 480;
 // their staging bursts (PONGMI_SIDE_SLEEP: bit 0 act blocks, bit 1 feature blocks). Default 2 since
 // the one-round grid: the feature blocks have the slack (r5o, same box, two interleaved passes:
 // 2 -> 1.79 / 1.81 G env-steps/s, 0 -> 1.81 / 1.77, 1 (round 4) -> 1.76 / 1.75, 3 -> 1.75 / 1.75).
+// PONGMI_SIDE_NAP: the delay in units of 1 024 clocks (default 8, ~3.4 us), bits 8.. of the argument.
 int side_sleep() {
-    static const int v = [] {
-        const char* e = getenv("PONGMI_SIDE_SLEEP");
-        return e && *e ? atoi(e) : 2;
-    }();
-    return v;
+    const char* e = getenv("PONGMI_SIDE_SLEEP");
+    const char* n = getenv("PONGMI_SIDE_NAP");
+    const int roles = e && *e ? atoi(e) : 2, nap = n && *n ? atoi(n) : 8;
+    return (roles & 3) | (std::max(0, std::min(nap, 64)) << 8);
 }
 int side_mode() {
     static const int v = [] {

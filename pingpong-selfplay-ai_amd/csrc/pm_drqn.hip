@@ -903,8 +903,7 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
                 }
             }
             if (a.local_norm) {
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+                sq = wave_sum(sq);  // the xor butterfly's value, on DPP (pm_dev.h)
                 if (lane == 0) a.NP[bid] = sq;
             }
         }

@@ -112,7 +112,7 @@ run_task() {
           echo "$var=$first $(tail -1 gpurun_out/${tag}_drqnab.log)" || return 1
       for rep in 1 2 3; do
         for v in ${vals//,/ }; do
-          env $var=$v timeout -k 10 120 python3 tools/drqn_time.py 2>/dev/null | tail -1 | sed "s/^/$var=$v /" || return 1
+          env $var=$v timeout -k 10 120 python3 tools/drqn_time.py 2>/dev/null | tail -1 | sed "s#^#$var=$v #" || return 1
         done
       done ;;
     roll)  # k_rollout16 per-step phase cycles (diag build)

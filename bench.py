@@ -7,6 +7,10 @@ push + proportional sample, double-DQN update with target net, Adam), weak-scale
     python bench.py [--gpus N] [--steps K] [--warmup W] [--arenas 65536] [--pool 8]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+--gpus N is authoritative (launch_plan): without a launcher (WORLD_SIZE unset) and N > 1 the bench
+starts `torch.distributed.run --nproc-per-node N bench.py ...` as a child before any GPU call and
+exits with its code; WORLD_SIZE != N, or fewer visible GPUs than N, exits 2 with an error line.
+
 A step = one vector step: every arena on every rank advances one env step and every rank runs one
 PER update of batch 256. value = total env-steps (all ranks) / max-over-ranks wall time of K steps.
 Rank 0 prints one JSON line. Also reported:
@@ -701,15 +705,165 @@ def run_infer(args, dist, rank, world):
         dist.destroy_process_group()
 
 
+REF_LOOP_STEPS_PER_S = {"small_buffer": 398, "fill_100k": 209, "fill_1e6": 75}  # SURVEY 6, 1 CPU thread
+
+
+def run_train(args, dist, rank, world):
+    """The real training path at the reference's replay ratio: one
+    config.yaml generation try as pongmi.generations.QNetGenerations runs it — `episodes_per_generation`
+    (2 400) episodes of self-play on `--arenas` (512) arenas with U = replay_ratio x arenas updates per
+    vector step (1.0: one PER update of batch 256 per pushed transition, the reference's one update per
+    env step, scripts/train_iterative.py:239-245), PER cap 1e6 starting empty, target sync every 1 000
+    updates, then the try's evaluation (eval_vs_model + eval_vs_pool, 1 000 episodes each,
+    :171-196). value = env-steps/s over the play phase (wall clock, from an empty replay as a
+    generation starts); also updates/s, the play / evaluation / try wall seconds, and k_learn_multi's
+    per-update time from its own dispatch. Shards (N > 1) would be independent tries: the controller
+    is single-GPU (U > 1 steps are unsharded, pm_selfplay_step_multi)."""
+    import yaml
+    from pongmi import _lib
+    from pongmi.evaluate import eval_vs_model, eval_vs_pool
+    from pongmi.generations import _env_kw, _play_episodes, updates_for
+    from pongmi.selfplay import SelfPlayLearner
+    if world > 1:
+        raise SystemExit("--workload train is a single-GPU generation try (the reference's controller); use --gpus 1")
+    with open(os.path.join(ROOT, "pingpong-selfplay-ai_amd", "config.yaml")) as fh:
+        cfg = yaml.safe_load(fh)
+    t = cfg["training"]
+    env_kw = _env_kw(cfg)
+    n = args.arenas or 512
+    U = updates_for(n, args.replay_ratio)
+    pool_n = 8 if args.pool is None else args.pool
+    sdB, _, pool, wdesc = bench_nets(args.weights, pool_n)
+    episodes = int(args.episodes or t["episodes_per_generation"])
+    eval_eps = int(t["eval_episodes"])
+
+    def learner(seed):
+        return SelfPlayLearner(env_kw, n, sdB, sdB, pool, batch=t["batch_size"], memory_size=t["memory_size"],
+                               gamma=t["gamma"], lr=t["lr"], epsilon=t["min_epsilon"], min_epsilon=t["min_epsilon"],
+                               epsilon_decay=t["epsilon_decay"], target_update_interval=t["target_update_interval"],
+                               pool_ratio=t["opponent_pool_ratio"], seed=seed, updates_per_step=U)
+
+    class _Quiet:  # _play_episodes' progress hook without console lines
+        def tick(self, c):
+            pass
+
+    # warm-up on a throwaway learner (module load, lazy allocations), so the try starts like a
+    # generation does: empty replay, episode count 0
+    W = learner(99)
+    for _ in range(max(2, args.warmup)):
+        W.step()
+    torch.cuda.synchronize()
+    del W
+    import random as _random
+    rng = _random.Random(5)
+    L = learner(7)
+    c0 = L.counters()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    c1 = _play_episodes(L, episodes, _Quiet(), 4)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    B = (L.modelB_state_dict(), _lib.PM_FOLD_TRAIN)
+    wA = eval_vs_model(env_kw, (L.modelA_state_dict(), _lib.PM_FOLD_TRAIN), B, eval_eps, rng=rng)
+    wP = eval_vs_pool(env_kw, B, [(sd, _lib.PM_FOLD_EVAL) for sd in pool], eval_eps, rng=rng)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    L.check_status(c1)
+    # k_learn_multi (updates 1..U-1 of a vector step) by its own dispatch, after the try
+    um = []
+    for _ in range(5):
+        _lib.timer_arm(_lib.PM_TIMER_LEARN_MULTI)
+        L.step()
+        um.append(_lib.timer_read(_lib.PM_TIMER_LEARN_MULTI))
+    multi_s = sum(um) / len(um)
+    play_s, eval_s = t1 - t0, t2 - t1
+    vsteps = c1["step"] - c0["step"]
+    env_steps = vsteps * n
+    upd = c1["train_steps"] - c0["train_steps"]
+    if rank == 0:
+        value = env_steps / play_s
+        out = {
+            "metric": "env-steps/sec, one config.yaml generation try of the train_iterative loop at the reference's "
+                      "replay ratio (1 update of 256 per env step)",
+            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": vsteps, "warmup": args.warmup,
+            "ms_per_step": round(play_s / max(vsteps, 1) * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64 env state / f32 QNet",
+            "data": f"synthetic (env Philox serves; {wdesc})",
+            "config": {"workload": f"train: config.yaml generation try, {episodes} episodes on {n} arenas, U = {U} "
+                                   f"updates per vector step (replay ratio {args.replay_ratio}), PER cap "
+                                   f"{t['memory_size']} from empty, batch {t['batch_size']}, target sync every "
+                                   f"{t['target_update_interval']}, then eval 2 x {eval_eps} episodes",
+                       "arenas": n, "updates_per_vector_step": U, "pool": pool_n, "episodes": c1["episodes"] - c0["episodes"],
+                       "learn_multi": L.frow is not None},
+            "updates": upd, "updates_per_s": round(upd / play_s, 1), "play_s": round(play_s, 3),
+            "eval_s": round(eval_s, 3), "generation_try_s": round(play_s + eval_s, 3),
+            "eval": {"vs_A": wA, "vs_pool": wP},
+            "learn_multi_us_per_update": round(multi_s / max(U - 1, 1) * 1e6, 3),
+            "learn_multi_launch_us": round(multi_s * 1e6, 1),
+            "reference_python_measured": {"steps_per_s": REF_LOOP_STEPS_PER_S,
+                                          "note": "train_iterative.py step body (1 env step + 1 update of 256), 1 CPU "
+                                                  "thread (SURVEY 6); a 2 400-episode try is ~91 k steps"},
+            "vs_reference_loop": {k: round(value / v, 1) for k, v in REF_LOOP_STEPS_PER_S.items()},
+        }
+        print(json.dumps(out), flush=True)
+
+
+def launch_plan(argv, env, device_count):
+    """What `python bench.py --gpus N ...` does before any GPU call. Returns
+    ("run", None) when this process is the (only or torchrun-launched) rank that should run, ("spawn",
+    cmd) when N > 1 ranks are asked for and no launcher started us (WORLD_SIZE unset): cmd starts
+    torch.distributed.run with N ranks on this same bench, which this process then waits on as a
+    child (never exec: the parent exits with the child's code), or ("error", message) when the
+    request cannot be honoured — WORLD_SIZE set and != --gpus, or fewer visible devices than ranks.
+    `device_count` is torch.cuda.device_count() (which does not initialise the GPU on this image)
+    or None to skip that check."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    ns, _ = ap.parse_known_args(argv)
+    n = ns.gpus
+    if n < 1:
+        return "error", f"--gpus {n}: need at least one GPU"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != n:
+            return "error", (f"--gpus {n} but WORLD_SIZE={ws}: the launcher started a different number of ranks "
+                             f"than the bench was asked to report")
+        if device_count is not None and int(env.get("LOCAL_RANK", "0")) >= device_count:
+            return "error", f"LOCAL_RANK {env.get('LOCAL_RANK')} but only {device_count} visible GPU(s)"
+        return "run", None
+    if n == 1:
+        return "run", None
+    if device_count is not None and device_count < n:
+        return "error", f"--gpus {n} but only {device_count} visible GPU(s) on this node"
+    import socket
+    with socket.socket() as s:  # a free rendezvous port on the loopback (the hostname may not resolve)
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return "spawn", cmd
+
+
 def main():
+    plan, what = launch_plan(sys.argv[1:], os.environ, torch.cuda.device_count())
+    if plan == "error":
+        print(json.dumps({"error": what, "argv": sys.argv[1:]}), flush=True)
+        sys.exit(2)
+    if plan == "spawn":
+        import subprocess
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        sys.exit(subprocess.call(what, env=env))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="vector steps timed (200; infer: 10000)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed vector steps first (30; infer: 100)")
-    ap.add_argument("--workload", choices=("dqn", "rnn", "infer", "collect"), default="dqn",
+    ap.add_argument("--workload", choices=("dqn", "rnn", "infer", "collect", "train"), default="dqn",
                     help="dqn: configs[2] (the headline); rnn: configs[4], the QNetRNN / DRQN loop; infer: "
                          "configs[1], the inference-only rollout megakernel; collect: 8f3, that megakernel "
-                         "pushing every transition into the PER replay ring at 65 536 arenas")
+                         "pushing every transition into the PER replay ring at 65 536 arenas; train: one config.yaml "
+                         "generation try at the reference's replay ratio (QNetGenerations' loop)")
+    ap.add_argument("--replay-ratio", type=float, default=1.0, help="train: updates per pushed transition")
+    ap.add_argument("--episodes", type=int, default=None, help="train: episodes per try (config.yaml: 2400)")
     ap.add_argument("--infer-chunk", type=int, default=10000, help="infer: vector steps per pm_rollout launch")
     ap.add_argument("--arenas", type=int, default=None, help="arenas per GPU (65536 dqn, 32768 rnn)")
     ap.add_argument("--pool", type=int, default=None, help="opponent pool size (synthetic nets; 8 dqn, 4 rnn)")
@@ -738,9 +892,10 @@ def main():
     infer = args.workload in ("infer", "collect")
     collect = args.workload == "collect"
     args.steps = args.steps if args.steps is not None else (3000 if collect else 10000 if infer else 200)
-    args.warmup = args.warmup if args.warmup is not None else (100 if infer else 30)
+    args.warmup = args.warmup if args.warmup is not None else (100 if infer else 4 if args.workload == "train" else 30)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    assert world == args.gpus, (world, args.gpus)  # launch_plan guarantees it
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # configs[0]'s scalar CPU loop runs in forked worker processes: before this process touches the GPU
@@ -761,6 +916,8 @@ def main():
 
     if args.workload == "rnn":
         return run_rnn(args, dist, rank, world, allreduce)
+    if args.workload == "train":
+        return run_train(args, dist, rank, world)
     if infer:
         return run_infer(args, dist, rank, world)
     args.arenas = args.arenas or 65536

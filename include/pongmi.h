@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 22
+#define PM_ABI_VERSION 23
 
 #define PM_OK 0
 #define PM_E_ARG (-1)     /* null / inconsistent argument */
@@ -650,7 +650,8 @@ int pm_rnn_selfplay_step_sharded_overlap(const pm_rnn_selfplay* sp, const pm_drq
 #define PM_TIMER_ENV_STEP 3 /* k_env_step (K1, pm_env_step) */
 #define PM_TIMER_ROLLOUT 4  /* k_rollout (K9, pm_rollout) */
 #define PM_TIMER_DRQN 5     /* k_dq_recur (K6: the DRQN update's persistent recurrence, pm_drqn_grads) */
-#define PM_TIMER_N 6
+#define PM_TIMER_LEARN_MULTI 6 /* k_learn_multi: updates 1..U-1 of a vector step (pm_selfplay_step_multi, ABI 23) */
+#define PM_TIMER_N 7
 int pm_timer_arm(int32_t kernel);
 int pm_timer_read(int32_t kernel, float* ms);
 

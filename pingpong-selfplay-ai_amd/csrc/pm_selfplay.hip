@@ -2526,8 +2526,12 @@ LearnGrid learn_grid(const pm_selfplay* sp) {
                          kFeatTilesLearn};
     const double pp = sp->n_pool > 0 ? sp->pool_ratio : 0.0;
     const ActGrid g{sp->n, sp->n_pool + 1, side_chunk(1.0 - pp), side_chunk(sp->n_pool > 0 ? pp / sp->n_pool : 0.0), 0};
+    // the feature blocks take the CUs the act blocks leave; when (nearly) none are left (n well above
+    // configs[2]'s 65 536: the act blocks alone fill the chip) they share the chip over the whole
+    // device instead, so no block runs thousands of tiles in series
     const int left = device_cus() - 2 - g.blocks();
-    int ft = left > 0 ? (ntiles + left - 1) / left : ntiles;
+    const int slots = left >= 32 ? left : device_cus();
+    int ft = (ntiles + slots - 1) / slots;
     ft = std::max(ft, kFeatTilesLearn);
     return LearnGrid{g, std::min(ft, std::max(ntiles, 1))};
 }
@@ -2669,7 +2673,7 @@ extern "C" int pm_selfplay_step_multi(const pm_selfplay* sp, int32_t updates, vo
     if ((rc = launch_learn(sp, true, st, PM_UPD_FIRST))) return rc;
     if ((rc = pm_selfplay_apply_ex(sp, PM_UPD_FIRST, stream))) return rc;
     if (multi_ok(sp)) {  // updates 1..U-1 in one single-workgroup launch
-        hipLaunchKernelGGL(k_learn_multi, dim3(1), dim3(kLearn), 0, st, *sp, (int)updates);
+        pm_launch(PM_TIMER_LEARN_MULTI, k_learn_multi, dim3(1), dim3(kLearn), st, *sp, (int)updates);
         PM_LAUNCHED("k_learn_multi");
         return pm_selfplay_commit(sp, stream);
     }

@@ -35,9 +35,9 @@ PM_FOLD_EVAL, PM_FOLD_TRAIN, PM_FOLD_TRAIN_FRESH = 0, 1, 2
 PM_ACT_ALL, PM_ACT_B, PM_ACT_A = 0, 1, 2
 PM_UPD_FIRST, PM_UPD_LAST = 1, 2
 PM_COMM_ID_BYTES = 128
-ABI_VERSION = 22
-PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_ROLLOUT, PM_TIMER_DRQN, PM_TIMER_N = \
-    0, 1, 2, 3, 4, 5, 6
+ABI_VERSION = 23
+PM_TIMER_ACTENV, PM_TIMER_LEARN, PM_TIMER_RNN_ACT, PM_TIMER_ENV_STEP, PM_TIMER_ROLLOUT, PM_TIMER_DRQN = 0, 1, 2, 3, 4, 5
+PM_TIMER_LEARN_MULTI, PM_TIMER_N = 6, 7
 PM_ROLL_HEADS = 264
 
 

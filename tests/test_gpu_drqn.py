@@ -3,13 +3,21 @@ torch autograd (tests/golden/drqn.npz) and against the float64 oracle (oracle.dr
 
 Tolerances (fp32 on the device; exact-f32 MFMA sums in a different order than torch's CPU GEMMs):
 loss / pre-clip norm rtol 1e-4; gradients rtol 5e-4 with atol 1e-5 x the tensor's largest magnitude
-(round 5: the kernel's measured worst was 0.40 of the round-4 bar of rtol 1e-3); 4e-5 x for the
-gradients of updates 1 and 2 from the device's trained parameters (ReLU decisions near 0, below). Parameters are
+(round 5: the kernel's measured worst was 0.40 of the round-4 bar of rtol 1e-3), every update, every
+tensor. The one exemption is targeted (_assert_grads_relu): an obs-stream ReLU whose pre-activation
+is within float32 rounding of 0 (|p| <= 64 * 2^-24 * sum|terms|, oracle.drqn_grads' relu_band) is a
+rounding decision the device may take the other way, so the device's gradient must equal, at the
+same bar, the oracle's gradient with SOME subset of those decisions flipped (the empty subset first);
+the decisions flipped and the elements whose reference they change are printed. Parameters are
 pinned by composition, with no sign band: every update's gradient is checked against the oracle run
 from the device's OWN pre-update parameters (so Adam's sign-of-rounding cannot drift the two apart),
 and clip + Adam given that gradient and the device's pre-clip norm is checked bit for bit against
-the float32 restatement oracle.clip_adam_f32 — every parameter, both moments, every update.
+the float32 restatement oracle.clip_adam_f32 — every parameter, both moments, every update. The
+parameters after the three fixture updates are also compared with the reference's own autograd run
+(final_sub.*) under the sign band that Adam's normalised step needs there (_assert_final_sub).
 """
+import itertools
+
 import numpy as np
 import pytest
 import torch
@@ -47,6 +55,45 @@ def _assert_grads(got, ref, what, atol_rel=1e-5):
     return worst
 
 
+def _grad_err(got, ref, atol_rel=1e-5):
+    """max over tensors of |got - ref| / (atol_rel max|ref| + GRAD_RTOL |ref|): <= 1 passes the bar."""
+    worst = 0.0
+    for k, r in ref.items():
+        tol = atol_rel * np.abs(r).max() + 1e-9
+        worst = max(worst, float(np.max(np.abs(got[k] - r) / (tol + GRAD_RTOL * np.abs(r)))))
+    return worst
+
+
+RELU_BAND = 64.0  # |p| <= RELU_BAND * 2^-24 * sum|terms|: the ReLU decision is a float32 rounding decision
+MAX_SITES = 10
+
+
+def _assert_grads_relu(got, orc, sd, tsd, batch, what):
+    """The device's gradient vs the float64 oracle at the full bar (atol 1e-5 max|g|), where the
+    oracle takes the device's side at each ReLU decision inside the float32 rounding band: subsets of
+    the band's decisions (the MAX_SITES closest to 0) are tried smallest first, and the first whose
+    flipped oracle gradient meets the bar is the one checked. Prints the band, the decisions the
+    device took the other way and, per tensor, the elements whose reference that moved by >= 0.1 x
+    the atol (the exempt elements: outside them the plain reference and the flipped one agree)."""
+    info = orc.drqn_grads(sd, tsd, *batch, relu_band=RELU_BAND)
+    order = np.argsort(info["margins"], kind="stable")[:MAX_SITES]
+    sites = [info["sites"][i] for i in order]
+    ref, flipped = info["grads"], ()
+    if _grad_err(got, ref) > 1.0:
+        for r in range(1, len(sites) + 1):
+            hit = next((c for c in itertools.combinations(sites, r)
+                        if _grad_err(got, g := orc.drqn_grads(sd, tsd, *batch, flip=c)["grads"]) <= 1.0), None)
+            if hit is not None:
+                ref, flipped = g, hit
+                break
+    exempt = {k: int(np.sum(np.abs(ref[k] - info["grads"][k]) >= 0.1 * (1e-5 * np.abs(info["grads"][k]).max())))
+              for k in ref}
+    print(f"\n{what}: {len(info['sites'])} ReLU decisions in the float32 band (margins "
+          f"{[round(info['margins'][i], 1) for i in order]}); the device took the other side at {len(flipped)}: "
+          f"{list(flipped)}; exempt elements {({k: v for k, v in exempt.items() if v}) or 0}")
+    return _assert_grads(got, ref, what), ref
+
+
 def _f64(sd):
     return {k: np.asarray(v, np.float64) for k, v in sd.items()}
 
@@ -79,6 +126,33 @@ def _snap(L):
 GRAD_RTOL = 5e-4
 
 
+def _assert_final_sub(L, gd, refs):
+    """The parameters after the three fixture updates vs the reference's own autograd run
+    (drqn.npz final_sub.*: every 8th element, make_golden_drqn.py). Adam normalises each element's
+    step to ~lr x sign(m), so an element whose gradient at some update is within the gradient bar of
+    zero (|g| <= 2e-5 x the tensor's max |g| in `refs`, the oracle gradients the updates were checked
+    against) may step the other way: that sign band gets 2 lr per update and is counted; every other
+    element must be within 1e-6 + 1e-5 |ref| (the round-4 check, kept beside the per-update
+    composition checks: ADVICE r5)."""
+    sd = L.state_dict()
+    nband = ntot = 0
+    worst = 0.0
+    for name in (n[len("final_sub."):] for n in gd if n.startswith("final_sub.")):
+        got = sd[name].numpy().astype(np.float64).reshape(-1)[::8]
+        ref = gd["final_sub." + name].astype(np.float64).reshape(-1)
+        band = np.zeros(ref.shape, bool)
+        for g in refs:
+            g = np.abs(np.asarray(g[name], np.float64))
+            band |= (g <= 2e-5 * g.max()).reshape(-1)[::8]
+        np.testing.assert_allclose(got[band], ref[band], rtol=0, atol=len(refs) * 2e-4 * 1.01, err_msg=f"{name} (band)")
+        np.testing.assert_allclose(got[~band], ref[~band], rtol=1e-5, atol=1e-6, err_msg=name)
+        nband += int(band.sum())
+        ntot += band.size
+        worst = max(worst, float(np.max(np.abs(got - ref)[~band] / (1e-6 + 1e-5 * np.abs(ref[~band])), initial=0.0)))
+    print(f"parameters after {len(refs)} updates vs the reference's autograd run: {nband} of {ntot} elements in the "
+          f"sign band; worst off-band error / (1e-6 + 1e-5 |ref|) {worst:.4f}")
+
+
 def test_drqn_update_matches_reference(golden, orc):
     """Three updates on the reference's fixture batches: loss and pre-clip norm vs the reference's
     autograd run every update, update 0's gradients vs autograd; every update's gradient vs the float64
@@ -86,7 +160,7 @@ def test_drqn_update_matches_reference(golden, orc):
     from pongmi.drqn import DRQNLearner
     gr, gd = golden("rnn"), golden("drqn")
     L = DRQNLearner(_sd(gr), batch=64, T=8)
-    worst = 0.0
+    worst, refs = 0.0, []
     for k in range(3):
         p0, m0, v0 = _snap(L)
         sd_before = _f64(L.state_dict())
@@ -98,14 +172,13 @@ def test_drqn_update_matches_reference(golden, orc):
         if k == 0:
             _assert_grads(_grads(L), {k2[len("u0_grad."):]: v for k2, v in gd.items() if k2.startswith("u0_grad.")},
                           "update 0 vs autograd")
-        info = orc.drqn_grads(sd_before, _f64(_sd(gr)), *_batch(gd, k))
-        # from trained parameters (updates 1, 2) a few feature pre-activations sit within float32
-        # rounding of the ReLU's 0, where the f32 device and the f64 oracle may take different sides:
-        # those W1 / W2 elements differ by ~2e-5 x max|g| (measured 2.2e-6 of ~0.1); update 0 (the
-        # fixture's parameters) keeps the 1e-5 bar
-        worst = max(worst, _assert_grads(_grads(L), info["grads"], f"update {k} vs oracle (device's own parameters)",
-                                         atol_rel=1e-5 if k == 0 else 4e-5))
+        # every update at the full bar; a ReLU decision inside the float32 band may go either way
+        # (round 5 measured one on update 1: 2 elements of features_extractor.2.weight off by 2.2e-6)
+        w, ref = _assert_grads_relu(_grads(L), orc, sd_before, _f64(_sd(gr)), _batch(gd, k),
+                                    f"update {k} vs oracle (device's own parameters)")
+        worst, refs = max(worst, w), refs + [ref]
         _assert_apply_exact(L, p0, m0, v0, k + 1, f"update {k}")
+    _assert_final_sub(L, gd, refs)
     # targetB untouched (interval 2000), epsilon buffers unchanged
     sd = L.state_dict()
     assert torch.equal(L.target_state_dict()["lstm.weight_hh_l0"], _sd(gr)["lstm.weight_hh_l0"])
@@ -137,7 +210,8 @@ def test_drqn_against_oracle_ragged(golden, orc, B, T):
     np.testing.assert_allclose(L.stats()["loss"], info["loss"], rtol=1e-4)
     p0, m0, v0 = _snap(L)
     L.apply()  # the sigma gradients (mu gradient x epsilon) are formed after the all-reduce, in apply
-    _assert_grads(_grads(L), info["grads"], f"B={B} T={T}")
+    _assert_grads_relu(_grads(L), orc, {k: v.astype(np.float64) for k, v in sd.items()},
+                       {k: v.astype(np.float64) for k, v in tsd.items()}, (obs, act, rew, nxt, done), f"B={B} T={T}")
     _assert_apply_exact(L, p0, m0, v0, 1, f"B={B} T={T}")
 
 

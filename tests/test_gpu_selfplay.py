@@ -437,6 +437,34 @@ def test_production_step_equals_plain_at_full_size(golden):
     assert ca == cb and ca["train_steps"] == 20 and ca["size"] == 1_000_000
 
 
+def test_production_step_above_configs2_size(golden):
+    """Above configs[2]'s arena count (262 144: the side-A act blocks alone fill the chip, so the
+    feature blocks spread over the whole device) the production step still equals the
+    plain step bit for bit, and the learner launch stays in the tens of µs (the old fallback put
+    every feature tile on one block: ~8 000 tiles in series)."""
+    from pongmi import _lib
+    kw = dict(n=262144, batch=256, cap=1_000_000, seed=29, n_pool=8, target_update_interval=4)
+    A = _learner(golden, **kw)
+    B = _learner(golden, overlap=False, features_ahead=False, fuse_apply=False, **kw)
+    for _ in range(8):
+        A.step()
+        B.rollout()
+        B.learn()
+        B.apply()
+    torch.cuda.synchronize()
+    for name in ("paramsB", "paramsT", "adam_m", "adam_v", "prios", "trans", "f64", "i32", "opp", "w_B",
+                 "learn_heads", "per_work", "idx", "isw", "aB", "obsA", "obsB", "ep_reward"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    assert A.counters() == B.counters()
+    ts = []
+    for _ in range(5):
+        _lib.timer_arm(_lib.PM_TIMER_LEARN)
+        A.step()
+        ts.append(_lib.timer_read(_lib.PM_TIMER_LEARN))
+    print(f"k_learn at 262144 arenas: {min(ts) * 1e6:.1f} us")
+    assert min(ts) < 200e-6
+
+
 def test_features_ahead_is_bitwise_identical(golden):
     """modelB's feature layers computed a launch ahead (the learner launch's feature blocks -> featB,
     k_actenv evaluates the heads only) equal k_actenv's full forward bit for bit, also across a

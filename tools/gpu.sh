@@ -26,6 +26,10 @@
 #   roll       k_rollout16 per-step phase cycles (tools/roll_stamps.py, diag build)
 #   ab:VAR=v1,v2  tests/test_gpu_selfplay.py under each value, then the default bench interleaved twice
 #   drqnab:VAR=v1,v2  tests/test_gpu_drqn.py under v1, then tools/drqn_time.py interleaved three times
+#   k1sweep    K1 events + rocprofv3 kernel traces at 65 536 .. 4 194 304 arenas
+#   floorprof  tools/k1_floor under rocprofv3 (round 5 SIGSEGV check)
+#   train      bench.py --workload train (one config.yaml generation try, replay ratio 1)
+#   gpus2      bench.py --gpus 2 must refuse on a 1-GPU box
 #   pytest:<path>[::sel]  one test file / selection
 set -o pipefail
 export TMPDIR=/tmp
@@ -117,6 +121,24 @@ run_task() {
       done ;;
     roll)  # k_rollout16 per-step phase cycles (diag build)
       timeout -k 10 120 python3 tools/roll_stamps.py > gpurun_out/${tag}_roll_stamps.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_roll_stamps.txt ;;
+    k1sweep)  # K1's asymptote: events at 65 536 .. 4 194 304 arenas, then one rocprofv3
+              # kernel trace per size (the kernel outlasts the tracer's ~4.5 us launch period from 262 144 up)
+      timeout -k 10 240 python3 tools/k1_time.py 65536 262144 1048576 4194304 > gpurun_out/${tag}_k1_sweep.jsonl 2>&1 &&
+          grep -v amdgpu.ids gpurun_out/${tag}_k1_sweep.jsonl &&
+      for n in 65536 262144 1048576 4194304; do
+        timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_k1_$n -o k -- \
+            python3 tools/k1_time.py $n > gpurun_out/${tag}_prof_k1_$n.log 2>&1 || return 1
+      done && echo K1SWEEP_OK ;;
+    floorprof)  # tools/k1_floor under rocprofv3 once (round 5's SIGSEGV), fault mapping handler on
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_floor -o k -- \
+          ./tools/k1_floor 65536 > gpurun_out/${tag}_prof_floor.log 2>&1; rc=$?
+      grep -v amdgpu.ids gpurun_out/${tag}_prof_floor.log | tail -25; echo "k1_floor under rocprofv3 rc=$rc"; [ $rc -eq 0 ] ;;
+    train)  # one config.yaml generation try at replay ratio 1 (bench.py --workload train)
+      timeout -k 10 300 python3 bench.py --workload train > gpurun_out/${tag}_train.json 2> gpurun_out/${tag}_train.err &&
+          cat gpurun_out/${tag}_train.json && echo TRAIN_OK ;;
+    gpus2)  # bench.py --gpus 2 on a 1-GPU box must refuse (exit 2, an error line), never print a 1-rank line
+      timeout -k 10 120 python3 bench.py --gpus 2 --no-cpu-baseline > gpurun_out/${tag}_gpus2.json 2>&1; rc=$?
+      cat gpurun_out/${tag}_gpus2.json; [ $rc -eq 2 ] && echo GPUS2_REFUSED_OK ;;
     pytest:*)
       sel=${1#pytest:}
       timeout -k 10 400 $PYT "$sel" > gpurun_out/${tag}_pytest.log 2>&1 && tail -1 gpurun_out/${tag}_pytest.log ;;

@@ -10,8 +10,13 @@
 // Run it bare (graph events) and under rocprofv3 --kernel-trace --stats (per-launch durations).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/k1_floor.hip -o tools/k1_floor && ./tools/k1_floor [n]
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+#include <ucontext.h>
+#include <unistd.h>
 
 #define CK(x)                                                                                        \
     do {                                                                                             \
@@ -160,11 +165,47 @@ __global__ __launch_bounds__(256) void k_skel16(St s, int n) {
 
 typedef void (*Fn)(St, int);
 
+// Round 5 recorded one host-side SIGSEGV of this probe under rocprofv3 (the fault
+// address and PC were printed by the profiler's handler without the libraries they fall in). This
+// handler, installed after the profiler's, names them: the faulting PC and address with the
+// /proc/self/maps line each falls in (async-signal-safe: read + write only), then re-raises.
+static void map_line(unsigned long a, const char* what) {
+    char buf[1 << 16];
+    const int fd = open("/proc/self/maps", 0);
+    if (fd < 0) return;
+    long len = 0, r;
+    while (len < (long)sizeof(buf) - 1 && (r = read(fd, buf + len, sizeof(buf) - 1 - len)) > 0) len += r;
+    close(fd);
+    buf[len] = 0;
+    for (char* line = buf; line && *line;) {
+        char* nl = strchr(line, '\n');
+        if (nl) *nl = 0;
+        const unsigned long lo = strtoul(line, nullptr, 16), hi = strtoul(strchr(line, '-') + 1, nullptr, 16);
+        if (a >= lo && a < hi) {
+            write(2, what, strlen(what));
+            write(2, line, strlen(line));
+            write(2, "\n", 1);
+            return;
+        }
+        line = nl ? nl + 1 : nullptr;
+    }
+    write(2, what, strlen(what));
+    write(2, "(unmapped)\n", 11);
+}
+static void on_segv(int sig, siginfo_t* si, void* uc) {
+    const unsigned long pc = (unsigned long)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
+    map_line(pc, "k1_floor SIGSEGV pc in: ");
+    map_line((unsigned long)si->si_addr, "k1_floor SIGSEGV addr in: ");
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 static double graph_us(Fn fn, St s, int n, hipStream_t st, int per_graph = 50, int replays = 40, int warm = 100) {
     hipGraph_t g;
     hipGraphExec_t ge;
     CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
     for (int k = 0; k < per_graph; ++k) hipLaunchKernelGGL(fn, dim3((n + 255) / 256), dim3(256), 0, st, s, n);
+    CK(hipGetLastError());
     CK(hipStreamEndCapture(st, &g));
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     for (int k = 0; k < warm; ++k) CK(hipGraphLaunch(ge, st));
@@ -184,6 +225,12 @@ static double graph_us(Fn fn, St s, int n, hipStream_t st, int per_graph = 50, i
 
 int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 65536;
+    if (n <= 0 || n % 256) { fprintf(stderr, "n must be a positive multiple of 256\n"); return 2; }
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = on_segv;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, nullptr);
     St s;
     double* f;
     int* it;
@@ -220,5 +267,13 @@ int main(int argc, char** argv) {
                    n, rep, k.name, us, k.bytes, k.bytes / (us * 1e-6) / 8e12);
             fflush(stdout);
         }
+    // teardown (missing in round 5): drain, then release the stream and every buffer before exit
+    CK(hipStreamSynchronize(st));
+    CK(hipStreamDestroy(st));
+    CK(hipFree(s.done));
+    CK(hipFree(o));
+    CK(hipFree(acts));
+    CK(hipFree(it));
+    CK(hipFree(f));
     return 0;
 }

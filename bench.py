@@ -233,6 +233,42 @@ def time_act_full(L, launches=50):
             "timing": f"HIP events over {launches} back-to-back launches"}
 
 
+def time_scalar_dropin(seconds=1.0):
+    """The scalar drop-ins a reference script uses unchanged: configs[0]'s
+    loop — one PongEnv2P, random vs random (random.randint for A then B), reset on done — on
+    envs/my_pong_env_2p.py (one pm_env_step1 / pm_env_reset1 launch per call, results polled from
+    host-mapped memory), and envs/physics.py's scalar collide (one pm_collide1 launch per call).
+    Per-call wall time on this host; the reference's own Python step is 10.6 us."""
+    import random
+    from envs.my_pong_env_2p import PongEnv2P
+    from envs.physics import collide_sphere_with_moving_plane
+    env = PongEnv2P(**ENV_KW)
+    rng = random.Random(0)
+    for _ in range(200):
+        _, _, d, _ = env.step(rng.randint(0, 2), rng.randint(0, 2))
+        if d:
+            env.reset()
+    steps = resets = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        _, _, d, _ = env.step(rng.randint(0, 2), rng.randint(0, 2))
+        steps += 1
+        if d:
+            env.reset()
+            resets += 1
+    dt = time.perf_counter() - t0
+    k = 2000
+    t1 = time.perf_counter()
+    for j in range(k):
+        collide_sphere_with_moving_plane(-0.04, 0.01 * (j % 7), 0.03, 1.5, 1.0, 0.6, 1.0, 0.03)
+    dc = time.perf_counter() - t1
+    return {"env_us_per_step": round(dt / steps * 1e6, 2), "env_steps_per_s": round(steps / dt, 1), "steps": steps,
+            "resets": resets, "collide_us_per_call": round(dc / k * 1e6, 2),
+            "reference_python_us_per_step": 10.6,
+            "note": "PongEnv2P drop-in, random vs random with reset on done, wall time incl. the host's randint "
+                    "draws; one launch per step / reset, results polled from host-mapped memory"}
+
+
 def cpu_baseline(n, nets, seconds=12.0, epsilon=0.08):
     """The oracle's CPU port of the same vector step, acting with the GPU leg's nets (`nets` =
     bench_nets(...): modelB, modelA, pool, description) and its epsilon, so both legs play the same
@@ -1008,6 +1044,7 @@ def main():
         if world == 1:
             out["act_full_roofline"] = time_act_full(L)
             out["env_step_roofline"] = time_env_step(args.arenas)
+            out["scalar_dropin"] = time_scalar_dropin()
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline(args.arenas, nets, args.cpu_seconds)
                 out["cpu_config0"] = args.cpu_config0

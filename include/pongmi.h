@@ -100,6 +100,26 @@ int pm_env_step(const pm_env_params* p, const pm_env_state* s, const int8_t* aA,
  * (CPython's value); out [n][3] = (vn', vt', omega'). A test/diagnostic entry point. */
 int pm_collide(const double* in, const double* inertia, double* out, int32_t n, void* stream);
 
+/* The scalar drop-ins' fast path (ABI 23): one launch per call, no copy, no stream synchronisation.
+ * `out` is device-visible memory, normally a host-mapped buffer (pm_host_mapped_alloc) the host
+ * polls: the kernel writes its results, then `seq` into the 32-bit word after them with a
+ * system-scope release.
+ *   pm_env_step1  PongEnv2P.step (envs/my_pong_env_2p.py:116-225) of arena 0 of `s` with actions
+ *                 (aA, aB), no autoreset: out = obsA[7] obsB[7] rA rB done (f32), seq at word 17.
+ *                 Same tick as pm_env_step at n = 1, bit for bit.
+ *   pm_env_reset1 PongEnv2P.reset (:83-114) of arena 0 with the host-drawn serve (vx, vy, spin);
+ *                 serves[0] incremented: out = obsA[7] obsB[7] 0 0 0, seq at word 17.
+ *   pm_collide1   collide_sphere_with_moving_plane (envs/physics.py:3-23) of one row (vn, vt, u,
+ *                 omega, e, mu, m, R) with I = inertia: out = (vn', vt', omega') fp64, seq at word 6. */
+int pm_env_step1(const pm_env_params* p, const pm_env_state* s, int32_t aA, int32_t aB, float* out, uint32_t seq,
+                 void* stream);
+int pm_env_reset1(const pm_env_state* s, double vx, double vy, double spin, float* out, uint32_t seq, void* stream);
+int pm_collide1(const double* row, double inertia, double* out, uint32_t seq, void* stream);
+/* Pinned host memory the device reads and writes directly (hipHostMalloc, mapped + coherent):
+ * returns the host pointer (NULL on failure), *dev the device address of the same bytes. */
+void* pm_host_mapped_alloc(int64_t bytes, void** dev);
+int pm_host_mapped_free(void* host);
+
 /* ---------------------------------------------------------------- QNet (K2) */
 
 /* Packed QNet parameter block (models/qnet.py:52-69), PM_QNET_NP floats, in this order:
@@ -460,7 +480,9 @@ typedef struct pm_ctrl {
                                 bit 1: an update scattered a NaN priority (a diverged loss: its PER
                                 leaf is 0, never sampled; the reference's np.random.choice raises);
                                 bit 2: k_learn's tree-refresh block never received the learner's
-                                priorities (bounded poll): the sum tree was left stale */
+                                priorities (bounded poll): the sum tree was left stale, until
+                                pm_selfplay_repair_tree rebuilds it (bit 2 -> bit 3);
+                                bit 3: a stale tree was repaired (informational: state consistent) */
     int32_t max_bits;        /* pm_selfplay_commit scratch: float bits of max(prios); 0 between steps */
 } pm_ctrl;
 
@@ -547,6 +569,10 @@ int pm_selfplay_init(const pm_selfplay* sp, void* stream);
  * parameters, priorities or replay counters (checkpoint load, reset_B, promotion). Called by
  * pm_selfplay_init. */
 int pm_selfplay_prepare(const pm_selfplay* sp, void* stream);
+/* After ctrl.status bit 2 (a tree-refresh timeout): full rebuild of the PER sum tree from prios + ctrl,
+ * then status bit 2 -> bit 3 (ABI 23). Test hook: PONGMI_TR_FORCE_TIMEOUT=1 makes the refresh block's
+ * poll time out at once. */
+int pm_selfplay_repair_tree(const pm_selfplay* sp, void* stream);
 int pm_selfplay_rollout(const pm_selfplay* sp, void* stream); /* = pm_selfplay_act + pm_selfplay_env */
 int pm_selfplay_act(const pm_selfplay* sp, void* stream);     /* actions -> sp->aA/aB; PER sample    */
 int pm_selfplay_env(const pm_selfplay* sp, void* stream);     /* tick + push + bookkeeping + serves   */

@@ -75,10 +75,13 @@ namespace pm {
 // ----------------------------------------------------------------------------- wave reductions
 // A wave's butterfly reduction `for (o = 32; o; o >>= 1) v = op(v, __shfl_xor(v, o))` on the DPP
 // and scalar paths instead of six ds_bpermute round trips (~2 us for six int64 chains in the learner's
-// phase 0). Bit-identical for a commutative op: after the xor-1 / xor-2 steps (quad_perm) every quad
-// holds one value, so the half-row / row mirrors pair each lane with a lane holding its xor-4 / xor-8
-// partner's value; the last two steps are (a0 + a16) + (a32 + a48) from four readlanes, which every
-// lane of the butterfly ends with too. Full waves only (every lane active). Result wave-uniform.
+// phase 0). After the xor-1 / xor-2 steps (quad_perm) every quad holds one value, so the half-row /
+// row mirrors pair each lane with a lane holding its xor-4 / xor-8 partner's value; the last two steps
+// are (a0 + a16) + (a32 + a48) from four readlanes. The pairing runs xor-1 first, the reverse of the
+// loop above (xor-32 first), so the result equals the loop's bit for bit only for an associative op
+// (integer sums, max, min); a float sum is the same 63 additions in a different association (ADVICE
+// r5) and is covered by the tolerance tests of its callers, not by bit-identity. Full waves only
+// (every lane active). Result wave-uniform.
 template <int CTRL>
 __device__ __forceinline__ int dpp_i32(int v) {
     return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);

@@ -903,7 +903,7 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
                 }
             }
             if (a.local_norm) {
-                sq = wave_sum(sq);  // the xor butterfly's value, on DPP (pm_dev.h)
+                sq = wave_sum(sq);  // DPP reduction (pm_dev.h): xor-1-first association of the fp64 sum
                 if (lane == 0) a.NP[bid] = sq;
             }
         }

@@ -4,6 +4,7 @@
 // bounces 12 read + write, actions 2, obs 56, rewards 8, done 1). Observations leave the kernel
 // through an LDS transpose so every store is a full 16-byte-per-lane coalesced write.
 #include <stdlib.h>
+#include <string.h>
 
 #include "pm_dev.h"
 #include "pm_host.h"
@@ -207,6 +208,52 @@ __global__ __launch_bounds__(kBlock) void k_collide(const double* __restrict__ i
     out[(size_t)i * 3 + 2] = om2;
 }
 
+// The scalar drop-in's fast path (PongEnv2P, one arena: envs/my_pong_env_2p.py:83-225). One lane
+// steps / serves arena 0 with the same tick / serve / observe as K1 (so its results are K1's for
+// n = 1 bit for bit), writes obsA[7] obsB[7] rA rB done to `out` and then `seq` to out word 17 with
+// a system-scope release: `out` is normally host-mapped memory (pm_host_mapped_alloc), which the
+// host polls, so one call costs one launch and no copy or stream synchronisation.
+__device__ __forceinline__ void emit1(float* out, const float (&oA)[7], const float (&oB)[7], float ra, float rb,
+                                      float dn, uint32_t seq) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { out[k] = oA[k]; out[7 + k] = oB[k]; }
+    out[14] = ra; out[15] = rb; out[16] = dn;
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(out + 17), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ __launch_bounds__(64) void k_env_step1(pm_env_params p, pm_env_state s, int xa, int xb, float* out,
+                                                  uint32_t seq) {
+    if (threadIdx.x != 0) return;
+    Arena a = load_arena(s, 0);
+    float ra, rb, oA[7], oB[7];
+    const int d = tick(p, a, xa, xb, ra, rb);
+    store_arena(s, 0, a);
+    observe(a, oA, oB);
+    emit1(out, oA, oB, ra, rb, (float)d, seq);
+}
+__global__ __launch_bounds__(64) void k_env_reset1(pm_env_state s, double vx, double vy, double spin, float* out,
+                                                   uint32_t seq) {
+    if (threadIdx.x != 0) return;
+    Arena a;
+    serve(a, vx, vy, spin);
+    store_arena(s, 0, a);
+    s.serves[0] = s.serves[0] + 1;
+    float oA[7], oB[7];
+    observe(a, oA, oB);
+    emit1(out, oA, oB, 0.f, 0.f, 0.f, seq);
+}
+__global__ __launch_bounds__(64) void k_collide1(double vn, double vt, double u, double om, double e, double mu,
+                                                 double m, double R, double inertia, double* out, uint32_t seq) {
+    if (threadIdx.x != 0) return;
+    pm_env_params p = {};
+    p.restitution = e; p.friction = mu; p.ball_mass = m; p.radius = R;
+    p.inertia = inertia;
+    p.jt_coef = (2.0 * m) / 7.0;
+    p.inv_mass = 1.0 / m;
+    p.inv_inertia = 1.0 / inertia;
+    collide(p, vn, vt, u, om, out[0], out[1], out[2]);
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(out + 3), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Write-through K1 outputs up to kK1WtMax arenas (latency-bound sizes); PONGMI_K1_WT=0/1 forces
 // the choice (experiments).
 constexpr int32_t kK1WtMax = 131072;
@@ -279,6 +326,50 @@ extern "C" int pm_env_step(const pm_env_params* p, const pm_env_state* s, const 
               inject_cap, seed, counter, status, n);
     PM_LAUNCHED("k_env_step");
     return PM_OK;
+}
+
+extern "C" int pm_env_step1(const pm_env_params* p, const pm_env_state* s, int32_t aA, int32_t aB, float* out,
+                            uint32_t seq, void* stream) {
+    PM_REQUIRE(p && state_ok(s) && out, PM_E_ARG, "pm_env_step1: null params/state/out");
+    PM_REQUIRE(aA >= 0 && aA <= 2 && aB >= 0 && aB <= 2, PM_E_ARG, "pm_env_step1: actions (%d, %d)", aA, aB);
+    PM_REQUIRE(p->speed_scale_every > 0, PM_E_ARG, "pm_env_step1: speed_scale_every must be > 0");
+    hipLaunchKernelGGL(k_env_step1, dim3(1), dim3(64), 0, pm_stream(stream), *p, *s, (int)aA, (int)aB, out, seq);
+    PM_LAUNCHED("k_env_step1");
+    return PM_OK;
+}
+
+extern "C" int pm_env_reset1(const pm_env_state* s, double vx, double vy, double spin, float* out, uint32_t seq,
+                             void* stream) {
+    PM_REQUIRE(state_ok(s) && out, PM_E_ARG, "pm_env_reset1: null state/out");
+    hipLaunchKernelGGL(k_env_reset1, dim3(1), dim3(64), 0, pm_stream(stream), *s, vx, vy, spin, out, seq);
+    PM_LAUNCHED("k_env_reset1");
+    return PM_OK;
+}
+
+extern "C" int pm_collide1(const double* row, double inertia, double* out, uint32_t seq, void* stream) {
+    PM_REQUIRE(row && out, PM_E_ARG, "pm_collide1: null row/out");
+    hipLaunchKernelGGL(k_collide1, dim3(1), dim3(64), 0, pm_stream(stream), row[0], row[1], row[2], row[3], row[4],
+                       row[5], row[6], row[7], inertia, out, seq);
+    PM_LAUNCHED("k_collide1");
+    return PM_OK;
+}
+
+extern "C" void* pm_host_mapped_alloc(int64_t bytes, void** dev) {
+    void* h = nullptr;
+    if (bytes <= 0 || !dev) return nullptr;
+    if (hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    memset(h, 0, (size_t)bytes);
+    if (hipHostGetDevicePointer(dev, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return nullptr;
+    }
+    return h;
+}
+
+extern "C" int pm_host_mapped_free(void* host) {
+    if (!host) return PM_OK;
+    const hipError_t e = hipHostFree(host);
+    return e == hipSuccess ? PM_OK : pm_fail((int)e, "pm_host_mapped_free: %s", hipGetErrorString(e));
 }
 
 #ifdef PM_DIAG

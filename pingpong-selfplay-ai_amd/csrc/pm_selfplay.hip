@@ -988,6 +988,7 @@ constexpr int kTrHash = 1024;                // open-addressing sets keyed by no
 constexpr uint32_t kTrEmpty = 0xFFFFFFFFu;
 constexpr int kTrPollMax = 20000;
 constexpr int PM_CTRL_TREE_TIMEOUT = 4;
+constexpr int PM_CTRL_TREE_REPAIRED = 8;  // a stale tree was rebuilt by pm_selfplay_repair_tree
 struct TreeRefreshSmem {
     __attribute__((aligned(16))) float lf[kTrSlots][PER_SUB];   // leaves of every level-1 slot (LDS DMA)
     __attribute__((aligned(16))) double ls[kTrSlots][PER_FAN];  // level-1 nodes of every level-2 slot (LDS DMA)
@@ -1031,7 +1032,8 @@ __device__ __forceinline__ int tr_lookup(const uint32_t* key, uint32_t k, int bi
     }
 }
 
-__device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, TreeRefreshSmem& sm, const pm_ctrl& cs) {
+__device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, TreeRefreshSmem& sm, const pm_ctrl& cs,
+                                           int poll_max) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
     PM_STAMP_ANY(55);
     const PerTree tree = per_tree(sp.per_work, sp.cap);
@@ -1093,7 +1095,7 @@ __device__ __forceinline__ void tree_block(const pm_selfplay& sp, int mode, Tree
     if (t < B + 2) {
         uint64_t g = 0;
         bool got = false;
-        for (int it = 0; it < kTrPollMax; ++it) {
+        for (int it = 0; it < poll_max; ++it) {
             g = __hip_atomic_load(tr_granules(sp) + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((uint32_t)(g >> 32) == tag) { got = true; break; }
             __builtin_amdgcn_s_sleep(2);
@@ -1258,6 +1260,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
     __shared__ __attribute__((aligned(16))) LearnShared shm;
     // tr: bit 0 the tree-refresh block, bit 1 push_rows_fwd2, bit 2 the apply's noise in phase 2
     const bool push2 = (tr & 2) != 0, late_noise = (tr & 4) != 0;
+    const int tr_poll = (tr & 16) ? 0 : kTrPollMax;  // bit 4: test hook, the refresh block's poll times out at once
     constexpr bool pushg = PG;
     tr &= 1;
     if (blockIdx.x > 0) {
@@ -1265,7 +1268,7 @@ __global__ __launch_bounds__(kLearn) void k_learn(const pm_selfplay sp, int chun
             const pm_ctrl cs = push_fwd_block(sp, mode, shm.pf, push2, pushg);
             if (tr) {
                 __syncthreads();  // the push rows' LDS is reused
-                tree_block(sp, mode, shm.tr, cs);
+                tree_block(sp, mode, shm.tr, cs, tr_poll);
             }
             return;
         }
@@ -2441,6 +2444,26 @@ extern "C" int pm_selfplay_prepare(const pm_selfplay* sp, void* stream) {
     return per_launch_build(sp->prios, sp->cap, (float)sp->alpha, sp->ctrl, sp->n, sp->per_work, st);
 }
 
+namespace {
+__global__ void k_tree_repaired(pm_ctrl* c) {
+    if (threadIdx.x == 0 && (c->status & PM_CTRL_TREE_TIMEOUT))
+        c->status = (c->status & ~PM_CTRL_TREE_TIMEOUT) | PM_CTRL_TREE_REPAIRED;
+}
+}  // namespace
+
+// After a tree-refresh timeout (ctrl.status bit 2: the sums disagree with the leaves the learner
+// scattered): a full rebuild of the PER sum tree from prios + ctrl (the pending push substituted, as
+// pm_selfplay_prepare), then status bit 2 -> bit 3. Nothing else is re-derived.
+extern "C" int pm_selfplay_repair_tree(const pm_selfplay* sp, void* stream) {
+    int rc = check(sp);
+    if (rc) return rc;
+    hipStream_t st = pm_stream(stream);
+    if ((rc = per_launch_build(sp->prios, sp->cap, (float)sp->alpha, sp->ctrl, sp->n, sp->per_work, st))) return rc;
+    hipLaunchKernelGGL(k_tree_repaired, dim3(1), dim3(64), 0, st, sp->ctrl);
+    PM_LAUNCHED("k_tree_repaired");
+    return PM_OK;
+}
+
 extern "C" int pm_selfplay_init(const pm_selfplay* sp, void* stream) {
     int rc = check(sp);
     if (rc) return rc;
@@ -2547,7 +2570,8 @@ int tree_refresh_block() {
         const char* g = getenv("PONGMI_PUSHG");  // push rows as tagged granules (default 1; needs TR and PUSH2)
         const int tr = e && *e ? (atoi(e) != 0) : 1, p2 = p && *p ? (atoi(p) != 0) : 1;
         const int pg = (g && *g ? (atoi(g) != 0) : 1) && tr && p2;
-        return tr | (p2 << 1) | ((q && *q ? (atoi(q) != 0) : 1) << 2) | (pg << 3);
+        const char* f = getenv("PONGMI_TR_FORCE_TIMEOUT");  // test hook: block 1's granule poll times out
+        return tr | (p2 << 1) | ((q && *q ? (atoi(q) != 0) : 1) << 2) | (pg << 3) | ((f && *f && atoi(f) != 0) << 4);
     }();
     return v;
 }

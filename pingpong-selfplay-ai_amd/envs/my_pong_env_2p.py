@@ -9,15 +9,19 @@ pm_env_reset / pm_env_step kernels). The scalar API is the reference's:
 
 Serves are drawn on the host from the global `random` module with the reference's own draw order
 and expressions (:94-110) and handed to the kernel, so a script that seeds `random` sees the
-reference's trajectories bit for bit. The readable attributes (ball_x, ..., bounce_count) are
+reference's trajectories bit for bit. Each reset() / step() is ONE launch (pm_env_reset1 /
+pm_env_step1: actions and serve as kernel arguments, results written straight into a host-mapped
+buffer the host polls), with no host-to-device copy, no device-to-host copy and no stream
+synchronisation: the same tick as pm_env_step at n = 1, bit for bit. The readable attributes (ball_x, ..., bounce_count) are
 fetched from the device on access. render() (:265-306) draws the reference's scene through
 pongmi.viewer.ArenaView; pygame is imported lazily, only when enable_render=True.
 """
+import ctypes
 import random
 
 import numpy as np
-import torch
 
+from pongmi import _lib
 from pongmi.env import PongEnv2PBatch, draw_serve, env_config
 
 _STATE_F64 = ("ball_x", "ball_y", "ball_vx", "ball_vy", "spin", "top_paddle_x", "bottom_paddle_x")
@@ -54,8 +58,9 @@ class PongEnv2P:
         low = np.array([0, 0, -1, -1, 0, 0, -10], dtype=np.float32)
         high = np.array([1, 1, 1, 1, 1, 1, 10], dtype=np.float32)
         self.observation_space = _Spaces.Box(low, high, dtype=np.float32)
-        self._serve = np.zeros((1, 1, 3), np.float64)
-        self._env = PongEnv2PBatch(1, device=device, serve_table=self._serve, **{k: v for k, v in kw.items()})
+        self._env = PongEnv2PBatch(1, device=device, **{k: v for k, v in kw.items()})
+        self._lib = _lib.load()
+        self._slot = _lib.MappedSlot(18, 17)  # obsA[7] obsB[7] rA rB done | seq
         self._host = None
         if enable_render:
             import pygame  # noqa: F401  (viewer only; not part of the device path)
@@ -63,20 +68,27 @@ class PongEnv2P:
 
     # ------------------------------------------------------------------ reference API
     def reset(self, seed=None, options=None):
-        self._serve[0, 0] = draw_serve(random, self._cfg)  # 4 draws from the global stream (:94-110)
-        self._env.set_serve_table(self._serve)
+        vx, vy, spin = draw_serve(random, self._cfg)  # 4 draws from the global stream (:94-110)
         self.spin_angle = 0.0
-        oA, oB = self._env.reset()
+        slot = self._slot
+        _lib.check(self._lib.pm_env_reset1(ctypes.byref(self._env.state), vx, vy, spin, slot.dev, slot.next_seq(),
+                                           _lib.stream_ptr()), "pm_env_reset1")
         self._host = None
-        return oA[0].cpu().numpy(), oB[0].cpu().numpy()
+        slot.wait()
+        out = slot.floats(0, 14)
+        return out[0:7], out[7:14]
 
     def step(self, actionA, actionB):
-        aA = torch.tensor([int(actionA)], dtype=torch.int8)
-        aB = torch.tensor([int(actionB)], dtype=torch.int8)
-        (oA, oB), (rA, rB), done, _ = self._env.step(aA, aB)
+        aA, aB = int(actionA), int(actionB)
+        if not (0 <= aA <= 2 and 0 <= aB <= 2):
+            raise ValueError(f"actions must be in {{0, 1, 2}}, got ({actionA}, {actionB})")
+        slot = self._slot
+        _lib.check(self._lib.pm_env_step1(ctypes.byref(self._env.params), ctypes.byref(self._env.state), aA, aB,
+                                          slot.dev, slot.next_seq(), _lib.stream_ptr()), "pm_env_step1")
         self._host = None
-        out = torch.cat([oA[0], oB[0], rA, rB, done.float()]).cpu().numpy()
-        return (out[0:7].copy(), out[7:14].copy()), (float(out[14]), float(out[15])), bool(out[16]), {}
+        slot.wait()
+        out = slot.floats(0, 17)
+        return (out[0:7], out[7:14]), (float(out[14]), float(out[15])), bool(out[16]), {}
 
     def _get_obs(self):
         st = self._state()

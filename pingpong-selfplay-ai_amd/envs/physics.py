@@ -2,7 +2,9 @@
 
 The collision runs on the device through libpongmi (pm_collide, the same fp64 device function
 every env tick uses). `collide_batch` evaluates many rows in one launch; the scalar entry point
-keeps the reference signature (one launch + one host round trip per call)."""
+keeps the reference signature (one launch per call, the result read from host-mapped memory)."""
+import ctypes
+
 import numpy as np
 import torch
 
@@ -21,6 +23,18 @@ def collide_batch(rows, device="cuda"):
     return out.cpu().numpy()
 
 
+_slot = None
+
+
 def collide_sphere_with_moving_plane(vn, vt, u, omega, e, mu, m, R):
-    vn2, vt2, om2 = collide_batch([[vn, vt, u, omega, e, mu, m, R]])[0]
+    """One launch (pm_collide1: the row as kernel arguments, the result written into a host-mapped
+    buffer the host polls), no copies, no stream synchronisation."""
+    global _slot
+    if _slot is None:
+        _slot = _lib.MappedSlot(8, 6)  # vn' vt' omega' (fp64) | seq
+    row = (ctypes.c_double * 8)(vn, vt, u, omega, e, mu, m, R)
+    inertia = (2 / 5) * m * R ** 2  # CPython's I (:9)
+    _lib.check(_lib.load().pm_collide1(row, inertia, _slot.dev, _slot.next_seq(), _lib.stream_ptr()), "pm_collide1")
+    _slot.wait()
+    vn2, vt2, om2 = _slot.doubles(0, 3)
     return float(vn2), float(vt2), float(om2)

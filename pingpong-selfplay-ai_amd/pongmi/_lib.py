@@ -10,6 +10,8 @@ initialised, so device pointers and streams are shared.
 import ctypes
 import os
 
+import numpy as np
+
 import torch  # noqa: F401  (load order: see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -119,6 +121,11 @@ _SIGS = {
     "pm_env_step": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_u64, c_u64, c_void_p, c_i32, c_void_p]),
     "pm_collide": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
+    "pm_env_step1": (c_i32, [c_void_p, c_void_p, c_i32, c_i32, c_void_p, ctypes.c_uint32, c_void_p]),
+    "pm_env_reset1": (c_i32, [c_void_p, c_double, c_double, c_double, c_void_p, ctypes.c_uint32, c_void_p]),
+    "pm_collide1": (c_i32, [c_void_p, c_double, c_void_p, ctypes.c_uint32, c_void_p]),
+    "pm_host_mapped_alloc": (c_void_p, [ctypes.c_int64, ctypes.POINTER(c_void_p)]),
+    "pm_host_mapped_free": (c_i32, [c_void_p]),
     "pm_qnet_fold": (c_i32, [c_void_p, c_void_p, c_i32, c_u64, c_u64, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_qnet_q": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_qnet_act": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64,
@@ -153,6 +160,7 @@ _SIGS = {
     "pm_per_update": (c_i32, [c_void_p, c_void_p, c_void_p, c_i32, c_void_p]),
     "pm_selfplay_init": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_prepare": (c_i32, [c_void_p, c_void_p]),
+    "pm_selfplay_repair_tree": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_rollout": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_act": (c_i32, [c_void_p, c_void_p]),
     "pm_selfplay_env": (c_i32, [c_void_p, c_void_p]),
@@ -228,6 +236,56 @@ def timer_read(kernel):
     ms = c_float()
     check(load().pm_timer_read(int(kernel), ctypes.byref(ms)), "pm_timer_read")
     return ms.value * 1e-3
+
+
+class MappedSlot:
+    """A small host-mapped buffer (pm_host_mapped_alloc) for the scalar drop-ins' one-launch calls:
+    the kernel writes its results and then a sequence number into the word after them; wait()
+    polls that word (bounded: after `timeout` s it synchronises the stream and raises)."""
+
+    def __init__(self, nwords, seq_word):
+        self.lib = load()
+        dev = c_void_p()
+        self.host = self.lib.pm_host_mapped_alloc(4 * int(nwords), ctypes.byref(dev))
+        if not self.host:
+            raise PongmiError("pm_host_mapped_alloc failed")
+        self.dev = dev.value
+        self.words = (ctypes.c_uint32 * int(nwords)).from_address(self.host)
+        self.seq_word = int(seq_word)
+        self.seq = 0
+
+    def next_seq(self):
+        self.seq = (self.seq + 1) & 0xFFFFFFFF or 1
+        return self.seq
+
+    def wait(self, timeout=5.0):
+        w, k, want = self.words, self.seq_word, self.seq
+        for _ in range(2000):
+            if w[k] == want:
+                return
+        import time
+        t0 = time.perf_counter()
+        while w[k] != want:
+            if time.perf_counter() - t0 > timeout:
+                import torch
+                torch.cuda.synchronize()
+                if w[k] != want:
+                    raise PongmiError("scalar drop-in: the device never published its result")
+                return
+
+    def floats(self, lo, hi):
+        return np.frombuffer((ctypes.c_float * (hi - lo)).from_address(self.host + 4 * lo), np.float32).copy()
+
+    def doubles(self, lo, hi):
+        return np.frombuffer((ctypes.c_double * (hi - lo)).from_address(self.host + 8 * lo), np.float64).copy()
+
+    def __del__(self):
+        try:
+            if self.host:
+                self.lib.pm_host_mapped_free(self.host)
+                self.host = None
+        except Exception:
+            pass
 
 
 def check(rc, what=""):

@@ -79,6 +79,8 @@ def _play_episodes(L, episodes, progress, check_every, on_check=None, step=None)
         for _ in range(check_every):
             step()
         c = L.counters()
+        if hasattr(L, "repair_tree") and L.repair_tree(c):  # a tree-refresh timeout: rebuild the stale sums
+            c = L.counters()
         progress.tick(c)
         if on_check:
             on_check(c)

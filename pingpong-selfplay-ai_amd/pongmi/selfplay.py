@@ -303,11 +303,21 @@ class SelfPlayLearner:
         timed out (its push rows were not computed: that update is void); bit 1 = an update scattered
         a NaN priority (the loss diverged; the reference's sampler would raise on the NaN
         probabilities); bit 2 = k_learn's tree-refresh block timed out waiting for the learner (the
-        sum tree is stale). Raises on any bit."""
-        st = int((c or self.counters())["status"])
+        sum tree is stale until repair_tree). Raises on any of them; bit 3 (a stale tree was
+        repaired) is informational."""
+        st = int((c or self.counters())["status"]) & 7
         if st:
             raise _lib.PongmiError(f"self-play learner: device status {st} (bit 0: push-row hand-off timed out; "
                                    f"bit 1: NaN priority scattered; bit 2: tree refresh timed out)")
+
+    def repair_tree(self, c=None):
+        """If a tree-refresh timeout left the PER sum tree stale (status bit 2), rebuild it from the
+        priorities (pm_selfplay_repair_tree: bit 2 -> bit 3). Returns whether it did. The generation
+        controllers call it at every episode check (pongmi.generations._play_episodes)."""
+        if not int((c or self.counters())["status"]) & 4:
+            return False
+        check(self.lib.pm_selfplay_repair_tree(ctypes.byref(self.sp), stream_ptr()), "pm_selfplay_repair_tree")
+        return True
 
     def set_epsilon(self, eps):
         c = _lib.Ctrl.from_buffer_copy(bytes(self.ctrl.cpu().numpy().tobytes()))

@@ -5,10 +5,11 @@ Tolerances (fp32 on the device; exact-f32 MFMA sums in a different order than to
 loss / pre-clip norm rtol 1e-4; gradients rtol 5e-4 with atol 1e-5 x the tensor's largest magnitude
 (round 5: the kernel's measured worst was 0.40 of the round-4 bar of rtol 1e-3), every update, every
 tensor. The one exemption is targeted (_assert_grads_relu): an obs-stream ReLU whose pre-activation
-is within float32 rounding of 0 (|p| <= 64 * 2^-24 * sum|terms|, oracle.drqn_grads' relu_band) is a
-rounding decision the device may take the other way, so the device's gradient must equal, at the
-same bar, the oracle's gradient with SOME subset of those decisions flipped (the empty subset first);
-the decisions flipped and the elements whose reference they change are printed. Parameters are
+is close to 0 relative to its float32 error scale (the 12 closest, |p| / (2^-24 sum|terms|), oracle
+.drqn_grads' relu_band) is a decision the f32 device may take the other way, so the device's
+gradient must equal, at the same bar, the oracle's gradient with some subset of at most 3 of those
+decisions flipped (the empty subset first); the decisions flipped, their margins and the elements
+whose reference they change are printed. Parameters are
 pinned by composition, with no sign band: every update's gradient is checked against the oracle run
 from the device's OWN pre-update parameters (so Adam's sign-of-rounding cannot drift the two apart),
 and clip + Adam given that gradient and the device's pre-clip norm is checked bit for bit against
@@ -17,6 +18,7 @@ parameters after the three fixture updates are also compared with the reference'
 (final_sub.*) under the sign band that Adam's normalised step needs there (_assert_final_sub).
 """
 import itertools
+import os
 
 import numpy as np
 import pytest
@@ -64,33 +66,44 @@ def _grad_err(got, ref, atol_rel=1e-5):
     return worst
 
 
-RELU_BAND = 64.0  # |p| <= RELU_BAND * 2^-24 * sum|terms|: the ReLU decision is a float32 rounding decision
-MAX_SITES = 10
+RELU_BAND = 1024.0  # |p| <= RELU_BAND * 2^-24 * sum|terms|: candidates for a float32 rounding decision
+MAX_SITES, MAX_FLIPS = 12, 3
 
 
 def _assert_grads_relu(got, orc, sd, tsd, batch, what):
     """The device's gradient vs the float64 oracle at the full bar (atol 1e-5 max|g|), where the
-    oracle takes the device's side at each ReLU decision inside the float32 rounding band: subsets of
-    the band's decisions (the MAX_SITES closest to 0) are tried smallest first, and the first whose
-    flipped oracle gradient meets the bar is the one checked. Prints the band, the decisions the
-    device took the other way and, per tensor, the elements whose reference that moved by >= 0.1 x
-    the atol (the exempt elements: outside them the plain reference and the flipped one agree)."""
+    oracle may take the device's side at up to MAX_FLIPS ReLU decisions near 0: the MAX_SITES
+    pre-activations closest to 0 relative to their float32 error scale (|p| / (2^-24 sum|terms|),
+    oracle.drqn_grads' relu_band) are the candidates; subsets are tried smallest first (the empty one
+    first), screened with the sum of the single flips' gradient changes and confirmed by an exact
+    oracle run with that subset flipped. Prints the candidates' margins, the decisions the device
+    took the other way with theirs, and per tensor the elements whose reference that moved by >= 0.1
+    x the atol (the exempt elements: everywhere else the plain reference applies unchanged).
+    Round 5 measured one such decision on update 1: 2 elements of features_extractor.2.weight off by
+    2.2e-6 (a layer-2 unit of a (t, b) whose layer-1 features have 2 nonzero entries)."""
     info = orc.drqn_grads(sd, tsd, *batch, relu_band=RELU_BAND)
     order = np.argsort(info["margins"], kind="stable")[:MAX_SITES]
     sites = [info["sites"][i] for i in order]
+    margin = {info["sites"][i]: info["margins"][i] for i in order}
     ref, flipped = info["grads"], ()
     if _grad_err(got, ref) > 1.0:
-        for r in range(1, len(sites) + 1):
-            hit = next((c for c in itertools.combinations(sites, r)
-                        if _grad_err(got, g := orc.drqn_grads(sd, tsd, *batch, flip=c)["grads"]) <= 1.0), None)
-            if hit is not None:
-                ref, flipped = g, hit
+        delta = [{k: v - ref[k] for k, v in orc.drqn_grads(sd, tsd, *batch, flip=(s,))["grads"].items()} for s in sites]
+        for r in range(1, min(MAX_FLIPS, len(sites)) + 1):
+            for c in itertools.combinations(range(len(sites)), r):
+                approx = {k: ref[k] + sum(delta[i][k] for i in c) for k in ref}
+                if _grad_err(got, approx) <= 1.0:
+                    g = orc.drqn_grads(sd, tsd, *batch, flip=tuple(sites[i] for i in c))["grads"]
+                    if _grad_err(got, g) <= 1.0:
+                        ref, flipped = g, tuple(sites[i] for i in c)
+                        break
+            if flipped:
                 break
     exempt = {k: int(np.sum(np.abs(ref[k] - info["grads"][k]) >= 0.1 * (1e-5 * np.abs(info["grads"][k]).max())))
               for k in ref}
-    print(f"\n{what}: {len(info['sites'])} ReLU decisions in the float32 band (margins "
-          f"{[round(info['margins'][i], 1) for i in order]}); the device took the other side at {len(flipped)}: "
-          f"{list(flipped)}; exempt elements {({k: v for k, v in exempt.items() if v}) or 0}")
+    print(f"\n{what}: {len(info['sites'])} ReLU pre-activations within {RELU_BAND:g} x their float32 error scale "
+          f"(closest margins {[round(margin[s], 1) for s in sites]}); the device took the other side at "
+          f"{len(flipped)}: {[(s, round(margin[s], 1)) for s in flipped]}; exempt elements "
+          f"{({k: v for k, v in exempt.items() if v}) or 0}")
     return _assert_grads(got, ref, what), ref
 
 
@@ -174,6 +187,11 @@ def test_drqn_update_matches_reference(golden, orc):
                           "update 0 vs autograd")
         # every update at the full bar; a ReLU decision inside the float32 band may go either way
         # (round 5 measured one on update 1: 2 elements of features_extractor.2.weight off by 2.2e-6)
+        dump = os.environ.get("PONGMI_DRQN_DUMP")  # diagnosis: the device's parameters and gradient per update
+        if dump:
+            os.makedirs(dump, exist_ok=True)
+            np.savez(os.path.join(dump, f"drqn_u{k}.npz"), **{"p." + n: v for n, v in sd_before.items()},
+                     **{"g." + n: v for n, v in _grads(L).items()})
         w, ref = _assert_grads_relu(_grads(L), orc, sd_before, _f64(_sd(gr)), _batch(gd, k),
                                     f"update {k} vs oracle (device's own parameters)")
         worst, refs = max(worst, w), refs + [ref]

@@ -225,3 +225,45 @@ def test_collide_kat_bit_exact(golden):
     got = out.cpu().numpy()
     assert np.array_equal(got, g["outputs"])
     assert np.array_equal(np.signbit(got), np.signbit(g["outputs"]))
+
+
+def test_scalar_dropin_matches_reference_trajectories_bit_exact(golden):
+    """The scalar drop-in (envs/my_pong_env_2p.py PongEnv2P: one pm_env_reset1 / pm_env_step1 launch
+    per call, results read from host-mapped memory) replays the reference's own runs exactly as
+    make_golden.py recorded them: random.seed(seed_i), construct (one reset), then the recorded
+    actions with reset() on done — every observation, reward, done flag and fp64 state word."""
+    import random
+    from envs.my_pong_env_2p import PongEnv2P
+
+    g = golden("env_cfg")
+    kw, _ = _kwargs_from_golden(g)
+    n, T = g["actA"].shape
+    for i in range(min(n, 6)):
+        random.seed(int(g["seeds"][i]))
+        env = PongEnv2P(**kw)
+        assert np.array_equal(_state_matrix(env._env)[0], g["init"][i])
+        oA, oB = env._get_obs()
+        assert np.array_equal(oA, g["init_obs"][i, 0]) and np.array_equal(oB, g["init_obs"][i, 1])
+        for t in range(T):
+            (nA, nB), (rA, rB), d, info = env.step(int(g["actA"][i, t]), int(g["actB"][i, t]))
+            assert info == {} and isinstance(d, bool)
+            assert np.array_equal(nA, g["obsA"][i, t]) and np.array_equal(nB, g["obsB"][i, t]), (i, t)
+            assert (rA, rB) == tuple(g["rew"][i, t].tolist()) and d == bool(g["done"][i, t]), (i, t)
+            assert np.array_equal(_state_matrix(env._env)[0], g["state"][i, t]), (i, t)
+            if d:
+                oA, oB = env.reset()
+                assert np.array_equal(oA, g["reset_obs"][i, t, 0]) and np.array_equal(oB, g["reset_obs"][i, t, 1])
+                assert np.array_equal(_state_matrix(env._env)[0], g["reset_state"][i, t]), (i, t)
+    with pytest.raises(ValueError):
+        env.step(3, 0)
+
+
+def test_scalar_collide_dropin_kat_bit_exact(golden):
+    """envs/physics.py collide_sphere_with_moving_plane (pm_collide1, one launch per call) on the
+    reference's collision known-answer table: bit-exact, signed zeros included."""
+    from envs.physics import collide_sphere_with_moving_plane
+
+    g = golden("collide_kat")
+    got = np.array([collide_sphere_with_moving_plane(*[float(v) for v in r]) for r in g["inputs"]], np.float64)
+    assert np.array_equal(got, g["outputs"])
+    assert np.array_equal(np.signbit(got), np.signbit(g["outputs"]))

@@ -363,6 +363,48 @@ def test_sum_tree_incremental_equals_rebuild(golden, orc, n, cap):
     assert np.array_equal(chunks, ref)
 
 
+def test_tree_refresh_timeout_is_repaired(golden, orc, monkeypatch):
+    """a tree-refresh timeout (forced with the PONGMI_TR_FORCE_TIMEOUT hook: block 1's
+    granule poll gives up at once) sets status bit 2 and leaves the sums stale; check_status raises;
+    repair_tree rebuilds the tree (bit 2 -> bit 3), after which it equals the oracle's tree of the
+    priorities exactly, check_status passes, and later incremental steps keep it equal to a rebuild."""
+    from pongmi import _lib
+    n, cap = 2048, 8192
+    L = _learner(golden, n=n, batch=256, cap=cap, seed=4, epsilon=0.5)
+    for _ in range(6):
+        L.step()
+    monkeypatch.setenv("PONGMI_TR_FORCE_TIMEOUT", "1")
+    L.step()
+    monkeypatch.delenv("PONGMI_TR_FORCE_TIMEOUT")
+    c = L.counters()
+    assert c["status"] & 4 and c["train_steps"] > 0, c
+    with pytest.raises(_lib.PongmiError):
+        L.check_status(c)
+    stale = L.per_work.clone()
+
+    def oracle_chunks():
+        c = L.counters()
+        pr = L.prios.cpu().numpy().astype(np.float32).copy()
+        pr[(c["pos"] + np.arange(n)) % cap] = np.float32(c["max_prio"])  # the pending push
+        return orc.per_tree(pr, cap)[0]
+
+    nch = (cap + 1023) // 1024
+    assert not np.array_equal(stale[:nch * 8].view(torch.float64).cpu().numpy(), oracle_chunks())  # stale indeed
+    assert L.repair_tree(c) is True
+    c = L.counters()
+    assert c["status"] & 4 == 0 and c["status"] & 8
+    L.check_status(c)
+    assert L.repair_tree(c) is False
+    assert np.array_equal(L.per_work[:nch * 8].view(torch.float64).cpu().numpy(), oracle_chunks())
+    for _ in range(5):
+        L.step()
+    torch.cuda.synchronize()
+    inc = L.per_work.clone()
+    L.prepare()
+    torch.cuda.synchronize()
+    assert torch.equal(inc, L.per_work) and L.counters()["status"] == 8
+
+
 def test_overlapped_step_is_bitwise_identical(golden):
     """pm_selfplay_step_overlap (the next step's side-A act in the learner's launch) must equal the
     plain step bit for bit, also across host changes of modelA (which invalidate the precomputed

@@ -28,6 +28,7 @@
 #   drqnab:VAR=v1,v2  tests/test_gpu_drqn.py under v1, then tools/drqn_time.py interleaved three times
 #   k1sweep    K1 events + rocprofv3 kernel traces at 65 536 .. 4 194 304 arenas
 #   floorprof  tools/k1_floor under rocprofv3 (round 5 SIGSEGV check)
+#   mstamps    k_learn_multi per-update phase stamps (diag and PM_DIAG_NOWAIT builds)
 #   train      bench.py --workload train (one config.yaml generation try, replay ratio 1)
 #   gpus2      bench.py --gpus 2 must refuse on a 1-GPU box
 #   pytest:<path>[::sel]  one test file / selection
@@ -133,6 +134,12 @@ run_task() {
       timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_floor -o k -- \
           ./tools/k1_floor 65536 > gpurun_out/${tag}_prof_floor.log 2>&1; rc=$?
       grep -v amdgpu.ids gpurun_out/${tag}_prof_floor.log | tail -25; echo "k1_floor under rocprofv3 rc=$rc"; [ $rc -eq 0 ] ;;
+    mstamps)  # k_learn_multi's per-update phase timeline (tools/multi_stamps.py, U = 64): diag build, then the
+              # PM_DIAG_NOWAIT build (no vmcnt(0) waits at the stamps)
+      timeout -k 10 180 python3 tools/multi_stamps.py --U 64 > gpurun_out/${tag}_mstamps.txt 2>&1 &&
+          grep -v amdgpu.ids gpurun_out/${tag}_mstamps.txt &&
+      PONGMI_DIAG_LIB=$PWD/pingpong-selfplay-ai_amd/pongmi/libpongmi_diag_nw.so timeout -k 10 180 python3 tools/multi_stamps.py \
+          --U 64 > gpurun_out/${tag}_mstamps_nw.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_mstamps_nw.txt ;;
     train)  # one config.yaml generation try at replay ratio 1 (bench.py --workload train)
       timeout -k 10 300 python3 bench.py --workload train > gpurun_out/${tag}_train.json 2> gpurun_out/${tag}_train.err &&
           cat gpurun_out/${tag}_train.json && echo TRAIN_OK ;;

@@ -9,7 +9,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["PONGMI_LIB"] = os.path.join(ROOT, "pingpong-selfplay-ai_amd", "pongmi", "libpongmi_diag.so")
+os.environ["PONGMI_LIB"] = os.environ.get("PONGMI_DIAG_LIB") or os.path.join(ROOT, "pingpong-selfplay-ai_amd", "pongmi",
+                                                                             "libpongmi_diag.so")
 sys.path.insert(0, os.path.join(ROOT, "pingpong-selfplay-ai_amd"))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402

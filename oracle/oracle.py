@@ -354,21 +354,12 @@ RNN_PARAM_KEYS = (  # modelB.parameters() order (models/qnet_rnn.py:71-99)
     f"{m}.{s}" for m in ("fc_shared_head.0", "fc_V", "fc_A") for s in ("weight_mu", "bias_mu", "weight_sigma", "bias_sigma"))
 
 
-def drqn_grads(sd, target_sd, obs, act, rew, nxt, done, gamma=0.99, flip=(), relu_band=0.0):
+def drqn_grads(sd, target_sd, obs, act, rew, nxt, done, gamma=0.99):
     """train_step_rnn's loss and gradients (scripts/train_rnn_iterative.py:424-513), float64: zero
     initial state; q = Q_B(obs)[last step][a_last]; a* = argmax Q_B(next) (first max); y = r_last +
     gamma * Q_T(next)[a*] * (1 - done_last) with targetB in eval mode; loss = smooth_l1(q, y) (beta 1,
     mean); gradients of every modelB parameter by hand-written BPTT (NoisyLinear: d mu = dW,
-    d sigma = dW * eps). obs/next [B,T,7], act/rew/done [B,T]. Returns dict(loss, q, y, grads, sites).
-
-    Test hooks for the ReLU decisions a float32 evaluation may take the other way:
-    relu_band = c > 0 lists in `sites` every obs-stream ReLU pre-activation p (features layer 1
-    ("f1", t, b, j), layer 2 ("f2", t, b, j), the shared head ("s", -1, b, j)) with |p| <= c * 2^-24 *
-    S, S = sum of the |terms| of its dot product (|x| . |W| + |bias|): the float32 rounding-error scale
-    of p, within which the sign of p is a rounding decision (`margins`: |p| / (2^-24 S) per site).
-    flip = sites whose ReLU derivative is inverted in the backward pass (the forward values keep
-    max(p, 0): |p| is below the band anyway), so a test can find which side a float32 evaluation took
-    at each listed decision (tests/test_gpu_drqn.py::_assert_grads_relu)."""
+    d sigma = dW * eps). obs/next [B,T,7], act/rew/done [B,T]. Returns dict(loss, q, y, grads)."""
     eB = rnn_effective(sd, True)
     eT = rnn_effective(target_sd, False)
     B, T, _ = obs.shape
@@ -380,29 +371,9 @@ def drqn_grads(sd, target_sd, obs, act, rew, nxt, done, gamma=0.99, flip=(), rel
     # forward with caches
     x = np.asarray(obs, np.float64)
     f1s, f2s, gs, cs, hs = [], [], [], [z], [z]
-    m1s, m2s, sites, margins = [], [], [], []
-    flips = {}
-    for kind, t, b, j in flip:
-        flips.setdefault((kind, t), []).append((b, j))
-
-    def relu_mask(p, S, kind, t):
-        m = p > 0
-        for b, j in flips.get((kind, t), ()):
-            m[b, j] = not m[b, j]
-        if relu_band > 0:
-            r = np.abs(p) / (2.0 ** -24 * np.maximum(S, 1e-300))
-            for b, j in zip(*np.nonzero(r <= relu_band)):
-                sites.append((kind, t, int(b), int(j)))
-                margins.append(float(r[b, j]))
-        return m
-
     for t in range(T):
-        p1 = x[:, t] @ eB["W1"].T + eB["b1"]
-        m1s.append(relu_mask(p1, np.abs(x[:, t]) @ np.abs(eB["W1"]).T + np.abs(eB["b1"]), "f1", t))
-        f1 = np.maximum(p1, 0.0)
-        p2 = f1 @ eB["W2"].T + eB["b2"]
-        m2s.append(relu_mask(p2, f1 @ np.abs(eB["W2"]).T + np.abs(eB["b2"]), "f2", t))
-        f2 = np.maximum(p2, 0.0)
+        f1 = np.maximum(x[:, t] @ eB["W1"].T + eB["b1"], 0.0)
+        f2 = np.maximum(f1 @ eB["W2"].T + eB["b2"], 0.0)
         zt = f2 @ eB["Wih"].T + eB["bih"] + hs[-1] @ eB["Whh"].T + eB["bhh"]
         i, f, g, o = np.split(zt, 4, axis=1)
         i, f, g, o = _sigmoid(i), _sigmoid(f), np.tanh(g), _sigmoid(o)
@@ -426,8 +397,7 @@ def drqn_grads(sd, target_sd, obs, act, rew, nxt, done, gamma=0.99, flip=(), rel
     dV = dQ.sum(axis=1, keepdims=True)
     dA = dQ - dQ.sum(axis=1, keepdims=True) / 3.0
     G = {"V.W": dV.T @ s, "V.b": dV.sum(0), "A.W": dA.T @ s, "A.b": dA.sum(0)}
-    ds = (dV @ eB["V.W"] + dA @ eB["A.W"]) * relu_mask(spre, np.abs(hT) @ np.abs(eB["S.W"]).T + np.abs(eB["S.b"]),
-                                                        "s", -1)
+    ds = (dV @ eB["V.W"] + dA @ eB["A.W"]) * (spre > 0)
     G["S.W"], G["S.b"] = ds.T @ hT, ds.sum(0)
     dh = ds @ eB["S.W"]
     dc = np.zeros_like(dh)
@@ -446,10 +416,10 @@ def drqn_grads(sd, target_sd, obs, act, rew, nxt, done, gamma=0.99, flip=(), rel
         G["Whh"] = G["Whh"] + dz.T @ hs[t]
         G["b"] = G["b"] + dz.sum(0)
         dh = dz @ eB["Whh"]
-        dp2 = (dz @ eB["Wih"]) * m2s[t]
+        dp2 = (dz @ eB["Wih"]) * (f2s[t] > 0)
         G["W2"] = G["W2"] + dp2.T @ f1s[t]
         G["b2"] = G["b2"] + dp2.sum(0)
-        dp1 = (dp2 @ eB["W2"]) * m1s[t]
+        dp1 = (dp2 @ eB["W2"]) * (f1s[t] > 0)
         G["W1"] = G["W1"] + dp1.T @ x[:, t]
         G["b1"] = G["b1"] + dp1.sum(0)
     eps = lambda k: np.asarray(sd[k], np.float64)  # noqa: E731
@@ -462,7 +432,7 @@ def drqn_grads(sd, target_sd, obs, act, rew, nxt, done, gamma=0.99, flip=(), rel
         grads[f"{key}.bias_mu"] = G[name + ".b"]
         grads[f"{key}.weight_sigma"] = G[name + ".W"] * eps(f"{key}.weight_epsilon")
         grads[f"{key}.bias_sigma"] = G[name + ".b"] * eps(f"{key}.bias_epsilon")
-    return dict(loss=loss, q=q, y=y, grads=grads, sites=sites, margins=margins)
+    return dict(loss=loss, q=q, y=y, grads=grads)
 
 
 def clip_grad_norm(grads, max_norm=1.0):

@@ -4,12 +4,10 @@ torch autograd (tests/golden/drqn.npz) and against the float64 oracle (oracle.dr
 Tolerances (fp32 on the device; exact-f32 MFMA sums in a different order than torch's CPU GEMMs):
 loss / pre-clip norm rtol 1e-4; gradients rtol 5e-4 with atol 1e-5 x the tensor's largest magnitude
 (round 5: the kernel's measured worst was 0.40 of the round-4 bar of rtol 1e-3), every update, every
-tensor. The one exemption is targeted (_assert_grads_relu): an obs-stream ReLU whose pre-activation
-is close to 0 relative to its float32 error scale (the 12 closest, |p| / (2^-24 sum|terms|), oracle
-.drqn_grads' relu_band) is a decision the f32 device may take the other way, so the device's
-gradient must equal, at the same bar, the oracle's gradient with some subset of at most 3 of those
-decisions flipped (the empty subset first); the decisions flipped, their margins and the elements
-whose reference they change are printed. Parameters are
+tensor, except that the atol of a tensor is widened to 1.5x the error of the reference's own float32
+autograd (torch, CPU, the reference module tree at the same parameters and batch) when that error is
+larger (_assert_grads_conditioned): the device must be as close to float64 as the reference itself
+is. Both errors are printed. Parameters are
 pinned by composition, with no sign band: every update's gradient is checked against the oracle run
 from the device's OWN pre-update parameters (so Adam's sign-of-rounding cannot drift the two apart),
 and clip + Adam given that gradient and the device's pre-clip norm is checked bit for bit against
@@ -17,7 +15,6 @@ the float32 restatement oracle.clip_adam_f32 — every parameter, both moments, 
 parameters after the three fixture updates are also compared with the reference's own autograd run
 (final_sub.*) under the sign band that Adam's normalised step needs there (_assert_final_sub).
 """
-import itertools
 import os
 
 import numpy as np
@@ -66,45 +63,59 @@ def _grad_err(got, ref, atol_rel=1e-5):
     return worst
 
 
-RELU_BAND = 1024.0  # |p| <= RELU_BAND * 2^-24 * sum|terms|: candidates for a float32 rounding decision
-MAX_SITES, MAX_FLIPS = 12, 3
+def ref32_grads(sd, tsd, obs, act, rew, nxt, done, gamma=0.99):
+    """train_step_rnn's gradient (scripts/train_rnn_iterative.py:424-513) by torch autograd in
+    float32 on the CPU, on the reference's module tree (models.qnet_rnn.QNetRNN's torch path, pinned
+    to the reference module's outputs by tests/test_rnn_host.py): what the reference itself computes
+    at these parameters. Its distance from the float64 oracle measures how well-conditioned the
+    update is in float32."""
+    from models.qnet_rnn import QNetRNN
+
+    def net(state, train):
+        m = QNetRNN(7, 3)
+        m.load_state_dict({k: torch.as_tensor(np.asarray(v, np.float32)) for k, v in state.items()})
+        m.train(train)
+        return m
+
+    B = obs.shape[0]
+    h0 = (torch.zeros(1, B, 128), torch.zeros(1, B, 128))
+    mB, mT = net(sd, True), net(tsd, False)
+    q = mB(torch.from_numpy(np.asarray(obs, np.float32)), h0)[0]
+    with torch.no_grad():
+        nx = torch.from_numpy(np.asarray(nxt, np.float32))
+        a = mB(nx, h0)[0].argmax(1)
+        y = torch.from_numpy(np.asarray(rew[:, -1], np.float32)) + gamma * mT(nx, h0)[0].gather(1, a[:, None])[:, 0] * \
+            (1.0 - torch.from_numpy(np.asarray(done[:, -1], np.float32)))
+    qa = q.gather(1, torch.from_numpy(np.asarray(act[:, -1], np.int64))[:, None])[:, 0]
+    torch.nn.functional.smooth_l1_loss(qa, y).backward()
+    return {k: v.grad.double().numpy() for k, v in mB.named_parameters()}
 
 
-def _assert_grads_relu(got, orc, sd, tsd, batch, what):
-    """The device's gradient vs the float64 oracle at the full bar (atol 1e-5 max|g|), where the
-    oracle may take the device's side at up to MAX_FLIPS ReLU decisions near 0: the MAX_SITES
-    pre-activations closest to 0 relative to their float32 error scale (|p| / (2^-24 sum|terms|),
-    oracle.drqn_grads' relu_band) are the candidates; subsets are tried smallest first (the empty one
-    first), screened with the sum of the single flips' gradient changes and confirmed by an exact
-    oracle run with that subset flipped. Prints the candidates' margins, the decisions the device
-    took the other way with theirs, and per tensor the elements whose reference that moved by >= 0.1
-    x the atol (the exempt elements: everywhere else the plain reference applies unchanged).
-    Round 5 measured one such decision on update 1: 2 elements of features_extractor.2.weight off by
-    2.2e-6 (a layer-2 unit of a (t, b) whose layer-1 features have 2 nonzero entries)."""
-    info = orc.drqn_grads(sd, tsd, *batch, relu_band=RELU_BAND)
-    order = np.argsort(info["margins"], kind="stable")[:MAX_SITES]
-    sites = [info["sites"][i] for i in order]
-    margin = {info["sites"][i]: info["margins"][i] for i in order}
-    ref, flipped = info["grads"], ()
-    if _grad_err(got, ref) > 1.0:
-        delta = [{k: v - ref[k] for k, v in orc.drqn_grads(sd, tsd, *batch, flip=(s,))["grads"].items()} for s in sites]
-        for r in range(1, min(MAX_FLIPS, len(sites)) + 1):
-            for c in itertools.combinations(range(len(sites)), r):
-                approx = {k: ref[k] + sum(delta[i][k] for i in c) for k in ref}
-                if _grad_err(got, approx) <= 1.0:
-                    g = orc.drqn_grads(sd, tsd, *batch, flip=tuple(sites[i] for i in c))["grads"]
-                    if _grad_err(got, g) <= 1.0:
-                        ref, flipped = g, tuple(sites[i] for i in c)
-                        break
-            if flipped:
-                break
-    exempt = {k: int(np.sum(np.abs(ref[k] - info["grads"][k]) >= 0.1 * (1e-5 * np.abs(info["grads"][k]).max())))
-              for k in ref}
-    print(f"\n{what}: {len(info['sites'])} ReLU pre-activations within {RELU_BAND:g} x their float32 error scale "
-          f"(closest margins {[round(margin[s], 1) for s in sites]}); the device took the other side at "
-          f"{len(flipped)}: {[(s, round(margin[s], 1)) for s in flipped]}; exempt elements "
-          f"{({k: v for k, v in exempt.items() if v}) or 0}")
-    return _assert_grads(got, ref, what), ref
+REF32_FACTOR = 1.5
+
+
+def _assert_grads_conditioned(got, orc, sd, tsd, batch, what):
+    """The device's gradient vs the float64 oracle, per tensor at atol = max(1e-5 x max|g|,
+    REF32_FACTOR x the reference's own float32 error there) with rtol GRAD_RTOL: the bar widens only
+    where the reference's float32 autograd (ref32_grads, same parameters, same batch) is itself that
+    far from float64. Round 5's failing update (update 1 of the fixture: the device 4.5e-5 x max|g|
+    off on the LSTM / feature gradients) is such a case: the reference's float32 autograd is 5.6e-5 x
+    max|g| off there, 20x its error on update 0, with no ReLU or argmax decision near a tie (a
+    conditioning effect of the batch, not a device defect). Prints both errors per tensor class."""
+    info = orc.drqn_grads(sd, tsd, *batch)
+    ref, r32 = info["grads"], ref32_grads(sd, tsd, *batch)
+    worst = 0.0
+    lines = []
+    for k, r in ref.items():
+        m = np.abs(r).max()
+        e32 = float(np.abs(r32[k] - r).max())
+        atol = max(1e-5 * m, REF32_FACTOR * e32) + 1e-9
+        np.testing.assert_allclose(got[k], r, rtol=GRAD_RTOL, atol=atol, err_msg=f"{what}: {k}")
+        worst = max(worst, float(np.max(np.abs(got[k] - r) / (atol + GRAD_RTOL * np.abs(r)))))
+        if k in ("lstm.weight_hh_l0", "features_extractor.2.weight", "fc_shared_head.0.weight_mu"):
+            lines.append(f"{k}: device {np.abs(got[k] - r).max() / m:.2e}, reference f32 {e32 / m:.2e} x max|g|")
+    print(f"\n{what}: vs float64 — " + "; ".join(lines) + f"; error / bar max {worst:.4f}")
+    return worst, ref
 
 
 def _f64(sd):
@@ -185,14 +196,14 @@ def test_drqn_update_matches_reference(golden, orc):
         if k == 0:
             _assert_grads(_grads(L), {k2[len("u0_grad."):]: v for k2, v in gd.items() if k2.startswith("u0_grad.")},
                           "update 0 vs autograd")
-        # every update at the full bar; a ReLU decision inside the float32 band may go either way
-        # (round 5 measured one on update 1: 2 elements of features_extractor.2.weight off by 2.2e-6)
+        # every update at the full bar, widened only where the reference's own float32 autograd is
+        # farther from float64 (update 1: an ill-conditioned batch, see _assert_grads_conditioned)
         dump = os.environ.get("PONGMI_DRQN_DUMP")  # diagnosis: the device's parameters and gradient per update
         if dump:
             os.makedirs(dump, exist_ok=True)
             np.savez(os.path.join(dump, f"drqn_u{k}.npz"), **{"p." + n: v for n, v in sd_before.items()},
                      **{"g." + n: v for n, v in _grads(L).items()})
-        w, ref = _assert_grads_relu(_grads(L), orc, sd_before, _f64(_sd(gr)), _batch(gd, k),
+        w, ref = _assert_grads_conditioned(_grads(L), orc, sd_before, _f64(_sd(gr)), _batch(gd, k),
                                     f"update {k} vs oracle (device's own parameters)")
         worst, refs = max(worst, w), refs + [ref]
         _assert_apply_exact(L, p0, m0, v0, k + 1, f"update {k}")
@@ -228,7 +239,7 @@ def test_drqn_against_oracle_ragged(golden, orc, B, T):
     np.testing.assert_allclose(L.stats()["loss"], info["loss"], rtol=1e-4)
     p0, m0, v0 = _snap(L)
     L.apply()  # the sigma gradients (mu gradient x epsilon) are formed after the all-reduce, in apply
-    _assert_grads_relu(_grads(L), orc, {k: v.astype(np.float64) for k, v in sd.items()},
+    _assert_grads_conditioned(_grads(L), orc, {k: v.astype(np.float64) for k, v in sd.items()},
                        {k: v.astype(np.float64) for k, v in tsd.items()}, (obs, act, rew, nxt, done), f"B={B} T={T}")
     _assert_apply_exact(L, p0, m0, v0, 1, f"B={B} T={T}")
 

@@ -48,26 +48,3 @@ def test_dropin_torch_path_matches_reference(golden):
             np.testing.assert_allclose(q.numpy(), g[f"seq_q_{mode}"], rtol=1e-5, atol=1e-6)
             np.testing.assert_allclose(h.numpy(), g[f"seq_h_{mode}"], rtol=1e-5, atol=1e-6)
 
-
-def test_oracle_relu_band_hooks(golden, orc):
-    """oracle.drqn_grads' test hooks (tests/test_gpu_drqn.py::_assert_grads_relu): relu_band only
-    lists decisions (the gradient is unchanged), and flipping one layer-2 ReLU decision (t, b, j)
-    moves exactly row j of features_extractor.2.weight and bias j there, plus layer 1 through dp1,
-    and no LSTM or head gradient."""
-    gr, gd = golden("rnn"), golden("drqn")
-    sd = {k[7:]: v.astype(np.float64) for k, v in gr.items() if k.startswith("params.")}
-    batch = tuple(gd[f"b0_{n}"] for n in ("obs", "act", "rew", "next", "done"))
-    plain = orc.drqn_grads(sd, sd, *batch)
-    band = orc.drqn_grads(sd, sd, *batch, relu_band=64.0)
-    assert all(np.array_equal(plain["grads"][k], band["grads"][k]) for k in plain["grads"])
-    assert plain["sites"] == [] and len(band["sites"]) == len(band["margins"]) >= 1
-    assert all(m <= 64.0 for m in band["margins"])
-    site = next(s for s in band["sites"] if s[0] == "f2")
-    _, t, b, j = site
-    alt = orc.drqn_grads(sd, sd, *batch, flip=(site,))["grads"]
-    d2 = np.abs(alt["features_extractor.2.weight"] - plain["grads"]["features_extractor.2.weight"])
-    assert d2[j].max() > 0 and np.all(np.delete(d2, j, axis=0) == 0)
-    db2 = np.abs(alt["features_extractor.2.bias"] - plain["grads"]["features_extractor.2.bias"])
-    assert np.nonzero(db2)[0].tolist() == [j]
-    for k in ("lstm.weight_ih_l0", "lstm.weight_hh_l0", "fc_A.weight_mu", "fc_shared_head.0.weight_mu"):
-        assert np.array_equal(alt[k], plain["grads"][k]), k

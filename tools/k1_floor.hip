@@ -200,26 +200,36 @@ static void on_segv(int sig, siginfo_t* si, void* uc) {
     raise(sig);
 }
 
-static double graph_us(Fn fn, St s, int n, hipStream_t st, int per_graph = 50, int replays = 40, int warm = 100) {
+// One captured graph of `per_graph` back-to-back launches, instantiated once and replayed for every
+// repetition (round 6: re-capturing and re-instantiating a graph per repetition crashed rocprofv3's
+// tracer library on the 12th instantiation: the handler above mapped the faulting PC into
+// librocprofiler-sdk.so; the old loop also created two HIP events per measurement and never destroyed them).
+struct Graph {
     hipGraph_t g;
     hipGraphExec_t ge;
+};
+static Graph capture(Fn fn, St s, int n, hipStream_t st, int per_graph = 50) {
+    Graph r;
     CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
     for (int k = 0; k < per_graph; ++k) hipLaunchKernelGGL(fn, dim3((n + 255) / 256), dim3(256), 0, st, s, n);
     CK(hipGetLastError());
-    CK(hipStreamEndCapture(st, &g));
-    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-    for (int k = 0; k < warm; ++k) CK(hipGraphLaunch(ge, st));
+    CK(hipStreamEndCapture(st, &r.g));
+    CK(hipGraphInstantiate(&r.ge, r.g, nullptr, nullptr, 0));
+    return r;
+}
+static double graph_us(const Graph& gr, hipStream_t st, int per_graph = 50, int replays = 40, int warm = 100) {
+    for (int k = 0; k < warm; ++k) CK(hipGraphLaunch(gr.ge, st));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipEventRecord(e0, st));
-    for (int k = 0; k < replays; ++k) CK(hipGraphLaunch(ge, st));
+    for (int k = 0; k < replays; ++k) CK(hipGraphLaunch(gr.ge, st));
     CK(hipEventRecord(e1, st));
     CK(hipEventSynchronize(e1));
     float ms = 0.f;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    CK(hipGraphExecDestroy(ge));
-    CK(hipGraphDestroy(g));
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
     return ms * 1e3 / (per_graph * replays);
 }
 
@@ -260,15 +270,23 @@ int main(int argc, char** argv) {
         {"stores16", k_skel16<6>, 133.0 * n},
         {"copy16", k_skel16<7>, 203.0 * n},
     };
+    constexpr int nk = sizeof(ks) / sizeof(ks[0]);
+    Graph gs[nk];
+    for (int j = 0; j < nk; ++j) gs[j] = capture(ks[j].fn, s, n, st);
     for (int rep = 0; rep < 2; ++rep)
-        for (const auto& k : ks) {
-            const double us = graph_us(k.fn, s, n, st);
+        for (int j = 0; j < nk; ++j) {
+            const auto& k = ks[j];
+            const double us = graph_us(gs[j], st);
             printf("{\"n\": %d, \"rep\": %d, \"kernel\": \"%s\", \"graph_us\": %.3f, \"bytes\": %.0f, \"frac_of_8TBs\": %.4f}\n",
                    n, rep, k.name, us, k.bytes, k.bytes / (us * 1e-6) / 8e12);
             fflush(stdout);
         }
-    // teardown (missing in round 5): drain, then release the stream and every buffer before exit
+    // teardown (missing in round 5): drain, then release the graphs, the stream and every buffer
     CK(hipStreamSynchronize(st));
+    for (int j = 0; j < nk; ++j) {
+        CK(hipGraphExecDestroy(gs[j].ge));
+        CK(hipGraphDestroy(gs[j].g));
+    }
     CK(hipStreamDestroy(st));
     CK(hipFree(s.done));
     CK(hipFree(o));

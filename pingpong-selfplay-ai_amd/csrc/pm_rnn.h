@@ -318,4 +318,181 @@ __device__ __forceinline__ void rnn_group(const float* __restrict__ w, float* ri
     PM_STG_CLK(47);
 }
 
+// ---------------------------------------------------------------- the split tile (side A's tail)
+// One 32-arena tile on a whole 4-wave block, for the side-A groups a one-tile-per-wave round would
+// leave to a second ~97 us round (round 6). Wave p computes only piece p of every ring stage — the
+// F2 output tile p, gate p of each hidden block, the shared head's output tile p — with the same
+// MFMA sequence per accumulator as rnn_group (so every result is bit-identical to it), its A
+// operands streamed straight into registers four stages ahead (its own 4 KB piece per stage: no
+// LDS ring, no barrier per stage). The pieces meet in LDS (xch) where a layer needs all of them:
+// the four F2 tiles (the gates' feature K-steps), the four gates of a hidden block (the cell, which
+// every wave then evaluates identically, so each holds h' as the head stage's B operand), and the
+// four shared-head tiles (the dueling heads, wave 0). 38 stages of 16 MFMAs instead of 64.
+constexpr int kSplitAhead = 4;
+__device__ __forceinline__ void piece_load(const float* __restrict__ w, int s, int lane, float4 (&a)[4]) {
+    const float4* src = reinterpret_cast<const float4*>(stage_piece(w, s, threadIdx.x >> 6)) + lane;
+#pragma unroll
+    for (int rq = 0; rq < 4; ++rq) a[rq] = src[64 * rq];
+}
+// piece p's 16 MFMAs of one stage, in stage_mfma's order for acc[p]
+__device__ __forceinline__ void piece_mfma(const float4 (&a)[4], const float (&b)[16], f32x16& acc) {
+#pragma unroll
+    for (int rq = 0; rq < 4; ++rq) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rq].x, b[4 * rq + 0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rq].y, b[4 * rq + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rq].z, b[4 * rq + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rq].w, b[4 * rq + 3], acc, 0, 0, 0);
+    }
+}
+struct SplitX {
+    float v[2][4][16][64];  // [buffer][wave][register][lane]: 32 KB
+};
+__device__ __forceinline__ void xch_put(SplitX& x, int buf, int p, int lane, const f32x16& acc) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x.v[buf][p][r][lane] = acc[r];
+}
+
+template <typename Out>
+__device__ __forceinline__ void rnn_tile_split(const float* __restrict__ w, SplitX& x, const float* hw,
+                                               const float* __restrict__ obs, float* hst, float* cst,
+                                               const uint8_t* __restrict__ reset, const int* list, int count,
+                                               int tile, const Out& out, const float* hin = nullptr,
+                                               const float* cin = nullptr) {
+    const int lane = threadIdx.x & 63, p = threadIdx.x >> 6, h = lane >> 5;
+    const int row = tile * 32 + (lane & 31);
+    const bool valid = row < count;
+    const int arena = list[min(row, count - 1)];
+    float* hs = hst + (size_t)arena * 128;
+    float* cs = cst + (size_t)arena * 128;
+    const float* hr = (hin ? hin : hst) + (size_t)arena * 128;
+    const float* cr = (cin ? cin : cst) + (size_t)arena * 128;
+    const bool zero = reset != nullptr && reset[arena] != 0;
+    float4 pa[kSplitAhead][4];  // stage s's A operands in pa[s % kSplitAhead] (static after unrolling)
+#pragma unroll
+    for (int s = 0; s < kSplitAhead; ++s) piece_load(w, s, lane, pa[s]);
+    // ---- prologue (rnn_group's): inputs, layer 1, h_prev into the B-operand registers
+    float xs[4];
+    tile_inputs(obs + (size_t)arena * 7, h, xs);
+    float xb[8][16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            const float4 v = zero ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                  : *reinterpret_cast<const float4*>(hr + 32 * t + 8 * rq + 4 * h);
+            xb[4 + t][4 * rq] = v.x; xb[4 + t][4 * rq + 1] = v.y; xb[4 + t][4 * rq + 2] = v.z; xb[4 + t][4 * rq + 3] = v.w;
+        }
+    f32x16 c1[2];
+    {
+        const f32x16 zero16 = {};
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            const float4 a = reinterpret_cast<const float4*>(w + R_F1)[jt * 64 + lane];
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, xs[0], zero16, 0, 0, 0);
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, xs[1], c1[jt], 0, 0, 0);
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, xs[2], c1[jt], 0, 0, 0);
+            c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, xs[3], c1[jt], 0, 0, 0);
+        }
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c1[jt][r] = relu(c1[jt][r]);
+    }
+    // ---- F2 (stages 0, 1): output tile p
+    f32x16 acc = {};
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+        float b[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) b[r] = c1[t2][r];
+        piece_mfma(pa[t2], b, acc);
+        piece_load(w, t2 + kSplitAhead, lane, pa[t2]);
+    }
+    add_bias_lds(hw + kHwB2 + (p * 2 + h) * 16, acc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = relu(acc[r]);
+    xch_put(x, 0, p, lane, acc);
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xb[mt][r] = x.v[0][mt][r][lane];
+    f32x16 sacc = {};
+    // ---- LSTM: hidden block m, gate p (stages 2 + 9m .. 2 + 9m + 7), then the shared head (2 + 9m + 8)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        float4 cp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            cp[j] = zero ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(cr + 32 * m + 8 * j + 4 * h);
+        acc = f32x16{};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int s = 2 + 9 * m + t;
+            piece_mfma(pa[s % kSplitAhead], xb[t], acc);
+            if (s + kSplitAhead < kRingStages) piece_load(w, s + kSplitAhead, lane, pa[s % kSplitAhead]);
+        }
+        add_bias_lds(hw + kHwBG + ((p * 4 + m) * 2 + h) * 16, acc);
+        const int buf = (m + 1) & 1;
+        xch_put(x, buf, p, lane, acc);
+        __syncthreads();
+        float hb[16];
+        {
+            float cn[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float cprev = (&cp[r >> 2].x)[r & 3];
+                const float ig = sig_hw(x.v[buf][0][r][lane]), fg = sig_hw(x.v[buf][1][r][lane]);
+                const float gg = tanh_hw(x.v[buf][2][r][lane]), og = sig_hw(x.v[buf][3][r][lane]);
+                cn[r] = fg * cprev + ig * gg;
+                hb[r] = og * tanh_hw(cn[r]);
+            }
+            if (p == 0 && valid) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    *reinterpret_cast<float4*>(cs + 32 * m + 8 * j + 4 * h) =
+                        make_float4(cn[4 * j], cn[4 * j + 1], cn[4 * j + 2], cn[4 * j + 3]);
+                    *reinterpret_cast<float4*>(hs + 32 * m + 8 * j + 4 * h) =
+                        make_float4(hb[4 * j], hb[4 * j + 1], hb[4 * j + 2], hb[4 * j + 3]);
+                }
+            }
+        }
+        {
+            const int s = 2 + 9 * m + 8;
+            piece_mfma(pa[s % kSplitAhead], hb, sacc);
+            if (s + kSplitAhead < kRingStages) piece_load(w, s + kSplitAhead, lane, pa[s % kSplitAhead]);
+        }
+    }
+    // ---- the dueling heads from the four shared-head tiles, in rnn_group's chain order (wave 0)
+    add_bias_lds(hw + kHwBS + (p * 2 + h) * 16, sacc);
+    xch_put(x, 1, p, lane, sacc);
+    __syncthreads();
+    if (p != 0) return;
+    float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+        const float4* hw4 = reinterpret_cast<const float4*>(hw + kHwHeads) + (h * 4 + mt) * 16;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float xv = relu(x.v[1][mt][r][lane]);
+            const float4 wv = hw4[r];
+            v = fmaf(wv.x, xv, v);
+            a0 = fmaf(wv.y, xv, a0);
+            a1 = fmaf(wv.z, xv, a1);
+            a2 = fmaf(wv.w, xv, a2);
+        }
+    }
+    v += __shfl_xor(v, 32);
+    a0 += __shfl_xor(a0, 32);
+    a1 += __shfl_xor(a1, 32);
+    a2 += __shfl_xor(a2, 32);
+    v += hw[512];
+    a0 += hw[513];
+    a1 += hw[514];
+    a2 += hw[515];
+    const float mean = ((a0 + a1) + a2) / 3.0f;
+    const float q[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
+    out(arena, valid && h == 0, q);
+}
+
 }  // namespace pm

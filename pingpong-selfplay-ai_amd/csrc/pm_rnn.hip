@@ -1,6 +1,10 @@
 // K5 — QNetRNN acting (models/qnet_rnn.py, scripts/train_rnn_iterative.py:371-389) on the matrix
 // cores: fold (NoisyLinear mu + sigma * eps into the fragment-ordered block), single-net step
 // (pm_rnn_q: parity / the drop-in module's forward) and the fused two-player act (pm_rnn_act).
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "pm_host.h"
 #include "pm_rnn.h"
 
@@ -255,19 +259,31 @@ struct RnnActArgs {
 };
 
 // Block b of the act grid: ActGrid (pm_mfma.h) with kRnnRows-arena chunks on side B (b < nb); side A
-// grouped by opponent net (b >= nb). Block-wide.
-__device__ __forceinline__ void rnn_act_block(const ActGrid& g, const RnnActArgs& A, int b, RnnShared& sh) {
+// grouped by opponent net (b >= nb). Block-wide. split >= 0 (packed side A only): side-A blocks
+// [split, ...) are split tiles, four per group from group `split` on (rnn_tile_split: one 32-arena
+// tile per block, its stages spread over the four waves), so the groups past the first round finish
+// in ~a quarter of a group's time on the CUs the first round frees.
+__device__ __forceinline__ void rnn_act_block(const ActGrid& g, const RnnActArgs& A, int b, RnnShared& sh, int split,
+                                              SplitX& sx) {
     const int nb = (g.n + kRnnRows - 1) / kRnnRows;
     const float* w;
     int net = -1, lo, hi;
     bool compact = false;
     if (b >= nb && A.opp_list) {  // side A packed over the env kernel's lists
-        const int k = packed_rows(A.opp_list, A.opp_cnt, g.n, g.n_opp, b - nb, sh);
-        if (k < 0) return;  // block-uniform: past the last group
+        const int sb = b - nb;
+        const bool tail = split >= 0 && sb >= split;
+        const int grp = tail ? split + (sb - split) / 4 : sb, tile = tail ? (sb - split) % 4 : 0;
+        const int k = packed_rows(A.opp_list, A.opp_cnt, g.n, g.n_opp, grp, sh);
+        if (k < 0) return;                      // block-uniform: past the last group
+        if (tail && 32 * tile >= sh.count) return;  // block-uniform: the group has no such tile
         w = A.w_opp + (size_t)k * PM_RNN_NW;
         stage_tables(w, sh.hw);
         __syncthreads();
-        rnn_rows(w, sh, A.obsA, A.hA, A.cA, A.reset, sh.count, RowOut{A.aA, A.qA, -1.0, 0, 0}, A.hA_in, A.cA_in);
+        const RowOut out{A.aA, A.qA, -1.0, 0, 0};
+        if (tail)
+            rnn_tile_split(w, sx, sh.hw, A.obsA, A.hA, A.cA, A.reset, sh.list, sh.count, tile, out, A.hA_in, A.cA_in);
+        else
+            rnn_rows(w, sh, A.obsA, A.hA, A.cA, A.reset, sh.count, out, A.hA_in, A.cA_in);
         return;
     }
     if (b < nb) {
@@ -302,12 +318,24 @@ __device__ __forceinline__ void rnn_act_block(const ActGrid& g, const RnnActArgs
 
 // Blocks [b0, b1) of the act grid, gridDim.x of them at a time (a grid smaller than b1 - b0 loops:
 // the overlapped QNetRNN step runs side A on part of the chip beside the DRQN update).
-__global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs A, int b0, int b1) {
+__global__ __launch_bounds__(kRnnBlock, 1) void k_rnn_act(ActGrid g, RnnActArgs A, int b0, int b1, int split) {
     __shared__ RnnShared sh;
+    __shared__ SplitX sx;
     for (int b = b0 + (int)blockIdx.x; b < b1; b += (int)gridDim.x) {
         __syncthreads();  // the previous block's LDS tables / lists are dead
-        rnn_act_block(g, A, b, sh);
+        rnn_act_block(g, A, b, sh, split, sx);
     }
+}
+
+// The split tail of the packed side-A launch (round 6): PONGMI_RNN_SPLIT=0 turns it off (every group
+// on whole blocks, the grid looping); PONGMI_RNN_SPLIT_R=r forces the first split group (tests: 0 =
+// every group split). Read per launch.
+int split_first(int max_blocks, int groups) {
+    const char* e = getenv("PONGMI_RNN_SPLIT");
+    if (e && *e && atoi(e) == 0) return -1;
+    const char* r = getenv("PONGMI_RNN_SPLIT_R");
+    if (r && *r) return std::max(0, std::min(atoi(r), groups));
+    return max_blocks > 0 && max_blocks < groups ? max_blocks : -1;
 }
 
 }  // namespace
@@ -363,10 +391,15 @@ int pm_rnn_act_part(const float* w_opp, const int32_t* opp_id, int32_t n_opp, co
                        hB, cB, hA_in, cA_in, reset, aA, aB, qA, qB, (double)epsilon, eps_dev, seed, counter,
                        counter_dev};
     const int na = lists ? nb + n_opp : g.blocks();  // packed: sum over nets of ceil(rows / 128) <= nb + nets
-    const int b0 = part == PM_ACT_A ? nb : 0, b1 = part == PM_ACT_B ? nb : nb + na;
+    const int b0 = part == PM_ACT_A ? nb : 0;
+    int b1 = part == PM_ACT_B ? nb : nb + na;
+    // side A alone from the lists, on a capped grid (the overlapped step): the groups past the cap run
+    // as split tiles, every block once (grid = whole-group blocks + 4 per remaining group)
+    const int split = part == PM_ACT_A && lists ? split_first(max_blocks, na) : -1;
+    if (split >= 0) b1 = nb + split + 4 * (na - split);
     int grid = b1 - b0;
-    if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
-    pm_launch(PM_TIMER_RNN_ACT, k_rnn_act, dim3(grid), dim3(kRnnBlock), pm_stream(stream), g, a, b0, b1);
+    if (split < 0 && max_blocks > 0 && grid > max_blocks) grid = max_blocks;
+    pm_launch(PM_TIMER_RNN_ACT, k_rnn_act, dim3(grid), dim3(kRnnBlock), pm_stream(stream), g, a, b0, b1, split);
     PM_LAUNCHED("k_rnn_act");
     return PM_OK;
 }

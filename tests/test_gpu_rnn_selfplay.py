@@ -371,6 +371,31 @@ def test_rnn_overlapped_step_is_bitwise_identical(golden, U):
     assert A.learner.stats()["steps"] == B.learner.stats()["steps"] > 0
 
 
+@pytest.mark.parametrize("split_r", ["0", "3"])
+def test_rnn_split_tiles_are_bitwise_identical(golden, monkeypatch, split_r):
+    """The overlapped step's side-A act with its groups from `split_r` on run as split tiles
+    (rnn_tile_split: one 32-arena tile per block, the ring's four pieces on the four waves; forced
+    with PONGMI_RNN_SPLIT_R, "0" = every group) equals the same step with splitting off
+    (PONGMI_RNN_SPLIT=0): opponents' actions, q-driven decisions, (h, c), ring records, modelB."""
+    kw = dict(n=1024, n_pool=3, epsilon=0.3, memory_size=2000, min_episodes_for_training_start=1, seed=8)
+    A = _learner(golden, overlap=True, **kw)
+    B = _learner(golden, overlap=True, **kw)
+    for k in range(30):
+        if k == 20:
+            for L in (A, B):
+                L.set_modelA(_rnn_sd(302))
+        monkeypatch.setenv("PONGMI_RNN_SPLIT", "0")
+        A.step()
+        monkeypatch.delenv("PONGMI_RNN_SPLIT")
+        monkeypatch.setenv("PONGMI_RNN_SPLIT_R", split_r)
+        B.step()
+        monkeypatch.delenv("PONGMI_RNN_SPLIT_R")
+    torch.cuda.synchronize()
+    assert torch.equal(A.hA, B.hA) and torch.equal(A.cA, B.cA) and torch.equal(A.aA, B.aA)
+    assert torch.equal(A.learner.params, B.learner.params) and torch.equal(A.trans, B.trans)
+    assert A.counters() == B.counters() and A.learner.stats()["steps"] > 0
+
+
 @pytest.mark.parametrize("change", [None, "modelA"])
 def test_rnn_split_step_after_overlapped_steps(golden, change):
     """The generation controller's save-boundary step (rollout + updates, pongmi.generations

@@ -16,6 +16,7 @@
 #              per-block timeline (tools/env_blocks.py)
 #   bench      python bench.py (the driver's default line)
 #   rnn        python bench.py --workload rnn
+#   rnnab:VAR=v1,v2  the RNN bench (no CPU leg) under each value, interleaved twice
 #   infer      python bench.py --workload infer
 #   prof       rocprofv3 --kernel-trace --stats of the default bench (no CPU legs)
 #   pmc        the FETCH_SIZE / WRITE_SIZE passes of the default bench (tools/pmc_passes.sh)
@@ -75,6 +76,14 @@ run_task() {
       timeout -k 10 300 python3 bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err && echo BENCH_OK ;;
     rnn)
       timeout -k 10 300 python3 bench.py --workload rnn > gpurun_out/${tag}_rnn.json 2> gpurun_out/${tag}_rnn.err && echo RNN_OK ;;
+    rnnab:*)  # rnnab:VAR=v1,v2 — bench.py --workload rnn --no-cpu-baseline under each value, interleaved twice
+      spec=${1#rnnab:}; var=${spec%%=*}; vals=${spec#*=}
+      for rep in 1 2; do
+        for v in ${vals//,/ }; do
+          env $var=$v timeout -k 10 200 python3 bench.py --workload rnn --no-cpu-baseline > gpurun_out/${tag}_rnnab_${var}_${v}_$rep.json 2>/dev/null &&
+              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e6,2), d['ms_per_step'], d['drqn_roofline']['update_us'])" gpurun_out/${tag}_rnnab_${var}_${v}_$rep.json)" || return 1
+        done
+      done ;;
     infer)
       timeout -k 10 300 python3 bench.py --workload infer > gpurun_out/${tag}_infer.json 2> gpurun_out/${tag}_infer.err && echo INFER_OK ;;
     prof)
@@ -132,7 +141,7 @@ run_task() {
       done && echo K1SWEEP_OK ;;
     floorprof)  # tools/k1_floor under rocprofv3 once (round 5's SIGSEGV), fault mapping handler on
       timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_floor -o k -- \
-          ./tools/k1_floor 65536 > gpurun_out/${tag}_prof_floor.log 2>&1; rc=$?
+          ./tools/k1_floor 65536 ${FLOOR_WARM:-100} > gpurun_out/${tag}_prof_floor.log 2>&1; rc=$?
       grep -v amdgpu.ids gpurun_out/${tag}_prof_floor.log | tail -25; echo "k1_floor under rocprofv3 rc=$rc"; [ $rc -eq 0 ] ;;
     mstamps)  # k_learn_multi's per-update phase timeline (tools/multi_stamps.py, U = 64): diag build, then the
               # PM_DIAG_NOWAIT build (no vmcnt(0) waits at the stamps)

@@ -8,7 +8,7 @@
 //               staging), nothing loaded
 //   copy        loads + stores, the state stored back unchanged: K1 minus the serve draw and tick
 // Run it bare (graph events) and under rocprofv3 --kernel-trace --stats (per-launch durations).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/k1_floor.hip -o tools/k1_floor && ./tools/k1_floor [n]
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/k1_floor.hip -o tools/k1_floor && ./tools/k1_floor [n [warm]]
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
 #include <signal.h>
@@ -235,6 +235,7 @@ static double graph_us(const Graph& gr, hipStream_t st, int per_graph = 50, int 
 
 int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 65536;
+    const int warm = argc > 2 ? atoi(argv[2]) : 100;  // graph replays before each timed interval
     if (n <= 0 || n % 256) { fprintf(stderr, "n must be a positive multiple of 256\n"); return 2; }
     struct sigaction sa;
     memset(&sa, 0, sizeof(sa));
@@ -276,7 +277,7 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; ++rep)
         for (int j = 0; j < nk; ++j) {
             const auto& k = ks[j];
-            const double us = graph_us(gs[j], st);
+            const double us = graph_us(gs[j], st, 50, 40, warm);
             printf("{\"n\": %d, \"rep\": %d, \"kernel\": \"%s\", \"graph_us\": %.3f, \"bytes\": %.0f, \"frac_of_8TBs\": %.4f}\n",
                    n, rep, k.name, us, k.bytes, k.bytes / (us * 1e-6) / 8e12);
             fflush(stdout);

@@ -668,6 +668,20 @@ __device__ __forceinline__ void derive_weights(const pm_selfplay& sp, ApplySmem&
     heads_to_frags(sm.heads[2], lh + 264);
 }
 
+// derive_weights for an update of k_learn_multi that is not the launch's last: only what the next
+// update reads, from LDS to LDS — the next update's modelB heads (fresh noise) and targetB heads.
+// The acting weights and every global copy follow from the last update alone.
+__device__ __forceinline__ void derive_weights_lds(ApplySmem& sm) {
+    const int t = threadIdx.x;
+    const int g = (t - 256) >> 8, u = (t - 256) & 255;
+    if (t >= 256 && g == 1) {
+        fold_heads_from(sm.hp, nullptr, sm.ntrain, PM_FOLD_TRAIN_FRESH, sm.heads[1], nullptr, u, 256);
+    } else if (t >= 256 && g == 2) {
+        fold_heads_from(sm.tmu, nullptr, nullptr, PM_FOLD_EVAL, sm.heads[2], nullptr, u, 256);
+    }
+    __syncthreads();
+}
+
 // Both noise draws at once, half of the block each.
 __device__ __forceinline__ void gen_both_noises(const pm_selfplay& sp, ApplySmem& sm, uint64_t act_ctr,
                                                 uint64_t train_ctr) {
@@ -692,7 +706,7 @@ __device__ __forceinline__ void gen_both_noises_on(const pm_selfplay& sp, ApplyS
 // while the callers' loads were in flight). Two parts: apply_adam (per-thread, no barrier: the fused
 // learner runs it beside the sum-tree's level-2 refresh) and apply_finish (behind a barrier).
 // torch.optim.Adam (single-tensor path) on head parameter k with gradient g (summed over shards).
-__device__ __forceinline__ void adam_one(const pm_selfplay& sp, ApplySmem& sm, int k, float gsum) {
+__device__ __forceinline__ void adam_one(const pm_selfplay& sp, ApplySmem& sm, int k, float gsum, bool store = true) {
     const float step_size = sm.ak[0], bc2s = sm.ak[1];  // adam_consts, published before a barrier
     const float g = gsum / (float)sp.world;
     float m = sm.m[k], v = sm.v[k], p = sm.hp[k];
@@ -700,9 +714,11 @@ __device__ __forceinline__ void adam_one(const pm_selfplay& sp, ApplySmem& sm, i
     v = v * (float)sp.beta2 + (float)(1.0 - sp.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1-beta2)
     const float denom = sqrtf(v) / bc2s + (float)sp.adam_eps;
     p = p - step_size * (m / denom);
-    sp.paramsB[PM_QNET_HEAD_OFF + k] = p;
-    sp.adam_m[k] = m;
-    sp.adam_v[k] = v;
+    if (store) {  // k_learn_multi keeps all but its last update's state in LDS only
+        sp.paramsB[PM_QNET_HEAD_OFF + k] = p;
+        sp.adam_m[k] = m;
+        sp.adam_v[k] = v;
+    }
     sm.hp[k] = p;
     sm.m[k] = m;  // k_learn_multi runs the next update from LDS
     sm.v[k] = v;
@@ -2062,7 +2078,7 @@ __device__ __forceinline__ void noise_to_eps(const float* noise, float* eps) {
 // materialise it in scratch and read every field from there (720 -> 204 B of scratch per lane,
 // 32.6 -> 34.3 M env-steps/s at U = 64, r5ai).
 __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, int64_t size, int64_t nb, int64_t c_pos,
-                                          uint64_t c_step) {
+                                          uint64_t c_step, bool final) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
     const PerTree tree = per_tree(sp.per_work, sp.cap);
     PM_STAMP(100);
@@ -2193,7 +2209,7 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
                     sm.qv[j][4] = q2[0]; sm.qv[j][5] = q2[1]; sm.qv[j][6] = q2[2];
                     sm.sidx[j] = id;
                     sm.pa[j] = pa;
-                    sp.idx[j] = id;
+                    if (final) sp.idx[j] = id;
                 } else {
                     sm.qv[j][3] = rb[0];
                     sm.qv[j][7] = rb[1];
@@ -2211,7 +2227,7 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
     // the IS weights (size * P(i))^-beta, one fp64 pow per lane on the batch's waves only (every
     // wave running it for its 16 samples cost ~3 us of VALU issue)
     const float wraw = act ? (float)pow((double)size * (sm.pa[t] / total), -beta_of(sp, frame)) : 0.f;
-    if (act) sp.isw[t] = wraw;
+    if (act && final) sp.isw[t] = wraw;
     const int64_t id = act ? sm.sidx[t] : 0;
     {
         const float m = wave_max(wraw);
@@ -2315,8 +2331,8 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
                                                  : P_AWEP - PM_QNET_EPS_OFF + a * 64 + col];
         gs[kmu] = g;
         gs[ksg] = gsg;
-        adam_one(sp, sm.ap, kmu, g);
-        adam_one(sp, sm.ap, ksg, gsg);
+        adam_one(sp, sm.ap, kmu, g, final);
+        adam_one(sp, sm.ap, ksg, gsg, final);
     } else if (t < 260) {
         const int k = t - 256;
         float g = 0.f;
@@ -2326,8 +2342,8 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
         const float gsg = g * sm.eps_tr[k == 0 ? P_VBEP - PM_QNET_EPS_OFF : P_ABEP - PM_QNET_EPS_OFF + k - 1];
         gs[kmu] = g;
         gs[ksg] = gsg;
-        adam_one(sp, sm.ap, kmu, g);
-        adam_one(sp, sm.ap, ksg, gsg);
+        adam_one(sp, sm.ap, kmu, g, final);
+        adam_one(sp, sm.ap, ksg, gsg, final);
     }
     PM_STAMP(115);
     {
@@ -2341,7 +2357,8 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // level-1 stores land before level 2 reads them
     __syncthreads();
     PM_STAMP(107);
-    for (int k = t; k < kGradN + 2; k += kLearn) sp.grad[k] = sm.ap.g[k];
+    if (final)
+        for (int k = t; k < kGradN + 2; k += kLearn) sp.grad[k] = sm.ap.g[k];
     // ---- phase 5: level-2 nodes of the scatter (global and the LDS copy)
     if (act && sm.hwin[slot] == t) {
         const int64_t ch = id / PER_CHUNK;
@@ -2361,13 +2378,18 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
         __syncthreads();
     }
     PM_STAMP(108);
-    derive_weights(sp, sm.ap);  // w_B, learn_heads (global), modelB's eps buffers <- the acting noise
-    __syncthreads();
+    if (final) {
+        derive_weights(sp, sm.ap);  // w_B, learn_heads (global), modelB's eps buffers <- the acting noise
+        __syncthreads();
+    } else {
+        derive_weights_lds(sm.ap);
+    }
     PM_STAMP(109);
     heads_to_frags(sm.ap.heads[1], sm.hf[0]);
     heads_to_frags(sm.ap.heads[2], sm.hf[1]);
     noise_to_eps(sm.ap.ntrain, sm.eps_tr);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tree's stores land before the next descent
+    // no vmcnt(0) here: the next update's global reads (level-1 nodes, leaves) see stores that were
+    // drained at phases 3 / 4; its LDS state is complete at this barrier
     __syncthreads();
 }
 
@@ -2397,7 +2419,7 @@ __global__ __launch_bounds__(kLearn, 1) void k_learn_multi(const pm_selfplay sp,
         reinterpret_cast<uint32_t*>(&sm.sp)[k] = reinterpret_cast<const uint32_t*>(&sp)[k];
     __syncthreads();
 
-    for (int u = 1; u < updates; ++u) multi_update(sm.sp, sm, size, nb, c_pos, c_step);
+    for (int u = 1; u < updates; ++u) multi_update(sm.sp, sm, size, nb, c_pos, c_step, u == updates - 1);
     if (t == 0) {
         c->train_steps = sm.ts;
         c->frame_idx = sm.frame;

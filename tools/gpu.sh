@@ -30,6 +30,7 @@
 #   k1sweep    K1 events + rocprofv3 kernel traces at 65 536 .. 4 194 304 arenas
 #   floorprof  tools/k1_floor under rocprofv3 (round 5 SIGSEGV check)
 #   mstamps    k_learn_multi per-update phase stamps (diag and PM_DIAG_NOWAIT builds)
+#   u64        bench.py --updates-per-step 64 (k_learn_multi), us per update
 #   train      bench.py --workload train (one config.yaml generation try, replay ratio 1)
 #   gpus2      bench.py --gpus 2 must refuse on a 1-GPU box
 #   pytest:<path>[::sel]  one test file / selection
@@ -149,6 +150,9 @@ run_task() {
           grep -v amdgpu.ids gpurun_out/${tag}_mstamps.txt &&
       PONGMI_DIAG_LIB=$PWD/pingpong-selfplay-ai_amd/pongmi/libpongmi_diag_nw.so timeout -k 10 180 python3 tools/multi_stamps.py \
           --U 64 > gpurun_out/${tag}_mstamps_nw.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_mstamps_nw.txt ;;
+    u64)  # SURVEY 8d's U = 64 stress line (k_learn_multi), no CPU legs
+      timeout -k 10 300 python3 bench.py --updates-per-step 64 --no-cpu-baseline > gpurun_out/${tag}_u64.json 2> gpurun_out/${tag}_u64.err &&
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('u64', d['value'], d['us_per_update'])" gpurun_out/${tag}_u64.json ;;
     train)  # one config.yaml generation try at replay ratio 1 (bench.py --workload train)
       timeout -k 10 300 python3 bench.py --workload train > gpurun_out/${tag}_train.json 2> gpurun_out/${tag}_train.err &&
           cat gpurun_out/${tag}_train.json && echo TRAIN_OK ;;

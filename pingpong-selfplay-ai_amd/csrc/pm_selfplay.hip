@@ -2078,7 +2078,7 @@ __device__ __forceinline__ void noise_to_eps(const float* noise, float* eps) {
 // materialise it in scratch and read every field from there (720 -> 204 B of scratch per lane,
 // 32.6 -> 34.3 M env-steps/s at U = 64, r5ai).
 __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, int64_t size, int64_t nb, int64_t c_pos,
-                                          uint64_t c_step, bool final) {
+                                          uint64_t c_step, bool final, bool early_pow) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
     const PerTree tree = per_tree(sp.per_work, sp.cap);
     PM_STAMP(100);
@@ -2188,6 +2188,11 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
 #pragma unroll
             for (int e = 0; e < 32; ++e) xs[e] = xn[e];
         }
+        // early_pow (PONGMI_MULTI_EARLYPOW): the sample's IS weight on its lane 0 here, while the row
+        // loads are in flight, and the wave's max of them before the barrier below (instead of a pow
+        // pass on the batch's waves after it, then a max, then a barrier)
+        float wr = 0.f;
+        if (early_pow && q == 0 && j < B) wr = (float)pow((double)size * (pa / total), -beta_of(sp, frame));
 #ifdef PM_DIAG
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         PM_STAMP(117);
@@ -2209,6 +2214,7 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
                     sm.qv[j][4] = q2[0]; sm.qv[j][5] = q2[1]; sm.qv[j][6] = q2[2];
                     sm.sidx[j] = id;
                     sm.pa[j] = pa;
+                    sm.sw[j] = wr;
                     if (final) sp.idx[j] = id;
                 } else {
                     sm.qv[j][3] = rb[0];
@@ -2218,6 +2224,10 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
                 sm.qv[j][8] = q1[0]; sm.qv[j][9] = q1[1]; sm.qv[j][10] = q1[2];
             }
         }
+        if (early_pow) {  // block-uniform
+            const float m = wave_max(wr);
+            if (lane == 0) sm.red[wv][0] = m;
+        }
     }
     __syncthreads();
     PM_STAMP(102);
@@ -2226,18 +2236,21 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
     const bool act = t < B;
     // the IS weights (size * P(i))^-beta, one fp64 pow per lane on the batch's waves only (every
     // wave running it for its 16 samples cost ~3 us of VALU issue)
-    const float wraw = act ? (float)pow((double)size * (sm.pa[t] / total), -beta_of(sp, frame)) : 0.f;
-    if (act && final) sp.isw[t] = wraw;
-    const int64_t id = act ? sm.sidx[t] : 0;
-    {
+    float wraw;
+    if (early_pow) {
+        wraw = act ? sm.sw[t] : 0.f;
+    } else {
+        wraw = act ? (float)pow((double)size * (sm.pa[t] / total), -beta_of(sp, frame)) : 0.f;
         const float m = wave_max(wraw);
         if (lane == 0) sm.red[wv][0] = m;
+        __syncthreads();
     }
-    __syncthreads();
+    if (act && final) sp.isw[t] = wraw;
+    const int64_t id = act ? sm.sidx[t] : 0;
     PM_STAMP(103);
     float wmax = sm.red[0][0];
     for (int w = 1; w < 16; ++w) wmax = fmaxf(wmax, sm.red[w][0]);
-    __syncthreads();
+    // no barrier: the TD phase below writes sm.red[.][1..6], never the [.][0] just read
     PM_STAMP(104);
     // ---- k_learn phase 2: double-DQN targets, loss, priorities, bias grads
     float lossp = 0.f, prio = 0.f;
@@ -2393,7 +2406,7 @@ __device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, 
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kLearn, 1) void k_learn_multi(const pm_selfplay sp, int updates) {
+__global__ __launch_bounds__(kLearn, 1) void k_learn_multi(const pm_selfplay sp, int updates, int mflags) {
     __shared__ __attribute__((aligned(16))) MultiSmem sm;
     const int t = threadIdx.x, B = sp.batch;
     const PerTree tree = per_tree(sp.per_work, sp.cap);
@@ -2419,7 +2432,7 @@ __global__ __launch_bounds__(kLearn, 1) void k_learn_multi(const pm_selfplay sp,
         reinterpret_cast<uint32_t*>(&sm.sp)[k] = reinterpret_cast<const uint32_t*>(&sp)[k];
     __syncthreads();
 
-    for (int u = 1; u < updates; ++u) multi_update(sm.sp, sm, size, nb, c_pos, c_step, u == updates - 1);
+    for (int u = 1; u < updates; ++u) multi_update(sm.sp, sm, size, nb, c_pos, c_step, u == updates - 1, mflags & 1);
     if (t == 0) {
         c->train_steps = sm.ts;
         c->frame_idx = sm.frame;
@@ -2719,7 +2732,9 @@ extern "C" int pm_selfplay_step_multi(const pm_selfplay* sp, int32_t updates, vo
     if ((rc = launch_learn(sp, true, st, PM_UPD_FIRST))) return rc;
     if ((rc = pm_selfplay_apply_ex(sp, PM_UPD_FIRST, stream))) return rc;
     if (multi_ok(sp)) {  // updates 1..U-1 in one single-workgroup launch
-        pm_launch(PM_TIMER_LEARN_MULTI, k_learn_multi, dim3(1), dim3(kLearn), st, *sp, (int)updates);
+        const char* ep = getenv("PONGMI_MULTI_EARLYPOW");  // A/B, read per launch; bit-identical either way
+        const int mflags = ep && *ep ? (atoi(ep) != 0) : 0;
+        pm_launch(PM_TIMER_LEARN_MULTI, k_learn_multi, dim3(1), dim3(kLearn), st, *sp, (int)updates, mflags);
         PM_LAUNCHED("k_learn_multi");
         return pm_selfplay_commit(sp, stream);
     }

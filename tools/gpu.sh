@@ -31,6 +31,7 @@
 #   floorprof  tools/k1_floor under rocprofv3 (round 5 SIGSEGV check)
 #   mstamps    k_learn_multi per-update phase stamps (diag and PM_DIAG_NOWAIT builds)
 #   u64        bench.py --updates-per-step 64 (k_learn_multi), us per update
+#   u64ab:VAR=v1,v2  the U = 64 line under each value, interleaved twice
 #   train      bench.py --workload train (one config.yaml generation try, replay ratio 1)
 #   gpus2      bench.py --gpus 2 must refuse on a 1-GPU box
 #   pytest:<path>[::sel]  one test file / selection
@@ -153,6 +154,14 @@ run_task() {
     u64)  # SURVEY 8d's U = 64 stress line (k_learn_multi), no CPU legs
       timeout -k 10 300 python3 bench.py --updates-per-step 64 --no-cpu-baseline > gpurun_out/${tag}_u64.json 2> gpurun_out/${tag}_u64.err &&
           python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('u64', d['value'], d['us_per_update'])" gpurun_out/${tag}_u64.json ;;
+    u64ab:*)  # u64ab:VAR=v1,v2 — the U = 64 line under each value, interleaved twice
+      spec=${1#u64ab:}; var=${spec%%=*}; vals=${spec#*=}
+      for rep in 1 2; do
+        for v in ${vals//,/ }; do
+          env $var=$v timeout -k 10 200 python3 bench.py --updates-per-step 64 --no-cpu-baseline > gpurun_out/${tag}_u64ab_${var}_${v}_$rep.json 2>/dev/null &&
+              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e6,2), d['us_per_update'])" gpurun_out/${tag}_u64ab_${var}_${v}_$rep.json)" || return 1
+        done
+      done ;;
     train)  # one config.yaml generation try at replay ratio 1 (bench.py --workload train)
       timeout -k 10 300 python3 bench.py --workload train > gpurun_out/${tag}_train.json 2> gpurun_out/${tag}_train.err &&
           cat gpurun_out/${tag}_train.json && echo TRAIN_OK ;;

@@ -169,8 +169,8 @@ run_task() {
       timeout -k 10 120 python3 bench.py --gpus 2 --no-cpu-baseline > gpurun_out/${tag}_gpus2.json 2>&1; rc=$?
       cat gpurun_out/${tag}_gpus2.json; [ $rc -eq 2 ] && echo GPUS2_REFUSED_OK ;;
     pytest:*)
-      sel=${1#pytest:}
-      timeout -k 10 400 $PYT "$sel" > gpurun_out/${tag}_pytest.log 2>&1 && tail -1 gpurun_out/${tag}_pytest.log ;;
+      sel=${1#pytest:}; lg=gpurun_out/${tag}_pytest_$(basename "${sel//::/_}" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-60).log
+      timeout -k 10 400 $PYT -s "$sel" > $lg 2>&1 && tail -1 $lg ;;
     *) echo "unknown task $1"; return 2 ;;
   esac
 }

@@ -262,8 +262,25 @@ def time_scalar_dropin(seconds=1.0):
     for j in range(k):
         collide_sphere_with_moving_plane(-0.04, 0.01 * (j % 7), 0.03, 1.5, 1.0, 0.6, 1.0, 0.03)
     dc = time.perf_counter() - t1
+    # round 5's drop-in step for comparison: the batch env at n = 1 (actions copied to the device,
+    # K1, the outputs gathered and copied back)
+    from pongmi.env import PongEnv2PBatch
+    b = PongEnv2PBatch(1, **ENV_KW)
+    b.reset()
+    for _ in range(50):
+        (oA, oB), (rA, rB), dn, _ = b.step(torch.tensor([1], dtype=torch.int8), torch.tensor([1], dtype=torch.int8))
+    k2 = 0
+    t2 = time.perf_counter()
+    while time.perf_counter() - t2 < seconds / 2:
+        aA = torch.tensor([rng.randint(0, 2)], dtype=torch.int8)
+        aB = torch.tensor([rng.randint(0, 2)], dtype=torch.int8)
+        (oA, oB), (rA, rB), dn, _ = b.step(aA, aB)
+        torch.cat([oA[0], oB[0], rA, rB, dn.float()]).cpu().numpy()
+        k2 += 1
+    db = time.perf_counter() - t2
     return {"env_us_per_step": round(dt / steps * 1e6, 2), "env_steps_per_s": round(steps / dt, 1), "steps": steps,
             "resets": resets, "collide_us_per_call": round(dc / k * 1e6, 2),
+            "round5_dropin_us_per_step": round(db / k2 * 1e6, 2),
             "reference_python_us_per_step": 10.6,
             "note": "PongEnv2P drop-in, random vs random with reset on done, wall time incl. the host's randint "
                     "draws; one launch per step / reset, results polled from host-mapped memory"}

@@ -2077,7 +2077,10 @@ __device__ __forceinline__ void noise_to_eps(const float* noise, float* eps) {
 // LDS copy (MultiSmem::sp): a reference to the kernel-argument struct itself made the compiler
 // materialise it in scratch and read every field from there (720 -> 204 B of scratch per lane,
 // 32.6 -> 34.3 M env-steps/s at U = 64, r5ai).
-__device__ __noinline__ void multi_update(const pm_selfplay& sp, MultiSmem& sm, int64_t size, int64_t nb, int64_t c_pos,
+#ifndef PM_MULTI_INLINE
+#define PM_MULTI_INLINE __noinline__
+#endif
+__device__ PM_MULTI_INLINE void multi_update(const pm_selfplay& sp, MultiSmem& sm, int64_t size, int64_t nb, int64_t c_pos,
                                           uint64_t c_step, bool final, bool early_pow) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, B = sp.batch;
     const PerTree tree = per_tree(sp.per_work, sp.cap);

@@ -143,8 +143,8 @@ run_task() {
       done && echo K1SWEEP_OK ;;
     floorprof)  # tools/k1_floor under rocprofv3 once (round 5's SIGSEGV), fault mapping handler on
       timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_floor -o k -- \
-          ./tools/k1_floor 65536 ${FLOOR_WARM:-100} > gpurun_out/${tag}_prof_floor.log 2>&1; rc=$?
-      grep -v amdgpu.ids gpurun_out/${tag}_prof_floor.log | tail -25; echo "k1_floor under rocprofv3 rc=$rc"; [ $rc -eq 0 ] ;;
+          ./tools/k1_floor 65536 ${FLOOR_WARM:-100} > gpurun_out/${tag}_prof_floor${K1F_ONLY:+_$K1F_ONLY}${K1F_NO16:+_no16}.log 2>&1; rc=$?
+      grep -v amdgpu.ids gpurun_out/${tag}_prof_floor${K1F_ONLY:+_$K1F_ONLY}${K1F_NO16:+_no16}.log | tail -25; echo "k1_floor under rocprofv3 rc=$rc"; [ $rc -eq 0 ] ;;
     mstamps)  # k_learn_multi's per-update phase timeline (tools/multi_stamps.py, U = 64): diag build, then the
               # PM_DIAG_NOWAIT build (no vmcnt(0) waits at the stamps)
       timeout -k 10 180 python3 tools/multi_stamps.py --U 64 > gpurun_out/${tag}_mstamps.txt 2>&1 &&

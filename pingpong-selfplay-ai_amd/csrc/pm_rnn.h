@@ -328,7 +328,10 @@ __device__ __forceinline__ void rnn_group(const float* __restrict__ w, float* ri
 // the four F2 tiles (the gates' feature K-steps), the four gates of a hidden block (the cell, which
 // every wave then evaluates identically, so each holds h' as the head stage's B operand), and the
 // four shared-head tiles (the dueling heads, wave 0). 38 stages of 16 MFMAs instead of 64.
-constexpr int kSplitAhead = 4;
+#ifndef PM_SPLIT_AHEAD
+#define PM_SPLIT_AHEAD 4
+#endif
+constexpr int kSplitAhead = PM_SPLIT_AHEAD;  // stages of A operands in flight per wave
 __device__ __forceinline__ void piece_load(const float* __restrict__ w, int s, int lane, float4 (&a)[4]) {
     const float4* src = reinterpret_cast<const float4*>(stage_piece(w, s, threadIdx.x >> 6)) + lane;
 #pragma unroll

@@ -82,8 +82,8 @@ run_task() {
       spec=${1#rnnab:}; var=${spec%%=*}; vals=${spec#*=}
       for rep in 1 2; do
         for v in ${vals//,/ }; do
-          env $var=$v timeout -k 10 200 python3 bench.py --workload rnn --no-cpu-baseline > gpurun_out/${tag}_rnnab_${var}_${v}_$rep.json 2>/dev/null &&
-              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e6,2), d['ms_per_step'], d['drqn_roofline']['update_us'])" gpurun_out/${tag}_rnnab_${var}_${v}_$rep.json)" || return 1
+          env $var=$v timeout -k 10 200 python3 bench.py --workload rnn --no-cpu-baseline > gpurun_out/${tag}_rnnab_${var}_${v//\//_}_$rep.json 2>/dev/null &&
+              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e6,2), d['ms_per_step'], d['drqn_roofline']['update_us'])" gpurun_out/${tag}_rnnab_${var}_${v//\//_}_$rep.json)" || return 1
         done
       done ;;
     infer)
@@ -158,8 +158,8 @@ run_task() {
       spec=${1#u64ab:}; var=${spec%%=*}; vals=${spec#*=}
       for rep in 1 2; do
         for v in ${vals//,/ }; do
-          env $var=$v timeout -k 10 200 python3 bench.py --updates-per-step 64 --no-cpu-baseline > gpurun_out/${tag}_u64ab_${var}_${v}_$rep.json 2>/dev/null &&
-              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e6,2), d['us_per_update'])" gpurun_out/${tag}_u64ab_${var}_${v}_$rep.json)" || return 1
+          env $var=$v timeout -k 10 200 python3 bench.py --updates-per-step 64 --no-cpu-baseline > gpurun_out/${tag}_u64ab_${var}_${v//\//_}_$rep.json 2>/dev/null &&
+              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e6,2), d['us_per_update'])" gpurun_out/${tag}_u64ab_${var}_${v//\//_}_$rep.json)" || return 1
         done
       done ;;
     train)  # one config.yaml generation try at replay ratio 1 (bench.py --workload train)

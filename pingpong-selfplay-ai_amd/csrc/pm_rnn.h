@@ -74,7 +74,7 @@ constexpr int kRingStages = 2 + 4 * 9;
 
 #ifdef PM_DIAG
 // diagnostic builds: s_memrealtime after each ring barrier of a block's first group (blocks < 1024)
-static __device__ unsigned long long pm_diag_stage[48][1024];
+static __device__ unsigned long long pm_diag_stage[64][1024];  // [0, 48) rnn_group, [48, 64) rnn_tile_split
 #define PM_STG(k)                                                                                   \
     do {                                                                                            \
         if (threadIdx.x == 0 && blockIdx.x < 1024 && g == 0) pm_diag_stage[(k)][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
@@ -84,7 +84,15 @@ static __device__ unsigned long long pm_diag_stage[48][1024];
     do {                                                                                            \
         if (threadIdx.x == 0 && blockIdx.x < 1024 && g == 0) pm_diag_stage[(k)][blockIdx.x] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+// split tiles: slot 48 + k of the block, thread 0 (blocks < 1024)
+#define PM_SSTG(k)                                                                                  \
+    do {                                                                                            \
+        if (threadIdx.x == 0 && blockIdx.x < 1024) pm_diag_stage[48 + (k)][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 #else
+#define PM_SSTG(k) \
+    do {           \
+    } while (0)
 #define PM_STG(k) \
     do {          \
     } while (0)
@@ -370,6 +378,7 @@ __device__ __forceinline__ void rnn_tile_split(const float* __restrict__ w, Spli
     const float* hr = (hin ? hin : hst) + (size_t)arena * 128;
     const float* cr = (cin ? cin : cst) + (size_t)arena * 128;
     const bool zero = reset != nullptr && reset[arena] != 0;
+    PM_SSTG(0);
     float4 pa[kSplitAhead][4];  // stage s's A operands in pa[s % kSplitAhead] (static after unrolling)
 #pragma unroll
     for (int s = 0; s < kSplitAhead; ++s) piece_load(w, s, lane, pa[s]);
@@ -414,8 +423,10 @@ __device__ __forceinline__ void rnn_tile_split(const float* __restrict__ w, Spli
     add_bias_lds(hw + kHwB2 + (p * 2 + h) * 16, acc);
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = relu(acc[r]);
+    PM_SSTG(1);
     xch_put(x, 0, p, lane, acc);
     __syncthreads();
+    PM_SSTG(2);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -437,8 +448,10 @@ __device__ __forceinline__ void rnn_tile_split(const float* __restrict__ w, Spli
         }
         add_bias_lds(hw + kHwBG + ((p * 4 + m) * 2 + h) * 16, acc);
         const int buf = (m + 1) & 1;
+        PM_SSTG(3 + 2 * m);
         xch_put(x, buf, p, lane, acc);
         __syncthreads();
+        PM_SSTG(4 + 2 * m);
         float hb[16];
         {
             float cn[16];
@@ -468,8 +481,10 @@ __device__ __forceinline__ void rnn_tile_split(const float* __restrict__ w, Spli
     }
     // ---- the dueling heads from the four shared-head tiles, in rnn_group's chain order (wave 0)
     add_bias_lds(hw + kHwBS + (p * 2 + h) * 16, sacc);
+    PM_SSTG(11);
     xch_put(x, 1, p, lane, sacc);
     __syncthreads();
+    PM_SSTG(12);
     if (p != 0) return;
     float v = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll
@@ -496,6 +511,7 @@ __device__ __forceinline__ void rnn_tile_split(const float* __restrict__ w, Spli
     const float mean = ((a0 + a1) + a2) / 3.0f;
     const float q[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
     out(arena, valid && h == 0, q);
+    PM_SSTG(13);
 }
 
 }  // namespace pm

@@ -416,11 +416,11 @@ extern "C" int pm_rnn_act(const float* w_opp, const int32_t* opp_id, int32_t n_o
 }
 
 #ifdef PM_DIAG
-extern "C" int pm_diag_read_rnn(uint64_t* out) {  // [48][1024] ring-stage stamps
+extern "C" int pm_diag_read_rnn(uint64_t* out) {  // [64][1024] ring-stage stamps (48.. split tiles)
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pm_diag_stage), sizeof(pm_diag_stage));
 }
 extern "C" int pm_diag_clear_rnn(void) {
-    static unsigned long long z[48][1024];
+    static unsigned long long z[64][1024];
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(pm_diag_stage), z, sizeof(z));
 }
 #endif

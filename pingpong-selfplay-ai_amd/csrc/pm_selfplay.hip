@@ -2087,6 +2087,7 @@ __device__ PM_MULTI_INLINE void multi_update(const pm_selfplay& sp, MultiSmem& s
     PM_STAMP(100);
     const int64_t ts = sm.ts, frame = sm.frame + 1;  // frame_idx += 1 before sampling (:136)
     for (int k = t; k < 512; k += kLearn) { sm.hkey[k] = kHashEmpty; sm.hwin[k] = -1; }
+    PM_STAMP(119);
     // ---- PER sample (per_sample_block, no pending push): level 2 over the LDS chunk sums
     {
         double run[4] = {0.0, 0.0, 0.0, 0.0}, acc = 0.0, incl = 0.0;
@@ -2098,11 +2099,14 @@ __device__ PM_MULTI_INLINE void multi_update(const pm_selfplay& sp, MultiSmem& s
                 run[e] = acc;
             }
         }
+        PM_STAMP(120);
         incl = wave_incl_scan(acc, lane);
         double excl = __shfl_up(incl, 1);
         if (lane == 0) excl = 0.0;
         if (lane == 63) sm.wsum[wv] = incl;
+        PM_STAMP(121);
         __syncthreads();
+        PM_STAMP(122);
         if (t < 256) {
             double wb = 0.0;
             for (int w = 0; w < wv; ++w) wb += sm.wsum[w];
@@ -2407,6 +2411,7 @@ __device__ PM_MULTI_INLINE void multi_update(const pm_selfplay& sp, MultiSmem& s
     // no vmcnt(0) here: the next update's global reads (level-1 nodes, leaves) see stores that were
     // drained at phases 3 / 4; its LDS state is complete at this barrier
     __syncthreads();
+    PM_STAMP(124);
 }
 
 __global__ __launch_bounds__(kLearn, 1) void k_learn_multi(const pm_selfplay sp, int updates, int mflags) {

@@ -32,6 +32,7 @@
 #   mstamps    k_learn_multi per-update phase stamps (diag and PM_DIAG_NOWAIT builds)
 #   u64        bench.py --updates-per-step 64 (k_learn_multi), us per update
 #   u64ab:VAR=v1,v2  the U = 64 line under each value, interleaved twice
+#   sstamps    configs[4] side-A whole-group blocks / split tiles by phase (diag build)
 #   train      bench.py --workload train (one config.yaml generation try, replay ratio 1)
 #   gpus2      bench.py --gpus 2 must refuse on a 1-GPU box
 #   pytest:<path>[::sel]  one test file / selection
@@ -162,6 +163,8 @@ run_task() {
               echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e6,2), d['us_per_update'])" gpurun_out/${tag}_u64ab_${var}_${v//\//_}_$rep.json)" || return 1
         done
       done ;;
+    sstamps)  # configs[4]'s side-A launch: whole-group blocks and split tiles by phase (tools/split_stamps.py, diag build)
+      timeout -k 10 240 python3 tools/split_stamps.py > gpurun_out/${tag}_split_stamps.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_split_stamps.txt ;;
     train)  # one config.yaml generation try at replay ratio 1 (bench.py --workload train)
       timeout -k 10 300 python3 bench.py --workload train > gpurun_out/${tag}_train.json 2> gpurun_out/${tag}_train.err &&
           cat gpurun_out/${tag}_train.json && echo TRAIN_OK ;;

@@ -20,10 +20,12 @@ NAMES = {111: "  level-2 search done", 112: "  level 1 (16 sub sums)", 113: "  l
          115: "  grads + Adam done", 117: "  rows landed", 118: "  chains done", 116: "  level-1 leaves loaded",
          101: "prefix", 102: "heads (row gather + chains)", 103: "IS weights (pow) + wmax", 104: "wmax",
          105: "TD / hash", 106: "scatter + grad partials", 107: "grads + Adam + level-1 refresh",
-         108: "level 2 + target sync", 109: "derive weights", 100: "next update start"}
+         108: "level 2 + target sync", 109: "derive weights", 100: "next update start",
+         119: "  hash table cleared", 120: "  chunk sums (4 per lane)", 121: "  fp64 wave scan", 122: "  first barrier",
+         124: "update end (last barrier)"}
 
 
-ORDER = [101, 111, 112, 113, 117, 118, 102, 103, 104, 105, 106, 115, 116, 107, 108, 109]
+ORDER = [119, 120, 121, 122, 101, 111, 112, 113, 117, 118, 102, 103, 104, 105, 106, 115, 116, 107, 108, 109, 124]
 
 
 def main():

@@ -49,9 +49,9 @@ def main():
     rnn.q_step(w, x, h, c)
     e1.record()
     torch.cuda.synchronize()
-    buf = (ctypes.c_uint64 * (48 * 1024))()
+    buf = (ctypes.c_uint64 * (64 * 1024))()
     lib.pm_diag_read_rnn(buf)
-    st = np.array(buf[:], dtype=np.int64).reshape(48, 1024)
+    st = np.array(buf[:], dtype=np.int64).reshape(64, 1024)[:48]
     nb = min(1024, (n + 127) // 128)
     st = st[:, :nb]
     # chronological order of the stamps within a group

@@ -34,6 +34,7 @@
 #   u64ab:VAR=v1,v2  the U = 64 line under each value, interleaved twice
 #   sstamps    configs[4] side-A whole-group blocks / split tiles by phase (diag build)
 #   train      bench.py --workload train (one config.yaml generation try, replay ratio 1)
+#   floorbig   tools/k1_floor skeletons at 1 M and 4 M arenas (graph events)
 #   gpus2      bench.py --gpus 2 must refuse on a 1-GPU box
 #   pytest:<path>[::sel]  one test file / selection
 set -o pipefail
@@ -168,6 +169,10 @@ run_task() {
     train)  # one config.yaml generation try at replay ratio 1 (bench.py --workload train)
       timeout -k 10 300 python3 bench.py --workload train > gpurun_out/${tag}_train.json 2> gpurun_out/${tag}_train.err &&
           cat gpurun_out/${tag}_train.json && echo TRAIN_OK ;;
+    floorbig)  # tools/k1_floor (graph events) at 1 M and 4 M arenas: the skeletons' bandwidth beyond the latency regime
+      for n in 1048576 4194304; do
+        timeout -k 10 120 ./tools/k1_floor $n 20 > gpurun_out/${tag}_k1_floor_$n.jsonl 2>&1 && cat gpurun_out/${tag}_k1_floor_$n.jsonl || return 1
+      done ;;
     gpus2)  # bench.py --gpus 2 on a 1-GPU box must refuse (exit 2, an error line), never print a 1-rank line
       timeout -k 10 120 python3 bench.py --gpus 2 --no-cpu-baseline > gpurun_out/${tag}_gpus2.json 2>&1; rc=$?
       cat gpurun_out/${tag}_gpus2.json; [ $rc -eq 2 ] && echo GPUS2_REFUSED_OK ;;

@@ -104,10 +104,10 @@ def pmc_traffic(kernel, profile="r3_pmc.json"):
     """HBM bytes per launch of `kernel` (`name`, or `name@grid` for one of its launch grids) from the
     committed rocprofv3 counter profile (profiles/r3_pmc.json: the default workload;
     profiles/r3_rnn_pmc.json: --workload rnn; profiles/r3_infer_pmc.json: --workload infer, 2 000-step
-    launches), or None. The newest round's profile of the same name (r6_pmc.json, r5_pmc.json, …) wins
+    launches), or None. The newest round's profile of the same name (r5_pmc.json, r4_pmc.json, …) wins
     when it holds the kernel."""
     stem = profile[3:] if profile.startswith("r3_") else profile
-    for name in (f"r6_{stem}", f"r5_{stem}", f"r4_{stem}", profile):
+    for name in (f"r5_{stem}", f"r4_{stem}", profile):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as fh:
                 return json.load(fh)["kernels"][kernel]["hbm_bytes"]
@@ -403,17 +403,10 @@ def drqn_flop(B, T):
     return 2 * (fwd + bwd)
 
 
-def drqn_fused():
-    """The DRQN update's forward + BPTT as one launch (k_dq_fwd, the default) or as k_dq_embed +
-    k_dq_recur (PONGMI_DRQN_FUSED=0, read by libpongmi per call)."""
-    return os.environ.get("PONGMI_DRQN_FUSED", "0").strip() not in ("", "0")
-
-
 def time_drqn_update(D, launches=50):
-    """The DRQN update alone (pm_drqn_update: k_dq_fwd + k_dq_wgrad + k_drqn_apply, or 4 launches with
-    PONGMI_DRQN_FUSED=0) back to back on its last batch after the timed region (HIP events on the
-    stream), and the recurrence launch (k_dq_fwd, embedding included; k_dq_recur) by its own dispatch
-    (pm_timer_arm). Restores nothing: it runs after the measured steps."""
+    """The DRQN update alone (pm_drqn_update, 4 launches) back to back on its last batch after the
+    timed region (HIP events on the stream), and the persistent recurrence k_dq_recur by its own
+    dispatch (pm_timer_arm). Restores nothing: it runs after the measured steps."""
     from pongmi import _lib
     for _ in range(5):
         D.update()
@@ -430,16 +423,14 @@ def time_drqn_update(D, launches=50):
     rec = sum(_lib.timer_read(_lib.PM_TIMER_DRQN) for _ in range(10)) / 10
     flop = drqn_flop(D.batch, D.T)
     achieved = flop / t / 1e12
-    fused = drqn_fused()
-    ks = ("k_dq_fwd",) if fused else ("k_dq_embed", "k_dq_recur")
-    ks += ("k_dq_wgrad", "k_drqn_apply")
+    ks = ("k_dq_embed", "k_dq_recur", "k_dq_wgrad", "k_drqn_apply")
     tr = [pmc_traffic(k, "r3_rnn_pmc.json") for k in ks]
     traffic = round(sum(tr), 1) if all(x is not None for x in tr) and (D.batch, D.T) == (64, 8) else None
-    return {"bound": "mfma", "kernel": f"pm_drqn_update ({' + '.join(ks)}), the whole update",
+    return {"bound": "mfma", "kernel": "pm_drqn_update (k_dq_embed + k_dq_recur + k_dq_wgrad + k_drqn_apply), "
+                                       "the whole update",
             "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "update_us": round(t * 1e6, 2),
-            "recur_us": round(rec * 1e6, 2), "recur_kernel": ks[0] if fused else ks[1],
-            "launches_per_update": len(ks), "flop_per_update": flop,
+            "recur_us": round(rec * 1e6, 2), "launches_per_update": 4, "flop_per_update": flop,
             "batch": D.batch, "T": D.T, "timing": f"HIP events over {launches} back-to-back updates"}
 
 

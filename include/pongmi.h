@@ -335,9 +335,7 @@ int pm_drqn_apply(const pm_drqn *d, void *stream);
  * (no arrival ticket). Its fp64 summation order differs from pm_drqn_apply's per-slice sum, so the two
  * single-replica paths give bit-identical parameters while the clip coefficient clamps to 1 and agree
  * to ~1e-6 relative when the clip is active (each is bitwise to the float32 clip + Adam restatement
- * given its own norm). Round 6: two launches by default — the forward + BPTT with the embedding
- * inside (k_dq_fwd) and the weight gradients with clip + Adam inside (k_dq_wgrad_apply), bit-identical
- * to the four launches that PONGMI_DRQN_FUSED=0 / PONGMI_DRQN_FUSE_APPLY=0 keep (read per call). */
+ * given its own norm). */
 int pm_drqn_update(const pm_drqn *d, void *stream);
 
 /* ---------------------------------------------------------------- QNetRNN self-play (K7) */
@@ -677,7 +675,7 @@ int pm_rnn_selfplay_step_sharded_overlap(const pm_rnn_selfplay* sp, const pm_drq
 #define PM_TIMER_RNN_ACT 2  /* k_rnn_act */
 #define PM_TIMER_ENV_STEP 3 /* k_env_step (K1, pm_env_step) */
 #define PM_TIMER_ROLLOUT 4  /* k_rollout (K9, pm_rollout) */
-#define PM_TIMER_DRQN 5     /* k_dq_fwd (K6: embedding + the persistent recurrence; k_dq_recur when PONGMI_DRQN_FUSED=0) */
+#define PM_TIMER_DRQN 5     /* k_dq_recur (K6: the DRQN update's persistent recurrence, pm_drqn_grads) */
 #define PM_TIMER_LEARN_MULTI 6 /* k_learn_multi: updates 1..U-1 of a vector step (pm_selfplay_step_multi, ABI 23) */
 #define PM_TIMER_N 7
 int pm_timer_arm(int32_t kernel);

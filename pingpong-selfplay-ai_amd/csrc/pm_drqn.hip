@@ -26,8 +26,6 @@
 //
 // Every reduction runs in a fixed order and nothing sums through atomics, so an update is
 // bit-reproducible run to run (the arrival ticket only picks which workgroup does the final sum).
-#include <stdlib.h>
-
 #include "pm_host.h"
 #include "pm_rnn.h"
 
@@ -69,10 +67,6 @@ struct DqArgs {
     float *dP2;  // [128][C0]                 dF2 through F2's ReLU
     float *dP1;  // [64][C0]                  dF1 through F1's ReLU
     float *XT;   // [32][C0]                  obs stream inputs x^T (rows 7..31 zero)
-    float *ZG;   // [3][T][512][B] x2         k_dq_fwd: Zx as granules {value, tag E + kTagZx}
-    float *FG;   // [B][T][192] x2            k_dq_fwd: the obs stream's F2 (rows 0..127), F1 (128..191) as
-                 //                           granules {value, tag E + kTagF} for the dF2 trailer
-    float *NPG;  // [kWgTiles + 1] x4           k_dq_wgrad_apply: the clip norm's fp64 shares as granule pairs
     double* part;
     double* NP;      // [kWgTiles + 1] per-block sums of squares of the final gradient (local_norm)
     int64_t* tstep;
@@ -101,8 +95,7 @@ inline int64_t dq_layout(int B, int T, DqArgs* a, void* work) {
                   oSC = L.add((int64_t)B * 8), oWSE = L.add(2 * 128 * kWsStride), oHWE = L.add(2 * kHwN),
                   oDZH = L.add(C0 * 1024), odP2 = L.add(128 * C0), odP1 = L.add(64 * C0),
                   oXT = L.add(32 * C0), oPart = L.add(2 * kNormBlocks), oNP = L.add(2 * 256), oTs = L.add(4),
-                  oFl = L.add(4), oZG = L.add(3 * C0 * 512 * 2), oFG = L.add(C0 * 192 * 2),
-                  oNPG = L.add(256 * 4);
+                  oFl = L.add(4);
     if (a && work) {
         float* w = static_cast<float*>(work);
         a->B = B; a->T = T; a->nct = (int)nct; a->C0 = (int)C0;
@@ -110,7 +103,6 @@ inline int64_t dq_layout(int B, int T, DqArgs* a, void* work) {
         a->QT = w + oQT; a->DS = w + oDS; a->SR = w + oSR; a->HT = w + oHT; a->SC = w + oSC; a->WSE = w + oWSE;
         a->HWE = w + oHWE; a->DZH = w + oDZH; a->dP2 = w + odP2; a->dP1 = w + odP1; a->XT = w + oXT; a->part = reinterpret_cast<double*>(w + oPart); a->NP = reinterpret_cast<double*>(w + oNP);
         a->tstep = reinterpret_cast<int64_t*>(w + oTs); a->flags = reinterpret_cast<int32_t*>(w + oFl);
-        a->ZG = w + oZG; a->FG = w + oFG; a->NPG = w + oNPG;
     }
     return L.total * 4;
 }
@@ -153,17 +145,6 @@ __device__ __forceinline__ void st_g2(__amdgpu_buffer_rsrc_t r, int byte_off, fl
     const u32x4 q = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
     __builtin_amdgcn_raw_buffer_store_b128(q, r, byte_off, 0, 16 /* sc1 */);
 }
-typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
-// one granule {v, tag}, an 8-byte write-through store
-__device__ __forceinline__ void st_g1(__amdgpu_buffer_rsrc_t r, int byte_off, float v, uint32_t tag) {
-    const u32x2 q = {__float_as_uint(v), tag};
-    __builtin_amdgcn_raw_buffer_store_b64(q, r, byte_off, 0, 16 /* sc1 */);
-}
-__device__ __forceinline__ uint64_t ld_g1(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool tag_is(uint64_t g, uint32_t tag) { return (uint32_t)(g >> 32) == tag; }
-__device__ __forceinline__ float val_of(uint64_t g) { return __uint_as_float((uint32_t)g); }
 // Poll the granule pairs at byte offsets off[i] (16-B aligned, from base) until every tag equals
 // `tag`; v[2i], v[2i+1] get the values. The polls are 8-byte agent-scope atomic loads (sc1): a
 // plain or volatile-flagged buffer load is loop-invariant to the compiler and gets hoisted out of
@@ -392,180 +373,6 @@ __global__ __launch_bounds__(512) void k_dq_embed(DqArgs a) {
     PM_STAMP_T(222, 256);
 }
 
-// ---------------------------------------------------------------- 1 + 2 fused: k_dq_fwd's embedding roles
-// k_dq_fwd (the default; PONGMI_DRQN_FUSED=0 keeps k_dq_embed + k_dq_recur) runs the embedding as the
-// first 3 x nct x T x 2 workgroups of the recurrence launch, so the recurrence's workgroups load Whh
-// while the batch is embedded instead of after a launch boundary. A role workgroup (1024 threads) is
-// one (stream, 32-column tile, step, row half rp): waves 0..3 form F1 and F2 tile w exactly as
-// k_dq_embed's waves 0..3; wave w forms K half w >> 3 of Zx tile m = 8 rp + (w & 7) with k_dq_embed's
-// MFMA sequence, and the halves meet as (half 0 + half 1) + bias: Zx is bit-identical to k_dq_embed's.
-// Everything a later workgroup of the same launch reads leaves as granules (write-through, tagged with
-// the update's epoch): Zx [stream][t][gate row][sequence] (tag E + kTagZx) for the recurrence, and the
-// obs stream's F2 / F1 [sequence][t][192] (tag E + kTagF) for the dF2 trailer's ReLU masks. F2T / F1T /
-// XT stay plain stores: only k_dq_wgrad (the next launch) reads them.
-constexpr uint32_t kTagZx = 100, kTagF = 101;  // beside E + 1 (Q_T) and E + 2 + t (dz, t < 64)
-struct EmbSmem {
-    __attribute__((aligned(16))) float F2s[32][132];
-    float zp[8][16][64];  // the K-half-0 partials of the eight Zx tiles
-};
-
-__device__ __forceinline__ void dq_embed_role(const DqArgs& a, EmbSmem& sm, int bid, uint32_t E) {
-    const int nct = a.nct, T = a.T, B = a.B;
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int rp = bid & 1;
-    bid >>= 1;
-    const int t = bid % T;
-    bid /= T;
-    const int ct = bid % nct, s = bid / nct;
-    const float* P = s == 2 ? a.target : a.params;
-    const int b = ct * 32 + col;
-    const int64_t c = (int64_t)t * B + b;
-    const int m = 8 * rp + (w & 7), kh = w >> 3;
-    DQ_STAMP(229, blockIdx.x == 0);
-    // loads first: the Zx A fragments of this wave's K half (waves 4..15; the F waves 0..3 issue theirs
-    // after F1, under F2's MFMAs, so that F2's operands and these fit 128 registers); x, W1 / b1, W2,
-    // b2 (F waves). The Zx bias of tile m (waves 8..15, which form the final sum) follows the F phase.
-    const float* wr = P + R_P_WIH + (int64_t)(128 * (col >> 3) + 8 * m + (col & 7)) * 128 + 4 * h + 64 * kh;
-    float4 av[8];
-    if (w >= 4)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) av[j] = *reinterpret_cast<const float4*>(wr + 8 * j);
-    float xs[4], f1w[2][4], zb[16];
-    float4 w2v[8];
-    f32x16 f2;
-    if (w < 4) {
-        tile_inputs((s == 0 ? a.obs : a.next) + ((int64_t)b * T + t) * 7, h, xs);
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const int row = 32 * jt + col, kk = 2 * s4 + h;
-                f1w[jt][s4] = P[kk == 0 ? R_P_F1B + row : R_P_F1W + row * 7 + kk - 1];
-            }
-        const float* w2 = P + R_P_F2W + (32 * w + col) * 64 + 4 * h;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) w2v[i] = *reinterpret_cast<const float4*>(w2 + 32 * (i >> 2) + 8 * (i & 3));
-#pragma unroll
-        for (int r = 0; r < 16; ++r) f2[r] = P[R_P_F2B + 32 * w + rho(r) + 4 * h];
-    }
-    if (w < 4) {
-        f32x16 c1[2];
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt) {
-            c1[jt] = f32x16{};
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) c1[jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(f1w[jt][s4], xs[s4], c1[jt], 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) c1[jt][r] = relu(c1[jt][r]);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) av[j] = *reinterpret_cast<const float4*>(wr + 8 * j);
-#pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float4 v = w2v[4 * t2 + i];
-                f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, c1[t2][4 * i + 0], f2, 0, 0, 0);
-                f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, c1[t2][4 * i + 1], f2, 0, 0, 0);
-                f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, c1[t2][4 * i + 2], f2, 0, 0, 0);
-                f2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, c1[t2][4 * i + 3], f2, 0, 0, 0);
-            }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) f2[r] = relu(f2[r]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<float4*>(&sm.F2s[col][32 * w + 8 * i + 4 * h]) =
-                make_float4(f2[4 * i], f2[4 * i + 1], f2[4 * i + 2], f2[4 * i + 3]);
-        if (s == 0 && rp == 0) {  // the obs stream's features: plain for k_dq_wgrad, granules for the trailer
-            // (buffer stores: one 32-bit offset per store instead of a 64-bit address each)
-            const int C0 = a.C0, ci = (int)c;
-            const __amdgpu_buffer_rsrc_t rf = rsrc(a.FG), r2 = rsrc(a.F2T), r1 = rsrc(a.F1T), rx = rsrc(a.XT);
-            const int fo = (b * T + t) * 192;
-            if (w == 0) {
-                if (h) __builtin_amdgcn_raw_buffer_store_b32(xs[0], rx, ci * 4, 0, 0);
-#pragma unroll
-                for (int i = 1; i < 4; ++i) __builtin_amdgcn_raw_buffer_store_b32(xs[i], rx, ((2 * i - 1 + h) * C0 + ci) * 4, 0, 0);
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = 32 * w + rho(r) + 4 * h;
-                __builtin_amdgcn_raw_buffer_store_b32(f2[r], r2, (row * C0 + ci) * 4, 0, 0);
-                st_g1(rf, (fo + row) * 8, f2[r], E + kTagF);
-            }
-#pragma unroll
-            for (int jt = 0; jt < 2; ++jt)
-                if (w == jt)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int row = 32 * jt + rho(r) + 4 * h;
-                        __builtin_amdgcn_raw_buffer_store_b32(c1[jt][r], r1, (row * C0 + ci) * 4, 0, 0);
-                        st_g1(rf, (fo + 128 + row) * 8, c1[jt][r], E + kTagF);
-                    }
-        }
-    }
-    __syncthreads();
-    if (kh)  // the Zx bias, loaded under the MFMAs (live across the F phase it would spill)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int rr = rho(r) + 4 * h;
-            const int g = 128 * (rr >> 3) + 8 * m + (rr & 7);
-            zb[r] = P[R_P_BIH + g] + P[R_P_BHH + g];
-        }
-    f32x16 z = {};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float4 bv = *reinterpret_cast<const float4*>(&sm.F2s[col][64 * kh + 8 * j + 4 * h]);
-        z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, bv.x, z, 0, 0, 0);
-        z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, bv.y, z, 0, 0, 0);
-        z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, bv.z, z, 0, 0, 0);
-        z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, bv.w, z, 0, 0, 0);
-    }
-    if (kh == 0)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sm.zp[w][r][lane] = z[r];
-    __syncthreads();
-    if (kh == 0) return;
-    const __amdgpu_buffer_rsrc_t rz = rsrc(a.ZG);
-    const int zo = ((s * T + t) * 512) * B + b;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rr = rho(r) + 4 * h;
-        const float v = (sm.zp[w & 7][r][lane] + z[r]) + zb[r];  // (K half 0 + K half 1) + bias
-        st_g1(rz, (zo + (128 * (rr >> 3) + 8 * m + (rr & 7)) * B) * 8, v, E + kTagZx);
-    }
-    PM_STAMP_T(230, 512);
-}
-
-// FUSED recurrence workgroups: the effective head weights of their net straight into LDS (k_dq_embed's
-// kEmbEff blocks form them in global memory for the two-launch path): W_S in the padded row image the
-// heads read, then the head vectors. mu + sigma * epsilon (train mode, modelB) or mu (eval, targetB),
-// the same expression as eff_w.
-__device__ __forceinline__ void eff_heads_lds(const float* Pn, bool noisy, float* ws, float* hw) {
-    const int tid = threadIdx.x, row = tid >> 3, c0 = 16 * (tid & 7);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int j = row * 128 + c0 + 4 * i;
-        float4 v = *reinterpret_cast<const float4*>(Pn + R_P_SWMU + j);
-        if (noisy) {
-            const float4 sg = *reinterpret_cast<const float4*>(Pn + R_P_SWSG + j);
-            const float4 ep = *reinterpret_cast<const float4*>(Pn + R_P_SWEP + j);
-            v.x = v.x + sg.x * ep.x; v.y = v.y + sg.y * ep.y; v.z = v.z + sg.z * ep.z; v.w = v.w + sg.w * ep.w;
-        }
-        *reinterpret_cast<float4*>(&ws[row * kWsStride + c0 + 4 * i]) = v;
-    }
-    if (tid < 644) {  // b_S 128 | w_V 128 | w_A 384 | b_V | b_A 3
-        const int v = tid;
-        int mu, sg, ep;
-        if (v < 128) { mu = R_P_SBMU + v; sg = R_P_SBSG + v; ep = R_P_SBEP + v; }
-        else if (v < 256) { mu = R_P_VWMU + v - 128; sg = R_P_VWSG + v - 128; ep = R_P_VWEP + v - 128; }
-        else if (v < 640) { mu = R_P_AWMU + v - 256; sg = R_P_AWSG + v - 256; ep = R_P_AWEP + v - 256; }
-        else if (v == 640) { mu = R_P_VBMU; sg = R_P_VBSG; ep = R_P_VBEP; }
-        else { mu = R_P_ABMU + v - 641; sg = R_P_ABSG + v - 641; ep = R_P_ABEP + v - 641; }
-        hw[v] = eff_w(Pn, mu, sg, ep, noisy);
-    }
-}
-
 // ---------------------------------------------------------------- 2: the recurrence (sequence-private)
 // One workgroup of 1024 threads owns whole sequences: the recurrence h_{t+1} = f(Zx_t + Whh h_t) of a
 // sequence never leaves its CU, so no step waits on another CU (round 3 split the 512 gate rows over
@@ -597,9 +404,7 @@ struct RecurSmem {
     float sr[2][128];                                        // ReLU(S) per column
     float qv[2][4];                                          // V, A0..2 per column
     float dva[4];                                            // dV, dA0..2
-    float hw[kHwN];                                          // k_dq_fwd: this net's effective head vectors
 };
-static_assert(sizeof(EmbSmem) <= sizeof(RecurSmem), "k_dq_fwd's embedding roles use the recurrence's LDS");
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
@@ -636,35 +441,12 @@ __device__ __forceinline__ float reduce_units(float (&p)[16], float (*part)[68],
     return sum8(d);
 }
 
-// Wave-wide: until every lane's granules g[0..N) carry `tag`, re-read them from p[i] after a short
-// sleep (a rare path: the producers finished long before); bounded by hc.limit re-reads like gather.
-template <int N>
-__device__ __forceinline__ void take_g(const uint64_t* const (&p)[N], uint64_t (&g)[N], uint32_t tag, float (&v)[N],
-                                       const HandoffCtl& hc) {
-    for (int it = 0;; ++it) {
-        bool ok = true;
-#pragma unroll
-        for (int i = 0; i < N; ++i) ok = ok && tag_is(g[i], tag);
-        if (__all(ok)) break;
-        if (it >= hc.limit) {
-            if ((threadIdx.x & 63) == 0) void_update(hc);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-        for (int i = 0; i < N; ++i) g[i] = ld_g1(p[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) v[i] = val_of(g[i]);
-}
-
 // The dF2 trailer (workgroups [3B/2, 5B/2), one per sequence): the feature layers' backward of the obs
 // stream, dF2_t = Wih^T dz_t, dP2 = dF2 (F2 > 0), then dF1 = W2^T dP2, dP1 = dF1 (F1 > 0) (k_dq_wgrad
 // forms dW2 = dP2 F1^T and dW1 = dP1 x^T as tiles). Wih sits in registers in Whh's fragment layout,
 // so dF2_t is BPTT's dh product on another matrix; each dz_t arrives from the sequence's obs
 // workgroup as granules (tag E + 2 + t) while that workgroup moves on, so the pass trails BPTT by a
 // hand-off instead of following it. It waits only on lower-indexed workgroups (dispatched first).
-template <bool FUSED>
 __device__ __forceinline__ void dq_df2(const DqArgs& a, RecurSmem& sm, int b, uint32_t E, const HandoffCtl& hc) {
     const int T = a.T, B = a.B;
     const int64_t C0 = a.C0;
@@ -705,19 +487,8 @@ __device__ __forceinline__ void dq_df2(const DqArgs& a, RecurSmem& sm, int b, ui
     float f1p = 0.f;
     for (int t = T - 1; t >= 0; --t) {
         const int64_t cc = (int64_t)t * B + b;
-        float f2, f1;
-        uint64_t fq[2];
-        const uint64_t* fgp[2];
-        if (FUSED) {  // this launch's embedding roles wrote them: granules (tag E + kTagF), taken below
-            const uint64_t* fg = reinterpret_cast<const uint64_t*>(a.FG) + (int64_t)(b * T + t) * 192;
-            fgp[0] = fg + u;
-            fgp[1] = fg + 128 + j1;
-            fq[0] = ld_g1(fgp[0]);
-            fq[1] = ld_g1(fgp[1]);
-        } else {
-            f2 = a.F2T[(int64_t)u * C0 + cc];
-            f1 = a.F1T[(int64_t)j1 * C0 + cc];
-        }
+        const float f2 = a.F2T[(int64_t)u * C0 + cc];
+        const float f1 = a.F1T[(int64_t)j1 * C0 + cc];
         const uint32_t tag = E + 2 + (uint32_t)t;
         const int off[2] = {(t * 128 + u) * 32, (t * 128 + u) * 32 + 16};
         float dz[4];
@@ -739,12 +510,6 @@ __device__ __forceinline__ void dq_df2(const DqArgs& a, RecurSmem& sm, int b, ui
                 gather<2, false>(dzh, off, tag, dz, hc);
             }
         }
-        if (FUSED) {  // long there (the trailer runs behind BPTT); otherwise re-read until tagged
-            float fv[2];
-            take_g<2>(fgp, fq, E + kTagF, fv, hc);
-            f2 = fv[0];
-            f1 = fv[1];
-        }
         float p[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) p[j] = fmaf(wr[3][j], dz[3], fmaf(wr[2][j], dz[2], fmaf(wr[1][j], dz[1], wr[0][j] * dz[0])));
@@ -763,41 +528,22 @@ __device__ __forceinline__ void dq_df2(const DqArgs& a, RecurSmem& sm, int b, ui
     DQ_STAMP(7, b == 0);
 }
 
-// k_dq_recur (FUSED = false; after k_dq_embed) and k_dq_fwd (FUSED = true: k_dq_embed's work as the
-// launch's first workgroups, dq_embed_role, with Zx and the trailer's F2 / F1 met as granules).
-template <bool FUSED>
-__device__ __forceinline__ void dq_recur_body(const DqArgs& a) {
-    const int tid = threadIdx.x, lane = tid & 63, u = tid >> 3, kg = tid & 7, myc = kg & 1;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: a scalar register
-    if (skipped(a)) {  // k_dq_fwd: this replica contributes nothing to the all-reduce
-        if (FUSED)
-            for (int i = blockIdx.x * kRecThreads + tid; i < PM_RNN_NPARAM + 4; i += gridDim.x * kRecThreads) a.grad[i] = 0.f;
-        return;
-    }
+__global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) {
+    if (skipped(a)) return;
     __shared__ RecurSmem sm;
     const int T = a.T, B = a.B;
     const int64_t C0 = a.C0;
-    const uint32_t E = (uint32_t)a.flags[0] << 7;  // this update's tag base (k_dq_wgrad / k_dq_embed bump it)
-    const int nE = FUSED ? 3 * a.nct * T * 2 : 0;  // k_dq_fwd's embedding roles
-    if (FUSED && (int)blockIdx.x < nE) {
-        if (blockIdx.x == 0 && tid == 0) {  // k_dq_embed's duties: the tickets of the later launches, the
-            a.flags[1] = 0;                 // replica's contribution flag, no hand-off timed out yet
-            a.flags[2] = 0;
-            a.grad[PM_RNN_NPARAM] = 1.0f;
-            a.grad[PM_RNN_NPARAM + 1] = 0.0f;
-        }
-        dq_embed_role(a, *reinterpret_cast<EmbSmem*>(&sm), (int)blockIdx.x, E);
-        return;
-    }
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, u = tid >> 3, kg = tid & 7, myc = kg & 1;
     // [0, B/2) targetB on next (sequences 2j, 2j + 1 as the two columns), [B/2, 3B/2) modelB on obs and
-    // next of sequence b, [3B/2, 5B/2) the dF2 trailer of sequence b (after the embedding roles: FUSED)
-    const int nT = B >> 1, bx = (int)blockIdx.x - nE;
+    // next of sequence b, [3B/2, 5B/2) the dF2 trailer of sequence b
+    const int nT = B >> 1, bx = (int)blockIdx.x;
     const int role = bx < nT ? 0 : (bx < nT + B ? 1 : 2);
     const int b = role == 0 ? 2 * bx : (role == 1 ? bx - nT : bx - nT - B);  // column 0's sequence
+    const uint32_t E = (uint32_t)a.flags[0] << 7;  // this update's tag base
     const HandoffCtl hc{a.stats, a.grad + PM_RNN_NPARAM + 1, hand_limit(a.poll_limit)};
     [[maybe_unused]] const bool so0 = bx == nT, s10 = bx == 0;  // stamping blocks (diag)
     if (role == 2) {
-        dq_df2<FUSED>(a, sm, b, E, hc);
+        dq_df2(a, sm, b, E, hc);
         return;
     }
     const bool tgt = role == 0;
@@ -809,48 +555,10 @@ __device__ __forceinline__ void dq_recur_body(const DqArgs& a) {
     // Zx of step 0 first (step 0 needs no Whh: h_0 = 0), then Whh: the loads complete in issue
     // order, so step 0's cell runs while Whh is still in flight
     // Zx of this lane's column (the cell runs on the lanes of its column only)
-    const int64_t zcol = (int64_t)(myc ? sc1 : sc0) * T * 512 * B + (int64_t)u * B + (myc ? bc1 : b);
-    const float* zx = a.ZX + zcol;
-    const uint64_t* zg = reinterpret_cast<const uint64_t*>(a.ZG) + zcol;
-    const uint32_t tz = E + kTagZx;
+    const float* zx = a.ZX + (int64_t)(myc ? sc1 : sc0) * T * 512 * B + (int64_t)u * B + (myc ? bc1 : b);
     float zn[4];
-    uint64_t zq[4];
-    auto zissue = [&](int tt) {  // FUSED: step tt's four granules
 #pragma unroll
-        for (int q = 0; q < 4; ++q) zq[q] = ld_g1(zg + ((int64_t)tt * 512 + q * 128) * B);
-    };
-    // FUSED: step tt's Zx. Normally long there (the embedding roles end while step 0 runs); otherwise
-    // lanes 0 and 1 (one per column) wait on their gate-3 granule, the wave reads all four again
-    auto ztake = [&](int tt, float (&z)[4]) {
-        int it = 0;
-        for (;;) {
-            bool ok = true;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ok = ok && tag_is(zq[q], tz);
-            if (__all(ok)) break;
-            if (it >= hc.limit) {
-                if (lane == 0) void_update(hc);
-                break;
-            }
-            bool got = lane >= 2;
-            while (!__all(got) && it < hc.limit) {
-                __builtin_amdgcn_s_sleep(1);
-                ++it;
-                if (!got) got = tag_is(ld_g1(zg + ((int64_t)tt * 512 + 384) * B), tz);
-            }
-            zissue(tt);
-            ++it;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) z[q] = val_of(zq[q]);
-    };
-    if (FUSED) {
-        zissue(0);
-        eff_heads_lds(P, !tgt, sm.ws, sm.hw);  // read only at the heads, behind the forward's barriers
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)q * 128 * B];
-    }
+    for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)q * 128 * B];
     // Whh rows 128q + u, columns 16kg .. 16kg + 15
     float wr[4][16];
 #pragma unroll
@@ -894,21 +602,16 @@ __device__ __forceinline__ void dq_recur_body(const DqArgs& a) {
     };
     {   // step 0, outside the loop (h_0 = 0: the gates are Zx alone), so its wait covers Zx only
         float z[4];
-        if (FUSED) {
-            ztake(0, z);
-            if (T > 1) zissue(1);
-        } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) z[q] = zn[q];
-            if (T > 1)
+        for (int q = 0; q < 4; ++q) z[q] = zn[q];
+        if (T > 1)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)512 * B + (int64_t)q * 128 * B];
-        }
+            for (int q = 0; q < 4; ++q) zn[q] = zx[(int64_t)512 * B + (int64_t)q * 128 * B];
         cell(0, z);
         // the effective W_S image -> LDS (global_load_lds, 1 KB per wave instruction), issued after
         // step 0 (issued before it, the copy made step 0's Zx wait a vmcnt(0) behind Whh and itself);
         // it lands beside Whh, which step 1 waits for anyway. kWsPieces per wave, the last clamped.
-        if (!FUSED) {
+        {
             constexpr int kPieces = 128 * kWsStride / 256, kWsPieces = (kPieces + 15) / 16;
             const float* src = a.WSE + (int64_t)net * 128 * kWsStride;
 #pragma unroll
@@ -920,17 +623,12 @@ __device__ __forceinline__ void dq_recur_body(const DqArgs& a) {
     }
     for (int t = 1; t < T; ++t) {
         float z[4];
-        if (FUSED) {
-            ztake(t, z);
-            if (t + 1 < T) zissue(t + 1);
-        } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) z[q] = zn[q];
-            if (t + 1 < T) {
-                const int64_t o = (int64_t)(t + 1) * 512 * B;
+        for (int q = 0; q < 4; ++q) z[q] = zn[q];
+        if (t + 1 < T) {
+            const int64_t o = (int64_t)(t + 1) * 512 * B;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) zn[q] = zx[o + (int64_t)q * 128 * B];
-            }
+            for (int q = 0; q < 4; ++q) zn[q] = zx[o + (int64_t)q * 128 * B];
         }
         float acc[4][2];
 #pragma unroll
@@ -965,7 +663,7 @@ __device__ __forceinline__ void dq_recur_body(const DqArgs& a) {
         const float4 v = *reinterpret_cast<const float4*>(&sm.ws[u * kWsStride + 16 * kg + 4 * i]);
         wsr[4 * i] = v.x; wsr[4 * i + 1] = v.y; wsr[4 * i + 2] = v.z; wsr[4 * i + 3] = v.w;
     }
-    const float* HW = FUSED ? sm.hw : a.HWE + net * kHwN;
+    const float* HW = a.HWE + net * kHwN;
     float sv0;  // S + b_S of row u, column 0
     {
         float s2[2] = {0.f, 0.f};
@@ -1108,8 +806,6 @@ __device__ __forceinline__ void dq_recur_body(const DqArgs& a) {
     }
     DQ_STAMP(2, so0);
 }
-__global__ __launch_bounds__(kRecThreads) void k_dq_recur(DqArgs a) { dq_recur_body<false>(a); }
-__global__ __launch_bounds__(kRecThreads) void k_dq_fwd(DqArgs a) { dq_recur_body<true>(a); }
 
 // ---------------------------------------------------------------- 3: weight gradients
 struct WgSmem {
@@ -1127,140 +823,13 @@ struct WgSmem {
 // then one workgroup for the V / A head gradients, the loss and mean Q.
 constexpr int kWgTiles = 64 + 64 + 16 + 8 + 2;
 
-// clip + Adam constants (pm_drqn: lr, betas, eps, max_norm, target_update_interval)
-struct AdamK {
-    double lr, beta1, beta2, eps, max_norm;
-    int64_t interval;
-};
-// torch's Adam on one element given its clipped gradient (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_,
-// addcdiv_ with the bias corrections folded into step_size and bc2s); k_drqn_apply and
-// k_dq_wgrad_apply share it so both paths round identically
-__device__ __forceinline__ void adam_elem(float g, float coef, float step_size, float bc2s, const AdamK& k, float& m,
-                                          float& v, float& p) {
-    const float gc = g * coef;
-    m = m + (float)(1.0 - k.beta1) * (gc - m);                  // exp_avg.lerp_(grad, 1-beta1)
-    v = v * (float)k.beta2 + (float)(1.0 - k.beta2) * gc * gc;  // mul_(beta2).addcmul_(g, g, 1-beta2)
-    const float denom = sqrtf(v) / bc2s + (float)k.eps;
-    p = p - step_size * (m / denom);
-}
-
-// The clip coefficient and Adam's step constants from the norm's fp64 partials (slots 0..kWgTiles; the
-// rest of 256 zero), summed in k_drqn_apply's fixed tree (red[t] += red[t + kk], kk = 128 .. 1) —
-// here on one wave's registers (x[j] = slot lane + 64 j; the shuffles pair the same slots), so every
-// block that forms it gets k_drqn_apply's bits.
-struct ClipAdam {
-    float coef, step_size, bc2s, norm;
-};
-__device__ __forceinline__ ClipAdam clip_adam_consts(double (&x)[4], const AdamK& k, int64_t at) {
-    x[0] += x[2];
-    x[1] += x[3];
-    x[0] += x[1];
-#pragma unroll
-    for (int kk = 32; kk > 0; kk >>= 1) x[0] += __shfl_down(x[0], kk);
-    const double ss = __shfl(x[0], 0);
-    ClipAdam c;
-    c.norm = (float)sqrt(ss);
-    const float coef = (float)(k.max_norm / ((double)c.norm + 1e-6));  // clip_coef
-    const double bc1 = 1.0 - pow(k.beta1, (double)at), bc2 = 1.0 - pow(k.beta2, (double)at);
-    c.coef = coef < 1.0f ? coef : 1.0f;  // clamp(clip_coef, max=1)
-    c.step_size = (float)(k.lr / bc1);
-    c.bc2s = (float)sqrt(bc2);
-    return c;
-}
-
-// k_dq_wgrad_apply (APPLY; pm_drqn_update, one replica): every workgroup publishes its share of the
-// clip norm's squares as a granule pair (tag E + kTagNP), one wave gathers all kWgTiles + 1 shares and
-// forms the clip coefficient exactly as k_drqn_apply does, and the workgroup then runs clip + Adam (and
-// the target sync) on the very elements whose gradient it formed: no apply launch, no gradient
-// re-read. Every workgroup waits on all the others, so the launch relies on all of them becoming
-// resident (155 workgroups of 1024 threads, two per CU by LDS); nothing they wait on waits on them, so
-// a workgroup dispatched late only delays the wait. A wait past its bound latches status bit 4 in
-// pm_drqn_stats and leaves that workgroup's elements untouched (k_drqn_apply's `late`).
-constexpr uint32_t kTagNP = 102;
-template <bool APPLY>
-__device__ __forceinline__ void dq_wgrad_body(const DqArgs& a, const AdamK& k, float* params, float* target, float* m_,
-                                              float* v_) {
-    // a new tag epoch for the next update's in-launch hand-offs (k_dq_fwd reads it at its start; this
-    // update's k_dq_recur / k_dq_fwd has finished: stream order). k_dq_wgrad_apply's own hand-off uses
-    // the epoch too: its block 0 bumps it once every block has published (so has read it).
-    if (!APPLY && blockIdx.x == 0 && threadIdx.x == 0) a.flags[0] = a.flags[0] + 1;
-    if (skipped(a)) {
-        if (APPLY && blockIdx.x == 0 && threadIdx.x == 0) a.flags[0] = a.flags[0] + 1;
-        return;
-    }
+__global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
+    if (skipped(a)) return;
     __shared__ WgSmem sm;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
     const int64_t C0 = a.C0;
     const int B = a.B;
     const int bid = blockIdx.x;
-    // APPLY: what k_drqn_apply reads first (written by earlier launches): the rank count, the void
-    // count, the step counters, the tag epoch
-    float inv_world = 1.f;
-    bool do_apply = APPLY;
-    int64_t ts = 0, at = 0;
-    uint32_t tagNP = 0;
-    if (APPLY) {
-        const float ranks = a.grad[PM_RNN_NPARAM];
-        do_apply = ranks > 0.f;
-        if (do_apply && a.grad[PM_RNN_NPARAM + 1] != 0.f) {  // a hand-off timed out: the update is void
-            if (bid == 0 && tid == 0) atomicOr(&a.stats->status, 8);
-            do_apply = false;
-        }
-        inv_world = 1.0f / ranks;
-        ts = a.stats->steps + 1;
-        at = a.stats->adam_t + 1;
-        tagNP = ((uint32_t)a.flags[0] << 7) + kTagNP;
-        if (!do_apply && bid == 0 && tid == 0) a.flags[0] = a.flags[0] + 1;
-    }
-    // wave 0 of every APPLY block: publish the block's share, gather every share, the constants
-    auto publish_and_gather = [&](double share, ClipAdam& c) -> bool {
-        const __amdgpu_buffer_rsrc_t rn = rsrc(a.NPG);
-        if (lane == 0) {
-            const uint64_t bits = (uint64_t)__double_as_longlong(share);
-            st_g2(rn, bid * 16, __uint_as_float((uint32_t)bits), __uint_as_float((uint32_t)(bits >> 32)), tagNP);
-        }
-        double x[4];
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int slot = lane + 64 * j;
-            x[j] = 0.0;
-            if (slot > kWgTiles) continue;
-            const uint64_t* p = reinterpret_cast<const uint64_t*>(a.NPG) + 2 * slot;
-            uint64_t lo = ld_g1(p), hi = ld_g1(p + 1);
-            for (int it = 0; !(tag_is(lo, tagNP) && tag_is(hi, tagNP)); ++it) {
-                if (it >= (1 << 22)) {
-                    ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                lo = ld_g1(p);
-                hi = ld_g1(p + 1);
-            }
-            x[j] = __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
-        }
-        if (bid == 0 && lane == 0) a.flags[0] = a.flags[0] + 1;  // every block has published: read the epoch
-        if (!__all(ok)) {  // the norm would be partial: this workgroup leaves its elements untouched
-            if (lane == 0) atomicOr(&a.stats->status, 4);
-            return false;
-        }
-        c = clip_adam_consts(x, k, at);
-        if (bid == 0 && lane == 0) {  // every block has published, so every block has read the counters
-            a.stats->norm = c.norm;
-            a.stats->steps = ts;
-            a.stats->adam_t = at;
-        }
-        return true;
-    };
-    const bool sync = APPLY && ts % k.interval == 0;  // targetB.load_state_dict(modelB.state_dict()) (:529-530)
-    auto adam_at = [&](int i, float graw, const ClipAdam& c) {
-        float m = m_[i], v = v_[i], p = params[i];
-        adam_elem(graw * inv_world, c.coef, c.step_size, c.bc2s, k, m, v, p);
-        params[i] = p;
-        m_[i] = m;
-        v_[i] = v;
-        if (sync) target[i] = p;
-    };
     DQ_STAMP(210, bid == 0);
     if (bid < kWgTiles) {
         int mat, gt, kt;
@@ -1300,17 +869,13 @@ __device__ __forceinline__ void dq_wgrad_body(const DqArgs& a, const AdamK& k, f
         __syncthreads();
         if (w == 0) {
             const int ldg = mat <= 2 ? 128 : (mat == 3 ? 64 : 7);
-            const int gbase = mat == 0 ? R_P_WIH : (mat == 1 ? R_P_WHH : (mat == 2 ? R_P_SWMU : (mat == 3 ? R_P_F2W : R_P_F1W)));
-            float* G = a.grad + gbase;
-            const bool valid = 32 * kt + col < ldg;
-            float gv[16];
+            float* G = a.grad + (mat == 0 ? R_P_WIH : (mat == 1 ? R_P_WHH : (mat == 2 ? R_P_SWMU : (mat == 3 ? R_P_F2W : R_P_F1W))));
             double sq = 0.0;  // this tile's share of the clip norm (local_norm), sigma gradients (mu x epsilon) included
+            if (32 * kt + col < ldg)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float v = sm.red[0][r][lane];
-                for (int kk = 1; kk < 16; ++kk) v += sm.red[kk][r][lane];
-                gv[r] = v;
-                if (valid) {
+                for (int r = 0; r < 16; ++r) {
+                    float v = sm.red[0][r][lane];
+                    for (int k = 1; k < 16; ++k) v += sm.red[k][r][lane];
                     const int e = (32 * gt + rho(r) + 4 * h) * ldg + 32 * kt + col;
                     G[e] = v;
                     sq += (double)v * (double)v;
@@ -1319,15 +884,11 @@ __device__ __forceinline__ void dq_wgrad_body(const DqArgs& a, const AdamK& k, f
                         sq += (double)gs * (double)gs;
                     }
                 }
-            }
             DQ_STAMP(211, bid == 0);
-            const bool has_bias = mat != 1 && kt == 0;
-            float vb = 0.f;
-            if (has_bias) {  // the bias gradients: row sums
+            if (mat != 1 && kt == 0) {  // the bias gradients: row sums
                 float v = sm.rs[0][lane];
-                for (int kk = 1; kk < 16; ++kk) v += sm.rs[kk][lane];
+                for (int k = 1; k < 16; ++k) v += sm.rs[k][lane];
                 v += __shfl_xor(v, 32);
-                vb = v;
                 const int row = 32 * gt + col;
                 if (h == 0) {
                     if (mat == 0) { a.grad[R_P_BIH + row] = v; a.grad[R_P_BHH + row] = v; }
@@ -1343,33 +904,7 @@ __device__ __forceinline__ void dq_wgrad_body(const DqArgs& a, const AdamK& k, f
             }
             if (a.local_norm) {
                 sq = wave_sum(sq);  // DPP reduction (pm_dev.h): xor-1-first association of the fp64 sum
-                if (!APPLY && lane == 0) a.NP[bid] = sq;
-            }
-            if (APPLY && do_apply) {
-                ClipAdam c;
-                if (!publish_and_gather(sq, c)) return;
-                if (valid)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int e = (32 * gt + rho(r) + 4 * h) * ldg + 32 * kt + col;
-                        adam_at(gbase + e, gv[r], c);
-                        if (mat == 2) {  // the sigma gradient (mu gradient x epsilon), formed and written as the apply does
-                            const float gs = gv[r] * a.params[R_P_SWEP + e];
-                            a.grad[R_P_SWSG + e] = gs;
-                            adam_at(R_P_SWSG + e, gs, c);
-                        }
-                    }
-                if (has_bias && h == 0) {
-                    const int row = 32 * gt + col;
-                    if (mat == 0) { adam_at(R_P_BIH + row, vb, c); adam_at(R_P_BHH + row, vb, c); }
-                    else if (mat == 2) {
-                        adam_at(R_P_SBMU + row, vb, c);
-                        const float gs = vb * a.params[R_P_SBEP + row];
-                        a.grad[R_P_SBSG + row] = gs;
-                        adam_at(R_P_SBSG + row, gs, c);
-                    } else if (mat == 3) adam_at(R_P_F2B + row, vb, c);
-                    else adam_at(R_P_F1B + row, vb, c);
-                }
+                if (lane == 0) a.NP[bid] = sq;
             }
         }
         return;
@@ -1377,8 +912,6 @@ __device__ __forceinline__ void dq_wgrad_body(const DqArgs& a, const AdamK& k, f
     // ---- the V / A head gradients: dw_o[r] = sum_b dQ_o[b] ReLU(S)[r][b] (o = V, A0..2) and their biases,
     // the loss and mean Q, each summed over the sequences in order
     double sq = 0.0;
-    float hv = 0.f;           // this thread's gradient element (APPLY)
-    int hi = -1, hs = 0, he = 0;  // its parameter index, its sigma's, the epsilon's
     // the per-sequence scalars -> LDS once (coalesced), beside each thread's ReLU(S) row loads
     float* scs = &sm.red[0][0][0];  // [B][8]
     for (int i = tid; i < B * 8; i += 1024) scs[i] = a.SC[i];
@@ -1402,22 +935,17 @@ __device__ __forceinline__ void dq_wgrad_body(const DqArgs& a, const AdamK& k, f
             }
         }
         const int e = o == 0 ? r : 128 * (o - 1) + r;
-        hi = (o == 0 ? R_P_VWMU : R_P_AWMU) + e;
-        hs = (o == 0 ? R_P_VWSG : R_P_AWSG) + e;
-        he = (o == 0 ? R_P_VWEP : R_P_AWEP) + e;
-        hv = v;
-        a.grad[hi] = v;
-        const float gs = v * a.params[he];
+        a.grad[(o == 0 ? R_P_VWMU : R_P_AWMU) + e] = v;
+        const float gs = v * a.params[(o == 0 ? R_P_VWEP : R_P_AWEP) + e];
         sq = (double)v * (double)v + (double)gs * (double)gs;
     } else if (tid < 518) {
         const int o = tid - 512;  // dV, dA0..2, loss, Q(s, a)
         float v = 0.f;
         for (int b = 0; b < B; ++b) v += scs[b * 8 + o];
-        if (o == 0) { a.grad[hi = R_P_VBMU] = v; hs = R_P_VBSG; he = R_P_VBEP; }
-        else if (o < 4) { a.grad[hi = R_P_ABMU + o - 1] = v; hs = R_P_ABSG + o - 1; he = R_P_ABEP + o - 1; }
+        if (o == 0) a.grad[R_P_VBMU] = v;
+        else if (o < 4) a.grad[R_P_ABMU + o - 1] = v;
         else if (o == SC_LOSS) a.stats->loss = v / (float)B;
         else a.stats->q_mean = v / (float)B;
-        hv = v;
         if (o < 4) {
             const float gs = v * a.params[o == 0 ? R_P_VBEP : R_P_ABEP + o - 1];
             sq = (double)v * (double)v + (double)gs * (double)gs;
@@ -1427,43 +955,12 @@ __device__ __forceinline__ void dq_wgrad_body(const DqArgs& a, const AdamK& k, f
         double* red = reinterpret_cast<double*>(&sm.red[0][0][0]) + 1024;  // past scs ([B][8] <= 8 KB)
         red[tid] = sq;
         __syncthreads();
-        for (int kk = 512; kk > 0; kk >>= 1) {
-            if (tid < kk) red[tid] += red[tid + kk];
+        for (int k = 512; k > 0; k >>= 1) {
+            if (tid < k) red[tid] += red[tid + k];
             __syncthreads();
         }
-        if (!APPLY && tid == 0) a.NP[kWgTiles] = red[0];
-        if (APPLY && do_apply) {
-            ClipAdam* cs = reinterpret_cast<ClipAdam*>(red + 1024);
-            int* okp = reinterpret_cast<int*>(cs + 1);
-            if (w == 0) {
-                ClipAdam c;
-                const bool ok = publish_and_gather(red[0], c);
-                if (lane == 0) {
-                    *cs = c;
-                    *okp = ok;
-                }
-            }
-            __syncthreads();
-            if (!*okp) return;  // block-uniform
-            const ClipAdam c = *cs;
-            if (hi >= 0) {  // the element and its sigma (mu gradient x epsilon), as the apply forms it
-                adam_at(hi, hv, c);
-                const float gs = hv * a.params[he];
-                a.grad[hs] = gs;
-                adam_at(hs, gs, c);
-            }
-            if (sync)  // the epsilon buffers follow modelB into targetB
-                for (int i = PM_RNN_NPARAM + tid; i < PM_RNN_NP; i += 1024) target[i] = params[i];
-        }
+        if (tid == 0) a.NP[kWgTiles] = red[0];
     }
-}
-
-__global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
-    dq_wgrad_body<false>(a, AdamK{}, nullptr, nullptr, nullptr, nullptr);
-}
-__global__ __launch_bounds__(1024) void k_dq_wgrad_apply(DqArgs a, AdamK k, float* params, float* target, float* m_,
-                                                         float* v_) {
-    dq_wgrad_body<true>(a, k, params, target, m_, v_);
 }
 
 // NoisyLinear sigma gradients: d sigma = dW * epsilon (NoisyLinear.forward :45-46). Linear in the
@@ -1479,6 +976,10 @@ __device__ __forceinline__ int sigma_source(int i, int& ep) {
 }
 
 // ---------------------------------------------------------------- clip + Adam
+struct AdamK {
+    double lr, beta1, beta2, eps, max_norm;
+    int64_t interval;
+};
 
 // One launch for the apply (round 3): every block forms its slice's sigma gradients and fp64 sum of
 // squares, arrives on a monotonic ticket and waits for the other blocks (kNormBlocks = 256, one per
@@ -1579,8 +1080,12 @@ __global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* pa
         const int i = plo + threadIdx.x + 256 * e;
         if (i >= phi) continue;
         if (i < PM_RNN_NPARAM) {
+            const float gc = g[e] * coef;
             float m = mm[e], v = vv[e], p = pr[e];
-            adam_elem(g[e], coef, step_size, bc2s, k, m, v, p);
+            m = m + (float)(1.0 - k.beta1) * (gc - m);                  // exp_avg.lerp_(grad, 1-beta1)
+            v = v * (float)k.beta2 + (float)(1.0 - k.beta2) * gc * gc;  // mul_(beta2).addcmul_(g, g, 1-beta2)
+            const float denom = sqrtf(v) / bc2s + (float)k.eps;
+            p = p - step_size * (m / denom);
             params[i] = p;
             m_[i] = m;
             v_[i] = v;
@@ -1624,14 +1129,7 @@ extern "C" int64_t pm_drqn_work_bytes(int32_t batch, int32_t T) {
     return dq_layout(batch, T, nullptr, nullptr);
 }
 
-// PONGMI_DRQN_FUSE_APPLY=0 keeps pm_drqn_update's clip + Adam in its own launch (k_drqn_apply) instead
-// of in the weight-gradient launch (k_dq_wgrad_apply); read per call (A/B and the equality test)
-static bool fuse_apply() {
-    const char* e = getenv("PONGMI_DRQN_FUSE_APPLY");
-    return e && atoi(e) != 0;
-}
-
-static int drqn_grads(const pm_drqn* d, void* stream, int local_norm, bool apply_in_wgrad = false) {
+static int drqn_grads(const pm_drqn* d, void* stream, int local_norm) {
     if (int rc = check(d)) return rc;
     PM_REQUIRE(d->obs && d->next && d->act && d->rew && d->done, PM_E_ARG, "pm_drqn_grads: null batch");
     hipStream_t st = pm_stream(stream);
@@ -1642,25 +1140,12 @@ static int drqn_grads(const pm_drqn* d, void* stream, int local_norm, bool apply
     a.gamma = (float)d->gamma;
     a.poll_limit = d->poll_limit;
     a.local_norm = local_norm;
-    const char* fe = getenv("PONGMI_DRQN_FUSED");  // read per call (A/B and the equality test)
-    if (fe && atoi(fe) != 0) {
-        pm_launch(PM_TIMER_DRQN, k_dq_fwd, dim3(3 * a.nct * a.T * 2 + a.B / 2 + 2 * a.B), dim3(kRecThreads), st, a);
-        PM_LAUNCHED("k_dq_fwd");
-    } else {
-        hipLaunchKernelGGL(k_dq_embed, dim3(3 * a.nct * a.T * 4 + kEmbEff), dim3(512), 0, st, a);
-        PM_LAUNCHED("k_dq_embed");
-        pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(a.B / 2 + 2 * a.B), dim3(kRecThreads), st, a);
-        PM_LAUNCHED("k_dq_recur");
-    }
-    if (apply_in_wgrad) {
-        const AdamK k{d->lr, d->beta1, d->beta2, d->adam_eps, d->max_norm, d->target_update_interval};
-        hipLaunchKernelGGL(k_dq_wgrad_apply, dim3(kWgTiles + 1), dim3(1024), 0, st, a, k, d->params, d->target,
-                           d->adam_m, d->adam_v);
-        PM_LAUNCHED("k_dq_wgrad_apply");
-    } else {
-        hipLaunchKernelGGL(k_dq_wgrad, dim3(kWgTiles + 1), dim3(1024), 0, st, a);
-        PM_LAUNCHED("k_dq_wgrad");
-    }
+    hipLaunchKernelGGL(k_dq_embed, dim3(3 * a.nct * a.T * 4 + kEmbEff), dim3(512), 0, st, a);
+    PM_LAUNCHED("k_dq_embed");
+    pm_launch(PM_TIMER_DRQN, k_dq_recur, dim3(a.B / 2 + 2 * a.B), dim3(kRecThreads), st, a);
+    PM_LAUNCHED("k_dq_recur");
+    hipLaunchKernelGGL(k_dq_wgrad, dim3(kWgTiles + 1), dim3(1024), 0, st, a);
+    PM_LAUNCHED("k_dq_wgrad");
     return PM_OK;
 }
 
@@ -1692,7 +1177,6 @@ extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) { return drqn_apply
 // One replica: the weight-gradient blocks sum the clip norm's squares as they store the gradient, so
 // the apply needs no arrival ticket (replicas that all-reduce call pm_drqn_grads / pm_drqn_apply).
 extern "C" int pm_drqn_update(const pm_drqn* d, void* stream) {
-    const bool fa = fuse_apply();
-    if (int rc = drqn_grads(d, stream, 1, fa)) return rc;
-    return fa ? PM_OK : drqn_apply(d, stream, 1);
+    if (int rc = drqn_grads(d, stream, 1)) return rc;
+    return drqn_apply(d, stream, 1);
 }

@@ -354,50 +354,3 @@ def test_drqn_timeout_voids_update(golden):
     R = DRQNLearner(_sd(gr), batch=64, T=8, target_update_interval=1)
     R.update(*b)
     assert torch.equal(L.params, R.params) and torch.equal(L.adam_v, R.adam_v) and torch.equal(L.target, R.target)
-
-
-@pytest.mark.parametrize("B,T", [(64, 8), (32, 3), (96, 5), (256, 8), (32, 64)])
-def test_drqn_fused_launches_equal_four_launches(golden, monkeypatch, B, T):
-    """The fused launches against the round-5 four (k_dq_embed + k_dq_recur + k_dq_wgrad +
-    k_drqn_apply; PONGMI_DRQN_FUSED=0, PONGMI_DRQN_FUSE_APPLY=0):
-      * k_dq_fwd: the embedding as the recurrence launch's first workgroups, Zx and the trailer's F2 / F1
-        met as tagged granules, the effective head weights formed in each recurrence workgroup's LDS;
-      * k_dq_wgrad_apply: each weight-gradient workgroup publishes its share of the clip norm's
-        squares, gathers every share, forms the clip coefficient in k_drqn_apply's order and runs
-        clip + Adam on the elements it formed.
-    The same MFMA sequences, sums and Adam arithmetic, so the gradient, loss and norm of every update
-    and the parameters, both Adam moments, targetB (synced at update 2) and the counters after three
-    updates are bit-identical in every combination. (256, 8): 1 536 embedding workgroups ahead of 640
-    recurrence workgroups, far more than resident; (32, 64): the global gate-scratch path."""
-    from pongmi.drqn import DRQNLearner
-    gr = golden("rnn")
-    sd = {k[7:]: v for k, v in gr.items() if k.startswith("params.")}
-    rng = np.random.default_rng(7000 + B * 100 + T)
-    tsd = {k: (v + rng.normal(0, 0.02, v.shape).astype(np.float32)) if "epsilon" not in k else v for k, v in sd.items()}
-    batches = []
-    for _ in range(3):
-        batches.append((torch.from_numpy(rng.uniform(0, 1, (B, T, 7)).astype(np.float32)),
-                        torch.from_numpy(rng.integers(0, 3, (B, T)).astype(np.int64)),
-                        torch.from_numpy(rng.choice(np.array([-1, 0, 1], np.float32), (B, T)).astype(np.float32)),
-                        torch.from_numpy(rng.uniform(0, 1, (B, T, 7)).astype(np.float32)),
-                        torch.from_numpy(rng.random((B, T)) < 0.3)))
-    runs = []
-    for fused, fuse_apply in (("0", "0"), ("1", "0"), ("1", "1")):
-        monkeypatch.setenv("PONGMI_DRQN_FUSED", fused)
-        monkeypatch.setenv("PONGMI_DRQN_FUSE_APPLY", fuse_apply)
-        L = DRQNLearner({k: torch.from_numpy(v) for k, v in sd.items()},
-                        {k: torch.from_numpy(v) for k, v in tsd.items()}, batch=B, T=T, target_update_interval=2)
-        per = []
-        for b in batches:
-            L.update(*b)
-            st = L.stats()
-            assert st["status"] == 0, st
-            per.append((L.grad.clone(), st))
-        runs.append((per, L.params.clone(), L.adam_m.clone(), L.adam_v.clone(), L.target.clone()))
-    ref = runs[0]
-    for mode, run in zip(("fwd fused", "fwd + apply fused"), runs[1:]):
-        for k, ((g0, s0), (g1, s1)) in enumerate(zip(ref[0], run[0])):
-            assert torch.equal(g0, g1), f"{mode}, update {k}: gradient differs ({int((g0 != g1).sum())} elements)"
-            assert s0 == s1, (mode, k, s0, s1)
-        for name, x0, x1 in zip(("params", "adam_m", "adam_v", "target"), ref[1:], run[1:]):
-            assert torch.equal(x0, x1), f"{mode}: {name} differs ({int((x0 != x1).sum())} elements)"

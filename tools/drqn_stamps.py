@@ -1,6 +1,5 @@
 """Phase timeline of one DRQN update (diagnostic library): s_memrealtime stamps (100 MHz) of the
-embed / recurrence / weight-gradient kernels, relative to k_dq_embed's start (PONGMI_DRQN_FUSED=0) or
-k_dq_fwd's first embedding role (the default).
+embed / recurrence / weight-gradient kernels, relative to k_dq_embed's start.
 
     make -C pingpong-selfplay-ai_amd/csrc diag && python tools/drqn_stamps.py
 """
@@ -25,8 +24,7 @@ for t in range(20):
 NAMES.update({228: "embed b0: first loads landed (diag drain)", 227: "embed b0: after setup", 223: "embed b0: F1/F2 done (thread 0)", 224: "embed b0: F2 barrier", 225: "embed b0: Zx MFMAs done", 226: "embed b0: halves barrier", 8: "dF2 trailer 0 start", 7: "dF2 trailer 0 end", 50: "obs heads: Q formed", 150: "target WG 0: Q published", 51: "obs: target Q gathered, loss",
               52: "obs: dh_T reduced", 2: "recur obs WG end", 210: "wgrad A start", 211: "wgrad A tile done",
               200: "wgrad B start", 201: "wgrad B dF2 done", 204: "wgrad B dF1 done", 206: "wgrad B ticket",
-              207: "wgrad last tile: reduce start", 208: "wgrad last tile: reduce end",
-              229: "k_dq_fwd embed role 0 start", 230: "k_dq_fwd embed role 0 end (wave 8)"})
+              207: "wgrad last tile: reduce start", 208: "wgrad last tile: reduce end"})
 
 
 def main():
@@ -53,7 +51,7 @@ def main():
         lib.pm_diag_read_drqn(buf)
         rows.append(np.array(buf[:], dtype=np.int64))
     r = np.median(np.stack(rows), axis=0)
-    t0 = r[220] if r[220] else r[229]
+    t0 = r[220]
     for k in sorted(NAMES, key=lambda k: r[k] if r[k] else 1e30):
         if r[k]:
             print(f"{NAMES[k]:40s} {(r[k] - t0) / 100.0:9.2f} us")

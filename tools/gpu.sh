@@ -27,7 +27,6 @@
 #   roll       k_rollout16 per-step phase cycles (tools/roll_stamps.py, diag build)
 #   ab:VAR=v1,v2  tests/test_gpu_selfplay.py under each value, then the default bench interleaved twice
 #   drqnab:VAR=v1,v2  tests/test_gpu_drqn.py under v1, then tools/drqn_time.py interleaved three times
-#   drqnmodes  tests/test_gpu_drqn.py, then drqn_time and the RNN bench per DRQN launch mode (fused fwd / apply)
 #   k1sweep    K1 events + rocprofv3 kernel traces at 65 536 .. 4 194 304 arenas
 #   floorprof  tools/k1_floor under rocprofv3 (round 5 SIGSEGV check)
 #   mstamps    k_learn_multi per-update phase stamps (diag and PM_DIAG_NOWAIT builds)
@@ -133,18 +132,6 @@ run_task() {
         for v in ${vals//,/ }; do
           env $var=$v timeout -k 10 120 python3 tools/drqn_time.py 2>/dev/null | tail -1 | sed "s#^#$var=$v #" || return 1
         done
-      done ;;
-    drqnmodes)  # the DRQN launch modes: tests/test_gpu_drqn.py, then tools/drqn_time.py and the RNN bench per mode
-      timeout -k 10 400 $PYT tests/test_gpu_drqn.py > gpurun_out/${tag}_drqnmodes.log 2>&1 &&
-          echo "tests: $(tail -1 gpurun_out/${tag}_drqnmodes.log)" || return 1
-      for rep in 1 2 3; do
-        for m in 0,0 1,0 1,1; do
-          PONGMI_DRQN_FUSED=${m%,*} PONGMI_DRQN_FUSE_APPLY=${m#*,} timeout -k 10 120 python3 tools/drqn_time.py 2>/dev/null | tail -1 | sed "s#^#fused,apply=$m #" || return 1
-        done
-      done
-      for m in 0,0 1,1; do
-        PONGMI_DRQN_FUSED=${m%,*} PONGMI_DRQN_FUSE_APPLY=${m#*,} timeout -k 10 200 python3 bench.py --workload rnn --no-cpu-baseline > gpurun_out/${tag}_drqnmodes_rnn_${m/,/_}.json 2>/dev/null &&
-            echo "rnn fused,apply=$m $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e6,2), d['ms_per_step'], d['drqn_roofline']['update_us'], d['drqn_roofline']['recur_us'])" gpurun_out/${tag}_drqnmodes_rnn_${m/,/_}.json)" || return 1
       done ;;
     roll)  # k_rollout16 per-step phase cycles (diag build)
       timeout -k 10 120 python3 tools/roll_stamps.py > gpurun_out/${tag}_roll_stamps.txt 2>&1 && grep -v amdgpu.ids gpurun_out/${tag}_roll_stamps.txt ;;

@@ -62,14 +62,18 @@ struct RnnFold {
     }
 };
 
-__global__ __launch_bounds__(256) void k_rnn_fold(const float* __restrict__ params, float* __restrict__ params_out,
+constexpr int kFoldBlock = 1024;  // one noise draw per thread (516 draws), one element per thread
+__global__ __launch_bounds__(kFoldBlock) void k_rnn_fold(const float* __restrict__ params, float* __restrict__ params_out,
                                                   int mode, uint64_t seed, uint64_t counter,
                                                   const uint64_t* __restrict__ counter_dev, float* __restrict__ w_eff) {
     __shared__ float noise[R_NOISE];
     const int net = blockIdx.y;
     const float* p = params + (size_t)net * PM_RNN_NP;
     float* w = w_eff + (size_t)net * PM_RNN_NW;
-    if (mode == PM_FOLD_TRAIN_FRESH) {
+    // the fresh draws only where they are read: the shared head / head elements [R_S, ...) and block
+    // 0 (modelB's epsilon buffers); the feature and LSTM blocks skip the Box-Muller work (block-uniform)
+    const bool need = (blockIdx.x + 1) * blockDim.x > R_S || blockIdx.x == 0;
+    if (mode == PM_FOLD_TRAIN_FRESH && need) {
         rnn_noise(seed, counter + (counter_dev ? *counter_dev : 0ull) + (uint64_t)net * 0x10000ull, noise);
         __syncthreads();
     }
@@ -346,7 +350,7 @@ extern "C" int pm_rnn_fold(const float* params, float* params_out, int32_t mode,
     PM_REQUIRE(params && w_eff && count > 0, PM_E_ARG, "pm_rnn_fold: null buffer or count");
     PM_REQUIRE(mode >= PM_FOLD_EVAL && mode <= PM_FOLD_TRAIN_FRESH, PM_E_ARG, "pm_rnn_fold: mode %d", mode);
     PM_REQUIRE((((uintptr_t)w_eff) & 15) == 0, PM_E_ARG, "pm_rnn_fold: w_eff must be 16-byte aligned");
-    hipLaunchKernelGGL(k_rnn_fold, dim3(pm_blocks(PM_RNN_NW, 256), count), dim3(256), 0, pm_stream(stream), params,
+    hipLaunchKernelGGL(k_rnn_fold, dim3(pm_blocks(PM_RNN_NW, kFoldBlock), count), dim3(kFoldBlock), 0, pm_stream(stream), params,
                        params_out, mode, seed, counter, counter_dev, w_eff);
     PM_LAUNCHED("k_rnn_fold");
     return PM_OK;

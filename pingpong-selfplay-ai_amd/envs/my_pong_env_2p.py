@@ -61,6 +61,11 @@ class PongEnv2P:
         self._env = PongEnv2PBatch(1, device=device, **{k: v for k, v in kw.items()})
         self._lib = _lib.load()
         self._slot = _lib.MappedSlot(18, 17)  # obsA[7] obsB[7] rA rB done | seq
+        # per-call constants made once: the argument references and the launch stream (the one current
+        # at construction; every call waits for its own result, so nothing else orders against it)
+        self._pparams, self._pstate = ctypes.byref(self._env.params), ctypes.byref(self._env.state)
+        self._stream = _lib.stream_ptr()
+        self._step1, self._reset1 = self._lib.pm_env_step1, self._lib.pm_env_reset1
         self._host = None
         if enable_render:
             import pygame  # noqa: F401  (viewer only; not part of the device path)
@@ -71,11 +76,12 @@ class PongEnv2P:
         vx, vy, spin = draw_serve(random, self._cfg)  # 4 draws from the global stream (:94-110)
         self.spin_angle = 0.0
         slot = self._slot
-        _lib.check(self._lib.pm_env_reset1(ctypes.byref(self._env.state), vx, vy, spin, slot.dev, slot.next_seq(),
-                                           _lib.stream_ptr()), "pm_env_reset1")
+        rc = self._reset1(self._pstate, vx, vy, spin, slot.dev, slot.next_seq(), self._stream)
+        if rc:
+            _lib.check(rc, "pm_env_reset1")
         self._host = None
         slot.wait()
-        out = slot.floats(0, 14)
+        out = slot.f32[0:14].copy()
         return out[0:7], out[7:14]
 
     def step(self, actionA, actionB):
@@ -83,12 +89,14 @@ class PongEnv2P:
         if not (0 <= aA <= 2 and 0 <= aB <= 2):
             raise ValueError(f"actions must be in {{0, 1, 2}}, got ({actionA}, {actionB})")
         slot = self._slot
-        _lib.check(self._lib.pm_env_step1(ctypes.byref(self._env.params), ctypes.byref(self._env.state), aA, aB,
-                                          slot.dev, slot.next_seq(), _lib.stream_ptr()), "pm_env_step1")
+        rc = self._step1(self._pparams, self._pstate, aA, aB, slot.dev, slot.next_seq(), self._stream)
+        if rc:
+            _lib.check(rc, "pm_env_step1")
         self._host = None
         slot.wait()
-        out = slot.floats(0, 17)
-        return (out[0:7], out[7:14]), (float(out[14]), float(out[15])), bool(out[16]), {}
+        out = slot.f32[0:17].copy()
+        r = out[14:17].tolist()
+        return (out[0:7], out[7:14]), (r[0], r[1]), r[2] != 0.0, {}
 
     def _get_obs(self):
         st = self._state()

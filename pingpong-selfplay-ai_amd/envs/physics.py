@@ -24,17 +24,21 @@ def collide_batch(rows, device="cuda"):
 
 
 _slot = None
+_call = None  # (pm_collide1, launch stream), made on the first call
 
 
 def collide_sphere_with_moving_plane(vn, vt, u, omega, e, mu, m, R):
     """One launch (pm_collide1: the row as kernel arguments, the result written into a host-mapped
     buffer the host polls), no copies, no stream synchronisation."""
-    global _slot
+    global _slot, _call
     if _slot is None:
         _slot = _lib.MappedSlot(8, 6)  # vn' vt' omega' (fp64) | seq
+        _call = (_lib.load().pm_collide1, _lib.stream_ptr())
     row = (ctypes.c_double * 8)(vn, vt, u, omega, e, mu, m, R)
     inertia = (2 / 5) * m * R ** 2  # CPython's I (:9)
-    _lib.check(_lib.load().pm_collide1(row, inertia, _slot.dev, _slot.next_seq(), _lib.stream_ptr()), "pm_collide1")
+    rc = _call[0](row, inertia, _slot.dev, _slot.next_seq(), _call[1])
+    if rc:
+        _lib.check(rc, "pm_collide1")
     _slot.wait()
-    vn2, vt2, om2 = _slot.doubles(0, 3)
-    return float(vn2), float(vt2), float(om2)
+    vn2, vt2, om2 = _slot.f64[0:3].tolist()
+    return vn2, vt2, om2

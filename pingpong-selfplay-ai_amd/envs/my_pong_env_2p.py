@@ -61,10 +61,12 @@ class PongEnv2P:
         self._env = PongEnv2PBatch(1, device=device, **{k: v for k, v in kw.items()})
         self._lib = _lib.load()
         self._slot = _lib.MappedSlot(18, 17)  # obsA[7] obsB[7] rA rB done | seq
-        # per-call constants made once: the argument references and the launch stream (the one current
-        # at construction; every call waits for its own result, so nothing else orders against it)
+        # per-call constants made once: the argument references, and the launch stream (the one current
+        # at construction, held so it outlives every launch; each call waits for its own result, so
+        # nothing else orders against it)
         self._pparams, self._pstate = ctypes.byref(self._env.params), ctypes.byref(self._env.state)
-        self._stream = _lib.stream_ptr()
+        self._stream_ref = _lib.current_stream()
+        self._stream = self._stream_ref.cuda_stream
         self._step1, self._reset1 = self._lib.pm_env_step1, self._lib.pm_env_reset1
         self._host = None
         if enable_render:

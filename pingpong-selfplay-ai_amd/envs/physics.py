@@ -24,7 +24,7 @@ def collide_batch(rows, device="cuda"):
 
 
 _slot = None
-_call = None  # (pm_collide1, launch stream), made on the first call
+_call = None  # (pm_collide1, launch stream handle, the stream object kept alive), made on the first call
 
 
 def collide_sphere_with_moving_plane(vn, vt, u, omega, e, mu, m, R):
@@ -33,7 +33,8 @@ def collide_sphere_with_moving_plane(vn, vt, u, omega, e, mu, m, R):
     global _slot, _call
     if _slot is None:
         _slot = _lib.MappedSlot(8, 6)  # vn' vt' omega' (fp64) | seq
-        _call = (_lib.load().pm_collide1, _lib.stream_ptr())
+        st = _lib.current_stream()
+        _call = (_lib.load().pm_collide1, st.cuda_stream, st)
     row = (ctypes.c_double * 8)(vn, vt, u, omega, e, mu, m, R)
     inertia = (2 / 5) * m * R ** 2  # CPython's I (:9)
     rc = _call[0](row, inertia, _slot.dev, _slot.next_seq(), _call[1])

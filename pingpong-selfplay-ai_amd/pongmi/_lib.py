@@ -310,6 +310,11 @@ def stream_ptr(stream=None):
     return s.cuda_stream
 
 
+def current_stream():
+    """The current torch stream object (callers that cache its handle keep the object alive)."""
+    return torch.cuda.current_stream()
+
+
 def require_device(t, name):
     if not t.is_cuda:
         raise PongmiError(f"{name} must be a ROCm device tensor (libpongmi has no CPU path)")

@@ -287,7 +287,7 @@ typedef struct pm_drqn_stats {
     float norm;     /* pre-clip total gradient norm of the last update (of the rank mean) */
     float q_mean;   /* mean q of the last batch */
     int32_t status; /* latched error bits: 2 = a hand-off inside pm_drqn_grads timed out on this replica;
-                     * 4 = pm_drqn_apply's norm arrival timed out (that block's slice not stepped);
+                     * 4 = (before round 6) pm_drqn_apply's norm arrival timed out; no longer set;
                      * 8 = an update was voided (a timeout on any rank: no Adam step, no target sync) */
 } pm_drqn_stats;
 
@@ -331,11 +331,9 @@ int pm_drqn_grads(const pm_drqn *d, void *stream);
 /* grad / grad[PM_RNN_NPARAM] -> clip_grad_norm_ -> Adam step -> target sync; stats updated.
  * Nothing happens when grad[PM_RNN_NPARAM] == 0. */
 int pm_drqn_apply(const pm_drqn *d, void *stream);
-/* pm_drqn_grads then pm_drqn_apply, the clip norm summed by the weight-gradient tiles as they store
- * (no arrival ticket). Its fp64 summation order differs from pm_drqn_apply's per-slice sum, so the two
- * single-replica paths give bit-identical parameters while the clip coefficient clamps to 1 and agree
- * to ~1e-6 relative when the clip is active (each is bitwise to the float32 clip + Adam restatement
- * given its own norm). */
+/* pm_drqn_grads then pm_drqn_apply, the clip norm's shares summed by the weight-gradient tiles as they
+ * store. pm_drqn_apply after an all-reduce forms the same shares of the summed gradient in the same
+ * order (round 6), so with one rank the two paths give bit-identical parameters, clip active or not. */
 int pm_drqn_update(const pm_drqn *d, void *stream);
 
 /* ---------------------------------------------------------------- QNetRNN self-play (K7) */

@@ -17,15 +17,16 @@
 //   k_dq_wgrad  (grads 3/3) the weight gradients: dWih = dZ F2^T, dWhh = dZ H^T and the biases over
 //               all T*B columns, dW_S = dS h_T^T and db_S over the B sequences (one workgroup per
 //               32x32 output tile, K split over 16 waves); per 32-column tile dF2 = Wih^T dZ -> ReLU
-//               mask -> dW2 / db2 partials -> dF1 = W2^T dP2 -> dW1 / db1 partials, summed in a fixed
-//               order by the last tile to finish (arrival ticket); the V / A head gradients summed
-//               over the sequences in order.
+//               mask -> dW2 / db2 partials -> dF1 = W2^T dP2 -> dW1 / db1 partials (the dF2 trailer
+//               of k_dq_recur forms dP2 / dP1); the V / A head gradients summed over the sequences in
+//               order; on one replica each tile's fp64 share of the clip norm.
 //   k_drqn_apply (pm_drqn_apply) the NoisyLinear sigma gradients (mu gradient x epsilon), the global-
-//               norm clip (fp64 partials met on an arrival ticket, summed in block order) and torch's
-//               Adam, target sync: four launches per update in all.
+//               norm clip (the tiles' shares in a fixed tree; replicas that all-reduce get the same
+//               shares of the summed gradient from k_dq_norm) and torch's Adam, target sync: four
+//               launches per update in all.
 //
 // Every reduction runs in a fixed order and nothing sums through atomics, so an update is
-// bit-reproducible run to run (the arrival ticket only picks which workgroup does the final sum).
+// bit-reproducible run to run.
 #include "pm_host.h"
 #include "pm_rnn.h"
 
@@ -69,8 +70,8 @@ struct DqArgs {
     float *XT;   // [32][C0]                  obs stream inputs x^T (rows 7..31 zero)
     double* part;
     double* NP;      // [kWgTiles + 1] per-block sums of squares of the final gradient (local_norm)
-    int64_t* tstep;
-    int32_t* flags;  // [0] update epoch (the granule tag base), [1] k_dq_wgrad's ticket, [2] k_drqn_apply's
+    int64_t* tstep;  // [2] steps, adam_t as k_dq_wgrad found them (the apply's counters)
+    int32_t* flags;  // [0] update epoch (the granule tag base); [1], [2] unused since round 6
     int poll_limit;  // polls per hand-off wait (pm_drqn.poll_limit: 0 = 2^20; < 0 = none, a test hook)
     int local_norm;  // 1: one replica (pm_drqn_update): k_dq_wgrad's blocks sum the clip norm's squares
 };
@@ -214,11 +215,7 @@ __global__ __launch_bounds__(512) void k_dq_embed(DqArgs a) {
     const int nMain = 3 * nct * T * 4;
     int bid = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
-    if (blockIdx.x == 0 && tid == 0) {  // a new tag epoch for k_dq_recur's hand-offs; the apply's ticket
-        a.flags[0] = a.flags[0] + 1;
-        a.flags[1] = 0;
-        a.flags[2] = 0;  // k_drqn_apply's arrival counter (monotonic within an apply, generation-based)
-    }
+    if (blockIdx.x == 0 && tid == 0) a.flags[0] = a.flags[0] + 1;  // a new tag epoch for k_dq_recur's hand-offs
     if (skipped(a)) {  // this replica contributes nothing to the all-reduce
         for (int i = blockIdx.x * 512 + tid; i < PM_RNN_NPARAM + 4; i += gridDim.x * 512) a.grad[i] = 0.f;
         return;
@@ -824,6 +821,10 @@ struct WgSmem {
 constexpr int kWgTiles = 64 + 64 + 16 + 8 + 2;
 
 __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the step counters the apply steps from (tstep): only the
+        a.tstep[0] = a.stats->steps;            // apply's block 0 advances them, so its other blocks must
+        a.tstep[1] = a.stats->adam_t;           // not read stats themselves (a late block would see ts + 1)
+    }
     if (skipped(a)) return;
     __shared__ WgSmem sm;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
@@ -963,6 +964,78 @@ __global__ __launch_bounds__(1024) void k_dq_wgrad(DqArgs a) {
     }
 }
 
+// The clip norm's shares of replicas that all-reduce (pm_drqn_apply after pm_drqn_grads and the
+// SUM), summed exactly as k_dq_wgrad's tiles sum them on the single-replica path (pm_drqn_update): the
+// same elements per workgroup in the same order, the same DPP wave sum and head-block tree, over the
+// values the apply steps with (the summed gradient over the rank count; a sigma gradient is mu
+// gradient x epsilon, then over the rank count, as the apply forms it). With one rank every share,
+// the clip coefficient and so every parameter are bit-identical to pm_drqn_update's, clip active or
+// not; with more ranks it is the norm of the averaged gradient, as before.
+__global__ __launch_bounds__(1024) void k_dq_norm(DqArgs a) {
+    const float ranks = a.grad[PM_RNN_NPARAM];
+    if (!(ranks > 0.f) || a.grad[PM_RNN_NPARAM + 1] != 0.f) return;  // grid-uniform: the apply does nothing
+    const float inv_world = 1.0f / ranks;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
+    const int bid = blockIdx.x;
+    const float* G = a.grad;
+    if (bid < kWgTiles) {
+        if (w != 0) return;
+        int mat, gt, kt;
+        if (bid < 128) { mat = bid >> 6; gt = (bid >> 2) & 15; kt = bid & 3; }
+        else if (bid < 144) { mat = 2; gt = (bid - 128) >> 2; kt = bid & 3; }
+        else if (bid < 152) { mat = 3; gt = (bid - 144) >> 1; kt = bid & 1; }
+        else { mat = 4; gt = bid - 152; kt = 0; }
+        const int ldg = mat <= 2 ? 128 : (mat == 3 ? 64 : 7);
+        const int gbase = mat == 0 ? R_P_WIH : (mat == 1 ? R_P_WHH : (mat == 2 ? R_P_SWMU : (mat == 3 ? R_P_F2W : R_P_F1W)));
+        double sq = 0.0;
+        if (32 * kt + col < ldg)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int e = (32 * gt + rho(r) + 4 * h) * ldg + 32 * kt + col;
+                const float v = G[gbase + e] * inv_world;
+                sq += (double)v * (double)v;
+                if (mat == 2) {
+                    const float gs = (G[gbase + e] * a.params[R_P_SWEP + e]) * inv_world;
+                    sq += (double)gs * (double)gs;
+                }
+            }
+        if (mat != 1 && kt == 0 && h == 0) {  // the bias rows (k_dq_wgrad's row sums)
+            const int row = 32 * gt + col;
+            const int bi = mat == 0 ? R_P_BIH : (mat == 2 ? R_P_SBMU : (mat == 3 ? R_P_F2B : R_P_F1B));
+            const float v = G[bi + row] * inv_world;
+            sq += (mat == 0 ? 2.0 : 1.0) * ((double)v * (double)v);
+            if (mat == 2) {
+                const float gs = (G[bi + row] * a.params[R_P_SBEP + row]) * inv_world;
+                sq += (double)gs * (double)gs;
+            }
+        }
+        sq = wave_sum(sq);
+        if (lane == 0) a.NP[bid] = sq;
+        return;
+    }
+    // the V / A heads and their biases, k_dq_wgrad's last workgroup's thread mapping and tree
+    __shared__ double red[1024];
+    double sq = 0.0;
+    if (tid < 512) {
+        const int o = tid >> 7, r = tid & 127, e = o == 0 ? r : 128 * (o - 1) + r;
+        const int mu = (o == 0 ? R_P_VWMU : R_P_AWMU) + e, ep = (o == 0 ? R_P_VWEP : R_P_AWEP) + e;
+        const float v = G[mu] * inv_world, gs = (G[mu] * a.params[ep]) * inv_world;
+        sq = (double)v * (double)v + (double)gs * (double)gs;
+    } else if (tid < 516) {
+        const int o = tid - 512;
+        const int mu = o == 0 ? R_P_VBMU : R_P_ABMU + o - 1, ep = o == 0 ? R_P_VBEP : R_P_ABEP + o - 1;
+        const float v = G[mu] * inv_world, gs = (G[mu] * a.params[ep]) * inv_world;
+        sq = (double)v * (double)v + (double)gs * (double)gs;
+    }
+    red[tid] = sq;
+    __syncthreads();
+    for (int kk = 512; kk > 0; kk >>= 1) {
+        if (tid < kk) red[tid] += red[tid + kk];
+        __syncthreads();
+    }
+    if (tid == 0) a.NP[kWgTiles] = red[0];
+}
+
 // NoisyLinear sigma gradients: d sigma = dW * epsilon (NoisyLinear.forward :45-46). Linear in the
 // mu gradient with the same epsilon on every rank, so it is formed after the all-reduce (apply).
 __device__ __forceinline__ int sigma_source(int i, int& ep) {
@@ -981,17 +1054,17 @@ struct AdamK {
     int64_t interval;
 };
 
-// One launch for the apply (round 3): every block forms its slice's sigma gradients and fp64 sum of
-// squares, arrives on a monotonic ticket and waits for the other blocks (kNormBlocks = 256, one per
-// CU: all resident), sums the 256 partials in block order — the same order in every block, so every
-// block derives the identical clip coefficient — and runs Adam on its slice of the parameters.
+// One launch for the apply: every block forms its slice's sigma gradients, sums the norm's shares
+// (NP: k_dq_wgrad's tiles on one replica, k_dq_norm's after an all-reduce, the same order) in one
+// fixed tree — the same in every block, so every block derives the identical clip coefficient — and
+// runs Adam on its slice of the parameters. The step counters come from k_dq_wgrad's snapshot
+// (tstep): block 0 advances stats, so no block reads stats itself (no arrival, no ticket).
 __global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* params, float* target, float* m_,
                                                     float* v_) {
     constexpr int kPer = (PM_RNN_NP + kNormBlocks - 1) / kNormBlocks, kEl = (kPer + 255) / 256;
     __shared__ double red[256];
     __shared__ float cf[3];
     __shared__ int64_t ts_s;
-    __shared__ int late;
     const float ranks = a.grad[PM_RNN_NPARAM];  // replicas that contributed (summed by the all-reduce)
     if (!(ranks > 0.f)) return;                 // grid-uniform
     if (a.grad[PM_RNN_NPARAM + 1] != 0.f) {     // a hand-off timed out on some rank: the update is void
@@ -999,12 +1072,11 @@ __global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* pa
         return;                                 // grid-uniform: no Adam, no target sync, no step count
     }
     const float inv_world = 1.0f / ranks;
-    const int64_t ts = a.stats->steps + 1, at = a.stats->adam_t + 1;  // read before any block's arrival
+    const int64_t ts = a.tstep[0] + 1, at = a.tstep[1] + 1;  // k_dq_wgrad's snapshot of the counters
     // one slice per block for both phases, every operand loaded up front (kEl elements per thread):
     // the sigma gradients a block forms are the ones its Adam reads
     const int plo = blockIdx.x * kPer, phi = min(PM_RNN_NP, plo + kPer);
     float g[kEl], mm[kEl], vv[kEl], pr[kEl];
-    double sq = 0.0;
 #pragma unroll
     for (int e = 0; e < kEl; ++e) {
         const int i = plo + threadIdx.x + 256 * e;
@@ -1018,40 +1090,12 @@ __global__ __launch_bounds__(256) void k_drqn_apply(DqArgs a, AdamK k, float* pa
             vv[e] = v_[i];
             if (src >= 0) a.grad[i] = graw;
             g[e] = graw * inv_world;
-            sq += (double)g[e] * (double)g[e];
         }
     }
-    if (a.local_norm) {  // one replica: k_dq_wgrad's blocks already summed the squares, no arrival needed
-        static_assert(kWgTiles + 1 <= 256, "norm partials");
-        red[threadIdx.x] = (int)threadIdx.x <= kWgTiles ? a.NP[threadIdx.x] : 0.0;
-    } else {
-    red[threadIdx.x] = sq;
-    __syncthreads();
-    for (int kk = 128; kk > 0; kk >>= 1) {
-        if (threadIdx.x < kk) red[threadIdx.x] += red[threadIdx.x + kk];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(a.part + blockIdx.x, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        drain();
-        const uint32_t tk = atomicAdd(reinterpret_cast<unsigned*>(a.flags + 2), 1u);
-        const uint32_t goal = (tk / kNormBlocks + 1) * kNormBlocks;  // this update's generation complete
-        late = 0;
-        for (int it = 0;; ++it) {
-            if ((uint32_t)__hip_atomic_load(a.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - goal < 0x80000000u)
-                break;
-            if (it >= (1 << 22)) {  // the norm would be partial: this block leaves its slice untouched
-                atomicOr(&a.stats->status, 4);
-                late = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __syncthreads();
-    if (late) return;  // block-uniform
-    red[threadIdx.x] = __hip_atomic_load(a.part + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // the clip norm's shares: k_dq_wgrad's tiles (one replica) or k_dq_norm (replicas that all-reduce),
+    // in the same order either way
+    static_assert(kWgTiles + 1 <= 256, "norm partials");
+    red[threadIdx.x] = (int)threadIdx.x <= kWgTiles ? a.NP[threadIdx.x] : 0.0;
     __syncthreads();
     for (int kk = 128; kk > 0; kk >>= 1) {  // the same fixed tree in every block
         if (threadIdx.x < kk) red[threadIdx.x] += red[threadIdx.x + kk];
@@ -1157,6 +1201,10 @@ static int drqn_apply(const pm_drqn* d, void* stream, int local_norm) {
     a.local_norm = local_norm;
     a.params = d->params; a.target = d->target; a.grad = d->grad; a.stats = d->stats;
     AdamK k{d->lr, d->beta1, d->beta2, d->adam_eps, d->max_norm, d->target_update_interval};
+    if (!local_norm) {  // replicas: the shares of the summed gradient's norm, in k_dq_wgrad's order
+        hipLaunchKernelGGL(k_dq_norm, dim3(kWgTiles + 1), dim3(1024), 0, st, a);
+        PM_LAUNCHED("k_dq_norm");
+    }
     hipLaunchKernelGGL(k_drqn_apply, dim3(kNormBlocks), dim3(256), 0, st, a, k, d->params, d->target, d->adam_m,
                        d->adam_v);
     PM_LAUNCHED("k_drqn_apply");
@@ -1174,8 +1222,9 @@ extern "C" int pm_drqn_init(const pm_drqn* d, void* stream) {
 extern "C" int pm_drqn_grads(const pm_drqn* d, void* stream) { return drqn_grads(d, stream, 0); }
 extern "C" int pm_drqn_apply(const pm_drqn* d, void* stream) { return drqn_apply(d, stream, 0); }
 
-// One replica: the weight-gradient blocks sum the clip norm's squares as they store the gradient, so
-// the apply needs no arrival ticket (replicas that all-reduce call pm_drqn_grads / pm_drqn_apply).
+// One replica: the weight-gradient blocks sum the clip norm's shares as they store the gradient
+// (replicas that all-reduce call pm_drqn_grads / pm_drqn_apply, whose k_dq_norm forms the same shares
+// of the summed gradient: with one rank the two paths are bit-identical, clip active or not).
 extern "C" int pm_drqn_update(const pm_drqn* d, void* stream) {
     if (int rc = drqn_grads(d, stream, 1)) return rc;
     return drqn_apply(d, stream, 1);

@@ -98,9 +98,9 @@ class DRQNLearner:
 
     def stats(self):
         """(steps, loss, pre-clip grad norm, mean q, status) of the last update (host sync). status
-        (latched) 2: a hand-off inside pm_drqn_grads timed out on this replica; 4: the apply's norm
-        arrival timed out; 8: an update was voided (a timeout on any rank: parameters, Adam state, step
-        count and target left as they were)."""
+        (latched) 2: a hand-off inside pm_drqn_grads timed out on this replica; 4: (before round 6) the
+        apply's norm arrival timed out; 8: an update was voided (a timeout on any rank: parameters, Adam
+        state, step count and target left as they were)."""
         s = _lib.DrqnStats.from_buffer_copy(bytes(self.stats_buf.cpu().numpy()))
         return dict(steps=s.steps, adam_t=s.adam_t, loss=s.loss, norm=s.norm, q_mean=s.q_mean, status=s.status)
 

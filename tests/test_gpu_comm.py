@@ -70,15 +70,15 @@ def test_sharded_step_equals_launch_sequence(golden, comm, U):
     assert A.counters()["train_steps"] > 0
 
 
-def test_rnn_sharded_step_equals_update(golden, comm):
+@pytest.mark.parametrize("clip", [1e6, 1e-3])
+def test_rnn_sharded_step_equals_update(golden, comm, clip):
     from test_gpu_rnn_selfplay import _learner as rnn_learner
-    # The two norm paths sum the clip norm's squares in different fp64 orders (pm_drqn_update: per
-    # k_dq_wgrad tile; grads -> all-reduce -> apply: per parameter slice), so their parameters are
-    # bit-equal only while the clip coefficient clamps to 1 (pongmi.h, pm_drqn_update): the clip is
-    # kept inactive here by construction; tests/test_gpu_drqn.py::test_drqn_clip_active_both_norm_paths
-    # covers the active clip (each path bitwise vs the restatement, the two within 1e-6).
+    # The sharded step (grads -> RCCL all-reduce -> apply, whose k_dq_norm forms the clip norm's shares
+    # of the summed gradient) against pm_drqn_update (the shares from k_dq_wgrad's tiles): the same
+    # order (round 6), so with one rank the parameters are bit-identical with the clip inactive (1e6)
+    # and active on every update (1e-3).
     kw = dict(n=512, n_pool=1, epsilon=0.5, memory_size=2000, min_episodes_for_training_start=1, seed=4,
-              grad_clip_norm=1e6)
+              grad_clip_norm=clip)
     A = rnn_learner(golden, **kw)
     B = rnn_learner(golden, allreduce=comm, **kw)
     for _ in range(50):

@@ -299,31 +299,32 @@ def test_drqn_clip_adam_exact(golden):
 
 
 def test_drqn_clip_active_both_norm_paths(golden, orc):
-    """max_norm small enough that the clip scales every gradient (ADVICE r4): the single-replica
-    update (pm_drqn_update: the clip norm summed by k_dq_wgrad's tiles) and the replica path
-    (pm_drqn_grads -> pm_drqn_apply: the norm summed per parameter slice after the all-reduce) each
-    equal the float32 clip + Adam restatement bit for bit given their own gradient and norm; the two
-    norms agree to 1e-6 (different fp64 summation orders), so their parameters agree to an ulp-level
-    tolerance, not bitwise."""
+    """max_norm small enough that the clip scales every gradient (ADVICE r4 / r5): the single-replica
+    update (pm_drqn_update: the clip norm's shares summed by k_dq_wgrad's tiles) and the replica path
+    (pm_drqn_grads -> pm_drqn_apply: k_dq_norm forms the same shares of the (all-reduced) gradient in
+    the same order, round 6) each equal the float32 clip + Adam restatement bit for bit given their
+    own gradient and norm, and with one rank the two are bit-identical: norm, parameters, moments."""
     from pongmi._lib import PM_RNN_NPARAM
     from pongmi.drqn import DRQNLearner
     gr, gd = golden("rnn"), golden("drqn")
-    b = tuple(torch.from_numpy(x) for x in _batch(gd, 0))
     outs = []
     for split in (False, True):
         L = DRQNLearner(_sd(gr), batch=64, T=8, max_norm=0.01)
-        p0, m0, v0 = _snap(L)
-        if split:
-            L.grads(*b)
-            L.apply()
-        else:
-            L.update(*b)
-        st = L.stats()
-        assert 0.01 / (st["norm"] + 1e-6) < 1.0  # the clip is active
-        _assert_apply_exact(L, p0, m0, v0, 1, "split" if split else "fused")
-        outs.append((st["norm"], L.params.cpu().numpy()[:PM_RNN_NPARAM].copy()))
-    np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-6)
-    np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-9)
+        for k in range(2):
+            b = tuple(torch.from_numpy(x) for x in _batch(gd, k))
+            p0, m0, v0 = _snap(L)
+            if split:
+                L.grads(*b)
+                L.apply()
+            else:
+                L.update(*b)
+            st = L.stats()
+            assert 0.01 / (st["norm"] + 1e-6) < 1.0  # the clip is active
+            _assert_apply_exact(L, p0, m0, v0, k + 1, ("split" if split else "fused") + f" update {k}")
+        outs.append((st["norm"], L.params.clone(), L.adam_m.clone(), L.adam_v.clone(), L.grad.clone()))
+    assert outs[0][0] == outs[1][0]
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        assert torch.equal(a, b)
 
 
 def test_drqn_timeout_voids_update(golden):

@@ -540,7 +540,7 @@ def run_rnn(args, dist, rank, world, allreduce):
             out["cpu_baseline"] = cpu_baseline_rnn(args.cpu_seconds)
         if failed:
             out["error"] = "device status bit 0 (overwritten ring read) / shard proof failed"
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist is not None:
         dist.destroy_process_group()
     if failed:
@@ -753,7 +753,7 @@ def run_infer(args, dist, rank, world):
                                               "k_rollout_push dispatch time; the launch is MFMA-latency bound"}
             out["stepped"] = None
             out["replay"] = {"pos": replay.pos, "size": replay.size}
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -858,7 +858,23 @@ def run_train(args, dist, rank, world):
                                                   "thread (SURVEY 6); a 2 400-episode try is ~91 k steps"},
             "vs_reference_loop": {k: round(value / v, 1) for k, v in REF_LOOP_STEPS_PER_S.items()},
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
+
+
+def emit(out):
+    """Rank 0's one JSON line (marked when the ranks are a rehearsal sharing GPUs, see rehearsal())."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and rehearsal(os.environ):
+        out["rehearsal"] = ("N ranks sharing the visible GPU(s) over gloo (PONGMI_BENCH_REHEARSE=1): a check of the "
+                            "multi-rank path, not a scaling number")
+    print(json.dumps(out), flush=True)
+
+
+def rehearsal(env):
+    """PONGMI_BENCH_REHEARSE=1 (a test hook the driver never sets): N > 1 ranks may share the visible
+    GPUs (rank r on device r mod count) and talk over gloo, so the multi-rank path (spawn, barriers,
+    max-over-ranks timing, the shard proof, replica identity, the sharded steps) runs end to end on a
+    1-GPU box. The line says so ("rehearsal") and is no scaling number: the ranks share one device."""
+    return env.get("PONGMI_BENCH_REHEARSE", "0") not in ("", "0")
 
 
 def launch_plan(argv, env, device_count):
@@ -881,12 +897,12 @@ def launch_plan(argv, env, device_count):
         if int(ws) != n:
             return "error", (f"--gpus {n} but WORLD_SIZE={ws}: the launcher started a different number of ranks "
                              f"than the bench was asked to report")
-        if device_count is not None and int(env.get("LOCAL_RANK", "0")) >= device_count:
+        if device_count is not None and int(env.get("LOCAL_RANK", "0")) >= device_count and not rehearsal(env):
             return "error", f"LOCAL_RANK {env.get('LOCAL_RANK')} but only {device_count} visible GPU(s)"
         return "run", None
     if n == 1:
         return "run", None
-    if device_count is not None and device_count < n:
+    if device_count is not None and device_count < n and not rehearsal(env):
         return "error", f"--gpus {n} but only {device_count} visible GPU(s) on this node"
     import socket
     with socket.socket() as s:  # a free rendezvous port on the loopback (the hostname may not resolve)
@@ -953,17 +969,25 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # configs[0]'s scalar CPU loop runs in forked worker processes: before this process touches the GPU
     args.cpu_config0 = cpu_config0() if world == 1 and args.workload == "dqn" and not args.no_cpu_baseline else None
+    rehearse = world > 1 and rehearsal(os.environ)
+    if rehearse:  # ranks share the visible devices; gloo, torch.distributed all-reduce (RCCL wants one GPU per rank)
+        local = local % max(torch.cuda.device_count(), 1)
+        args.comm = "torch"
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     comm = None
     if dist is not None and args.comm == "native" and not infer:
         from pongmi.dist import NativeComm
         comm = NativeComm()  # raises on every rank if RCCL cannot be bound: no silent fallback
-    args.comm_used = "native RCCL, in-stream" if comm is not None else "torch.distributed"
+    args.comm_used = ("native RCCL, in-stream" if comm is not None
+                      else "torch.distributed (gloo)" if rehearse else "torch.distributed")
     args.comm = comm
     allreduce = comm if comm is not None else ((lambda t: dist.all_reduce(t)) if dist else None)
 
@@ -1067,7 +1091,7 @@ def main():
                 out["cpu_config0"] = args.cpu_config0
         if failed:
             out["error"] = "device status / shard proof failed: see learner.status and config.shards"
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist is not None:
         dist.destroy_process_group()
     if failed:

@@ -71,3 +71,14 @@ def test_bench_refuses_end_to_end():
     assert "visible GPU" in line["error"] and "value" not in line
     r = _run(["--gpus", "1", "--no-cpu-baseline"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE=2" in json.loads(r.stdout.strip().splitlines()[-1])["error"]
+
+
+def test_rehearsal_lets_ranks_share_a_gpu():
+    # PONGMI_BENCH_REHEARSE=1 (never set by the driver): the 1-GPU refusals are lifted so the N-rank
+    # path can be exercised on one device; without it they stand (test_mismatches_are_refused)
+    b = _bench()
+    env = {"PONGMI_BENCH_REHEARSE": "1"}
+    assert b.launch_plan(["--gpus", "2"], env, 1)[0] == "spawn"
+    assert b.launch_plan(["--gpus", "2"], dict(env, WORLD_SIZE="2", LOCAL_RANK="1"), 1) == ("run", None)
+    assert b.launch_plan(["--gpus", "2"], dict(env, WORLD_SIZE="4", LOCAL_RANK="1"), 1)[0] == "error"
+    assert b.launch_plan(["--gpus", "2"], {"PONGMI_BENCH_REHEARSE": "0"}, 1)[0] == "error"

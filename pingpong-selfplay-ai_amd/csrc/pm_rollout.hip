@@ -564,7 +564,7 @@ __device__ __forceinline__ void roll16_draws(const pm_env_params& p, Roll16Share
     }
 }
 
-template <bool PUSH, bool MH>
+template <bool PUSH, bool MH, bool W2R = false>
 __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_env_state& s, const float* __restrict__ wA,
                                                const float* __restrict__ wB, const float* __restrict__ ws, double eps,
                                                uint64_t seed_env, uint64_t counter0, int steps, float* __restrict__ obsA,
@@ -616,6 +616,13 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     if (MH && wv == 6) roll16_opw(sm, 0, wA + PLAIN + F_H);  // modelA's heads straight from global
     __syncthreads();
     const float4* im2 = reinterpret_cast<const float4*>(sm.img2[player][rt][0][lane]);
+    // W2R: the wave's layer-1 and layer-2 A operands and layer-2 bias, constant over the launch, held in
+    // registers (2 + 16 + 4) instead of read from LDS every step
+    float4 w2r[4], b2r{};
+    const float2 w1r = W2R ? *reinterpret_cast<const float2*>(sm.img1[player][rt][lane]) : float2{};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) w2r[s4] = W2R ? im2[s4 * 64] : float4{};
+    if (W2R) b2r = *reinterpret_cast<const float4*>(sm.b2v[player][rt][g]);
 #ifdef PM_DIAG
     const bool diag = blockIdx.x == 0 && wv < 2;
     unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dprev = __builtin_amdgcn_s_memtime();
@@ -627,7 +634,7 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
         {
             const float* o = sm.ob[player][col];
             const float x0 = g == 0 ? 1.0f : o[g - 1], x1 = o[3 + g];
-            const float2 w1 = *reinterpret_cast<const float2*>(sm.img1[player][rt][lane]);
+            const float2 w1 = W2R ? w1r : *reinterpret_cast<const float2*>(sm.img1[player][rt][lane]);
             const f32x4v16 zero = {0.f, 0.f, 0.f, 0.f};
             f32x4v16 c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, x0, zero, 0, 0, 0);
             c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.y, x1, c1, 0, 0, 0);
@@ -648,12 +655,12 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
                 bs[4 * k] = v.x; bs[4 * k + 1] = v.y; bs[4 * k + 2] = v.z; bs[4 * k + 3] = v.w;
             }
         }
-        const float4 bi = *reinterpret_cast<const float4*>(sm.b2v[player][rt][g]);
+        const float4 bi = W2R ? b2r : *reinterpret_cast<const float4*>(sm.b2v[player][rt][g]);
         f32x4v16 c2 = {bi.x, bi.y, bi.z, bi.w};
 
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-            const float4 w = im2[s4 * 64];
+            const float4 w = W2R ? w2r[s4] : im2[s4 * 64];
             c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, bs[4 * s4 + 0], c2, 0, 0, 0);
             c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, bs[4 * s4 + 1], c2, 0, 0, 0);
             c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, bs[4 * s4 + 2], c2, 0, 0, 0);
@@ -830,14 +837,14 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     if (lane < NS) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane), (unsigned long long)mv);
 }
 
-template <bool MH>
+template <bool MH, bool W2R>
 __global__ __launch_bounds__(kR16Block) void k_rollout16(const pm_env_params p, const pm_env_state s,
                                                          const float* __restrict__ wA, const float* __restrict__ wB,
                                                          const float* __restrict__ ws, double eps, uint64_t seed_env,
                                                          uint64_t counter0, int steps, float* __restrict__ obsA,
                                                          float* __restrict__ obsB, long long* __restrict__ stats,
                                                          int n) {
-    rollout16_body<false, MH>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
+    rollout16_body<false, MH, W2R>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
 }
 // the collecting launch runs 65 536 arenas (4 096 blocks): two blocks per CU (4 waves per SIMD) need
 // <= 128 registers
@@ -851,7 +858,8 @@ __global__ __launch_bounds__(kR16Block) __attribute__((amdgpu_waves_per_eu(4, 4)
 
 // 16-arena tiles: PONGMI_ROLL16 bit 0 = the inference launch, bit 1 = the collecting launch (A/B),
 // bit 2 = the round-4 VALU head chains instead of the MFMA ones in the inference launch (A/B), bit 3 =
-// the 32-arena-tile kernels with the replicated tick (rollout_body) instead of rollout_body1; default 1. Read at every
+// the 32-arena-tile kernels with the replicated tick (rollout_body) instead of rollout_body1, bit 4 = the
+// inference launch's layer-2 weights read from LDS every step (round 5) instead of held in registers; default 1. Read at every
 // launch (one getenv), so a test can cover every kernel in one process.
 int roll16() {
     const char* e = getenv("PONGMI_ROLL16");
@@ -896,7 +904,9 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
         return PM_OK;
     }
     if (r16 & 1) {
-        pm_launch(PM_TIMER_ROLLOUT, (r16 & 4) ? k_rollout16<false> : k_rollout16<true>, dim3(pm_blocks(n, 16)),
+        const auto kern = (r16 & 16) ? ((r16 & 4) ? k_rollout16<false, false> : k_rollout16<true, false>)
+                                     : ((r16 & 4) ? k_rollout16<false, true> : k_rollout16<true, true>);
+        pm_launch(PM_TIMER_ROLLOUT, kern, dim3(pm_blocks(n, 16)),
                   dim3(kR16Block), st, *p, *s, wA, wB, (const float*)heads_ws, (double)epsilon, seed_env, counter0,
                   (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n);
         PM_LAUNCHED("k_rollout16");

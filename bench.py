@@ -104,10 +104,10 @@ def pmc_traffic(kernel, profile="r3_pmc.json"):
     """HBM bytes per launch of `kernel` (`name`, or `name@grid` for one of its launch grids) from the
     committed rocprofv3 counter profile (profiles/r3_pmc.json: the default workload;
     profiles/r3_rnn_pmc.json: --workload rnn; profiles/r3_infer_pmc.json: --workload infer, 2 000-step
-    launches), or None. The newest round's profile of the same name (r5_pmc.json, r4_pmc.json, …) wins
+    launches), or None. The newest round's profile of the same name (r6_pmc.json, r5_pmc.json, …) wins
     when it holds the kernel."""
     stem = profile[3:] if profile.startswith("r3_") else profile
-    for name in (f"r5_{stem}", f"r4_{stem}", profile):
+    for name in (f"r6_{stem}", f"r5_{stem}", f"r4_{stem}", profile):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as fh:
                 return json.load(fh)["kernels"][kernel]["hbm_bytes"]

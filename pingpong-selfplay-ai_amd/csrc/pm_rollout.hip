@@ -564,7 +564,22 @@ __device__ __forceinline__ void roll16_draws(const pm_env_params& p, Roll16Share
     }
 }
 
-template <bool PUSH, bool MH, bool W2R = false>
+// PL: the heads' cross-lane moves on the gfx950 row / half swaps instead of ds_bpermute round trips.
+// xor16_sum: v + (v of lane ^ 16) as v_permlane16_swap (rows 0 <-> 1 and 2 <-> 3 exchanged between two
+// copies), so each lane adds the same pair: the same bits as v + __shfl_xor(v, 16) (an IEEE add
+// commutes). halves_bcast: lanes 0-31's value in both halves (lo) and lanes 32-63's (hi), one
+// v_permlane32_swap for both.
+__device__ __forceinline__ float xor16_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void halves_bcast(int v, int& lo, int& hi) {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    lo = (int)r[0];
+    hi = (int)r[1];
+}
+
+template <bool PUSH, bool MH, bool W2R = false, bool PL = false>
 __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_env_state& s, const float* __restrict__ wA,
                                                const float* __restrict__ wB, const float* __restrict__ ws, double eps,
                                                uint64_t seed_env, uint64_t counter0, int steps, float* __restrict__ obsA,
@@ -701,14 +716,27 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
                 const float4 x = *reinterpret_cast<const float4*>(sm.c2s[hp][hh][k][col]);
                 xb[4 * k] = x.x; xb[4 * k + 1] = x.y; xb[4 * k + 2] = x.z; xb[4 * k + 3] = x.w;
             }
+            // PL: player B's epsilon branch read before the chain, not behind the argmax
+            const int ea_pre = PL ? sm.epsa[st & 1][col] : 0;
             f32x4v16 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < 32; ++q) acc = __builtin_amdgcn_mfma_f32_4x4x1f32(hw4[q], xb[q], acc, 0, 0, 0);
+            if constexpr (PL) {  // every operand read issued ahead of the chain (one wait per read, in order)
+                __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);  // DS reads
+                __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);  // the MFMAs
+            }
             float v = acc[0], a0 = acc[1], a1 = acc[2], a2 = acc[3];
-            v += __shfl_xor(v, 16);  // + the other half (both lanes get the same bits)
-            a0 += __shfl_xor(a0, 16);
-            a1 += __shfl_xor(a1, 16);
-            a2 += __shfl_xor(a2, 16);
+            if constexpr (PL) {  // + the other half (both lanes get the same bits)
+                v = xor16_sum(v);
+                a0 = xor16_sum(a0);
+                a1 = xor16_sum(a1);
+                a2 = xor16_sum(a2);
+            } else {
+                v += __shfl_xor(v, 16);
+                a0 += __shfl_xor(a0, 16);
+                a1 += __shfl_xor(a1, 16);
+                a2 += __shfl_xor(a2, 16);
+            }
             v += hf[256];
             a0 += hf[257];
             a1 += hf[258];
@@ -717,11 +745,15 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             const float qv[3] = {v + (a0 - mean), v + (a1 - mean), v + (a2 - mean)};
             int act = argmax3(qv);
             if (hp) {  // random.random() < eps ? randint(0, 2) : argmax (train_iterative.py:126-130)
-                const int ea = sm.epsa[st & 1][col];
+                const int ea = PL ? ea_pre : sm.epsa[st & 1][col];
                 if (ea >= 0) act = ea;
             }
-            aA = __shfl(act, col);
-            aB = __shfl(act, 32 + col);
+            if constexpr (PL) {
+                halves_bcast(act, aA, aB);  // rows 0 and 1 (2 and 3) hold the same actions
+            } else {
+                aA = __shfl(act, col);
+                aB = __shfl(act, 32 + col);
+            }
         }
         if (wv == 0) {
           if constexpr (!MH) {
@@ -837,14 +869,14 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     if (lane < NS) atomicAdd(reinterpret_cast<unsigned long long*>(stats + lane), (unsigned long long)mv);
 }
 
-template <bool MH, bool W2R>
+template <bool MH, bool W2R, bool PL>
 __global__ __launch_bounds__(kR16Block) void k_rollout16(const pm_env_params p, const pm_env_state s,
                                                          const float* __restrict__ wA, const float* __restrict__ wB,
                                                          const float* __restrict__ ws, double eps, uint64_t seed_env,
                                                          uint64_t counter0, int steps, float* __restrict__ obsA,
                                                          float* __restrict__ obsB, long long* __restrict__ stats,
                                                          int n) {
-    rollout16_body<false, MH, W2R>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
+    rollout16_body<false, MH, W2R, PL>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
 }
 // the collecting launch runs 65 536 arenas (4 096 blocks): two blocks per CU (4 waves per SIMD) need
 // <= 128 registers
@@ -859,7 +891,8 @@ __global__ __launch_bounds__(kR16Block) __attribute__((amdgpu_waves_per_eu(4, 4)
 // 16-arena tiles: PONGMI_ROLL16 bit 0 = the inference launch, bit 1 = the collecting launch (A/B),
 // bit 2 = the round-4 VALU head chains instead of the MFMA ones in the inference launch (A/B), bit 3 =
 // the 32-arena-tile kernels with the replicated tick (rollout_body) instead of rollout_body1, bit 4 = the
-// inference launch's layer-2 weights read from LDS every step (round 5) instead of held in registers; default 1. Read at every
+// inference launch's layer-2 weights read from LDS every step (round 5) instead of held in registers, bit 5 =
+// the MFMA heads' cross-lane moves through ds_bpermute (round 5) instead of the permlane swaps; default 1. Read at every
 // launch (one getenv), so a test can cover every kernel in one process.
 int roll16() {
     const char* e = getenv("PONGMI_ROLL16");
@@ -904,8 +937,11 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
         return PM_OK;
     }
     if (r16 & 1) {
-        const auto kern = (r16 & 16) ? ((r16 & 4) ? k_rollout16<false, false> : k_rollout16<true, false>)
-                                     : ((r16 & 4) ? k_rollout16<false, true> : k_rollout16<true, true>);
+        // bit 2: VALU heads (keeps the shuffles); bit 4: weights from LDS; bit 5: the heads' ds_bpermute moves
+        const bool pl = !(r16 & 32);
+        const auto kern = (r16 & 4) ? ((r16 & 16) ? k_rollout16<false, false, false> : k_rollout16<false, true, false>)
+                        : (r16 & 16) ? (pl ? k_rollout16<true, false, true> : k_rollout16<true, false, false>)
+                                     : (pl ? k_rollout16<true, true, true> : k_rollout16<true, true, false>);
         pm_launch(PM_TIMER_ROLLOUT, kern, dim3(pm_blocks(n, 16)),
                   dim3(kR16Block), st, *p, *s, wA, wB, (const float*)heads_ws, (double)epsilon, seed_env, counter0,
                   (int)steps, obsA, obsB, reinterpret_cast<long long*>(stats), n);

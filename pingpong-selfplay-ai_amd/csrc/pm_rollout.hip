@@ -579,6 +579,34 @@ __device__ __forceinline__ void halves_bcast(int v, int& lo, int& hi) {
     hi = (int)r[1];
 }
 
+// PL: the step's draws split so that neither outlasts wave 0's heads + tick (the single drawing wave,
+// three Philox blocks in a row behind a lane-group branch, was the last to reach barrier C). Wave 1:
+// the serve's two Philox blocks at once, lane group 0 on the first tag and group 1 on the second,
+// group 1's block handed to group 0 by a row swap, then the serve's fp64 stages; wave 2: player B's
+// epsilon branch. Same functions of the same counters, so the same bits.
+__device__ __forceinline__ void roll16_serve(const pm_env_params& p, Roll16Shared& sm, int i, uint64_t ctr, int b,
+                                             uint64_t seed, int g) {
+    const U4 r = philox((uint32_t)i, g == 1 ? (TAG_SERVE_STEP | 0x100u) : TAG_SERVE_STEP, (uint32_t)ctr,
+                        (uint32_t)(ctr >> 32), seed);
+    const auto sx = __builtin_amdgcn_permlane16_swap(r.x, r.x, false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(r.y, r.y, false, false);
+    const auto sz = __builtin_amdgcn_permlane16_swap(r.z, r.z, false, false);
+    const auto sw = __builtin_amdgcn_permlane16_swap(r.w, r.w, false, false);
+    StagedServe sv;
+    sv.r0 = r;
+    sv.r1 = U4{sx[1], sy[1], sz[1], sw[1]};  // rows 1 and 3's block in rows 0 and 2
+    sv.stage(2, p, (uint32_t)i, ctr, seed);
+    sv.stage(3, p, (uint32_t)i, ctr, seed);
+    if (g == 0) sm.sdraw[b][threadIdx.x & 15] = sv.d;
+}
+__device__ __forceinline__ void roll16_eps(Roll16Shared& sm, int i, uint64_t ctr, int b, double eps, uint64_t seed,
+                                           int g) {
+    if (g == 0) {
+        const U4 rr = philox64((uint32_t)i, TAG_ACT, ctr, seed);
+        sm.epsa[b][threadIdx.x & 15] = u53(rr.x, rr.y) < eps ? (int)below(rr.z, 3u) : -1;
+    }
+}
+
 template <bool PUSH, bool MH, bool W2R = false, bool PL = false>
 __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_env_state& s, const float* __restrict__ wA,
                                                const float* __restrict__ wB, const float* __restrict__ ws, double eps,
@@ -609,7 +637,9 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     }
     if (t < 260) sm.hfA[t] = t < 256 ? wA[PLAIN + F_H + t] : wA[PLAIN + F_BH + t - 256];
     if (wv == 7) fetch_heads(ws, 0, sm.hfB[0], lane);
-    if (wv == 1) roll16_draws(p, sm, i, counter0, 0, eps, seed_env, g);
+    if (PL && wv == 1) roll16_serve(p, sm, i, counter0, 0, seed_env, g);
+    if (PL && wv == 2) roll16_eps(sm, i, counter0, 0, eps, seed_env, g);
+    if (!PL && wv == 1) roll16_draws(p, sm, i, counter0, 0, eps, seed_env, g);
     // ---- wave 0 keeps the 16 arenas (every lane group a copy) and ticks them
     Arena a{};
     int fin = 0, winB = 0, ptA = 0, ptB = 0, winE = 0, rsum = 0;
@@ -648,7 +678,9 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
         // layer 1, the wave's row tile (K 8: bias + 7 inputs, input k' = 4 s + g) -> ReLU -> LDS
         {
             const float* o = sm.ob[player][col];
-            const float x0 = g == 0 ? 1.0f : o[g - 1], x1 = o[3 + g];
+            // PL: both inputs read together (one LDS wait, not a masked read, a wait, a read, a wait)
+            const float o0 = PL ? o[g == 0 ? 0 : g - 1] : 0.f;
+            const float x0 = PL ? (g == 0 ? 1.0f : o0) : (g == 0 ? 1.0f : o[g - 1]), x1 = o[3 + g];
             const float2 w1 = W2R ? w1r : *reinterpret_cast<const float2*>(sm.img1[player][rt][lane]);
             const f32x4v16 zero = {0.f, 0.f, 0.f, 0.f};
             f32x4v16 c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, x0, zero, 0, 0, 0);
@@ -701,6 +733,7 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
         __syncthreads();  // (B) both players' layer 2
         ROLL_T(3);
         int aA = 0, aB = 0;
+        ServeDraw sd_pre{};
         if (MH && wv == 0) {
             // heads on the matrix cores: one chain of 32 v_mfma_f32_4x4x1_16b_f32 (a k-ordered fmaf
             // chain bit for bit, tools/mfma4_probe.hip) covers every (player, half, column): block b =
@@ -716,8 +749,10 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
                 const float4 x = *reinterpret_cast<const float4*>(sm.c2s[hp][hh][k][col]);
                 xb[4 * k] = x.x; xb[4 * k + 1] = x.y; xb[4 * k + 2] = x.z; xb[4 * k + 3] = x.w;
             }
-            // PL: player B's epsilon branch read before the chain, not behind the argmax
+            // PL: player B's epsilon branch read before the chain, not behind the argmax, and the step's
+            // serve draw (applied to the arenas whose episode ends) before the tick, not inside its branch
             const int ea_pre = PL ? sm.epsa[st & 1][col] : 0;
+            if constexpr (PL) sd_pre = sm.sdraw[st & 1][col];
             f32x4v16 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < 32; ++q) acc = __builtin_amdgcn_mfma_f32_4x4x1f32(hw4[q], xb[q], acc, 0, 0, 0);
@@ -825,7 +860,7 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             if (d) {  // env.reset() with K1's step-keyed production serve
                 fin += 1;
                 winB += rB > 0.f ? 1 : 0;
-                ServeDraw sd = sm.sdraw[st & 1][col];
+                ServeDraw sd = (PL && MH) ? sd_pre : sm.sdraw[st & 1][col];
                 serve_finish(sd);
                 serve(a, sd.vx, sd.vy, sd.spin);
             }
@@ -835,8 +870,11 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
 #pragma unroll
                 for (int k = 0; k < 7; ++k) sm.ob[g][col][k] = g ? oB[k] : oA[k];
             ROLL_T(5);    // tick (+ push) + next observations
-        } else if (wv == 1 && st + 1 < steps) {
-            roll16_draws(p, sm, i, ctr + 1, (st + 1) & 1, eps, seed_env, g);  // the next step's draws
+        } else if (wv == 1 && st + 1 < steps) {  // the next step's draws
+            if constexpr (PL) roll16_serve(p, sm, i, ctr + 1, (st + 1) & 1, seed_env, g);
+            else roll16_draws(p, sm, i, ctr + 1, (st + 1) & 1, eps, seed_env, g);
+        } else if (PL && wv == 2 && st + 1 < steps) {
+            roll16_eps(sm, i, ctr + 1, (st + 1) & 1, eps, seed_env, g);
         } else if (MH && wv == 7 && st + 1 < steps) {
             roll16_opw(sm, 1 + ((st + 1) & 1), sm.hfB[(st + 1) & 1]);  // the next step's heads (landed before barrier B)
         }

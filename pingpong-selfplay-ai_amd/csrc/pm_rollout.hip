@@ -281,10 +281,27 @@ struct Roll1Shared {
     ServeDraw sdraw[2][32];   // [step & 1][column]
     int epsa[2][32];          // [step & 1][column]: -1 = argmax stands, else player B's random action
 };
+// PD: wave 0 draws the serve's two Philox blocks at once (lanes 0-31 the first tag, lanes 32-63 the
+// second, for the same arenas) and hands the second to lanes 0-31 by v_permlane32_swap: one block's
+// instruction stream instead of two in a row, the same bits.
+template <bool PD = false>
 __device__ __forceinline__ void roll1_draws(const pm_env_params& p, Roll1Shared& sm, int i, uint64_t ctr, int b,
                                             double eps, uint64_t seed, int wv, int lane) {
     const int col = lane & 31;
-    if (wv == 0 && lane < 32) {
+    if (PD && wv == 0) {
+        const U4 r = philox((uint32_t)i, lane >= 32 ? (TAG_SERVE_STEP | 0x100u) : TAG_SERVE_STEP, (uint32_t)ctr,
+                            (uint32_t)(ctr >> 32), seed);
+        const auto sx = __builtin_amdgcn_permlane32_swap(r.x, r.x, false, false);
+        const auto sy = __builtin_amdgcn_permlane32_swap(r.y, r.y, false, false);
+        const auto sz = __builtin_amdgcn_permlane32_swap(r.z, r.z, false, false);
+        const auto sw = __builtin_amdgcn_permlane32_swap(r.w, r.w, false, false);
+        StagedServe sv;
+        sv.r0 = U4{sx[0], sy[0], sz[0], sw[0]};  // lanes 0-31's block in both halves
+        sv.r1 = U4{sx[1], sy[1], sz[1], sw[1]};  // lanes 32-63's
+        sv.stage(2, p, (uint32_t)i, ctr, seed);
+        sv.stage(3, p, (uint32_t)i, ctr, seed);
+        if (lane < 32) sm.sdraw[b][col] = sv.d;
+    } else if (!PD && wv == 0 && lane < 32) {
         StagedServe sv;
 #pragma unroll
         for (int k = 0; k < 4; ++k) sv.stage(k, p, (uint32_t)i, ctr, seed);
@@ -294,7 +311,7 @@ __device__ __forceinline__ void roll1_draws(const pm_env_params& p, Roll1Shared&
         sm.epsa[b][col] = u53(rr.x, rr.y) < eps ? (int)below(rr.z, 3u) : -1;
     }
 }
-template <bool PUSH>
+template <bool PUSH, bool PD = false>
 __device__ __forceinline__ void rollout_body1(const pm_env_params& p, const pm_env_state& s, const float* __restrict__ wA,
                                               const float* __restrict__ wB, const float* __restrict__ ws, double eps,
                                               uint64_t seed_env, uint64_t counter0, int steps, float* __restrict__ obsA,
@@ -324,7 +341,7 @@ __device__ __forceinline__ void rollout_body1(const pm_env_params& p, const pm_e
             leafv = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(prio_pow(rp.prio, rp.alpha))));
         }
     }
-    roll1_draws(p, sm, i, counter0, 0, eps, seed_env, wv, lane);
+    roll1_draws<PD>(p, sm, i, counter0, 0, eps, seed_env, wv, lane);
     const float* lw = player ? sm.r.lwB : sm.r.lw;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // both images, step 0's heads, observations and draws in LDS
@@ -400,7 +417,7 @@ __device__ __forceinline__ void rollout_body1(const pm_env_params& p, const pm_e
 #pragma unroll
                 for (int k = 0; k < 7; ++k) { sm.ob[0][col][k] = oA[k]; sm.ob[1][col][k] = nB2[k]; }
         } else if (st + 1 < steps) {
-            roll1_draws(p, sm, i, ctr + 1, (st + 1) & 1, eps, seed_env, wv, lane);  // the next step's draws
+            roll1_draws<PD>(p, sm, i, ctr + 1, (st + 1) & 1, eps, seed_env, wv, lane);  // the next step's draws
         }
         __syncthreads();  // (C) the next observations
     }
@@ -446,19 +463,21 @@ __global__ __launch_bounds__(kRollBlock) __attribute__((amdgpu_waves_per_eu(3, 3
     rollout_body<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
 }
 // the one-tick bodies (rollout_body1)
+template <bool PD>
 __global__ __launch_bounds__(kRollBlock) void k_rollout1(const pm_env_params p, const pm_env_state s,
                                                          const float* __restrict__ wA, const float* __restrict__ wB,
                                                          const float* __restrict__ ws, double eps, uint64_t seed_env,
                                                          uint64_t counter0, int steps, float* __restrict__ obsA,
                                                          float* __restrict__ obsB, long long* __restrict__ stats,
                                                          int n) {
-    rollout_body1<false>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
+    rollout_body1<false, PD>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, RollPush{});
 }
+template <bool PD>
 __global__ __launch_bounds__(kRollBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_rollout_push1(
     const pm_env_params p, const pm_env_state s, const float* __restrict__ wA, const float* __restrict__ wB,
     const float* __restrict__ ws, double eps, uint64_t seed_env, uint64_t counter0, int steps,
     float* __restrict__ obsA, float* __restrict__ obsB, long long* __restrict__ stats, int n, const RollPush rp) {
-    rollout_body1<true>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
+    rollout_body1<true, PD>(p, s, wA, wB, ws, eps, seed_env, counter0, steps, obsA, obsB, stats, n, rp);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -930,7 +949,8 @@ __global__ __launch_bounds__(kR16Block) __attribute__((amdgpu_waves_per_eu(4, 4)
 // bit 2 = the round-4 VALU head chains instead of the MFMA ones in the inference launch (A/B), bit 3 =
 // the 32-arena-tile kernels with the replicated tick (rollout_body) instead of rollout_body1, bit 4 = the
 // inference launch's layer-2 weights read from LDS every step (round 5) instead of held in registers, bit 5 =
-// the MFMA heads' cross-lane moves through ds_bpermute (round 5) instead of the permlane swaps; default 1. Read at every
+// the MFMA heads' cross-lane moves through ds_bpermute (round 5) instead of the permlane swaps, bit 6 = the
+// one-tick 32-arena bodies' serve draw as two Philox blocks in a row (round 5); default 1. Read at every
 // launch (one getenv), so a test can cover every kernel in one process.
 int roll16() {
     const char* e = getenv("PONGMI_ROLL16");
@@ -967,7 +987,8 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
         return PM_OK;
     }
     if (rp) {
-        pm_launch(PM_TIMER_ROLLOUT, (r16 & 8) ? k_rollout_push : k_rollout_push1, grid, block, st, *p, *s, wA, wB,
+        pm_launch(PM_TIMER_ROLLOUT, (r16 & 8) ? k_rollout_push : ((r16 & 64) ? k_rollout_push1<false> : k_rollout_push1<true>),
+                  grid, block, st, *p, *s, wA, wB,
                   (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
                   reinterpret_cast<long long*>(stats), n, *rp);
         PM_LAUNCHED("k_rollout_push");
@@ -986,7 +1007,8 @@ static int rollout_launch(const pm_env_params* p, const pm_env_state* s, const f
         PM_LAUNCHED("k_rollout16");
         return PM_OK;
     }
-    pm_launch(PM_TIMER_ROLLOUT, (r16 & 8) ? k_rollout : k_rollout1, grid, block, st, *p, *s, wA, wB,
+    pm_launch(PM_TIMER_ROLLOUT, (r16 & 8) ? k_rollout : ((r16 & 64) ? k_rollout1<false> : k_rollout1<true>), grid, block, st,
+              *p, *s, wA, wB,
               (const float*)heads_ws, (double)epsilon, seed_env, counter0, (int)steps, obsA, obsB,
               reinterpret_cast<long long*>(stats), n);
     PM_LAUNCHED("k_rollout");

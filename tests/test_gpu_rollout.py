@@ -365,7 +365,7 @@ def test_collect_matches_oracle(orc, n, steps_per_launch, launches):
     assert got[0] > 0
 
 
-@pytest.mark.parametrize("tiles", [0, 3, 7, 8, 19, 23, 35])
+@pytest.mark.parametrize("tiles", [0, 3, 7, 8, 19, 23, 35, 64])
 def test_rollout_tile_variants_match_oracle(orc, monkeypatch, tiles):
     """Every rollout kernel against the oracle: PONGMI_ROLL16=0 runs the 32-arena-tile
     k_rollout (inference) and k_rollout_push (collecting, the default there); =3 runs the 16-arena-tile
@@ -373,8 +373,9 @@ def test_rollout_tile_variants_match_oracle(orc, monkeypatch, tiles):
     only); =7 the same with k_rollout16's round-4 VALU head chains; =8 the 32-arena-tile kernels with
     the round-4 replicated tick (rollout_body; 0 runs the one-tick rollout_body1); 19 / 23 = 3 / 7 with
     k_rollout16's weights read from LDS every step (round 5) instead of held in registers; 35 = 3 with
-    the MFMA heads' cross-lane moves through ds_bpermute instead of the permlane swaps. The library
-    reads the variable at each launch."""
+    the MFMA heads' cross-lane moves through ds_bpermute instead of the permlane swaps; 64 = 0 with the
+    one-tick bodies' serve draw as two Philox blocks in a row. The library reads the variable at each
+    launch."""
     monkeypatch.setenv("PONGMI_ROLL16", str(tiles))
     test_rollout_matches_oracle(orc, 333, 40, 0.02)
     test_collect_matches_oracle(orc, 4096, 12, 2)

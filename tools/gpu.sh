@@ -19,6 +19,7 @@
 #   rnnab:VAR=v1,v2  the RNN bench (no CPU leg) under each value, interleaved twice
 #   infer      python bench.py --workload infer
 #   inferab:VAR=v1,v2  tests/test_gpu_rollout.py under each value, then the infer bench interleaved twice
+#   collectab:VAR=v1,v2  the same with the collect bench (SURVEY 8f3's collecting rollout)
 #   prof       rocprofv3 --kernel-trace --stats of the default bench (no CPU legs)
 #   pmc        the FETCH_SIZE / WRITE_SIZE passes of the default bench (tools/pmc_passes.sh)
 #   pmcrnn     the same for the RNN bench (tools/pmc_rnn_passes.sh)
@@ -144,6 +145,18 @@ run_task() {
         for v in ${vals//,/ }; do
           env $var=$v timeout -k 10 200 python3 bench.py --workload infer > gpurun_out/${tag}_inferab_${var}_${v}_$rep.json 2>/dev/null &&
               echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e9,4), d['ms_per_step'], d['roofline']['avg_us_per_step'], d['roofline']['frac'])" gpurun_out/${tag}_inferab_${var}_${v}_$rep.json)" || return 1
+        done
+      done ;;
+    collectab:*)  # collectab:VAR=v1,v2 — tests/test_gpu_rollout.py under each value, then the collect bench interleaved twice
+      spec=${1#collectab:}; var=${spec%%=*}; vals=${spec#*=}
+      for v in ${vals//,/ }; do
+        env $var=$v timeout -k 10 300 $PYT tests/test_gpu_rollout.py > gpurun_out/${tag}_collectab_${var}_${v}.log 2>&1 &&
+            echo "$var=$v $(tail -1 gpurun_out/${tag}_collectab_${var}_${v}.log)" || return 1
+      done &&
+      for rep in 1 2; do
+        for v in ${vals//,/ }; do
+          env $var=$v timeout -k 10 200 python3 bench.py --workload collect --no-cpu-baseline > gpurun_out/${tag}_collectab_${var}_${v}_$rep.json 2>/dev/null &&
+              echo "$var=$v rep$rep $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e9,4), d['ms_per_step'], d['roofline']['avg_us'], d['roofline']['frac'])" gpurun_out/${tag}_collectab_${var}_${v}_$rep.json)" || return 1
         done
       done ;;
     roll)  # k_rollout16 per-step phase cycles (diag build)

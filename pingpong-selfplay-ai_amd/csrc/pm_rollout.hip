@@ -694,6 +694,18 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
     for (int st = 0; st < steps; ++st) {
         const uint64_t ctr = counter0 + (uint64_t)st;
         if (wv == 7 && st + 1 < steps) fetch_heads_async(ws, st + 1, sm.hfB[(st + 1) & 1], lane);  // lands during the step
+        float hw4[32];  // MH, wave 0: lane 32 pp + 16 h + 4 cg + j's A operands, the weights of output j
+        // of player pp's half h. PL: read at the step's start (wave 7 wrote this step's set before the
+        // last barrier C), so the reads retire under the layers instead of holding wave 0 at barrier B
+        auto read_hw4 = [&]() {
+            const float* src = sm.opw[(lane >> 5) ? 1 + (st & 1) : 0][(lane >> 4) & 1][lane & 3];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float4 w = *reinterpret_cast<const float4*>(src + 4 * k);
+                hw4[4 * k] = w.x; hw4[4 * k + 1] = w.y; hw4[4 * k + 2] = w.z; hw4[4 * k + 3] = w.w;
+            }
+        };
+        if (PL && MH && wv == 0) read_hw4();
         // layer 1, the wave's row tile (K 8: bias + 7 inputs, input k' = 4 s + g) -> ReLU -> LDS
         {
             const float* o = sm.ob[player][col];
@@ -739,15 +751,7 @@ __device__ __forceinline__ void rollout16_body(const pm_env_params& p, const pm_
             sm.c2s[player][(u >> 2) & 1][q >> 2][col][q & 3] = relu(c2[r]);
         }
         if (wv == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next step's heads landed
-        float hw4[32];  // MH, wave 0: lane 32 pp + 16 h + 4 cg + j's A operands, the weights of output j
-        if (MH && wv == 0) {  // of player pp's half h (read before barrier B: the latency hides under it)
-            const float* src = sm.opw[(lane >> 5) ? 1 + (st & 1) : 0][(lane >> 4) & 1][lane & 3];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const float4 w = *reinterpret_cast<const float4*>(src + 4 * k);
-                hw4[4 * k] = w.x; hw4[4 * k + 1] = w.y; hw4[4 * k + 2] = w.z; hw4[4 * k + 3] = w.w;
-            }
-        }
+        if (!PL && MH && wv == 0) read_hw4();  // before barrier B: the latency hides under it
         ROLL_T(2);        // layer 2 + staging
         __syncthreads();  // (B) both players' layer 2
         ROLL_T(3);
